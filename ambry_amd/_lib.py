@@ -1,0 +1,93 @@
+"""ctypes binding of libambrycrc.so (the C ABI declared in include/ambrycrc.h).
+
+The shared library is built in-tree (``make -C ambry_amd`` or
+``__graft_entry__.build()``). There is no fallback: if the library is missing
+or fails to load, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libambrycrc.so")
+
+AMBRYCRC_OK = 0
+AMBRYCRC_EINVAL = -1
+AMBRYCRC_EHIP = -2
+AMBRYCRC_ENOMEM = -3
+AMBRYCRC_ENOINIT = -4
+AMBRYCRC_ENODEV = -5
+
+# (name, restype, argtypes) for every symbol include/ambrycrc.h declares.
+_u8p = ctypes.c_void_p
+_SIGNATURES = [
+    ("ambrycrc_init", ctypes.c_int, [ctypes.c_int]),
+    ("ambrycrc_shutdown", ctypes.c_int, []),
+    ("ambrycrc_strerror", ctypes.c_char_p, [ctypes.c_int]),
+    ("ambrycrc_version", ctypes.c_char_p, []),
+    ("ambrycrc_update", ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]),
+    ("ambrycrc_update_byte", ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_int]),
+    ("ambrycrc_combine", ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]),
+    ("ambrycrc_zeros", ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint64]),
+    ("ambrycrc_workspace_bytes", ctypes.c_size_t, [ctypes.c_size_t]),
+    ("ambrycrc_batch_dev", ctypes.c_int,
+     [_u8p, _u8p, _u8p, _u8p, _u8p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    ("ambrycrc_verify_dev", ctypes.c_int,
+     [_u8p, _u8p, _u8p, _u8p, _u8p, _u8p, _u8p, _u8p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
+      ctypes.c_void_p]),
+    ("ambrycrc_batch_host", ctypes.c_int,
+     [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32),
+      ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t, ctypes.c_int, ctypes.c_int]),
+    ("ambrycrc_set_tile_log2", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    ("ambrycrc_set_variant", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    ("ambrycrc_set_grid", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    ("ambrycrc_timing_enable", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    ("ambrycrc_timing_collect", ctypes.c_int,
+     [ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),
+    ("ambrycrc_grid_size", ctypes.c_int, [ctypes.c_int]),
+    ("ambrycrc_fill_random_dev", ctypes.c_int,
+     [_u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]),
+    ("ambrycrc_debug_table_image", ctypes.c_long, [ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t]),
+]
+
+EXPORTED = [s[0] for s in _SIGNATURES]
+
+_lock = threading.Lock()
+_lib = None
+
+
+class AmbryCrcError(RuntimeError):
+    def __init__(self, code: int, what: str):
+        self.code = code
+        super().__init__(f"{what}: {strerror(code)} ({code})")
+
+
+def lib() -> ctypes.CDLL:
+    """Load libambrycrc.so (raises if it is absent: no fallback path exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise ImportError(
+                    f"{LIB_PATH} not built; run `make -C {_HERE}` or __graft_entry__.build()")
+            handle = ctypes.CDLL(LIB_PATH)
+            for name, res, args in _SIGNATURES:
+                fn = getattr(handle, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = handle
+    return _lib
+
+
+def strerror(code: int) -> str:
+    return lib().ambrycrc_strerror(code).decode()
+
+
+def check(rc: int, what: str) -> int:
+    if rc < 0:
+        raise AmbryCrcError(rc, what)
+    return rc

@@ -1,0 +1,569 @@
+// ambrycrc.cpp -- host side of libambrycrc: C ABI (include/ambrycrc.h),
+// per-device contexts, kernel launches, host streaming primitives and the
+// pinned-staging host-resident batch path.
+#include "../../include/ambrycrc.h"
+
+#include <hip/hip_runtime.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <vector>
+
+#include "crc32_gf2.h"
+#include "crc32_kernels.h"
+#include "crc32_layout.h"
+
+using namespace ambrycrc;
+
+namespace {
+
+// ------------------------------------------------------------ host tables
+struct HostTables {
+  uint32_t t[8][256];
+  uint32_t xpow2[64];
+  HostTables() {
+    slice_tables(t, 8);
+    xpow8_pow2_table(xpow2);
+  }
+};
+
+const HostTables& host_tables() {
+  static const HostTables tables;  // C++11 thread-safe static init
+  return tables;
+}
+
+// Register-level slice-by-8 (the register is the bit-inverted CRC, as Crc32.java keeps it).
+uint32_t host_update_reg(uint32_t c, const uint8_t* p, size_t n) {
+  const HostTables& h = host_tables();
+  while (n >= 8) {
+    uint32_t lo, hi;
+    memcpy(&lo, p, 4);
+    memcpy(&hi, p + 4, 4);
+    lo ^= c;
+    c = h.t[7][lo & 0xff] ^ h.t[6][(lo >> 8) & 0xff] ^ h.t[5][(lo >> 16) & 0xff] ^ h.t[4][lo >> 24] ^
+        h.t[3][hi & 0xff] ^ h.t[2][(hi >> 8) & 0xff] ^ h.t[1][(hi >> 16) & 0xff] ^ h.t[0][hi >> 24];
+    p += 8;
+    n -= 8;
+  }
+  while (n--) c = (c >> 8) ^ h.t[0][(c ^ *p++) & 0xff];
+  return c;
+}
+
+uint32_t host_xpow8(uint64_t n) {
+  const HostTables& h = host_tables();
+  uint32_t r = kOne;
+  for (int k = 0; n; ++k, n >>= 1)
+    if (n & 1) r = gf2_mul(r, h.xpow2[k]);
+  return r;
+}
+
+// ------------------------------------------------------------ LDS image
+std::vector<uint32_t> build_table_image() {
+  const uint32_t words = kLdsBytes / 4 + 64;
+  std::vector<uint32_t> img(words, 0u);
+  uint32_t t[4][256];
+  slice_tables(t, 4);
+  for (uint32_t j = 0; j < 4; ++j)
+    for (uint32_t b = 0; b < 256; ++b)
+      for (uint32_t l = 0; l < 32; ++l) {
+        const uint32_t addr = ((j >> 1) << 16) | (b << 8) | ((j & 1) << 7) | (l << 2);
+        img[addr / 4] = t[j][b];
+      }
+  auto put_nib = [&](uint32_t off, uint32_t c) {
+    uint32_t nt[8][16];
+    nibble_tables(c, nt);
+    for (int n = 0; n < 8; ++n)
+      for (int x = 0; x < 16; ++x) img[(kNibBase + off + 64u * n + 4u * x) / 4] = nt[n][x];
+  };
+  put_nib(kFoldOff, host_xpow8(kBlockBytes));
+  for (uint32_t l = 0; l < kTreeLevels; ++l) put_nib(kTreeOff + kNibSetBytes * l, host_xpow8(16ull << l));
+  for (uint32_t k = 0; k < kPowTables; ++k) put_nib(kPowOff + kNibSetBytes * k, host_xpow8(1ull << k));
+  const HostTables& h = host_tables();
+  for (int k = 0; k < 64; ++k) img[kLdsBytes / 4 + k] = h.xpow2[k];
+  return img;
+}
+
+// ------------------------------------------------------------ contexts
+constexpr int kMaxDevices = 64;
+constexpr size_t kSlabBytes = 256ull << 20;   // host-path staging slab
+constexpr size_t kSlabChunks = 1u << 16;      // max chunk pieces per slab
+
+struct EventPair {
+  hipEvent_t a, b;
+};
+
+struct HostSlab {
+  uint8_t* h_data = nullptr;   // pinned
+  uint64_t* h_meta = nullptr;  // pinned: off[kSlabChunks], len[kSlabChunks]
+  uint32_t* h_out = nullptr;   // pinned
+  uint8_t* d_data = nullptr;
+  uint64_t* d_meta = nullptr;
+  uint32_t* d_out = nullptr;
+  void* d_ws = nullptr;
+  hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;
+};
+
+struct DevCtx {
+  int device = -1;
+  int num_cu = 0;
+  int grid = 0;
+  int variant = 0;
+  int tile_log2 = 18;
+  uint32_t* d_img = nullptr;
+  void* d_ws = nullptr;
+  size_t ws_bytes = 0;
+  bool timing = false;
+  std::vector<EventPair> pending, free_events;
+  bool slabs_ready = false;
+  HostSlab slab[2];
+  std::mutex mu;  // guards ws growth, events, slabs
+};
+
+std::mutex g_mu;
+DevCtx* g_ctx[kMaxDevices] = {nullptr};
+
+int hip_err(hipError_t e) { return e == hipSuccess ? AMBRYCRC_OK : AMBRYCRC_EHIP; }
+
+DevCtx* ctx_for(int device) {
+  if (device < 0 || device >= kMaxDevices) return nullptr;
+  std::lock_guard<std::mutex> g(g_mu);
+  return g_ctx[device];
+}
+
+DevCtx* ctx_current() {
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  return ctx_for(dev);
+}
+
+size_t ws_need(size_t n) { return ((n + 1) * sizeof(uint32_t) + 255) & ~size_t(255); }
+
+int ensure_ws(DevCtx* c, size_t need) {
+  if (c->ws_bytes >= need) return AMBRYCRC_OK;
+  const size_t sz = std::max(need, c->ws_bytes * 2);
+  if (c->d_ws) {
+    (void)hipDeviceSynchronize();  // the old workspace may still be in use by queued work
+    (void)hipFree(c->d_ws);
+  }
+  c->d_ws = nullptr;
+  c->ws_bytes = 0;
+  if (hipMalloc(&c->d_ws, sz) != hipSuccess) return AMBRYCRC_ENOMEM;
+  c->ws_bytes = sz;
+  return AMBRYCRC_OK;
+}
+
+int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len, const uint32_t* crc_in,
+                  uint32_t* out, size_t n, void* ws, hipStream_t s) {
+  if (n == 0) return AMBRYCRC_OK;
+  PlanArgs p;
+  p.off = off;
+  p.len = len;
+  p.n = (uint32_t)n;
+  p.tile_log2 = (uint32_t)c->tile_log2;
+  p.tile_start = static_cast<uint32_t*>(ws);
+  p.out = out;
+  hipError_t e = launch_plan(p, s);
+  if (e != hipSuccess) return AMBRYCRC_EHIP;
+  TilesArgs t;
+  t.base = base;
+  t.off = off;
+  t.len = len;
+  t.crc_in = crc_in;
+  t.n = (uint32_t)n;
+  t.tile_log2 = (uint32_t)c->tile_log2;
+  t.tile_start = p.tile_start;
+  t.img = c->d_img;
+  t.out = out;
+  EventPair ev{nullptr, nullptr};
+  if (c->timing) {
+    std::lock_guard<std::mutex> g(c->mu);
+    if (!c->free_events.empty()) {
+      ev = c->free_events.back();
+      c->free_events.pop_back();
+    } else if (hipEventCreate(&ev.a) != hipSuccess || hipEventCreate(&ev.b) != hipSuccess) {
+      return AMBRYCRC_EHIP;
+    }
+    if (hipEventRecord(ev.a, s) != hipSuccess) return AMBRYCRC_EHIP;
+  }
+  e = launch_tiles(t, c->grid, c->variant, s);
+  if (e != hipSuccess) return AMBRYCRC_EHIP;
+  if (c->timing) {
+    if (hipEventRecord(ev.b, s) != hipSuccess) return AMBRYCRC_EHIP;
+    std::lock_guard<std::mutex> g(c->mu);
+    c->pending.push_back(ev);
+  }
+  return AMBRYCRC_OK;
+}
+
+int resolve(DevCtx** out_ctx, void** ws, size_t ws_bytes, size_t n) {
+  DevCtx* c = ctx_current();
+  if (!c) return AMBRYCRC_ENOINIT;
+  const size_t need = ws_need(n);
+  if (*ws) {
+    if (ws_bytes < need) return AMBRYCRC_EINVAL;
+  } else {
+    std::lock_guard<std::mutex> g(c->mu);
+    int rc = ensure_ws(c, need);
+    if (rc) return rc;
+    *ws = c->d_ws;
+  }
+  *out_ctx = c;
+  return AMBRYCRC_OK;
+}
+
+int setup_slabs(DevCtx* c) {
+  if (c->slabs_ready) return AMBRYCRC_OK;
+  for (auto& s : c->slab) {
+    if (hipHostMalloc(reinterpret_cast<void**>(&s.h_data), kSlabBytes, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void**>(&s.h_meta), 2 * kSlabChunks * sizeof(uint64_t),
+                      hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void**>(&s.h_out), kSlabChunks * sizeof(uint32_t), hipHostMallocDefault) !=
+            hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&s.d_data), kSlabBytes) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&s.d_meta), 2 * kSlabChunks * sizeof(uint64_t)) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&s.d_out), kSlabChunks * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&s.d_ws, ws_need(kSlabChunks)) != hipSuccess)
+      return AMBRYCRC_ENOMEM;
+    if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess) return AMBRYCRC_EHIP;
+    if (hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess) return AMBRYCRC_EHIP;
+  }
+  c->slabs_ready = true;
+  return AMBRYCRC_OK;
+}
+
+void free_ctx(DevCtx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)hipDeviceSynchronize();
+  if (c->d_img) (void)hipFree(c->d_img);
+  if (c->d_ws) (void)hipFree(c->d_ws);
+  for (auto& e : c->pending) {
+    (void)hipEventDestroy(e.a);
+    (void)hipEventDestroy(e.b);
+  }
+  for (auto& e : c->free_events) {
+    (void)hipEventDestroy(e.a);
+    (void)hipEventDestroy(e.b);
+  }
+  if (c->slabs_ready) {
+    for (auto& s : c->slab) {
+      (void)hipHostFree(s.h_data);
+      (void)hipHostFree(s.h_meta);
+      (void)hipHostFree(s.h_out);
+      (void)hipFree(s.d_data);
+      (void)hipFree(s.d_meta);
+      (void)hipFree(s.d_out);
+      (void)hipFree(s.d_ws);
+      (void)hipStreamDestroy(s.stream);
+      (void)hipEventDestroy(s.done);
+    }
+  }
+  delete c;
+}
+
+}  // namespace
+
+// ================================================================= C ABI
+extern "C" {
+
+const char* ambrycrc_strerror(int code) {
+  switch (code) {
+    case AMBRYCRC_OK: return "ok";
+    case AMBRYCRC_EINVAL: return "invalid argument";
+    case AMBRYCRC_EHIP: return "HIP runtime error";
+    case AMBRYCRC_ENOMEM: return "out of memory";
+    case AMBRYCRC_ENOINIT: return "ambrycrc_init() not called for the current device";
+    case AMBRYCRC_ENODEV: return "no usable gfx950 device";
+    default: return "unknown error";
+  }
+}
+
+const char* ambrycrc_version(void) { return "ambrycrc 0.1.0 gfx950"; }
+
+uint32_t ambrycrc_update(uint32_t crc, const void* p, size_t n) {
+  if (!p || n == 0) return crc;
+  return ~host_update_reg(~crc, static_cast<const uint8_t*>(p), n);
+}
+
+uint32_t ambrycrc_update_byte(uint32_t crc, int b) {
+  const HostTables& h = host_tables();
+  uint32_t c = ~crc;
+  c = (c >> 8) ^ h.t[0][(c ^ (uint32_t)b) & 0xff];
+  return ~c;
+}
+
+uint32_t ambrycrc_combine(uint32_t crc1, uint32_t crc2, uint64_t len2) {
+  return gf2_mul(crc1, host_xpow8(len2)) ^ crc2;
+}
+
+uint32_t ambrycrc_zeros(uint32_t crc, uint64_t n) {
+  // register' = register * x^(8n); value = ~register.
+  return ~gf2_mul(~crc, host_xpow8(n));
+}
+
+int ambrycrc_init(int device) {
+  if (device < 0 || device >= kMaxDevices) return AMBRYCRC_EINVAL;
+  std::lock_guard<std::mutex> g(g_mu);
+  if (g_ctx[device]) return AMBRYCRC_OK;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || device >= count) return AMBRYCRC_ENODEV;
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  if (hipSetDevice(device) != hipSuccess) return AMBRYCRC_EHIP;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return AMBRYCRC_EHIP;
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    (void)hipSetDevice(prev);
+    return AMBRYCRC_ENODEV;
+  }
+  DevCtx* c = new DevCtx();
+  c->device = device;
+  c->num_cu = prop.multiProcessorCount;
+  c->grid = c->num_cu;
+  if (const char* v = getenv("AMBRYCRC_TILE_LOG2")) c->tile_log2 = std::min(30, std::max(12, atoi(v)));
+  if (const char* v = getenv("AMBRYCRC_VARIANT")) c->variant = atoi(v);
+  std::vector<uint32_t> img = build_table_image();
+  if (hipMalloc(reinterpret_cast<void**>(&c->d_img), img.size() * 4) != hipSuccess) {
+    delete c;
+    return AMBRYCRC_ENOMEM;
+  }
+  if (hipMemcpy(c->d_img, img.data(), img.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+    free_ctx(c);
+    return AMBRYCRC_EHIP;
+  }
+  if (ensure_ws(c, ws_need(1u << 16)) != AMBRYCRC_OK) {
+    free_ctx(c);
+    return AMBRYCRC_ENOMEM;
+  }
+  g_ctx[device] = c;
+  (void)hipSetDevice(prev);
+  return AMBRYCRC_OK;
+}
+
+int ambrycrc_shutdown(void) {
+  std::lock_guard<std::mutex> g(g_mu);
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  for (int d = 0; d < kMaxDevices; ++d) {
+    free_ctx(g_ctx[d]);
+    g_ctx[d] = nullptr;
+  }
+  (void)hipSetDevice(prev);
+  return AMBRYCRC_OK;
+}
+
+size_t ambrycrc_workspace_bytes(size_t n) { return ws_need(n); }
+
+int ambrycrc_batch_dev(const uint8_t* d_base, const uint64_t* d_off, const uint64_t* d_len, const uint32_t* d_crc_in,
+                       uint32_t* d_out, size_t n, void* d_ws, size_t ws_bytes, hipStream_t stream) {
+  if (n == 0) return AMBRYCRC_OK;
+  if (!d_base || !d_off || !d_len || !d_out || n >= (1ull << 31)) return AMBRYCRC_EINVAL;
+  DevCtx* c = nullptr;
+  int rc = resolve(&c, &d_ws, ws_bytes, n);
+  if (rc) return rc;
+  return enqueue_batch(c, d_base, d_off, d_len, d_crc_in, d_out, n, d_ws, stream);
+}
+
+int ambrycrc_verify_dev(const uint8_t* d_base, const uint64_t* d_off, const uint64_t* d_len, const uint32_t* d_crc_in,
+                        const uint32_t* d_expected, uint32_t* d_out, uint8_t* d_mismatch, uint32_t* d_mismatch_count,
+                        size_t n, void* d_ws, size_t ws_bytes, hipStream_t stream) {
+  if (n == 0) return AMBRYCRC_OK;
+  if (!d_base || !d_off || !d_len || !d_expected || n >= (1ull << 31)) return AMBRYCRC_EINVAL;
+  DevCtx* c = nullptr;
+  // Without a caller d_out, the CRCs live in the workspace right after tile_start.
+  const size_t extra = d_out ? 0 : ((n * sizeof(uint32_t) + 255) & ~size_t(255));
+  if (d_ws && ws_bytes < ws_need(n) + extra) return AMBRYCRC_EINVAL;
+  int rc = resolve(&c, &d_ws, d_ws ? ws_bytes : 0, n);
+  if (rc) return rc;
+  if (!d_out) {
+    std::lock_guard<std::mutex> g(c->mu);
+    if (d_ws == c->d_ws) {
+      rc = ensure_ws(c, ws_need(n) + extra);
+      if (rc) return rc;
+      d_ws = c->d_ws;
+    }
+    d_out = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(d_ws) + ws_need(n));
+  }
+  rc = enqueue_batch(c, d_base, d_off, d_len, d_crc_in, d_out, n, d_ws, stream);
+  if (rc) return rc;
+  return hip_err(launch_verify(d_out, d_expected, d_mismatch, d_mismatch_count, (uint32_t)n, stream));
+}
+
+int ambrycrc_batch_host(const void* const* ptrs, const uint64_t* lens, const uint32_t* crc_in, uint32_t* out, size_t n,
+                        int device, int pinned) {
+  if (n == 0) return AMBRYCRC_OK;
+  if (!ptrs || !lens || !out) return AMBRYCRC_EINVAL;
+  DevCtx* c = ctx_for(device);
+  if (!c) return AMBRYCRC_ENOINIT;
+  std::lock_guard<std::mutex> g(c->mu);
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  if (hipSetDevice(device) != hipSuccess) return AMBRYCRC_EHIP;
+  int rc = setup_slabs(c);
+  if (rc) return rc;
+
+  // Pieces: chunks are cut at slab boundaries; pieces of one chunk are combined on the host.
+  struct Piece {
+    size_t chunk;
+    uint64_t pos, len;
+  };
+  std::vector<uint32_t> acc(n, 0u);
+  for (size_t i = 0; i < n; ++i) acc[i] = crc_in ? crc_in[i] : 0u;
+
+  size_t ci = 0;
+  uint64_t cpos = 0;
+  int k = 0;
+  std::vector<Piece> inflight[2];
+  auto drain = [&](int which) -> int {
+    HostSlab& s = c->slab[which];
+    if (inflight[which].empty()) return AMBRYCRC_OK;
+    if (hipEventSynchronize(s.done) != hipSuccess) return AMBRYCRC_EHIP;
+    for (size_t j = 0; j < inflight[which].size(); ++j) {
+      const Piece& p = inflight[which][j];
+      acc[p.chunk] = gf2_mul(acc[p.chunk], host_xpow8(p.len)) ^ s.h_out[j];  // combine(acc, piece, len)
+    }
+    inflight[which].clear();
+    return AMBRYCRC_OK;
+  };
+  while (ci < n) {
+    const int w = k & 1;
+    rc = drain(w);  // the slab we are about to refill
+    if (rc) break;
+    HostSlab& s = c->slab[w];
+    uint64_t used = 0;
+    size_t np = 0;
+    while (ci < n && np < kSlabChunks) {
+      const uint64_t rem = lens[ci] - cpos;
+      const uint64_t room = kSlabBytes - used;
+      if (rem > 0 && room < 16) break;
+      const uint64_t take = std::min(rem, room);
+      if (take > 0 && !ptrs[ci]) {
+        rc = AMBRYCRC_EINVAL;
+        break;
+      }
+      const uint8_t* src = static_cast<const uint8_t*>(ptrs[ci]) + cpos;
+      if (pinned) {
+        if (take && hipMemcpyAsync(s.d_data + used, src, take, hipMemcpyHostToDevice, s.stream) != hipSuccess) {
+          rc = AMBRYCRC_EHIP;
+          break;
+        }
+      } else if (take) {
+        memcpy(s.h_data + used, src, take);
+      }
+      s.h_meta[np] = used;
+      s.h_meta[kSlabChunks + np] = take;
+      inflight[w].push_back({ci, cpos, take});
+      ++np;
+      used = (used + take + 15) & ~uint64_t(15);
+      cpos += take;
+      if (cpos >= lens[ci]) {
+        ++ci;
+        cpos = 0;
+      }
+      if (used >= kSlabBytes) break;
+    }
+    if (rc) break;
+    if (!pinned && used &&
+        hipMemcpyAsync(s.d_data, s.h_data, std::min<uint64_t>(used, kSlabBytes), hipMemcpyHostToDevice, s.stream) !=
+            hipSuccess) {
+      rc = AMBRYCRC_EHIP;
+      break;
+    }
+    if (hipMemcpyAsync(s.d_meta, s.h_meta, 2 * kSlabChunks * sizeof(uint64_t), hipMemcpyHostToDevice, s.stream) !=
+        hipSuccess) {
+      rc = AMBRYCRC_EHIP;
+      break;
+    }
+    rc = enqueue_batch(c, s.d_data, s.d_meta, s.d_meta + kSlabChunks, nullptr, s.d_out, np, s.d_ws, s.stream);
+    if (rc) break;
+    if (hipMemcpyAsync(s.h_out, s.d_out, np * sizeof(uint32_t), hipMemcpyDeviceToHost, s.stream) != hipSuccess ||
+        hipEventRecord(s.done, s.stream) != hipSuccess) {
+      rc = AMBRYCRC_EHIP;
+      break;
+    }
+    ++k;
+  }
+  int rc2 = drain(k & 1);  // older slab first: pieces must combine in order
+  int rc3 = drain((k + 1) & 1);
+  (void)hipSetDevice(prev);
+  if (rc) return rc;
+  if (rc2) return rc2;
+  if (rc3) return rc3;
+  for (size_t i = 0; i < n; ++i) out[i] = acc[i];
+  return AMBRYCRC_OK;
+}
+
+int ambrycrc_set_tile_log2(int device, int tile_log2) {
+  DevCtx* c = ctx_for(device);
+  if (!c) return AMBRYCRC_ENOINIT;
+  if (tile_log2 < 12 || tile_log2 > 30) return AMBRYCRC_EINVAL;
+  c->tile_log2 = tile_log2;
+  return AMBRYCRC_OK;
+}
+
+int ambrycrc_set_variant(int device, int variant) {
+  DevCtx* c = ctx_for(device);
+  if (!c) return AMBRYCRC_ENOINIT;
+  if (variant < 0 || variant > 3) return AMBRYCRC_EINVAL;
+  c->variant = variant;
+  return AMBRYCRC_OK;
+}
+
+int ambrycrc_set_grid(int device, int workgroups) {
+  DevCtx* c = ctx_for(device);
+  if (!c) return AMBRYCRC_ENOINIT;
+  if (workgroups < 0) return AMBRYCRC_EINVAL;
+  c->grid = workgroups ? workgroups : c->num_cu;
+  return AMBRYCRC_OK;
+}
+
+int ambrycrc_grid_size(int device) {
+  DevCtx* c = ctx_for(device);
+  return c ? c->grid : 0;
+}
+
+int ambrycrc_timing_enable(int device, int enable) {
+  DevCtx* c = ctx_for(device);
+  if (!c) return AMBRYCRC_ENOINIT;
+  c->timing = enable != 0;
+  return AMBRYCRC_OK;
+}
+
+int ambrycrc_timing_collect(int device, double* total_ms, int* launches) {
+  DevCtx* c = ctx_for(device);
+  if (!c) return AMBRYCRC_ENOINIT;
+  std::lock_guard<std::mutex> g(c->mu);
+  double sum = 0;
+  int cnt = 0;
+  for (auto& e : c->pending) {
+    if (hipEventSynchronize(e.b) != hipSuccess) return AMBRYCRC_EHIP;
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, e.a, e.b) != hipSuccess) return AMBRYCRC_EHIP;
+    sum += ms;
+    ++cnt;
+    c->free_events.push_back(e);
+  }
+  c->pending.clear();
+  if (total_ms) *total_ms = sum;
+  if (launches) *launches = cnt;
+  return AMBRYCRC_OK;
+}
+
+int ambrycrc_fill_random_dev(uint8_t* d_dst, uint64_t nbytes, uint64_t seed, uint64_t stream_off,
+                             hipStream_t stream) {
+  if (nbytes == 0) return AMBRYCRC_OK;
+  if (!d_dst || (reinterpret_cast<uintptr_t>(d_dst) & 15) || (stream_off & 15)) return AMBRYCRC_EINVAL;
+  return hip_err(launch_fill(d_dst, nbytes, seed, stream_off, stream));
+}
+
+long ambrycrc_debug_table_image(uint32_t* out, size_t max_words) {
+  std::vector<uint32_t> img = build_table_image();
+  if (!out || max_words < img.size()) return AMBRYCRC_EINVAL;
+  memcpy(out, img.data(), img.size() * 4);
+  return (long)(img.size() * 4);
+}
+
+}  // extern "C"

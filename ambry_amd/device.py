@@ -1,0 +1,126 @@
+"""Device-resident batch API over torch-allocated HBM (thin layer on the C ABI).
+
+Torch is only plumbing here: it allocates HBM and provides the stream; every
+CRC is computed by libambrycrc's gfx950 kernels via ``ambrycrc_batch_dev`` /
+``ambrycrc_verify_dev``. Offsets/lengths are int64 device tensors (uint64 in
+the ABI), CRCs are int32 device tensors holding the uint32 bit patterns
+(``.view(torch.uint32)`` / numpy ``.view(np.uint32)`` to read them).
+"""
+from __future__ import annotations
+
+import ctypes
+
+from ._lib import check, lib
+
+
+def _torch():
+    import torch  # deferred: CPU-only tests import this module without a GPU
+
+    return torch
+
+
+def _stream_handle(stream=None) -> int:
+    torch = _torch()
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+def _ptr(t) -> ctypes.c_void_p | None:
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def init(device: int = 0) -> None:
+    check(lib().ambrycrc_init(device), f"ambrycrc_init({device})")
+
+
+def _check_batch(base, off, length, n):
+    torch = _torch()
+    if base.dtype != torch.uint8 or not base.is_cuda:
+        raise TypeError("base must be a uint8 CUDA tensor")
+    for name, t in (("off", off), ("len", length)):
+        if t.dtype != torch.int64 or not t.is_cuda or t.numel() != n or not t.is_contiguous():
+            raise TypeError(f"{name} must be a contiguous int64 CUDA tensor of {n} elements")
+
+
+def crc32_batch(base, off, length, crc_in=None, out=None, workspace=None, stream=None):
+    """out[i] = crc32(crc_in[i] or 0, base[off[i]:off[i]+len[i]]) for every chunk i (on the GPU)."""
+    torch = _torch()
+    n = off.numel()
+    _check_batch(base, off, length, n)
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=base.device)
+    ws, ws_bytes = (None, 0) if workspace is None else (_ptr(workspace), workspace.numel())
+    check(lib().ambrycrc_batch_dev(_ptr(base), _ptr(off), _ptr(length), _ptr(crc_in), _ptr(out), n, ws, ws_bytes,
+                                   ctypes.c_void_p(_stream_handle(stream))), "ambrycrc_batch_dev")
+    return out
+
+
+def crc32_verify(base, off, length, expected, crc_in=None, out=None, stream=None):
+    """Returns (crc int32[n], mismatch uint8[n], mismatch_count int32[1]) computed on the GPU."""
+    torch = _torch()
+    n = off.numel()
+    _check_batch(base, off, length, n)
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=base.device)
+    mismatch = torch.empty(n, dtype=torch.uint8, device=base.device)
+    count = torch.zeros(1, dtype=torch.int32, device=base.device)
+    check(lib().ambrycrc_verify_dev(_ptr(base), _ptr(off), _ptr(length), _ptr(crc_in), _ptr(expected), _ptr(out),
+                                    _ptr(mismatch), _ptr(count), n, None, 0,
+                                    ctypes.c_void_p(_stream_handle(stream))), "ambrycrc_verify_dev")
+    return out, mismatch, count
+
+
+def fill_random(buf, seed: int, stream_off: int = 0, stream=None) -> None:
+    """Deterministic splitmix64 bytes (same stream as oracle_fill_splitmix)."""
+    check(lib().ambrycrc_fill_random_dev(_ptr(buf), buf.numel(), seed & (2**64 - 1), stream_off,
+                                         ctypes.c_void_p(_stream_handle(stream))), "ambrycrc_fill_random_dev")
+
+
+def crc32_batch_host(chunks, device: int = 0, pinned: bool = False, crc_in=None):
+    """CRC of host buffers through pinned staging + hipMemcpyAsync (PCIe-inclusive path).
+
+    ``chunks``: sequence of objects exposing ``data_ptr()``/``numel()`` (uint8
+    CPU tensors) or (address, length) tuples.
+    """
+    n = len(chunks)
+    ptrs = (ctypes.c_void_p * n)()
+    lens = (ctypes.c_uint64 * n)()
+    for i, c in enumerate(chunks):
+        if isinstance(c, tuple):
+            ptrs[i], lens[i] = c
+        else:
+            ptrs[i], lens[i] = c.data_ptr(), c.numel()
+    out = (ctypes.c_uint32 * n)()
+    cin = None
+    if crc_in is not None:
+        cin = (ctypes.c_uint32 * n)(*[int(x) & 0xFFFFFFFF for x in crc_in])
+    check(lib().ambrycrc_batch_host(ptrs, lens, cin, out, n, device, 1 if pinned else 0), "ambrycrc_batch_host")
+    return list(out)
+
+
+def set_tile_log2(device: int, tile_log2: int) -> None:
+    check(lib().ambrycrc_set_tile_log2(device, tile_log2), "ambrycrc_set_tile_log2")
+
+
+def set_variant(device: int, variant: int) -> None:
+    check(lib().ambrycrc_set_variant(device, variant), "ambrycrc_set_variant")
+
+
+def set_grid(device: int, workgroups: int) -> None:
+    check(lib().ambrycrc_set_grid(device, workgroups), "ambrycrc_set_grid")
+
+
+def grid_size(device: int = 0) -> int:
+    return lib().ambrycrc_grid_size(device)
+
+
+def timing_enable(device: int, enable: bool = True) -> None:
+    check(lib().ambrycrc_timing_enable(device, 1 if enable else 0), "ambrycrc_timing_enable")
+
+
+def timing_collect(device: int = 0):
+    """(sum of tiles-kernel ms, launches) since the last collect (HIP events on the launch stream)."""
+    ms = ctypes.c_double()
+    cnt = ctypes.c_int()
+    check(lib().ambrycrc_timing_collect(device, ctypes.byref(ms), ctypes.byref(cnt)), "ambrycrc_timing_collect")
+    return ms.value, cnt.value

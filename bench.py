@@ -1,0 +1,274 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident CRC-32 over 4 MiB blob chunks (BASELINE.json metric, config C3).
+
+One step = one pass of the hot path (ambrycrc_batch_dev: plan + tiles kernels)
+over one batch of 8,192 x 4 MiB chunks (32 GiB) resident in HBM on every rank.
+N>1: one process per GPU (torchrun), each rank owns its own 8,192-chunk shard
+(weak scaling; C5 = 524,288 chunks = 8 such steps on 8 GPUs) and the 4-byte
+CRCs are all-gathered over RCCL once per step.
+
+Prints ONE JSON line (rank 0). Besides the driver contract it carries:
+  roofline      tiles-kernel algorithmic bytes / its HIP-event-timed duration vs 8 TB/s
+  cpu_baseline  the oracle's restatement of Crc32.java (kind "port") on host cores, bounded sample
+  host_path     pinned-host -> HBM -> CRC rate (PCIe-inclusive; never `value`)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+METRIC = "GiB/s device-resident CRC32 over 4 MiB blob chunks; % of HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+CONFIGS = {
+    # name: (chunks per GPU, chunk bytes, description)
+    "c3": (8192, 4 << 20, "C3: 8,192 x 4 MiB large-blob router chunks per GPU"),
+    "c2": (65536, 64 << 10, "C2: 65,536 x 64 KiB small-object chunks per GPU"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS) + ["c4"])
+    ap.add_argument("--variant", type=int, default=None)
+    ap.add_argument("--tile-log2", type=int, default=None)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-path", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--quiet", action="store_true", help="no progress lines on stderr")
+    return ap.parse_args()
+
+
+def log(args, *msg):
+    if not args.quiet:
+        print("[bench]", *msg, file=sys.stderr, flush=True)
+
+
+def build_workload(torch, dev, args, rank):
+    from ambry_amd import device as D
+
+    if args.config == "c4":
+        from datagen import zipf_sizes
+
+        sizes = zipf_sizes(32768)
+        off = [0]
+        for s in sizes[:-1]:
+            off.append(off[-1] + ((int(s) + 15) // 16) * 16)
+        total = off[-1] + int(sizes[-1])
+        import numpy as np
+
+        off_t = torch.tensor(np.asarray(off, dtype=np.int64), device=dev)
+        len_t = torch.tensor(sizes.astype(np.int64), device=dev)
+        desc = "C4: 32,768 Zipf(1.2) chunks 4 KiB-4 MiB (verify-on-read sizes)"
+        n = len(sizes)
+        chunk = None
+    else:
+        n, chunk, desc = CONFIGS[args.config]
+        total = n * chunk
+        off_t = torch.arange(n, dtype=torch.int64, device=dev) * chunk
+        len_t = torch.full((n,), chunk, dtype=torch.int64, device=dev)
+    buf = torch.empty(total, dtype=torch.uint8, device=dev)
+    D.fill_random(buf, 0xA3B1C2D3 ^ (rank * 0x9E3779B97F4A7C15 & (2**64 - 1)), 0)
+    torch.cuda.synchronize()
+    return buf, off_t, len_t, n, total, chunk, desc
+
+
+def cpu_baseline(buf, off_t, len_t, n, args):
+    """Oracle (C restatement of Crc32.java slice-by-8) on host cores over a bounded sample."""
+    import numpy as np
+
+    from conftest import ORACLE_SO, Oracle
+
+    if not os.path.exists(ORACLE_SO):
+        return None
+    orc = Oracle()
+    sample_chunks = min(n, 64)
+    off = off_t[:sample_chunks].cpu().numpy()
+    ln = len_t[:sample_chunks].cpu().numpy()
+    lo, hi = int(off[0]), int(off[-1] + ln[-1])
+    host = buf[lo:hi].cpu().numpy()
+    off = off - lo
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    res = {}
+    for th in (1, threads):
+        t0 = time.perf_counter()
+        passes = 0
+        while True:
+            out = orc.batch(host, off, ln, threads=th)
+            passes += 1
+            el = time.perf_counter() - t0
+            if el >= args.cpu_seconds / 2 or passes >= 1000:
+                break
+        res[th] = (passes * int(ln.sum()) / el / 2**30, passes, out)
+    gibs, passes, out = res[threads]
+    return {
+        "value": round(gibs, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+        "sample": f"{sample_chunks} chunks x {int(ln[0]) if len(set(ln.tolist())) == 1 else 'mixed'} B "
+                  f"(first chunks of the same workload, D2H-copied) x {passes} passes; oracle/crc32_ref.c "
+                  f"slice-by-8 restating Crc32.java:55-98, {threads} pthreads",
+        "single_thread_gibs": round(res[1][0], 3),
+        "_out": out,
+    }
+
+
+def host_path_rate(torch, args):
+    """Pinned host buffers -> PCIe -> HBM -> CRC -> host (ambrycrc_batch_host); DESIGN.md only."""
+    from ambry_amd import device as D
+
+    nchunks, chunk = 512, 4 << 20  # 2 GiB
+    host = torch.empty(nchunks * chunk, dtype=torch.uint8).pin_memory()
+    host.view(torch.int64).random_()
+    chunks = [(host.data_ptr() + i * chunk, chunk) for i in range(nchunks)]
+    D.crc32_batch_host(chunks[:8], device=0, pinned=True)  # warm staging
+    t0 = time.perf_counter()
+    D.crc32_batch_host(chunks, device=0, pinned=True)
+    el = time.perf_counter() - t0
+    return {"value": round(nchunks * chunk / el / 2**30, 2), "unit": "GiB/s",
+            "sample": f"{nchunks} x 4 MiB pinned host chunks, one synchronous ambrycrc_batch_host call"}
+
+
+def main():
+    args = parse()
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(args, f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from ambry_amd import device as D
+
+    D.init(dev.index)
+    if args.variant is not None:
+        D.set_variant(dev.index, args.variant)
+    if args.tile_log2 is not None:
+        D.set_tile_log2(dev.index, args.tile_log2)
+
+    log(args, f"rank {rank}/{world}: building workload {args.config}")
+    buf, off_t, len_t, n, total, chunk, desc = build_workload(torch, dev, args, rank)
+    gathered = torch.empty(world * n, dtype=torch.int32, device=dev) if world > 1 else None
+
+    def step():
+        out = D.crc32_batch(buf, off_t, len_t)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, out)
+        return out
+
+    for _ in range(args.warmup):
+        out = step()
+    torch.cuda.synchronize()
+    D.timing_collect(dev.index)  # drop warmup events
+    D.timing_enable(dev.index, True)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for i in range(args.steps):
+        out = step()
+    ev1.record()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    D.timing_enable(dev.index, False)
+    kern_ms, launches = D.timing_collect(dev.index)
+    ev_ms = ev0.elapsed_time(ev1)
+
+    elapsed = wall
+    if dist:
+        t = torch.tensor([wall], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    crcs = out.cpu().numpy().view("uint32")
+    step_bytes = total  # per rank
+    value = world * step_bytes * args.steps / elapsed / 2**30
+    kern_avg_s = kern_ms / max(1, launches) / 1e3
+    alg_bytes = total + 4 * n  # chunk bytes read + 4 B CRC written per chunk (offset/len arrays excluded)
+    achieved = alg_bytes / kern_avg_s / 1e9 if kern_avg_s > 0 else None
+
+    result = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (device splitmix64 bytes; no dataset)",
+        "config": {"workload": desc, "chunks_per_gpu": n, "chunk_bytes": chunk, "bytes_per_gpu_step": total,
+                   "parallelism": f"shard{world}" + ("+rccl_allgather" if world > 1 else ""),
+                   "tile_log2": None, "grid_workgroups": D.grid_size(dev.index)},
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "crc32_tiles_kernel",
+            "achieved": round(achieved, 1) if achieved else None,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+            "traffic": None,
+            "kernel_avg_ms": round(kern_avg_s * 1e3, 4),
+            "algorithmic_bytes_per_launch": alg_bytes,
+            "value_frac_of_peak": round(value * 2**30 / 1e9 / world / HBM_PEAK_GBS, 4),
+        },
+        "timing": {"wall_s": round(elapsed, 4), "stream_event_ms": round(ev_ms, 3), "kernel_launches": launches},
+    }
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc) and args.config == "c3":
+        try:
+            with open(pmc) as f:
+                p = json.load(f)
+            result["roofline"]["traffic"] = p.get("hbm_bytes_per_launch")
+            result["roofline"]["traffic_source"] = p.get("source")
+        except Exception:
+            pass
+
+    if rank == 0 and world == 1:
+        if not args.no_cpu_baseline:
+            log(args, "cpu baseline")
+            cb = cpu_baseline(buf, off_t, len_t, n, args)
+            if cb is not None:
+                ref = cb.pop("_out")
+                cb["parity_vs_gpu"] = bool((ref == crcs[:len(ref)]).all())
+                result["cpu_baseline"] = cb
+        if not args.no_host_path and args.config == "c3":
+            log(args, "host-resident path")
+            del buf
+            torch.cuda.empty_cache()
+            result["host_path"] = host_path_rate(torch, args)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

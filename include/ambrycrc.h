@@ -1,0 +1,160 @@
+/*
+ * ambrycrc.h -- C ABI of libambrycrc, the MI355X (gfx950) CRC-32 engine for
+ * Ambry's per-record / per-chunk checksum path.
+ *
+ * Function: CRC-32/ISO-HDLC (reflected poly 0xEDB88320, init/xorout 0xFFFFFFFF),
+ * bit-exact with com.github.ambry.utils.Crc32 and java.util.zip.CRC32.
+ *
+ * Value convention: zlib-style *finalized* CRCs. A running CRC starts at 0 and
+ * ambrycrc_update(crc, p, n) returns the value Checksum.getValue() would report
+ * after update(p, 0, n) on a checksum whose getValue() was `crc`. Ambry's
+ * Crc32 keeps the bit-inverted register internally (Crc32.java:37-52); its
+ * register equals ~value.
+ *
+ * Ownership: the caller owns every buffer. The library never frees caller
+ * memory and never retains a pointer past the call (for *_dev functions: past
+ * completion of the work it enqueued on the caller's stream). Device tables
+ * and the default workspace belong to a per-device context created by
+ * ambrycrc_init().
+ *
+ * Errors: every int-returning function returns AMBRYCRC_OK (0) or a negative
+ * code; nothing aborts or throws across the ABI. A CRC *mismatch* is data
+ * (ambrycrc_verify_dev's flags), not an error.
+ *
+ * Threading: the host functions are reentrant with no mutable global state.
+ * The *_dev functions may be called from several host threads; each call
+ * enqueues on the caller's stream. Calls that share the context's default
+ * workspace (d_ws == NULL) must not overlap on different streams; pass a
+ * per-stream workspace (ambrycrc_workspace_bytes) to run them concurrently.
+ */
+#ifndef AMBRYCRC_H
+#define AMBRYCRC_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include <hip/hip_runtime_api.h> /* hipStream_t */
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AMBRYCRC_OK 0
+#define AMBRYCRC_EINVAL (-1)   /* bad argument (null pointer, bad size, alignment) */
+#define AMBRYCRC_EHIP (-2)     /* a HIP runtime call failed */
+#define AMBRYCRC_ENOMEM (-3)   /* device or pinned-host allocation failed */
+#define AMBRYCRC_ENOINIT (-4)  /* ambrycrc_init() not called for the current device */
+#define AMBRYCRC_ENODEV (-5)   /* no usable gfx950 device */
+
+/* ---------------------------------------------------------------- lifecycle */
+
+/* Create the context of `device` (LDS table image in HBM, default workspace).
+ * Idempotent. Replaces nothing in the reference: Ambry's Crc32 tables are static
+ * (Crc32.java:154-179); this is where their device copy is made. */
+int ambrycrc_init(int device);
+
+/* Release every context. Outstanding work must have completed. */
+int ambrycrc_shutdown(void);
+
+/* Static, human-readable description of an error code. */
+const char* ambrycrc_strerror(int code);
+
+/* Library version string ("ambrycrc <semver> gfx950"). */
+const char* ambrycrc_version(void);
+
+/* ------------------------------------------------- host streaming primitives */
+
+/* Continue a finalized CRC over n host bytes (CPU; for the small, per-record
+ * updates that cannot amortize a device round trip).
+ * Replaces Crc32.update(byte[],int,int) (ambry-utils/.../utils/Crc32.java:55-98),
+ * Crc32.update(ByteBuffer) (:100-143) and java.util.zip.CRC32.update as used by
+ * CrcInputStream.read/updateCrc (ambry-utils/.../utils/CrcInputStream.java:46-71). */
+uint32_t ambrycrc_update(uint32_t crc, const void* p, size_t n);
+
+/* One byte: Crc32.update(int b) (Crc32.java:146-148). */
+uint32_t ambrycrc_update_byte(uint32_t crc, int b);
+
+/* crc(A||B) from crc(A), crc(B) and |B| (zlib crc32_combine semantics). No Java
+ * counterpart in Ambry; it is what lets a chunk be split across lanes/GPUs and
+ * lets a blob record's CRC be derived from the blob's (PutMessageFormatInputStream.java:116-120). */
+uint32_t ambrycrc_combine(uint32_t crc1, uint32_t crc2, uint64_t len2);
+
+/* CRC of n zero bytes continuing from crc (HardDeleteMessageFormatInputStream's
+ * ZeroBytesInputStream records, ambry-messageformat/.../HardDeleteMessageFormatInputStream.java:58-124). */
+uint32_t ambrycrc_zeros(uint32_t crc, uint64_t n);
+
+/* ------------------------------------------------ device-resident batch path */
+
+/* Bytes of device workspace a batch of n chunks needs. */
+size_t ambrycrc_workspace_bytes(size_t n);
+
+/* CRC-32 of n independent chunks in HBM:
+ *   d_out[i] = crc32(d_crc_in ? d_crc_in[i] : 0, d_base + d_off[i], d_len[i]).
+ * d_off/d_len/d_crc_in/d_out are device arrays; chunks may have any alignment
+ * and length (0 included) and may overlap. Enqueued on `stream`; asynchronous.
+ * d_ws/ws_bytes: optional workspace (>= ambrycrc_workspace_bytes(n)); NULL uses
+ * the context's. Batch form of Crc32.update(ByteBuffer) + getValue() as the
+ * router runs it per chunk (ambry-router/.../PutOperation.java:1700-1703 fill,
+ * :2033-2054 verifyCRC) and of the blob-record CRC
+ * (ambry-messageformat/.../MessageFormatRecord.java:1797-1832). */
+int ambrycrc_batch_dev(const uint8_t* d_base, const uint64_t* d_off, const uint64_t* d_len,
+                       const uint32_t* d_crc_in, uint32_t* d_out, size_t n, void* d_ws, size_t ws_bytes,
+                       hipStream_t stream);
+
+/* As ambrycrc_batch_dev, then compare with d_expected: d_mismatch[i] = 1 iff the
+ * CRC differs (either output pointer may be NULL; *d_mismatch_count is
+ * incremented per mismatch, caller zeroes it). d_out may be NULL (internal).
+ * Batch form of the `actualCRC != expectedCRC` checks of verify-on-read:
+ * MessageFormatRecord.java:1184-1190, 1642-1646, 1823-1829; PutOperation.java:2040-2050. */
+int ambrycrc_verify_dev(const uint8_t* d_base, const uint64_t* d_off, const uint64_t* d_len,
+                        const uint32_t* d_crc_in, const uint32_t* d_expected, uint32_t* d_out,
+                        uint8_t* d_mismatch, uint32_t* d_mismatch_count, size_t n, void* d_ws,
+                        size_t ws_bytes, hipStream_t stream);
+
+/* ------------------------------------------------------- host-resident batch */
+
+/* CRC-32 of n host chunks (ptrs[i], lens[i]) on `device`: chunks are packed into
+ * pinned staging buffers, copied with hipMemcpyAsync on two streams
+ * (double-buffered, copy of slab k+1 overlapping the kernels of slab k) and
+ * CRC'd in HBM. Synchronous. Inputs that already live in pinned memory
+ * (hipHostMalloc / hipHostRegister'd Netty arenas) are copied without a
+ * host-side memcpy when `pinned` is nonzero.
+ * This is the PUT path's entry: the bytes start in a Netty ByteBuf
+ * (ambry-network/.../NettyServerRequest.java:35,54) or a FileChannel prefetch
+ * (ambry-store/.../StoreMessageReadSet.java:170-188). */
+int ambrycrc_batch_host(const void* const* ptrs, const uint64_t* lens, const uint32_t* crc_in, uint32_t* out,
+                        size_t n, int device, int pinned);
+
+/* ------------------------------------------------------- tuning / telemetry */
+
+/* Tile size (log2 bytes, 12..30) the device path splits chunks into. Default 18. */
+int ambrycrc_set_tile_log2(int device, int tile_log2);
+/* Kernel variant (unroll / load policy) of the tiles kernel; 0 = default. */
+int ambrycrc_set_variant(int device, int variant);
+/* Grid size of the persistent tiles kernel (workgroups; 0 = one per CU). */
+int ambrycrc_set_grid(int device, int workgroups);
+
+/* When enabled, every tiles-kernel launch is bracketed by HIP events on the
+ * caller's stream; ambrycrc_timing_collect() waits for them and returns the sum
+ * and count of the kernel durations since the last collect. */
+int ambrycrc_timing_enable(int device, int enable);
+int ambrycrc_timing_collect(int device, double* total_ms, int* launches);
+
+/* Number of workgroups the tiles kernel launches with on `device` (0 if unknown). */
+int ambrycrc_grid_size(int device);
+
+/* ------------------------------------------------------- synthetic data */
+
+/* Fill d_dst with the deterministic splitmix64 byte stream (byte i = byte i&7 of
+ * splitmix64_mix(seed + ((stream_off+i)/8 + 1) * 0x9E3779B97F4A7C15)).
+ * d_dst must be 16-B aligned and stream_off a multiple of 16. For benchmarks. */
+int ambrycrc_fill_random_dev(uint8_t* d_dst, uint64_t nbytes, uint64_t seed, uint64_t stream_off,
+                             hipStream_t stream);
+
+/* Copy of the LDS table image (kLdsBytes + 256 B) into host memory `out` (for
+ * tests that model the kernel on the CPU). Returns the byte size, or <0. */
+long ambrycrc_debug_table_image(uint32_t* out, size_t max_words);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AMBRYCRC_H */

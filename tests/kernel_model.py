@@ -1,0 +1,143 @@
+"""CPU model of the gfx950 tiles kernel (ambry_amd/csrc/crc32_kernels.hip).
+
+Test infrastructure: it replays the kernel's arithmetic -- the LDS image built
+by libambrycrc (ambrycrc_debug_table_image), v_perm_b32 address formation,
+slice-by-4 steps, nibble-table multiplies, the per-lane 1 KiB block hop, the
+6-level wave tree and the tile/chunk decomposition -- lane by lane in numpy,
+so that layout or algebra mistakes show up on the CPU before a GPU run. It is
+checked against zlib/the oracle in tests/test_kernel_model.py.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+K_SLICE_BYTES = 128 * 1024
+K_NIB_BASE = K_SLICE_BYTES
+K_NIB_SET = 512
+K_FOLD_OFF = 0
+K_TREE_OFF = K_FOLD_OFF + K_NIB_SET
+K_POW_OFF = K_TREE_OFF + 6 * K_NIB_SET
+K_POW_TABLES = 36
+K_LDS_BYTES = K_NIB_BASE + K_POW_OFF + K_POW_TABLES * K_NIB_SET
+BLOCK = 1024
+LANES = np.arange(64, dtype=np.uint32)
+
+
+def table_image():
+    from ambry_amd._lib import lib
+
+    words = K_LDS_BYTES // 4 + 64
+    buf = (ctypes.c_uint32 * words)()
+    nbytes = lib().ambrycrc_debug_table_image(buf, words)
+    assert nbytes == words * 4, nbytes
+    return np.frombuffer(buf, dtype=np.uint32).copy()
+
+
+class KernelModel:
+    def __init__(self, img=None):
+        self.img = table_image() if img is None else img
+        self.xpow2 = self.img[K_LDS_BYTES // 4:]
+        col = (LANES & 31) << 2
+        self.L = [((j >> 1) << 16) | ((j & 1) << 7) | col for j in range(4)]
+
+    def lds(self, addr):
+        return self.img[np.asarray(addr, dtype=np.int64) >> 2]
+
+    @staticmethod
+    def perm(L, x, k):
+        # v_perm_b32(L, x, 0x0C06_k_04): byte0 = L.b0, byte1 = x.b_k, byte2 = L.b2, byte3 = 0
+        return (L & 0xFF) | (((x >> (8 * k)) & 0xFF) << 8) | (((L >> 16) & 0xFF) << 16)
+
+    def slice4(self, x, xin):
+        t = (self.lds(self.perm(self.L[3], x, 0)) ^ self.lds(self.perm(self.L[2], x, 1)) ^
+             self.lds(self.perm(self.L[1], x, 2)) ^ self.lds(self.perm(self.L[0], x, 3)))
+        return (t ^ xin).astype(np.uint32)
+
+    def rpiece(self, w, xin):
+        s = self.slice4(w[:, 0], w[:, 1])
+        s = self.slice4(s, w[:, 2])
+        s = self.slice4(s, w[:, 3])
+        return self.slice4(s, xin)
+
+    def nib_mul(self, v, set_off):
+        v = np.asarray(v, dtype=np.uint32)
+        r = np.zeros_like(v)
+        for n in range(8):
+            r ^= self.lds(K_NIB_BASE + set_off + 64 * n + (((v >> (4 * n)) & 15) << 2))
+        return r
+
+    def shift_bytes(self, v, n):
+        v = np.uint32(v)
+        k = 0
+        while n:
+            if n & 1:
+                if k < K_POW_TABLES:
+                    v = self.nib_mul(np.array([v], dtype=np.uint32), K_POW_OFF + K_NIB_SET * k)[0]
+                else:
+                    v = np.uint32(gf2_mul(int(v), int(self.xpow2[k])))
+            n >>= 1
+            k += 1
+        return int(v)
+
+    def body_crc(self, mem: np.ndarray, bs: int, be: int) -> int:
+        nb = (be - bs + BLOCK - 1) // BLOCK
+        if nb == 0:
+            return 0
+        v0 = be - nb * BLOCK
+        s = np.zeros(64, dtype=np.uint32)
+        for b in range(nb):
+            p = v0 + b * BLOCK + 16 * LANES.astype(np.int64)
+            w = np.zeros((64, 4), dtype=np.uint32)
+            for lane in range(64):
+                if p[lane] + 16 > bs:
+                    raw = bytearray(mem[p[lane]:p[lane] + 16].tobytes())
+                    cut = bs - p[lane]
+                    for i in range(max(0, cut)):
+                        raw[i] = 0
+                    w[lane] = np.frombuffer(bytes(raw), dtype="<u4")
+            fold = self.nib_mul(s, K_FOLD_OFF) if b else np.zeros(64, dtype=np.uint32)
+            s = self.rpiece(w, fold)
+        for lvl in range(6):
+            o = s[LANES ^ (1 << lvl)]
+            sh = self.nib_mul(o, K_TREE_OFF + K_NIB_SET * lvl)
+            s = np.where((LANES & (1 << lvl)) != 0, s ^ sh, s).astype(np.uint32)
+        return int(s[63])
+
+    def batch(self, mem: np.ndarray, off, length, crc_in=None, tile_log2: int = 18):
+        """Replays plan + tiles kernels; returns the list of CRCs."""
+        tile = 1 << tile_log2
+        out = []
+        for c, (cs, ln) in enumerate(zip(off, length)):
+            cs, ln = int(cs), int(ln)
+            ce = cs + ln
+            cb = max(cs, ce & ~15)
+            nt = max(1, (cb - cs + tile - 1) >> tile_log2)
+            acc = 0
+            for q in range(nt):
+                m = nt - 1 - q
+                be = cb - m * tile
+                bs = max(cs, be - tile if be > tile else 0)
+                r = self.body_crc(mem, bs, be)
+                r = self.shift_bytes(r, (ce - cb) + m * tile)
+                if m == 0:
+                    tr = 0
+                    for p in range(cb, ce):
+                        tr = (tr >> 8) ^ int(self.lds(((tr ^ int(mem[p])) & 0xFF) << 8))
+                    r ^= tr
+                if q == 0:
+                    cin = 0 if crc_in is None else int(crc_in[c])
+                    r ^= self.shift_bytes((~cin) & 0xFFFFFFFF, ln) ^ 0xFFFFFFFF
+                acc ^= r
+            out.append(acc & 0xFFFFFFFF)
+        return out
+
+
+def gf2_mul(a: int, b: int) -> int:
+    p = 0
+    for i in range(32):
+        if (a >> (31 - i)) & 1:
+            p ^= b
+        b = (b >> 1) ^ (0xEDB88320 if b & 1 else 0)
+    return p

@@ -1,0 +1,126 @@
+"""C ABI: libambrycrc loads, exports every declared symbol, and its host primitives agree
+with the oracle and golden vectors. No device compute here (CPU-only container)."""
+import os
+import re
+import zlib
+
+import numpy as np
+from datagen import stream_bytes
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    text = open(os.path.join(ROOT, "include", "ambrycrc.h")).read()
+    return sorted(set(re.findall(r"\b(ambrycrc_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_exports_every_declared_symbol(ambry):
+    lib = ambry.lib()
+    decl = declared_symbols()
+    assert len(decl) >= 20
+    for name in decl:
+        assert hasattr(lib, name), name
+    assert sorted(ambry.EXPORTED) == decl
+
+
+def test_version_and_errors(ambry):
+    lib = ambry.lib()
+    assert lib.ambrycrc_version().decode().startswith("ambrycrc")
+    for code in (0, -1, -2, -3, -4, -5):
+        assert lib.ambrycrc_strerror(code)
+
+
+def test_host_update_golden(ambry, vectors):
+    for v in vectors["known_answers"] + vectors["message_headers"]:
+        assert ambry.crc32(bytes.fromhex(v["hex"])) == int(v["crc"], 16), v["name"]
+    for v in vectors["random"]:
+        data = stream_bytes(int(v["seed"], 16), v["offset"], v["len"]).tobytes()
+        assert ambry.crc32(data, int(v["crc_in"], 16)) == int(v["crc"], 16)
+
+
+def test_host_update_vs_oracle(ambry, oracle):
+    data = stream_bytes(3, 0, 10000)
+    for n in list(range(0, 40)) + [999, 4096, 10000]:
+        assert ambry.crc32(data[:n].tobytes()) == oracle.crc32(data[:n])
+
+
+def test_crc32_object_mirrors_java(ambry):
+    """Crc32Test.crcTest + update(int)/update(byte[],off,len)/update(ByteBuffer) semantics."""
+    from ambry_amd.crc32 import ByteBufferLike, Crc32
+
+    buf = bytearray(stream_bytes(42, 0, 4000).tobytes())
+    c = Crc32()
+    c.update(buf, 0, 4000)
+    v1 = c.getValue()
+    c = Crc32()
+    c.update(buf, 0, 4000)
+    assert c.getValue() == v1 == zlib.crc32(bytes(buf))
+    buf[3999] = (~buf[3999]) & 0xFF
+    c = Crc32()
+    c.update(buf, 0, 4000)
+    assert c.getValue() != v1
+    # split: bytes, single ints, ByteBuffer (consumed: position == limit afterwards)
+    c = Crc32()
+    c.update(buf, 0, 10)
+    for i in range(10, 20):
+        c.update(buf[i])
+    bb = ByteBufferLike(bytes(buf), position=20)
+    c.update_buffer(bb)
+    assert bb.position == bb.limit == 4000
+    assert c.getValue() == zlib.crc32(bytes(buf))
+    c.reset()
+    assert c.getValue() == 0
+    empty = ByteBufferLike(b"", 0)
+    c.update_buffer(empty)
+    assert c.getValue() == 0
+
+
+def test_combine_and_zeros(ambry, oracle, vectors):
+    data = stream_bytes(8, 0, 100000).tobytes()
+    for cut in (0, 1, 15, 16, 4096, 99999, 100000):
+        a, b = data[:cut], data[cut:]
+        assert ambry.combine(zlib.crc32(a), zlib.crc32(b), len(b)) == zlib.crc32(data)
+        assert ambry.combine(zlib.crc32(a), zlib.crc32(b), len(b)) == oracle.combine(zlib.crc32(a), zlib.crc32(b),
+                                                                                      len(b))
+    for v in vectors["zero_runs"]:
+        assert ambry.zeros(0, v["len"]) == int(v["crc"], 16)
+    assert ambry.zeros(0x12345678, 777) == zlib.crc32(bytes(777), 0x12345678)
+    assert ambry.zeros(5, 0) == 5
+
+
+def test_table_image_layout(ambry):
+    """The LDS image's slice region holds T0..T3 at the v_perm-addressed, lane-replicated slots."""
+    import ctypes
+
+    from kernel_model import K_LDS_BYTES
+
+    words = K_LDS_BYTES // 4 + 64
+    buf = (ctypes.c_uint32 * words)()
+    assert ambry.lib().ambrycrc_debug_table_image(buf, words) == words * 4
+    img = np.frombuffer(buf, dtype=np.uint32)
+    T = [[0] * 256 for _ in range(4)]
+    for b in range(256):
+        c = b
+        for _ in range(8):
+            c = (c >> 1) ^ 0xEDB88320 if c & 1 else c >> 1
+        T[0][b] = c
+    for j in range(1, 4):
+        for b in range(256):
+            T[j][b] = (T[j - 1][b] >> 8) ^ T[0][T[j - 1][b] & 0xFF]
+    for j in range(4):
+        for lane in (0, 5, 31):
+            for b in (0, 1, 128, 255):
+                addr = ((j >> 1) << 16) | (b << 8) | ((j & 1) << 7) | (lane << 2)
+                assert img[addr >> 2] == T[j][b]
+
+
+def test_batch_dev_without_init_fails_loudly(ambry):
+    """No silent fallback: without a device context the device entry point errors."""
+    import ctypes
+
+    from ambry_amd._lib import AMBRYCRC_ENOINIT
+
+    rc = ambry.lib().ambrycrc_batch_dev(ctypes.c_void_p(16), ctypes.c_void_p(16), ctypes.c_void_p(16), None,
+                                        ctypes.c_void_p(16), 1, None, 0, None)
+    assert rc == AMBRYCRC_ENOINIT

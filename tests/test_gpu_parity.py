@@ -1,0 +1,253 @@
+"""GPU parity: libambrycrc's gfx950 kernels (through the C ABI) vs the CPU oracle and golden vectors.
+
+Bit-exact comparisons only (integer path). Full-size configs (C2, C3) are checked
+through size-independent properties: per-chunk samples against the oracle, the
+whole region as one chunk vs the combine-fold of the per-chunk CRCs, determinism.
+"""
+import numpy as np
+import pytest
+
+from datagen import stream_bytes, zipf_sizes
+
+pytestmark = pytest.mark.gpu
+
+
+def _torch():
+    import torch
+
+    return torch
+
+
+def dev_bytes(arr: np.ndarray):
+    torch = _torch()
+    return torch.from_numpy(np.ascontiguousarray(arr, dtype=np.uint8)).cuda()
+
+
+def dev_u64(vals):
+    torch = _torch()
+    return torch.tensor(np.asarray(vals, dtype=np.int64), dtype=torch.int64, device="cuda")
+
+
+def host_u32(t):
+    return t.cpu().numpy().view(np.uint32)
+
+
+def run_batch(gpu, mem_np, off, ln, crc_in=None, mem_dev=None):
+    torch = _torch()
+    base = dev_bytes(mem_np) if mem_dev is None else mem_dev
+    cin = None if crc_in is None else torch.from_numpy(np.asarray(crc_in, dtype=np.uint32).view(np.int32)).cuda()
+    out = gpu.crc32_batch(base, dev_u64(off), dev_u64(ln), crc_in=cin)
+    torch.cuda.synchronize()
+    return host_u32(out)
+
+
+def test_fill_matches_generator(gpu):
+    torch = _torch()
+    for n, soff in ((1 << 20, 0), (12345, 16), (17, 4096)):
+        buf = torch.empty(n, dtype=torch.uint8, device="cuda")
+        gpu.fill_random(buf, 0xA3B1C2D3, soff)
+        torch.cuda.synchronize()
+        assert np.array_equal(buf.cpu().numpy(), stream_bytes(0xA3B1C2D3, soff, n))
+
+
+def test_known_answers_on_device(gpu, vectors):
+    items = [bytes.fromhex(v["hex"]) for v in vectors["known_answers"] + vectors["message_headers"]]
+    items += [bytes(v["len"]) for v in vectors["zero_runs"]]
+    expect = [int(v["crc"], 16) for v in vectors["known_answers"] + vectors["message_headers"] + vectors["zero_runs"]]
+    pos, off, mem = 0, [], bytearray()
+    for i, b in enumerate(items):
+        pad = (-(len(mem)) + (i % 16)) % 64  # varied alignment
+        mem += bytes(pad)
+        off.append(len(mem))
+        mem += b
+    got = run_batch(gpu, np.frombuffer(bytes(mem), dtype=np.uint8), off, [len(b) for b in items])
+    assert list(got) == expect
+
+
+def test_golden_random_vectors(gpu, vectors):
+    rnd = vectors["random"]
+    mem, off, ln, cin = bytearray(), [], [], []
+    for v in rnd:
+        data = stream_bytes(int(v["seed"], 16), v["offset"], v["len"]).tobytes()
+        mem += bytes((v["offset"] - len(mem)) % 64)  # keep the fixture's misalignment
+        off.append(len(mem))
+        ln.append(len(data))
+        cin.append(int(v["crc_in"], 16))
+        mem += data
+    got = run_batch(gpu, np.frombuffer(bytes(mem), dtype=np.uint8), off, ln, crc_in=cin)
+    assert [f"0x{x:08x}" for x in got] == [v["crc"] for v in rnd]
+
+
+def test_every_small_length_and_alignment(gpu, oracle):
+    mem = stream_bytes(99, 0, 1 << 16)
+    off, ln = [], []
+    for a in range(16):
+        for n in range(0, 80):
+            off.append(1000 + 113 * len(off) % 60000 // 16 * 16 + a)
+            ln.append(n)
+    got = run_batch(gpu, mem, off, ln)
+    assert np.array_equal(got, oracle.batch(mem, off, ln))
+
+
+@pytest.mark.parametrize("tile_log2", [12, 13, 16, 18, 20])
+def test_ragged_batch_tile_sizes(gpu, oracle, tile_log2):
+    rng = np.random.default_rng(tile_log2)
+    mem = stream_bytes(5, 0, 24 << 20)
+    n = 300
+    ln = rng.integers(0, 3 << 20, size=n)
+    ln[:20] = [0, 1, 15, 16, 17, 1023, 1024, 1025, 4095, 4096, 4097, 65535, 65536, 65537, 262143, 262144, 262145,
+               (1 << 20) - 1, 1 << 20, (1 << 20) + 1]
+    off = rng.integers(0, (24 << 20) - (3 << 20), size=n)
+    off[::3] = off[::3] // 16 * 16
+    gpu.set_tile_log2(0, tile_log2)
+    try:
+        got = run_batch(gpu, mem, off, ln)
+    finally:
+        gpu.set_tile_log2(0, 18)
+    assert np.array_equal(got, oracle.batch(mem, off, ln, threads=8))
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+def test_kernel_variants(gpu, oracle, variant):
+    rng = np.random.default_rng(100 + variant)
+    mem = stream_bytes(6, 0, 16 << 20)
+    ln = rng.integers(0, 2 << 20, size=64)
+    off = rng.integers(0, (16 << 20) - (2 << 20), size=64)
+    gpu.set_variant(0, variant)
+    try:
+        got = run_batch(gpu, mem, off, ln)
+    finally:
+        gpu.set_variant(0, 0)
+    assert np.array_equal(got, oracle.batch(mem, off, ln, threads=8))
+
+
+def test_crc_in_streaming_composition(gpu, oracle):
+    """update(A) then update(B) == update(A||B): PutOperation's slice-by-slice fill (PutOperation.java:1700-1703)."""
+    torch = _torch()
+    mem = stream_bytes(12, 0, 9 << 20)
+    base = dev_bytes(mem)
+    cuts = [0, 1, 16, 1000, 1 << 20, (4 << 20) + 3, 9 << 20]
+    whole = oracle.crc32(mem)
+    for cut in cuts:
+        a = gpu.crc32_batch(base, dev_u64([0]), dev_u64([cut]))
+        b = gpu.crc32_batch(base, dev_u64([cut]), dev_u64([(9 << 20) - cut]), crc_in=a)
+        torch.cuda.synchronize()
+        assert host_u32(b)[0] == whole
+
+
+def test_verify_flags_zipf(gpu, oracle):
+    """C4 in miniature: Zipf sizes, 1% single-bit flips; flags must match exactly."""
+    torch = _torch()
+    sizes = zipf_sizes(2000, seed=20261015) // 16  # scaled down 16x (256 B .. 256 KiB)
+    off = np.concatenate([[0], np.cumsum((sizes + 15) // 16 * 16)[:-1]]).astype(np.int64)
+    total = int(off[-1] + sizes[-1])
+    mem = stream_bytes(20261015, 0, total)
+    expected = oracle.batch(mem, off, sizes, threads=8)
+    rng = np.random.default_rng(1)
+    bad = rng.choice(len(sizes), size=20, replace=False)
+    corrupt = mem.copy()
+    for i in bad:
+        pos = off[i] + rng.integers(0, sizes[i])
+        corrupt[pos] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    exp_dev = torch.from_numpy(expected.view(np.int32)).cuda()
+    crc, mism, count = gpu.crc32_verify(dev_bytes(corrupt), dev_u64(off), dev_u64(sizes), exp_dev)
+    torch.cuda.synchronize()
+    flags = mism.cpu().numpy()
+    assert set(np.nonzero(flags)[0]) == set(int(i) for i in bad)
+    assert int(count.item()) == len(bad)
+    assert np.array_equal(host_u32(crc), oracle.batch(corrupt, off, sizes, threads=8))
+
+
+def test_overlapping_and_repeated_chunks(gpu, oracle):
+    mem = stream_bytes(31, 0, 1 << 20)
+    off = [0, 0, 5, 5, 100, 0, 65536]
+    ln = [1 << 20, 1 << 20, 1000, 1000, 200000, 0, 300000]
+    assert np.array_equal(run_batch(gpu, mem, off, ln), oracle.batch(mem, off, ln))
+
+
+def test_separate_workspaces_two_streams(gpu, oracle):
+    torch = _torch()
+    from ambry_amd._lib import lib
+
+    mem = stream_bytes(44, 0, 8 << 20)
+    base = dev_bytes(mem)
+    n = 128
+    rng = np.random.default_rng(3)
+    off = rng.integers(0, 4 << 20, size=n)
+    ln = rng.integers(0, 4 << 20, size=n)
+    wsz = lib().ambrycrc_workspace_bytes(n)
+    outs = []
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for s in streams:
+        ws = torch.empty(wsz, dtype=torch.uint8, device="cuda")
+        with torch.cuda.stream(s):
+            outs.append((gpu.crc32_batch(base, dev_u64(off), dev_u64(ln), workspace=ws, stream=s), ws))
+    torch.cuda.synchronize()
+    exp = oracle.batch(mem, off, ln, threads=8)
+    for o, _ in outs:
+        assert np.array_equal(host_u32(o), exp)
+
+
+def _full_size_check(gpu, oracle, n_chunks, chunk, seed, sample):
+    """Whole config resident in HBM; sampled chunks vs oracle; region-as-one-chunk vs combine-fold."""
+    torch = _torch()
+    import ambry_amd
+
+    total = n_chunks * chunk
+    buf = torch.empty(total, dtype=torch.uint8, device="cuda")
+    gpu.fill_random(buf, seed, 0)
+    off = dev_u64(np.arange(n_chunks, dtype=np.int64) * chunk)
+    ln = dev_u64(np.full(n_chunks, chunk, dtype=np.int64))
+    out1 = gpu.crc32_batch(buf, off, ln)
+    out2 = gpu.crc32_batch(buf, off, ln)
+    whole = gpu.crc32_batch(buf, dev_u64([0]), dev_u64([total]))
+    torch.cuda.synchronize()
+    c1, c2 = host_u32(out1), host_u32(out2)
+    assert np.array_equal(c1, c2)
+    fold = 0
+    for c in c1:
+        fold = ambry_amd.combine(fold, int(c), chunk)
+    assert fold == int(host_u32(whole)[0])
+    rng = np.random.default_rng(seed)
+    for i in sorted(set([0, n_chunks - 1] + list(rng.integers(0, n_chunks, size=sample)))):
+        data = buf[i * chunk:(i + 1) * chunk].cpu().numpy()
+        assert oracle.crc32(data) == int(c1[i]), i
+    del buf
+
+
+def test_c2_full_size(gpu, oracle):
+    """C2: 65,536 x 64 KiB."""
+    _full_size_check(gpu, oracle, 65536, 64 << 10, 0xC2, sample=64)
+
+
+def test_c3_full_size(gpu, oracle):
+    """C3 (headline): 8,192 x 4 MiB = 32 GiB resident."""
+    _full_size_check(gpu, oracle, 8192, 4 << 20, 0xC3, sample=12)
+
+
+def test_host_resident_path(gpu, oracle):
+    """ambrycrc_batch_host: pageable and pinned inputs, including a chunk larger than one staging slab."""
+    torch = _torch()
+    rng = np.random.default_rng(8)
+    lens = [0, 1, 17, 4096, 1 << 20, (300 << 20) + 5, 65536, 3]
+    chunks = [torch.from_numpy(stream_bytes(int(rng.integers(1 << 30)), 0, n)) for n in lens]
+    exp = [oracle.crc32(c.numpy()) for c in chunks]
+    assert gpu.crc32_batch_host(chunks, device=0, pinned=False) == exp
+    pinned = [c.pin_memory() for c in chunks]
+    assert gpu.crc32_batch_host(pinned, device=0, pinned=True) == exp
+    cin = [(i * 0x01000193) & 0xFFFFFFFF for i in range(len(lens))]
+    exp2 = [oracle.crc32(c.numpy(), ci) for c, ci in zip(chunks, cin)]
+    assert gpu.crc32_batch_host(chunks, device=0, pinned=False, crc_in=cin) == exp2
+
+
+def test_timing_hook(gpu):
+    torch = _torch()
+    gpu.timing_enable(0, True)
+    try:
+        buf = torch.empty(64 << 20, dtype=torch.uint8, device="cuda")
+        gpu.fill_random(buf, 1, 0)
+        gpu.crc32_batch(buf, dev_u64([0]), dev_u64([64 << 20]))
+        ms, cnt = gpu.timing_collect(0)
+        assert cnt == 1 and ms > 0
+    finally:
+        gpu.timing_enable(0, False)
