@@ -113,15 +113,17 @@ __device__ __forceinline__ uint32_t body_crc(const uint8_t* __restrict__ base, u
                                              uint32_t lane, const LaneConst& k) {
   const uint64_t nb = (be - bs + kBlockBytes - 1) / kBlockBytes;
   if (nb == 0) return 0u;
-  const uint64_t v0 = be - nb * kBlockBytes;
+  // The virtual start may precede the allocation (chunk in its first KiB): signed
+  // arithmetic, and only lanes whose piece reaches bs ever form a load address.
+  const int64_t v0 = (int64_t)be - (int64_t)(nb * kBlockBytes);
   const u32x4* q = reinterpret_cast<const u32x4*>(base + v0) + lane;
 
   // Block 0 carries the (possibly unaligned) start: mask what lies before bs.
   u32x4 w = {0u, 0u, 0u, 0u};
-  const uint64_t p = v0 + 16u * lane;
-  if (p + 16u > bs) {
-    w = ld16<NT>(q);
-    if (p < bs) {
+  const int64_t p = v0 + 16 * (int64_t)lane;
+  if (p + 16 > (int64_t)bs) {  // => p >= floor16(bs) >= 0: inside the caller's buffer
+    w = ld16<NT>(reinterpret_cast<const u32x4*>(base + p));
+    if (p < (int64_t)bs) {
       const uint32_t cut = (uint32_t)(bs - p);  // 1..15 leading bytes to drop
 #pragma unroll
       for (int d = 0; d < 4; ++d) {

@@ -92,6 +92,8 @@ class KernelModel:
             w = np.zeros((64, 4), dtype=np.uint32)
             for lane in range(64):
                 if p[lane] + 16 > bs:
+                    # the kernel's load-address invariant: inside [floor16(bs), be)
+                    assert (bs & ~15) <= p[lane] and p[lane] + 16 <= be, (bs, be, p[lane])
                     raw = bytearray(mem[p[lane]:p[lane] + 16].tobytes())
                     cut = bs - p[lane]
                     for i in range(max(0, cut)):

@@ -20,7 +20,7 @@ def _torch():
 
 def dev_bytes(arr: np.ndarray):
     torch = _torch()
-    return torch.from_numpy(np.ascontiguousarray(arr, dtype=np.uint8)).cuda()
+    return torch.from_numpy(np.array(arr, dtype=np.uint8, copy=True)).cuda()
 
 
 def dev_u64(vals):
