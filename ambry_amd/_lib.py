@@ -40,7 +40,6 @@ _SIGNATURES = [
     ("ambrycrc_batch_host", ctypes.c_int,
      [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32),
       ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t, ctypes.c_int, ctypes.c_int]),
-    ("ambrycrc_set_tile_log2", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     ("ambrycrc_set_variant", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     ("ambrycrc_set_grid", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     ("ambrycrc_timing_enable", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
@@ -49,6 +48,7 @@ _SIGNATURES = [
     ("ambrycrc_grid_size", ctypes.c_int, [ctypes.c_int]),
     ("ambrycrc_fill_random_dev", ctypes.c_int,
      [_u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]),
+    ("ambrycrc_debug_readbw_dev", ctypes.c_int, [_u8p, ctypes.c_uint64, _u8p, ctypes.c_int, ctypes.c_void_p]),
     ("ambrycrc_debug_table_image", ctypes.c_long, [ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t]),
 ]
 

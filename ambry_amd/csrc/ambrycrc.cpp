@@ -110,8 +110,7 @@ struct DevCtx {
   int device = -1;
   int num_cu = 0;
   int grid = 0;
-  int variant = 0;
-  int tile_log2 = 18;
+  int variant = 1;  // U=8, nontemporal loads, rolling prefetch (tools/sweep.py)
   uint32_t* d_img = nullptr;
   void* d_ws = nullptr;
   size_t ws_bytes = 0;
@@ -139,7 +138,11 @@ DevCtx* ctx_current() {
   return ctx_for(dev);
 }
 
-size_t ws_need(size_t n) { return ((n + 1) * sizeof(uint32_t) + 255) & ~size_t(255); }
+// workspace: byte_start[n+1] | block_sum[ceil(n/kPlanPerBlock)]  (uint64)
+size_t ws_need(size_t n) {
+  const size_t blocks = (n + kPlanPerBlock - 1) / kPlanPerBlock;
+  return ((n + 1 + blocks) * sizeof(uint64_t) + 255) & ~size_t(255);
+}
 
 int ensure_ws(DevCtx* c, size_t need) {
   if (c->ws_bytes >= need) return AMBRYCRC_OK;
@@ -161,20 +164,20 @@ int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uin
   PlanArgs p;
   p.off = off;
   p.len = len;
+  p.crc_in = crc_in;
   p.n = (uint32_t)n;
-  p.tile_log2 = (uint32_t)c->tile_log2;
-  p.tile_start = static_cast<uint32_t*>(ws);
+  p.byte_start = static_cast<uint64_t*>(ws);
+  p.block_sum = p.byte_start + n + 1;
   p.out = out;
   hipError_t e = launch_plan(p, s);
   if (e != hipSuccess) return AMBRYCRC_EHIP;
-  TilesArgs t;
+  SweepArgs t;
   t.base = base;
   t.off = off;
   t.len = len;
   t.crc_in = crc_in;
   t.n = (uint32_t)n;
-  t.tile_log2 = (uint32_t)c->tile_log2;
-  t.tile_start = p.tile_start;
+  t.byte_start = p.byte_start;
   t.img = c->d_img;
   t.out = out;
   EventPair ev{nullptr, nullptr};
@@ -188,7 +191,7 @@ int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uin
     }
     if (hipEventRecord(ev.a, s) != hipSuccess) return AMBRYCRC_EHIP;
   }
-  e = launch_tiles(t, c->grid, c->variant, s);
+  e = launch_sweep(t, c->grid, c->variant, s);
   if (e != hipSuccess) return AMBRYCRC_EHIP;
   if (c->timing) {
     if (hipEventRecord(ev.b, s) != hipSuccess) return AMBRYCRC_EHIP;
@@ -323,7 +326,6 @@ int ambrycrc_init(int device) {
   c->device = device;
   c->num_cu = prop.multiProcessorCount;
   c->grid = c->num_cu;
-  if (const char* v = getenv("AMBRYCRC_TILE_LOG2")) c->tile_log2 = std::min(30, std::max(12, atoi(v)));
   if (const char* v = getenv("AMBRYCRC_VARIANT")) c->variant = atoi(v);
   std::vector<uint32_t> img = build_table_image();
   if (hipMalloc(reinterpret_cast<void**>(&c->d_img), img.size() * 4) != hipSuccess) {
@@ -496,18 +498,10 @@ int ambrycrc_batch_host(const void* const* ptrs, const uint64_t* lens, const uin
   return AMBRYCRC_OK;
 }
 
-int ambrycrc_set_tile_log2(int device, int tile_log2) {
-  DevCtx* c = ctx_for(device);
-  if (!c) return AMBRYCRC_ENOINIT;
-  if (tile_log2 < 12 || tile_log2 > 30) return AMBRYCRC_EINVAL;
-  c->tile_log2 = tile_log2;
-  return AMBRYCRC_OK;
-}
-
 int ambrycrc_set_variant(int device, int variant) {
   DevCtx* c = ctx_for(device);
   if (!c) return AMBRYCRC_ENOINIT;
-  if (variant < 0 || variant > 3) return AMBRYCRC_EINVAL;
+  if (variant < 0 || variant >= kNumVariants) return AMBRYCRC_EINVAL;
   c->variant = variant;
   return AMBRYCRC_OK;
 }
@@ -557,6 +551,14 @@ int ambrycrc_fill_random_dev(uint8_t* d_dst, uint64_t nbytes, uint64_t seed, uin
   if (nbytes == 0) return AMBRYCRC_OK;
   if (!d_dst || (reinterpret_cast<uintptr_t>(d_dst) & 15) || (stream_off & 15)) return AMBRYCRC_EINVAL;
   return hip_err(launch_fill(d_dst, nbytes, seed, stream_off, stream));
+}
+
+int ambrycrc_debug_readbw_dev(const uint8_t* d_base, uint64_t nbytes, uint32_t* d_out, int variant,
+                              hipStream_t stream) {
+  DevCtx* c = ctx_current();
+  if (!c) return AMBRYCRC_ENOINIT;
+  if (!d_base || !d_out) return AMBRYCRC_EINVAL;
+  return hip_err(launch_readbw(d_base, nbytes, d_out, c->grid, variant, stream));
 }
 
 long ambrycrc_debug_table_image(uint32_t* out, size_t max_words) {

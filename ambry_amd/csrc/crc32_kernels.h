@@ -7,30 +7,38 @@
 namespace ambrycrc {
 
 struct PlanArgs {
-  const uint64_t* off;   // [n] byte offsets of chunks from base
-  const uint64_t* len;   // [n] chunk lengths
+  const uint64_t* off;     // [n] byte offsets of chunks from base
+  const uint64_t* len;     // [n] chunk lengths
+  const uint32_t* crc_in;  // [n] or null
   uint32_t n;
-  uint32_t tile_log2;
-  uint32_t* tile_start;  // [n+1] exclusive prefix of tiles per chunk; [n] = total
-  uint32_t* out;         // [n] zeroed here, XOR-accumulated by the tiles kernel
+  uint64_t* byte_start;    // [n+1] exclusive scan of len; [n] = total bytes
+  uint64_t* block_sum;     // [ceil(n / kPlanPerBlock)] scratch
+  uint32_t* out;           // [n] initialised here, XOR-accumulated by the sweep kernel
 };
 
-struct TilesArgs {
+constexpr uint32_t kPlanPerBlock = 2048;  // chunks per planning workgroup
+constexpr uint64_t kShareQuantum = 1024;  // per-wave byte shares are multiples of this
+
+struct SweepArgs {
   const uint8_t* base;
   const uint64_t* off;
   const uint64_t* len;
   const uint32_t* crc_in;  // [n] or null: zlib-style running CRC to continue from
   uint32_t n;
-  uint32_t tile_log2;
-  const uint32_t* tile_start;
+  const uint64_t* byte_start;
   const uint32_t* img;     // LDS image (kLdsBytes) followed by 64 words x^(8*2^k)
   uint32_t* out;
 };
 
+// sweep-kernel variants: {U = 8,8,4,16} x {rolling prefetch (0-3), batch loads (4-7)}; 1,5 = nontemporal
+constexpr int kNumVariants = 8;
+
 hipError_t launch_plan(const PlanArgs& a, hipStream_t s);
-hipError_t launch_tiles(const TilesArgs& a, int grid, int variant, hipStream_t s);
+hipError_t launch_sweep(const SweepArgs& a, int grid, int variant, hipStream_t s);
 hipError_t launch_verify(const uint32_t* crc, const uint32_t* expected, uint8_t* mismatch, uint32_t* count,
                          uint32_t n, hipStream_t s);
+hipError_t launch_readbw(const uint8_t* base, uint64_t nbytes, uint32_t* out, int grid, int variant,
+                         hipStream_t s);
 hipError_t launch_fill(uint8_t* dst, uint64_t nbytes, uint64_t seed, uint64_t stream_off, hipStream_t s);
 
 }  // namespace ambrycrc

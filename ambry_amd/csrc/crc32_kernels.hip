@@ -7,21 +7,22 @@
 // MessageFormatRecord.java:1797-1832). Results are bit-exact CRC-32/ISO-HDLC.
 //
 // Work decomposition
-//   chunk  -> tiles of <= 2^tile_log2 bytes, aligned to the chunk's 16-B-aligned
-//             end (so every tile but the first is a whole number of 16-B pieces)
-//   tile   -> one wavefront; the wave sweeps the tile in 1 KiB blocks, lane l
-//             owning bytes [16l, 16l+16) of every block (one coalesced
+//   batch  -> the chunks viewed as one concatenated byte stream; wave w of the
+//             persistent grid owns an equal share [w*S, (w+1)*S) of it (exact byte
+//             balance for any chunk-size mix), cut points snapped to 16 B in memory
+//   segment-> a (wave, chunk) intersection; the wave sweeps it in 1 KiB blocks,
+//             lane l owning bytes [16l, 16l+16) of every block (one coalesced
 //             global_load_dwordx4 per block per lane)
 //   lane   -> slice-by-4 over its 16-B piece using LDS byte tables that one
 //             v_perm_b32 addresses; the lane state hops one block with an
 //             x^(8*1024) nibble-table multiply (independent of the piece's own
 //             table walk, so consecutive pieces overlap)
 //   wave   -> 6-level xor-shuffle tree, level l shifting by 16*2^l bytes
-//   tile   -> shifted by its distance to the chunk end and atomically XORed into
+//   segment-> shifted by its distance to the chunk end and atomically XORed into
 //             out[chunk] (XOR is exact and order-free => deterministic)
 //
 // LDS layout: crc32_layout.h. One 1024-thread workgroup per CU (the image is
-// ~150 KiB), persistent over the tile list.
+// ~150 KiB), persistent: each wave walks its own byte share.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -108,7 +109,7 @@ __device__ __forceinline__ u32x4 ld16(const u32x4* p) {
 // Raw CRC of body [bs, be) (be 16-aligned, bs <= be arbitrary), returned in lane 63
 // (other lanes: junk). Bytes below bs are treated as zeros, which leave a zero
 // register unchanged, so the virtual range is aligned down to whole 1 KiB blocks.
-template <int U, bool NT>
+template <int U, bool NT, bool PIPE>
 __device__ __forceinline__ uint32_t body_crc(const uint8_t* __restrict__ base, uint64_t bs, uint64_t be,
                                              uint32_t lane, const LaneConst& k) {
   const uint64_t nb = (be - bs + kBlockBytes - 1) / kBlockBytes;
@@ -136,12 +137,33 @@ __device__ __forceinline__ uint32_t body_crc(const uint8_t* __restrict__ base, u
   uint32_t s = rpiece(w, k, 0u);
 
   uint64_t b = 1;
-  for (; b + U <= nb; b += U) {
-    u32x4 buf[U];
+  if constexpr (PIPE) {
+    // Rolling prefetch: the slot a piece is consumed from is refilled with the piece
+    // U blocks ahead, so each lane keeps U x 16 B loads in flight continuously.
+    if (nb >= 1 + 2 * (uint64_t)U) {
+      u32x4 buf[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) buf[u] = ld16<NT>(q + (b + u) * (kBlockBytes / 16));
+      for (int u = 0; u < U; ++u) buf[u] = ld16<NT>(q + (b + u) * (kBlockBytes / 16));
+      for (; b + 2 * U <= nb; b += U) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) s = rpiece(buf[u], k, nib_mul(s, kFoldOff));
+        for (int u = 0; u < U; ++u) {
+          const u32x4 w = buf[u];
+          buf[u] = ld16<NT>(q + (b + U + u) * (kBlockBytes / 16));
+          s = rpiece(w, k, nib_mul(s, kFoldOff));
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) s = rpiece(buf[u], k, nib_mul(s, kFoldOff));
+      b += U;
+    }
+  } else {
+    for (; b + U <= nb; b += U) {
+      u32x4 buf[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) buf[u] = ld16<NT>(q + (b + u) * (kBlockBytes / 16));
+#pragma unroll
+      for (int u = 0; u < U; ++u) s = rpiece(buf[u], k, nib_mul(s, kFoldOff));
+    }
   }
   for (; b < nb; ++b) {
     const u32x4 x = ld16<NT>(q + b * (kBlockBytes / 16));
@@ -158,19 +180,19 @@ __device__ __forceinline__ uint32_t body_crc(const uint8_t* __restrict__ base, u
   return s;
 }
 
-// Find chunk c with tile_start[c] <= t < tile_start[c+1], searching [lo, n).
-__device__ __forceinline__ uint32_t find_chunk(const uint32_t* __restrict__ tile_start, uint32_t n, uint32_t t,
-                                               uint32_t lo, uint32_t lane) {
-  uint32_t hi = n;
+// Largest c in [0, n) with byte_start[c] <= g (byte_start nondecreasing, byte_start[0] = 0).
+// 64-ary search: one coalesced probe per lane per round, log64(n) rounds.
+__device__ __forceinline__ uint32_t find_chunk(const uint64_t* __restrict__ byte_start, uint32_t n, uint64_t g,
+                                               uint32_t lane) {
+  uint32_t lo = 0, hi = n;  // invariant: byte_start[lo] <= g, answer in [lo, hi)
   while (hi - lo > 1) {
     const uint32_t step = (hi - lo + 63) / 64;
     const uint32_t idx = lo + lane * step;
-    const bool ok = idx < hi && tile_start[idx] <= t;
+    const bool ok = idx < hi && byte_start[idx] <= g;
     const uint64_t m = __ballot(ok);
     const uint32_t last = 63u - (uint32_t)__builtin_clzll(m);
-    const uint32_t nlo = lo + last * step;
     const uint32_t nhi = lo + (last + 1) * step;
-    lo = nlo;
+    lo = lo + last * step;
     hi = nhi < hi ? nhi : hi;
   }
   return lo;
@@ -181,9 +203,21 @@ __device__ __forceinline__ uint64_t aligned_end(uint64_t s, uint64_t e) {
   return b < s ? s : b;
 }
 
-template <int U, bool NT>
-__global__ __launch_bounds__(1024) void crc32_tiles_kernel(TilesArgs a) {
-  // Stage the table image (SLICE + nibble constants) into LDS once per workgroup.
+// Chunk-relative cut for global stream position g inside chunk c (0 < r < len):
+// snapped so the memory address is 16-B aligned. Pure function of (g, chunk), so the
+// two waves meeting at g agree on it.
+__device__ __forceinline__ uint64_t snap_cut(uint64_t cs, uint64_t len, uint64_t r) {
+  const uint64_t a = (cs + r + 15) & ~uint64_t(15);
+  const uint64_t rr = a - cs;
+  return rr < len ? rr : len;
+}
+
+// Persistent sweep: wave w owns global bytes [w*share, (w+1)*share) of the batch viewed
+// as one concatenated stream (byte_start = exclusive scan of len), i.e. an equal share of
+// bytes whatever the chunk-size mix. Each (wave, chunk) intersection is a segment whose
+// raw CRC is shifted to the chunk end and XORed into out[chunk].
+template <int U, bool NT, bool PIPE>
+__global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
   {
     const u32x4* src = reinterpret_cast<const u32x4*>(a.img);
     u32x4* dst = reinterpret_cast<u32x4*>(g_lds);
@@ -194,75 +228,100 @@ __global__ __launch_bounds__(1024) void crc32_tiles_kernel(TilesArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t waves_per_block = blockDim.x >> 6;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * waves_per_block + (threadIdx.x >> 6));
-  const uint32_t nwaves = gridDim.x * waves_per_block;
-  const uint32_t total = a.tile_start[a.n];
+  const uint64_t nwaves = (uint64_t)gridDim.x * waves_per_block;
+  const uint64_t total = a.byte_start[a.n];
+  const uint64_t share = ((total + nwaves - 1) / nwaves + kShareQuantum - 1) & ~uint64_t(kShareQuantum - 1);
+  const uint64_t g0 = (uint64_t)wave * share;
+  if (share == 0 || g0 >= total) return;
+  const uint64_t g1 = g0 + share < total ? g0 + share : total;
   const uint32_t* xpow2 = a.img + kLdsBytes / 4;
   const LaneConst k = make_lane_const(lane);
-  const uint64_t tile = 1ull << a.tile_log2;
 
-  uint32_t c_lo = 0;
-  for (uint32_t t = wave; t < total; t += nwaves) {
-    const uint32_t c = __builtin_amdgcn_readfirstlane(find_chunk(a.tile_start, a.n, t, c_lo, lane));
-    c_lo = c;
+  for (uint32_t c = __builtin_amdgcn_readfirstlane(find_chunk(a.byte_start, a.n, g0, lane)); c < a.n; ++c) {
+    const uint64_t bsc = a.byte_start[c];
+    if (bsc >= g1) break;
+    const uint64_t len = a.len[c];
+    if (len == 0) continue;  // empty chunks are finished by the plan kernel
     const uint64_t cs = a.off[c];
-    const uint64_t ce = cs + a.len[c];
+    const uint64_t ce = cs + len;
     const uint64_t cb = aligned_end(cs, ce);
-    const uint32_t nt = a.tile_start[c + 1] - a.tile_start[c];
-    const uint32_t q = t - a.tile_start[c];  // 0 = first tile of the chunk
-    const uint64_t m = nt - 1 - q;           // tiles after this one
-    const uint64_t be = cb - m * tile;
-    const uint64_t bs0 = be > tile ? be - tile : 0;
-    const uint64_t bs = bs0 > cs ? bs0 : cs;
-
-    uint32_t r = body_crc<U, NT>(a.base, bs, be, lane, k);
-    r = __builtin_amdgcn_readlane(r, 63);
-    r = shift_bytes(r, (ce - cb) + m * tile, xpow2);
-    if (m == 0) {  // trailing <16 bytes of the chunk, byte-wise through T0 (lane column 0)
+    const uint64_t r0 = g0 > bsc ? snap_cut(cs, len, g0 - bsc) : 0;
+    const uint64_t r1 = g1 - bsc < len ? snap_cut(cs, len, g1 - bsc) : len;
+    if (r0 >= r1) continue;
+    const uint64_t sa = cs + r0, se = cs + r1;
+    const uint64_t be = se == ce ? cb : se;  // 16-B aligned body end
+    uint32_t r = 0;
+    if (sa < be) {
+      r = body_crc<U, NT, PIPE>(a.base, sa, be, lane, k);
+      r = __builtin_amdgcn_readlane(r, 63);
+      r = shift_bytes(r, ce - be, xpow2);
+    }
+    if (se == ce) {  // trailing < 16 bytes, byte-wise through T0 (lane column 0)
       uint32_t tr = 0;
-      for (uint64_t p = cb; p < ce; ++p) tr = (tr >> 8) ^ lds_rd(((tr ^ a.base[p]) & 0xffu) << 8);
+      for (uint64_t p = sa > cb ? sa : cb; p < ce; ++p) tr = (tr >> 8) ^ lds_rd(((tr ^ a.base[p]) & 0xffu) << 8);
       r ^= tr;
     }
-    if (q == 0) {  // initial register: ~crc_in advanced over the whole chunk, plus xor-out
+    if (r0 == 0) {  // initial register ~crc_in advanced over the chunk, plus xor-out
       const uint32_t cin = a.crc_in ? a.crc_in[c] : 0u;
-      r ^= shift_bytes(~cin, ce - cs, xpow2) ^ 0xFFFFFFFFu;
+      r ^= shift_bytes(~cin, len, xpow2) ^ 0xFFFFFFFFu;
     }
     if (lane == 0) atomicXor(&a.out[c], r);
   }
 }
 
-// Exclusive scan of per-chunk tile counts (one workgroup) + zero the outputs.
-__global__ __launch_bounds__(1024) void crc32_plan_kernel(PlanArgs a) {
-  __shared__ uint32_t part[1024];
-  const uint32_t tid = threadIdx.x;
-  const uint32_t per = (a.n + 1023u) / 1024u;
-  const uint32_t lo = tid * per;
-  const uint32_t hi = lo + per < a.n ? lo + per : a.n;
-  uint32_t sum = 0;
-  for (uint32_t c = lo; c < hi; ++c) {
-    const uint64_t cs = a.off[c];
-    const uint64_t cb = aligned_end(cs, cs + a.len[c]);
-    const uint64_t body = cb - cs;
-    const uint64_t nt = (body + (1ull << a.tile_log2) - 1) >> a.tile_log2;
-    sum += nt ? (uint32_t)nt : 1u;
-    a.out[c] = 0u;
+// ------------------------------------------------------------------ planning
+// byte_start = exclusive scan of len (64-bit), in two small launches: count (per-block
+// sums) and scan (block-local scans + carry of earlier blocks). Blocks of 256 threads
+// own kPlanPerBlock consecutive chunks, visited in rounds of 256 (coalesced). The scan
+// also initialises out[]: 0 for chunks the sweep will XOR into, crc_in (the CRC of
+// nothing continued from crc_in) for empty chunks.
+__device__ __forceinline__ uint64_t block_scan256(uint64_t v, uint64_t* total) {
+  __shared__ uint64_t wsum[4];
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t o = __shfl_up(v, d);
+    if (lane >= (uint32_t)d) v += o;
   }
-  part[tid] = sum;
+  if (lane == 63) wsum[wv] = v;
   __syncthreads();
-  for (uint32_t d = 1; d < 1024; d <<= 1) {  // Hillis-Steele inclusive scan
-    const uint32_t v = tid >= d ? part[tid - d] : 0u;
-    __syncthreads();
-    part[tid] += v;
-    __syncthreads();
+  uint64_t before = 0;
+  for (uint32_t i = 0; i < wv; ++i) before += wsum[i];
+  *total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  __syncthreads();
+  return v + before;
+}
+
+__global__ __launch_bounds__(256) void crc32_plan_count_kernel(PlanArgs a) {
+  const uint32_t base = blockIdx.x * kPlanPerBlock;
+  uint64_t sum = 0;
+  for (uint32_t r = 0; r < kPlanPerBlock; r += 256) {
+    const uint32_t c = base + r + threadIdx.x;
+    if (c < a.n) sum += a.len[c];
   }
-  uint32_t run = part[tid] - sum;  // exclusive prefix of this thread's range
-  for (uint32_t c = lo; c < hi; ++c) {
-    a.tile_start[c] = run;
-    const uint64_t cs = a.off[c];
-    const uint64_t cb = aligned_end(cs, cs + a.len[c]);
-    const uint64_t nt = (cb - cs + (1ull << a.tile_log2) - 1) >> a.tile_log2;
-    run += nt ? (uint32_t)nt : 1u;
+  uint64_t total;
+  (void)block_scan256(sum, &total);
+  if (threadIdx.x == 0) a.block_sum[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(256) void crc32_plan_scan_kernel(PlanArgs a) {
+  uint64_t part = 0;
+  for (uint32_t i = threadIdx.x; i < blockIdx.x; i += 256) part += a.block_sum[i];
+  uint64_t carry;
+  (void)block_scan256(part, &carry);
+  const uint32_t base = blockIdx.x * kPlanPerBlock;
+  for (uint32_t r = 0; r < kPlanPerBlock; r += 256) {
+    const uint32_t c = base + r + threadIdx.x;
+    const uint64_t v = c < a.n ? a.len[c] : 0u;
+    uint64_t round_total;
+    const uint64_t incl = block_scan256(v, &round_total);
+    if (c < a.n) {
+      a.byte_start[c] = carry + incl - v;
+      a.out[c] = v ? 0u : (a.crc_in ? a.crc_in[c] : 0u);
+      if (c == a.n - 1) a.byte_start[a.n] = carry + incl;
+    }
+    carry += round_total;
   }
-  if (tid == 1023) a.tile_start[a.n] = part[1023];
 }
 
 __global__ void crc32_verify_kernel(const uint32_t* __restrict__ crc, const uint32_t* __restrict__ expected,
@@ -301,16 +360,26 @@ __global__ void fill_splitmix_kernel(uint8_t* __restrict__ dst, uint64_t nbytes,
 
 // ---------------------------------------------------------------- launchers
 hipError_t launch_plan(const PlanArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(crc32_plan_kernel, dim3(1), dim3(1024), 0, s, a);
+  const uint32_t blocks = (a.n + kPlanPerBlock - 1) / kPlanPerBlock;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL(crc32_plan_count_kernel, dim3(blocks), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(crc32_plan_scan_kernel, dim3(blocks), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
-hipError_t launch_tiles(const TilesArgs& a, int grid, int variant, hipStream_t s) {
+hipError_t launch_sweep(const SweepArgs& a, int grid, int variant, hipStream_t s) {
   switch (variant) {
-    case 0: hipLaunchKernelGGL((crc32_tiles_kernel<8, false>), dim3(grid), dim3(1024), 0, s, a); break;
-    case 1: hipLaunchKernelGGL((crc32_tiles_kernel<8, true>), dim3(grid), dim3(1024), 0, s, a); break;
-    case 2: hipLaunchKernelGGL((crc32_tiles_kernel<4, false>), dim3(grid), dim3(1024), 0, s, a); break;
-    case 3: hipLaunchKernelGGL((crc32_tiles_kernel<16, false>), dim3(grid), dim3(1024), 0, s, a); break;
+#define AMBRY_TILES_CASE(V, U, NT, PIPE) \
+  case V: hipLaunchKernelGGL((crc32_sweep_kernel<U, NT, PIPE>), dim3(grid), dim3(1024), 0, s, a); break;
+    AMBRY_TILES_CASE(0, 8, false, true)
+    AMBRY_TILES_CASE(1, 8, true, true)
+    AMBRY_TILES_CASE(2, 4, false, true)
+    AMBRY_TILES_CASE(3, 16, false, true)
+    AMBRY_TILES_CASE(4, 8, false, false)
+    AMBRY_TILES_CASE(5, 8, true, false)
+    AMBRY_TILES_CASE(6, 4, false, false)
+    AMBRY_TILES_CASE(7, 16, false, false)
+#undef AMBRY_TILES_CASE
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -330,6 +399,72 @@ hipError_t launch_fill(uint8_t* dst, uint64_t nbytes, uint64_t seed, uint64_t st
   if (blocks > 65536) blocks = 65536;
   if (blocks == 0) blocks = 1;
   hipLaunchKernelGGL(fill_splitmix_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, dst, nbytes, seed, stream_off);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------- read-bandwidth probe
+// Same grid, occupancy and per-lane access pattern as crc32_sweep_kernel (256 KiB
+// tiles per wave, lane l reading bytes [16l, 16l+16) of each KiB, rolling U=8
+// prefetch) with the CRC arithmetic replaced by an XOR: the achievable read roof
+// for this access shape. Variant 1 uses nontemporal loads; variant 2 is a plain
+// grid-stride dwordx4 stream over 8x more, smaller workgroups.
+template <bool NT>
+__global__ __launch_bounds__(1024) void readbw_tiles_kernel(const uint8_t* __restrict__ base, uint64_t nbytes,
+                                                            uint32_t* __restrict__ out) {
+  constexpr int U = 8;
+  constexpr uint64_t kTile = 256u << 10;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+  const uint64_t ntiles = nbytes / kTile;
+  uint32_t x = 0;
+  for (uint64_t t = wave; t < ntiles; t += nwaves) {
+    const u32x4* q = reinterpret_cast<const u32x4*>(base + t * kTile) + lane;
+    constexpr uint64_t nb = kTile / kBlockBytes;
+    u32x4 buf[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) buf[u] = ld16<NT>(q + u * 64);
+    for (uint64_t b = 0; b + 2 * U <= nb; b += U) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const u32x4 w = buf[u];
+        buf[u] = ld16<NT>(q + (b + U + u) * 64);
+        x ^= w.x ^ w.y ^ w.z ^ w.w;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) x ^= buf[u].x ^ buf[u].y ^ buf[u].z ^ buf[u].w;
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = x;
+}
+
+__global__ __launch_bounds__(256) void readbw_stream_kernel(const u32x4* __restrict__ p, uint64_t n16,
+                                                            uint32_t* __restrict__ out) {
+  constexpr int U = 8;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  uint32_t x = 0;
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + (U - 1) * stride < n16; i += U * stride) {
+    u32x4 w[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) w[u] = __builtin_nontemporal_load(p + i + u * stride);
+#pragma unroll
+    for (int u = 0; u < U; ++u) x ^= w[u].x ^ w[u].y ^ w[u].z ^ w[u].w;
+  }
+  for (; i < n16; i += stride) x ^= p[i].x;
+  out[blockIdx.x * blockDim.x + threadIdx.x] = x;
+}
+
+hipError_t launch_readbw(const uint8_t* base, uint64_t nbytes, uint32_t* out, int grid, int variant, hipStream_t s) {
+  switch (variant) {
+    case 0: hipLaunchKernelGGL(readbw_tiles_kernel<false>, dim3(grid), dim3(1024), 0, s, base, nbytes, out); break;
+    case 1: hipLaunchKernelGGL(readbw_tiles_kernel<true>, dim3(grid), dim3(1024), 0, s, base, nbytes, out); break;
+    case 2:
+      hipLaunchKernelGGL(readbw_stream_kernel, dim3(grid * 4 * 8), dim3(256), 0, s,
+                         reinterpret_cast<const u32x4*>(base), nbytes / 16, out);
+      break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

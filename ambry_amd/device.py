@@ -98,10 +98,6 @@ def crc32_batch_host(chunks, device: int = 0, pinned: bool = False, crc_in=None)
     return list(out)
 
 
-def set_tile_log2(device: int, tile_log2: int) -> None:
-    check(lib().ambrycrc_set_tile_log2(device, tile_log2), "ambrycrc_set_tile_log2")
-
-
 def set_variant(device: int, variant: int) -> None:
     check(lib().ambrycrc_set_variant(device, variant), "ambrycrc_set_variant")
 
@@ -119,7 +115,7 @@ def timing_enable(device: int, enable: bool = True) -> None:
 
 
 def timing_collect(device: int = 0):
-    """(sum of tiles-kernel ms, launches) since the last collect (HIP events on the launch stream)."""
+    """(sum of sweep-kernel ms, launches) since the last collect (HIP events on the launch stream)."""
     ms = ctypes.c_double()
     cnt = ctypes.c_int()
     check(lib().ambrycrc_timing_collect(device, ctypes.byref(ms), ctypes.byref(cnt)), "ambrycrc_timing_collect")

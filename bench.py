@@ -1,14 +1,14 @@
 #!/usr/bin/env python3
 """bench.py -- device-resident CRC-32 over 4 MiB blob chunks (BASELINE.json metric, config C3).
 
-One step = one pass of the hot path (ambrycrc_batch_dev: plan + tiles kernels)
+One step = one pass of the hot path (ambrycrc_batch_dev: plan + sweep kernels)
 over one batch of 8,192 x 4 MiB chunks (32 GiB) resident in HBM on every rank.
 N>1: one process per GPU (torchrun), each rank owns its own 8,192-chunk shard
 (weak scaling; C5 = 524,288 chunks = 8 such steps on 8 GPUs) and the 4-byte
 CRCs are all-gathered over RCCL once per step.
 
 Prints ONE JSON line (rank 0). Besides the driver contract it carries:
-  roofline      tiles-kernel algorithmic bytes / its HIP-event-timed duration vs 8 TB/s
+  roofline      sweep-kernel algorithmic bytes / its HIP-event-timed duration vs 8 TB/s
   cpu_baseline  the oracle's restatement of Crc32.java (kind "port") on host cores, bounded sample
   host_path     pinned-host -> HBM -> CRC rate (PCIe-inclusive; never `value`)
 """
@@ -41,7 +41,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS) + ["c4"])
     ap.add_argument("--variant", type=int, default=None)
-    ap.add_argument("--tile-log2", type=int, default=None)
+    ap.add_argument("--grid", type=int, default=None, help="sweep-kernel workgroups (default: one per CU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-path", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -162,8 +162,8 @@ def main():
     D.init(dev.index)
     if args.variant is not None:
         D.set_variant(dev.index, args.variant)
-    if args.tile_log2 is not None:
-        D.set_tile_log2(dev.index, args.tile_log2)
+    if args.grid is not None:
+        D.set_grid(dev.index, args.grid)
 
     log(args, f"rank {rank}/{world}: building workload {args.config}")
     buf, off_t, len_t, n, total, chunk, desc = build_workload(torch, dev, args, rank)
@@ -226,10 +226,11 @@ def main():
         "data": "synthetic (device splitmix64 bytes; no dataset)",
         "config": {"workload": desc, "chunks_per_gpu": n, "chunk_bytes": chunk, "bytes_per_gpu_step": total,
                    "parallelism": f"shard{world}" + ("+rccl_allgather" if world > 1 else ""),
-                   "tile_log2": None, "grid_workgroups": D.grid_size(dev.index)},
+                   "kernel_variant": args.variant if args.variant is not None else 1,
+                   "grid_workgroups": D.grid_size(dev.index)},
         "roofline": {
             "bound": "hbm",
-            "kernel": "crc32_tiles_kernel",
+            "kernel": "crc32_sweep_kernel",
             "achieved": round(achieved, 1) if achieved else None,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

@@ -126,20 +126,19 @@ int ambrycrc_batch_host(const void* const* ptrs, const uint64_t* lens, const uin
 
 /* ------------------------------------------------------- tuning / telemetry */
 
-/* Tile size (log2 bytes, 12..30) the device path splits chunks into. Default 18. */
-int ambrycrc_set_tile_log2(int device, int tile_log2);
-/* Kernel variant (unroll / load policy) of the tiles kernel; 0 = default. */
+/* Variant (unroll depth / load policy / prefetch scheme, 0..7) of the sweep kernel;
+ * default 1 = 8 blocks in flight per lane, nontemporal loads, rolling prefetch. */
 int ambrycrc_set_variant(int device, int variant);
-/* Grid size of the persistent tiles kernel (workgroups; 0 = one per CU). */
+/* Grid size of the persistent sweep kernel (workgroups; 0 = one per CU). */
 int ambrycrc_set_grid(int device, int workgroups);
 
-/* When enabled, every tiles-kernel launch is bracketed by HIP events on the
+/* When enabled, every sweep-kernel launch is bracketed by HIP events on the
  * caller's stream; ambrycrc_timing_collect() waits for them and returns the sum
  * and count of the kernel durations since the last collect. */
 int ambrycrc_timing_enable(int device, int enable);
 int ambrycrc_timing_collect(int device, double* total_ms, int* launches);
 
-/* Number of workgroups the tiles kernel launches with on `device` (0 if unknown). */
+/* Number of workgroups the sweep kernel launches with on `device` (0 if unknown). */
 int ambrycrc_grid_size(int device);
 
 /* ------------------------------------------------------- synthetic data */
@@ -149,6 +148,13 @@ int ambrycrc_grid_size(int device);
  * d_dst must be 16-B aligned and stream_off a multiple of 16. For benchmarks. */
 int ambrycrc_fill_random_dev(uint8_t* d_dst, uint64_t nbytes, uint64_t seed, uint64_t stream_off,
                              hipStream_t stream);
+
+/* Read-bandwidth probe (no CRC arithmetic) over [d_base, d_base+nbytes) with the
+ * sweep kernel's grid and access pattern (variant 0; 1 = nontemporal; 2 = plain
+ * grid-stride stream). d_out needs grid*1024 words. Measures the achievable HBM
+ * read roof the CRC sweep kernel is compared against. */
+int ambrycrc_debug_readbw_dev(const uint8_t* d_base, uint64_t nbytes, uint32_t* d_out, int variant,
+                              hipStream_t stream);
 
 /* Copy of the LDS table image (kLdsBytes + 256 B) into host memory `out` (for
  * tests that model the kernel on the CPU). Returns the byte size, or <0. */

@@ -1,14 +1,15 @@
-"""CPU model of the gfx950 tiles kernel (ambry_amd/csrc/crc32_kernels.hip).
+"""CPU model of the gfx950 sweep kernel (ambry_amd/csrc/crc32_kernels.hip).
 
 Test infrastructure: it replays the kernel's arithmetic -- the LDS image built
 by libambrycrc (ambrycrc_debug_table_image), v_perm_b32 address formation,
 slice-by-4 steps, nibble-table multiplies, the per-lane 1 KiB block hop, the
-6-level wave tree and the tile/chunk decomposition -- lane by lane in numpy,
+6-level wave tree and the byte-balanced wave/segment decomposition -- lane by lane in numpy,
 so that layout or algebra mistakes show up on the CPU before a GPU run. It is
 checked against zlib/the oracle in tests/test_kernel_model.py.
 """
 from __future__ import annotations
 
+import bisect
 import ctypes
 
 import numpy as np
@@ -107,33 +108,61 @@ class KernelModel:
             s = np.where((LANES & (1 << lvl)) != 0, s ^ sh, s).astype(np.uint32)
         return int(s[63])
 
-    def batch(self, mem: np.ndarray, off, length, crc_in=None, tile_log2: int = 18):
-        """Replays plan + tiles kernels; returns the list of CRCs."""
-        tile = 1 << tile_log2
-        out = []
-        for c, (cs, ln) in enumerate(zip(off, length)):
-            cs, ln = int(cs), int(ln)
-            ce = cs + ln
-            cb = max(cs, ce & ~15)
-            nt = max(1, (cb - cs + tile - 1) >> tile_log2)
-            acc = 0
-            for q in range(nt):
-                m = nt - 1 - q
-                be = cb - m * tile
-                bs = max(cs, be - tile if be > tile else 0)
-                r = self.body_crc(mem, bs, be)
-                r = self.shift_bytes(r, (ce - cb) + m * tile)
-                if m == 0:
+    def batch(self, mem: np.ndarray, off, length, crc_in=None, nwaves: int = 4096, quantum: int = 1024):
+        """Replays plan + sweep kernels with `nwaves` waves; returns the list of CRCs."""
+        n = len(off)
+        off = [int(x) for x in off]
+        length = [int(x) for x in length]
+        byte_start = [0]
+        for ln in length:
+            byte_start.append(byte_start[-1] + ln)
+        total = byte_start[n]
+        out = [0 if length[c] else (0 if crc_in is None else int(crc_in[c])) for c in range(n)]
+        share = ((total + nwaves - 1) // nwaves + quantum - 1) // quantum * quantum
+        for w in range(nwaves):
+            g0 = w * share
+            if share == 0 or g0 >= total:
+                break
+            g1 = min(total, g0 + share)
+            c = bisect.bisect_right(byte_start, g0, 0, n) - 1
+            while c < n:
+                bsc = byte_start[c]
+                if bsc >= g1:
+                    break
+                ln = length[c]
+                if ln == 0:
+                    c += 1
+                    continue
+                cs = off[c]
+                ce = cs + ln
+                cb = max(cs, ce & ~15)
+                r0 = snap_cut(cs, ln, g0 - bsc) if g0 > bsc else 0
+                r1 = snap_cut(cs, ln, g1 - bsc) if g1 - bsc < ln else ln
+                if r0 >= r1:
+                    c += 1
+                    continue
+                sa, se = cs + r0, cs + r1
+                be = cb if se == ce else se
+                assert be % 16 == 0 or be == cs, (sa, se, be)
+                r = 0
+                if sa < be:
+                    r = self.shift_bytes(self.body_crc(mem, sa, be), ce - be)
+                if se == ce:
                     tr = 0
-                    for p in range(cb, ce):
+                    for p in range(max(sa, cb), ce):
                         tr = (tr >> 8) ^ int(self.lds(((tr ^ int(mem[p])) & 0xFF) << 8))
                     r ^= tr
-                if q == 0:
+                if r0 == 0:
                     cin = 0 if crc_in is None else int(crc_in[c])
                     r ^= self.shift_bytes((~cin) & 0xFFFFFFFF, ln) ^ 0xFFFFFFFF
-                acc ^= r
-            out.append(acc & 0xFFFFFFFF)
-        return out
+                out[c] ^= r
+                c += 1
+        return [x & 0xFFFFFFFF for x in out]
+
+
+def snap_cut(cs: int, ln: int, r: int) -> int:
+    a = (cs + r + 15) & ~15
+    return min(a - cs, ln)
 
 
 def gf2_mul(a: int, b: int) -> int:

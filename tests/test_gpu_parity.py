@@ -89,9 +89,10 @@ def test_every_small_length_and_alignment(gpu, oracle):
     assert np.array_equal(got, oracle.batch(mem, off, ln))
 
 
-@pytest.mark.parametrize("tile_log2", [12, 13, 16, 18, 20])
-def test_ragged_batch_tile_sizes(gpu, oracle, tile_log2):
-    rng = np.random.default_rng(tile_log2)
+@pytest.mark.parametrize("grid", [1, 3, 17, 256, 0])
+def test_ragged_batch_grid_sizes(gpu, oracle, grid):
+    """Different persistent-grid sizes move every wave cut point through the chunks."""
+    rng = np.random.default_rng(grid)
     mem = stream_bytes(5, 0, 24 << 20)
     n = 300
     ln = rng.integers(0, 3 << 20, size=n)
@@ -99,15 +100,15 @@ def test_ragged_batch_tile_sizes(gpu, oracle, tile_log2):
                (1 << 20) - 1, 1 << 20, (1 << 20) + 1]
     off = rng.integers(0, (24 << 20) - (3 << 20), size=n)
     off[::3] = off[::3] // 16 * 16
-    gpu.set_tile_log2(0, tile_log2)
+    gpu.set_grid(0, grid)
     try:
         got = run_batch(gpu, mem, off, ln)
     finally:
-        gpu.set_tile_log2(0, 18)
+        gpu.set_grid(0, 0)
     assert np.array_equal(got, oracle.batch(mem, off, ln, threads=8))
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", list(range(8)))
 def test_kernel_variants(gpu, oracle, variant):
     rng = np.random.default_rng(100 + variant)
     mem = stream_bytes(6, 0, 16 << 20)
@@ -117,7 +118,7 @@ def test_kernel_variants(gpu, oracle, variant):
     try:
         got = run_batch(gpu, mem, off, ln)
     finally:
-        gpu.set_variant(0, 0)
+        gpu.set_variant(0, 1)
     assert np.array_equal(got, oracle.batch(mem, off, ln, threads=8))
 
 
@@ -156,6 +157,17 @@ def test_verify_flags_zipf(gpu, oracle):
     assert set(np.nonzero(flags)[0]) == set(int(i) for i in bad)
     assert int(count.item()) == len(bad)
     assert np.array_equal(host_u32(crc), oracle.batch(corrupt, off, sizes, threads=8))
+
+
+def test_empty_chunks_and_crc_in(gpu, oracle):
+    """Zero-length chunks return crc_in unchanged (Crc32.update on an empty buffer is a no-op, Crc32.java:101-103)."""
+    mem = stream_bytes(2, 0, 1 << 16)
+    off = [0, 100, 100, 200, 5000, 5000, 0]
+    ln = [0, 0, 50, 0, 0, 3000, 0]
+    cin = [0, 0x1234, 0x55AA, 0xFFFFFFFF, 7, 9, 0xDEADBEEF]
+    got = run_batch(gpu, mem, off, ln, crc_in=cin)
+    assert np.array_equal(got, oracle.batch(mem, off, ln, crc_in=np.array(cin, dtype=np.uint32)))
+    assert got[1] == 0x1234 and got[3] == 0xFFFFFFFF
 
 
 def test_overlapping_and_repeated_chunks(gpu, oracle):

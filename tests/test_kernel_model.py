@@ -1,4 +1,4 @@
-"""CPU replay of the gfx950 tiles kernel's arithmetic (tests/kernel_model.py) against the oracle.
+"""CPU replay of the gfx950 sweep kernel's arithmetic (tests/kernel_model.py) against the oracle.
 
 Catches LDS-layout / GF(2) / tiling mistakes without a GPU; the real kernel is
 checked by tests/test_gpu_parity.py on the MI355X."""
@@ -18,12 +18,12 @@ CASES = [(0, 0), (0, 1), (3, 5), (16, 16), (5, 15), (5, 16), (5, 17), (0, 1024),
          (100, 70000), (13, 65536 + 7), (64, 200000), (4095, 4097), (1, 1)]
 
 
-@pytest.mark.parametrize("tile_log2", [12, 13, 18])
-def test_model_matches_oracle(model, oracle, tile_log2):
+@pytest.mark.parametrize("nwaves", [1, 2, 3, 7, 64, 4096])
+def test_model_matches_oracle(model, oracle, nwaves):
     mem = stream_bytes(123, 0, 300000)
     off = [c[0] for c in CASES]
     ln = [c[1] for c in CASES]
-    got = model.batch(mem, off, ln, tile_log2=tile_log2)
+    got = model.batch(mem, off, ln, nwaves=nwaves)
     exp = list(oracle.batch(mem, off, ln))
     assert got == exp
 
@@ -33,7 +33,16 @@ def test_model_crc_in(model, oracle):
     off = [c[0] for c in CASES[:10]]
     ln = [c[1] for c in CASES[:10]]
     cin = np.array([(i * 0x9E3779B9) & 0xFFFFFFFF for i in range(10)], dtype=np.uint32)
-    assert model.batch(mem, off, ln, crc_in=cin, tile_log2=12) == list(oracle.batch(mem, off, ln, crc_in=cin))
+    for nw in (1, 5, 300):
+        assert model.batch(mem, off, ln, crc_in=cin, nwaves=nw) == list(oracle.batch(mem, off, ln, crc_in=cin))
+
+
+def test_model_cut_points_everywhere(model, oracle):
+    """Wave cuts landing in every residue of a chunk (incl. its last 15 bytes) must tile it exactly."""
+    mem = stream_bytes(5, 0, 20000)
+    for cs, ln in ((3, 4000), (16, 4096), (1, 1040), (0, 17)):
+        for nw in range(2, 12):
+            assert model.batch(mem, [cs], [ln], nwaves=nw, quantum=16) == list(oracle.batch(mem, [cs], [ln]))
 
 
 def test_model_large_shift_slow_path(model):
