@@ -110,7 +110,7 @@ struct DevCtx {
   int device = -1;
   int num_cu = 0;
   int grid = 0;
-  int variant = 1;  // U=8, nontemporal loads, rolling prefetch (tools/sweep.py)
+  int variant = 0;  // U=8, nontemporal loads, rolling prefetch, 2 pieces interleaved (tools/sweep.py)
   uint32_t* d_img = nullptr;
   void* d_ws = nullptr;
   size_t ws_bytes = 0;

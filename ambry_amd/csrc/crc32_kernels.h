@@ -30,7 +30,10 @@ struct SweepArgs {
   uint32_t* out;
 };
 
-// sweep-kernel variants: {U = 8,8,4,16} x {rolling prefetch (0-3), batch loads (4-7)}; 1,5 = nontemporal
+// sweep-kernel variants (U = loads in flight per lane, NT = nontemporal, PIPE = rolling prefetch,
+// IL = two pieces interleaved): 0 U8/NT/PIPE/IL (default), 1 U8/NT/PIPE, 2 U4/NT/PIPE,
+// 3 U12/NT/PIPE/IL, 4 U8/PIPE/IL (temporal loads), 5 U8/NT batch loads, 6 U4/NT/PIPE/IL,
+// 7 U8 batch loads (temporal)
 constexpr int kNumVariants = 8;
 
 hipError_t launch_plan(const PlanArgs& a, hipStream_t s);

@@ -78,6 +78,10 @@ __device__ __forceinline__ uint32_t rpiece(u32x4 w, const LaneConst& k, uint32_t
   return slice4(s, k, xin);
 }
 
+// Two pieces whose first three table steps are independent of the running state,
+// interleaved in source so a wave keeps two LDS dependency chains in flight.
+__device__ __forceinline__ uint32_t rpiece_pair(u32x4 w0, u32x4 w1, const LaneConst& k, uint32_t s);
+
 // v * C mod P where C's nibble tables sit at kNibBase + set_off (conflict-free, 8 lookups).
 __device__ __forceinline__ uint32_t nib_mul(uint32_t v, uint32_t set_off) {
   uint32_t t[8];
@@ -97,6 +101,17 @@ __device__ __forceinline__ uint32_t shift_bytes(uint32_t v, uint64_t n, const ui
   return v;
 }
 
+__device__ __forceinline__ uint32_t rpiece_pair(u32x4 w0, u32x4 w1, const LaneConst& k, uint32_t s) {
+  uint32_t x0 = slice4(w0.x, k, w0.y);
+  uint32_t x1 = slice4(w1.x, k, w1.y);
+  x0 = slice4(x0, k, w0.z);
+  x1 = slice4(x1, k, w1.z);
+  x0 = slice4(x0, k, w0.w);
+  x1 = slice4(x1, k, w1.w);
+  s = slice4(x0, k, nib_mul(s, kFoldOff));
+  return slice4(x1, k, nib_mul(s, kFoldOff));
+}
+
 template <bool NT>
 __device__ __forceinline__ u32x4 ld16(const u32x4* p) {
   if constexpr (NT) {
@@ -109,7 +124,7 @@ __device__ __forceinline__ u32x4 ld16(const u32x4* p) {
 // Raw CRC of body [bs, be) (be 16-aligned, bs <= be arbitrary), returned in lane 63
 // (other lanes: junk). Bytes below bs are treated as zeros, which leave a zero
 // register unchanged, so the virtual range is aligned down to whole 1 KiB blocks.
-template <int U, bool NT, bool PIPE>
+template <int U, bool NT, bool PIPE, bool IL>
 __device__ __forceinline__ uint32_t body_crc(const uint8_t* __restrict__ base, uint64_t bs, uint64_t be,
                                              uint32_t lane, const LaneConst& k) {
   const uint64_t nb = (be - bs + kBlockBytes - 1) / kBlockBytes;
@@ -145,11 +160,21 @@ __device__ __forceinline__ uint32_t body_crc(const uint8_t* __restrict__ base, u
 #pragma unroll
       for (int u = 0; u < U; ++u) buf[u] = ld16<NT>(q + (b + u) * (kBlockBytes / 16));
       for (; b + 2 * U <= nb; b += U) {
+        if constexpr (IL) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const u32x4 w = buf[u];
-          buf[u] = ld16<NT>(q + (b + U + u) * (kBlockBytes / 16));
-          s = rpiece(w, k, nib_mul(s, kFoldOff));
+          for (int u = 0; u < U; u += 2) {
+            const u32x4 w0 = buf[u], w1 = buf[u + 1];
+            buf[u] = ld16<NT>(q + (b + U + u) * (kBlockBytes / 16));
+            buf[u + 1] = ld16<NT>(q + (b + U + u + 1) * (kBlockBytes / 16));
+            s = rpiece_pair(w0, w1, k, s);
+          }
+        } else {
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const u32x4 w = buf[u];
+            buf[u] = ld16<NT>(q + (b + U + u) * (kBlockBytes / 16));
+            s = rpiece(w, k, nib_mul(s, kFoldOff));
+          }
         }
       }
 #pragma unroll
@@ -216,7 +241,7 @@ __device__ __forceinline__ uint64_t snap_cut(uint64_t cs, uint64_t len, uint64_t
 // as one concatenated stream (byte_start = exclusive scan of len), i.e. an equal share of
 // bytes whatever the chunk-size mix. Each (wave, chunk) intersection is a segment whose
 // raw CRC is shifted to the chunk end and XORed into out[chunk].
-template <int U, bool NT, bool PIPE>
+template <int U, bool NT, bool PIPE, bool IL>
 __global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
   {
     const u32x4* src = reinterpret_cast<const u32x4*>(a.img);
@@ -252,7 +277,7 @@ __global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
     const uint64_t be = se == ce ? cb : se;  // 16-B aligned body end
     uint32_t r = 0;
     if (sa < be) {
-      r = body_crc<U, NT, PIPE>(a.base, sa, be, lane, k);
+      r = body_crc<U, NT, PIPE, IL>(a.base, sa, be, lane, k);
       r = __builtin_amdgcn_readlane(r, 63);
       r = shift_bytes(r, ce - be, xpow2);
     }
@@ -369,16 +394,16 @@ hipError_t launch_plan(const PlanArgs& a, hipStream_t s) {
 
 hipError_t launch_sweep(const SweepArgs& a, int grid, int variant, hipStream_t s) {
   switch (variant) {
-#define AMBRY_TILES_CASE(V, U, NT, PIPE) \
-  case V: hipLaunchKernelGGL((crc32_sweep_kernel<U, NT, PIPE>), dim3(grid), dim3(1024), 0, s, a); break;
-    AMBRY_TILES_CASE(0, 8, false, true)
-    AMBRY_TILES_CASE(1, 8, true, true)
-    AMBRY_TILES_CASE(2, 4, false, true)
-    AMBRY_TILES_CASE(3, 16, false, true)
-    AMBRY_TILES_CASE(4, 8, false, false)
-    AMBRY_TILES_CASE(5, 8, true, false)
-    AMBRY_TILES_CASE(6, 4, false, false)
-    AMBRY_TILES_CASE(7, 16, false, false)
+#define AMBRY_TILES_CASE(V, U, NT, PIPE, IL) \
+  case V: hipLaunchKernelGGL((crc32_sweep_kernel<U, NT, PIPE, IL>), dim3(grid), dim3(1024), 0, s, a); break;
+    AMBRY_TILES_CASE(0, 8, true, true, true)
+    AMBRY_TILES_CASE(1, 8, true, true, false)
+    AMBRY_TILES_CASE(2, 4, true, true, false)
+    AMBRY_TILES_CASE(3, 12, true, true, true)
+    AMBRY_TILES_CASE(4, 8, false, true, true)
+    AMBRY_TILES_CASE(5, 8, true, false, false)
+    AMBRY_TILES_CASE(6, 4, true, true, true)
+    AMBRY_TILES_CASE(7, 8, false, false, false)
 #undef AMBRY_TILES_CASE
     default: return hipErrorInvalidValue;
   }

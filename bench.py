@@ -121,6 +121,26 @@ def cpu_baseline(buf, off_t, len_t, n, args):
     }
 
 
+def measure_read_roof(torch, D, buf, total, device):
+    """Read-only probe (ambrycrc_debug_readbw_dev variant 1: the sweep kernel's grid and access
+    shape, nontemporal loads, no CRC arithmetic) over the same HBM buffer: best of 5 launches, GB/s."""
+    from ambry_amd._lib import check, lib
+
+    nbytes = total & ~((256 << 10) - 1)
+    scratch = torch.empty(D.grid_size(device) * 1024, dtype=torch.int32, device=buf.device)
+    best = None
+    for _ in range(5):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        check(lib().ambrycrc_debug_readbw_dev(buf.data_ptr(), nbytes, scratch.data_ptr(), 1,
+                                              torch.cuda.current_stream().cuda_stream), "readbw")
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1)
+        best = ms if best is None else min(best, ms)
+    return round(nbytes / (best / 1e3) / 1e9, 1)
+
+
 def host_path_rate(torch, args):
     """Pinned host buffers -> PCIe -> HBM -> CRC -> host (ambrycrc_batch_host); DESIGN.md only."""
     from ambry_amd import device as D
@@ -204,6 +224,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    read_roof = measure_read_roof(torch, D, buf, total, dev.index) if args.config != "c4" else None
     crcs = out.cpu().numpy().view("uint32")
     step_bytes = total  # per rank
     value = world * step_bytes * args.steps / elapsed / 2**30
@@ -226,7 +247,7 @@ def main():
         "data": "synthetic (device splitmix64 bytes; no dataset)",
         "config": {"workload": desc, "chunks_per_gpu": n, "chunk_bytes": chunk, "bytes_per_gpu_step": total,
                    "parallelism": f"shard{world}" + ("+rccl_allgather" if world > 1 else ""),
-                   "kernel_variant": args.variant if args.variant is not None else 1,
+                   "kernel_variant": args.variant if args.variant is not None else 0,
                    "grid_workgroups": D.grid_size(dev.index)},
         "roofline": {
             "bound": "hbm",
@@ -239,6 +260,9 @@ def main():
             "kernel_avg_ms": round(kern_avg_s * 1e3, 4),
             "algorithmic_bytes_per_launch": alg_bytes,
             "value_frac_of_peak": round(value * 2**30 / 1e9 / world / HBM_PEAK_GBS, 4),
+            "measured_read_roof": read_roof,
+            "frac_of_measured_read_roof": (round(achieved / read_roof, 4)
+                                           if achieved and read_roof else None),
         },
         "timing": {"wall_s": round(elapsed, 4), "stream_event_ms": round(ev_ms, 3), "kernel_launches": launches},
     }

@@ -127,7 +127,8 @@ int ambrycrc_batch_host(const void* const* ptrs, const uint64_t* lens, const uin
 /* ------------------------------------------------------- tuning / telemetry */
 
 /* Variant (unroll depth / load policy / prefetch scheme, 0..7) of the sweep kernel;
- * default 1 = 8 blocks in flight per lane, nontemporal loads, rolling prefetch. */
+ * default 0 = 8 blocks in flight per lane, nontemporal loads, rolling prefetch,
+ * two pieces' table walks interleaved. */
 int ambrycrc_set_variant(int device, int variant);
 /* Grid size of the persistent sweep kernel (workgroups; 0 = one per CU). */
 int ambrycrc_set_grid(int device, int workgroups);

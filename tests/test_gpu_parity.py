@@ -118,7 +118,7 @@ def test_kernel_variants(gpu, oracle, variant):
     try:
         got = run_batch(gpu, mem, off, ln)
     finally:
-        gpu.set_variant(0, 1)
+        gpu.set_variant(0, 0)
     assert np.array_equal(got, oracle.batch(mem, off, ln, threads=8))
 
 

@@ -1,0 +1,76 @@
+#!/usr/bin/env python3
+"""Condense rocprofv3 outputs (gpurun_out/prof_*) into committed profiles/ files.
+
+  profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (as emitted)
+  profiles/<tag>_pmc_summary.json   per-dispatch averages of every PMC counter for the sweep kernel
+  profiles/pmc_traffic.json         HBM bytes per sweep-kernel launch, read by bench.py as roofline.traffic
+
+Traffic correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE and WRITE_SIZE are in KiB;
+on gfx950 FETCH_SIZE reads exactly half the bytes of a wide coalesced stream, so
+hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024. Each counter comes from its own
+--pmc pass.
+"""
+from __future__ import annotations
+
+import argparse
+import collections
+import csv
+import json
+import os
+import shutil
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def pmc_avgs(path, kernel_substr):
+    rows = list(csv.DictReader(open(path)))
+    agg = collections.defaultdict(list)
+    for r in rows:
+        if kernel_substr in r["Kernel_Name"]:
+            agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in agg.items()}, {k: len(v) for k, v in agg.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--src", default=os.path.join(ROOT, "gpurun_out"))
+    ap.add_argument("--tag", required=True)
+    ap.add_argument("--kernel", default="crc32_sweep_kernel")
+    ap.add_argument("--alg-bytes", type=int, default=8192 * (4 << 20) + 4 * 8192)
+    args = ap.parse_args()
+    out = os.path.join(ROOT, "profiles")
+    os.makedirs(out, exist_ok=True)
+    shutil.copy(os.path.join(args.src, "prof_kt", "kt_kernel_stats.csv"),
+                os.path.join(out, f"{args.tag}_kernel_stats.csv"))
+    summary = {"kernel": args.kernel, "passes": {}}
+    counters = {}
+    for name in ("prof_fetch", "prof_write", "prof_sq"):
+        p = os.path.join(args.src, name, "pmc_counter_collection.csv")
+        if os.path.exists(p):
+            avg, cnt = pmc_avgs(p, args.kernel)
+            summary["passes"][name] = {"avg": avg, "dispatches": cnt}
+            counters.update(avg)
+    with open(os.path.join(args.src, "prof_kt", "kt_kernel_stats.csv")) as f:
+        for r in csv.DictReader(f):
+            if args.kernel in r["Name"]:
+                summary["kernel_trace"] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
+                                           "min_ns": float(r["MinNs"]), "max_ns": float(r["MaxNs"])}
+    if "FETCH_SIZE" in counters:
+        hbm = (2 * counters["FETCH_SIZE"] + counters.get("WRITE_SIZE", 0.0)) * 1024
+        summary["hbm_bytes_per_launch"] = hbm
+        summary["algorithmic_bytes_per_launch"] = args.alg_bytes
+        summary["traffic_over_algorithmic"] = hbm / args.alg_bytes
+        with open(os.path.join(out, "pmc_traffic.json"), "w") as f:
+            json.dump({"hbm_bytes_per_launch": round(hbm),
+                       "source": f"profiles/{args.tag}_pmc_summary.json: (2*FETCH_SIZE + WRITE_SIZE) KiB, "
+                                 "separate rocprofv3 --pmc passes of bench.py (C3)",
+                       "kernel": args.kernel}, f, indent=1)
+    if "GRBM_GUI_ACTIVE" in counters and "kernel_trace" in summary:
+        summary["effective_clock_ghz_est"] = counters["GRBM_GUI_ACTIVE"] / 8 / (summary["kernel_trace"]["avg_ns"])
+    with open(os.path.join(out, f"{args.tag}_pmc_summary.json"), "w") as f:
+        json.dump(summary, f, indent=1)
+    print(json.dumps(summary, indent=1))
+
+
+if __name__ == "__main__":
+    main()
