@@ -561,6 +561,96 @@ int ambrycrc_debug_readbw_dev(const uint8_t* d_base, uint64_t nbytes, uint32_t* 
   return hip_err(launch_readbw(d_base, nbytes, d_out, c->grid, variant, stream));
 }
 
+size_t ambrycrc_messages_workspace_bytes(size_t m) {
+  const size_t j = (size_t)kMsgSlots * m;
+  const size_t jobs = (j * 2 * sizeof(uint64_t) + j * 2 * sizeof(uint32_t) + j + 255) & ~size_t(255);
+  return jobs + ws_need(j);
+}
+
+int ambrycrc_verify_messages_dev(const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off, size_t m,
+                                 uint32_t* d_status, uint64_t* d_msg_end, void* d_ws, size_t ws_bytes,
+                                 hipStream_t stream) {
+  if (m == 0) return AMBRYCRC_OK;
+  if (!d_region || !d_msg_off || !d_status || (size_t)kMsgSlots * m >= (1ull << 31)) return AMBRYCRC_EINVAL;
+  DevCtx* c = ctx_current();
+  if (!c) return AMBRYCRC_ENOINIT;
+  const size_t need = ambrycrc_messages_workspace_bytes(m);
+  if (d_ws) {
+    if (ws_bytes < need) return AMBRYCRC_EINVAL;
+  } else {
+    std::lock_guard<std::mutex> g(c->mu);
+    int rc = ensure_ws(c, need);
+    if (rc) return rc;
+    d_ws = c->d_ws;
+  }
+  const size_t j = (size_t)kMsgSlots * m;
+  uint8_t* w = static_cast<uint8_t*>(d_ws);
+  MsgArgs a;
+  a.region = d_region;
+  a.region_len = region_len;
+  a.msg_off = d_msg_off;
+  a.m = m;
+  a.img = c->d_img;
+  a.job_off = reinterpret_cast<uint64_t*>(w);
+  a.job_len = a.job_off + j;
+  a.expected = reinterpret_cast<uint32_t*>(a.job_len + j);
+  uint32_t* crc = a.expected + j;
+  uint8_t* mism = reinterpret_cast<uint8_t*>(crc + j);
+  a.mismatch = mism;
+  a.status = d_status;
+  a.msg_end = d_msg_end;
+  void* batch_ws = w + ((j * 2 * sizeof(uint64_t) + j * 2 * sizeof(uint32_t) + j + 255) & ~size_t(255));
+  if (launch_msg_parse(a, stream) != hipSuccess) return AMBRYCRC_EHIP;
+  int rc = enqueue_batch(c, d_region, a.job_off, a.job_len, nullptr, crc, j, batch_ws, stream);
+  if (rc) return rc;
+  if (launch_verify(crc, a.expected, mism, nullptr, (uint32_t)j, stream) != hipSuccess) return AMBRYCRC_EHIP;
+  return hip_err(launch_msg_reduce(a, stream));
+}
+
+size_t ambrycrc_chain_messages_host(const uint8_t* region, uint64_t region_len, uint64_t start, uint64_t* offs,
+                                    size_t max) {
+  if (!region || !offs) return 0;
+  auto be16 = [](const uint8_t* p) { return (uint32_t)((p[0] << 8) | p[1]); };
+  auto be32 = [](const uint8_t* p) {
+    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+  };
+  auto be64 = [&](const uint8_t* p) { return ((uint64_t)be32(p) << 32) | be32(p + 4); };
+  size_t cnt = 0;
+  uint64_t off = start;
+  while (cnt < max && off < region_len && region_len - off >= 2) {
+    const uint8_t* p = region + off;
+    const int v = (int16_t)be16(p);
+    const uint32_t h = v == 1 ? 34u : v == 2 ? 38u : v == 3 ? 40u : 0u;
+    if (h == 0 || region_len - off < h) break;
+    if ((uint64_t)ambrycrc_update(0, p, h - 8) != be64(p + h - 8)) break;
+    int64_t total;
+    int32_t rel[5];
+    if (v == 1) {
+      total = (int64_t)be64(p + 2);
+      rel[0] = -1;
+      for (int k = 0; k < 4; ++k) rel[k + 1] = (int32_t)be32(p + 10 + 4 * k);
+    } else if (v == 2) {
+      total = (int64_t)be64(p + 2);
+      for (int k = 0; k < 5; ++k) rel[k] = (int32_t)be32(p + 10 + 4 * k);
+    } else {
+      total = (int64_t)be64(p + 4);
+      for (int k = 0; k < 5; ++k) rel[k] = (int32_t)be32(p + 12 + 4 * k);
+    }
+    int64_t first = -1;
+    for (int k = 0; k < 5; ++k)
+      if (rel[k] != -1) {
+        first = rel[k];
+        break;
+      }
+    if (total <= 0 || first < (int64_t)h || (uint64_t)total > region_len - off ||
+        (uint64_t)first > region_len - off - (uint64_t)total)
+      break;
+    offs[cnt++] = off;
+    off += (uint64_t)first + (uint64_t)total;
+  }
+  return cnt;
+}
+
 long ambrycrc_debug_table_image(uint32_t* out, size_t max_words) {
   std::vector<uint32_t> img = build_table_image();
   if (!out || max_words < img.size()) return AMBRYCRC_EINVAL;

@@ -36,6 +36,27 @@ struct SweepArgs {
 // 7 U8 batch loads (temporal)
 constexpr int kNumVariants = 8;
 
+// Message verify (message_kernels.hip): kMsgSlots CRC jobs per message, slot order
+// encryption key, blob properties, update, user metadata, blob.
+constexpr int kMsgSlots = 5;
+
+struct MsgArgs {
+  const uint8_t* region;
+  uint64_t region_len;
+  const uint64_t* msg_off;  // [m]
+  uint64_t m;
+  const uint32_t* img;      // table image (T0 used by the header CRC)
+  uint64_t* job_off;        // [5m]
+  uint64_t* job_len;        // [5m]
+  uint32_t* expected;       // [5m]
+  const uint8_t* mismatch;  // [5m]
+  uint32_t* status;         // [m]
+  uint64_t* msg_end;        // [m] or null
+};
+
+hipError_t launch_msg_parse(const MsgArgs& a, hipStream_t s);
+hipError_t launch_msg_reduce(const MsgArgs& a, hipStream_t s);
+
 hipError_t launch_plan(const PlanArgs& a, hipStream_t s);
 hipError_t launch_sweep(const SweepArgs& a, int grid, int variant, hipStream_t s);
 hipError_t launch_verify(const uint32_t* crc, const uint32_t* expected, uint8_t* mismatch, uint32_t* count,

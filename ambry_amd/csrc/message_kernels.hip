@@ -1,0 +1,163 @@
+// message_kernels.hip -- batched verify of Ambry PUT / update messages in a log region
+// (SURVEY.md §8f next #1): the GPU form of deserializeBlobAll's CRC checks
+// (ambry-messageformat/.../MessageFormatRecord.java:257-303), BlobStoreRecovery's
+// per-message verification (ambry-store/.../BlobStoreRecovery.java:43-110) and
+// ValidatingTransformer's replication check (ValidatingTransformer.java:46-104).
+//
+// Pipeline (all on the caller's stream):
+//   msg_parse_kernel   one thread per message: header version, header CRC (<= 32 B,
+//                      byte-wise through T0), header constraints, and up to five record
+//                      CRC jobs (enc key, properties, update, user metadata, blob) =
+//                      [record start, record end - 8) with the stored big-endian CRC
+//   plan + sweep       the batch CRC engine over the 5m jobs (crc32_kernels.hip)
+//   verify             mismatch flags
+//   msg_reduce_kernel  per-message status bits
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/ambrycrc.h"
+#include "crc32_kernels.h"
+#include "crc32_layout.h"
+
+namespace ambrycrc {
+
+__device__ __forceinline__ uint32_t be16(const uint8_t* p) { return ((uint32_t)p[0] << 8) | p[1]; }
+__device__ __forceinline__ uint32_t be32(const uint8_t* p) {
+  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+__device__ __forceinline__ uint64_t be64(const uint8_t* p) { return ((uint64_t)be32(p) << 32) | be32(p + 4); }
+
+// T0[b] lives at LDS-image word (b << 8) / 4 (slice table 0, lane column 0).
+__device__ __forceinline__ uint32_t crc_small(const uint8_t* p, uint32_t n, const uint32_t* __restrict__ img) {
+  uint32_t c = 0xFFFFFFFFu;
+  for (uint32_t i = 0; i < n; ++i) c = (c >> 8) ^ img[((c ^ p[i]) & 0xffu) << 6];
+  return ~c;
+}
+
+__constant__ uint32_t kRecordBit[5] = {AMBRYCRC_MSG_ENCKEY_CRC, AMBRYCRC_MSG_PROPS_CRC, AMBRYCRC_MSG_UPDATE_CRC,
+                                       AMBRYCRC_MSG_USERMETA_CRC, AMBRYCRC_MSG_BLOB_CRC};
+
+__global__ __launch_bounds__(256) void msg_parse_kernel(MsgArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.m) return;
+  const uint64_t off = a.msg_off[i];
+  for (int k = 0; k < kMsgSlots; ++k) {
+    a.job_off[kMsgSlots * i + k] = 0;
+    a.job_len[kMsgSlots * i + k] = 0;
+    a.expected[kMsgSlots * i + k] = 0;
+  }
+  uint32_t status = 0;
+  uint64_t end = 0;
+  do {
+    if (off > a.region_len || a.region_len - off < 2) {
+      status = AMBRYCRC_MSG_BAD_LAYOUT;
+      break;
+    }
+    const uint8_t* p = a.region + off;
+    const int v = (int16_t)be16(p);
+    const uint32_t h = v == 1 ? 34u : v == 2 ? 38u : v == 3 ? 40u : 0u;
+    if (h == 0) {
+      status = AMBRYCRC_MSG_BAD_VERSION;
+      break;
+    }
+    if (a.region_len - off < h) {
+      status = AMBRYCRC_MSG_BAD_LAYOUT;
+      break;
+    }
+    if ((uint64_t)crc_small(p, h - 8, a.img) != be64(p + h - 8)) {  // verifyHeader: nothing else is read
+      status = AMBRYCRC_MSG_HEADER_CRC;
+      break;
+    }
+    int64_t total;
+    int32_t rel[kMsgSlots];
+    if (v == 1) {
+      total = (int64_t)be64(p + 2);
+      rel[0] = -1;
+      for (int k = 0; k < 4; ++k) rel[k + 1] = (int32_t)be32(p + 10 + 4 * k);
+    } else if (v == 2) {
+      total = (int64_t)be64(p + 2);
+      for (int k = 0; k < 5; ++k) rel[k] = (int32_t)be32(p + 10 + 4 * k);
+    } else {
+      if ((int16_t)be16(p + 2) < 0) {  // lifeVersion >= 0
+        status = AMBRYCRC_MSG_BAD_LAYOUT;
+        break;
+      }
+      total = (int64_t)be64(p + 4);
+      for (int k = 0; k < 5; ++k) rel[k] = (int32_t)be32(p + 12 + 4 * k);
+    }
+    // checkHeaderConstraints (MessageFormatRecord.java:985-1030), exact put / update shapes
+    const bool is_put = rel[1] != -1 && rel[2] == -1 && rel[3] != -1 && rel[4] != -1;
+    const bool is_upd = rel[2] != -1 && rel[0] == -1 && rel[1] == -1 && rel[3] == -1 && rel[4] == -1;
+    if (total <= 0 || !(is_put || is_upd)) {
+      status = AMBRYCRC_MSG_BAD_LAYOUT;
+      break;
+    }
+    int64_t prev = -1, first = -1;
+    bool ok = true;
+    for (int k = 0; k < kMsgSlots; ++k) {
+      if (rel[k] == -1) continue;
+      if (rel[k] <= prev || rel[k] < (int32_t)h) ok = false;
+      if (first < 0) first = rel[k];
+      prev = rel[k];
+    }
+    if (!ok || (uint64_t)total > a.region_len - off || (uint64_t)first > a.region_len - off - (uint64_t)total) {
+      status = AMBRYCRC_MSG_BAD_LAYOUT;
+      break;
+    }
+    end = (uint64_t)first + (uint64_t)total;
+    for (int k = 0; k < kMsgSlots && ok; ++k) {
+      if (rel[k] == -1) continue;
+      uint64_t e = end;
+      for (int j = k + 1; j < kMsgSlots; ++j)
+        if (rel[j] != -1) {
+          e = (uint64_t)rel[j];
+          break;
+        }
+      if (e < (uint64_t)rel[k] + 8) ok = false;
+    }
+    if (!ok) {
+      status = AMBRYCRC_MSG_BAD_LAYOUT;
+      end = 0;
+      break;
+    }
+    for (int k = 0; k < kMsgSlots; ++k) {
+      if (rel[k] == -1) continue;
+      uint64_t e = end;
+      for (int j = k + 1; j < kMsgSlots; ++j)
+        if (rel[j] != -1) {
+          e = (uint64_t)rel[j];
+          break;
+        }
+      const uint64_t stored = be64(p + e - 8);
+      if (stored >> 32) status |= kRecordBit[k];  // a CRC32 never has upper bits: mismatch regardless
+      a.job_off[kMsgSlots * i + k] = off + (uint64_t)rel[k];
+      a.job_len[kMsgSlots * i + k] = e - (uint64_t)rel[k] - 8;
+      a.expected[kMsgSlots * i + k] = (uint32_t)stored;
+    }
+  } while (false);
+  a.status[i] = status;
+  if (a.msg_end) a.msg_end[i] = end ? off + end : 0;
+}
+
+__global__ __launch_bounds__(256) void msg_reduce_kernel(MsgArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.m) return;
+  uint32_t s = a.status[i];
+  for (int k = 0; k < kMsgSlots; ++k)
+    if (a.mismatch[kMsgSlots * i + k]) s |= kRecordBit[k];
+  a.status[i] = s;
+}
+
+hipError_t launch_msg_parse(const MsgArgs& a, hipStream_t s) {
+  if (a.m == 0) return hipSuccess;
+  hipLaunchKernelGGL(msg_parse_kernel, dim3((uint32_t)((a.m + 255) / 256)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_msg_reduce(const MsgArgs& a, hipStream_t s) {
+  if (a.m == 0) return hipSuccess;
+  hipLaunchKernelGGL(msg_reduce_kernel, dim3((uint32_t)((a.m + 255) / 256)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace ambrycrc

@@ -120,3 +120,34 @@ def timing_collect(device: int = 0):
     cnt = ctypes.c_int()
     check(lib().ambrycrc_timing_collect(device, ctypes.byref(ms), ctypes.byref(cnt)), "ambrycrc_timing_collect")
     return ms.value, cnt.value
+
+
+def messages_workspace_bytes(m: int) -> int:
+    return lib().ambrycrc_messages_workspace_bytes(m)
+
+
+def verify_messages(region, msg_off, stream=None, want_end: bool = True):
+    """GPU verify of every CRC of the messages starting at msg_off (int64 CUDA tensor) in `region`.
+
+    Returns (status int32[m] of AMBRYCRC_MSG_* bits, msg_end int64[m] or None).
+    """
+    torch = _torch()
+    if region.dtype != torch.uint8 or not region.is_cuda:
+        raise TypeError("region must be a uint8 CUDA tensor")
+    if msg_off.dtype != torch.int64 or not msg_off.is_cuda or not msg_off.is_contiguous():
+        raise TypeError("msg_off must be a contiguous int64 CUDA tensor")
+    m = msg_off.numel()
+    status = torch.empty(m, dtype=torch.int32, device=region.device)
+    end = torch.empty(m, dtype=torch.int64, device=region.device) if want_end else None
+    check(lib().ambrycrc_verify_messages_dev(_ptr(region), region.numel(), _ptr(msg_off), m, _ptr(status),
+                                             _ptr(end), None, 0, ctypes.c_void_p(_stream_handle(stream))),
+          "ambrycrc_verify_messages_dev")
+    return status, end
+
+
+def chain_messages_host(region: bytes, start: int = 0, max_messages: int = 1 << 20):
+    """Offsets of consecutive messages from `start` in a host buffer (BlobStoreRecovery's hop)."""
+    buf = (ctypes.c_char * len(region)).from_buffer_copy(region)
+    offs = (ctypes.c_uint64 * max_messages)()
+    n = lib().ambrycrc_chain_messages_host(ctypes.cast(buf, ctypes.c_void_p), len(region), start, offs, max_messages)
+    return list(offs[:n])

@@ -110,6 +110,43 @@ int ambrycrc_verify_dev(const uint8_t* d_base, const uint64_t* d_off, const uint
                         uint8_t* d_mismatch, uint32_t* d_mismatch_count, size_t n, void* d_ws,
                         size_t ws_bytes, hipStream_t stream);
 
+/* ------------------------------------------------- message-level verify (§8f) */
+
+/* Per-message status bits of ambrycrc_verify_messages_dev (0 = every CRC matches). */
+#define AMBRYCRC_MSG_HEADER_CRC (1u << 0)   /* header CRC (verifyHeader, MessageFormatRecord.java:1132-1145) */
+#define AMBRYCRC_MSG_ENCKEY_CRC (1u << 1)   /* BlobEncryptionKey_Format_V1 (:1588-1600) */
+#define AMBRYCRC_MSG_PROPS_CRC (1u << 2)    /* BlobProperties_Format_V1 (:1179-1195) */
+#define AMBRYCRC_MSG_UPDATE_CRC (1u << 3)   /* Update_Format_V1..V3 (:1215-1420) */
+#define AMBRYCRC_MSG_USERMETA_CRC (1u << 4) /* UserMetadata_Format_V1 (:1637-1649) */
+#define AMBRYCRC_MSG_BLOB_CRC (1u << 5)     /* Blob_Format_V1..V3 (:1668-1833) */
+#define AMBRYCRC_MSG_BAD_VERSION (1u << 8)  /* MessageFormatErrorCodes.UnknownFormatVersion */
+#define AMBRYCRC_MSG_BAD_LAYOUT (1u << 9)   /* HeaderConstraintError, or the message overruns the region */
+
+/* Bytes of device workspace ambrycrc_verify_messages_dev needs for m messages. */
+size_t ambrycrc_messages_workspace_bytes(size_t m);
+
+/* Verify every CRC of m PUT / update messages that start at d_msg_off[i] inside
+ * [d_region, d_region + region_len): header (V1/V2/V3), encryption key, blob
+ * properties, update, user metadata and blob records. d_status[i] gets the
+ * AMBRYCRC_MSG_* bits (all corrupt records, not just the first: the reference's
+ * deserializeBlobAll throws at the first, which is the lowest record bit set).
+ * A corrupt header stops the message there, as verifyHeader does. d_msg_end[i]
+ * (nullable) gets the offset one past the message, or 0 when unparseable.
+ * Batch form of deserializeBlobAll's checks (MessageFormatRecord.java:257-303),
+ * BlobStoreRecovery.recover (BlobStoreRecovery.java:43-110) and
+ * ValidatingTransformer.transform (ValidatingTransformer.java:46-104). */
+int ambrycrc_verify_messages_dev(const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off, size_t m,
+                                 uint32_t* d_status, uint64_t* d_msg_end, void* d_ws, size_t ws_bytes,
+                                 hipStream_t stream);
+
+/* Host-side message chain for a log region in host memory (the sequential hop of
+ * BlobStoreRecovery.recover, BlobStoreRecovery.java:43-110): starting at `start`,
+ * read each header (V1/V2/V3, header CRC checked) and follow its size to the next
+ * message; stops at the first unparseable header or region end. Writes up to
+ * `max` message offsets to offs; returns the count. */
+size_t ambrycrc_chain_messages_host(const uint8_t* region, uint64_t region_len, uint64_t start, uint64_t* offs,
+                                    size_t max);
+
 /* ------------------------------------------------------- host-resident batch */
 
 /* CRC-32 of n host chunks (ptrs[i], lens[i]) on `device`: chunks are packed into

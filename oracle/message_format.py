@@ -1,0 +1,212 @@
+"""oracle/message_format.py -- TEST INFRASTRUCTURE ONLY (never imported by the product).
+
+CPU restatement of Ambry's on-disk/on-wire message record layouts, used to
+build fixture log regions and to decide, per message, what
+deserializeBlobAll / update-record deserialization would report. It is the
+parity checker for ambrycrc_verify_messages_dev.
+
+Restated from ambry-messageformat/src/main/java/com/github/ambry/messageformat/:
+  MessageFormatRecord.java
+    :44-61     Version_Field_Size_In_Bytes = 2, Crc_Size = 8, header/record versions,
+               Message_Header_Invalid_Relative_Offset = -1
+    :467-486   MessageHeader_Format_V1.serializeHeader (version, totalSize, 4 relative offsets, CRC)
+    :696-725   MessageHeader_Format_V2.serializeHeader (+ encryption-key relative offset)
+    :951-981   MessageHeader_Format_V3.serializeHeader (+ lifeVersion)
+    :985-1030  checkHeaderConstraints (totalSize > 0, lifeVersion >= 0, put vs update offsets)
+    :1132-1145 verifyHeader / verifyCrc: CRC32 over header minus trailing 8 B
+    :1162-1195 BlobProperties_Format_V1 (version, BlobPropertiesSerDe bytes, CRC)
+    :1322-1379 Update_Format_V3 (version, account, container, updateTime, type, sub-record, CRC)
+    :1568-1601 BlobEncryptionKey_Format_V1 (version, int size, key, CRC)
+    :1619-1650 UserMetadata_Format_V1 (version, int size, content, CRC)
+    :1717-1755 Blob_Format_V2 (version, blobType, long size, content, CRC)
+    :1777-1833 Blob_Format_V3 (version, blobType, isCompressed, long size, content, CRC)
+    :257-303   deserializeBlobAll: header verified first (corrupt header -> no record parsed),
+               then encryption key (if present), blob properties, user metadata, blob.
+  PutMessageFormatInputStream.java:76-124,133-162 (record order and relative offsets)
+  BlobPropertiesSerDe.java:43-103 (VERSION_5 layout)
+Every record's CRC covers [record start, record end - 8) and is stored as a
+big-endian long with the upper 32 bits zero. CRCs come from zlib.crc32, the
+function java.util.zip.CRC32 computes.
+"""
+from __future__ import annotations
+
+import struct
+import zlib
+
+CRC_SIZE = 8
+INVALID = -1
+HEADER_SIZE = {1: 34, 2: 38, 3: 40}
+
+# status bits (mirrors include/ambrycrc.h AMBRYCRC_MSG_*)
+HEADER_CRC = 1 << 0
+ENCKEY_CRC = 1 << 1
+PROPS_CRC = 1 << 2
+UPDATE_CRC = 1 << 3
+USERMETA_CRC = 1 << 4
+BLOB_CRC = 1 << 5
+BAD_VERSION = 1 << 8
+BAD_LAYOUT = 1 << 9
+
+RECORD_BITS = (ENCKEY_CRC, PROPS_CRC, UPDATE_CRC, USERMETA_CRC, BLOB_CRC)  # slot order enc, bp, upd, um, blob
+
+
+def _crc_long(b: bytes) -> bytes:
+    return struct.pack(">q", zlib.crc32(b))
+
+
+def header(version, total, enc, bp, upd, um, blob, life=0):
+    if version == 1:
+        body = struct.pack(">hqiiii", 1, total, bp, upd, um, blob)
+    elif version == 2:
+        body = struct.pack(">hqiiiii", 2, total, enc, bp, upd, um, blob)
+    else:
+        body = struct.pack(">hhqiiiii", 3, life, total, enc, bp, upd, um, blob)
+    return body + _crc_long(body)
+
+
+def store_key(blob_id: str) -> bytes:
+    """MockId-style key bytes: short length + id (ambry-test-utils/.../store/MockId.java:47-77)."""
+    raw = blob_id.encode()
+    return struct.pack(">h", len(raw)) + raw
+
+
+def _int_string(s):
+    if s is None:
+        return struct.pack(">i", 0)
+    raw = s.encode()
+    return struct.pack(">i", len(raw)) + raw
+
+
+def blob_properties_bytes(blob_size, service_id="servid", owner_id="owner", content_type="application/octet",
+                          ttl=-1, private=False, creation_ms=1_700_000_000_000, account=101, container=5,
+                          encrypted=False, content_encoding=None, filename=None, reserved=None):
+    """BlobPropertiesSerDe.serializeBlobProperties, VERSION_5 (BlobPropertiesSerDe.java:80-103)."""
+    out = struct.pack(">hqbqq", 5, ttl, 1 if private else 0, creation_ms, blob_size)
+    out += _int_string(content_type) + _int_string(owner_id) + _int_string(service_id)
+    out += struct.pack(">hhb", account, container, 1 if encrypted else 0)
+    out += _int_string(content_encoding) + _int_string(filename) + _int_string(reserved)
+    return out
+
+
+def props_record(props: bytes) -> bytes:
+    body = struct.pack(">h", 1) + props
+    return body + _crc_long(body)
+
+
+def enckey_record(key: bytes) -> bytes:
+    body = struct.pack(">hi", 1, len(key)) + key
+    return body + _crc_long(body)
+
+
+def usermeta_record(um: bytes) -> bytes:
+    body = struct.pack(">hi", 1, len(um)) + um
+    return body + _crc_long(body)
+
+
+def blob_record(content: bytes, version=3, blob_type=0, compressed=False) -> bytes:
+    if version == 2:
+        body = struct.pack(">hhq", 2, blob_type, len(content)) + content
+    else:
+        body = struct.pack(">hhbq", 3, blob_type, 1 if compressed else 0, len(content)) + content
+    return body + _crc_long(body)
+
+
+def update_record_v3(account=101, container=5, update_ms=1_700_000_000_123, kind="ttl", expiry=1_800_000_000_000):
+    """Update_Format_V3 (MessageFormatRecord.java:1322-1379): TTL update / delete / undelete sub-records."""
+    types = {"delete": 0, "ttl": 1, "undelete": 2}
+    body = struct.pack(">hhhqh", 3, account, container, update_ms, types[kind])
+    if kind == "ttl":
+        body += struct.pack(">hq", 1, expiry)
+    else:
+        body += struct.pack(">h", 1)
+    return body + _crc_long(body)
+
+
+def put_message(key: bytes, props: bytes, usermeta: bytes, content: bytes, version=3, enc_key=None, life=0,
+                blob_version=None, compressed=False) -> bytes:
+    """PutMessageFormatInputStream: header, key, [encryption key], properties, user metadata, blob."""
+    h = HEADER_SIZE[version]
+    enc = enckey_record(enc_key) if (enc_key is not None and version >= 2) else b""
+    pr = props_record(props)
+    um = usermeta_record(usermeta)
+    bl = blob_record(content, version=blob_version or (3 if version != 1 else 3), compressed=compressed)
+    total = len(enc) + len(pr) + len(um) + len(bl)
+    enc_off = h + len(key) if enc else INVALID
+    bp_off = h + len(key) + len(enc)
+    um_off = bp_off + len(pr)
+    blob_off = um_off + len(um)
+    return header(version, total, enc_off, bp_off, INVALID, um_off, blob_off, life) + key + enc + pr + um + bl
+
+
+def update_message(key: bytes, version=3, life=1, **kw) -> bytes:
+    h = HEADER_SIZE[version]
+    rec = update_record_v3(**kw)
+    return header(version, len(rec), INVALID, INVALID, h + len(key), INVALID, INVALID, life) + key + rec
+
+
+def _be16(b, o):
+    return struct.unpack_from(">h", b, o)[0]
+
+
+def _be32(b, o):
+    return struct.unpack_from(">i", b, o)[0]
+
+
+def _be64(b, o):
+    return struct.unpack_from(">q", b, o)[0]
+
+
+def parse_header(region: bytes, off: int):
+    """(version, total, [enc, bp, upd, um, blob]) or None when the version is unknown."""
+    v = _be16(region, off)
+    if v == 1:
+        total = _be64(region, off + 2)
+        rel = [INVALID] + [_be32(region, off + 10 + 4 * i) for i in range(4)]
+    elif v == 2:
+        total = _be64(region, off + 2)
+        rel = [_be32(region, off + 10 + 4 * i) for i in range(5)]
+    elif v == 3:
+        total = _be64(region, off + 4)
+        rel = [_be32(region, off + 12 + 4 * i) for i in range(5)]
+    else:
+        return None
+    return v, total, rel
+
+
+def verify_message(region: bytes, off: int):
+    """(status bits, message end offset or 0) -- deserializeBlobAll / update-record semantics."""
+    if off + 2 > len(region):
+        return BAD_LAYOUT, 0
+    v = _be16(region, off)
+    if v not in HEADER_SIZE:
+        return BAD_VERSION, 0
+    h = HEADER_SIZE[v]
+    if off + h > len(region):
+        return BAD_LAYOUT, 0
+    stored = _be64(region, off + h - CRC_SIZE)
+    if zlib.crc32(region[off:off + h - CRC_SIZE]) != stored:
+        return HEADER_CRC, 0  # verifyHeader throws before any record is read
+    _, total, rel = parse_header(region, off)
+    if v == 3 and _be16(region, off + 2) < 0:  # lifeVersion >= 0 (checkHeaderConstraints, :990-1003)
+        return BAD_LAYOUT, 0
+    enc, bp, upd, um, blob = rel
+    is_put = bp != INVALID and upd == INVALID and um != INVALID and blob != INVALID
+    is_upd = upd != INVALID and bp == INVALID and um == INVALID and blob == INVALID and enc == INVALID
+    if total <= 0 or not (is_put or is_upd):
+        return BAD_LAYOUT, 0
+    present = [(k, r) for k, r in enumerate(rel) if r != INVALID]
+    starts = [r for _, r in present]
+    if starts[0] < h or any(b <= a for a, b in zip(starts, starts[1:])):
+        return BAD_LAYOUT, 0
+    end = starts[0] + total
+    if off + end > len(region):
+        return BAD_LAYOUT, 0
+    status = 0
+    for i, (k, s) in enumerate(present):
+        e = starts[i + 1] if i + 1 < len(present) else end
+        if e - s < CRC_SIZE:
+            return BAD_LAYOUT, 0
+        stored = _be64(region, off + e - CRC_SIZE)
+        if zlib.crc32(region[off + s:off + e - CRC_SIZE]) != stored:
+            status |= RECORD_BITS[k]
+    return status, off + end

@@ -1,0 +1,70 @@
+"""GPU parity for ambrycrc_verify_messages_dev against oracle/message_format.py (§8f next #1).
+
+Bit-exact per-message status and message-end offsets on log regions mixing PUT
+messages (header V1/V2/V3, with and without encryption-key records, blobs from
+0 B to ~300 KB) and update messages, with random single-bit corruptions, an
+unknown header version and a message truncated by the region end."""
+import struct
+
+import numpy as np
+import pytest
+
+from test_message_format import MF, build_region
+
+pytestmark = pytest.mark.gpu
+
+
+def run(gpu, region: bytes, offs):
+    import torch
+
+    r = torch.from_numpy(np.frombuffer(region, dtype=np.uint8).copy()).cuda()
+    o = torch.tensor(np.asarray(offs, dtype=np.int64), device="cuda")
+    status, end = gpu.verify_messages(r, o)
+    torch.cuda.synchronize()
+    return status.cpu().numpy().view(np.uint32).tolist(), end.cpu().numpy().tolist()
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_region_status_matches_oracle(gpu, seed):
+    region, offs, expect = build_region(n=600, seed=seed, corrupt_frac=0.1)
+    st, end = run(gpu, region, offs)
+    assert st == [s for s, _ in expect]
+    assert end == [e for _, e in expect]
+    assert sum(1 for s in st if s) >= 30
+
+
+def test_bad_version_truncated_and_out_of_range(gpu):
+    region, offs, _ = build_region(n=50, seed=9, corrupt_frac=0.0)
+    junk = struct.pack(">h", 7) + bytes(60)  # unknown header version
+    region2 = region + junk
+    last_msg = MF.put_message(MF.store_key("tail"), MF.blob_properties_bytes(5000), b"m" * 10, bytes(5000))
+    truncated = region2 + last_msg[:-100]
+    offs2 = offs + [len(region), len(region2), len(truncated) - 1, len(truncated) + 10]
+    expect = [MF.verify_message(truncated, o) if o + 2 <= len(truncated) else (MF.BAD_LAYOUT, 0) for o in offs2]
+    st, end = run(gpu, truncated, offs2)
+    assert st == [s for s, _ in expect]
+    assert end == [e for _, e in expect]
+    assert st[-4] == MF.BAD_VERSION and st[-3] == MF.BAD_LAYOUT
+
+
+def test_each_record_kind_flagged(gpu):
+    key = MF.store_key("id1")
+    msg = MF.put_message(key, MF.blob_properties_bytes(4096), b"u" * 1000, bytes(range(256)) * 16, version=3,
+                         enc_key=b"k" * 100)
+    upd = MF.update_message(key)
+    h, kl = 40, len(key)
+    enc_at = h + kl + 10
+    props_at = h + kl + len(MF.enckey_record(b"k" * 100)) + 10
+    um_at = len(msg) - len(MF.blob_record(bytes(4096))) - 500
+    blob_at = len(msg) - 1000
+    cases = [(msg, 5, MF.HEADER_CRC), (msg, enc_at, MF.ENCKEY_CRC), (msg, props_at, MF.PROPS_CRC),
+             (msg, um_at, MF.USERMETA_CRC), (msg, blob_at, MF.BLOB_CRC), (upd, h + kl + 3, MF.UPDATE_CRC),
+             (msg, len(msg) - 2, MF.BLOB_CRC)]
+    region, offs = bytearray(), []
+    for base, pos, _ in cases:
+        b = bytearray(base)
+        b[pos] ^= 0x01
+        offs.append(len(region))
+        region += b
+    st, _ = run(gpu, bytes(region), offs)
+    assert st == [bit for _, _, bit in cases]

@@ -1,0 +1,97 @@
+"""§8f next #1 -- message-level verify: oracle/message_format.py (CPU restatement of the
+record layouts) pinned against the reference tests' deterministic headers, and the
+host-side message chain of libambrycrc checked against it."""
+import struct
+import zlib
+
+import numpy as np
+import pytest
+
+from datagen import stream_bytes
+
+import importlib.util
+import os
+
+_spec = importlib.util.spec_from_file_location(
+    "message_format", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle",
+                                   "message_format.py"))
+MF = importlib.util.module_from_spec(_spec)
+_spec.loader.exec_module(MF)
+
+
+def build_region(n=300, seed=7, corrupt_frac=0.1, big_every=17):
+    """A log region of PUT (V1/V2/V3, +/- encryption key) and update messages, some corrupted.
+    Returns (region bytes, message offsets, expected status list from the oracle)."""
+    rng = np.random.default_rng(seed)
+    out = bytearray()
+    offs = []
+    for i in range(n):
+        key = MF.store_key(f"blob-{i:06d}-{seed}")
+        kind = rng.integers(0, 10)
+        if kind == 0:
+            msg = MF.update_message(key, version=3, kind=["ttl", "delete", "undelete"][i % 3])
+        else:
+            ver = [1, 2, 3, 3][int(rng.integers(0, 4))]
+            size = int(rng.integers(0, 5000)) if i % big_every else int(rng.integers(60000, 300000))
+            content = stream_bytes(seed * 100003 + i, 0, size).tobytes()
+            um = stream_bytes(seed + i, 7, int(rng.integers(0, 1200))).tobytes()
+            enc = stream_bytes(i, 3, 100).tobytes() if (ver >= 2 and i % 2) else None
+            msg = MF.put_message(key, MF.blob_properties_bytes(size), um, content, version=ver, enc_key=enc,
+                                 life=int(i % 3), compressed=bool(i % 5 == 0))
+        offs.append(len(out))
+        out += msg
+    region = bytearray(out)
+    for i in rng.choice(n, size=int(n * corrupt_frac), replace=False):
+        start = offs[i]
+        end = offs[i + 1] if i + 1 < n else len(region)
+        pos = int(rng.integers(start, end))
+        region[pos] ^= 1 << int(rng.integers(0, 8))
+    region = bytes(region)
+    expect = [MF.verify_message(region, o) for o in offs]
+    return region, offs, expect
+
+
+def test_oracle_headers_match_golden(vectors):
+    hv = {h["name"]: h for h in vectors["message_headers"]}
+    h1 = MF.header(1, 1000, -1, 10, -1, 20, 30)
+    assert h1[:26].hex() == hv["MessageHeader_Format_V1 (MessageFormatRecordTest.java:70)"]["hex"]
+    assert struct.unpack(">q", h1[26:])[0] == int(hv["MessageHeader_Format_V1 (MessageFormatRecordTest.java:70)"]["crc"], 16)
+    h3 = MF.header(3, 1000, 5, 10, -1, 20, 30, life=2)
+    assert h3[:32].hex() == hv["MessageHeader_Format_V3 (MessageFormatRecordTest.java:115)"]["hex"]
+    assert struct.unpack(">q", h3[32:])[0] == 0xA4893031
+
+
+def test_clean_messages_verify_and_chain(ambry):
+    region, offs, expect = build_region(n=120, corrupt_frac=0.0)
+    assert all(s == 0 for s, _ in expect)
+    ends = [e for _, e in expect]
+    assert ends[:-1] == offs[1:] and ends[-1] == len(region)
+    from ambry_amd.device import chain_messages_host
+
+    assert chain_messages_host(region, 0) == offs
+
+
+def test_oracle_detects_every_single_bit_flip():
+    """MessageFormatRecordTest.deserializeTest / BlobStoreRecoveryTest.crcErrorRecoveryTest: one corrupted byte
+    anywhere in a message is reported (header bit, a record bit, or a layout error) -- except inside the
+    store key, which Ambry's format does not cover with any CRC (the key is validated by StoreKeyFactory)."""
+    key = MF.store_key("id1")
+    msg = MF.put_message(key, MF.blob_properties_bytes(4096), b"u" * 1000, stream_bytes(1, 0, 4096).tobytes(),
+                         version=3, enc_key=b"k" * 100)
+    assert MF.verify_message(msg, 0) == (0, len(msg))
+    rng = np.random.default_rng(0)
+    key_span = range(40, 40 + len(key))
+    for pos in list(range(0, 200)) + list(rng.integers(200, len(msg), size=200)):
+        bad = bytearray(msg)
+        bad[pos] ^= 0x10
+        st, _ = MF.verify_message(bytes(bad), 0)
+        assert (st == 0) == (pos in key_span), pos
+
+
+def test_chain_stops_at_corrupt_header(ambry):
+    region, offs, _ = build_region(n=40, corrupt_frac=0.0)
+    bad = bytearray(region)
+    bad[offs[25] + 3] ^= 0xFF
+    from ambry_amd.device import chain_messages_host
+
+    assert chain_messages_host(bytes(bad), 0) == offs[:25]
