@@ -110,7 +110,7 @@ struct DevCtx {
   int device = -1;
   int num_cu = 0;
   int grid = 0;
-  int variant = 0;  // U=8, nontemporal loads, rolling prefetch, 2 pieces interleaved (tools/sweep.py)
+  int variant = 0;  // U=8, NT loads, rolling prefetch, 2 pieces interleaved, descriptor window (tools/sweep.py)
   uint32_t* d_img = nullptr;
   void* d_ws = nullptr;
   size_t ws_bytes = 0;
@@ -496,6 +496,23 @@ int ambrycrc_batch_host(const void* const* ptrs, const uint64_t* lens, const uin
   if (rc3) return rc3;
   for (size_t i = 0; i < n; ++i) out[i] = acc[i];
   return AMBRYCRC_OK;
+}
+
+int ambrycrc_range_checksums_host(const uint8_t* file, uint64_t file_len, const int64_t* first, const int64_t* second,
+                                  size_t n, uint32_t* out, int device) {
+  if (n == 0) return AMBRYCRC_OK;
+  if (!first || !second || !out || (!file && file_len)) return AMBRYCRC_EINVAL;
+  for (size_t i = 0; i < n; ++i)
+    if (first[i] < 0 || second[i] < 0 || first[i] > second[i]) return AMBRYCRC_EINVAL;
+  std::vector<const void*> ptrs(n);
+  std::vector<uint64_t> lens(n);
+  for (size_t i = 0; i < n; ++i) {
+    const uint64_t a = std::min<uint64_t>((uint64_t)first[i], file_len);
+    const uint64_t b = std::min<uint64_t>((uint64_t)second[i], file_len);
+    ptrs[i] = file ? file + a : nullptr;
+    lens[i] = b - a;
+  }
+  return ambrycrc_batch_host(ptrs.data(), lens.data(), nullptr, out, n, device, 0);
 }
 
 int ambrycrc_set_variant(int device, int variant) {

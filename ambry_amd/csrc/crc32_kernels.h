@@ -31,9 +31,9 @@ struct SweepArgs {
 };
 
 // sweep-kernel variants (U = loads in flight per lane, NT = nontemporal, PIPE = rolling prefetch,
-// IL = two pieces interleaved): 0 U8/NT/PIPE/IL (default), 1 U8/NT/PIPE, 2 U4/NT/PIPE,
-// 3 U12/NT/PIPE/IL, 4 U8/PIPE/IL (temporal loads), 5 U8/NT batch loads, 6 U4/NT/PIPE/IL,
-// 7 U8 batch loads (temporal)
+// IL = two pieces interleaved, WIN = descriptors fetched 64 per wave-load, else one-ahead scalar
+// prefetch): 0 U8/NT/PIPE/IL/WIN (default), 1 = 0 without WIN, 2 U8/NT/PIPE/WIN, 3 U4/NT/PIPE/WIN,
+// 4 U8/PIPE/IL/WIN (temporal loads), 5 U8/NT batch loads, 6 U4/NT/PIPE/IL/WIN, 7 U8 batch (temporal)
 constexpr int kNumVariants = 8;
 
 // Message verify (message_kernels.hip): kMsgSlots CRC jobs per message, slot order

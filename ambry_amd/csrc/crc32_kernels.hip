@@ -44,6 +44,27 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
+// Cross-lane moves without LDS: DPP row shifts / broadcasts (lanes with no source read 0).
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xf, false);
+}
+
+// Value of lane (l - 2^lvl) delivered to every lane l with bit lvl set (the tree's left partner):
+// row_shr:1/2/4/8 inside 16-lane rows, then row_bcast:15 (rows 1,3) and row_bcast:31 (rows 2,3).
+template <int LVL>
+__device__ __forceinline__ uint32_t tree_partner(uint32_t v) {
+  if constexpr (LVL < 4) return dpp<0x110 + (1 << LVL), 0xf>(v);
+  else if constexpr (LVL == 4) return dpp<0x142, 0xa>(v);
+  else return dpp<0x143, 0xc>(v);
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t lane) {
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, lane);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), lane);
+  return ((uint64_t)hi << 32) | lo;
+}
+
 // Per-lane address constants for slice table j: region bit, (j&1)*128, lane column.
 struct LaneConst {
   uint32_t L0, L1, L2, L3;
@@ -121,6 +142,32 @@ __device__ __forceinline__ u32x4 ld16(const u32x4* p) {
   }
 }
 
+template <int LVL>
+__device__ __forceinline__ uint32_t tree_level(uint32_t s, uint32_t lane) {
+  const uint32_t sh = nib_mul(tree_partner<LVL>(s), kTreeOff + kNibSetBytes * LVL);
+  return (lane & (1u << LVL)) ? (s ^ sh) : s;
+}
+
+// Raw CRC (zero register) of the t < 16 bytes at p, lane-parallel: lane j holds byte j, whose
+// contribution is T0[b] advanced over the t-1-j bytes after it = T_{k&3}[b] * x^(32*(k>>2)),
+// k = t-1-j; then an XOR over the 16 lanes of row 0. Result valid in every lane of row 0.
+__device__ __forceinline__ uint32_t tail_crc(const uint8_t* __restrict__ p, uint32_t t, uint32_t lane) {
+  uint32_t v = 0;
+  if (lane < t) {
+    const uint32_t b = p[lane];
+    const uint32_t k = t - 1 - lane;
+    const uint32_t j = k & 3;
+    v = lds_rd(((j >> 1) << 16) | (b << 8) | ((j & 1) << 7) | ((lane & 31) << 2));
+    if (k & 4) v = nib_mul(v, kPowOff + kNibSetBytes * 2);  // x^(8*4)
+    if (k & 8) v = nib_mul(v, kPowOff + kNibSetBytes * 3);  // x^(8*8)
+  }
+  v ^= dpp<0x128, 0xf>(v);  // row_ror:8
+  v ^= dpp<0x124, 0xf>(v);  // row_ror:4
+  v ^= dpp<0x122, 0xf>(v);  // row_ror:2
+  v ^= dpp<0x121, 0xf>(v);  // row_ror:1
+  return v;
+}
+
 // Raw CRC of body [bs, be) (be 16-aligned, bs <= be arbitrary), returned in lane 63
 // (other lanes: junk). Bytes below bs are treated as zeros, which leave a zero
 // register unchanged, so the virtual range is aligned down to whole 1 KiB blocks.
@@ -195,13 +242,14 @@ __device__ __forceinline__ uint32_t body_crc(const uint8_t* __restrict__ base, u
     s = rpiece(x, k, nib_mul(s, kFoldOff));
   }
 
-  // Lane l's stream ends 16(63-l) bytes before be: xor-tree with shifts 16*2^lvl.
-#pragma unroll
-  for (int lvl = 0; lvl < 6; ++lvl) {
-    const uint32_t o = __shfl_xor(s, 1 << lvl);
-    const uint32_t sh = nib_mul(o, kTreeOff + kNibSetBytes * lvl);
-    s = (lane & (1u << lvl)) ? (s ^ sh) : s;
-  }
+  // Lane l's stream ends 16(63-l) bytes before be: xor-tree with shifts 16*2^lvl,
+  // partners delivered by DPP (no LDS round trip for the move itself).
+  s = tree_level<0>(s, lane);
+  s = tree_level<1>(s, lane);
+  s = tree_level<2>(s, lane);
+  s = tree_level<3>(s, lane);
+  s = tree_level<4>(s, lane);
+  s = tree_level<5>(s, lane);
   return s;
 }
 
@@ -241,7 +289,7 @@ __device__ __forceinline__ uint64_t snap_cut(uint64_t cs, uint64_t len, uint64_t
 // as one concatenated stream (byte_start = exclusive scan of len), i.e. an equal share of
 // bytes whatever the chunk-size mix. Each (wave, chunk) intersection is a segment whose
 // raw CRC is shifted to the chunk end and XORed into out[chunk].
-template <int U, bool NT, bool PIPE, bool IL>
+template <int U, bool NT, bool PIPE, bool IL, bool WIN>
 __global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
   {
     const u32x4* src = reinterpret_cast<const u32x4*>(a.img);
@@ -262,17 +310,17 @@ __global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
   const uint32_t* xpow2 = a.img + kLdsBytes / 4;
   const LaneConst k = make_lane_const(lane);
 
-  for (uint32_t c = __builtin_amdgcn_readfirstlane(find_chunk(a.byte_start, a.n, g0, lane)); c < a.n; ++c) {
-    const uint64_t bsc = a.byte_start[c];
-    if (bsc >= g1) break;
-    const uint64_t len = a.len[c];
-    if (len == 0) continue;  // empty chunks are finished by the plan kernel
-    const uint64_t cs = a.off[c];
+  uint64_t init_len = ~0ull;  // one-entry cache of the init term for crc_in == 0
+  uint32_t init_term = 0;
+  uint32_t c = __builtin_amdgcn_readfirstlane(find_chunk(a.byte_start, a.n, g0, lane));
+
+  // One segment: raw CRC of its body, shifted to the chunk end, + tail + init, XORed into out[ci].
+  auto segment = [&](uint32_t ci, uint64_t bsc, uint64_t len, uint64_t cs, uint32_t cin) {
     const uint64_t ce = cs + len;
     const uint64_t cb = aligned_end(cs, ce);
     const uint64_t r0 = g0 > bsc ? snap_cut(cs, len, g0 - bsc) : 0;
     const uint64_t r1 = g1 - bsc < len ? snap_cut(cs, len, g1 - bsc) : len;
-    if (r0 >= r1) continue;
+    if (r0 >= r1) return;
     const uint64_t sa = cs + r0, se = cs + r1;
     const uint64_t be = se == ce ? cb : se;  // 16-B aligned body end
     uint32_t r = 0;
@@ -281,16 +329,67 @@ __global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
       r = __builtin_amdgcn_readlane(r, 63);
       r = shift_bytes(r, ce - be, xpow2);
     }
-    if (se == ce) {  // trailing < 16 bytes, byte-wise through T0 (lane column 0)
-      uint32_t tr = 0;
-      for (uint64_t p = sa > cb ? sa : cb; p < ce; ++p) tr = (tr >> 8) ^ lds_rd(((tr ^ a.base[p]) & 0xffu) << 8);
-      r ^= tr;
+    if (se == ce && ce > cb) {  // trailing < 16 bytes, lane-parallel
+      const uint64_t t0 = sa > cb ? sa : cb;
+      r ^= __builtin_amdgcn_readlane(tail_crc(a.base + t0, (uint32_t)(ce - t0), lane), 0);
     }
     if (r0 == 0) {  // initial register ~crc_in advanced over the chunk, plus xor-out
-      const uint32_t cin = a.crc_in ? a.crc_in[c] : 0u;
-      r ^= shift_bytes(~cin, len, xpow2) ^ 0xFFFFFFFFu;
+      if (cin == 0) {
+        if (len != init_len) {
+          init_term = shift_bytes(0xFFFFFFFFu, len, xpow2) ^ 0xFFFFFFFFu;
+          init_len = len;
+        }
+        r ^= init_term;
+      } else {
+        r ^= shift_bytes(~cin, len, xpow2) ^ 0xFFFFFFFFu;
+      }
     }
-    if (lane == 0) atomicXor(&a.out[c], r);
+    if (lane == 0) atomicXor(&a.out[ci], r);
+  };
+
+  if constexpr (WIN) {
+    // Descriptors fetched 64 at a time (lane j <- chunk c+j), read back with readlane:
+    // one load round trip per 64 chunks (costs 7 VGPRs live across the body).
+    bool done = false;
+    while (!done && c < a.n) {
+      const uint32_t cnt = a.n - c < 64u ? a.n - c : 64u;
+      uint64_t w_bs = ~0ull, w_len = 0, w_off = 0;
+      uint32_t w_cin = 0;
+      if (lane < cnt) {
+        w_bs = a.byte_start[c + lane];
+        w_len = a.len[c + lane];
+        w_off = a.off[c + lane];
+        w_cin = a.crc_in ? a.crc_in[c + lane] : 0u;
+      }
+      for (uint32_t j = 0; j < cnt; ++j) {
+        const uint64_t bsc = readlane64(w_bs, j);
+        if (bsc >= g1) {
+          done = true;
+          break;
+        }
+        const uint64_t len = readlane64(w_len, j);
+        if (len == 0) continue;  // empty chunks are finished by the plan kernel
+        segment(c + j, bsc, len, readlane64(w_off, j), __builtin_amdgcn_readlane(w_cin, j));
+      }
+      c += cnt;
+    }
+  } else {
+    // One-ahead prefetch of the next descriptor into scalar registers while this chunk runs.
+    uint64_t n_bs = a.byte_start[c], n_len = a.len[c], n_off = a.off[c];
+    uint32_t n_cin = a.crc_in ? a.crc_in[c] : 0u;
+    while (c < a.n) {
+      const uint64_t bsc = n_bs, len = n_len, cs = n_off;
+      const uint32_t cin = n_cin;
+      if (bsc >= g1) break;
+      if (c + 1 < a.n) {
+        n_bs = a.byte_start[c + 1];
+        n_len = a.len[c + 1];
+        n_off = a.off[c + 1];
+        n_cin = a.crc_in ? a.crc_in[c + 1] : 0u;
+      }
+      if (len != 0) segment(c, bsc, len, cs, cin);  // empty chunks are finished by the plan kernel
+      ++c;
+    }
   }
 }
 
@@ -394,16 +493,16 @@ hipError_t launch_plan(const PlanArgs& a, hipStream_t s) {
 
 hipError_t launch_sweep(const SweepArgs& a, int grid, int variant, hipStream_t s) {
   switch (variant) {
-#define AMBRY_TILES_CASE(V, U, NT, PIPE, IL) \
-  case V: hipLaunchKernelGGL((crc32_sweep_kernel<U, NT, PIPE, IL>), dim3(grid), dim3(1024), 0, s, a); break;
-    AMBRY_TILES_CASE(0, 8, true, true, true)
-    AMBRY_TILES_CASE(1, 8, true, true, false)
-    AMBRY_TILES_CASE(2, 4, true, true, false)
-    AMBRY_TILES_CASE(3, 12, true, true, true)
-    AMBRY_TILES_CASE(4, 8, false, true, true)
-    AMBRY_TILES_CASE(5, 8, true, false, false)
-    AMBRY_TILES_CASE(6, 4, true, true, true)
-    AMBRY_TILES_CASE(7, 8, false, false, false)
+#define AMBRY_TILES_CASE(V, U, NT, PIPE, IL, WIN) \
+  case V: hipLaunchKernelGGL((crc32_sweep_kernel<U, NT, PIPE, IL, WIN>), dim3(grid), dim3(1024), 0, s, a); break;
+    AMBRY_TILES_CASE(0, 8, true, true, true, true)
+    AMBRY_TILES_CASE(1, 8, true, true, true, false)
+    AMBRY_TILES_CASE(2, 8, true, true, false, true)
+    AMBRY_TILES_CASE(3, 4, true, true, false, true)
+    AMBRY_TILES_CASE(4, 8, false, true, true, true)
+    AMBRY_TILES_CASE(5, 8, true, false, false, true)
+    AMBRY_TILES_CASE(6, 4, true, true, true, true)
+    AMBRY_TILES_CASE(7, 8, false, false, false, true)
 #undef AMBRY_TILES_CASE
     default: return hipErrorInvalidValue;
   }

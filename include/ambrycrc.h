@@ -161,6 +161,18 @@ size_t ambrycrc_chain_messages_host(const uint8_t* region, uint64_t region_len, 
 int ambrycrc_batch_host(const void* const* ptrs, const uint64_t* lens, const uint32_t* crc_in, uint32_t* out,
                         size_t n, int device, int pinned);
 
+/* CRC-32 of byte ranges of one file image in host memory, on `device` (§8f row 3).
+ * Replaces FileStore.getChecksumsForRanges (ambry-store/.../FileStore.java:567-595)
+ * with its exact semantics: range i covers [first[i], second[i]) -- `second - first`
+ * bytes, as the reference computes `size` (StoreFileCopyHandler.getChecksumRanges
+ * builds second = start + size - 1, so the last byte of each range is not covered) --
+ * truncated at EOF like the reference's FileChannel.read, empty past EOF. Returns
+ * AMBRYCRC_EINVAL, computing nothing, if any range has first < 0, second < 0 or
+ * first > second (the reference's IllegalArgumentException). out[i] is the value
+ * the reference renders with Long.toString. */
+int ambrycrc_range_checksums_host(const uint8_t* file, uint64_t file_len, const int64_t* first, const int64_t* second,
+                                  size_t n, uint32_t* out, int device);
+
 /* ------------------------------------------------------- tuning / telemetry */
 
 /* Variant (unroll depth / load policy / prefetch scheme, 0..7) of the sweep kernel;

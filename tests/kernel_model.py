@@ -108,6 +108,21 @@ class KernelModel:
             s = np.where((LANES & (1 << lvl)) != 0, s ^ sh, s).astype(np.uint32)
         return int(s[63])
 
+    def tail_crc(self, mem, p0: int, t: int) -> int:
+        """Lane-parallel tail (kernel tail_crc): lane j: T_{k&3}[b_j] * x^(32*(k>>2)), k = t-1-j; XOR."""
+        acc = 0
+        for lane in range(t):
+            b = int(mem[p0 + lane])
+            k = t - 1 - lane
+            j = k & 3
+            v = int(self.lds(((j >> 1) << 16) | (b << 8) | ((j & 1) << 7) | ((lane & 31) << 2)))
+            if k & 4:
+                v = int(self.nib_mul(np.array([v], dtype=np.uint32), K_POW_OFF + K_NIB_SET * 2)[0])
+            if k & 8:
+                v = int(self.nib_mul(np.array([v], dtype=np.uint32), K_POW_OFF + K_NIB_SET * 3)[0])
+            acc ^= v
+        return acc
+
     def batch(self, mem: np.ndarray, off, length, crc_in=None, nwaves: int = 4096, quantum: int = 1024):
         """Replays plan + sweep kernels with `nwaves` waves; returns the list of CRCs."""
         n = len(off)
@@ -147,11 +162,8 @@ class KernelModel:
                 r = 0
                 if sa < be:
                     r = self.shift_bytes(self.body_crc(mem, sa, be), ce - be)
-                if se == ce:
-                    tr = 0
-                    for p in range(max(sa, cb), ce):
-                        tr = (tr >> 8) ^ int(self.lds(((tr ^ int(mem[p])) & 0xFF) << 8))
-                    r ^= tr
+                if se == ce and ce > cb:
+                    r ^= self.tail_crc(mem, max(sa, cb), ce - max(sa, cb))
                 if r0 == 0:
                     cin = 0 if crc_in is None else int(crc_in[c])
                     r ^= self.shift_bytes((~cin) & 0xFFFFFFFF, ln) ^ 0xFFFFFFFF
