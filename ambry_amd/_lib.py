@@ -45,6 +45,10 @@ _SIGNATURES = [
     ("ambrycrc_batch_host", ctypes.c_int,
      [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32),
       ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t, ctypes.c_int, ctypes.c_int]),
+    ("ambrycrc_put_crcs", ctypes.c_int,
+     [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_void_p),
+      ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint64),
+      ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),
     ("ambrycrc_range_checksums_host", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
       ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint32), ctypes.c_int]),

@@ -498,6 +498,21 @@ int ambrycrc_batch_host(const void* const* ptrs, const uint64_t* lens, const uin
   return AMBRYCRC_OK;
 }
 
+int ambrycrc_put_crcs(const uint8_t* const* fields, const uint64_t* field_len, const uint8_t* const* prefix,
+                      const uint64_t* prefix_len, const uint32_t* blob_crc, const uint64_t* blob_len, size_t n,
+                      uint32_t* wire_out, uint32_t* record_out) {
+  if (n == 0) return AMBRYCRC_OK;
+  if (!blob_crc || !blob_len) return AMBRYCRC_EINVAL;
+  if (wire_out && (!fields || !field_len)) return AMBRYCRC_EINVAL;
+  if (record_out && (!prefix || !prefix_len)) return AMBRYCRC_EINVAL;
+  for (size_t i = 0; i < n; ++i) {
+    const uint32_t xb = host_xpow8(blob_len[i]);  // shared by both combines
+    if (wire_out) wire_out[i] = gf2_mul(ambrycrc_update(0, fields[i], field_len[i]), xb) ^ blob_crc[i];
+    if (record_out) record_out[i] = gf2_mul(ambrycrc_update(0, prefix[i], prefix_len[i]), xb) ^ blob_crc[i];
+  }
+  return AMBRYCRC_OK;
+}
+
 int ambrycrc_range_checksums_host(const uint8_t* file, uint64_t file_len, const int64_t* first, const int64_t* second,
                                   size_t n, uint32_t* out, int device) {
   if (n == 0) return AMBRYCRC_OK;

@@ -161,6 +161,20 @@ size_t ambrycrc_chain_messages_host(const uint8_t* region, uint64_t region_len, 
 int ambrycrc_batch_host(const void* const* ptrs, const uint64_t* lens, const uint32_t* crc_in, uint32_t* out,
                         size_t n, int device, int pinned);
 
+/* One-pass PUT CRCs (§8f row 2). For each of n PUT requests whose blob CRC blob_crc[i]
+ * (over blob_len[i] bytes, e.g. from ambrycrc_batch_dev/ambrycrc_batch_host) is known:
+ *   wire_out[i]   = crc32(fields[i] || blob)   -- PutRequest.prepareBuffer's CRC over blobId,
+ *                   properties, user metadata, blobType, key, isCompressed, blobSize and the blob
+ *                   (ambry-protocol/.../PutRequest.java:238-283), verified by PutRequest_V5.readFrom
+ *                   (:497-521)
+ *   record_out[i] = crc32(prefix[i] || blob)   -- the Blob_Format_V3 record CRC seeded by its 13-B
+ *                   prefix (MessageFormatRecord.java:1789-1795, PutMessageFormatInputStream.java:116-120)
+ * so the blob bytes are scanned once instead of twice (three times counting the receive check).
+ * fields/prefix are host byte arrays; either output may be NULL. Host-only arithmetic. */
+int ambrycrc_put_crcs(const uint8_t* const* fields, const uint64_t* field_len, const uint8_t* const* prefix,
+                      const uint64_t* prefix_len, const uint32_t* blob_crc, const uint64_t* blob_len, size_t n,
+                      uint32_t* wire_out, uint32_t* record_out);
+
 /* CRC-32 of byte ranges of one file image in host memory, on `device` (§8f row 3).
  * Replaces FileStore.getChecksumsForRanges (ambry-store/.../FileStore.java:567-595)
  * with its exact semantics: range i covers [first[i], second[i]) -- `second - first`
