@@ -533,7 +533,7 @@ int ambrycrc_range_checksums_host(const uint8_t* file, uint64_t file_len, const 
 int ambrycrc_set_variant(int device, int variant) {
   DevCtx* c = ctx_for(device);
   if (!c) return AMBRYCRC_ENOINIT;
-  if (variant < 0 || variant >= kNumVariants) return AMBRYCRC_EINVAL;
+  if ((variant < 0 || variant >= kNumVariants) && variant != kDiagNoFold) return AMBRYCRC_EINVAL;
   c->variant = variant;
   return AMBRYCRC_OK;
 }

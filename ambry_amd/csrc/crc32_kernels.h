@@ -35,6 +35,7 @@ struct SweepArgs {
 // prefetch): 0 U8/NT/PIPE/IL/WIN (default), 1 = 0 without WIN, 2 U8/NT/PIPE/WIN, 3 U4/NT/PIPE/WIN,
 // 4 U8/PIPE/IL/WIN (temporal loads), 5 U8/NT batch loads, 6 U4/NT/PIPE/IL/WIN, 7 U8 batch (temporal)
 constexpr int kNumVariants = 8;
+constexpr int kDiagNoFold = 100;  // diagnostic timing build, selectable via ambrycrc_set_variant only
 
 // Message verify (message_kernels.hip): kMsgSlots CRC jobs per message, slot order
 // encryption key, blob properties, update, user metadata, blob.

@@ -122,6 +122,27 @@ __device__ __forceinline__ uint32_t shift_bytes(uint32_t v, uint64_t n, const ui
   return v;
 }
 
+template <int DIAG>
+__device__ __forceinline__ uint32_t fold(uint32_t s) {
+  if constexpr (DIAG == 1) {
+    return s ^ (s >> 7);  // diagnostic timing build: no LDS fold (wrong CRC)
+  } else {
+    return nib_mul(s, kFoldOff);
+  }
+}
+
+template <int DIAG>
+__device__ __forceinline__ uint32_t rpiece_pair_d(u32x4 w0, u32x4 w1, const LaneConst& k, uint32_t s) {
+  uint32_t x0 = slice4(w0.x, k, w0.y);
+  uint32_t x1 = slice4(w1.x, k, w1.y);
+  x0 = slice4(x0, k, w0.z);
+  x1 = slice4(x1, k, w1.z);
+  x0 = slice4(x0, k, w0.w);
+  x1 = slice4(x1, k, w1.w);
+  s = slice4(x0, k, fold<DIAG>(s));
+  return slice4(x1, k, fold<DIAG>(s));
+}
+
 __device__ __forceinline__ uint32_t rpiece_pair(u32x4 w0, u32x4 w1, const LaneConst& k, uint32_t s) {
   uint32_t x0 = slice4(w0.x, k, w0.y);
   uint32_t x1 = slice4(w1.x, k, w1.y);
@@ -171,7 +192,7 @@ __device__ __forceinline__ uint32_t tail_crc(const uint8_t* __restrict__ p, uint
 // Raw CRC of body [bs, be) (be 16-aligned, bs <= be arbitrary), returned in lane 63
 // (other lanes: junk). Bytes below bs are treated as zeros, which leave a zero
 // register unchanged, so the virtual range is aligned down to whole 1 KiB blocks.
-template <int U, bool NT, bool PIPE, bool IL>
+template <int U, bool NT, bool PIPE, bool IL, int DIAG = 0>
 __device__ __forceinline__ uint32_t body_crc(const uint8_t* __restrict__ base, uint64_t bs, uint64_t be,
                                              uint32_t lane, const LaneConst& k) {
   const uint64_t nb = (be - bs + kBlockBytes - 1) / kBlockBytes;
@@ -213,7 +234,7 @@ __device__ __forceinline__ uint32_t body_crc(const uint8_t* __restrict__ base, u
             const u32x4 w0 = buf[u], w1 = buf[u + 1];
             buf[u] = ld16<NT>(q + (b + U + u) * (kBlockBytes / 16));
             buf[u + 1] = ld16<NT>(q + (b + U + u + 1) * (kBlockBytes / 16));
-            s = rpiece_pair(w0, w1, k, s);
+            s = rpiece_pair_d<DIAG>(w0, w1, k, s);
           }
         } else {
 #pragma unroll
@@ -289,7 +310,7 @@ __device__ __forceinline__ uint64_t snap_cut(uint64_t cs, uint64_t len, uint64_t
 // as one concatenated stream (byte_start = exclusive scan of len), i.e. an equal share of
 // bytes whatever the chunk-size mix. Each (wave, chunk) intersection is a segment whose
 // raw CRC is shifted to the chunk end and XORed into out[chunk].
-template <int U, bool NT, bool PIPE, bool IL, bool WIN>
+template <int U, bool NT, bool PIPE, bool IL, bool WIN, int DIAG = 0>
 __global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
   {
     const u32x4* src = reinterpret_cast<const u32x4*>(a.img);
@@ -325,7 +346,7 @@ __global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
     const uint64_t be = se == ce ? cb : se;  // 16-B aligned body end
     uint32_t r = 0;
     if (sa < be) {
-      r = body_crc<U, NT, PIPE, IL>(a.base, sa, be, lane, k);
+      r = body_crc<U, NT, PIPE, IL, DIAG>(a.base, sa, be, lane, k);
       r = __builtin_amdgcn_readlane(r, 63);
       r = shift_bytes(r, ce - be, xpow2);
     }
@@ -503,6 +524,9 @@ hipError_t launch_sweep(const SweepArgs& a, int grid, int variant, hipStream_t s
     AMBRY_TILES_CASE(5, 8, true, false, false, true)
     AMBRY_TILES_CASE(6, 4, true, true, true, true)
     AMBRY_TILES_CASE(7, 8, false, false, false, true)
+    case kDiagNoFold:  // timing-only diagnostic (wrong CRCs): FOLD lookups removed
+      hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, true, true, 1>), dim3(grid), dim3(1024), 0, s, a);
+      break;
 #undef AMBRY_TILES_CASE
     default: return hipErrorInvalidValue;
   }
