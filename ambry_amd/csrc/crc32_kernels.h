@@ -34,7 +34,9 @@ struct SweepArgs {
 // IL = two pieces interleaved, WIN = descriptors fetched 64 per wave-load, else one-ahead scalar
 // prefetch): 0 U8/NT/PIPE/IL/WIN (default), 1 = 0 without WIN, 2 U8/NT/PIPE/WIN, 3 U4/NT/PIPE/WIN,
 // 4 U8/PIPE/IL/WIN (temporal loads), 5 U8/NT batch loads, 6 U4/NT/PIPE/IL/WIN, 7 U8 batch (temporal)
-constexpr int kNumVariants = 8;
+// 8 R=2 strided lane runs (U8 loads in flight), 9 R=4 strided runs (U8), 10 R=4 strided (U4),
+// 11 R=2 strided (U4), 12 64-B runs by quad transpose of coalesced loads (U8), 13 same (U4)
+constexpr int kNumVariants = 14;
 constexpr int kDiagNoFold = 100;  // diagnostic timing build, selectable via ambrycrc_set_variant only
 
 // Message verify (message_kernels.hip): kMsgSlots CRC jobs per message, slot order

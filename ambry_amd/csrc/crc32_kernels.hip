@@ -274,6 +274,214 @@ __device__ __forceinline__ uint32_t body_crc(const uint8_t* __restrict__ base, u
   return s;
 }
 
+// Raw CRC of [bs, be) with R-piece lane runs: lane l owns bytes [16R*l, 16R*(l+1)) of every
+// super-block of 1024*R bytes (R strided dwordx4 loads per lane, 16R B apart across lanes), so
+// its state hops -- one x^(8*1024R) nibble multiply -- once per R pieces instead of once per
+// piece. Fold and tree constants are POW entries: x^(8*1024R) = POW[10+lg R], tree level l
+// shifts by 16R*2^l = POW[4+lg R+l]. UB super-blocks stay in flight (rolling prefetch).
+template <int R>
+__device__ __forceinline__ uint32_t run_crc(const u32x4 (&w)[R], const LaneConst& k, uint32_t xin) {
+  uint32_t x = w[0].x;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    x = slice4(x, k, w[r].y);
+    x = slice4(x, k, w[r].z);
+    x = slice4(x, k, w[r].w);
+    x = slice4(x, k, r + 1 < R ? w[r + 1].x : xin);
+  }
+  return x;
+}
+
+template <int LR, int LVL>
+__device__ __forceinline__ uint32_t tree_level_pow(uint32_t s, uint32_t lane) {
+  const uint32_t sh = nib_mul(tree_partner<LVL>(s), kPowOff + kNibSetBytes * (4 + LR + LVL));
+  return (lane & (1u << LVL)) ? (s ^ sh) : s;
+}
+
+template <int UB, bool NT, int LR>
+__device__ __forceinline__ uint32_t body_crc_runs(const uint8_t* __restrict__ base, uint64_t bs, uint64_t be,
+                                                  uint32_t lane, const LaneConst& k) {
+  constexpr int R = 1 << LR;
+  constexpr uint64_t SB = (uint64_t)kBlockBytes * R;
+  constexpr uint32_t kFold = kPowOff + kNibSetBytes * (10 + LR);
+  const uint64_t nb = (be - bs + SB - 1) / SB;
+  if (nb == 0) return 0u;
+  const int64_t v0 = (int64_t)be - (int64_t)(nb * SB);  // may precede the allocation: signed
+  const int64_t lane0 = v0 + 16 * R * (int64_t)lane;
+  // super-block 0 carries the (possibly unaligned) start
+  u32x4 w[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    w[r] = u32x4{0u, 0u, 0u, 0u};
+    const int64_t p = lane0 + 16 * r;
+    if (p + 16 > (int64_t)bs) {  // => p >= floor16(bs) >= 0
+      w[r] = ld16<NT>(reinterpret_cast<const u32x4*>(base + p));
+      if (p < (int64_t)bs) {
+        const uint32_t cut = (uint32_t)(bs - p);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const int lo = (int)cut - 4 * d;
+          const uint32_t m = lo <= 0 ? 0xFFFFFFFFu : (lo >= 4 ? 0u : (0xFFFFFFFFu << (8 * lo)));
+          w[r][d] &= m;
+        }
+      }
+    }
+  }
+  uint32_t s = run_crc<R>(w, k, 0u);
+  const u32x4* q = reinterpret_cast<const u32x4*>(base + lane0);  // super-block b, piece r: q[b*64R + r]
+  uint64_t b = 1;
+  if (nb >= 1 + 2 * (uint64_t)UB) {
+    u32x4 buf[UB][R];
+#pragma unroll
+    for (int u = 0; u < UB; ++u)
+#pragma unroll
+      for (int r = 0; r < R; ++r) buf[u][r] = ld16<NT>(q + (b + u) * (SB / 16) + r);
+    for (; b + 2 * UB <= nb; b += UB) {
+#pragma unroll
+      for (int u = 0; u < UB; ++u) {
+        u32x4 cur[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          cur[r] = buf[u][r];
+          buf[u][r] = ld16<NT>(q + (b + UB + u) * (SB / 16) + r);
+        }
+        s = run_crc<R>(cur, k, nib_mul(s, kFold));
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UB; ++u) s = run_crc<R>(buf[u], k, nib_mul(s, kFold));
+    b += UB;
+  }
+  for (; b < nb; ++b) {
+    u32x4 cur[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) cur[r] = ld16<NT>(q + b * (SB / 16) + r);
+    s = run_crc<R>(cur, k, nib_mul(s, kFold));
+  }
+  s = tree_level_pow<LR, 0>(s, lane);
+  s = tree_level_pow<LR, 1>(s, lane);
+  s = tree_level_pow<LR, 2>(s, lane);
+  s = tree_level_pow<LR, 3>(s, lane);
+  s = tree_level_pow<LR, 4>(s, lane);
+  s = tree_level_pow<LR, 5>(s, lane);
+  return s;
+}
+
+// ---- 64-B lane runs from coalesced loads (variant 12 and up) ----
+// Per 4 KiB super-block each lane l = 4m+j issues 4 coalesced 1 KiB loads (block i, piece l),
+// then a 4x4 transpose of 16-B elements inside its quad (two DPP quad_perm butterfly stages)
+// leaves lane (m, j) holding the 64-B run [64m, 64m+64) of block j: the state hops once per
+// 64 B (x^(8*4096) = POW[12]) instead of once per 16 B. Tree: lane bits 2..5 merge the runs of
+// one block (shifts 64..512 B = POW[6..9]), bits 0..1 merge the blocks (1024, 2048 B).
+template <int CTRL>
+__device__ __forceinline__ uint32_t dppq(uint32_t v) {  // quad_perm: every lane has a source
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, true);
+}
+
+__device__ __forceinline__ void quad_transpose(u32x4 (&x)[4], uint32_t lane) {
+  // DPP is convergent: every move is issued in all lanes, then v_cndmask picks (no branches).
+  const bool t1 = lane & 1u, t2 = lane & 2u;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const uint32_t p0 = dppq<0xB1>(x[0][d]), p1 = dppq<0xB1>(x[1][d]);
+    const uint32_t p2 = dppq<0xB1>(x[2][d]), p3 = dppq<0xB1>(x[3][d]);
+    const uint32_t a0 = t1 ? p1 : x[0][d];
+    const uint32_t a1 = t1 ? x[1][d] : p0;
+    const uint32_t a2 = t1 ? p3 : x[2][d];
+    const uint32_t a3 = t1 ? x[3][d] : p2;
+    const uint32_t q0 = dppq<0x4E>(a0), q1 = dppq<0x4E>(a1);
+    const uint32_t q2 = dppq<0x4E>(a2), q3 = dppq<0x4E>(a3);
+    x[0][d] = t2 ? q2 : a0;
+    x[2][d] = t2 ? a2 : q0;
+    x[1][d] = t2 ? q3 : a1;
+    x[3][d] = t2 ? a3 : q1;
+  }
+}
+
+template <int BIT, int POWK>
+__device__ __forceinline__ uint32_t tree_level_t4(uint32_t s, uint32_t lane) {
+  uint32_t o;
+  if constexpr (BIT == 0) o = dpp<0x111, 0xf>(s);       // row_shr:1
+  else if constexpr (BIT == 1) o = dpp<0x112, 0xf>(s);  // row_shr:2
+  else if constexpr (BIT == 2) o = dpp<0x114, 0xf>(s);  // row_shr:4
+  else if constexpr (BIT == 3) o = dpp<0x118, 0xf>(s);  // row_shr:8
+  else o = __shfl_xor(s, 1 << BIT);                     // 16, 32: across rows
+  const uint32_t sh = nib_mul(o, kPowOff + kNibSetBytes * POWK);
+  return (lane & (1u << BIT)) ? (s ^ sh) : s;
+}
+
+template <int UB, bool NT>
+__device__ __forceinline__ uint32_t body_crc_t4(const uint8_t* __restrict__ base, uint64_t bs, uint64_t be,
+                                                uint32_t lane, const LaneConst& k) {
+  constexpr uint64_t SB = 4 * (uint64_t)kBlockBytes;
+  constexpr uint32_t kFold = kPowOff + kNibSetBytes * 12;
+  const uint64_t nb = (be - bs + SB - 1) / SB;
+  if (nb == 0) return 0u;
+  const int64_t v0 = (int64_t)be - (int64_t)(nb * SB);  // may precede the allocation: signed
+  u32x4 x[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    x[i] = u32x4{0u, 0u, 0u, 0u};
+    const int64_t p = v0 + (int64_t)kBlockBytes * i + 16 * (int64_t)lane;
+    if (p + 16 > (int64_t)bs) {  // => p >= floor16(bs) >= 0
+      x[i] = ld16<NT>(reinterpret_cast<const u32x4*>(base + p));
+      if (p < (int64_t)bs) {
+        const uint32_t cut = (uint32_t)(bs - p);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const int lo = (int)cut - 4 * d;
+          const uint32_t m = lo <= 0 ? 0xFFFFFFFFu : (lo >= 4 ? 0u : (0xFFFFFFFFu << (8 * lo)));
+          x[i][d] &= m;
+        }
+      }
+    }
+  }
+  quad_transpose(x, lane);
+  uint32_t s = run_crc<4>(x, k, 0u);
+  const u32x4* q = reinterpret_cast<const u32x4*>(base + v0) + lane;  // super-block b, block i: q[b*256 + i*64]
+  uint64_t b = 1;
+  if (nb >= 1 + 2 * (uint64_t)UB) {
+    u32x4 buf[UB][4];
+#pragma unroll
+    for (int u = 0; u < UB; ++u)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) buf[u][i] = ld16<NT>(q + (b + u) * 256 + i * 64);
+    for (; b + 2 * UB <= nb; b += UB) {
+#pragma unroll
+      for (int u = 0; u < UB; ++u) {
+        u32x4 cur[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          cur[i] = buf[u][i];
+          buf[u][i] = ld16<NT>(q + (b + UB + u) * 256 + i * 64);
+        }
+        quad_transpose(cur, lane);
+        s = run_crc<4>(cur, k, nib_mul(s, kFold));
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      quad_transpose(buf[u], lane);
+      s = run_crc<4>(buf[u], k, nib_mul(s, kFold));
+    }
+    b += UB;
+  }
+  for (; b < nb; ++b) {
+    u32x4 cur[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) cur[i] = ld16<NT>(q + b * 256 + i * 64);
+    quad_transpose(cur, lane);
+    s = run_crc<4>(cur, k, nib_mul(s, kFold));
+  }
+  s = tree_level_t4<2, 6>(s, lane);
+  s = tree_level_t4<3, 7>(s, lane);
+  s = tree_level_t4<4, 8>(s, lane);
+  s = tree_level_t4<5, 9>(s, lane);
+  s = tree_level_t4<0, 10>(s, lane);
+  s = tree_level_t4<1, 11>(s, lane);
+  return s;
+}
+
 // Largest c in [0, n) with byte_start[c] <= g (byte_start nondecreasing, byte_start[0] = 0).
 // 64-ary search: one coalesced probe per lane per round, log64(n) rounds.
 __device__ __forceinline__ uint32_t find_chunk(const uint64_t* __restrict__ byte_start, uint32_t n, uint64_t g,
@@ -310,7 +518,7 @@ __device__ __forceinline__ uint64_t snap_cut(uint64_t cs, uint64_t len, uint64_t
 // as one concatenated stream (byte_start = exclusive scan of len), i.e. an equal share of
 // bytes whatever the chunk-size mix. Each (wave, chunk) intersection is a segment whose
 // raw CRC is shifted to the chunk end and XORed into out[chunk].
-template <int U, bool NT, bool PIPE, bool IL, bool WIN, int DIAG = 0>
+template <int U, bool NT, bool PIPE, bool IL, bool WIN, int DIAG = 0, int LR = 0>
 __global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
   {
     const u32x4* src = reinterpret_cast<const u32x4*>(a.img);
@@ -346,7 +554,13 @@ __global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
     const uint64_t be = se == ce ? cb : se;  // 16-B aligned body end
     uint32_t r = 0;
     if (sa < be) {
-      r = body_crc<U, NT, PIPE, IL, DIAG>(a.base, sa, be, lane, k);
+      if constexpr (LR < 0) {
+        r = body_crc_t4<(U >> 2) < 1 ? 1 : (U >> 2), NT>(a.base, sa, be, lane, k);
+      } else if constexpr (LR > 0) {
+        r = body_crc_runs<(U >> LR) < 1 ? 1 : (U >> LR), NT, LR>(a.base, sa, be, lane, k);
+      } else {
+        r = body_crc<U, NT, PIPE, IL, DIAG>(a.base, sa, be, lane, k);
+      }
       r = __builtin_amdgcn_readlane(r, 63);
       r = shift_bytes(r, ce - be, xpow2);
     }
@@ -524,6 +738,12 @@ hipError_t launch_sweep(const SweepArgs& a, int grid, int variant, hipStream_t s
     AMBRY_TILES_CASE(5, 8, true, false, false, true)
     AMBRY_TILES_CASE(6, 4, true, true, true, true)
     AMBRY_TILES_CASE(7, 8, false, false, false, true)
+    case 8: hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, false, true, 0, 1>), dim3(grid), dim3(1024), 0, s, a); break;
+    case 9: hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, false, true, 0, 2>), dim3(grid), dim3(1024), 0, s, a); break;
+    case 10: hipLaunchKernelGGL((crc32_sweep_kernel<4, true, true, false, true, 0, 2>), dim3(grid), dim3(1024), 0, s, a); break;
+    case 11: hipLaunchKernelGGL((crc32_sweep_kernel<4, true, true, false, true, 0, 1>), dim3(grid), dim3(1024), 0, s, a); break;
+    case 12: hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, false, true, 0, -2>), dim3(grid), dim3(1024), 0, s, a); break;
+    case 13: hipLaunchKernelGGL((crc32_sweep_kernel<4, true, true, false, true, 0, -2>), dim3(grid), dim3(1024), 0, s, a); break;
     case kDiagNoFold:  // timing-only diagnostic (wrong CRCs): FOLD lookups removed
       hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, true, true, 1>), dim3(grid), dim3(1024), 0, s, a);
       break;

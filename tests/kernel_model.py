@@ -82,29 +82,40 @@ class KernelModel:
             k += 1
         return int(v)
 
-    def body_crc(self, mem: np.ndarray, bs: int, be: int) -> int:
-        nb = (be - bs + BLOCK - 1) // BLOCK
+    def body_crc(self, mem: np.ndarray, bs: int, be: int, run: int = 1) -> int:
+        """Raw CRC of [bs, be): lane l owns the run of `run` 16-B pieces at 16*run*l of every
+        super-block of 1024*run bytes; the lane state hops one super-block per run
+        (x^(8*1024*run) = POW[10+log2 run]); tree level l shifts by 16*run*2^l (POW[4+log2 run+l])."""
+        lr = run.bit_length() - 1
+        sb = BLOCK * run
+        nb = (be - bs + sb - 1) // sb
         if nb == 0:
             return 0
-        v0 = be - nb * BLOCK
+        v0 = be - nb * sb
         s = np.zeros(64, dtype=np.uint32)
         for b in range(nb):
-            p = v0 + b * BLOCK + 16 * LANES.astype(np.int64)
-            w = np.zeros((64, 4), dtype=np.uint32)
-            for lane in range(64):
-                if p[lane] + 16 > bs:
-                    # the kernel's load-address invariant: inside [floor16(bs), be)
-                    assert (bs & ~15) <= p[lane] and p[lane] + 16 <= be, (bs, be, p[lane])
-                    raw = bytearray(mem[p[lane]:p[lane] + 16].tobytes())
-                    cut = bs - p[lane]
-                    for i in range(max(0, cut)):
-                        raw[i] = 0
-                    w[lane] = np.frombuffer(bytes(raw), dtype="<u4")
-            fold = self.nib_mul(s, K_FOLD_OFF) if b else np.zeros(64, dtype=np.uint32)
-            s = self.rpiece(w, fold)
+            w = np.zeros((run, 64, 4), dtype=np.uint32)
+            for r in range(run):
+                p = v0 + b * sb + 16 * run * LANES.astype(np.int64) + 16 * r
+                for lane in range(64):
+                    if p[lane] + 16 > bs:
+                        # the kernel's load-address invariant: inside [floor16(bs), be)
+                        assert (bs & ~15) <= p[lane] and p[lane] + 16 <= be, (bs, be, p[lane])
+                        raw = bytearray(mem[p[lane]:p[lane] + 16].tobytes())
+                        cut = bs - p[lane]
+                        for i in range(max(0, cut)):
+                            raw[i] = 0
+                        w[r, lane] = np.frombuffer(bytes(raw), dtype="<u4")
+            fold = (self.nib_mul(s, K_POW_OFF + K_NIB_SET * (10 + lr)) if b
+                    else np.zeros(64, dtype=np.uint32))
+            x = w[0][:, 0]
+            words = [w[r][:, i] for r in range(run) for i in range(4)]
+            for i in range(1, 4 * run):
+                x = self.slice4(x, words[i])
+            s = self.slice4(x, fold)
         for lvl in range(6):
             o = s[LANES ^ (1 << lvl)]
-            sh = self.nib_mul(o, K_TREE_OFF + K_NIB_SET * lvl)
+            sh = self.nib_mul(o, K_POW_OFF + K_NIB_SET * (4 + lr + lvl))
             s = np.where((LANES & (1 << lvl)) != 0, s ^ sh, s).astype(np.uint32)
         return int(s[63])
 
@@ -123,7 +134,48 @@ class KernelModel:
             acc ^= v
         return acc
 
-    def batch(self, mem: np.ndarray, off, length, crc_in=None, nwaves: int = 4096, quantum: int = 1024):
+    def body_crc_t4(self, mem: np.ndarray, bs: int, be: int) -> int:
+        """Coalesced loads + 4x4 quad transpose (sweep variant 12): per 4 KiB super-block, lane
+        l = 4m+j loads piece l of each of the 4 blocks, then the quad transpose gives it the 64-B run
+        [64m, 64m+64) of block j; fold x^(8*4096) once per run; tree over lane bits 2,3,4,5
+        (shifts 64..512 B) then 0,1 (1024, 2048 B)."""
+        sb = 4096
+        nb = (be - bs + sb - 1) // sb
+        if nb == 0:
+            return 0
+        v0 = be - nb * sb
+        s = np.zeros(64, dtype=np.uint32)
+        for b in range(nb):
+            X = np.zeros((4, 64, 4), dtype=np.uint32)  # X[i][lane] = block i, piece lane
+            for i in range(4):
+                for lane in range(64):
+                    p = v0 + b * sb + 1024 * i + 16 * lane
+                    if p + 16 > bs:
+                        assert (bs & ~15) <= p and p + 16 <= be, (bs, be, p)
+                        raw = bytearray(mem[p:p + 16].tobytes())
+                        for t in range(max(0, bs - p)):
+                            raw[t] = 0
+                        X[i, lane] = np.frombuffer(bytes(raw), dtype="<u4")
+            # quad transpose: lane (m, j) element t <- lane (m, t) element j
+            Y = np.zeros_like(X)
+            for lane in range(64):
+                m, j = lane >> 2, lane & 3
+                for t in range(4):
+                    Y[t, lane] = X[j, 4 * m + t]
+            fold = self.nib_mul(s, K_POW_OFF + K_NIB_SET * 12) if b else np.zeros(64, dtype=np.uint32)
+            words = [Y[t][:, c] for t in range(4) for c in range(4)]
+            x = words[0]
+            for c in range(1, 16):
+                x = self.slice4(x, words[c])
+            s = self.slice4(x, fold)
+        for bit, k in ((2, 6), (3, 7), (4, 8), (5, 9), (0, 10), (1, 11)):
+            o = s[LANES ^ (1 << bit)]
+            sh = self.nib_mul(o, K_POW_OFF + K_NIB_SET * k)
+            s = np.where((LANES & (1 << bit)) != 0, s ^ sh, s).astype(np.uint32)
+        return int(s[63])
+
+    def batch(self, mem: np.ndarray, off, length, crc_in=None, nwaves: int = 4096, quantum: int = 1024,
+              run: int = 1):
         """Replays plan + sweep kernels with `nwaves` waves; returns the list of CRCs."""
         n = len(off)
         off = [int(x) for x in off]
@@ -161,7 +213,8 @@ class KernelModel:
                 assert be % 16 == 0 or be == cs, (sa, se, be)
                 r = 0
                 if sa < be:
-                    r = self.shift_bytes(self.body_crc(mem, sa, be), ce - be)
+                    body = self.body_crc_t4(mem, sa, be) if run == -4 else self.body_crc(mem, sa, be, run)
+                    r = self.shift_bytes(body, ce - be)
                 if se == ce and ce > cb:
                     r ^= self.tail_crc(mem, max(sa, cb), ce - max(sa, cb))
                 if r0 == 0:

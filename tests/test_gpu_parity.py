@@ -108,7 +108,7 @@ def test_ragged_batch_grid_sizes(gpu, oracle, grid):
     assert np.array_equal(got, oracle.batch(mem, off, ln, threads=8))
 
 
-@pytest.mark.parametrize("variant", list(range(8)))
+@pytest.mark.parametrize("variant", list(range(14)))
 def test_kernel_variants(gpu, oracle, variant):
     rng = np.random.default_rng(100 + variant)
     mem = stream_bytes(6, 0, 16 << 20)

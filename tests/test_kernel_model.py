@@ -28,6 +28,17 @@ def test_model_matches_oracle(model, oracle, nwaves):
     assert got == exp
 
 
+@pytest.mark.parametrize("run", [2, 4, -4])
+def test_model_lane_runs(model, oracle, run):
+    """R-piece lane runs (variants 8-11) and the quad-transposed 64-B runs (run=-4, variant 12)."""
+    mem = stream_bytes(321, 0, 300000)
+    off = [c[0] for c in CASES]
+    ln = [c[1] for c in CASES]
+    exp = list(oracle.batch(mem, off, ln))
+    for nw in (1, 3, 64):
+        assert model.batch(mem, off, ln, nwaves=nw, run=run) == exp
+
+
 def test_model_crc_in(model, oracle):
     mem = stream_bytes(77, 0, 100000)
     off = [c[0] for c in CASES[:10]]
