@@ -45,6 +45,9 @@ _SIGNATURES = [
     ("ambrycrc_batch_host", ctypes.c_int,
      [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32),
       ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t, ctypes.c_int, ctypes.c_int]),
+    ("ambrycrc_batch_multi", ctypes.c_int,
+     [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32),
+      ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t, ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_int]),
     ("ambrycrc_put_crcs", ctypes.c_int,
      [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_void_p),
       ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint64),

@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "crc32_gf2.h"
@@ -495,6 +496,43 @@ int ambrycrc_batch_host(const void* const* ptrs, const uint64_t* lens, const uin
   if (rc2) return rc2;
   if (rc3) return rc3;
   for (size_t i = 0; i < n; ++i) out[i] = acc[i];
+  return AMBRYCRC_OK;
+}
+
+int ambrycrc_batch_multi(const void* const* ptrs, const uint64_t* lens, const uint32_t* crc_in, uint32_t* out,
+                         size_t n, const int* devices, int ndev, int pinned) {
+  if (ndev <= 0 || ndev > kMaxDevices * 8) return AMBRYCRC_EINVAL;
+  if (n == 0) return AMBRYCRC_OK;
+  if (!ptrs || !lens || !out) return AMBRYCRC_EINVAL;
+  std::vector<int> dev(ndev);
+  for (int g = 0; g < ndev; ++g) {
+    dev[g] = devices ? devices[g] : g;
+    if (!ctx_for(dev[g])) return AMBRYCRC_ENOINIT;
+  }
+  // Range g = [cut[g], cut[g+1]): the first chunk index whose byte prefix reaches g/ndev of the total.
+  uint64_t total = 0;
+  for (size_t i = 0; i < n; ++i) total += lens[i];
+  std::vector<size_t> cut(ndev + 1, n);
+  cut[0] = 0;
+  uint64_t prefix = 0;
+  int g = 1;
+  for (size_t i = 0; i < n && g < ndev; ++i) {
+    while (g < ndev && (unsigned __int128)prefix * ndev >= (unsigned __int128)total * g) cut[g++] = i;
+    prefix += lens[i];
+  }
+  std::vector<int> rc(ndev, AMBRYCRC_OK);
+  std::vector<std::thread> th;
+  th.reserve(ndev);
+  for (int r = 0; r < ndev; ++r) {
+    const size_t a = cut[r], b = cut[r + 1];
+    if (a >= b) continue;
+    th.emplace_back([&, r, a, b] {
+      rc[r] = ambrycrc_batch_host(ptrs + a, lens + a, crc_in ? crc_in + a : nullptr, out + a, b - a, dev[r], pinned);
+    });
+  }
+  for (auto& t : th) t.join();
+  for (int r = 0; r < ndev; ++r)
+    if (rc[r]) return rc[r];
   return AMBRYCRC_OK;
 }
 

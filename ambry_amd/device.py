@@ -76,12 +76,7 @@ def fill_random(buf, seed: int, stream_off: int = 0, stream=None) -> None:
                                          ctypes.c_void_p(_stream_handle(stream))), "ambrycrc_fill_random_dev")
 
 
-def crc32_batch_host(chunks, device: int = 0, pinned: bool = False, crc_in=None):
-    """CRC of host buffers through pinned staging + hipMemcpyAsync (PCIe-inclusive path).
-
-    ``chunks``: sequence of objects exposing ``data_ptr()``/``numel()`` (uint8
-    CPU tensors) or (address, length) tuples.
-    """
+def _host_chunks(chunks, crc_in):
     n = len(chunks)
     ptrs = (ctypes.c_void_p * n)()
     lens = (ctypes.c_uint64 * n)()
@@ -90,11 +85,31 @@ def crc32_batch_host(chunks, device: int = 0, pinned: bool = False, crc_in=None)
             ptrs[i], lens[i] = c
         else:
             ptrs[i], lens[i] = c.data_ptr(), c.numel()
-    out = (ctypes.c_uint32 * n)()
     cin = None
     if crc_in is not None:
         cin = (ctypes.c_uint32 * n)(*[int(x) & 0xFFFFFFFF for x in crc_in])
+    return n, ptrs, lens, cin
+
+
+def crc32_batch_host(chunks, device: int = 0, pinned: bool = False, crc_in=None):
+    """CRC of host buffers through pinned staging + hipMemcpyAsync (PCIe-inclusive path).
+
+    ``chunks``: sequence of objects exposing ``data_ptr()``/``numel()`` (uint8
+    CPU tensors) or (address, length) tuples.
+    """
+    n, ptrs, lens, cin = _host_chunks(chunks, crc_in)
+    out = (ctypes.c_uint32 * n)()
     check(lib().ambrycrc_batch_host(ptrs, lens, cin, out, n, device, 1 if pinned else 0), "ambrycrc_batch_host")
+    return list(out)
+
+
+def crc32_batch_multi(chunks, devices, pinned: bool = False, crc_in=None):
+    """ambrycrc_batch_multi: host chunks split by bytes over ``devices`` (one host thread each)."""
+    n, ptrs, lens, cin = _host_chunks(chunks, crc_in)
+    out = (ctypes.c_uint32 * n)()
+    devs = (ctypes.c_int * len(devices))(*devices)
+    check(lib().ambrycrc_batch_multi(ptrs, lens, cin, out, n, devs, len(devices), 1 if pinned else 0),
+          "ambrycrc_batch_multi")
     return list(out)
 
 
@@ -120,6 +135,11 @@ def timing_collect(device: int = 0):
     cnt = ctypes.c_int()
     check(lib().ambrycrc_timing_collect(device, ctypes.byref(ms), ctypes.byref(cnt)), "ambrycrc_timing_collect")
     return ms.value, cnt.value
+
+
+def workspace_bytes(n: int) -> int:
+    """Bytes of caller workspace ambrycrc_batch_dev needs for n chunks."""
+    return lib().ambrycrc_workspace_bytes(n)
 
 
 def messages_workspace_bytes(m: int) -> int:

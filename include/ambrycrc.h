@@ -161,6 +161,18 @@ size_t ambrycrc_chain_messages_host(const uint8_t* region, uint64_t region_len, 
 int ambrycrc_batch_host(const void* const* ptrs, const uint64_t* lens, const uint32_t* crc_in, uint32_t* out,
                         size_t n, int device, int pinned);
 
+/* ambrycrc_batch_host across several GPUs of this process: the n
+ * chunks are split into ndev contiguous ranges of about equal BYTES (mixed sizes are
+ * balanced by bytes, not by count), range g runs ambrycrc_batch_host on devices[g]
+ * from its own host thread, and the calls are joined. devices == NULL means
+ * 0..ndev-1; a device may appear more than once (its ranges then run one after the
+ * other). Every listed device must have been ambrycrc_init'ed. Returns the first
+ * nonzero status of any range; out[] is complete only on AMBRYCRC_OK.
+ * This is the single-JVM form of the per-GPU sharding the bench runs as one
+ * process per GPU: a storage node scanning many partitions in one process. */
+int ambrycrc_batch_multi(const void* const* ptrs, const uint64_t* lens, const uint32_t* crc_in, uint32_t* out,
+                         size_t n, const int* devices, int ndev, int pinned);
+
 /* One-pass PUT CRCs (§8f row 2). For each of n PUT requests whose blob CRC blob_crc[i]
  * (over blob_len[i] bytes, e.g. from ambrycrc_batch_dev/ambrycrc_batch_host) is known:
  *   wire_out[i]   = crc32(fields[i] || blob)   -- PutRequest.prepareBuffer's CRC over blobId,

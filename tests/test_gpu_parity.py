@@ -252,6 +252,32 @@ def test_host_resident_path(gpu, oracle):
     assert gpu.crc32_batch_host(chunks, device=0, pinned=False, crc_in=cin) == exp2
 
 
+@pytest.mark.parametrize("ndev", [1, 3, 16])
+def test_batch_multi(gpu, oracle, ndev):
+    """ambrycrc_batch_multi: byte-balanced ranges, one host thread each. The 1-GPU box lists
+    device 0 ndev times, which exercises the partitioning (more ranges than chunks at 16,
+    empty chunks, a chunk dominating the bytes) and the concurrent per-range calls."""
+    torch = _torch()
+    rng = np.random.default_rng(80 + ndev)
+    lens = [0, 5, (40 << 20) + 3, 0, 4096, 1 << 20, 65536, 17, 0, 1000, 8 << 20]
+    chunks = [torch.from_numpy(stream_bytes(int(rng.integers(1 << 30)), 0, n)) for n in lens]
+    cin = [(i * 0x9E3779B9) & 0xFFFFFFFF for i in range(len(lens))]
+    exp = [oracle.crc32(c.numpy(), ci) for c, ci in zip(chunks, cin)]
+    assert gpu.crc32_batch_multi(chunks, [0] * ndev, crc_in=cin) == exp
+    assert gpu.crc32_batch_multi(chunks[:2], [0] * ndev) == [oracle.crc32(c.numpy()) for c in chunks[:2]]
+
+
+def test_batch_multi_rejects_uninitialised_device(gpu):
+    from ambry_amd._lib import AmbryCrcError, lib
+
+    torch = _torch()
+    if torch.cuda.device_count() > 7:
+        pytest.skip("device 7 may legitimately be initialised on an 8-GPU node")
+    with pytest.raises(AmbryCrcError):
+        gpu.crc32_batch_multi([torch.zeros(10, dtype=torch.uint8)], [0, 7])
+    assert lib().ambrycrc_batch_multi(None, None, None, None, 0, None, 0, 0) != 0  # ndev = 0
+
+
 def test_timing_hook(gpu):
     torch = _torch()
     gpu.timing_enable(0, True)

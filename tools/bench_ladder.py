@@ -1,0 +1,158 @@
+#!/usr/bin/env python3
+"""Per-size table on Crc32Benchmark's ladder (SURVEY.md §8a a14 / §8d "CPU baseline").
+
+Crc32Benchmark.java:43-44 times one buffer per call at sizes 100 B ... 4 MiB
+(10 buffers, 500 iterations) and reports µs per call. For each ladder size this prints:
+  gpu_batch   chunks of that size packed at 16-B-aligned offsets, about --gib of them in
+              HBM, one ambrycrc_batch_dev call (plan + sweep); sweep-kernel time (HIP
+              events, ambrycrc timing hook) and stream wall time, median of --reps
+  gpu_call    ONE chunk per ambrycrc_batch_dev call, µs per call (stream wall): the
+              latency floor a Crc32Benchmark-style caller sees
+  cpu         oracle/crc32_ref.c (C restatement of Crc32.java slice-by-8) and zlib.crc32
+              (the java.util.zip.CRC32 stand-in), one thread, µs per call and GB/s, over
+              10 buffers x enough iterations for ~0.3 s
+One JSON line per size. --no-gpu runs the CPU columns only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+import zlib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+LADDER = [100, 1 << 10, 4 << 10, 16 << 10, 64 << 10, 256 << 10, 1 << 20, 4 << 20]
+
+
+def cpu_row(size: int, target_s: float = 0.3):
+    import numpy as np
+
+    from conftest import Oracle
+    from datagen import stream_bytes
+
+    orc = Oracle()
+    bufs = [stream_bytes(0xB0 + i, 0, size) for i in range(10)]
+    raw = [b.tobytes() for b in bufs]
+    ptrs = [(b, b.ctypes.data) for b in bufs]
+    fn = orc.L.oracle_crc32
+    for b, r in zip(bufs, raw):
+        assert fn(0, b.ctypes.data, size) == zlib.crc32(r)
+    out = {}
+    for name, call in (("restatement", lambda i: fn(0, ptrs[i][1], size)), ("zlib", lambda i: zlib.crc32(raw[i]))):
+        iters, el = 1, 0.0
+        while True:
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                for i in range(10):
+                    call(i)
+            el = time.perf_counter() - t0
+            if el > target_s:
+                break
+            iters *= 4
+        us = el / (iters * 10) * 1e6
+        out[name] = {"us_per_call": round(us, 3), "GBps": round(size / us / 1e3, 3)}
+    # Python->C call overhead (measured with a 0-byte call) is included in the per-call numbers.
+    t0 = time.perf_counter()
+    for _ in range(100000):
+        fn(0, ptrs[0][1], 0)
+    out["call_overhead_us"] = round((time.perf_counter() - t0) / 100000 * 1e6, 3)
+    return out
+
+
+def gpu_rows(size: int, gib: float, reps: int):
+    import numpy as np
+    import torch
+
+    from ambry_amd import device as D
+
+    stride = (size + 15) // 16 * 16
+    n = max(1, int(gib * 2**30) // stride)
+    buf = torch.empty(n * stride, dtype=torch.uint8, device="cuda")
+    D.fill_random(buf, 0xA1 + size, 0)
+    off = torch.arange(n, dtype=torch.int64, device="cuda") * stride
+    ln = torch.full((n,), size, dtype=torch.int64, device="cuda")
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    ws = torch.empty(D.workspace_bytes(n), dtype=torch.uint8, device="cuda")
+    D.crc32_batch(buf, off, ln, out=out, workspace=ws)
+    torch.cuda.synchronize()
+    # spot-check a few chunks against zlib
+    idx = [0, n // 2, n - 1]
+    host = buf.view(n, stride)[idx, :size].cpu().numpy()
+    got = out[idx].cpu().numpy().view(np.uint32)
+    assert [zlib.crc32(h.tobytes()) for h in host] == list(got), "ladder parity"
+    t_pre = time.perf_counter()
+    while time.perf_counter() - t_pre < 0.3:
+        D.crc32_batch(buf, off, ln, out=out, workspace=ws)
+        torch.cuda.synchronize()
+    kt, wt = [], []
+    D.timing_enable(0, True)
+    try:
+        for _ in range(reps):
+            D.timing_collect(0)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            D.crc32_batch(buf, off, ln, out=out, workspace=ws)
+            e1.record()
+            torch.cuda.synchronize()
+            wt.append(e0.elapsed_time(e1))
+            ms, cnt = D.timing_collect(0)
+            kt.append(ms)
+    finally:
+        D.timing_enable(0, False)
+    k, w = statistics.median(kt), statistics.median(wt)
+    batch = {"chunks": n, "bytes": n * size, "kernel_ms": round(k, 4), "wall_ms": round(w, 4),
+             "kernel_GBps": round(n * size / k / 1e6, 1), "wall_GiBps": round(n * size / (w / 1e3) / 2**30, 1),
+             "meta_bytes_per_chunk": 16 + 4}
+    # single-chunk calls
+    o1, l1 = off[:1].clone(), ln[:1].clone()
+    out1 = torch.empty(1, dtype=torch.int32, device="cuda")
+    ws1 = torch.empty(D.workspace_bytes(1), dtype=torch.uint8, device="cuda")
+    for _ in range(50):
+        D.crc32_batch(buf, o1, l1, out=out1, workspace=ws1)
+    torch.cuda.synchronize()
+    calls = 500
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(calls):
+        D.crc32_batch(buf, o1, l1, out=out1, workspace=ws1)
+    e1.record()
+    torch.cuda.synchronize()
+    host_us = (time.perf_counter() - t0) / calls * 1e6
+    call = {"us_per_call_stream": round(e0.elapsed_time(e1) / calls * 1e3, 2), "us_per_call_host": round(host_us, 2)}
+    del buf, off, ln, out, ws
+    torch.cuda.empty_cache()
+    return batch, call
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gib", type=float, default=2.0)
+    ap.add_argument("--reps", type=int, default=7)
+    ap.add_argument("--no-gpu", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+    if not args.no_gpu:
+        import torch
+
+        from ambry_amd import device as D
+
+        torch.cuda.set_device(0)
+        D.init(0)
+    for size in LADDER:
+        row = {"size": size}
+        if not args.no_cpu:
+            row["cpu_1thread"] = cpu_row(size)
+        if not args.no_gpu:
+            row["gpu_batch"], row["gpu_call"] = gpu_rows(size, args.gib, args.reps)
+        print(json.dumps(row), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -125,12 +125,14 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--no-gpu", action="store_true")
     ap.add_argument("--variants", default="0")
+    ap.add_argument("--cases", default="64k,4m,4k", help="subset of 64k,4m,4k")
     args = ap.parse_args()
     mf = load_mf()
     print(json.dumps(c1_cpu(mf)), flush=True)
     if args.no_gpu:
         return
-    for m, s in ((65536, 64 << 10), (4096, 4 << 20), (262144, 4 << 10)):
+    cases = {"64k": (65536, 64 << 10), "4m": (4096, 4 << 20), "4k": (262144, 4 << 10)}
+    for m, s in (cases[c] for c in args.cases.split(",")):
         for v in [int(x) for x in args.variants.split(",")]:
             print(json.dumps(gpu_region(mf, m, s, args.reps, v)), flush=True)
 
