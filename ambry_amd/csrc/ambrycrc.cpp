@@ -139,10 +139,11 @@ DevCtx* ctx_current() {
   return ctx_for(dev);
 }
 
-// workspace: byte_start[n+1] | block_sum[ceil(n/kPlanPerBlock)]  (uint64)
+// workspace: byte_start[n+1] | block_sum[B] | block_small[B] | small_total (uint64) |
+//            small_idx[n] (uint32), B = ceil(n / kPlanPerBlock)
 size_t ws_need(size_t n) {
   const size_t blocks = (n + kPlanPerBlock - 1) / kPlanPerBlock;
-  return ((n + 1 + blocks) * sizeof(uint64_t) + 255) & ~size_t(255);
+  return ((n + 2 + 2 * blocks) * sizeof(uint64_t) + n * sizeof(uint32_t) + 255) & ~size_t(255);
 }
 
 int ensure_ws(DevCtx* c, size_t need) {
@@ -168,8 +169,16 @@ int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uin
   p.crc_in = crc_in;
   p.n = (uint32_t)n;
   p.byte_start = static_cast<uint64_t*>(ws);
+  const size_t blocks = (n + kPlanPerBlock - 1) / kPlanPerBlock;
   p.block_sum = p.byte_start + n + 1;
+  p.block_small = p.block_sum + blocks;
+  p.small_total = p.block_small + blocks;
+  p.small_idx = reinterpret_cast<uint32_t*>(p.small_total + 1);
   p.out = out;
+  // variants >= 14: variant 0's sweep plus the group kernel for small whole chunks
+  const int sweep_variant = c->variant >= 14 && c->variant < kNumVariants ? 0 : c->variant;
+  const int group_mode = c->variant >= 14 && c->variant < kNumVariants ? c->variant - 13 : 0;
+  p.small_max = group_small_max(group_mode);
   hipError_t e = launch_plan(p, s);
   if (e != hipSuccess) return AMBRYCRC_EHIP;
   SweepArgs t;
@@ -181,6 +190,9 @@ int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uin
   t.byte_start = p.byte_start;
   t.img = c->d_img;
   t.out = out;
+  t.small_max = p.small_max;
+  t.small_total = p.small_total;
+  t.small_idx = p.small_idx;
   EventPair ev{nullptr, nullptr};
   if (c->timing) {
     std::lock_guard<std::mutex> g(c->mu);
@@ -192,7 +204,9 @@ int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uin
     }
     if (hipEventRecord(ev.a, s) != hipSuccess) return AMBRYCRC_EHIP;
   }
-  e = launch_sweep(t, c->grid, c->variant, s);
+  e = launch_group(t, c->grid, group_mode, s);
+  if (e != hipSuccess) return AMBRYCRC_EHIP;
+  e = launch_sweep(t, c->grid, sweep_variant, s);
   if (e != hipSuccess) return AMBRYCRC_EHIP;
   if (c->timing) {
     if (hipEventRecord(ev.b, s) != hipSuccess) return AMBRYCRC_EHIP;
@@ -571,7 +585,8 @@ int ambrycrc_range_checksums_host(const uint8_t* file, uint64_t file_len, const 
 int ambrycrc_set_variant(int device, int variant) {
   DevCtx* c = ctx_for(device);
   if (!c) return AMBRYCRC_ENOINIT;
-  if ((variant < 0 || variant >= kNumVariants) && variant != kDiagNoFold) return AMBRYCRC_EINVAL;
+  if ((variant < 0 || variant >= kNumVariants) && (variant < kDiagNoFold || variant > kDiagNoFold + 2))
+    return AMBRYCRC_EINVAL;
   c->variant = variant;
   return AMBRYCRC_OK;
 }

@@ -14,6 +14,10 @@ struct PlanArgs {
   uint64_t* byte_start;    // [n+1] exclusive scan of len; [n] = total bytes
   uint64_t* block_sum;     // [ceil(n / kPlanPerBlock)] scratch
   uint32_t* out;           // [n] initialised here, XOR-accumulated by the sweep kernel
+  uint64_t small_max;      // chunks with 0 < len <= small_max go to the group kernel (0: none)
+  uint64_t* block_small;   // [ceil(n / kPlanPerBlock)] scratch
+  uint64_t* small_total;   // [1] number of small chunks
+  uint32_t* small_idx;     // [n] their indices, ascending (compacted list for the group kernel)
 };
 
 constexpr uint32_t kPlanPerBlock = 2048;  // chunks per planning workgroup
@@ -28,7 +32,22 @@ struct SweepArgs {
   const uint64_t* byte_start;
   const uint32_t* img;     // LDS image (kLdsBytes) followed by 64 words x^(8*2^k)
   uint32_t* out;
+  uint64_t small_max;      // sweep: skip chunks with len <= small_max; group kernel: take them
+  const uint64_t* small_total;
+  const uint32_t* small_idx;
 };
+
+// Group kernel shapes (mode -> G lanes per chunk, NB blocks of 16G bytes): small_max = 16*G*NB.
+// 0 = off, 1 = G16/NB8 (2 KiB), 2 = G16/NB16 (4 KiB), 3 = G32/NB8 (4 KiB), 4 = G16/NB32 (8 KiB),
+// 5 = G16/NB64 (16 KiB), 6 = G32/NB32 (16 KiB)
+constexpr int kNumGroupModes = 7;
+constexpr uint64_t group_small_max(int mode) {
+  return mode == 1 ? 2048u
+         : (mode == 2 || mode == 3) ? 4096u
+         : mode == 4 ? 8192u
+         : (mode == 5 || mode == 6) ? 16384u
+                                    : 0u;
+}
 
 // sweep-kernel variants (U = loads in flight per lane, NT = nontemporal, PIPE = rolling prefetch,
 // IL = two pieces interleaved, WIN = descriptors fetched 64 per wave-load, else one-ahead scalar
@@ -36,7 +55,8 @@ struct SweepArgs {
 // 4 U8/PIPE/IL/WIN (temporal loads), 5 U8/NT batch loads, 6 U4/NT/PIPE/IL/WIN, 7 U8 batch (temporal)
 // 8 R=2 strided lane runs (U8 loads in flight), 9 R=4 strided runs (U8), 10 R=4 strided (U4),
 // 11 R=2 strided (U4), 12 64-B runs by quad transpose of coalesced loads (U8), 13 same (U4)
-constexpr int kNumVariants = 14;
+// 14..19 = 0 plus the group kernel (modes 1..6) for small whole chunks
+constexpr int kNumVariants = 20;
 constexpr int kDiagNoFold = 100;  // diagnostic timing build, selectable via ambrycrc_set_variant only
 
 // Message verify (message_kernels.hip): kMsgSlots CRC jobs per message, slot order
@@ -62,6 +82,7 @@ hipError_t launch_msg_reduce(const MsgArgs& a, hipStream_t s);
 
 hipError_t launch_plan(const PlanArgs& a, hipStream_t s);
 hipError_t launch_sweep(const SweepArgs& a, int grid, int variant, hipStream_t s);
+hipError_t launch_group(const SweepArgs& a, int grid, int mode, hipStream_t s);
 hipError_t launch_verify(const uint32_t* crc, const uint32_t* expected, uint8_t* mismatch, uint32_t* count,
                          uint32_t n, hipStream_t s);
 hipError_t launch_readbw(const uint8_t* base, uint64_t nbytes, uint32_t* out, int grid, int variant,

@@ -65,6 +65,12 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t lane) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src) {
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, (int)src);
+  const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), (int)src);
+  return ((uint64_t)hi << 32) | lo;
+}
+
 // Per-lane address constants for slice table j: region bit, (j&1)*128, lane column.
 struct LaneConst {
   uint32_t L0, L1, L2, L3;
@@ -189,20 +195,12 @@ __device__ __forceinline__ uint32_t tail_crc(const uint8_t* __restrict__ p, uint
   return v;
 }
 
-// Raw CRC of body [bs, be) (be 16-aligned, bs <= be arbitrary), returned in lane 63
-// (other lanes: junk). Bytes below bs are treated as zeros, which leave a zero
-// register unchanged, so the virtual range is aligned down to whole 1 KiB blocks.
-template <int U, bool NT, bool PIPE, bool IL, int DIAG = 0>
-__device__ __forceinline__ uint32_t body_crc(const uint8_t* __restrict__ base, uint64_t bs, uint64_t be,
-                                             uint32_t lane, const LaneConst& k) {
-  const uint64_t nb = (be - bs + kBlockBytes - 1) / kBlockBytes;
-  if (nb == 0) return 0u;
-  // The virtual start may precede the allocation (chunk in its first KiB): signed
-  // arithmetic, and only lanes whose piece reaches bs ever form a load address.
-  const int64_t v0 = (int64_t)be - (int64_t)(nb * kBlockBytes);
-  const u32x4* q = reinterpret_cast<const u32x4*>(base + v0) + lane;
-
-  // Block 0 carries the (possibly unaligned) start: mask what lies before bs.
+// Block 0 of a body whose virtual start v0 = be - nb*1024 may precede bs: lane l's 16 B at
+// v0 + 16l, zero where they lie before bs (zeros leave a zero register unchanged). Only
+// lanes whose piece reaches bs form an address, so v0 may precede the allocation.
+template <bool NT>
+__device__ __forceinline__ u32x4 load_block0(const uint8_t* __restrict__ base, int64_t v0, uint64_t bs,
+                                             uint32_t lane) {
   u32x4 w = {0u, 0u, 0u, 0u};
   const int64_t p = v0 + 16 * (int64_t)lane;
   if (p + 16 > (int64_t)bs) {  // => p >= floor16(bs) >= 0: inside the caller's buffer
@@ -217,39 +215,67 @@ __device__ __forceinline__ uint32_t body_crc(const uint8_t* __restrict__ base, u
       }
     }
   }
-  uint32_t s = rpiece(w, k, 0u);
+  return w;
+}
 
-  uint64_t b = 1;
+// Raw CRC of body [bs, be) (be 16-aligned, bs <= be arbitrary), returned in lane 63
+// (other lanes: junk). Bytes below bs are treated as zeros, which leave a zero
+// register unchanged, so the virtual range is aligned down to whole 1 KiB blocks.
+template <int U, bool NT, bool PIPE, bool IL, int DIAG = 0>
+__device__ __forceinline__ uint32_t body_crc(const uint8_t* __restrict__ base, uint64_t bs, uint64_t be,
+                                             uint32_t lane, const LaneConst& k) {
+  const uint64_t nb = (be - bs + kBlockBytes - 1) / kBlockBytes;
+  if (nb == 0) return 0u;
+  // The virtual start may precede the allocation (chunk in its first KiB): signed
+  // arithmetic, and only lanes whose piece reaches bs ever form a load address.
+  const int64_t v0 = (int64_t)be - (int64_t)(nb * kBlockBytes);
+  const u32x4* q = reinterpret_cast<const u32x4*>(base + v0) + lane;
+
+  uint32_t s = 0u;  // fold(0) == 0, so block 0 takes the same step as every other block
   if constexpr (PIPE) {
+    // Prime: blocks 0..min(U,nb)-1 are all issued before the first is used, so a short
+    // segment (a 4 KiB record = 4 blocks) costs one memory round trip, not one per block.
+    u32x4 buf[U];
+    buf[0] = load_block0<NT>(base, v0, bs, lane);
+#pragma unroll
+    for (int u = 1; u < U; ++u) buf[u] = (uint64_t)u < nb ? ld16<NT>(q + u * (kBlockBytes / 16)) : u32x4{0u, 0u, 0u, 0u};
     // Rolling prefetch: the slot a piece is consumed from is refilled with the piece
     // U blocks ahead, so each lane keeps U x 16 B loads in flight continuously.
-    if (nb >= 1 + 2 * (uint64_t)U) {
-      u32x4 buf[U];
+    uint64_t b = 0;
+    for (; b + 2 * U <= nb; b += U) {
+      if constexpr (IL) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) buf[u] = ld16<NT>(q + (b + u) * (kBlockBytes / 16));
-      for (; b + 2 * U <= nb; b += U) {
-        if constexpr (IL) {
+        for (int u = 0; u < U; u += 2) {
+          const u32x4 w0 = buf[u], w1 = buf[u + 1];
+          buf[u] = ld16<NT>(q + (b + U + u) * (kBlockBytes / 16));
+          buf[u + 1] = ld16<NT>(q + (b + U + u + 1) * (kBlockBytes / 16));
+          s = rpiece_pair_d<DIAG>(w0, w1, k, s);
+        }
+      } else {
 #pragma unroll
-          for (int u = 0; u < U; u += 2) {
-            const u32x4 w0 = buf[u], w1 = buf[u + 1];
-            buf[u] = ld16<NT>(q + (b + U + u) * (kBlockBytes / 16));
-            buf[u + 1] = ld16<NT>(q + (b + U + u + 1) * (kBlockBytes / 16));
-            s = rpiece_pair_d<DIAG>(w0, w1, k, s);
-          }
-        } else {
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            const u32x4 w = buf[u];
-            buf[u] = ld16<NT>(q + (b + U + u) * (kBlockBytes / 16));
-            s = rpiece(w, k, nib_mul(s, kFoldOff));
-          }
+        for (int u = 0; u < U; ++u) {
+          const u32x4 w = buf[u];
+          buf[u] = ld16<NT>(q + (b + U + u) * (kBlockBytes / 16));
+          s = rpiece(w, k, nib_mul(s, kFoldOff));
         }
       }
-#pragma unroll
-      for (int u = 0; u < U; ++u) s = rpiece(buf[u], k, nib_mul(s, kFoldOff));
-      b += U;
     }
+    // Drain (nb - b < 2U): consume the slots, refilling each with its block U ahead if
+    // there is one, then consume the refills. Predicates are wave-uniform.
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (b + u < nb) {
+        const u32x4 w = buf[u];
+        if (b + U + u < nb) buf[u] = ld16<NT>(q + (b + U + u) * (kBlockBytes / 16));
+        s = rpiece(w, k, nib_mul(s, kFoldOff));
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (b + U + u < nb) s = rpiece(buf[u], k, nib_mul(s, kFoldOff));
   } else {
+    s = rpiece(load_block0<NT>(base, v0, bs, lane), k, 0u);
+    uint64_t b = 1;
     for (; b + U <= nb; b += U) {
       u32x4 buf[U];
 #pragma unroll
@@ -257,14 +283,15 @@ __device__ __forceinline__ uint32_t body_crc(const uint8_t* __restrict__ base, u
 #pragma unroll
       for (int u = 0; u < U; ++u) s = rpiece(buf[u], k, nib_mul(s, kFoldOff));
     }
-  }
-  for (; b < nb; ++b) {
-    const u32x4 x = ld16<NT>(q + b * (kBlockBytes / 16));
-    s = rpiece(x, k, nib_mul(s, kFoldOff));
+    for (; b < nb; ++b) {
+      const u32x4 x = ld16<NT>(q + b * (kBlockBytes / 16));
+      s = rpiece(x, k, nib_mul(s, kFoldOff));
+    }
   }
 
   // Lane l's stream ends 16(63-l) bytes before be: xor-tree with shifts 16*2^lvl,
   // partners delivered by DPP (no LDS round trip for the move itself).
+  if constexpr (DIAG == 3) return s ^ __shfl_xor(s, 1);  // diagnostic timing build: no tree (wrong CRC)
   s = tree_level<0>(s, lane);
   s = tree_level<1>(s, lane);
   s = tree_level<2>(s, lane);
@@ -482,6 +509,208 @@ __device__ __forceinline__ uint32_t body_crc_t4(const uint8_t* __restrict__ base
   return s;
 }
 
+__device__ __forceinline__ uint64_t aligned_end(uint64_t s, uint64_t e) {
+  uint64_t b = e & ~uint64_t(15);
+  return b < s ? s : b;
+}
+
+// ---- group mode: whole small chunks, G lanes each, 64/G chunks per wave ----
+// Per chunk the wave-mode fixed cost is a 6-level tree and the dependent LDS chain of
+// each 1 KiB block; for 1-4 KiB chunks that, not HBM, sets the rate. A G-lane group
+// takes a whole chunk instead: lane gl owns bytes [16gl, 16gl+16) of every 16G-byte
+// block, fold x^(8*16G) = POW[log2 16G], a log2(G)-level tree, and 64/G chunks' chains
+// run in the same instructions. The initial register ~crc_in is XORed into the chunk's
+// first four bytes where they are loaded (plus ~crc_in >> 8len when len < 4), which
+// removes the per-chunk shift over len. Model: tests/kernel_model.py group_crc.
+
+// XOR the initial register's little-endian bytes (at addresses [cs, cs+4)) into the
+// 16-B piece at address p.
+__device__ __forceinline__ u32x4 xor_init(u32x4 w, int64_t p, uint64_t cs, uint32_t rinit) {
+  const int64_t o = (int64_t)cs - p;  // init offset inside the piece
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const int64_t od = o - 4 * d;
+    if (od >= 0 && od < 4) w[d] ^= rinit << (8 * (uint32_t)od);
+    else if (od < 0 && od > -4) w[d] ^= rinit >> (8 * (uint32_t)(-od));
+  }
+  return w;
+}
+
+template <int G>
+__device__ __forceinline__ constexpr uint32_t nib_fold_off() {  // x^(8*16G) = POW[log2 16G]
+  return kPowOff + kNibSetBytes * (G == 16 ? 8u : 9u);
+}
+
+// The NB blocks of a group chunk, block B at p0 + B*BB (BB = 16G), one struct member each
+// (no array, so nothing becomes a promoted vector that predicated writes copy whole).
+// prime() issues blocks 0..P-1; chain() folds block B in order and, as it takes B,
+// issues block B+P into member B+P: P blocks in flight per lane, ~4P VGPRs live.
+// Bytes before cs read as zero; the piece holding [cs, cs+4) gets the initial register.
+struct GroupCtx {
+  const uint8_t* __restrict__ base;
+  int64_t p0;
+  uint64_t cs;
+  bool body;
+  uint32_t nbw;
+  uint32_t rinit;
+};
+
+template <bool NT, int BB>
+__device__ __forceinline__ u32x4 group_load(const GroupCtx& g, int b) {
+  const int64_t p = g.p0 + (int64_t)b * BB;
+  u32x4 w = {0u, 0u, 0u, 0u};
+  if ((uint32_t)b < g.nbw && g.body && p + 16 > (int64_t)g.cs)  // => floor16(cs) <= p < cb
+    w = ld16<NT>(reinterpret_cast<const u32x4*>(g.base + p));
+  return w;
+}
+
+template <int B, int NB, int P, bool NT, int BB>
+struct GroupBlocksT {
+  u32x4 w;
+  GroupBlocksT<B + 1, NB, P, NT, BB> next;
+  template <int D>
+  __device__ __forceinline__ u32x4& at() {
+    if constexpr (D == 0) return w;
+    else return next.template at<D - 1>();
+  }
+  __device__ __forceinline__ void prime(const GroupCtx& g) {
+    if constexpr (B < P) {
+      w = group_load<NT, BB>(g, B);
+      next.prime(g);
+    }
+  }
+  __device__ __forceinline__ uint32_t chain(const GroupCtx& g, const LaneConst& k, uint32_t s, uint32_t fold_off) {
+    if ((uint32_t)B >= g.nbw) return s;
+    u32x4 x = w;
+    if constexpr (B + P < NB) at<P>() = group_load<NT, BB>(g, B + P);
+    const int64_t p = g.p0 + (int64_t)B * BB;
+    if (p < (int64_t)g.cs + 4 && p + 16 > (int64_t)g.cs) {
+      x = xor_init(x, p, g.cs, g.rinit);
+      if (p < (int64_t)g.cs) {
+        const uint32_t cut = (uint32_t)((int64_t)g.cs - p);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const int lo = (int)cut - 4 * d;
+          const uint32_t m = lo <= 0 ? 0xFFFFFFFFu : (lo >= 4 ? 0u : (0xFFFFFFFFu << (8 * lo)));
+          x[d] &= m;
+        }
+      }
+    }
+    s = rpiece(x, k, B ? nib_mul(s, fold_off) : 0u);
+    return next.chain(g, k, s, fold_off);
+  }
+};
+template <int NB, int P, bool NT, int BB>
+struct GroupBlocksT<NB, NB, P, NT, BB> {
+  template <int D>
+  __device__ __forceinline__ u32x4& at();  // never instantiated: refills stop at NB
+  __device__ __forceinline__ void prime(const GroupCtx&) {}
+  __device__ __forceinline__ uint32_t chain(const GroupCtx&, const LaneConst&, uint32_t s, uint32_t) { return s; }
+};
+
+// Finalized CRC of chunk [cs, cs+len) continued from cin, valid in the first lane of the
+// lane's group. nbw: wave-uniform block count (max over the groups); shorter chunks get
+// leading zero blocks, which leave a zero register unchanged and issue no loads.
+template <int G, int NB, bool NT>
+__device__ __forceinline__ uint32_t group_crc(const uint8_t* __restrict__ base, uint64_t cs, uint64_t len,
+                                              uint32_t cin, uint32_t nbw, uint32_t lane, const LaneConst& k) {
+  constexpr uint32_t BB = 16u * G;
+  const uint32_t gl = lane & (G - 1);
+  const uint32_t rinit = ~cin;
+  const uint64_t ce = cs + len;
+  const uint64_t cb = aligned_end(cs, ce);
+  const bool body = cb > cs;  // => cb is 16-B aligned
+  const int64_t p0 = (int64_t)cb - (int64_t)nbw * BB + 16 * (int64_t)gl;
+  // all NB blocks' loads in flight before the first is used (GroupBlocks: one member per
+  // block, so nothing becomes a promoted vector that predicated writes would copy whole)
+  const GroupCtx g{base, p0, cs, body, nbw, rinit};
+  GroupBlocksT<0, NB, (NB < 8 ? NB : 8), NT, (int)BB> blk;
+  blk.prime(g);
+  const uint32_t s = blk.chain(g, k, 0u, nib_fold_off<G>());
+  uint32_t r = s;
+  if (nbw) {
+    r = tree_level<0>(r, lane);
+    r = tree_level<1>(r, lane);
+    r = tree_level<2>(r, lane);
+    r = tree_level<3>(r, lane);
+    if constexpr (G == 32) r = tree_level<4>(r, lane);
+  }
+  r = __shfl(r, (int)(lane | (G - 1)));  // the group's body CRC, from its last lane
+  const uint32_t t = (uint32_t)(ce - cb);  // trailing < 16 bytes
+  if (t & 1u) r = nib_mul(r, kPowOff + kNibSetBytes * 0);
+  if (t & 2u) r = nib_mul(r, kPowOff + kNibSetBytes * 1);
+  if (t & 4u) r = nib_mul(r, kPowOff + kNibSetBytes * 2);
+  if (t & 8u) r = nib_mul(r, kPowOff + kNibSetBytes * 3);
+  uint32_t v = 0;
+  if (gl < t) {
+    const uint64_t a = cb + gl;
+    uint32_t byte = base[a];
+    if (a < cs + 4) byte ^= (rinit >> (8 * (uint32_t)(a - cs))) & 0xFFu;
+    const uint32_t kk = t - 1 - gl;
+    const uint32_t j = kk & 3;
+    v = lds_rd(((j >> 1) << 16) | (byte << 8) | ((j & 1) << 7) | ((lane & 31) << 2));
+    if (kk & 4) v = nib_mul(v, kPowOff + kNibSetBytes * 2);  // x^(8*4)
+    if (kk & 8) v = nib_mul(v, kPowOff + kNibSetBytes * 3);  // x^(8*8)
+  }
+  v ^= dpp<0x128, 0xf>(v);  // xor over the 16-lane row: row_ror 8, 4, 2, 1
+  v ^= dpp<0x124, 0xf>(v);
+  v ^= dpp<0x122, 0xf>(v);
+  v ^= dpp<0x121, 0xf>(v);
+  uint32_t crc = r ^ v ^ 0xFFFFFFFFu;
+  if (len < 4) crc ^= rinit >> (8 * (uint32_t)len);
+  return crc;
+}
+
+// Group kernel: every chunk with 0 < len <= a.small_max (= 16*G*NB), whole, from the
+// plan's compacted list small_idx[0..small_total). Wave w takes list entries
+// [w*K, (w+1)*K), K a multiple of 64/G, in rounds of 64/G chunks (one per group). The
+// sweep kernel skips these chunks (the plan gives them no byte share).
+template <int G, int NB, bool NT>
+__global__ __launch_bounds__(1024) void crc32_group_kernel(SweepArgs a) {
+  constexpr uint32_t S = 64 / G;
+  const uint64_t ns = *a.small_total;
+  if (ns == 0) return;  // uniform: every wave leaves before the LDS fill
+  {
+    const u32x4* src = reinterpret_cast<const u32x4*>(a.img);
+    u32x4* dst = reinterpret_cast<u32x4*>(g_lds);
+    for (uint32_t i = threadIdx.x; i < kLdsBytes / 16; i += blockDim.x) dst[i] = src[i];
+  }
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t waves_per_block = blockDim.x >> 6;
+  // wave-major over workgroups: the first list ranges land on different CUs/XCDs
+  const uint32_t wave = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * gridDim.x + blockIdx.x);
+  const uint64_t nwaves = (uint64_t)gridDim.x * waves_per_block;
+  const uint64_t per = ((ns + nwaves - 1) / nwaves + S - 1) / S * S;
+  const uint64_t i0 = (uint64_t)wave * per;
+  if (i0 >= ns) return;
+  const uint64_t i1 = i0 + per < ns ? i0 + per : ns;
+  const LaneConst k = make_lane_const(lane);
+  const uint32_t gi = lane / G;
+#pragma unroll 1
+  for (uint64_t i = i0; i < i1; i += S) {
+    const bool act = i + gi < i1;
+    const uint32_t ci = act ? a.small_idx[i + gi] : 0u;
+    uint64_t len = 0, off = 0;
+    uint32_t cin = 0;
+    if (act) {
+      len = a.len[ci];
+      off = a.off[ci];
+      cin = a.crc_in ? a.crc_in[ci] : 0u;
+    }
+    const uint64_t cb = aligned_end(off, off + len);
+    const uint32_t nb = (uint32_t)((cb - off + 16 * G - 1) / (16 * G));
+    uint32_t nbw = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < S; ++q) {
+      const uint32_t x = __builtin_amdgcn_readlane(nb, q * G);
+      nbw = x > nbw ? x : nbw;
+    }
+    const uint32_t crc = group_crc<G, NB, NT>(a.base, off, len, cin, nbw, lane, k);
+    if ((lane & (G - 1)) == 0 && act) a.out[ci] = crc;  // whole chunks: plain stores
+  }
+}
+
 // Largest c in [0, n) with byte_start[c] <= g (byte_start nondecreasing, byte_start[0] = 0).
 // 64-ary search: one coalesced probe per lane per round, log64(n) rounds.
 __device__ __forceinline__ uint32_t find_chunk(const uint64_t* __restrict__ byte_start, uint32_t n, uint64_t g,
@@ -498,11 +727,6 @@ __device__ __forceinline__ uint32_t find_chunk(const uint64_t* __restrict__ byte
     hi = nhi < hi ? nhi : hi;
   }
   return lo;
-}
-
-__device__ __forceinline__ uint64_t aligned_end(uint64_t s, uint64_t e) {
-  uint64_t b = e & ~uint64_t(15);
-  return b < s ? s : b;
 }
 
 // Chunk-relative cut for global stream position g inside chunk c (0 < r < len):
@@ -543,13 +767,15 @@ __global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
   uint32_t init_term = 0;
   uint32_t c = __builtin_amdgcn_readfirstlane(find_chunk(a.byte_start, a.n, g0, lane));
 
-  // One segment: raw CRC of its body, shifted to the chunk end, + tail + init, XORed into out[ci].
-  auto segment = [&](uint32_t ci, uint64_t bsc, uint64_t len, uint64_t cs, uint32_t cin) {
+  // One segment: raw CRC of its body, shifted to the chunk end, + tail + init (wave-uniform).
+  // *whole: the segment is the entire chunk, so no other wave contributes to out[ci].
+  auto segment = [&](uint64_t bsc, uint64_t len, uint64_t cs, uint32_t cin, bool* whole) -> uint32_t {
     const uint64_t ce = cs + len;
     const uint64_t cb = aligned_end(cs, ce);
     const uint64_t r0 = g0 > bsc ? snap_cut(cs, len, g0 - bsc) : 0;
     const uint64_t r1 = g1 - bsc < len ? snap_cut(cs, len, g1 - bsc) : len;
-    if (r0 >= r1) return;
+    *whole = r0 == 0 && r1 == len;
+    if (r0 >= r1) return 0u;
     const uint64_t sa = cs + r0, se = cs + r1;
     const uint64_t be = se == ce ? cb : se;  // 16-B aligned body end
     uint32_t r = 0;
@@ -579,12 +805,21 @@ __global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
         r ^= shift_bytes(~cin, len, xpow2) ^ 0xFFFFFFFFu;
       }
     }
-    if (lane == 0) atomicXor(&a.out[ci], r);
+    return r;
+  };
+  // A partial segment shares its chunk with a neighbouring wave: combine by XOR.
+  auto emit_partial = [&](uint32_t ci, uint32_t r) {
+    if constexpr (DIAG == 2) {  // diagnostic timing build: no per-segment atomic (wrong CRCs)
+      if (lane == 0 && r == 0x9E3779B9u) a.out[ci] = r;
+    } else {
+      if (lane == 0) atomicXor(&a.out[ci], r);
+    }
   };
 
   if constexpr (WIN) {
     // Descriptors fetched 64 at a time (lane j <- chunk c+j), read back with readlane:
-    // one load round trip per 64 chunks (costs 7 VGPRs live across the body).
+    // one load round trip per 64 chunks. byte_start only seeds a scalar running sum, so
+    // 5 VGPRs stay live across the body.
     bool done = false;
     while (!done && c < a.n) {
       const uint32_t cnt = a.n - c < 64u ? a.n - c : 64u;
@@ -596,15 +831,25 @@ __global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
         w_off = a.off[c + lane];
         w_cin = a.crc_in ? a.crc_in[c + lane] : 0u;
       }
-      for (uint32_t j = 0; j < cnt; ++j) {
-        const uint64_t bsc = readlane64(w_bs, j);
+      uint64_t bsc = readlane64(w_bs, 0);
+      for (uint32_t j = 0; j < cnt;) {
         if (bsc >= g1) {
           done = true;
           break;
         }
         const uint64_t len = readlane64(w_len, j);
-        if (len == 0) continue;  // empty chunks are finished by the plan kernel
-        segment(c + j, bsc, len, readlane64(w_off, j), __builtin_amdgcn_readlane(w_cin, j));
+        const uint64_t span = len > a.small_max ? len : 0;  // small chunks: group kernel
+        if (span != 0) {  // empty chunks are finished by the plan kernel
+          bool whole;
+          const uint32_t r = segment(bsc, len, readlane64(w_off, j), __builtin_amdgcn_readlane(w_cin, j), &whole);
+          if (whole && DIAG != 2) {
+            if (lane == 0) a.out[c + j] = r;  // no other wave contributes to this chunk
+          } else {
+            emit_partial(c + j, r);
+          }
+        }
+        bsc += span;
+        ++j;
       }
       c += cnt;
     }
@@ -622,7 +867,10 @@ __global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
         n_off = a.off[c + 1];
         n_cin = a.crc_in ? a.crc_in[c + 1] : 0u;
       }
-      if (len != 0) segment(c, bsc, len, cs, cin);  // empty chunks are finished by the plan kernel
+      if (len != 0 && len > a.small_max) {  // empty chunks: plan kernel; small ones: group kernel
+        bool whole;
+        emit_partial(c, segment(bsc, len, cs, cin, &whole));
+      }
       ++c;
     }
   }
@@ -651,35 +899,63 @@ __device__ __forceinline__ uint64_t block_scan256(uint64_t v, uint64_t* total) {
   return v + before;
 }
 
+// Bytes a chunk contributes to the sweep's byte shares: chunks the group kernel takes
+// whole (len <= small_max) contribute none.
+__device__ __forceinline__ uint64_t share_len(uint64_t len, uint64_t small_max) {
+  return len > small_max ? len : 0u;
+}
+
+__device__ __forceinline__ bool is_small(uint64_t len, uint64_t small_max) { return len != 0 && len <= small_max; }
+
 __global__ __launch_bounds__(256) void crc32_plan_count_kernel(PlanArgs a) {
   const uint32_t base = blockIdx.x * kPlanPerBlock;
-  uint64_t sum = 0;
+  uint64_t sum = 0, nsmall = 0;
   for (uint32_t r = 0; r < kPlanPerBlock; r += 256) {
     const uint32_t c = base + r + threadIdx.x;
-    if (c < a.n) sum += a.len[c];
+    if (c < a.n) {
+      const uint64_t len = a.len[c];
+      sum += share_len(len, a.small_max);
+      nsmall += is_small(len, a.small_max);
+    }
   }
-  uint64_t total;
+  uint64_t total, total_small;
   (void)block_scan256(sum, &total);
-  if (threadIdx.x == 0) a.block_sum[blockIdx.x] = total;
+  (void)block_scan256(nsmall, &total_small);
+  if (threadIdx.x == 0) {
+    a.block_sum[blockIdx.x] = total;
+    a.block_small[blockIdx.x] = total_small;
+  }
 }
 
 __global__ __launch_bounds__(256) void crc32_plan_scan_kernel(PlanArgs a) {
-  uint64_t part = 0;
-  for (uint32_t i = threadIdx.x; i < blockIdx.x; i += 256) part += a.block_sum[i];
-  uint64_t carry;
+  uint64_t part = 0, part_small = 0;
+  for (uint32_t i = threadIdx.x; i < blockIdx.x; i += 256) {
+    part += a.block_sum[i];
+    part_small += a.block_small[i];
+  }
+  uint64_t carry, carry_small;
   (void)block_scan256(part, &carry);
+  (void)block_scan256(part_small, &carry_small);
   const uint32_t base = blockIdx.x * kPlanPerBlock;
   for (uint32_t r = 0; r < kPlanPerBlock; r += 256) {
     const uint32_t c = base + r + threadIdx.x;
-    const uint64_t v = c < a.n ? a.len[c] : 0u;
-    uint64_t round_total;
+    const uint64_t len = c < a.n ? a.len[c] : 0u;
+    const uint64_t v = share_len(len, a.small_max);
+    const uint64_t sm = is_small(len, a.small_max);
+    uint64_t round_total, round_small;
     const uint64_t incl = block_scan256(v, &round_total);
+    const uint64_t incl_small = block_scan256(sm, &round_small);
     if (c < a.n) {
       a.byte_start[c] = carry + incl - v;
-      a.out[c] = v ? 0u : (a.crc_in ? a.crc_in[c] : 0u);
-      if (c == a.n - 1) a.byte_start[a.n] = carry + incl;
+      a.out[c] = len ? 0u : (a.crc_in ? a.crc_in[c] : 0u);
+      if (sm) a.small_idx[carry_small + incl_small - 1] = c;
+      if (c == a.n - 1) {
+        a.byte_start[a.n] = carry + incl;
+        *a.small_total = carry_small + incl_small;
+      }
     }
     carry += round_total;
+    carry_small += round_small;
   }
 }
 
@@ -744,10 +1020,26 @@ hipError_t launch_sweep(const SweepArgs& a, int grid, int variant, hipStream_t s
     case 11: hipLaunchKernelGGL((crc32_sweep_kernel<4, true, true, false, true, 0, 1>), dim3(grid), dim3(1024), 0, s, a); break;
     case 12: hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, false, true, 0, -2>), dim3(grid), dim3(1024), 0, s, a); break;
     case 13: hipLaunchKernelGGL((crc32_sweep_kernel<4, true, true, false, true, 0, -2>), dim3(grid), dim3(1024), 0, s, a); break;
-    case kDiagNoFold:  // timing-only diagnostic (wrong CRCs): FOLD lookups removed
-      hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, true, true, 1>), dim3(grid), dim3(1024), 0, s, a);
-      break;
+    // timing-only diagnostics (wrong CRCs): 100 FOLD lookups removed, 101 no per-segment
+    // atomic, 102 no wave tree
+    case kDiagNoFold: hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, true, true, 1>), dim3(grid), dim3(1024), 0, s, a); break;
+    case kDiagNoFold + 1: hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, true, true, 2>), dim3(grid), dim3(1024), 0, s, a); break;
+    case kDiagNoFold + 2: hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, true, true, 3>), dim3(grid), dim3(1024), 0, s, a); break;
 #undef AMBRY_TILES_CASE
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_group(const SweepArgs& a, int grid, int mode, hipStream_t s) {
+  switch (mode) {
+    case 0: return hipSuccess;
+    case 1: hipLaunchKernelGGL((crc32_group_kernel<16, 8, true>), dim3(grid), dim3(1024), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((crc32_group_kernel<16, 16, true>), dim3(grid), dim3(1024), 0, s, a); break;
+    case 3: hipLaunchKernelGGL((crc32_group_kernel<32, 8, true>), dim3(grid), dim3(1024), 0, s, a); break;
+    case 4: hipLaunchKernelGGL((crc32_group_kernel<16, 32, true>), dim3(grid), dim3(1024), 0, s, a); break;
+    case 5: hipLaunchKernelGGL((crc32_group_kernel<16, 64, true>), dim3(grid), dim3(1024), 0, s, a); break;
+    case 6: hipLaunchKernelGGL((crc32_group_kernel<32, 32, true>), dim3(grid), dim3(1024), 0, s, a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -174,9 +174,84 @@ class KernelModel:
             s = np.where((LANES & (1 << bit)) != 0, s ^ sh, s).astype(np.uint32)
         return int(s[63])
 
+    def group_crc(self, mem: np.ndarray, segs, G: int, nbmax: int):
+        """Group mode (sweep kernel group_crc): 64/G whole small chunks at once, lane gl of group gi
+        owning bytes [16gl, 16gl+16) of every 16G-byte block of chunk gi, the initial register
+        ~crc_in XORed into the chunk's first 4 bytes (r0 XOR'd into data, plus r0 >> 8len when
+        len < 4), fold x^(8*16G) = POW[log2 16G], a log2(G)-level tree, the < 16-B tail
+        lane-parallel. segs: [(cs, len, cin)] with len <= 16G*nbmax. Returns finalized CRCs."""
+        BB = 16 * G
+        lg = BB.bit_length() - 1
+        out = []
+        for cs, ln, cin in segs:
+            assert len(segs) <= 64 // G
+            rinit = (~cin) & 0xFFFFFFFF
+            ce = cs + ln
+            cb = max(cs, ce & ~15)
+            nb = (cb - cs + BB - 1) // BB
+            assert nb <= nbmax
+            v0 = cb - nb * BB
+            gl = np.arange(G, dtype=np.int64)
+
+            def init_bytes(addr, nbytes):
+                """XOR mask of the init register over bytes [addr, addr+nbytes) (little-endian)."""
+                m = 0
+                for i in range(nbytes):
+                    o = addr + i - cs
+                    if 0 <= o < 4:
+                        m |= ((rinit >> (8 * o)) & 0xFF) << (8 * i)
+                return m
+
+            s = np.zeros(G, dtype=np.uint32)
+            for b in range(nb):
+                w = np.zeros((G, 4), dtype=np.uint32)
+                for lane in range(G):
+                    p = v0 + b * BB + 16 * lane
+                    if p + 16 > cs:
+                        assert (cs & ~15) <= p and p + 16 <= cb
+                        raw = int.from_bytes(mem[p:p + 16].tobytes(), "little") ^ init_bytes(p, 16)
+                        raw &= ~((1 << (8 * max(0, cs - p))) - 1)  # bytes before cs read as zero
+                        w[lane] = np.frombuffer(raw.to_bytes(16, "little"), dtype="<u4")
+                fold = self.nib_mul(s, K_POW_OFF + K_NIB_SET * lg) if b else np.zeros(G, dtype=np.uint32)
+                L = [x[:G] for x in self.L]
+                save = self.L
+                self.L = L
+                x = self.slice4(w[:, 0], w[:, 1])
+                x = self.slice4(x, w[:, 2])
+                x = self.slice4(x, w[:, 3])
+                s = self.slice4(x, fold)
+                self.L = save
+            for lvl in range(G.bit_length() - 1):
+                o = s[gl ^ (1 << lvl)]
+                sh = self.nib_mul(o, K_TREE_OFF + K_NIB_SET * lvl)
+                s = np.where((gl & (1 << lvl)) != 0, s ^ sh, s).astype(np.uint32)
+            body = int(s[G - 1])
+            t = ce - cb
+            for bit in range(4):
+                if (t >> bit) & 1:
+                    body = int(self.nib_mul(np.array([body], dtype=np.uint32), K_POW_OFF + K_NIB_SET * bit)[0])
+            tail = 0
+            for lane in range(t):
+                bval = int(mem[cb + lane]) ^ init_bytes(cb + lane, 1)
+                k = t - 1 - lane
+                j = k & 3
+                v = int(self.lds(((j >> 1) << 16) | (bval << 8) | ((j & 1) << 7) | ((lane & 31) << 2)))
+                if k & 4:
+                    v = int(self.nib_mul(np.array([v], dtype=np.uint32), K_POW_OFF + K_NIB_SET * 2)[0])
+                if k & 8:
+                    v = int(self.nib_mul(np.array([v], dtype=np.uint32), K_POW_OFF + K_NIB_SET * 3)[0])
+                tail ^= v
+            crc = body ^ tail ^ 0xFFFFFFFF
+            if ln < 4:
+                crc ^= rinit >> (8 * ln)
+            out.append(crc & 0xFFFFFFFF)
+        return out
+
     def batch(self, mem: np.ndarray, off, length, crc_in=None, nwaves: int = 4096, quantum: int = 1024,
-              run: int = 1):
-        """Replays plan + sweep kernels with `nwaves` waves; returns the list of CRCs."""
+              run: int = 1, group=None, min_share: int = 0):
+        """Replays plan + sweep kernels with `nwaves` waves; returns the list of CRCs.
+        group=(G, nbmax): runs of whole chunks of <= 16*G*nbmax bytes inside a 64-descriptor
+        window go through group_crc, up to 64/G at a time, as the kernel's group mode does."""
         n = len(off)
         off = [int(x) for x in off]
         length = [int(x) for x in length]
@@ -186,16 +261,36 @@ class KernelModel:
         total = byte_start[n]
         out = [0 if length[c] else (0 if crc_in is None else int(crc_in[c])) for c in range(n)]
         share = ((total + nwaves - 1) // nwaves + quantum - 1) // quantum * quantum
+        share = max(share, min_share)
         for w in range(nwaves):
             g0 = w * share
             if share == 0 or g0 >= total:
                 break
             g1 = min(total, g0 + share)
             c = bisect.bisect_right(byte_start, g0, 0, n) - 1
+            win_end = c + 64
             while c < n:
                 bsc = byte_start[c]
                 if bsc >= g1:
                     break
+                if c >= win_end:
+                    win_end += 64
+                if group is not None:
+                    G, nbmax = group
+
+                    def small(i):
+                        return (i < min(n, win_end) and byte_start[i] < g1 and length[i] <= 16 * G * nbmax
+                                and byte_start[i] >= g0 and byte_start[i] + length[i] <= g1)
+
+                    if small(c):
+                        run_ = [c]
+                        while len(run_) < 64 // G and small(run_[-1] + 1):
+                            run_.append(run_[-1] + 1)
+                        segs = [(off[i], length[i], 0 if crc_in is None else int(crc_in[i])) for i in run_]
+                        for i, v in zip(run_, self.group_crc(mem, segs, G, nbmax)):
+                            out[i] = v  # whole chunk: plain store
+                        c = run_[-1] + 1
+                        continue
                 ln = length[c]
                 if ln == 0:
                     c += 1

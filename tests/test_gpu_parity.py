@@ -108,7 +108,7 @@ def test_ragged_batch_grid_sizes(gpu, oracle, grid):
     assert np.array_equal(got, oracle.batch(mem, off, ln, threads=8))
 
 
-@pytest.mark.parametrize("variant", list(range(14)))
+@pytest.mark.parametrize("variant", list(range(20)))
 def test_kernel_variants(gpu, oracle, variant):
     rng = np.random.default_rng(100 + variant)
     mem = stream_bytes(6, 0, 16 << 20)
@@ -120,6 +120,32 @@ def test_kernel_variants(gpu, oracle, variant):
     finally:
         gpu.set_variant(0, 0)
     assert np.array_equal(got, oracle.batch(mem, off, ln, threads=8))
+
+
+@pytest.mark.parametrize("variant", [0, 14, 15, 16, 17, 18, 19])
+@pytest.mark.parametrize("grid", [0, 1, 5])
+def test_small_chunk_group_kernel(gpu, oracle, variant, grid):
+    """Group kernel (variants 14-16): whole chunks <= 2/4 KiB, G lanes each, init register
+    folded into the data. Lengths 0..5000 at every alignment, crc_in, large chunks between."""
+    rng = np.random.default_rng(700 + variant * 10 + grid)
+    mem = stream_bytes(70 + variant, 0, 8 << 20)
+    n = 5000
+    ln = rng.integers(0, 20000 if variant >= 17 else 5000, size=n)
+    ln[:46] = list(range(0, 20)) + [255, 256, 257, 511, 512, 513, 2047, 2048, 2049, 4095, 4096, 4097,
+                                    1 << 20, 3, 2, 1, 0, 16, 17, 33, 8191, 8192, 8193, 16383, 16384, 16385]
+    ln[::97] = rng.integers(5000, 1 << 20, size=len(ln[::97]))  # large chunks mixed in
+    off = rng.integers(0, (8 << 20) - (1 << 20), size=n)
+    off[:16] = np.arange(16)  # chunks in the first bytes of the allocation
+    cin = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32)
+    cin[::3] = 0
+    gpu.set_variant(0, variant)
+    gpu.set_grid(0, grid)
+    try:
+        got = run_batch(gpu, mem, off, ln, crc_in=cin)
+    finally:
+        gpu.set_variant(0, 0)
+        gpu.set_grid(0, 0)
+    assert np.array_equal(got, oracle.batch(mem, off, ln, crc_in=cin, threads=8))
 
 
 def test_crc_in_streaming_composition(gpu, oracle):

@@ -62,3 +62,22 @@ def test_model_large_shift_slow_path(model):
 
     for n in (1 << 36, (1 << 37) + 12345, (1 << 40) - 1):
         assert model.shift_bytes(0xFFFFFFFF ^ 0x1234, n) ^ 0xFFFFFFFF == ambry_amd.zeros(0x1234, n)
+
+
+@pytest.mark.parametrize("group", [(16, 8), (16, 16), (32, 8)])
+def test_model_group_mode(model, oracle, group):
+    """Group mode: whole small chunks, 64/G at a time, init register folded into the data.
+    Lengths 0..~4 KiB at every end/start residue, mixed with chunks too big for a group."""
+    G, nbmax = group
+    rng = np.random.default_rng(G * 100 + nbmax)
+    mem = stream_bytes(17, 0, 400000)
+    smax = 16 * G * nbmax
+    ln = [0, 1, 2, 3, 4, 5, 15, 16, 17, 31, 255, 256, 257, 1000, smax - 1, smax, smax + 1, 20000]
+    ln += [int(x) for x in rng.integers(0, smax + 1, size=40)]
+    off = [int(x) for x in rng.integers(0, 380000, size=len(ln))]
+    off[:5] = [0, 1, 15, 17, 33]
+    cin = np.array([(i * 0x9E3779B9 + 5) & 0xFFFFFFFF for i in range(len(ln))], dtype=np.uint32)
+    exp = list(oracle.batch(mem, off, ln, crc_in=cin))
+    for nw, ms in ((1, 0), (3, 0), (7, 32768)):
+        assert model.batch(mem, off, ln, crc_in=cin, nwaves=nw, group=group, min_share=ms) == exp
+    assert model.batch(mem, off, ln, nwaves=2, group=group) == list(oracle.batch(mem, off, ln))

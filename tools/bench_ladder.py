@@ -65,7 +65,7 @@ def cpu_row(size: int, target_s: float = 0.3):
     return out
 
 
-def gpu_rows(size: int, gib: float, reps: int):
+def gpu_rows(size: int, gib: float, reps: int, variant: int = 0, check: bool = True):
     import numpy as np
     import torch
 
@@ -79,13 +79,15 @@ def gpu_rows(size: int, gib: float, reps: int):
     ln = torch.full((n,), size, dtype=torch.int64, device="cuda")
     out = torch.empty(n, dtype=torch.int32, device="cuda")
     ws = torch.empty(D.workspace_bytes(n), dtype=torch.uint8, device="cuda")
+    D.set_variant(0, variant)
     D.crc32_batch(buf, off, ln, out=out, workspace=ws)
     torch.cuda.synchronize()
     # spot-check a few chunks against zlib
     idx = [0, n // 2, n - 1]
     host = buf.view(n, stride)[idx, :size].cpu().numpy()
     got = out[idx].cpu().numpy().view(np.uint32)
-    assert [zlib.crc32(h.tobytes()) for h in host] == list(got), "ladder parity"
+    if check:
+        assert [zlib.crc32(h.tobytes()) for h in host] == list(got), "ladder parity"
     t_pre = time.perf_counter()
     while time.perf_counter() - t_pre < 0.3:
         D.crc32_batch(buf, off, ln, out=out, workspace=ws)
@@ -126,6 +128,7 @@ def gpu_rows(size: int, gib: float, reps: int):
     torch.cuda.synchronize()
     host_us = (time.perf_counter() - t0) / calls * 1e6
     call = {"us_per_call_stream": round(e0.elapsed_time(e1) / calls * 1e3, 2), "us_per_call_host": round(host_us, 2)}
+    D.set_variant(0, 0)
     del buf, off, ln, out, ws
     torch.cuda.empty_cache()
     return batch, call
@@ -137,6 +140,8 @@ def main():
     ap.add_argument("--reps", type=int, default=7)
     ap.add_argument("--no-gpu", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--variants", default="0", help="sweep variants (>= 100: timing diagnostics, no parity)")
+    ap.add_argument("--sizes", default=None, help="subset of the ladder, comma separated bytes")
     args = ap.parse_args()
     if not args.no_gpu:
         import torch
@@ -145,13 +150,18 @@ def main():
 
         torch.cuda.set_device(0)
         D.init(0)
-    for size in LADDER:
+    sizes = LADDER if not args.sizes else [int(x) for x in args.sizes.split(",")]
+    for size in sizes:
         row = {"size": size}
         if not args.no_cpu:
             row["cpu_1thread"] = cpu_row(size)
         if not args.no_gpu:
-            row["gpu_batch"], row["gpu_call"] = gpu_rows(size, args.gib, args.reps)
-        print(json.dumps(row), flush=True)
+            for v in [int(x) for x in args.variants.split(",")]:
+                row["variant"] = v
+                row["gpu_batch"], row["gpu_call"] = gpu_rows(size, args.gib, args.reps, v, check=v < 100)
+                print(json.dumps(row), flush=True)
+        else:
+            print(json.dumps(row), flush=True)
 
 
 if __name__ == "__main__":
