@@ -56,6 +56,7 @@ _SIGNATURES = [
      [ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
       ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint32), ctypes.c_int]),
     ("ambrycrc_set_variant", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    ("ambrycrc_get_variant", ctypes.c_int, [ctypes.c_int]),
     ("ambrycrc_set_grid", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     ("ambrycrc_timing_enable", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     ("ambrycrc_timing_collect", ctypes.c_int,

@@ -111,7 +111,10 @@ struct DevCtx {
   int device = -1;
   int num_cu = 0;
   int grid = 0;
-  int variant = 0;  // U=8, NT loads, rolling prefetch, 2 pieces interleaved, descriptor window (tools/sweep.py)
+  // 20: sweep variant 0 (U=8, NT loads, rolling prefetch, 2 pieces interleaved, descriptor
+  // window) with the group phase G16/NB32 fused in for whole chunks <= 8 KiB
+  // (tools/bench_ladder.py, tools/sweep.py)
+  int variant = 20;
   uint32_t* d_img = nullptr;
   void* d_ws = nullptr;
   size_t ws_bytes = 0;
@@ -176,9 +179,14 @@ int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uin
   p.small_idx = reinterpret_cast<uint32_t*>(p.small_total + 1);
   p.out = out;
   // variants >= 14: variant 0's sweep plus the group kernel for small whole chunks
-  const int sweep_variant = c->variant >= 14 && c->variant < kNumVariants ? 0 : c->variant;
-  const int group_mode = c->variant >= 14 && c->variant < kNumVariants ? c->variant - 13 : 0;
-  p.small_max = group_small_max(group_mode);
+  // 20, 21: the group phase fused into the sweep launch (sweep variant = the variant itself)
+  const bool grouped = c->variant >= 14 && c->variant < 20;
+  const int sweep_variant = grouped ? 0 : c->variant;
+  const int group_mode = grouped ? c->variant - 13 : 0;
+  p.small_max = c->variant == 20   ? group_small_max(4)
+                : c->variant == 21 ? group_small_max(2)
+                : c->variant == 22 ? group_small_max(5)
+                                   : group_small_max(group_mode);
   hipError_t e = launch_plan(p, s);
   if (e != hipSuccess) return AMBRYCRC_EHIP;
   SweepArgs t;
@@ -589,6 +597,11 @@ int ambrycrc_set_variant(int device, int variant) {
     return AMBRYCRC_EINVAL;
   c->variant = variant;
   return AMBRYCRC_OK;
+}
+
+int ambrycrc_get_variant(int device) {
+  DevCtx* c = ctx_for(device);
+  return c ? c->variant : AMBRYCRC_ENOINIT;
 }
 
 int ambrycrc_set_grid(int device, int workgroups) {

@@ -22,6 +22,7 @@ struct PlanArgs {
 
 constexpr uint32_t kPlanPerBlock = 2048;  // chunks per planning workgroup
 constexpr uint64_t kShareQuantum = 1024;  // per-wave byte shares are multiples of this
+constexpr uint64_t kMinShare = 16384;     // ... and at least this (see crc32_sweep_kernel)
 
 struct SweepArgs {
   const uint8_t* base;
@@ -55,8 +56,9 @@ constexpr uint64_t group_small_max(int mode) {
 // 4 U8/PIPE/IL/WIN (temporal loads), 5 U8/NT batch loads, 6 U4/NT/PIPE/IL/WIN, 7 U8 batch (temporal)
 // 8 R=2 strided lane runs (U8 loads in flight), 9 R=4 strided runs (U8), 10 R=4 strided (U4),
 // 11 R=2 strided (U4), 12 64-B runs by quad transpose of coalesced loads (U8), 13 same (U4)
-// 14..19 = 0 plus the group kernel (modes 1..6) for small whole chunks
-constexpr int kNumVariants = 20;
+// 14..19 = 0 plus the group kernel (modes 1..6) for small whole chunks; 20, 21, 22 = 0 with the
+// group phase (G16/NB32, G16/NB16, G16/NB64: chunks <= 8, 4, 16 KiB) fused into the sweep launch
+constexpr int kNumVariants = 23;
 constexpr int kDiagNoFold = 100;  // diagnostic timing build, selectable via ambrycrc_set_variant only
 
 // Message verify (message_kernels.hip): kMsgSlots CRC jobs per message, slot order

@@ -541,11 +541,12 @@ __device__ __forceinline__ constexpr uint32_t nib_fold_off() {  // x^(8*16G) = P
   return kPowOff + kNibSetBytes * (G == 16 ? 8u : 9u);
 }
 
-// The NB blocks of a group chunk, block B at p0 + B*BB (BB = 16G), one struct member each
-// (no array, so nothing becomes a promoted vector that predicated writes copy whole).
-// prime() issues blocks 0..P-1; chain() folds block B in order and, as it takes B,
-// issues block B+P into member B+P: P blocks in flight per lane, ~4P VGPRs live.
-// Bytes before cs read as zero; the piece holding [cs, cs+4) gets the initial register.
+// The blocks of a group chunk, block b at p0 + b*BB (BB = 16G), through a ring of P struct
+// members (no array, so nothing becomes a promoted vector that predicated writes copy
+// whole): prime() issues blocks 0..P-1; a runtime loop steps P blocks at a time, member U
+// folding block b0+U and refilling with block b0+U+P. P blocks in flight per lane, ~4P
+// VGPRs, code size independent of the chunk-size cap. Bytes before cs read as zero; the
+// piece holding [cs, cs+4) gets the initial register XORed in.
 struct GroupCtx {
   const uint8_t* __restrict__ base;
   int64_t p0;
@@ -564,26 +565,22 @@ __device__ __forceinline__ u32x4 group_load(const GroupCtx& g, int b) {
   return w;
 }
 
-template <int B, int NB, int P, bool NT, int BB>
-struct GroupBlocksT {
+template <int U, int P, bool NT, int BB>
+struct GroupRingT {
   u32x4 w;
-  GroupBlocksT<B + 1, NB, P, NT, BB> next;
-  template <int D>
-  __device__ __forceinline__ u32x4& at() {
-    if constexpr (D == 0) return w;
-    else return next.template at<D - 1>();
-  }
+  GroupRingT<U + 1, P, NT, BB> next;
   __device__ __forceinline__ void prime(const GroupCtx& g) {
-    if constexpr (B < P) {
-      w = group_load<NT, BB>(g, B);
-      next.prime(g);
-    }
+    w = group_load<NT, BB>(g, U);
+    next.prime(g);
   }
-  __device__ __forceinline__ uint32_t chain(const GroupCtx& g, const LaneConst& k, uint32_t s, uint32_t fold_off) {
-    if ((uint32_t)B >= g.nbw) return s;
+  // Blocks b0+U for U = 0..P-1: member U holds block b0+U and is refilled with b0+U+P.
+  __device__ __forceinline__ uint32_t step(const GroupCtx& g, const LaneConst& k, uint32_t b0, uint32_t s,
+                                           uint32_t fold_off) {
+    const uint32_t b = b0 + U;
+    if (b >= g.nbw) return s;
     u32x4 x = w;
-    if constexpr (B + P < NB) at<P>() = group_load<NT, BB>(g, B + P);
-    const int64_t p = g.p0 + (int64_t)B * BB;
+    w = group_load<NT, BB>(g, (int)(b + P));
+    const int64_t p = g.p0 + (int64_t)b * BB;
     if (p < (int64_t)g.cs + 4 && p + 16 > (int64_t)g.cs) {
       x = xor_init(x, p, g.cs, g.rinit);
       if (p < (int64_t)g.cs) {
@@ -596,16 +593,16 @@ struct GroupBlocksT {
         }
       }
     }
-    s = rpiece(x, k, B ? nib_mul(s, fold_off) : 0u);
-    return next.chain(g, k, s, fold_off);
+    s = rpiece(x, k, b ? nib_mul(s, fold_off) : 0u);
+    return next.step(g, k, b0, s, fold_off);
   }
 };
-template <int NB, int P, bool NT, int BB>
-struct GroupBlocksT<NB, NB, P, NT, BB> {
-  template <int D>
-  __device__ __forceinline__ u32x4& at();  // never instantiated: refills stop at NB
+template <int P, bool NT, int BB>
+struct GroupRingT<P, P, NT, BB> {
   __device__ __forceinline__ void prime(const GroupCtx&) {}
-  __device__ __forceinline__ uint32_t chain(const GroupCtx&, const LaneConst&, uint32_t s, uint32_t) { return s; }
+  __device__ __forceinline__ uint32_t step(const GroupCtx&, const LaneConst&, uint32_t, uint32_t s, uint32_t) {
+    return s;
+  }
 };
 
 // Finalized CRC of chunk [cs, cs+len) continued from cin, valid in the first lane of the
@@ -624,9 +621,12 @@ __device__ __forceinline__ uint32_t group_crc(const uint8_t* __restrict__ base, 
   // all NB blocks' loads in flight before the first is used (GroupBlocks: one member per
   // block, so nothing becomes a promoted vector that predicated writes would copy whole)
   const GroupCtx g{base, p0, cs, body, nbw, rinit};
-  GroupBlocksT<0, NB, (NB < 8 ? NB : 8), NT, (int)BB> blk;
-  blk.prime(g);
-  const uint32_t s = blk.chain(g, k, 0u, nib_fold_off<G>());
+  constexpr int P = NB < 8 ? NB : 8;
+  GroupRingT<0, P, NT, (int)BB> ring;
+  ring.prime(g);
+  uint32_t s = 0;
+#pragma unroll 1
+  for (uint32_t b0 = 0; b0 < nbw; b0 += P) s = ring.step(g, k, b0, s, nib_fold_off<G>());
   uint32_t r = s;
   if (nbw) {
     r = tree_level<0>(r, lane);
@@ -665,27 +665,21 @@ __device__ __forceinline__ uint32_t group_crc(const uint8_t* __restrict__ base, 
 // plan's compacted list small_idx[0..small_total). Wave w takes list entries
 // [w*K, (w+1)*K), K a multiple of 64/G, in rounds of 64/G chunks (one per group). The
 // sweep kernel skips these chunks (the plan gives them no byte share).
+// List entries of wave `wave` (wave-major numbering): [wave*K, (wave+1)*K), K a multiple of
+// 64/G so every round fills all groups.
+template <int G>
+__device__ __forceinline__ uint64_t group_per(uint64_t ns, uint64_t nwaves) {
+  return ((ns + nwaves - 1) / nwaves + 64 / G - 1) / (64 / G) * (64 / G);
+}
+
 template <int G, int NB, bool NT>
-__global__ __launch_bounds__(1024) void crc32_group_kernel(SweepArgs a) {
+__device__ __forceinline__ void group_phase(const SweepArgs& a, uint64_t ns, uint32_t wave, uint64_t nwaves,
+                                            uint32_t lane, const LaneConst& k) {
   constexpr uint32_t S = 64 / G;
-  const uint64_t ns = *a.small_total;
-  if (ns == 0) return;  // uniform: every wave leaves before the LDS fill
-  {
-    const u32x4* src = reinterpret_cast<const u32x4*>(a.img);
-    u32x4* dst = reinterpret_cast<u32x4*>(g_lds);
-    for (uint32_t i = threadIdx.x; i < kLdsBytes / 16; i += blockDim.x) dst[i] = src[i];
-  }
-  __syncthreads();
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t waves_per_block = blockDim.x >> 6;
-  // wave-major over workgroups: the first list ranges land on different CUs/XCDs
-  const uint32_t wave = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * gridDim.x + blockIdx.x);
-  const uint64_t nwaves = (uint64_t)gridDim.x * waves_per_block;
-  const uint64_t per = ((ns + nwaves - 1) / nwaves + S - 1) / S * S;
+  const uint64_t per = group_per<G>(ns, nwaves);
   const uint64_t i0 = (uint64_t)wave * per;
   if (i0 >= ns) return;
   const uint64_t i1 = i0 + per < ns ? i0 + per : ns;
-  const LaneConst k = make_lane_const(lane);
   const uint32_t gi = lane / G;
 #pragma unroll 1
   for (uint64_t i = i0; i < i1; i += S) {
@@ -709,6 +703,26 @@ __global__ __launch_bounds__(1024) void crc32_group_kernel(SweepArgs a) {
     const uint32_t crc = group_crc<G, NB, NT>(a.base, off, len, cin, nbw, lane, k);
     if ((lane & (G - 1)) == 0 && act) a.out[ci] = crc;  // whole chunks: plain stores
   }
+}
+
+// Group kernel: every chunk with 0 < len <= a.small_max (= 16*G*NB), whole, from the
+// plan's compacted list small_idx[0..small_total), 64/G chunks per round (one per group).
+// The sweep kernel skips these chunks (the plan gives them no byte share).
+template <int G, int NB, bool NT>
+__global__ __launch_bounds__(1024) void crc32_group_kernel(SweepArgs a) {
+  const uint64_t ns = *a.small_total;
+  if (ns == 0) return;  // uniform: every wave leaves before the LDS fill
+  {
+    const u32x4* src = reinterpret_cast<const u32x4*>(a.img);
+    u32x4* dst = reinterpret_cast<u32x4*>(g_lds);
+    for (uint32_t i = threadIdx.x; i < kLdsBytes / 16; i += blockDim.x) dst[i] = src[i];
+  }
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u;
+  // wave-major over workgroups: the first list ranges land on different CUs/XCDs
+  const uint32_t wave = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * gridDim.x + blockIdx.x);
+  const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  group_phase<G, NB, NT>(a, ns, wave, nwaves, lane, make_lane_const(lane));
 }
 
 // Largest c in [0, n) with byte_start[c] <= g (byte_start nondecreasing, byte_start[0] = 0).
@@ -742,8 +756,21 @@ __device__ __forceinline__ uint64_t snap_cut(uint64_t cs, uint64_t len, uint64_t
 // as one concatenated stream (byte_start = exclusive scan of len), i.e. an equal share of
 // bytes whatever the chunk-size mix. Each (wave, chunk) intersection is a segment whose
 // raw CRC is shifted to the chunk end and XORed into out[chunk].
-template <int U, bool NT, bool PIPE, bool IL, bool WIN, int DIAG = 0, int LR = 0>
+template <int U, bool NT, bool PIPE, bool IL, bool WIN, int DIAG = 0, int LR = 0, int GG = 0, int GNB = 0>
 __global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
+  // Shares are wave-major over workgroups (share i -> wave i / gridDim.x of workgroup
+  // i % gridDim.x), so when a batch has fewer shares than waves they spread over every
+  // CU. A share is at least kMinShare bytes: a lone large chunk is cut into ~total/16 KiB
+  // segments, not one per wave (each segment ends in an atomic on the chunk's word).
+  const uint32_t waves_per_block = blockDim.x >> 6;
+  const uint64_t nwaves = (uint64_t)gridDim.x * waves_per_block;
+  const uint64_t total = a.byte_start[a.n];
+  uint64_t share = ((total + nwaves - 1) / nwaves + kShareQuantum - 1) & ~uint64_t(kShareQuantum - 1);
+  share = share < kMinShare ? kMinShare : share;
+  // Fused group phase (GG > 0): the workgroup first takes its part of the small-chunk list.
+  const uint64_t ns = GG > 0 ? *a.small_total : 0;
+  const bool grp = GG > 0 && ns > 0 && (uint64_t)blockIdx.x * group_per<(GG > 0 ? GG : 16)>(ns, nwaves) < ns;
+  if ((uint64_t)blockIdx.x * share >= total && !grp) return;  // uniform: no work for this workgroup
   {
     const u32x4* src = reinterpret_cast<const u32x4*>(a.img);
     u32x4* dst = reinterpret_cast<u32x4*>(g_lds);
@@ -752,13 +779,12 @@ __global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
   __syncthreads();
 
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t waves_per_block = blockDim.x >> 6;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * waves_per_block + (threadIdx.x >> 6));
-  const uint64_t nwaves = (uint64_t)gridDim.x * waves_per_block;
-  const uint64_t total = a.byte_start[a.n];
-  const uint64_t share = ((total + nwaves - 1) / nwaves + kShareQuantum - 1) & ~uint64_t(kShareQuantum - 1);
+  const uint32_t wave = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * gridDim.x + blockIdx.x);
+  if constexpr (GG > 0) {
+    if (grp) group_phase<GG, GNB, NT>(a, ns, wave, nwaves, lane, make_lane_const(lane));
+  }
   const uint64_t g0 = (uint64_t)wave * share;
-  if (share == 0 || g0 >= total) return;
+  if (g0 >= total) return;
   const uint64_t g1 = g0 + share < total ? g0 + share : total;
   const uint32_t* xpow2 = a.img + kLdsBytes / 4;
   const LaneConst k = make_lane_const(lane);
@@ -997,7 +1023,8 @@ __global__ void fill_splitmix_kernel(uint8_t* __restrict__ dst, uint64_t nbytes,
 hipError_t launch_plan(const PlanArgs& a, hipStream_t s) {
   const uint32_t blocks = (a.n + kPlanPerBlock - 1) / kPlanPerBlock;
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL(crc32_plan_count_kernel, dim3(blocks), dim3(256), 0, s, a);
+  // one planning block needs no per-block sums (its carry is 0)
+  if (blocks > 1) hipLaunchKernelGGL(crc32_plan_count_kernel, dim3(blocks), dim3(256), 0, s, a);
   hipLaunchKernelGGL(crc32_plan_scan_kernel, dim3(blocks), dim3(256), 0, s, a);
   return hipGetLastError();
 }
@@ -1020,6 +1047,10 @@ hipError_t launch_sweep(const SweepArgs& a, int grid, int variant, hipStream_t s
     case 11: hipLaunchKernelGGL((crc32_sweep_kernel<4, true, true, false, true, 0, 1>), dim3(grid), dim3(1024), 0, s, a); break;
     case 12: hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, false, true, 0, -2>), dim3(grid), dim3(1024), 0, s, a); break;
     case 13: hipLaunchKernelGGL((crc32_sweep_kernel<4, true, true, false, true, 0, -2>), dim3(grid), dim3(1024), 0, s, a); break;
+    // 0 with the group phase fused in (small chunks first, same launch and LDS fill)
+    case 20: hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, true, true, 0, 0, 16, 32>), dim3(grid), dim3(1024), 0, s, a); break;
+    case 21: hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, true, true, 0, 0, 16, 16>), dim3(grid), dim3(1024), 0, s, a); break;
+    case 22: hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, true, true, 0, 0, 16, 64>), dim3(grid), dim3(1024), 0, s, a); break;
     // timing-only diagnostics (wrong CRCs): 100 FOLD lookups removed, 101 no per-segment
     // atomic, 102 no wave tree
     case kDiagNoFold: hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, true, true, 1>), dim3(grid), dim3(1024), 0, s, a); break;

@@ -6,7 +6,7 @@
 //
 // Pipeline (all on the caller's stream):
 //   msg_parse_kernel   one thread per message: header version, header CRC (<= 32 B,
-//                      byte-wise through T0), header constraints, and up to five record
+//                      slice-by-4 through LDS tables), header constraints, and up to five record
 //                      CRC jobs (enc key, properties, update, user metadata, blob) =
 //                      [record start, record end - 8) with the stored big-endian CRC
 //   plan + sweep       the batch CRC engine over the 5m jobs (crc32_kernels.hip)
@@ -27,10 +27,27 @@ __device__ __forceinline__ uint32_t be32(const uint8_t* p) {
 }
 __device__ __forceinline__ uint64_t be64(const uint8_t* p) { return ((uint64_t)be32(p) << 32) | be32(p + 4); }
 
-// T0[b] lives at LDS-image word (b << 8) / 4 (slice table 0, lane column 0).
-__device__ __forceinline__ uint32_t crc_small(const uint8_t* p, uint32_t n, const uint32_t* __restrict__ img) {
+// Slice-by-4 tables T0..T3 (T_j[b] = b advanced over j further zero bytes), 4 KiB, staged
+// into LDS per workgroup from the table image: T_j[b] sits at image byte
+// (j>>1)<<16 | b<<8 | (j&1)<<7 (lane column 0), crc32_layout.h.
+__device__ __forceinline__ void stage_slice_tables(uint32_t* __restrict__ t, const uint32_t* __restrict__ img) {
+  for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) {
+    const uint32_t j = i >> 8, b = i & 255u;
+    t[i] = img[(((j >> 1) << 16) | (b << 8) | ((j & 1) << 7)) >> 2];
+  }
+}
+
+// CRC-32 of n <= 32 header bytes: slice-by-4 over whole words (the loads are independent
+// of the register chain, so they issue together), byte-wise tail.
+__device__ __forceinline__ uint32_t crc_small(const uint8_t* p, uint32_t n, const uint32_t* __restrict__ t) {
   uint32_t c = 0xFFFFFFFFu;
-  for (uint32_t i = 0; i < n; ++i) c = (c >> 8) ^ img[((c ^ p[i]) & 0xffu) << 6];
+  uint32_t i = 0;
+  for (; i + 4 <= n; i += 4) {
+    const uint32_t x = c ^ ((uint32_t)p[i] | ((uint32_t)p[i + 1] << 8) | ((uint32_t)p[i + 2] << 16) |
+                            ((uint32_t)p[i + 3] << 24));
+    c = t[768 + (x & 0xffu)] ^ t[512 + ((x >> 8) & 0xffu)] ^ t[256 + ((x >> 16) & 0xffu)] ^ t[x >> 24];
+  }
+  for (; i < n; ++i) c = (c >> 8) ^ t[(c ^ p[i]) & 0xffu];
   return ~c;
 }
 
@@ -38,6 +55,9 @@ __constant__ uint32_t kRecordBit[5] = {AMBRYCRC_MSG_ENCKEY_CRC, AMBRYCRC_MSG_PRO
                                        AMBRYCRC_MSG_USERMETA_CRC, AMBRYCRC_MSG_BLOB_CRC};
 
 __global__ __launch_bounds__(256) void msg_parse_kernel(MsgArgs a) {
+  __shared__ uint32_t tbl[1024];
+  stage_slice_tables(tbl, a.img);
+  __syncthreads();
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.m) return;
   const uint64_t off = a.msg_off[i];
@@ -64,7 +84,7 @@ __global__ __launch_bounds__(256) void msg_parse_kernel(MsgArgs a) {
       status = AMBRYCRC_MSG_BAD_LAYOUT;
       break;
     }
-    if ((uint64_t)crc_small(p, h - 8, a.img) != be64(p + h - 8)) {  // verifyHeader: nothing else is read
+    if ((uint64_t)crc_small(p, h - 8, tbl) != be64(p + h - 8)) {  // verifyHeader: nothing else is read
       status = AMBRYCRC_MSG_HEADER_CRC;
       break;
     }

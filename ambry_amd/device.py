@@ -117,6 +117,10 @@ def set_variant(device: int, variant: int) -> None:
     check(lib().ambrycrc_set_variant(device, variant), "ambrycrc_set_variant")
 
 
+def get_variant(device: int = 0) -> int:
+    return check(lib().ambrycrc_get_variant(device), "ambrycrc_get_variant")
+
+
 def set_grid(device: int, workgroups: int) -> None:
     check(lib().ambrycrc_set_grid(device, workgroups), "ambrycrc_set_grid")
 

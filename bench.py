@@ -257,7 +257,7 @@ def main():
         "data": "synthetic (device splitmix64 bytes; no dataset)",
         "config": {"workload": desc, "chunks_per_gpu": n, "chunk_bytes": chunk, "bytes_per_gpu_step": total,
                    "parallelism": f"shard{world}" + ("+rccl_allgather" if world > 1 else ""),
-                   "kernel_variant": args.variant if args.variant is not None else 0,
+                   "kernel_variant": D.get_variant(dev.index),
                    "grid_workgroups": D.grid_size(dev.index)},
         "roofline": {
             "bound": "hbm",

@@ -108,21 +108,22 @@ def test_ragged_batch_grid_sizes(gpu, oracle, grid):
     assert np.array_equal(got, oracle.batch(mem, off, ln, threads=8))
 
 
-@pytest.mark.parametrize("variant", list(range(20)))
+@pytest.mark.parametrize("variant", list(range(23)))
 def test_kernel_variants(gpu, oracle, variant):
     rng = np.random.default_rng(100 + variant)
     mem = stream_bytes(6, 0, 16 << 20)
     ln = rng.integers(0, 2 << 20, size=64)
     off = rng.integers(0, (16 << 20) - (2 << 20), size=64)
+    default = gpu.get_variant(0)
     gpu.set_variant(0, variant)
     try:
         got = run_batch(gpu, mem, off, ln)
     finally:
-        gpu.set_variant(0, 0)
+        gpu.set_variant(0, default)
     assert np.array_equal(got, oracle.batch(mem, off, ln, threads=8))
 
 
-@pytest.mark.parametrize("variant", [0, 14, 15, 16, 17, 18, 19])
+@pytest.mark.parametrize("variant", [0, 14, 15, 16, 17, 18, 19, 20, 21, 22])
 @pytest.mark.parametrize("grid", [0, 1, 5])
 def test_small_chunk_group_kernel(gpu, oracle, variant, grid):
     """Group kernel (variants 14-16): whole chunks <= 2/4 KiB, G lanes each, init register
@@ -138,12 +139,13 @@ def test_small_chunk_group_kernel(gpu, oracle, variant, grid):
     off[:16] = np.arange(16)  # chunks in the first bytes of the allocation
     cin = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32)
     cin[::3] = 0
+    default = gpu.get_variant(0)
     gpu.set_variant(0, variant)
     gpu.set_grid(0, grid)
     try:
         got = run_batch(gpu, mem, off, ln, crc_in=cin)
     finally:
-        gpu.set_variant(0, 0)
+        gpu.set_variant(0, default)
         gpu.set_grid(0, 0)
     assert np.array_equal(got, oracle.batch(mem, off, ln, crc_in=cin, threads=8))
 

@@ -26,6 +26,7 @@ def test_model_matches_oracle(model, oracle, nwaves):
     got = model.batch(mem, off, ln, nwaves=nwaves)
     exp = list(oracle.batch(mem, off, ln))
     assert got == exp
+    assert model.batch(mem, off, ln, nwaves=nwaves, min_share=16384, group=(16, 32)) == exp  # kernel defaults
 
 
 @pytest.mark.parametrize("run", [2, 4, -4])

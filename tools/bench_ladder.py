@@ -79,6 +79,7 @@ def gpu_rows(size: int, gib: float, reps: int, variant: int = 0, check: bool = T
     ln = torch.full((n,), size, dtype=torch.int64, device="cuda")
     out = torch.empty(n, dtype=torch.int32, device="cuda")
     ws = torch.empty(D.workspace_bytes(n), dtype=torch.uint8, device="cuda")
+    default = D.get_variant(0)
     D.set_variant(0, variant)
     D.crc32_batch(buf, off, ln, out=out, workspace=ws)
     torch.cuda.synchronize()
@@ -128,7 +129,7 @@ def gpu_rows(size: int, gib: float, reps: int, variant: int = 0, check: bool = T
     torch.cuda.synchronize()
     host_us = (time.perf_counter() - t0) / calls * 1e6
     call = {"us_per_call_stream": round(e0.elapsed_time(e1) / calls * 1e3, 2), "us_per_call_host": round(host_us, 2)}
-    D.set_variant(0, 0)
+    D.set_variant(0, default)
     del buf, off, ln, out, ws
     torch.cuda.empty_cache()
     return batch, call
@@ -140,7 +141,7 @@ def main():
     ap.add_argument("--reps", type=int, default=7)
     ap.add_argument("--no-gpu", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--variants", default="0", help="sweep variants (>= 100: timing diagnostics, no parity)")
+    ap.add_argument("--variants", default="17", help="sweep variants (>= 100: timing diagnostics, no parity)")
     ap.add_argument("--sizes", default=None, help="subset of the ladder, comma separated bytes")
     args = ap.parse_args()
     if not args.no_gpu:
