@@ -111,10 +111,10 @@ struct DevCtx {
   int device = -1;
   int num_cu = 0;
   int grid = 0;
-  // 20: sweep variant 0 (U=8, NT loads, rolling prefetch, 2 pieces interleaved, descriptor
-  // window) with the group phase G16/NB32 fused in for whole chunks <= 8 KiB
-  // (tools/bench_ladder.py, tools/sweep.py)
-  int variant = 20;
+  // 22: sweep variant 0 (U=8, NT loads, rolling prefetch, 2 pieces interleaved, descriptor
+  // window) with the group phase G16/NB64 fused in for whole chunks <= 16 KiB in batches of
+  // >= kGroupMinChunks chunks (tools/bench_ladder.py, tools/sweep.py)
+  int variant = 22;
   uint32_t* d_img = nullptr;
   void* d_ws = nullptr;
   size_t ws_bytes = 0;
@@ -187,6 +187,7 @@ int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uin
                 : c->variant == 21 ? group_small_max(2)
                 : c->variant == 22 ? group_small_max(5)
                                    : group_small_max(group_mode);
+  if (n < kGroupMinChunks) p.small_max = 0;
   hipError_t e = launch_plan(p, s);
   if (e != hipSuccess) return AMBRYCRC_EHIP;
   SweepArgs t;

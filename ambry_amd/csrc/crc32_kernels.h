@@ -15,9 +15,9 @@ struct PlanArgs {
   uint64_t* block_sum;     // [ceil(n / kPlanPerBlock)] scratch
   uint32_t* out;           // [n] initialised here, XOR-accumulated by the sweep kernel
   uint64_t small_max;      // chunks with 0 < len <= small_max go to the group kernel (0: none)
-  uint64_t* block_small;   // [ceil(n / kPlanPerBlock)] scratch
+  uint64_t* block_small;   // [ceil(n / kPlanPerBlock)] scratch: 4 x 16-bit size-class counts
   uint64_t* small_total;   // [1] number of small chunks
-  uint32_t* small_idx;     // [n] their indices, ascending (compacted list for the group kernel)
+  uint32_t* small_idx;     // [n] their indices, grouped by size class, ascending within a class
 };
 
 constexpr uint32_t kPlanPerBlock = 2048;  // chunks per planning workgroup
@@ -42,6 +42,9 @@ struct SweepArgs {
 // 0 = off, 1 = G16/NB8 (2 KiB), 2 = G16/NB16 (4 KiB), 3 = G32/NB8 (4 KiB), 4 = G16/NB32 (8 KiB),
 // 5 = G16/NB64 (16 KiB), 6 = G32/NB32 (16 KiB)
 constexpr int kNumGroupModes = 7;
+// Batches of fewer chunks than this take the sweep (wave mode) for every chunk: with idle
+// waves to spare, 64 lanes per chunk beat a 16-lane group's 4x longer chain on latency.
+constexpr size_t kGroupMinChunks = 16384;
 constexpr uint64_t group_small_max(int mode) {
   return mode == 1 ? 2048u
          : (mode == 2 || mode == 3) ? 4096u

@@ -933,56 +933,102 @@ __device__ __forceinline__ uint64_t share_len(uint64_t len, uint64_t small_max) 
 
 __device__ __forceinline__ bool is_small(uint64_t len, uint64_t small_max) { return len != 0 && len <= small_max; }
 
+// Size class of a small chunk (<= 256 B, 1 KiB, 4 KiB, more): the compacted list is
+// ordered by class, so a group-phase round (64/G consecutive entries) holds chunks of
+// similar length and its chain -- the longest chunk's block count -- wastes little.
+__device__ __forceinline__ uint32_t small_class(uint64_t len) {
+  return len <= 256 ? 0u : len <= 1024 ? 1u : len <= 4096 ? 2u : 3u;
+}
+// Per-chunk class indicator packed as 16-bit fields (a plan block has <= 2048 chunks).
+__device__ __forceinline__ uint64_t class_onehot(uint64_t len, uint64_t small_max) {
+  return is_small(len, small_max) ? (1ull << (16 * small_class(len))) : 0ull;
+}
+__device__ __forceinline__ uint64_t field16(uint64_t v, uint32_t c) { return (v >> (16 * c)) & 0xFFFFu; }
+
 __global__ __launch_bounds__(256) void crc32_plan_count_kernel(PlanArgs a) {
   const uint32_t base = blockIdx.x * kPlanPerBlock;
-  uint64_t sum = 0, nsmall = 0;
+  uint64_t sum = 0, cls = 0;
   for (uint32_t r = 0; r < kPlanPerBlock; r += 256) {
     const uint32_t c = base + r + threadIdx.x;
     if (c < a.n) {
       const uint64_t len = a.len[c];
       sum += share_len(len, a.small_max);
-      nsmall += is_small(len, a.small_max);
+      cls += class_onehot(len, a.small_max);
     }
   }
-  uint64_t total, total_small;
+  uint64_t total, total_cls;
   (void)block_scan256(sum, &total);
-  (void)block_scan256(nsmall, &total_small);
+  (void)block_scan256(cls, &total_cls);
   if (threadIdx.x == 0) {
     a.block_sum[blockIdx.x] = total;
-    a.block_small[blockIdx.x] = total_small;
+    a.block_small[blockIdx.x] = total_cls;  // packed: 4 x 16-bit class counts
   }
 }
 
-__global__ __launch_bounds__(256) void crc32_plan_scan_kernel(PlanArgs a) {
-  uint64_t part = 0, part_small = 0;
-  for (uint32_t i = threadIdx.x; i < blockIdx.x; i += 256) {
-    part += a.block_sum[i];
-    part_small += a.block_small[i];
+// Per-class sum over plan blocks [0, nb) of the packed counts (64-bit per class).
+__device__ __forceinline__ void class_sums(const uint64_t* __restrict__ block_small, uint32_t nb, uint64_t (&out)[4]) {
+  uint64_t part[4] = {0, 0, 0, 0};
+  for (uint32_t i = threadIdx.x; i < nb; i += 256) {
+    const uint64_t v = block_small[i];
+#pragma unroll
+    for (uint32_t c = 0; c < 4; ++c) part[c] += field16(v, c);
   }
-  uint64_t carry, carry_small;
+#pragma unroll
+  for (uint32_t c = 0; c < 4; ++c) (void)block_scan256(part[c], &out[c]);
+}
+
+__global__ __launch_bounds__(256) void crc32_plan_scan_kernel(PlanArgs a) {
+  const uint32_t nblocks = gridDim.x;
+  uint64_t part = 0;
+  for (uint32_t i = threadIdx.x; i < blockIdx.x; i += 256) part += a.block_sum[i];
+  uint64_t carry;
   (void)block_scan256(part, &carry);
-  (void)block_scan256(part_small, &carry_small);
+  // class c's list entries start at base[c] = chunks of classes < c; this block's at base[c] + earlier[c]
+  uint64_t cls_carry[4] = {0, 0, 0, 0}, cls_total[4] = {0, 0, 0, 0};
+  if (a.small_max) {
+    if (nblocks > 1) {
+      class_sums(a.block_small, blockIdx.x, cls_carry);
+      class_sums(a.block_small, nblocks, cls_total);
+    } else {  // no count launch: count this (only) block here
+      uint64_t cls = 0;
+      for (uint32_t r = 0; r < kPlanPerBlock; r += 256) {
+        const uint32_t c = r + threadIdx.x;
+        if (c < a.n) cls += class_onehot(a.len[c], a.small_max);
+      }
+      uint64_t t;
+      (void)block_scan256(cls, &t);
+#pragma unroll
+      for (uint32_t c = 0; c < 4; ++c) cls_total[c] = field16(t, c);
+    }
+  }
+  uint64_t cls_base[4];
+  cls_base[0] = 0;
+  cls_base[1] = cls_total[0];
+  cls_base[2] = cls_base[1] + cls_total[1];
+  cls_base[3] = cls_base[2] + cls_total[2];
   const uint32_t base = blockIdx.x * kPlanPerBlock;
   for (uint32_t r = 0; r < kPlanPerBlock; r += 256) {
     const uint32_t c = base + r + threadIdx.x;
     const uint64_t len = c < a.n ? a.len[c] : 0u;
     const uint64_t v = share_len(len, a.small_max);
-    const uint64_t sm = is_small(len, a.small_max);
-    uint64_t round_total, round_small;
+    const uint64_t oh = c < a.n ? class_onehot(len, a.small_max) : 0ull;
+    uint64_t round_total, round_cls;
     const uint64_t incl = block_scan256(v, &round_total);
-    const uint64_t incl_small = block_scan256(sm, &round_small);
+    const uint64_t incl_cls = block_scan256(oh, &round_cls);
     if (c < a.n) {
       a.byte_start[c] = carry + incl - v;
       a.out[c] = len ? 0u : (a.crc_in ? a.crc_in[c] : 0u);
-      if (sm) a.small_idx[carry_small + incl_small - 1] = c;
-      if (c == a.n - 1) {
-        a.byte_start[a.n] = carry + incl;
-        *a.small_total = carry_small + incl_small;
+      if (oh) {
+        const uint32_t k = small_class(len);
+        a.small_idx[cls_base[k] + cls_carry[k] + field16(incl_cls, k) - 1] = c;
       }
+      if (c == a.n - 1) a.byte_start[a.n] = carry + incl;
     }
     carry += round_total;
-    carry_small += round_small;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) cls_carry[k] += field16(round_cls, k);
   }
+  if (blockIdx.x == 0 && threadIdx.x == 0) *a.small_total = cls_base[3] + cls_total[3];
 }
 
 __global__ void crc32_verify_kernel(const uint32_t* __restrict__ crc, const uint32_t* __restrict__ expected,

@@ -204,10 +204,12 @@ int ambrycrc_range_checksums_host(const uint8_t* file, uint64_t file_len, const 
 /* Kernel variant (0..22; crc32_kernels.h lists them). 0..13: sweep-kernel shapes (blocks in
  * flight per lane, load policy, prefetch scheme, lane runs) for every chunk; 14..19: sweep
  * variant 0 plus a separate group kernel for whole chunks up to 2..16 KiB; 20..22: the
- * group phase fused into the sweep launch (chunks <= 8, 4, 16 KiB). Default 20 = sweep 0
- * (8 blocks in flight per lane, nontemporal loads, rolling prefetch, two pieces' table
- * walks interleaved) with the G16 group phase for whole chunks <= 8 KiB. 100..102 are
- * timing diagnostics that produce wrong CRCs. ambrycrc_get_variant returns the current one. */
+ * group phase fused into the sweep launch (chunks <= 8, 4, 16 KiB). Group modes engage for
+ * batches of >= 16384 chunks; smaller batches take the sweep for every chunk (latency).
+ * Default 22 = sweep 0 (8 blocks in flight per lane, nontemporal loads, rolling prefetch,
+ * two pieces' table walks interleaved) with the G16 group phase for whole chunks <= 16 KiB.
+ * 100..102 are timing diagnostics that produce wrong CRCs. ambrycrc_get_variant returns
+ * the current one. */
 int ambrycrc_set_variant(int device, int variant);
 int ambrycrc_get_variant(int device);
 /* Grid size of the persistent sweep kernel (workgroups; 0 = one per CU). */

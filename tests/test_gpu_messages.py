@@ -33,6 +33,15 @@ def test_region_status_matches_oracle(gpu, seed):
     assert sum(1 for s in st if s) >= 30
 
 
+def test_many_small_messages_group_phase(gpu):
+    """4,000 messages = 20,000 record jobs (>= 16,384): the small records take the group phase."""
+    region, offs, expect = build_region(n=4000, seed=11, corrupt_frac=0.05, big_every=10**9)
+    st, end = run(gpu, region, offs)
+    assert st == [s for s, _ in expect]
+    assert end == [e for _, e in expect]
+    assert sum(1 for s in st if s) >= 150
+
+
 def test_bad_version_truncated_and_out_of_range(gpu):
     region, offs, _ = build_region(n=50, seed=9, corrupt_frac=0.0)
     junk = struct.pack(">h", 7) + bytes(60)  # unknown header version

@@ -124,17 +124,18 @@ def test_kernel_variants(gpu, oracle, variant):
 
 
 @pytest.mark.parametrize("variant", [0, 14, 15, 16, 17, 18, 19, 20, 21, 22])
-@pytest.mark.parametrize("grid", [0, 1, 5])
+@pytest.mark.parametrize("grid", [0, 3])
 def test_small_chunk_group_kernel(gpu, oracle, variant, grid):
-    """Group kernel (variants 14-16): whole chunks <= 2/4 KiB, G lanes each, init register
-    folded into the data. Lengths 0..5000 at every alignment, crc_in, large chunks between."""
+    """Group phase (variants 14-22): whole chunks <= 2..16 KiB, G lanes each, init register
+    folded into the data, size-classed rounds. Lengths 0..20000 at every alignment, crc_in,
+    large chunks between; batches of >= 16384 chunks so the group modes engage."""
     rng = np.random.default_rng(700 + variant * 10 + grid)
     mem = stream_bytes(70 + variant, 0, 8 << 20)
-    n = 5000
+    n = 20000  # >= kGroupMinChunks (16384): group modes engage
     ln = rng.integers(0, 20000 if variant >= 17 else 5000, size=n)
     ln[:46] = list(range(0, 20)) + [255, 256, 257, 511, 512, 513, 2047, 2048, 2049, 4095, 4096, 4097,
                                     1 << 20, 3, 2, 1, 0, 16, 17, 33, 8191, 8192, 8193, 16383, 16384, 16385]
-    ln[::97] = rng.integers(5000, 1 << 20, size=len(ln[::97]))  # large chunks mixed in
+    ln[::397] = rng.integers(5000, 1 << 20, size=len(ln[::397]))  # large chunks mixed in
     off = rng.integers(0, (8 << 20) - (1 << 20), size=n)
     off[:16] = np.arange(16)  # chunks in the first bytes of the allocation
     cin = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32)
