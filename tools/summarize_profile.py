@@ -22,12 +22,22 @@ import shutil
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def pmc_avgs(path, kernel_substr):
-    rows = list(csv.DictReader(open(path)))
-    agg = collections.defaultdict(list)
+def pmc_avgs(path, kernel_substr, size_counter):
+    """Per-counter averages over the kernel's C3-sized dispatches only.
+
+    bench.py also launches the sweep kernel for its clock pre-warm (same size), the CPU-baseline
+    parity check (64 chunks) and the host-path slabs; a dispatch counts when its size_counter
+    value is at least half the largest one seen."""
+    rows = [r for r in csv.DictReader(open(path)) if kernel_substr in r["Kernel_Name"]]
+    per = collections.defaultdict(dict)
     for r in rows:
-        if kernel_substr in r["Kernel_Name"]:
-            agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+        per[r["Dispatch_Id"]][r["Counter_Name"]] = float(r["Counter_Value"])
+    top = max((d.get(size_counter, 0.0) for d in per.values()), default=0.0)
+    keep = [d for d in per.values() if d.get(size_counter, 0.0) >= 0.5 * top]
+    agg = collections.defaultdict(list)
+    for d in keep:
+        for k, v in d.items():
+            agg[k].append(v)
     return {k: sum(v) / len(v) for k, v in agg.items()}, {k: len(v) for k, v in agg.items()}
 
 
@@ -44,17 +54,28 @@ def main():
                 os.path.join(out, f"{args.tag}_kernel_stats.csv"))
     summary = {"kernel": args.kernel, "passes": {}}
     counters = {}
-    for name in ("prof_fetch", "prof_write", "prof_sq"):
+    for name, size_counter in (("prof_fetch", "FETCH_SIZE"), ("prof_write", "WRITE_SIZE"),
+                               ("prof_sq", "GRBM_GUI_ACTIVE")):
         p = os.path.join(args.src, name, "pmc_counter_collection.csv")
         if os.path.exists(p):
-            avg, cnt = pmc_avgs(p, args.kernel)
+            avg, cnt = pmc_avgs(p, args.kernel, size_counter)
             summary["passes"][name] = {"avg": avg, "dispatches": cnt}
             counters.update(avg)
     with open(os.path.join(args.src, "prof_kt", "kt_kernel_stats.csv")) as f:
         for r in csv.DictReader(f):
             if args.kernel in r["Name"]:
-                summary["kernel_trace"] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
-                                           "min_ns": float(r["MinNs"]), "max_ns": float(r["MaxNs"])}
+                summary["kernel_trace_all_dispatches"] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
+                                                          "min_ns": float(r["MinNs"]), "max_ns": float(r["MaxNs"])}
+    # C3-sized dispatches (>= half the longest): pre-warm + warmup + timed steps
+    trace = os.path.join(args.src, "prof_kt", "kt_kernel_trace.csv")
+    if os.path.exists(trace):
+        d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(open(trace))
+             if args.kernel in r["Kernel_Name"]]
+        big = sorted(x for x in d if x >= 0.5 * max(d))
+        summary["kernel_trace"] = {"calls": len(big), "avg_ns": sum(big) / len(big), "median_ns": big[len(big) // 2],
+                                   "min_ns": big[0], "max_ns": big[-1],
+                                   "selection": "sweep dispatches >= 0.5 x the longest (C3-sized)"}
+
     if "FETCH_SIZE" in counters:
         hbm = (2 * counters["FETCH_SIZE"] + counters.get("WRITE_SIZE", 0.0)) * 1024
         summary["hbm_bytes_per_launch"] = hbm
