@@ -25,6 +25,7 @@
 #include <stddef.h>
 #include <string.h>
 #include <pthread.h>
+#include <zlib.h>
 
 #define ORACLE_POLY 0xEDB88320u
 
@@ -174,9 +175,31 @@ static void* batch_worker(void* arg) {
   return NULL;
 }
 
+/* The same batch through the system zlib's crc32_z (1.2.11 here): the function
+ * java.util.zip.CRC32 wraps, timed as the second CPU baseline SURVEY.md §8d asks for. */
+static void* zlib_worker(void* arg) {
+  batch_job_t* j = (batch_job_t*)arg;
+  for (size_t i = j->lo; i < j->hi; ++i)
+    j->out[i] = (uint32_t)crc32_z(j->crc_in ? j->crc_in[i] : 0u, j->base + j->off[i], (z_size_t)j->len[i]);
+  return NULL;
+}
+
+static int run_batch(void* (*worker)(void*), const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                     const uint32_t* crc_in, uint32_t* out, size_t n, int threads);
+
+int oracle_zlib_batch(const uint8_t* base, const uint64_t* off, const uint64_t* len, const uint32_t* crc_in,
+                      uint32_t* out, size_t n, int threads) {
+  return run_batch(zlib_worker, base, off, len, crc_in, out, n, threads);
+}
+
 int oracle_crc32_batch(const uint8_t* base, const uint64_t* off, const uint64_t* len,
                        const uint32_t* crc_in, uint32_t* out, size_t n, int threads) {
   ensure_tables();
+  return run_batch(batch_worker, base, off, len, crc_in, out, n, threads);
+}
+
+static int run_batch(void* (*worker)(void*), const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                     const uint32_t* crc_in, uint32_t* out, size_t n, int threads) {
   if (threads < 1) threads = 1;
   if (threads > 256) threads = 256;
   pthread_t tid[256];
@@ -188,9 +211,9 @@ int oracle_crc32_batch(const uint8_t* base, const uint64_t* off, const uint64_t*
     if (lo >= hi) break;
     jobs[t] = (batch_job_t){base, off, len, crc_in, out, lo, hi};
     if (threads == 1) {
-      batch_worker(&jobs[t]);
+      worker(&jobs[t]);
     } else {
-      if (pthread_create(&tid[t], NULL, batch_worker, &jobs[t]) != 0) return -1;
+      if (pthread_create(&tid[t], NULL, worker, &jobs[t]) != 0) return -1;
       started++;
     }
   }

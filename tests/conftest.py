@@ -68,6 +68,8 @@ class Oracle:
         L.oracle_crc32_batch.restype = ctypes.c_int
         L.oracle_crc32_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        L.oracle_zlib_batch.restype = ctypes.c_int
+        L.oracle_zlib_batch.argtypes = L.oracle_crc32_batch.argtypes
         self.L = L
 
     @staticmethod
@@ -89,7 +91,8 @@ class Oracle:
     def combine(self, c1, c2, len2):
         return self.L.oracle_crc32_combine(c1, c2, len2)
 
-    def batch(self, mem, off, length, crc_in=None, threads=1):
+    def batch(self, mem, off, length, crc_in=None, threads=1, zlib=False):
+        """Per-chunk CRCs on the CPU: the Crc32.java restatement, or (zlib=True) the system zlib."""
         import numpy as np
 
         mem = np.ascontiguousarray(mem)
@@ -97,7 +100,8 @@ class Oracle:
         length = np.ascontiguousarray(length, dtype=np.uint64)
         out = np.zeros(len(off), dtype=np.uint32)
         cin = None if crc_in is None else np.ascontiguousarray(crc_in, dtype=np.uint32)
-        rc = self.L.oracle_crc32_batch(mem.ctypes.data_as(ctypes.c_void_p), off.ctypes.data_as(ctypes.c_void_p),
+        fn = self.L.oracle_zlib_batch if zlib else self.L.oracle_crc32_batch
+        rc = fn(mem.ctypes.data_as(ctypes.c_void_p), off.ctypes.data_as(ctypes.c_void_p),
                                        length.ctypes.data_as(ctypes.c_void_p),
                                        None if cin is None else cin.ctypes.data_as(ctypes.c_void_p),
                                        out.ctypes.data_as(ctypes.c_void_p), len(off), threads)

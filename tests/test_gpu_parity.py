@@ -266,6 +266,36 @@ def test_c3_full_size(gpu, oracle):
     _full_size_check(gpu, oracle, 8192, 4 << 20, 0xC3, sample=12)
 
 
+def test_c4_full_size_verify(gpu, oracle):
+    """C4 as SURVEY.md §8d defines it: 32,768 Zipf(1.2) chunks of 4 KiB-4 MiB (9.21 GiB) packed at
+    16-B offsets, expected CRCs from the CPU oracle over every chunk, single-bit flips injected
+    into 1 % of the chunks on the device; the mismatch flags must name exactly those chunks."""
+    torch = _torch()
+    sizes = zipf_sizes(32768)
+    off = np.concatenate([[0], np.cumsum((sizes + 15) // 16 * 16)[:-1]]).astype(np.int64)
+    total = int(off[-1] + sizes[-1])
+    buf = torch.empty(total, dtype=torch.uint8, device="cuda")
+    gpu.fill_random(buf, 0xC4, 0)
+    torch.cuda.synchronize()
+    expected = oracle.batch(buf.cpu().numpy(), off, sizes, threads=16)  # oracle over every chunk
+    rng = np.random.default_rng(0xC4)
+    bad = np.sort(rng.choice(len(sizes), size=len(sizes) // 100, replace=False))
+    pos = off[bad] + (rng.random(len(bad)) * sizes[bad]).astype(np.int64)
+    bits = torch.from_numpy((1 << rng.integers(0, 8, size=len(bad))).astype(np.uint8)).cuda()
+    pos_t = torch.from_numpy(pos).cuda()
+    buf[pos_t] ^= bits
+    exp_dev = torch.from_numpy(expected.view(np.int32)).cuda()
+    crc, mism, count = gpu.crc32_verify(buf, dev_u64(off), dev_u64(sizes), exp_dev)
+    torch.cuda.synchronize()
+    flags = mism.cpu().numpy()
+    assert np.array_equal(np.nonzero(flags)[0], bad)
+    assert int(count.item()) == len(bad)
+    good = np.ones(len(sizes), dtype=bool)
+    good[bad] = False
+    assert np.array_equal(host_u32(crc)[good], expected[good])
+    del buf
+
+
 def test_host_resident_path(gpu, oracle):
     """ambrycrc_batch_host: pageable and pinned inputs, including a chunk larger than one staging slab."""
     torch = _torch()

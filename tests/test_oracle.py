@@ -93,3 +93,21 @@ def test_batch_threads(oracle):
     exp = [zlib.crc32(mem[o:o + n].tobytes()) for o, n in zip(off, ln)]
     for th in (1, 3):
         assert list(oracle.batch(mem, off, ln, threads=th)) == exp
+
+
+def test_zlib_batch_matches_restatement(oracle):
+    """oracle_zlib_batch (system zlib crc32_z, the java.util.zip.CRC32 stand-in timed by bench.py's
+    cpu_baseline) and the Crc32.java restatement agree chunk for chunk, with and without crc_in."""
+    import numpy as np
+
+    from datagen import stream_bytes
+
+    rng = np.random.default_rng(5)
+    mem = stream_bytes(8, 0, 1 << 20)
+    ln = rng.integers(0, 70000, size=200)
+    off = rng.integers(0, (1 << 20) - 70000, size=200)
+    cin = rng.integers(0, 1 << 32, size=200, dtype=np.uint64).astype(np.uint32)
+    for c in (None, cin):
+        for th in (1, 4):
+            assert np.array_equal(oracle.batch(mem, off, ln, crc_in=c, threads=th, zlib=True),
+                                  oracle.batch(mem, off, ln, crc_in=c, threads=th))
