@@ -185,7 +185,7 @@ int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uin
   const int group_mode = grouped ? c->variant - 13 : 0;
   p.small_max = c->variant == 20   ? group_small_max(4)
                 : c->variant == 21 ? group_small_max(2)
-                : c->variant == 22 ? group_small_max(5)
+                : c->variant == 22 || c->variant == 23 ? group_small_max(5)
                                    : group_small_max(group_mode);
   if (n < kGroupMinChunks) p.small_max = 0;
   hipError_t e = launch_plan(p, s);

@@ -61,7 +61,8 @@ constexpr uint64_t group_small_max(int mode) {
 // 11 R=2 strided (U4), 12 64-B runs by quad transpose of coalesced loads (U8), 13 same (U4)
 // 14..19 = 0 plus the group kernel (modes 1..6) for small whole chunks; 20, 21, 22 = 0 with the
 // group phase (G16/NB32, G16/NB16, G16/NB64: chunks <= 8, 4, 16 KiB) fused into the sweep launch
-constexpr int kNumVariants = 23;
+// 23 = 13 (quad-transposed 64-B lane runs, U4) with the G16/NB64 group phase fused in
+constexpr int kNumVariants = 24;
 constexpr int kDiagNoFold = 100;  // diagnostic timing build, selectable via ambrycrc_set_variant only
 
 // Message verify (message_kernels.hip): kMsgSlots CRC jobs per message, slot order

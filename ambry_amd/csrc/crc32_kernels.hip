@@ -1097,6 +1097,8 @@ hipError_t launch_sweep(const SweepArgs& a, int grid, int variant, hipStream_t s
     case 20: hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, true, true, 0, 0, 16, 32>), dim3(grid), dim3(1024), 0, s, a); break;
     case 21: hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, true, true, 0, 0, 16, 16>), dim3(grid), dim3(1024), 0, s, a); break;
     case 22: hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, true, true, 0, 0, 16, 64>), dim3(grid), dim3(1024), 0, s, a); break;
+    // 13 (64-B lane runs by quad transpose, U4) with the G16/NB64 group phase fused in
+    case 23: hipLaunchKernelGGL((crc32_sweep_kernel<4, true, true, false, true, 0, -2, 16, 64>), dim3(grid), dim3(1024), 0, s, a); break;
     // timing-only diagnostics (wrong CRCs): 100 FOLD lookups removed, 101 no per-segment
     // atomic, 102 no wave tree
     case kDiagNoFold: hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, true, true, 1>), dim3(grid), dim3(1024), 0, s, a); break;
