@@ -8,6 +8,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -88,8 +91,12 @@ std::vector<uint32_t> build_table_image() {
 
 // ------------------------------------------------------------ contexts
 constexpr int kMaxDevices = 64;
-constexpr size_t kSlabBytes = 256ull << 20;   // host-path staging slab
-constexpr size_t kSlabChunks = 1u << 16;      // max chunk pieces per slab
+// Host path: a ring of kSlabs staging slabs per device. Up to kSlabs-1 slabs are in
+// flight (H2D copy, kernels, D2H of CRCs on the slab's stream) while the host fills
+// the next one; 64 MiB keeps the pipeline's fill and drain short (1.2 ms at PCIe rate).
+constexpr int kSlabs = 4;
+constexpr size_t kSlabBytes = 64ull << 20;    // host-path staging slab
+constexpr size_t kSlabChunks = 1u << 14;      // max chunk pieces per slab
 
 struct EventPair {
   hipEvent_t a, b;
@@ -121,7 +128,7 @@ struct DevCtx {
   bool timing = false;
   std::vector<EventPair> pending, free_events;
   bool slabs_ready = false;
-  HostSlab slab[2];
+  HostSlab slab[kSlabs];
   std::mutex mu;  // guards ws growth, events, slabs
 };
 
@@ -129,6 +136,132 @@ std::mutex g_mu;
 DevCtx* g_ctx[kMaxDevices] = {nullptr};
 
 int hip_err(hipError_t e) { return e == hipSuccess ? AMBRYCRC_OK : AMBRYCRC_EHIP; }
+
+// ------------------------------------------------------------ staging copy pool
+// Pageable host chunks (a Netty direct ByteBuf, a FileChannel read buffer) must be
+// memcpy'd into a pinned slab before the DMA engine can move them. One core copies
+// ~25 GB/s, half of PCIe Gen5 x16, so the slab fill is split over a few worker
+// threads (AMBRYCRC_COPY_THREADS, default 8; 1 disables the pool). Process-wide,
+// started on first use; jobs from concurrent callers interleave safely.
+class CopyPool {
+ public:
+  static CopyPool& get() {
+    static CopyPool pool;
+    return pool;
+  }
+  int threads() const { return nthreads_; }
+  // Runs fn(0..parts-1) across the workers and the calling thread; returns when all are done.
+  void run(int parts, const std::function<void(int)>& fn) {
+    if (parts <= 1 || workers_.empty()) {
+      for (int i = 0; i < parts; ++i) fn(i);
+      return;
+    }
+    Batch b{&fn, parts};
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (int i = 1; i < parts; ++i) queue_.push_back({&b, i});
+    }
+    cv_.notify_all();
+    fn(0);
+    finish_one(b);
+    // help with this batch's remaining parts instead of idling
+    for (;;) {
+      Job j{nullptr, 0};
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        for (size_t q = 0; q < queue_.size(); ++q)
+          if (queue_[q].batch == &b) {
+            j = queue_[q];
+            queue_.erase(queue_.begin() + q);
+            break;
+          }
+      }
+      if (!j.batch) break;
+      (*j.batch->fn)(j.part);
+      finish_one(b);
+    }
+    std::unique_lock<std::mutex> lk(b.mu);
+    b.cv.wait(lk, [&] { return b.left == 0; });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : workers_) t.join();
+  }
+
+ private:
+  struct Batch {
+    const std::function<void(int)>* fn;
+    int left;
+    std::mutex mu;
+    std::condition_variable cv;
+  };
+  struct Job {
+    Batch* batch;
+    int part;
+  };
+  CopyPool() {
+    int t = 8;
+    if (const char* e = getenv("AMBRYCRC_COPY_THREADS")) t = atoi(e);
+    nthreads_ = std::max(1, std::min(t, 64));
+    for (int i = 1; i < nthreads_; ++i) workers_.emplace_back([this] { loop(); });
+  }
+  static void finish_one(Batch& b) {
+    std::lock_guard<std::mutex> g(b.mu);
+    if (--b.left == 0) b.cv.notify_all();
+  }
+  void loop() {
+    for (;;) {
+      Job j;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || !queue_.empty(); });
+        if (stop_ && queue_.empty()) return;
+        j = queue_.front();
+        queue_.erase(queue_.begin());
+      }
+      (*j.batch->fn)(j.part);
+      finish_one(*j.batch);
+    }
+  }
+  int nthreads_ = 1;
+  std::vector<std::thread> workers_;
+  std::vector<Job> queue_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  bool stop_ = false;
+};
+
+struct CopyJob {
+  uint8_t* dst;
+  const uint8_t* src;
+  uint64_t n;
+};
+
+// Copies the jobs (disjoint destinations) with the pool: the slab's bytes are split into
+// `parts` equal ranges, each thread copying its range of every job it overlaps.
+void parallel_copy(const std::vector<CopyJob>& jobs, uint64_t total) {
+  if (jobs.empty()) return;
+  CopyPool& pool = CopyPool::get();
+  const int parts = (int)std::min<uint64_t>((uint64_t)pool.threads(), std::max<uint64_t>(1, total >> 20));
+  if (parts <= 1) {
+    for (const CopyJob& j : jobs) memcpy(j.dst, j.src, j.n);
+    return;
+  }
+  std::vector<uint64_t> start(jobs.size() + 1, 0);
+  for (size_t i = 0; i < jobs.size(); ++i) start[i + 1] = start[i] + jobs[i].n;
+  pool.run(parts, [&](int p) {
+    const uint64_t lo = total * (uint64_t)p / (uint64_t)parts, hi = total * (uint64_t)(p + 1) / (uint64_t)parts;
+    size_t i = std::upper_bound(start.begin(), start.end(), lo) - start.begin() - 1;
+    for (; i < jobs.size() && start[i] < hi; ++i) {
+      const uint64_t a = std::max(lo, start[i]), b = std::min(hi, start[i + 1]);
+      if (b > a) memcpy(jobs[i].dst + (a - start[i]), jobs[i].src + (a - start[i]), b - a);
+    }
+  });
+}
 
 DevCtx* ctx_for(int device) {
   if (device < 0 || device >= kMaxDevices) return nullptr;
@@ -441,8 +574,9 @@ int ambrycrc_batch_host(const void* const* ptrs, const uint64_t* lens, const uin
 
   size_t ci = 0;
   uint64_t cpos = 0;
-  int k = 0;
-  std::vector<Piece> inflight[2];
+  int k = 0;  // slabs issued; slab k uses ring entry k % kSlabs
+  std::vector<Piece> inflight[kSlabs];
+  std::vector<CopyJob> copies;
   auto drain = [&](int which) -> int {
     HostSlab& s = c->slab[which];
     if (inflight[which].empty()) return AMBRYCRC_OK;
@@ -455,12 +589,13 @@ int ambrycrc_batch_host(const void* const* ptrs, const uint64_t* lens, const uin
     return AMBRYCRC_OK;
   };
   while (ci < n) {
-    const int w = k & 1;
-    rc = drain(w);  // the slab we are about to refill
+    const int w = k % kSlabs;
+    rc = drain(w);  // the oldest slab in flight: the one we are about to refill
     if (rc) break;
     HostSlab& s = c->slab[w];
     uint64_t used = 0;
     size_t np = 0;
+    copies.clear();
     while (ci < n && np < kSlabChunks) {
       const uint64_t rem = lens[ci] - cpos;
       const uint64_t room = kSlabBytes - used;
@@ -477,7 +612,7 @@ int ambrycrc_batch_host(const void* const* ptrs, const uint64_t* lens, const uin
           break;
         }
       } else if (take) {
-        memcpy(s.h_data + used, src, take);
+        copies.push_back({s.h_data + used, src, take});
       }
       s.h_meta[np] = used;
       s.h_meta[kSlabChunks + np] = take;
@@ -492,14 +627,20 @@ int ambrycrc_batch_host(const void* const* ptrs, const uint64_t* lens, const uin
       if (used >= kSlabBytes) break;
     }
     if (rc) break;
-    if (!pinned && used &&
-        hipMemcpyAsync(s.d_data, s.h_data, std::min<uint64_t>(used, kSlabBytes), hipMemcpyHostToDevice, s.stream) !=
-            hipSuccess) {
-      rc = AMBRYCRC_EHIP;
-      break;
+    if (!pinned && used) {
+      uint64_t bytes = 0;
+      for (const CopyJob& j : copies) bytes += j.n;
+      parallel_copy(copies, bytes);  // overlaps the DMA of the slabs already issued
+      if (hipMemcpyAsync(s.d_data, s.h_data, std::min<uint64_t>(used, kSlabBytes), hipMemcpyHostToDevice,
+                         s.stream) != hipSuccess) {
+        rc = AMBRYCRC_EHIP;
+        break;
+      }
     }
-    if (hipMemcpyAsync(s.d_meta, s.h_meta, 2 * kSlabChunks * sizeof(uint64_t), hipMemcpyHostToDevice, s.stream) !=
-        hipSuccess) {
+    if (hipMemcpyAsync(s.d_meta, s.h_meta, np * sizeof(uint64_t), hipMemcpyHostToDevice, s.stream) !=
+            hipSuccess ||
+        hipMemcpyAsync(s.d_meta + kSlabChunks, s.h_meta + kSlabChunks, np * sizeof(uint64_t),
+                       hipMemcpyHostToDevice, s.stream) != hipSuccess) {
       rc = AMBRYCRC_EHIP;
       break;
     }
@@ -512,12 +653,16 @@ int ambrycrc_batch_host(const void* const* ptrs, const uint64_t* lens, const uin
     }
     ++k;
   }
-  int rc2 = drain(k & 1);  // older slab first: pieces must combine in order
-  int rc3 = drain((k + 1) & 1);
+  // Oldest slab first: pieces of one chunk must combine in order. On error, still wait
+  // for everything issued so no DMA targets a slab the next call refills.
+  int rc2 = AMBRYCRC_OK;
+  for (int d = 0; d < kSlabs; ++d) {
+    const int r = drain((k + d) % kSlabs);
+    if (!rc2) rc2 = r;
+  }
   (void)hipSetDevice(prev);
   if (rc) return rc;
   if (rc2) return rc2;
-  if (rc3) return rc3;
   for (size_t i = 0; i < n; ++i) out[i] = acc[i];
   return AMBRYCRC_OK;
 }
