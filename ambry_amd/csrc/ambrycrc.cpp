@@ -118,10 +118,12 @@ struct DevCtx {
   int device = -1;
   int num_cu = 0;
   int grid = 0;
-  // 22: sweep variant 0 (U=8, NT loads, rolling prefetch, 2 pieces interleaved, descriptor
-  // window) with the group phase G16/NB64 fused in for whole chunks <= 16 KiB in batches of
-  // >= kGroupMinChunks chunks (tools/bench_ladder.py, tools/sweep.py)
-  int variant = 22;
+  // 25: 64-B lane runs (four coalesced 1 KiB loads per 4 KiB super-block, quad transpose by
+  // v_cndmask_b32_dpp, one x^(8*4096) fold per 64 B), U4 loads in flight, with the group
+  // phase G16/NB64 fused in for whole chunks <= 16 KiB in batches of >= kGroupMinChunks
+  // chunks. On C3 it beat 23 (the same with separate DPP moves and selects) by 1.2-1.9 %
+  // and 22 (16-B pieces, fold per piece) by 2-5 % (tools/sweep.py; profiles/r01d_*).
+  int variant = 25;
   uint32_t* d_img = nullptr;
   void* d_ws = nullptr;
   size_t ws_bytes = 0;
@@ -318,7 +320,7 @@ int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uin
   const int group_mode = grouped ? c->variant - 13 : 0;
   p.small_max = c->variant == 20   ? group_small_max(4)
                 : c->variant == 21 ? group_small_max(2)
-                : c->variant == 22 || c->variant == 23 ? group_small_max(5)
+                : c->variant >= 22 ? group_small_max(5)
                                    : group_small_max(group_mode);
   if (n < kGroupMinChunks) p.small_max = 0;
   hipError_t e = launch_plan(p, s);

@@ -62,7 +62,11 @@ constexpr uint64_t group_small_max(int mode) {
 // 14..19 = 0 plus the group kernel (modes 1..6) for small whole chunks; 20, 21, 22 = 0 with the
 // group phase (G16/NB32, G16/NB16, G16/NB64: chunks <= 8, 4, 16 KiB) fused into the sweep launch
 // 23 = 13 (quad-transposed 64-B lane runs, U4) with the G16/NB64 group phase fused in
-constexpr int kNumVariants = 24;
+// 24 = 12 (quad-transposed 64-B lane runs, U8) with the G16/NB64 group phase fused in
+// (8 waves per CU with 256 VGPRs and U8/U16 prefetch lost 3-14 % to these at 16 waves: the
+// 4 waves per SIMD hide the LDS chains better; the TPB template parameter is kept)
+// 25 = 23 with the quad transposes' lane selects fused into DPP moves (v_cndmask_b32_dpp)
+constexpr int kNumVariants = 26;
 constexpr int kDiagNoFold = 100;  // diagnostic timing build, selectable via ambrycrc_set_variant only
 
 // Message verify (message_kernels.hip): kMsgSlots CRC jobs per message, slot order

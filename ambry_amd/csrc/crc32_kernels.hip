@@ -425,6 +425,45 @@ __device__ __forceinline__ void quad_transpose(u32x4 (&x)[4], uint32_t lane) {
   }
 }
 
+// The same transpose with the lane selects fused into the DPP moves: v_cndmask_b32_dpp
+// computes vcc ? src1 : dpp(src0), so each stage is 4 VALU ops per dword instead of 4 DPP
+// moves + 4 v_cndmask_b32_e64 (the compiler cannot fuse them: its selects take the lane
+// mask from an SGPR pair, the VOP3 form, which has no DPP encoding on gfx9). 8 VALU per
+// dword per transpose instead of 16. s_nop 1 on entry and exit covers the gfx9 hazard of
+// a DPP read within 2 wait states of the VALU write of its source.
+__device__ __forceinline__ void quad_transpose_asm(u32x4 (&x)[4]) {
+  const uint64_t m1 = 0xAAAAAAAAAAAAAAAAull, n1 = 0x5555555555555555ull;  // lane & 1 set / clear
+  const uint64_t m2 = 0xCCCCCCCCCCCCCCCCull, n2 = 0x3333333333333333ull;  // lane & 2 set / clear
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    uint32_t a0, a1, a2, a3, y0, y1, y2, y3;
+    asm volatile(
+        "s_nop 1\n\t"
+        "s_mov_b64 vcc, %[n1]\n\t"
+        "v_cndmask_b32_dpp %[a0], %[x1], %[x0], vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_cndmask_b32_dpp %[a2], %[x3], %[x2], vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "s_mov_b64 vcc, %[m1]\n\t"
+        "v_cndmask_b32_dpp %[a1], %[x0], %[x1], vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_cndmask_b32_dpp %[a3], %[x2], %[x3], vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "s_mov_b64 vcc, %[n2]\n\t"
+        "v_cndmask_b32_dpp %[y0], %[a2], %[a0], vcc quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_cndmask_b32_dpp %[y1], %[a3], %[a1], vcc quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "s_mov_b64 vcc, %[m2]\n\t"
+        "v_cndmask_b32_dpp %[y2], %[a0], %[a2], vcc quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_cndmask_b32_dpp %[y3], %[a1], %[a3], vcc quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1"
+        : [a0] "=&v"(a0), [a1] "=&v"(a1), [a2] "=&v"(a2), [a3] "=&v"(a3), [y0] "=&v"(y0), [y1] "=&v"(y1),
+          [y2] "=&v"(y2), [y3] "=&v"(y3)
+        : [x0] "v"(x[0][d]), [x1] "v"(x[1][d]), [x2] "v"(x[2][d]), [x3] "v"(x[3][d]), [m1] "s"(m1), [n1] "s"(n1),
+          [m2] "s"(m2), [n2] "s"(n2)
+        : "vcc");
+    x[0][d] = y0;
+    x[1][d] = y1;
+    x[2][d] = y2;
+    x[3][d] = y3;
+  }
+}
+
 template <int BIT, int POWK>
 __device__ __forceinline__ uint32_t tree_level_t4(uint32_t s, uint32_t lane) {
   uint32_t o;
@@ -437,7 +476,13 @@ __device__ __forceinline__ uint32_t tree_level_t4(uint32_t s, uint32_t lane) {
   return (lane & (1u << BIT)) ? (s ^ sh) : s;
 }
 
-template <int UB, bool NT>
+template <bool ASMT>
+__device__ __forceinline__ void qt(u32x4 (&x)[4], uint32_t lane) {
+  if constexpr (ASMT) quad_transpose_asm(x);
+  else quad_transpose(x, lane);
+}
+
+template <int UB, bool NT, bool ASMT = false>
 __device__ __forceinline__ uint32_t body_crc_t4(const uint8_t* __restrict__ base, uint64_t bs, uint64_t be,
                                                 uint32_t lane, const LaneConst& k) {
   constexpr uint64_t SB = 4 * (uint64_t)kBlockBytes;
@@ -463,7 +508,7 @@ __device__ __forceinline__ uint32_t body_crc_t4(const uint8_t* __restrict__ base
       }
     }
   }
-  quad_transpose(x, lane);
+  qt<ASMT>(x, lane);
   uint32_t s = run_crc<4>(x, k, 0u);
   const u32x4* q = reinterpret_cast<const u32x4*>(base + v0) + lane;  // super-block b, block i: q[b*256 + i*64]
   uint64_t b = 1;
@@ -482,13 +527,13 @@ __device__ __forceinline__ uint32_t body_crc_t4(const uint8_t* __restrict__ base
           cur[i] = buf[u][i];
           buf[u][i] = ld16<NT>(q + (b + UB + u) * 256 + i * 64);
         }
-        quad_transpose(cur, lane);
+        qt<ASMT>(cur, lane);
         s = run_crc<4>(cur, k, nib_mul(s, kFold));
       }
     }
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
-      quad_transpose(buf[u], lane);
+      qt<ASMT>(buf[u], lane);
       s = run_crc<4>(buf[u], k, nib_mul(s, kFold));
     }
     b += UB;
@@ -497,7 +542,7 @@ __device__ __forceinline__ uint32_t body_crc_t4(const uint8_t* __restrict__ base
     u32x4 cur[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) cur[i] = ld16<NT>(q + b * 256 + i * 64);
-    quad_transpose(cur, lane);
+    qt<ASMT>(cur, lane);
     s = run_crc<4>(cur, k, nib_mul(s, kFold));
   }
   s = tree_level_t4<2, 6>(s, lane);
@@ -756,8 +801,9 @@ __device__ __forceinline__ uint64_t snap_cut(uint64_t cs, uint64_t len, uint64_t
 // as one concatenated stream (byte_start = exclusive scan of len), i.e. an equal share of
 // bytes whatever the chunk-size mix. Each (wave, chunk) intersection is a segment whose
 // raw CRC is shifted to the chunk end and XORed into out[chunk].
-template <int U, bool NT, bool PIPE, bool IL, bool WIN, int DIAG = 0, int LR = 0, int GG = 0, int GNB = 0>
-__global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
+template <int U, bool NT, bool PIPE, bool IL, bool WIN, int DIAG = 0, int LR = 0, int GG = 0, int GNB = 0,
+          int TPB = 1024>
+__global__ __launch_bounds__(TPB) void crc32_sweep_kernel(SweepArgs a) {
   // Shares are wave-major over workgroups (share i -> wave i / gridDim.x of workgroup
   // i % gridDim.x), so when a batch has fewer shares than waves they spread over every
   // CU. A share is at least kMinShare bytes: a lone large chunk is cut into ~total/16 KiB
@@ -807,7 +853,7 @@ __global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
     uint32_t r = 0;
     if (sa < be) {
       if constexpr (LR < 0) {
-        r = body_crc_t4<(U >> 2) < 1 ? 1 : (U >> 2), NT>(a.base, sa, be, lane, k);
+        r = body_crc_t4<(U >> 2) < 1 ? 1 : (U >> 2), NT, LR == -3>(a.base, sa, be, lane, k);
       } else if constexpr (LR > 0) {
         r = body_crc_runs<(U >> LR) < 1 ? 1 : (U >> LR), NT, LR>(a.base, sa, be, lane, k);
       } else {
@@ -1099,6 +1145,9 @@ hipError_t launch_sweep(const SweepArgs& a, int grid, int variant, hipStream_t s
     case 22: hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, true, true, 0, 0, 16, 64>), dim3(grid), dim3(1024), 0, s, a); break;
     // 13 (64-B lane runs by quad transpose, U4) with the G16/NB64 group phase fused in
     case 23: hipLaunchKernelGGL((crc32_sweep_kernel<4, true, true, false, true, 0, -2, 16, 64>), dim3(grid), dim3(1024), 0, s, a); break;
+    case 24: hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, false, true, 0, -2, 16, 64>), dim3(grid), dim3(1024), 0, s, a); break;
+    // 23 with the transposes' selects fused into the DPP moves (v_cndmask_b32_dpp)
+    case 25: hipLaunchKernelGGL((crc32_sweep_kernel<4, true, true, false, true, 0, -3, 16, 64>), dim3(grid), dim3(1024), 0, s, a); break;
     // timing-only diagnostics (wrong CRCs): 100 FOLD lookups removed, 101 no per-segment
     // atomic, 102 no wave tree
     case kDiagNoFold: hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, true, true, 1>), dim3(grid), dim3(1024), 0, s, a); break;
@@ -1177,6 +1226,35 @@ __global__ __launch_bounds__(1024) void readbw_tiles_kernel(const uint8_t* __res
   out[blockIdx.x * blockDim.x + threadIdx.x] = x;
 }
 
+// Contiguous per-wave shares (the sweep's layout: share = nbytes / waves, in 1 KiB
+// blocks), optionally entered at a wave-dependent rotation so concurrent waves sit at
+// different offsets of their shares (probes for channel/bank hot spots).
+template <bool ROT>
+__global__ __launch_bounds__(1024) void readbw_share_kernel(const uint8_t* __restrict__ base, uint64_t nbytes,
+                                                            uint32_t* __restrict__ out) {
+  constexpr int U = 8;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * gridDim.x + blockIdx.x);
+  const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+  const uint64_t nb = nbytes / kBlockBytes / nwaves;  // blocks per wave
+  const u32x4* q = reinterpret_cast<const u32x4*>(base + (uint64_t)wave * nb * kBlockBytes) + lane;
+  const uint64_t rot = ROT ? ((uint64_t)wave * 97u) % (nb ? nb : 1) : 0;
+  uint32_t x = 0;
+  uint64_t b = 0;
+  for (; b + U <= nb; b += U) {
+    u32x4 w[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      uint64_t bb = b + u + rot;
+      bb = bb >= nb ? bb - nb : bb;
+      w[u] = __builtin_nontemporal_load(q + bb * 64);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) x ^= w[u].x ^ w[u].y ^ w[u].z ^ w[u].w;
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = x;
+}
+
 __global__ __launch_bounds__(256) void readbw_stream_kernel(const u32x4* __restrict__ p, uint64_t n16,
                                                             uint32_t* __restrict__ out) {
   constexpr int U = 8;
@@ -1198,6 +1276,8 @@ hipError_t launch_readbw(const uint8_t* base, uint64_t nbytes, uint32_t* out, in
   switch (variant) {
     case 0: hipLaunchKernelGGL(readbw_tiles_kernel<false>, dim3(grid), dim3(1024), 0, s, base, nbytes, out); break;
     case 1: hipLaunchKernelGGL(readbw_tiles_kernel<true>, dim3(grid), dim3(1024), 0, s, base, nbytes, out); break;
+    case 3: hipLaunchKernelGGL(readbw_share_kernel<false>, dim3(grid), dim3(1024), 0, s, base, nbytes, out); break;
+    case 4: hipLaunchKernelGGL(readbw_share_kernel<true>, dim3(grid), dim3(1024), 0, s, base, nbytes, out); break;
     case 2:
       hipLaunchKernelGGL(readbw_stream_kernel, dim3(grid * 4 * 8), dim3(256), 0, s,
                          reinterpret_cast<const u32x4*>(base), nbytes / 16, out);

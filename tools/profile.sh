@@ -10,11 +10,14 @@
 set -euo pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-ARGS=${BENCH_ARGS:-"--steps 5 --warmup 2"}
+# the kernel-trace pass profiles the bench command itself (default arguments unless
+# BENCH_ARGS is set); the counter passes skip the CPU baseline and host path to stay short
+ARGS=${BENCH_ARGS:-""}
+PMC_ARGS=${PMC_BENCH_ARGS:-"--steps 5 --warmup 2 --no-cpu-baseline --no-host-path"}
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_kt -o kt -- python3 bench.py $ARGS > gpurun_out/prof_kt.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch -o pmc -- python3 bench.py $ARGS > gpurun_out/prof_fetch.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write -o pmc -- python3 bench.py $ARGS > gpurun_out/prof_write.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_WAVE_CYCLES GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/prof_sq -o pmc -- python3 bench.py $ARGS > gpurun_out/prof_sq.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch -o pmc -- python3 bench.py $PMC_ARGS > gpurun_out/prof_fetch.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write -o pmc -- python3 bench.py $PMC_ARGS > gpurun_out/prof_write.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_WAVE_CYCLES GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/prof_sq -o pmc -- python3 bench.py $PMC_ARGS > gpurun_out/prof_sq.log 2>&1
 # rocprofv3 nests outputs under a host/pid directory: flatten the files summarize_profile.py reads
 for d in prof_kt prof_fetch prof_write prof_sq; do
   find gpurun_out/$d -mindepth 2 -name '*.csv' -exec cp {} gpurun_out/$d/ \;

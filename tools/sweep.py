@@ -62,7 +62,7 @@ def main():
 
     configs = []
     if args.readbw:
-        configs += [("readbw", v, None) for v in (0, 1, 2)]
+        configs += [("readbw", v, None) for v in (0, 1, 2, 3, 4)]
     for v in [int(x) for x in args.variants.split(",") if x]:
         for t in [int(x) for x in args.grids.split(",") if x]:
             configs.append(("crc", v, t))
