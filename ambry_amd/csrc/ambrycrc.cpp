@@ -118,12 +118,15 @@ struct DevCtx {
   int device = -1;
   int num_cu = 0;
   int grid = 0;
-  // 25: 64-B lane runs (four coalesced 1 KiB loads per 4 KiB super-block, quad transpose by
-  // v_cndmask_b32_dpp, one x^(8*4096) fold per 64 B), U4 loads in flight, with the group
-  // phase G16/NB64 fused in for whole chunks <= 16 KiB in batches of >= kGroupMinChunks
-  // chunks. On C3 it beat 23 (the same with separate DPP moves and selects) by 1.2-1.9 %
-  // and 22 (16-B pieces, fold per piece) by 2-5 % (tools/sweep.py; profiles/r01d_*).
-  int variant = 25;
+  // 26: 64-B lane runs (four coalesced 1 KiB loads per 4 KiB super-block, quad transpose by
+  // v_cndmask_b32_dpp, one x^(8*4096) fold per 64 B), U4 loads in flight; plus, for batches
+  // of >= kGroupMinChunks chunks, whole chunks <= 16 KiB in the fused group phase, each size
+  // class spread over all waves with a class-sized group (G = 4 / 8 / 16 lanes).
+  // Measured (tools/sweep.py, bench_ladder.py, bench_messages.py; profiles/r01d_*): the
+  // DPP-fused transpose beat 23 by 1.2-1.9 % on C3; the class-sized group phase took 100 B
+  // chunks from 0.51 to 1.29 TB/s, 1 KiB from 3.8 to 4.8 TB/s and the 4 KiB-blob message
+  // verify from 1.96 to 2.96 TiB/s.
+  int variant = 26;
   uint32_t* d_img = nullptr;
   void* d_ws = nullptr;
   size_t ws_bytes = 0;
@@ -277,11 +280,12 @@ DevCtx* ctx_current() {
   return ctx_for(dev);
 }
 
-// workspace: byte_start[n+1] | block_sum[B] | block_small[B] | small_total (uint64) |
+// workspace: byte_start[n+1] | block_sum[B] | block_small[B] | small_total[4] (uint64:
+//            total, start of size classes 1..3 in small_idx) |
 //            small_idx[n] (uint32), B = ceil(n / kPlanPerBlock)
 size_t ws_need(size_t n) {
   const size_t blocks = (n + kPlanPerBlock - 1) / kPlanPerBlock;
-  return ((n + 2 + 2 * blocks) * sizeof(uint64_t) + n * sizeof(uint32_t) + 255) & ~size_t(255);
+  return ((n + 5 + 2 * blocks) * sizeof(uint64_t) + n * sizeof(uint32_t) + 255) & ~size_t(255);
 }
 
 int ensure_ws(DevCtx* c, size_t need) {
@@ -311,7 +315,7 @@ int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uin
   p.block_sum = p.byte_start + n + 1;
   p.block_small = p.block_sum + blocks;
   p.small_total = p.block_small + blocks;
-  p.small_idx = reinterpret_cast<uint32_t*>(p.small_total + 1);
+  p.small_idx = reinterpret_cast<uint32_t*>(p.small_total + 4);
   p.out = out;
   // variants >= 14: variant 0's sweep plus the group kernel for small whole chunks
   // 20, 21: the group phase fused into the sweep launch (sweep variant = the variant itself)

@@ -16,7 +16,7 @@ struct PlanArgs {
   uint32_t* out;           // [n] initialised here, XOR-accumulated by the sweep kernel
   uint64_t small_max;      // chunks with 0 < len <= small_max go to the group kernel (0: none)
   uint64_t* block_small;   // [ceil(n / kPlanPerBlock)] scratch: 4 x 16-bit size-class counts
-  uint64_t* small_total;   // [1] number of small chunks
+  uint64_t* small_total;   // [4] number of small chunks; start of size classes 1..3 in small_idx
   uint32_t* small_idx;     // [n] their indices, grouped by size class, ascending within a class
 };
 
@@ -34,7 +34,7 @@ struct SweepArgs {
   const uint32_t* img;     // LDS image (kLdsBytes) followed by 64 words x^(8*2^k)
   uint32_t* out;
   uint64_t small_max;      // sweep: skip chunks with len <= small_max; group kernel: take them
-  const uint64_t* small_total;
+  const uint64_t* small_total;  // [4] as PlanArgs
   const uint32_t* small_idx;
 };
 
@@ -66,7 +66,9 @@ constexpr uint64_t group_small_max(int mode) {
 // (8 waves per CU with 256 VGPRs and U8/U16 prefetch lost 3-14 % to these at 16 waves: the
 // 4 waves per SIMD hide the LDS chains better; the TPB template parameter is kept)
 // 25 = 23 with the quad transposes' lane selects fused into DPP moves (v_cndmask_b32_dpp)
-constexpr int kNumVariants = 26;
+// 26 = 25 with the group phase sized and balanced per size class (G = 4 for <= 256 B, 8 for
+// <= 1 KiB, 16 above; every class spread over all waves)
+constexpr int kNumVariants = 27;
 constexpr int kDiagNoFold = 100;  // diagnostic timing build, selectable via ambrycrc_set_variant only
 
 // Message verify (message_kernels.hip): kMsgSlots CRC jobs per message, slot order

@@ -750,6 +750,152 @@ __device__ __forceinline__ void group_phase(const SweepArgs& a, uint64_t ns, uin
   }
 }
 
+// ---- class-sized, class-balanced group phase (variant 26) ----
+// group_phase gives every wave an equal COUNT of list entries, and the list is sorted by
+// size class, so a batch of mixed records (a PUT message's 60 B properties, 1 KiB user
+// metadata, 4 KiB blob) puts all the 4 KiB records on a third of the waves; and it runs
+// every class with G = 16, so a 100 B chunk pays a 256 B block and a 4-level tree. Here
+// each class is spread over all waves separately, with a group width sized to the class:
+//   class 0 (<= 256 B): G = 4,  64 B blocks, 16 chunks per round
+//   class 1 (<= 1 KiB): G = 8, 128 B blocks,  8 chunks per round
+//   class 2 (<= 4 KiB): G = 16, 256 B blocks, 4 chunks per round; class 3 (<= 16 KiB) too.
+// The trailing t < 16 bytes go 16/G per lane: lane gl takes the bytes at distance
+// k in [16/G*(G-1-gl), 16/G*(G-gl)) from the chunk end, T_{k&3}[b], then one shift by
+// x^(32*(k>>2)) per lane, then an xor over the group.
+
+template <int G>
+__device__ __forceinline__ constexpr uint32_t group_fold_off() {  // x^(8*16G) = POW[log2 16G]
+  return kPowOff + kNibSetBytes * (G == 4 ? 6u : G == 8 ? 7u : G == 16 ? 8u : 9u);
+}
+
+// xor over the G lanes of each group; result in every lane of the group
+template <int G>
+__device__ __forceinline__ uint32_t group_xor(uint32_t v) {
+  if constexpr (G == 16) {  // whole rows: row_ror 8, 4, 2, 1
+    v ^= dpp<0x128, 0xf>(v);
+    v ^= dpp<0x124, 0xf>(v);
+    v ^= dpp<0x122, 0xf>(v);
+    v ^= dpp<0x121, 0xf>(v);
+  } else {
+    static_assert(G == 4 || G == 8, "group width");
+    v ^= dppq<0xB1>(v);  // lane ^ 1
+    v ^= dppq<0x4E>(v);  // lane ^ 2
+    if constexpr (G == 8) v ^= (uint32_t)__shfl_xor((int)v, 4);
+  }
+  return v;
+}
+
+template <int G, int NB, bool NT>
+__device__ __forceinline__ uint32_t group_crc_g(const uint8_t* __restrict__ base, uint64_t cs, uint64_t len,
+                                                uint32_t cin, uint32_t nbw, uint32_t lane, const LaneConst& k) {
+  constexpr uint32_t BB = 16u * G;
+  constexpr uint32_t BPL = 16u / G;  // trailing bytes per lane
+  const uint32_t gl = lane & (G - 1);
+  const uint32_t rinit = ~cin;
+  const uint64_t ce = cs + len;
+  const uint64_t cb = aligned_end(cs, ce);
+  const bool body = cb > cs;
+  const int64_t p0 = (int64_t)cb - (int64_t)nbw * BB + 16 * (int64_t)gl;
+  const GroupCtx g{base, p0, cs, body, nbw, rinit};
+  constexpr int P = NB < 8 ? NB : 8;
+  GroupRingT<0, P, NT, (int)BB> ring;
+  ring.prime(g);
+  uint32_t s = 0;
+#pragma unroll 1
+  for (uint32_t b0 = 0; b0 < nbw; b0 += P) s = ring.step(g, k, b0, s, group_fold_off<G>());
+  uint32_t r = s;
+  if (nbw) {
+    r = tree_level<0>(r, lane);
+    r = tree_level<1>(r, lane);
+    if constexpr (G >= 8) r = tree_level<2>(r, lane);
+    if constexpr (G >= 16) r = tree_level<3>(r, lane);
+    if constexpr (G >= 32) r = tree_level<4>(r, lane);
+  }
+  r = __shfl(r, (int)(lane | (G - 1)));  // the group's body CRC, from its last lane
+  const uint32_t t = (uint32_t)(ce - cb);  // trailing < 16 bytes
+  if (t & 1u) r = nib_mul(r, kPowOff + kNibSetBytes * 0);
+  if (t & 2u) r = nib_mul(r, kPowOff + kNibSetBytes * 1);
+  if (t & 4u) r = nib_mul(r, kPowOff + kNibSetBytes * 2);
+  if (t & 8u) r = nib_mul(r, kPowOff + kNibSetBytes * 3);
+  uint32_t v = 0;
+  const uint32_t k0 = BPL * (G - 1 - gl);  // this lane's bytes sit at distance k0..k0+BPL-1 from the end
+  if (k0 < t) {
+#pragma unroll
+    for (uint32_t i = 0; i < BPL; ++i) {
+      const uint32_t kk = k0 + i;
+      if (kk < t) {
+        const uint64_t at = ce - 1 - kk;
+        uint32_t byte = base[at];
+        if (at < cs + 4) byte ^= (rinit >> (8 * (uint32_t)(at - cs))) & 0xFFu;
+        const uint32_t j = kk & 3;
+        v ^= lds_rd(((j >> 1) << 16) | (byte << 8) | ((j & 1) << 7) | ((lane & 31) << 2));
+      }
+    }
+    if (k0 & 4) v = nib_mul(v, kPowOff + kNibSetBytes * 2);  // x^(8*4)
+    if (k0 & 8) v = nib_mul(v, kPowOff + kNibSetBytes * 3);  // x^(8*8)
+  }
+  v = group_xor<G>(v);
+  uint32_t crc = r ^ v ^ 0xFFFFFFFFu;
+  if (len < 4) crc ^= rinit >> (8 * (uint32_t)len);
+  return crc;
+}
+
+// One size class [lo, hi) of the list, spread over all waves: wave w takes entries
+// [lo + w*per, lo + (w+1)*per), per a multiple of 64/G.
+template <int G, int NB, bool NT>
+__device__ __forceinline__ void group_class(const SweepArgs& a, uint64_t lo, uint64_t hi, uint32_t wave,
+                                            uint64_t nwaves, uint32_t lane, const LaneConst& k) {
+  constexpr uint32_t S = 64 / G;
+  if (hi <= lo) return;
+  const uint64_t per = group_per<G>(hi - lo, nwaves);
+  const uint64_t i0 = lo + (uint64_t)wave * per;
+  if (i0 >= hi) return;
+  const uint64_t i1 = i0 + per < hi ? i0 + per : hi;
+  const uint32_t gi = lane / G;
+#pragma unroll 1
+  for (uint64_t i = i0; i < i1; i += S) {
+    const bool act = i + gi < i1;
+    const uint32_t ci = act ? a.small_idx[i + gi] : 0u;
+    uint64_t len = 0, off = 0;
+    uint32_t cin = 0;
+    if (act) {
+      len = a.len[ci];
+      off = a.off[ci];
+      cin = a.crc_in ? a.crc_in[ci] : 0u;
+    }
+    const uint64_t cb = aligned_end(off, off + len);
+    const uint32_t nb = (uint32_t)((cb - off + 16 * G - 1) / (16 * G));
+    uint32_t nbw = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < S; ++q) {
+      const uint32_t x = __builtin_amdgcn_readlane(nb, q * G);
+      nbw = x > nbw ? x : nbw;
+    }
+    const uint32_t crc = group_crc_g<G, NB, NT>(a.base, off, len, cin, nbw, lane, k);
+    if ((lane & (G - 1)) == 0 && act) a.out[ci] = crc;
+  }
+}
+
+// class bounds from the plan: small_total = {total, start of class 1, 2, 3}
+__device__ __forceinline__ bool group_cls_has_work(const SweepArgs& a, uint32_t first_wave, uint64_t nwaves) {
+  const uint64_t c0 = 0, c1 = a.small_total[1], c2 = a.small_total[2], c3 = a.small_total[3];
+  const uint64_t c4 = a.small_total[0];
+  return (c1 > c0 && first_wave * group_per<4>(c1 - c0, nwaves) < c1 - c0) ||
+         (c2 > c1 && first_wave * group_per<8>(c2 - c1, nwaves) < c2 - c1) ||
+         (c3 > c2 && first_wave * group_per<16>(c3 - c2, nwaves) < c3 - c2) ||
+         (c4 > c3 && first_wave * group_per<16>(c4 - c3, nwaves) < c4 - c3);
+}
+
+template <bool NT>
+__device__ __forceinline__ void group_phase_cls(const SweepArgs& a, uint32_t wave, uint64_t nwaves, uint32_t lane,
+                                                const LaneConst& k) {
+  const uint64_t c1 = a.small_total[1], c2 = a.small_total[2], c3 = a.small_total[3], c4 = a.small_total[0];
+  group_class<4, 4, NT>(a, 0, c1, wave, nwaves, lane, k);
+  group_class<8, 8, NT>(a, c1, c2, wave, nwaves, lane, k);
+  group_class<16, 16, NT>(a, c2, c3, wave, nwaves, lane, k);
+  group_class<16, 64, NT>(a, c3, c4, wave, nwaves, lane, k);
+}
+
 // Group kernel: every chunk with 0 < len <= a.small_max (= 16*G*NB), whole, from the
 // plan's compacted list small_idx[0..small_total), 64/G chunks per round (one per group).
 // The sweep kernel skips these chunks (the plan gives them no byte share).
@@ -802,7 +948,7 @@ __device__ __forceinline__ uint64_t snap_cut(uint64_t cs, uint64_t len, uint64_t
 // bytes whatever the chunk-size mix. Each (wave, chunk) intersection is a segment whose
 // raw CRC is shifted to the chunk end and XORed into out[chunk].
 template <int U, bool NT, bool PIPE, bool IL, bool WIN, int DIAG = 0, int LR = 0, int GG = 0, int GNB = 0,
-          int TPB = 1024>
+          int TPB = 1024, int GV = 1>
 __global__ __launch_bounds__(TPB) void crc32_sweep_kernel(SweepArgs a) {
   // Shares are wave-major over workgroups (share i -> wave i / gridDim.x of workgroup
   // i % gridDim.x), so when a batch has fewer shares than waves they spread over every
@@ -815,7 +961,9 @@ __global__ __launch_bounds__(TPB) void crc32_sweep_kernel(SweepArgs a) {
   share = share < kMinShare ? kMinShare : share;
   // Fused group phase (GG > 0): the workgroup first takes its part of the small-chunk list.
   const uint64_t ns = GG > 0 ? *a.small_total : 0;
-  const bool grp = GG > 0 && ns > 0 && (uint64_t)blockIdx.x * group_per<(GG > 0 ? GG : 16)>(ns, nwaves) < ns;
+  const bool grp = GG > 0 && ns > 0 &&
+                   (GV == 3 ? group_cls_has_work(a, blockIdx.x, nwaves)
+                            : (uint64_t)blockIdx.x * group_per<(GG > 0 ? GG : 16)>(ns, nwaves) < ns);
   if ((uint64_t)blockIdx.x * share >= total && !grp) return;  // uniform: no work for this workgroup
   {
     const u32x4* src = reinterpret_cast<const u32x4*>(a.img);
@@ -827,7 +975,10 @@ __global__ __launch_bounds__(TPB) void crc32_sweep_kernel(SweepArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * gridDim.x + blockIdx.x);
   if constexpr (GG > 0) {
-    if (grp) group_phase<GG, GNB, NT>(a, ns, wave, nwaves, lane, make_lane_const(lane));
+    if (grp) {
+      if constexpr (GV == 3) group_phase_cls<NT>(a, wave, nwaves, lane, make_lane_const(lane));
+      else group_phase<GG, GNB, NT>(a, ns, wave, nwaves, lane, make_lane_const(lane));
+    }
   }
   const uint64_t g0 = (uint64_t)wave * share;
   if (g0 >= total) return;
@@ -1074,7 +1225,12 @@ __global__ __launch_bounds__(256) void crc32_plan_scan_kernel(PlanArgs a) {
 #pragma unroll
     for (uint32_t k = 0; k < 4; ++k) cls_carry[k] += field16(round_cls, k);
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) *a.small_total = cls_base[3] + cls_total[3];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    a.small_total[0] = cls_base[3] + cls_total[3];
+    a.small_total[1] = cls_base[1];
+    a.small_total[2] = cls_base[2];
+    a.small_total[3] = cls_base[3];
+  }
 }
 
 __global__ void crc32_verify_kernel(const uint32_t* __restrict__ crc, const uint32_t* __restrict__ expected,
@@ -1148,6 +1304,8 @@ hipError_t launch_sweep(const SweepArgs& a, int grid, int variant, hipStream_t s
     case 24: hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, false, true, 0, -2, 16, 64>), dim3(grid), dim3(1024), 0, s, a); break;
     // 23 with the transposes' selects fused into the DPP moves (v_cndmask_b32_dpp)
     case 25: hipLaunchKernelGGL((crc32_sweep_kernel<4, true, true, false, true, 0, -3, 16, 64>), dim3(grid), dim3(1024), 0, s, a); break;
+    // 25 with the class-sized (G = 4/8/16/16), class-balanced group phase
+    case 26: hipLaunchKernelGGL((crc32_sweep_kernel<4, true, true, false, true, 0, -3, 16, 64, 1024, 3>), dim3(grid), dim3(1024), 0, s, a); break;
     // timing-only diagnostics (wrong CRCs): 100 FOLD lookups removed, 101 no per-segment
     // atomic, 102 no wave tree
     case kDiagNoFold: hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, true, true, 1>), dim3(grid), dim3(1024), 0, s, a); break;
