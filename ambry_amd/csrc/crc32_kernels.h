@@ -68,6 +68,8 @@ constexpr uint64_t group_small_max(int mode) {
 // 25 = 23 with the quad transposes' lane selects fused into DPP moves (v_cndmask_b32_dpp)
 // 26 = 25 with the group phase sized and balanced per size class (G = 4 for <= 256 B, 8 for
 // <= 1 KiB, 16 above; every class spread over all waves)
+// (prefetching the group rounds' list entries and descriptors two stages ahead measured no
+// gain over 26: the 16 waves per CU already hide that latency)
 constexpr int kNumVariants = 27;
 constexpr int kDiagNoFold = 100;  // diagnostic timing build, selectable via ambrycrc_set_variant only
 

@@ -797,6 +797,12 @@ __device__ __forceinline__ uint32_t group_crc_g(const uint8_t* __restrict__ base
   const bool body = cb > cs;
   const int64_t p0 = (int64_t)cb - (int64_t)nbw * BB + 16 * (int64_t)gl;
   const GroupCtx g{base, p0, cs, body, nbw, rinit};
+  const uint32_t t = (uint32_t)(ce - cb);  // trailing < 16 bytes
+  const uint32_t k0 = BPL * (G - 1 - gl);  // this lane's bytes sit at distance k0..k0+BPL-1 from the end
+  // the trailing bytes are loaded with the blocks, not after the chain (one round trip)
+  uint32_t tb[BPL];
+#pragma unroll
+  for (uint32_t i = 0; i < BPL; ++i) tb[i] = k0 + i < t ? base[ce - 1 - (k0 + i)] : 0u;
   constexpr int P = NB < 8 ? NB : 8;
   GroupRingT<0, P, NT, (int)BB> ring;
   ring.prime(g);
@@ -812,20 +818,18 @@ __device__ __forceinline__ uint32_t group_crc_g(const uint8_t* __restrict__ base
     if constexpr (G >= 32) r = tree_level<4>(r, lane);
   }
   r = __shfl(r, (int)(lane | (G - 1)));  // the group's body CRC, from its last lane
-  const uint32_t t = (uint32_t)(ce - cb);  // trailing < 16 bytes
   if (t & 1u) r = nib_mul(r, kPowOff + kNibSetBytes * 0);
   if (t & 2u) r = nib_mul(r, kPowOff + kNibSetBytes * 1);
   if (t & 4u) r = nib_mul(r, kPowOff + kNibSetBytes * 2);
   if (t & 8u) r = nib_mul(r, kPowOff + kNibSetBytes * 3);
   uint32_t v = 0;
-  const uint32_t k0 = BPL * (G - 1 - gl);  // this lane's bytes sit at distance k0..k0+BPL-1 from the end
   if (k0 < t) {
 #pragma unroll
     for (uint32_t i = 0; i < BPL; ++i) {
       const uint32_t kk = k0 + i;
       if (kk < t) {
         const uint64_t at = ce - 1 - kk;
-        uint32_t byte = base[at];
+        uint32_t byte = tb[i];
         if (at < cs + 4) byte ^= (rinit >> (8 * (uint32_t)(at - cs))) & 0xFFu;
         const uint32_t j = kk & 3;
         v ^= lds_rd(((j >> 1) << 16) | (byte << 8) | ((j & 1) << 7) | ((lane & 31) << 2));
