@@ -21,11 +21,29 @@
 
 namespace ambrycrc {
 
-__device__ __forceinline__ uint32_t be16(const uint8_t* p) { return ((uint32_t)p[0] << 8) | p[1]; }
-__device__ __forceinline__ uint32_t be32(const uint8_t* p) {
-  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+// Big-endian fields at arbitrary byte offsets: one unaligned global load each (gfx9 global
+// memory runs in unaligned access mode; the compiler emits global_load_dword[x2] for these
+// memcpys), where byte-wise reads cost a load per byte.
+__device__ __forceinline__ uint32_t be16(const uint8_t* p) {
+  uint16_t v;
+  __builtin_memcpy(&v, p, 2);
+  return __builtin_bswap16(v);
 }
-__device__ __forceinline__ uint64_t be64(const uint8_t* p) { return ((uint64_t)be32(p) << 32) | be32(p + 4); }
+__device__ __forceinline__ uint32_t be32(const uint8_t* p) {
+  uint32_t v;
+  __builtin_memcpy(&v, p, 4);
+  return __builtin_bswap32(v);
+}
+__device__ __forceinline__ uint64_t be64(const uint8_t* p) {
+  uint64_t v;
+  __builtin_memcpy(&v, p, 8);
+  return __builtin_bswap64(v);
+}
+__device__ __forceinline__ uint32_t le32(const uint8_t* p) {
+  uint32_t v;
+  __builtin_memcpy(&v, p, 4);
+  return v;
+}
 
 // Slice-by-4 tables T0..T3 (T_j[b] = b advanced over j further zero bytes), 4 KiB, staged
 // into LDS per workgroup from the table image: T_j[b] sits at image byte
@@ -43,8 +61,7 @@ __device__ __forceinline__ uint32_t crc_small(const uint8_t* p, uint32_t n, cons
   uint32_t c = 0xFFFFFFFFu;
   uint32_t i = 0;
   for (; i + 4 <= n; i += 4) {
-    const uint32_t x = c ^ ((uint32_t)p[i] | ((uint32_t)p[i + 1] << 8) | ((uint32_t)p[i + 2] << 16) |
-                            ((uint32_t)p[i + 3] << 24));
+    const uint32_t x = c ^ le32(p + i);
     c = t[768 + (x & 0xffu)] ^ t[512 + ((x >> 8) & 0xffu)] ^ t[256 + ((x >> 16) & 0xffu)] ^ t[x >> 24];
   }
   for (; i < n; ++i) c = (c >> 8) ^ t[(c ^ p[i]) & 0xffu];
