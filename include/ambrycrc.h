@@ -201,13 +201,14 @@ int ambrycrc_range_checksums_host(const uint8_t* file, uint64_t file_len, const 
 
 /* ------------------------------------------------------- tuning / telemetry */
 
-/* Kernel variant (0..22; crc32_kernels.h lists them). 0..13: sweep-kernel shapes (blocks in
+/* Kernel variant (0..26; crc32_kernels.h lists them). 0..13: sweep-kernel shapes (blocks in
  * flight per lane, load policy, prefetch scheme, lane runs) for every chunk; 14..19: sweep
- * variant 0 plus a separate group kernel for whole chunks up to 2..16 KiB; 20..22: the
- * group phase fused into the sweep launch (chunks <= 8, 4, 16 KiB). Group modes engage for
- * batches of >= 16384 chunks; smaller batches take the sweep for every chunk (latency).
- * Default 22 = sweep 0 (8 blocks in flight per lane, nontemporal loads, rolling prefetch,
- * two pieces' table walks interleaved) with the G16 group phase for whole chunks <= 16 KiB.
+ * variant 0 plus a separate group kernel for whole chunks up to 2..16 KiB; 20..26: the
+ * group phase fused into the sweep launch. Group modes engage for batches of >= 16384
+ * chunks; smaller batches take the sweep for every chunk (latency).
+ * Default 26 = 64-B lane runs (coalesced loads, quad transpose by v_cndmask_b32_dpp, one
+ * fold per 64 B) with the group phase for whole chunks <= 16 KiB sized per size class
+ * (4 / 8 / 16 lanes per chunk) and spread over all waves per class.
  * 100..102 are timing diagnostics that produce wrong CRCs. ambrycrc_get_variant returns
  * the current one. */
 int ambrycrc_set_variant(int device, int variant);
@@ -233,8 +234,9 @@ int ambrycrc_fill_random_dev(uint8_t* d_dst, uint64_t nbytes, uint64_t seed, uin
                              hipStream_t stream);
 
 /* Read-bandwidth probe (no CRC arithmetic) over [d_base, d_base+nbytes) with the
- * sweep kernel's grid and access pattern (variant 0; 1 = nontemporal; 2 = plain
- * grid-stride stream). d_out needs grid*1024 words. Measures the achievable HBM
+ * sweep kernel's grid and access pattern (variant 0: 256 KiB tiles; 1 = the same with
+ * nontemporal loads; 2 = plain grid-stride stream; 3 = contiguous per-wave shares, NT;
+ * 4 = shares entered at a per-wave rotation, NT). d_out needs grid*1024 words. Measures the achievable HBM
  * read roof the CRC sweep kernel is compared against. */
 int ambrycrc_debug_readbw_dev(const uint8_t* d_base, uint64_t nbytes, uint32_t* d_out, int variant,
                               hipStream_t stream);
