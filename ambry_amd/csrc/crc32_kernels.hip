@@ -36,6 +36,24 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __shared__ __attribute__((aligned(16))) uint32_t g_lds[kLdsBytes / 4];
 
+// Stage the table image into LDS with LDS-DMA (global_load_lds_dwordx4: 1 KiB per wave
+// instruction, no VGPR round trip), all of a wave's ~10 loads in flight together, then one
+// wait and a barrier. A load -> ds_write loop serialises on vmcnt(0) per iteration: ~10
+// memory round trips, which was most of a single-chunk call's sweep-kernel time.
+__device__ __forceinline__ void fill_lds(const uint32_t* __restrict__ img) {
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  constexpr uint32_t kChunks = (kLdsBytes + 1023) / 1024;
+  for (uint32_t c = wave; c < kChunks; c += nw) {
+    const uint32_t byte = c * 1024 + lane * 16;
+    if (byte < kLdsBytes)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(reinterpret_cast<const uint8_t*>(img) + byte),
+          (__attribute__((address_space(3))) void*)(reinterpret_cast<uint8_t*>(g_lds) + c * 1024), 16, 0, 0);
+  }
+  __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0): the DMA writes have landed
+  __syncthreads();
+}
+
 __device__ __forceinline__ uint32_t lds_rd(uint32_t byte_addr) {
   return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(g_lds) + byte_addr);
 }
@@ -907,12 +925,7 @@ template <int G, int NB, bool NT>
 __global__ __launch_bounds__(1024) void crc32_group_kernel(SweepArgs a) {
   const uint64_t ns = *a.small_total;
   if (ns == 0) return;  // uniform: every wave leaves before the LDS fill
-  {
-    const u32x4* src = reinterpret_cast<const u32x4*>(a.img);
-    u32x4* dst = reinterpret_cast<u32x4*>(g_lds);
-    for (uint32_t i = threadIdx.x; i < kLdsBytes / 16; i += blockDim.x) dst[i] = src[i];
-  }
-  __syncthreads();
+  fill_lds(a.img);
   const uint32_t lane = threadIdx.x & 63u;
   // wave-major over workgroups: the first list ranges land on different CUs/XCDs
   const uint32_t wave = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * gridDim.x + blockIdx.x);
@@ -969,12 +982,7 @@ __global__ __launch_bounds__(TPB) void crc32_sweep_kernel(SweepArgs a) {
                    (GV == 3 ? group_cls_has_work(a, blockIdx.x, nwaves)
                             : (uint64_t)blockIdx.x * group_per<(GG > 0 ? GG : 16)>(ns, nwaves) < ns);
   if ((uint64_t)blockIdx.x * share >= total && !grp) return;  // uniform: no work for this workgroup
-  {
-    const u32x4* src = reinterpret_cast<const u32x4*>(a.img);
-    u32x4* dst = reinterpret_cast<u32x4*>(g_lds);
-    for (uint32_t i = threadIdx.x; i < kLdsBytes / 16; i += blockDim.x) dst[i] = src[i];
-  }
-  __syncthreads();
+  fill_lds(a.img);
 
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * gridDim.x + blockIdx.x);
@@ -1146,10 +1154,18 @@ __device__ __forceinline__ uint64_t class_onehot(uint64_t len, uint64_t small_ma
 }
 __device__ __forceinline__ uint64_t field16(uint64_t v, uint32_t c) { return (v >> (16 * c)) & 0xFFFFu; }
 
+// Chunks of plan block `base` rounded up to whole 256-chunk rounds: the last block (and a
+// one-block batch) stops at n instead of running all kPlanPerBlock / 256 scan rounds.
+__device__ __forceinline__ uint32_t plan_span(uint32_t n, uint32_t base) {
+  const uint32_t left = n - base;
+  return left < kPlanPerBlock ? (left + 255u) & ~255u : kPlanPerBlock;
+}
+
 __global__ __launch_bounds__(256) void crc32_plan_count_kernel(PlanArgs a) {
   const uint32_t base = blockIdx.x * kPlanPerBlock;
+  const uint32_t span = plan_span(a.n, base);
   uint64_t sum = 0, cls = 0;
-  for (uint32_t r = 0; r < kPlanPerBlock; r += 256) {
+  for (uint32_t r = 0; r < span; r += 256) {
     const uint32_t c = base + r + threadIdx.x;
     if (c < a.n) {
       const uint64_t len = a.len[c];
@@ -1192,7 +1208,7 @@ __global__ __launch_bounds__(256) void crc32_plan_scan_kernel(PlanArgs a) {
       class_sums(a.block_small, nblocks, cls_total);
     } else {  // no count launch: count this (only) block here
       uint64_t cls = 0;
-      for (uint32_t r = 0; r < kPlanPerBlock; r += 256) {
+      for (uint32_t r = 0; r < plan_span(a.n, 0); r += 256) {
         const uint32_t c = r + threadIdx.x;
         if (c < a.n) cls += class_onehot(a.len[c], a.small_max);
       }
@@ -1208,7 +1224,8 @@ __global__ __launch_bounds__(256) void crc32_plan_scan_kernel(PlanArgs a) {
   cls_base[2] = cls_base[1] + cls_total[1];
   cls_base[3] = cls_base[2] + cls_total[2];
   const uint32_t base = blockIdx.x * kPlanPerBlock;
-  for (uint32_t r = 0; r < kPlanPerBlock; r += 256) {
+  const uint32_t span = plan_span(a.n, base);
+  for (uint32_t r = 0; r < span; r += 256) {
     const uint32_t c = base + r + threadIdx.x;
     const uint64_t len = c < a.n ? a.len[c] : 0u;
     const uint64_t v = share_len(len, a.small_max);

@@ -129,6 +129,28 @@ def gpu_rows(size: int, gib: float, reps: int, variant: int = 0, check: bool = T
     torch.cuda.synchronize()
     host_us = (time.perf_counter() - t0) / calls * 1e6
     call = {"us_per_call_stream": round(e0.elapsed_time(e1) / calls * 1e3, 2), "us_per_call_host": round(host_us, 2)}
+    # the same calls straight through the C ABI (ctypes, arguments prepared once): what a JNI
+    # caller pays, without the torch wrapper's per-call tensor checks and stream lookup
+    import ctypes
+
+    from ambry_amd._lib import lib
+
+    L = lib()
+    args = (ctypes.c_void_p(buf.data_ptr()), ctypes.c_void_p(o1.data_ptr()), ctypes.c_void_p(l1.data_ptr()), None,
+            ctypes.c_void_p(out1.data_ptr()), 1, ctypes.c_void_p(ws1.data_ptr()), ws1.numel(),
+            ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    fn = L.ambrycrc_batch_dev
+    for _ in range(50):
+        fn(*args)
+    torch.cuda.synchronize()
+    e0.record()
+    t0 = time.perf_counter()
+    for _ in range(calls):
+        fn(*args)
+    e1.record()
+    torch.cuda.synchronize()
+    call["us_per_call_abi_host"] = round((time.perf_counter() - t0) / calls * 1e6, 2)
+    call["us_per_call_abi_stream"] = round(e0.elapsed_time(e1) / calls * 1e3, 2)
     D.set_variant(0, default)
     del buf, off, ln, out, ws
     torch.cuda.empty_cache()
