@@ -280,12 +280,12 @@ DevCtx* ctx_current() {
   return ctx_for(dev);
 }
 
-// workspace: byte_start[n+1] | block_sum[B] | block_small[B] | small_total[4] (uint64:
-//            total, start of size classes 1..3 in small_idx) |
+// workspace: byte_start[n+1] | block_sum[B] | block_small[B] | small_total[5] (uint64:
+//            total, start of size classes 1..3 in small_idx, dynamic share counter) |
 //            small_idx[n] (uint32), B = ceil(n / kPlanPerBlock)
 size_t ws_need(size_t n) {
   const size_t blocks = (n + kPlanPerBlock - 1) / kPlanPerBlock;
-  return ((n + 5 + 2 * blocks) * sizeof(uint64_t) + n * sizeof(uint32_t) + 255) & ~size_t(255);
+  return ((n + 6 + 2 * blocks) * sizeof(uint64_t) + n * sizeof(uint32_t) + 255) & ~size_t(255);
 }
 
 int ensure_ws(DevCtx* c, size_t need) {
@@ -315,7 +315,7 @@ int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uin
   p.block_sum = p.byte_start + n + 1;
   p.block_small = p.block_sum + blocks;
   p.small_total = p.block_small + blocks;
-  p.small_idx = reinterpret_cast<uint32_t*>(p.small_total + 4);
+  p.small_idx = reinterpret_cast<uint32_t*>(p.small_total + 5);
   p.out = out;
   // variants >= 14: variant 0's sweep plus the group kernel for small whole chunks
   // 20, 21: the group phase fused into the sweep launch (sweep variant = the variant itself)
@@ -340,6 +340,7 @@ int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uin
   t.out = out;
   t.small_max = p.small_max;
   t.small_total = p.small_total;
+  t.claim = p.small_total + 4;
   t.small_idx = p.small_idx;
   EventPair ev{nullptr, nullptr};
   if (c->timing) {

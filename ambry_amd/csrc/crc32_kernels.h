@@ -16,7 +16,8 @@ struct PlanArgs {
   uint32_t* out;           // [n] initialised here, XOR-accumulated by the sweep kernel
   uint64_t small_max;      // chunks with 0 < len <= small_max go to the group kernel (0: none)
   uint64_t* block_small;   // [ceil(n / kPlanPerBlock)] scratch: 4 x 16-bit size-class counts
-  uint64_t* small_total;   // [4] number of small chunks; start of size classes 1..3 in small_idx
+  uint64_t* small_total;   // [5] number of small chunks; start of size classes 1..3 in small_idx;
+                           // [4] the sweep's dynamic share counter (zeroed here)
   uint32_t* small_idx;     // [n] their indices, grouped by size class, ascending within a class
 };
 
@@ -35,6 +36,7 @@ struct SweepArgs {
   uint32_t* out;
   uint64_t small_max;      // sweep: skip chunks with len <= small_max; group kernel: take them
   const uint64_t* small_total;  // [4] as PlanArgs
+  uint64_t* claim;              // = PlanArgs small_total + 4 (dynamic shares, variant 27)
   const uint32_t* small_idx;
 };
 
@@ -70,6 +72,10 @@ constexpr uint64_t group_small_max(int mode) {
 // <= 1 KiB, 16 above; every class spread over all waves)
 // (prefetching the group rounds' list entries and descriptors two stages ahead measured no
 // gain over 26: the 16 waves per CU already hide that latency)
+// (dynamic shares -- share/8 bytes each, the rest claimed from an atomic counter after a
+// static first one; the DYN template parameter -- lost 0.6 % on C3, 1.3 % on C4 and 12 % on
+// C2: each claim pays a chunk search and a descriptor reload, and the tail it would
+// shorten was not there)
 constexpr int kNumVariants = 27;
 constexpr int kDiagNoFold = 100;  // diagnostic timing build, selectable via ambrycrc_set_variant only
 

@@ -965,7 +965,7 @@ __device__ __forceinline__ uint64_t snap_cut(uint64_t cs, uint64_t len, uint64_t
 // bytes whatever the chunk-size mix. Each (wave, chunk) intersection is a segment whose
 // raw CRC is shifted to the chunk end and XORed into out[chunk].
 template <int U, bool NT, bool PIPE, bool IL, bool WIN, int DIAG = 0, int LR = 0, int GG = 0, int GNB = 0,
-          int TPB = 1024, int GV = 1>
+          int TPB = 1024, int GV = 1, int DYN = 0>
 __global__ __launch_bounds__(TPB) void crc32_sweep_kernel(SweepArgs a) {
   // Shares are wave-major over workgroups (share i -> wave i / gridDim.x of workgroup
   // i % gridDim.x), so when a batch has fewer shares than waves they spread over every
@@ -992,15 +992,22 @@ __global__ __launch_bounds__(TPB) void crc32_sweep_kernel(SweepArgs a) {
       else group_phase<GG, GNB, NT>(a, ns, wave, nwaves, lane, make_lane_const(lane));
     }
   }
-  const uint64_t g0 = (uint64_t)wave * share;
+  // DYN > 0: shares of share/DYN bytes (>= kMinShare); wave w starts with share w, then
+  // claims share nwaves + atomicAdd(claim) until none is left, so waves that run fast (or
+  // start early) take more and the launch's tail shortens.
+  uint64_t S = share;
+  if constexpr (DYN > 0) {
+    S = (share / DYN + kShareQuantum - 1) & ~uint64_t(kShareQuantum - 1);
+    S = S < kMinShare ? kMinShare : S;
+  }
+  uint64_t g0 = (uint64_t)wave * S;
   if (g0 >= total) return;
-  const uint64_t g1 = g0 + share < total ? g0 + share : total;
+  uint64_t g1 = g0 + S < total ? g0 + S : total;
   const uint32_t* xpow2 = a.img + kLdsBytes / 4;
   const LaneConst k = make_lane_const(lane);
 
   uint64_t init_len = ~0ull;  // one-entry cache of the init term for crc_in == 0
   uint32_t init_term = 0;
-  uint32_t c = __builtin_amdgcn_readfirstlane(find_chunk(a.byte_start, a.n, g0, lane));
 
   // One segment: raw CRC of its body, shifted to the chunk end, + tail + init (wave-uniform).
   // *whole: the segment is the entire chunk, so no other wave contributes to out[ci].
@@ -1051,6 +1058,8 @@ __global__ __launch_bounds__(TPB) void crc32_sweep_kernel(SweepArgs a) {
     }
   };
 
+  for (;;) {
+  uint32_t c = __builtin_amdgcn_readfirstlane(find_chunk(a.byte_start, a.n, g0, lane));
   if constexpr (WIN) {
     // Descriptors fetched 64 at a time (lane j <- chunk c+j), read back with readlane:
     // one load round trip per 64 chunks. byte_start only seeds a scalar running sum, so
@@ -1108,6 +1117,16 @@ __global__ __launch_bounds__(TPB) void crc32_sweep_kernel(SweepArgs a) {
       }
       ++c;
     }
+  }
+  if constexpr (DYN == 0) {
+    break;
+  } else {
+    uint64_t nx = 0;
+    if (lane == 0) nx = atomicAdd(reinterpret_cast<unsigned long long*>(a.claim), 1ull);
+    g0 = (nwaves + readlane64(nx, 0)) * S;
+    if (g0 >= total) break;
+    g1 = g0 + S < total ? g0 + S : total;
+  }
   }
 }
 
@@ -1247,6 +1266,7 @@ __global__ __launch_bounds__(256) void crc32_plan_scan_kernel(PlanArgs a) {
     for (uint32_t k = 0; k < 4; ++k) cls_carry[k] += field16(round_cls, k);
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
+    a.small_total[4] = 0;  // the sweep's dynamic share counter
     a.small_total[0] = cls_base[3] + cls_total[3];
     a.small_total[1] = cls_base[1];
     a.small_total[2] = cls_base[2];
