@@ -76,7 +76,8 @@ constexpr uint64_t group_small_max(int mode) {
 // static first one; the DYN template parameter -- lost 0.6 % on C3, 1.3 % on C4 and 12 % on
 // C2: each claim pays a chunk search and a descriptor reload, and the tail it would
 // shorten was not there)
-constexpr int kNumVariants = 27;
+// 27 = 26 with 64-B lane runs (quad transpose) in the 16-lane groups of classes 2-3
+constexpr int kNumVariants = 28;
 constexpr int kDiagNoFold = 100;  // diagnostic timing build, selectable via ambrycrc_set_variant only
 
 // Message verify (message_kernels.hip): kMsgSlots CRC jobs per message, slot order

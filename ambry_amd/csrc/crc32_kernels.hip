@@ -862,11 +862,101 @@ __device__ __forceinline__ uint32_t group_crc_g(const uint8_t* __restrict__ base
   return crc;
 }
 
+// Group body with 64-B lane runs (G = 16, classes 2-3 of variant 26): the wave-mode
+// transpose inside each 16-lane group. A 1 KiB super-block is 4 loads per lane (load i:
+// lane gl <- bytes [16gl, 16gl+16) of 256-B block i, 256 B contiguous per group); the quad
+// transpose leaves lane gl = 4m + j holding the 64-B run [64m, 64m+64) of block j, which
+// it walks as one 16-step slice-by-4 chain; the lane state hops one super-block with
+// FOLD = x^(8*1024). Tree: gl bits 2, 3 merge the runs of a block (64, 128 B = POW[6, 7]),
+// bits 0, 1 the blocks (256, 512 B = POW[8, 9]). 18 LDS reads per 16 B-lane piece... per
+// KiB of chunk, against 24 for the 16-B-piece body; one super-block prefetched.
+template <bool NT>
+__device__ __forceinline__ void group_fix_piece(u32x4& w, int64_t p, uint64_t cs, uint32_t rinit) {
+  if (p < (int64_t)cs + 4 && p + 16 > (int64_t)cs) {
+    w = xor_init(w, p, cs, rinit);
+    if (p < (int64_t)cs) {
+      const uint32_t cut = (uint32_t)((int64_t)cs - p);
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const int lo = (int)cut - 4 * d;
+        const uint32_t m = lo <= 0 ? 0xFFFFFFFFu : (lo >= 4 ? 0u : (0xFFFFFFFFu << (8 * lo)));
+        w[d] &= m;
+      }
+    }
+  }
+}
+
+template <bool NT>
+__device__ __forceinline__ void group_load_sb(const GroupCtx& g, uint32_t sb, u32x4 (&x)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t p = g.p0 + (int64_t)sb * 1024 + 256 * i;
+    x[i] = u32x4{0u, 0u, 0u, 0u};
+    if (sb < g.nbw && g.body && p + 16 > (int64_t)g.cs)  // => floor16(cs) <= p < cb
+      x[i] = ld16<NT>(reinterpret_cast<const u32x4*>(g.base + p));
+  }
+}
+
+template <bool NT>
+__device__ __forceinline__ uint32_t group_crc_t4(const uint8_t* __restrict__ base, uint64_t cs, uint64_t len,
+                                                 uint32_t cin, uint32_t nbw, uint32_t lane, const LaneConst& k) {
+  constexpr uint32_t G = 16;
+  const uint32_t gl = lane & (G - 1);
+  const uint32_t rinit = ~cin;
+  const uint64_t ce = cs + len;
+  const uint64_t cb = aligned_end(cs, ce);
+  const bool body = cb > cs;
+  const int64_t p0 = (int64_t)cb - (int64_t)nbw * 1024 + 16 * (int64_t)gl;
+  const GroupCtx g{base, p0, cs, body, nbw, rinit};
+  const uint32_t t = (uint32_t)(ce - cb);
+  const uint32_t k0 = G - 1 - gl;  // trailing byte at distance k0 from the end (one per lane)
+  const uint32_t tb = k0 < t ? base[ce - 1 - k0] : 0u;
+  u32x4 nx[4];
+  group_load_sb<NT>(g, 0, nx);
+  uint32_t s = 0;
+#pragma unroll 1
+  for (uint32_t sb = 0; sb < nbw; ++sb) {
+    u32x4 x[4] = {nx[0], nx[1], nx[2], nx[3]};
+    group_load_sb<NT>(g, sb + 1, nx);  // none past nbw
+#pragma unroll
+    for (int i = 0; i < 4; ++i) group_fix_piece<NT>(x[i], p0 + (int64_t)sb * 1024 + 256 * i, cs, rinit);
+    quad_transpose_asm(x);
+    s = run_crc<4>(x, k, sb ? nib_mul(s, kFoldOff) : 0u);
+  }
+  uint32_t r = s;
+  if (nbw) {
+    r = tree_level_t4<2, 6>(r, lane);
+    r = tree_level_t4<3, 7>(r, lane);
+    r = tree_level_t4<0, 8>(r, lane);
+    r = tree_level_t4<1, 9>(r, lane);
+  }
+  r = __shfl(r, (int)(lane | (G - 1)));
+  if (t & 1u) r = nib_mul(r, kPowOff + kNibSetBytes * 0);
+  if (t & 2u) r = nib_mul(r, kPowOff + kNibSetBytes * 1);
+  if (t & 4u) r = nib_mul(r, kPowOff + kNibSetBytes * 2);
+  if (t & 8u) r = nib_mul(r, kPowOff + kNibSetBytes * 3);
+  uint32_t v = 0;
+  if (k0 < t) {
+    const uint64_t at = ce - 1 - k0;
+    uint32_t byte = tb;
+    if (at < cs + 4) byte ^= (rinit >> (8 * (uint32_t)(at - cs))) & 0xFFu;
+    const uint32_t j = k0 & 3;
+    v = lds_rd(((j >> 1) << 16) | (byte << 8) | ((j & 1) << 7) | ((lane & 31) << 2));
+    if (k0 & 4) v = nib_mul(v, kPowOff + kNibSetBytes * 2);
+    if (k0 & 8) v = nib_mul(v, kPowOff + kNibSetBytes * 3);
+  }
+  v = group_xor<G>(v);
+  uint32_t crc = r ^ v ^ 0xFFFFFFFFu;
+  if (len < 4) crc ^= rinit >> (8 * (uint32_t)len);
+  return crc;
+}
+
 // One size class [lo, hi) of the list, spread over all waves: wave w takes entries
 // [lo + w*per, lo + (w+1)*per), per a multiple of 64/G.
-template <int G, int NB, bool NT>
+template <int G, int NB, bool NT, bool T4 = false>
 __device__ __forceinline__ void group_class(const SweepArgs& a, uint64_t lo, uint64_t hi, uint32_t wave,
                                             uint64_t nwaves, uint32_t lane, const LaneConst& k) {
+  static_assert(!T4 || G == 16, "64-B run group body needs 16-lane groups");
   constexpr uint32_t S = 64 / G;
   if (hi <= lo) return;
   const uint64_t per = group_per<G>(hi - lo, nwaves);
@@ -886,14 +976,17 @@ __device__ __forceinline__ void group_class(const SweepArgs& a, uint64_t lo, uin
       cin = a.crc_in ? a.crc_in[ci] : 0u;
     }
     const uint64_t cb = aligned_end(off, off + len);
-    const uint32_t nb = (uint32_t)((cb - off + 16 * G - 1) / (16 * G));
+    constexpr uint32_t BLK = T4 ? 64 * G : 16 * G;  // bytes per chain step
+    const uint32_t nb = (uint32_t)((cb - off + BLK - 1) / BLK);
     uint32_t nbw = 0;
 #pragma unroll
     for (uint32_t q = 0; q < S; ++q) {
       const uint32_t x = __builtin_amdgcn_readlane(nb, q * G);
       nbw = x > nbw ? x : nbw;
     }
-    const uint32_t crc = group_crc_g<G, NB, NT>(a.base, off, len, cin, nbw, lane, k);
+    uint32_t crc;
+    if constexpr (T4) crc = group_crc_t4<NT>(a.base, off, len, cin, nbw, lane, k);
+    else crc = group_crc_g<G, NB, NT>(a.base, off, len, cin, nbw, lane, k);
     if ((lane & (G - 1)) == 0 && act) a.out[ci] = crc;
   }
 }
@@ -908,14 +1001,14 @@ __device__ __forceinline__ bool group_cls_has_work(const SweepArgs& a, uint32_t 
          (c4 > c3 && first_wave * group_per<16>(c4 - c3, nwaves) < c4 - c3);
 }
 
-template <bool NT>
+template <bool NT, bool T4 = false>
 __device__ __forceinline__ void group_phase_cls(const SweepArgs& a, uint32_t wave, uint64_t nwaves, uint32_t lane,
                                                 const LaneConst& k) {
   const uint64_t c1 = a.small_total[1], c2 = a.small_total[2], c3 = a.small_total[3], c4 = a.small_total[0];
   group_class<4, 4, NT>(a, 0, c1, wave, nwaves, lane, k);
   group_class<8, 8, NT>(a, c1, c2, wave, nwaves, lane, k);
-  group_class<16, 16, NT>(a, c2, c3, wave, nwaves, lane, k);
-  group_class<16, 64, NT>(a, c3, c4, wave, nwaves, lane, k);
+  group_class<16, 16, NT, T4>(a, c2, c3, wave, nwaves, lane, k);
+  group_class<16, 64, NT, T4>(a, c3, c4, wave, nwaves, lane, k);
 }
 
 // Group kernel: every chunk with 0 < len <= a.small_max (= 16*G*NB), whole, from the
@@ -979,7 +1072,7 @@ __global__ __launch_bounds__(TPB) void crc32_sweep_kernel(SweepArgs a) {
   // Fused group phase (GG > 0): the workgroup first takes its part of the small-chunk list.
   const uint64_t ns = GG > 0 ? *a.small_total : 0;
   const bool grp = GG > 0 && ns > 0 &&
-                   (GV == 3 ? group_cls_has_work(a, blockIdx.x, nwaves)
+                   (GV >= 3 ? group_cls_has_work(a, blockIdx.x, nwaves)
                             : (uint64_t)blockIdx.x * group_per<(GG > 0 ? GG : 16)>(ns, nwaves) < ns);
   if ((uint64_t)blockIdx.x * share >= total && !grp) return;  // uniform: no work for this workgroup
   fill_lds(a.img);
@@ -988,7 +1081,7 @@ __global__ __launch_bounds__(TPB) void crc32_sweep_kernel(SweepArgs a) {
   const uint32_t wave = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * gridDim.x + blockIdx.x);
   if constexpr (GG > 0) {
     if (grp) {
-      if constexpr (GV == 3) group_phase_cls<NT>(a, wave, nwaves, lane, make_lane_const(lane));
+      if constexpr (GV >= 3) group_phase_cls<NT, GV == 4>(a, wave, nwaves, lane, make_lane_const(lane));
       else group_phase<GG, GNB, NT>(a, ns, wave, nwaves, lane, make_lane_const(lane));
     }
   }
@@ -1347,6 +1440,8 @@ hipError_t launch_sweep(const SweepArgs& a, int grid, int variant, hipStream_t s
     case 25: hipLaunchKernelGGL((crc32_sweep_kernel<4, true, true, false, true, 0, -3, 16, 64>), dim3(grid), dim3(1024), 0, s, a); break;
     // 25 with the class-sized (G = 4/8/16/16), class-balanced group phase
     case 26: hipLaunchKernelGGL((crc32_sweep_kernel<4, true, true, false, true, 0, -3, 16, 64, 1024, 3>), dim3(grid), dim3(1024), 0, s, a); break;
+    // 26 with 64-B lane runs in the 16-lane groups of size classes 2-3 (4-16 KiB)
+    case 27: hipLaunchKernelGGL((crc32_sweep_kernel<4, true, true, false, true, 0, -3, 16, 64, 1024, 4>), dim3(grid), dim3(1024), 0, s, a); break;
     // timing-only diagnostics (wrong CRCs): 100 FOLD lookups removed, 101 no per-segment
     // atomic, 102 no wave tree
     case kDiagNoFold: hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, true, true, 1>), dim3(grid), dim3(1024), 0, s, a); break;
