@@ -122,13 +122,13 @@ struct DevCtx {
   // v_cndmask_b32_dpp, one x^(8*4096) fold per 64 B), U4 loads in flight; plus, for batches
   // of >= kGroupMinChunks chunks, whole chunks <= 16 KiB in the fused group phase, each size
   // class spread over all waves with a class-sized group (G = 4 / 8 / 16 lanes), and 64-B
-  // lane runs inside the 16-lane groups of the 4-16 KiB classes.
+  // lane runs inside the 8- and 16-lane groups (classes 1-3, 257 B - 16 KiB).
   // Measured (tools/sweep.py, bench_ladder.py, bench_messages.py; profiles/r01d_*): the
   // DPP-fused transpose beat 23 by 1.2-1.9 % on C3; the class-sized group phase took 100 B
   // chunks from 0.51 to 1.6 TB/s, 1 KiB from 3.8 to 5.0 TB/s and the 4 KiB-blob message
   // verify from 1.96 to 3.1 TiB/s; the group runs took 4 KiB chunks from 5.5 to 5.9 TB/s
-  // and 16 KiB from 5.9 to 6.5.
-  int variant = 27;
+  // and 16 KiB from 5.9 to 6.5, and in the 8-lane groups 512 B - 1 KiB chunks by 3-4 %.
+  int variant = 28;
   uint32_t* d_img = nullptr;
   void* d_ws = nullptr;
   size_t ws_bytes = 0;

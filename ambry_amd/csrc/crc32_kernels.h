@@ -77,7 +77,8 @@ constexpr uint64_t group_small_max(int mode) {
 // C2: each claim pays a chunk search and a descriptor reload, and the tail it would
 // shorten was not there)
 // 27 = 26 with 64-B lane runs (quad transpose) in the 16-lane groups of classes 2-3
-constexpr int kNumVariants = 28;
+// 28 = 27 with 64-B lane runs in the 8-lane groups of class 1 (257 B - 1 KiB) too
+constexpr int kNumVariants = 29;
 constexpr int kDiagNoFold = 100;  // diagnostic timing build, selectable via ambrycrc_set_variant only
 
 // Message verify (message_kernels.hip): kMsgSlots CRC jobs per message, slot order

@@ -886,50 +886,61 @@ __device__ __forceinline__ void group_fix_piece(u32x4& w, int64_t p, uint64_t cs
   }
 }
 
-template <bool NT>
+template <bool NT, int G>
 __device__ __forceinline__ void group_load_sb(const GroupCtx& g, uint32_t sb, u32x4 (&x)[4]) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int64_t p = g.p0 + (int64_t)sb * 1024 + 256 * i;
+    const int64_t p = g.p0 + (int64_t)sb * (64 * G) + (16 * G) * i;
     x[i] = u32x4{0u, 0u, 0u, 0u};
     if (sb < g.nbw && g.body && p + 16 > (int64_t)g.cs)  // => floor16(cs) <= p < cb
       x[i] = ld16<NT>(reinterpret_cast<const u32x4*>(g.base + p));
   }
 }
 
-template <bool NT>
+// Merge of the lanes' run states inside a group: gl bits 2.. (the runs of one block, shifts
+// 64 B * 2^b = POW[6 + b]), then bits 0, 1 (the blocks, 16G B * 2^b = POW[log2(16G) + b]).
+template <int G>
+__device__ __forceinline__ uint32_t group_tree_t4(uint32_t r, uint32_t lane) {
+  constexpr uint32_t LB = G == 8 ? 7u : 8u;  // log2(16G)
+  r = tree_level_t4<2, 6>(r, lane);
+  if constexpr (G == 16) r = tree_level_t4<3, 7>(r, lane);
+  r = tree_level_t4<0, LB>(r, lane);
+  r = tree_level_t4<1, LB + 1>(r, lane);
+  return r;
+}
+
+template <bool NT, int G>
 __device__ __forceinline__ uint32_t group_crc_t4(const uint8_t* __restrict__ base, uint64_t cs, uint64_t len,
                                                  uint32_t cin, uint32_t nbw, uint32_t lane, const LaneConst& k) {
-  constexpr uint32_t G = 16;
+  static_assert(G == 8 || G == 16, "64-B run groups are 8 or 16 lanes");
+  constexpr uint32_t BPL = 16u / G;  // trailing bytes per lane
+  constexpr uint32_t kFold = G == 16 ? kFoldOff : kPowOff + kNibSetBytes * 9;  // x^(8*64G)
   const uint32_t gl = lane & (G - 1);
   const uint32_t rinit = ~cin;
   const uint64_t ce = cs + len;
   const uint64_t cb = aligned_end(cs, ce);
   const bool body = cb > cs;
-  const int64_t p0 = (int64_t)cb - (int64_t)nbw * 1024 + 16 * (int64_t)gl;
+  const int64_t p0 = (int64_t)cb - (int64_t)nbw * (64 * G) + 16 * (int64_t)gl;
   const GroupCtx g{base, p0, cs, body, nbw, rinit};
   const uint32_t t = (uint32_t)(ce - cb);
-  const uint32_t k0 = G - 1 - gl;  // trailing byte at distance k0 from the end (one per lane)
-  const uint32_t tb = k0 < t ? base[ce - 1 - k0] : 0u;
+  const uint32_t k0 = BPL * (G - 1 - gl);
+  uint32_t tb[BPL];
+#pragma unroll
+  for (uint32_t i = 0; i < BPL; ++i) tb[i] = k0 + i < t ? base[ce - 1 - (k0 + i)] : 0u;
   u32x4 nx[4];
-  group_load_sb<NT>(g, 0, nx);
+  group_load_sb<NT, G>(g, 0, nx);
   uint32_t s = 0;
 #pragma unroll 1
   for (uint32_t sb = 0; sb < nbw; ++sb) {
     u32x4 x[4] = {nx[0], nx[1], nx[2], nx[3]};
-    group_load_sb<NT>(g, sb + 1, nx);  // none past nbw
+    group_load_sb<NT, G>(g, sb + 1, nx);  // none past nbw
 #pragma unroll
-    for (int i = 0; i < 4; ++i) group_fix_piece<NT>(x[i], p0 + (int64_t)sb * 1024 + 256 * i, cs, rinit);
+    for (int i = 0; i < 4; ++i) group_fix_piece<NT>(x[i], p0 + (int64_t)sb * (64 * G) + (16 * G) * i, cs, rinit);
     quad_transpose_asm(x);
-    s = run_crc<4>(x, k, sb ? nib_mul(s, kFoldOff) : 0u);
+    s = run_crc<4>(x, k, sb ? nib_mul(s, kFold) : 0u);
   }
   uint32_t r = s;
-  if (nbw) {
-    r = tree_level_t4<2, 6>(r, lane);
-    r = tree_level_t4<3, 7>(r, lane);
-    r = tree_level_t4<0, 8>(r, lane);
-    r = tree_level_t4<1, 9>(r, lane);
-  }
+  if (nbw) r = group_tree_t4<G>(r, lane);
   r = __shfl(r, (int)(lane | (G - 1)));
   if (t & 1u) r = nib_mul(r, kPowOff + kNibSetBytes * 0);
   if (t & 2u) r = nib_mul(r, kPowOff + kNibSetBytes * 1);
@@ -937,11 +948,17 @@ __device__ __forceinline__ uint32_t group_crc_t4(const uint8_t* __restrict__ bas
   if (t & 8u) r = nib_mul(r, kPowOff + kNibSetBytes * 3);
   uint32_t v = 0;
   if (k0 < t) {
-    const uint64_t at = ce - 1 - k0;
-    uint32_t byte = tb;
-    if (at < cs + 4) byte ^= (rinit >> (8 * (uint32_t)(at - cs))) & 0xFFu;
-    const uint32_t j = k0 & 3;
-    v = lds_rd(((j >> 1) << 16) | (byte << 8) | ((j & 1) << 7) | ((lane & 31) << 2));
+#pragma unroll
+    for (uint32_t i = 0; i < BPL; ++i) {
+      const uint32_t kk = k0 + i;
+      if (kk < t) {
+        const uint64_t at = ce - 1 - kk;
+        uint32_t byte = tb[i];
+        if (at < cs + 4) byte ^= (rinit >> (8 * (uint32_t)(at - cs))) & 0xFFu;
+        const uint32_t j = kk & 3;
+        v ^= lds_rd(((j >> 1) << 16) | (byte << 8) | ((j & 1) << 7) | ((lane & 31) << 2));
+      }
+    }
     if (k0 & 4) v = nib_mul(v, kPowOff + kNibSetBytes * 2);
     if (k0 & 8) v = nib_mul(v, kPowOff + kNibSetBytes * 3);
   }
@@ -956,7 +973,7 @@ __device__ __forceinline__ uint32_t group_crc_t4(const uint8_t* __restrict__ bas
 template <int G, int NB, bool NT, bool T4 = false>
 __device__ __forceinline__ void group_class(const SweepArgs& a, uint64_t lo, uint64_t hi, uint32_t wave,
                                             uint64_t nwaves, uint32_t lane, const LaneConst& k) {
-  static_assert(!T4 || G == 16, "64-B run group body needs 16-lane groups");
+  static_assert(!T4 || G == 8 || G == 16, "64-B run group body needs 8- or 16-lane groups");
   constexpr uint32_t S = 64 / G;
   if (hi <= lo) return;
   const uint64_t per = group_per<G>(hi - lo, nwaves);
@@ -985,7 +1002,7 @@ __device__ __forceinline__ void group_class(const SweepArgs& a, uint64_t lo, uin
       nbw = x > nbw ? x : nbw;
     }
     uint32_t crc;
-    if constexpr (T4) crc = group_crc_t4<NT>(a.base, off, len, cin, nbw, lane, k);
+    if constexpr (T4) crc = group_crc_t4<NT, G>(a.base, off, len, cin, nbw, lane, k);
     else crc = group_crc_g<G, NB, NT>(a.base, off, len, cin, nbw, lane, k);
     if ((lane & (G - 1)) == 0 && act) a.out[ci] = crc;
   }
@@ -1001,12 +1018,12 @@ __device__ __forceinline__ bool group_cls_has_work(const SweepArgs& a, uint32_t 
          (c4 > c3 && first_wave * group_per<16>(c4 - c3, nwaves) < c4 - c3);
 }
 
-template <bool NT, bool T4 = false>
+template <bool NT, bool T4 = false, bool T4C1 = false>
 __device__ __forceinline__ void group_phase_cls(const SweepArgs& a, uint32_t wave, uint64_t nwaves, uint32_t lane,
                                                 const LaneConst& k) {
   const uint64_t c1 = a.small_total[1], c2 = a.small_total[2], c3 = a.small_total[3], c4 = a.small_total[0];
   group_class<4, 4, NT>(a, 0, c1, wave, nwaves, lane, k);
-  group_class<8, 8, NT>(a, c1, c2, wave, nwaves, lane, k);
+  group_class<8, 8, NT, T4C1>(a, c1, c2, wave, nwaves, lane, k);
   group_class<16, 16, NT, T4>(a, c2, c3, wave, nwaves, lane, k);
   group_class<16, 64, NT, T4>(a, c3, c4, wave, nwaves, lane, k);
 }
@@ -1081,7 +1098,7 @@ __global__ __launch_bounds__(TPB) void crc32_sweep_kernel(SweepArgs a) {
   const uint32_t wave = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * gridDim.x + blockIdx.x);
   if constexpr (GG > 0) {
     if (grp) {
-      if constexpr (GV >= 3) group_phase_cls<NT, GV == 4>(a, wave, nwaves, lane, make_lane_const(lane));
+      if constexpr (GV >= 3) group_phase_cls<NT, GV >= 4, GV == 5>(a, wave, nwaves, lane, make_lane_const(lane));
       else group_phase<GG, GNB, NT>(a, ns, wave, nwaves, lane, make_lane_const(lane));
     }
   }
@@ -1442,6 +1459,8 @@ hipError_t launch_sweep(const SweepArgs& a, int grid, int variant, hipStream_t s
     case 26: hipLaunchKernelGGL((crc32_sweep_kernel<4, true, true, false, true, 0, -3, 16, 64, 1024, 3>), dim3(grid), dim3(1024), 0, s, a); break;
     // 26 with 64-B lane runs in the 16-lane groups of size classes 2-3 (4-16 KiB)
     case 27: hipLaunchKernelGGL((crc32_sweep_kernel<4, true, true, false, true, 0, -3, 16, 64, 1024, 4>), dim3(grid), dim3(1024), 0, s, a); break;
+    // 27 with 64-B lane runs in the 8-lane groups of class 1 (257 B - 1 KiB) too
+    case 28: hipLaunchKernelGGL((crc32_sweep_kernel<4, true, true, false, true, 0, -3, 16, 64, 1024, 5>), dim3(grid), dim3(1024), 0, s, a); break;
     // timing-only diagnostics (wrong CRCs): 100 FOLD lookups removed, 101 no per-segment
     // atomic, 102 no wave tree
     case kDiagNoFold: hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, true, true, 1>), dim3(grid), dim3(1024), 0, s, a); break;
