@@ -91,7 +91,7 @@ struct MsgArgs {
   const uint64_t* msg_off;  // [m]
   uint64_t m;
   const uint32_t* img;      // table image (T0 used by the header CRC)
-  uint64_t* job_off;        // [5m]
+  uint64_t* job_off;        // [5m], slot-major: job k*m + i = slot k of message i
   uint64_t* job_len;        // [5m]
   uint32_t* expected;       // [5m]
   const uint8_t* mismatch;  // [5m]

@@ -8,7 +8,8 @@
 //   msg_parse_kernel   one thread per message: header version, header CRC (<= 32 B,
 //                      slice-by-4 through LDS tables), header constraints, and up to five record
 //                      CRC jobs (enc key, properties, update, user metadata, blob) =
-//                      [record start, record end - 8) with the stored big-endian CRC
+//                      [record start, record end - 8) with the stored big-endian CRC; job
+//                      k*m + i is slot k of message i (slot-major: coalesced stores)
 //   plan + sweep       the batch CRC engine over the 5m jobs (crc32_kernels.hip)
 //   verify             mismatch flags
 //   msg_reduce_kernel  per-message status bits
@@ -84,11 +85,10 @@ __global__ __launch_bounds__(256) void msg_parse_kernel(MsgArgs a) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.m) return;
   const uint64_t off = a.msg_off[i];
-  for (int k = 0; k < kMsgSlots; ++k) {
-    a.job_off[kMsgSlots * i + k] = 0;
-    a.job_len[kMsgSlots * i + k] = 0;
-    a.expected[kMsgSlots * i + k] = 0;
-  }
+  // Jobs are slot-major (job k*m + i = slot k of message i), so each slot's store below is
+  // one coalesced wave store; every slot is written exactly once.
+  uint64_t jo[kMsgSlots] = {0, 0, 0, 0, 0}, jl[kMsgSlots] = {0, 0, 0, 0, 0};
+  uint32_t ex[kMsgSlots] = {0, 0, 0, 0, 0};
   uint32_t status = 0;
   uint64_t end = 0;
   do {
@@ -173,11 +173,17 @@ __global__ __launch_bounds__(256) void msg_parse_kernel(MsgArgs a) {
         }
       const uint64_t stored = be64(p + e - 8);
       if (stored >> 32) status |= kRecordBit[k];  // a CRC32 never has upper bits: mismatch regardless
-      a.job_off[kMsgSlots * i + k] = off + (uint64_t)rel[k];
-      a.job_len[kMsgSlots * i + k] = e - (uint64_t)rel[k] - 8;
-      a.expected[kMsgSlots * i + k] = (uint32_t)stored;
+      jo[k] = off + (uint64_t)rel[k];
+      jl[k] = e - (uint64_t)rel[k] - 8;
+      ex[k] = (uint32_t)stored;
     }
   } while (false);
+#pragma unroll
+  for (int k = 0; k < kMsgSlots; ++k) {
+    a.job_off[(uint64_t)k * a.m + i] = jo[k];
+    a.job_len[(uint64_t)k * a.m + i] = jl[k];
+    a.expected[(uint64_t)k * a.m + i] = ex[k];
+  }
   a.status[i] = status;
   if (a.msg_end) a.msg_end[i] = end ? off + end : 0;
 }
@@ -187,7 +193,7 @@ __global__ __launch_bounds__(256) void msg_reduce_kernel(MsgArgs a) {
   if (i >= a.m) return;
   uint32_t s = a.status[i];
   for (int k = 0; k < kMsgSlots; ++k)
-    if (a.mismatch[kMsgSlots * i + k]) s |= kRecordBit[k];
+    if (a.mismatch[(uint64_t)k * a.m + i]) s |= kRecordBit[k];
   a.status[i] = s;
 }
 
