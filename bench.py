@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--prewarm-s", type=float, default=0.3, help="untimed clock-ramp run before warmup")
     ap.add_argument("--quiet", action="store_true", help="no progress lines on stderr")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="init the RCCL process group and all-gather even at WORLD_SIZE=1 (exercises the N>1 path)")
     return ap.parse_args()
 
 
@@ -195,6 +197,12 @@ def host_path_rate(torch, args):
 
 def main():
     args = parse()
+    # stdout carries exactly one JSON line (rank 0). Native libraries print to fd 1 on their
+    # own (RCCL's version banner at communicator init), so fd 1 is pointed at stderr for
+    # the run and the result is written to a saved copy of the original stdout.
+    sys.stdout.flush()
+    result_fd = os.dup(1)
+    os.dup2(2, 1)
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -203,10 +211,14 @@ def main():
     if world != args.gpus:
         log(args, f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     dist = None
-    if world > 1:
+    use_dist = world > 1 or args.force_dist
+    if use_dist:
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
@@ -223,11 +235,11 @@ def main():
 
     log(args, f"rank {rank}/{world}: building workload {args.config}")
     buf, off_t, len_t, n, total, chunk, desc = build_workload(torch, dev, args, rank)
-    gathered = torch.empty(world * n, dtype=torch.int32, device=dev) if world > 1 else None
+    gathered = torch.empty(world * n, dtype=torch.int32, device=dev) if use_dist else None
 
     def step():
         out = D.crc32_batch(buf, off_t, len_t)
-        if world > 1:
+        if use_dist:
             dist.all_gather_into_tensor(gathered, out)
         return out
 
@@ -269,6 +281,12 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    allgather_ok = None
+    if use_dist:  # this rank's CRCs must sit at its slot of the gathered vector
+        allgather_ok = bool(torch.equal(gathered[rank * n:(rank + 1) * n], out))
+        flag = torch.tensor([1 if allgather_ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        allgather_ok = bool(flag.item())
     read_roof = measure_read_roof(torch, D, buf, buf.numel(), dev.index) if args.config != "c4" else None
     crcs = out.cpu().numpy().view("uint32")
     step_bytes = total  # per rank
@@ -291,7 +309,7 @@ def main():
         "dtype": "u8",
         "data": "synthetic (device splitmix64 bytes; no dataset)",
         "config": {"workload": desc, "chunks_per_gpu": n, "chunk_bytes": chunk, "bytes_per_gpu_step": total,
-                   "parallelism": f"shard{world}" + ("+rccl_allgather" if world > 1 else ""),
+                   "parallelism": f"shard{world}" + ("+rccl_allgather" if use_dist else ""),
                    "kernel_variant": D.get_variant(dev.index),
                    "grid_workgroups": D.grid_size(dev.index)},
         "roofline": {
@@ -310,6 +328,7 @@ def main():
                                            if achieved and read_roof else None),
         },
         "timing": {"wall_s": round(elapsed, 4), "stream_event_ms": round(ev_ms, 3), "kernel_launches": launches},
+        "allgather_ok": allgather_ok,
     }
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc) and args.config == "c3":
@@ -335,7 +354,8 @@ def main():
             torch.cuda.empty_cache()
             result["host_path"] = host_path_rate(torch, args)
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        sys.stdout.flush()
+        os.write(result_fd, (json.dumps(result) + "\n").encode())
     if dist:
         dist.destroy_process_group()
 
