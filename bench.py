@@ -120,8 +120,18 @@ def cpu_baseline(buf, off_t, len_t, n, args):
             res[(zl, th)] = (passes * int(ln.sum()) / el / 2**30, passes, out)
     assert np.array_equal(res[(True, threads)][2], res[(False, threads)][2]), "zlib vs restatement"
     gibs, passes, out = res[(False, threads)]
+    cpu_model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu_model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
     return {
         "value": round(gibs, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+        "cpu_model": cpu_model, "nproc": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
         "sample": f"{sample_chunks} chunks x {int(ln[0]) if len(set(ln.tolist())) == 1 else 'mixed'} B "
                   f"(first chunks of the same workload, D2H-copied) x {passes} passes; oracle/crc32_ref.c "
                   f"slice-by-8 restating Crc32.java:55-98, {threads} pthreads",
