@@ -78,6 +78,8 @@ constexpr uint64_t group_small_max(int mode) {
 // shorten was not there)
 // 27 = 26 with 64-B lane runs (quad transpose) in the 16-lane groups of classes 2-3
 // 28 = 27 with 64-B lane runs in the 8-lane groups of class 1 (257 B - 1 KiB) too
+// (two super-blocks, 8 loads per lane, in flight in the sweep body: -6 % on C3, -4 % on C2
+// at the 128-VGPR cap)
 constexpr int kNumVariants = 29;
 constexpr int kDiagNoFold = 100;  // diagnostic timing build, selectable via ambrycrc_set_variant only
 
