@@ -348,3 +348,22 @@ def test_timing_hook(gpu):
         assert cnt == 1 and ms > 0
     finally:
         gpu.timing_enable(0, False)
+
+
+@pytest.mark.parametrize("shift", [1, 3, 8, 13])
+def test_misaligned_base_pointer(gpu, oracle, shift):
+    """d_base itself off 16-B alignment (a ByteBuf slice at any address): every chunk's
+    alignment math is relative to d_base, so the kernels must still be bit-exact and read
+    nothing before d_base. Wave mode and the group phase (>= 16384 chunks) both run."""
+    rng = np.random.default_rng(900 + shift)
+    mem = stream_bytes(90 + shift, 0, 6 << 20)
+    full = dev_bytes(mem)
+    base = full[shift:]  # data_ptr() = allocation + shift
+    view = mem[shift:]
+    for n, hi in ((300, 1 << 20), (20000, 20000)):
+        ln = rng.integers(0, hi, size=n)
+        ln[:6] = [0, 1, 15, 16, 17, 4095]
+        off = rng.integers(0, len(view) - hi, size=n)
+        off[:4] = [0, 1, 2, 3]  # chunks at the very start of the shifted base
+        got = run_batch(gpu, view, off, ln, mem_dev=base)
+        assert np.array_equal(got, oracle.batch(view, off, ln, threads=8)), (shift, n)
