@@ -367,3 +367,31 @@ def test_misaligned_base_pointer(gpu, oracle, shift):
         off[:4] = [0, 1, 2, 3]  # chunks at the very start of the shifted base
         got = run_batch(gpu, view, off, ln, mem_dev=base)
         assert np.array_equal(got, oracle.batch(view, off, ln, threads=8)), (shift, n)
+
+
+def test_hip_graph_capture_and_replay(gpu, oracle):
+    """ambrycrc_batch_dev with a caller workspace is stream-capture safe:
+    captured once into a HIP graph and replayed after the bytes change, it CRCs the new bytes."""
+    torch = _torch()
+    mem = stream_bytes(31, 0, 3 << 20)
+    base = dev_bytes(mem)
+    off = dev_u64([0, 5, 4096, 1 << 20])
+    ln = dev_u64([100, 70000, 1 << 20, (2 << 20) - 3])
+    out = torch.empty(4, dtype=torch.int32, device="cuda")
+    ws = torch.empty(gpu.workspace_bytes(4), dtype=torch.uint8, device="cuda")
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        gpu.crc32_batch(base, off, ln, out=out, workspace=ws)
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g, stream=s):
+            gpu.crc32_batch(base, off, ln, out=out, workspace=ws)
+    torch.cuda.synchronize()
+    offs, lens = [0, 5, 4096, 1 << 20], [100, 70000, 1 << 20, (2 << 20) - 3]
+    for seed in (32, 33):
+        new = stream_bytes(seed, 0, 3 << 20)
+        base.copy_(torch.from_numpy(new).cuda())
+        g.replay()
+        torch.cuda.synchronize()
+        assert np.array_equal(host_u32(out), oracle.batch(new, offs, lens)), seed

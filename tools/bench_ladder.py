@@ -151,6 +151,26 @@ def gpu_rows(size: int, gib: float, reps: int, variant: int = 0, check: bool = T
     torch.cuda.synchronize()
     call["us_per_call_abi_host"] = round((time.perf_counter() - t0) / calls * 1e6, 2)
     call["us_per_call_abi_stream"] = round(e0.elapsed_time(e1) / calls * 1e3, 2)
+    # the same call captured once in a HIP graph (torch.cuda.CUDAGraph) and replayed:
+    # the launch-bound single-chunk case without per-launch submission cost
+    g = torch.cuda.CUDAGraph()
+    cap = torch.cuda.Stream()
+    cap.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(cap):
+        D.crc32_batch(buf, o1, l1, out=out1, workspace=ws1)  # warm on the capture stream
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g, stream=cap):
+            D.crc32_batch(buf, o1, l1, out=out1, workspace=ws1)
+    torch.cuda.synchronize()
+    for _ in range(20):
+        g.replay()
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(calls):
+        g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    call["us_per_call_graph_stream"] = round(e0.elapsed_time(e1) / calls * 1e3, 2)
     D.set_variant(0, default)
     del buf, off, ln, out, ws
     torch.cuda.empty_cache()
