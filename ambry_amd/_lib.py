@@ -29,6 +29,7 @@ _SIGNATURES = [
     ("ambrycrc_version", ctypes.c_char_p, []),
     ("ambrycrc_update", ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]),
     ("ambrycrc_update_byte", ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_int]),
+    ("ambrycrc_host_impl", ctypes.c_char_p, []),
     ("ambrycrc_combine", ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]),
     ("ambrycrc_zeros", ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint64]),
     ("ambrycrc_workspace_bytes", ctypes.c_size_t, [ctypes.c_size_t]),

@@ -18,6 +18,7 @@
 #include "crc32_gf2.h"
 #include "crc32_kernels.h"
 #include "crc32_layout.h"
+#include "host_crc.h"
 
 using namespace ambrycrc;
 
@@ -36,23 +37,6 @@ struct HostTables {
 const HostTables& host_tables() {
   static const HostTables tables;  // C++11 thread-safe static init
   return tables;
-}
-
-// Register-level slice-by-8 (the register is the bit-inverted CRC, as Crc32.java keeps it).
-uint32_t host_update_reg(uint32_t c, const uint8_t* p, size_t n) {
-  const HostTables& h = host_tables();
-  while (n >= 8) {
-    uint32_t lo, hi;
-    memcpy(&lo, p, 4);
-    memcpy(&hi, p + 4, 4);
-    lo ^= c;
-    c = h.t[7][lo & 0xff] ^ h.t[6][(lo >> 8) & 0xff] ^ h.t[5][(lo >> 16) & 0xff] ^ h.t[4][lo >> 24] ^
-        h.t[3][hi & 0xff] ^ h.t[2][(hi >> 8) & 0xff] ^ h.t[1][(hi >> 16) & 0xff] ^ h.t[0][hi >> 24];
-    p += 8;
-    n -= 8;
-  }
-  while (n--) c = (c >> 8) ^ h.t[0][(c ^ *p++) & 0xff];
-  return c;
 }
 
 uint32_t host_xpow8(uint64_t n) {
@@ -456,6 +440,8 @@ uint32_t ambrycrc_update(uint32_t crc, const void* p, size_t n) {
   if (!p || n == 0) return crc;
   return ~host_update_reg(~crc, static_cast<const uint8_t*>(p), n);
 }
+
+const char* ambrycrc_host_impl(void) { return host_impl_name(host_impl()); }
 
 uint32_t ambrycrc_update_byte(uint32_t crc, int b) {
   const HostTables& h = host_tables();

@@ -120,6 +120,7 @@ def cpu_baseline(buf, off_t, len_t, n, args):
             res[(zl, th)] = (passes * int(ln.sum()) / el / 2**30, passes, out)
     assert np.array_equal(res[(True, threads)][2], res[(False, threads)][2]), "zlib vs restatement"
     gibs, passes, out = res[(False, threads)]
+    clmul = host_clmul_rate(host, off, ln, out, threads, args.cpu_seconds / 4)
     cpu_model = None
     try:
         with open("/proc/cpuinfo") as f:
@@ -139,8 +140,53 @@ def cpu_baseline(buf, off_t, len_t, n, args):
         "zlib": {"gibs": round(res[(True, threads)][0], 3), "cores": threads,
                  "single_thread_gibs": round(res[(True, 1)][0], 3),
                  "what": "system zlib 1.2.11 crc32_z (the function java.util.zip.CRC32 wraps), same sample"},
+        "host_clmul": clmul,
         "_out": out,
     }
+
+
+def host_clmul_rate(host, off, ln, expect, threads, seconds):
+    """The library's own CPU path (ambrycrc_update: carry-less-multiply fold, the class of
+    HotSpot's CRC32 intrinsic) on the same sample, 1 thread and `threads` threads (ctypes
+    releases the GIL for the call). Not the baseline: a check on what the JVM could do."""
+    import ctypes
+    import threading
+
+    import numpy as np
+
+    import ambry_amd
+
+    lib = ambry_amd.lib()
+    base = host.ctypes.data
+    offs, lens = [int(o) for o in off], [int(x) for x in ln]
+    got = np.array([lib.ambrycrc_update(0, base + o, n) for o, n in zip(offs, lens)], dtype=np.uint32)
+    ok = bool(np.array_equal(got, np.asarray(expect, dtype=np.uint32)))
+
+    def run(th):
+        passes = [0] * th
+        stop = time.perf_counter() + seconds
+
+        def worker(t):
+            idx = list(range(t, len(offs), th))
+            while True:
+                for i in idx:
+                    lib.ambrycrc_update(0, ctypes.c_void_p(base + offs[i]), lens[i])
+                passes[t] += 1
+                if time.perf_counter() >= stop:
+                    break
+
+        t0 = time.perf_counter()
+        ws = [threading.Thread(target=worker, args=(t,)) for t in range(th)]
+        for w in ws:
+            w.start()
+        for w in ws:
+            w.join()
+        el = time.perf_counter() - t0
+        return sum(passes[t] * sum(lens[t::th]) for t in range(th)) / el / 2**30
+
+    return {"impl": lib.ambrycrc_host_impl().decode(), "single_thread_gibs": round(run(1), 3),
+            "gibs": round(run(threads), 3), "cores": threads, "parity_vs_port": ok,
+            "what": "libambrycrc ambrycrc_update on the host (CLMUL fold; HotSpot-intrinsic class), same sample"}
 
 
 def measure_read_roof(torch, D, buf, total, device):

@@ -73,6 +73,14 @@ uint32_t ambrycrc_update(uint32_t crc, const void* p, size_t n);
 /* One byte: Crc32.update(int b) (Crc32.java:146-148). */
 uint32_t ambrycrc_update_byte(uint32_t crc, int b);
 
+/* Name of the CPU implementation ambrycrc_update runs: "vpclmul" (AVX-512
+ * carry-less-multiply fold), "pclmul" (SSE fold) or "slice8" (the table loop of
+ * Crc32.java:55-98). Chosen once per process from the CPU's features; the
+ * environment variable AMBRYCRC_HOST_IMPL can lower it (tests, benches). Inputs
+ * under 64 B always take slice8. No Java counterpart (HotSpot's CRC32 intrinsic
+ * makes the same choice inside the JVM). */
+const char* ambrycrc_host_impl(void);
+
 /* crc(A||B) from crc(A), crc(B) and |B| (zlib crc32_combine semantics). No Java
  * counterpart in Ambry; it is what lets a chunk be split across lanes/GPUs and
  * lets a blob record's CRC be derived from the blob's (PutMessageFormatInputStream.java:116-120). */

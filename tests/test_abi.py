@@ -124,3 +124,36 @@ def test_batch_dev_without_init_fails_loudly(ambry):
     rc = ambry.lib().ambrycrc_batch_dev(ctypes.c_void_p(16), ctypes.c_void_p(16), ctypes.c_void_p(16), None,
                                         ctypes.c_void_p(16), 1, None, 0, None)
     assert rc == AMBRYCRC_ENOINIT
+
+
+def test_host_update_every_cpu_impl():
+    """Each host implementation (slice-by-8, SSE PCLMULQDQ fold, AVX-512 VPCLMULQDQ fold) is
+    bit-exact with zlib (java.util.zip.CRC32's function) at every length 0..1100 (crossing the
+    64 B and 256 B dispatch points and every fold remainder), at unaligned offsets, with a
+    running crc_in, and at large sizes. Each runs in its own process (the choice is per process)."""
+    import subprocess
+    import sys
+
+    code = r"""
+import sys, zlib
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import ambry_amd
+rng = np.random.default_rng(7)
+d = rng.integers(0, 256, (1 << 20) + 64, dtype=np.uint8).tobytes()
+for n in list(range(0, 1101)) + [4095, 4096, 65535, 65536, 1 << 20]:
+    for off in (0, 3, 13):
+        b = d[off:off + n]
+        for ci in (0, 0xDEADBEEF):
+            assert ambry_amd.crc32(b, ci) == zlib.crc32(b, ci), (n, off, ci)
+print(ambry_amd.lib().ambrycrc_host_impl().decode())
+"""
+    seen = []
+    for impl in ("slice8", "pclmul", "vpclmul"):
+        env = dict(os.environ, AMBRYCRC_HOST_IMPL=impl)
+        r = subprocess.run([sys.executable, "-c", code, ROOT], env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        seen.append(r.stdout.strip())
+    assert seen[0] == "slice8"
+    # a CPU without the feature keeps the best it has; this image's Xeon has both
+    assert seen[1] in ("slice8", "pclmul") and seen[2] in ("slice8", "pclmul", "vpclmul")
