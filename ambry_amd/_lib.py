@@ -62,6 +62,8 @@ _SIGNATURES = [
     ("ambrycrc_timing_enable", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     ("ambrycrc_timing_collect", ctypes.c_int,
      [ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),
+    ("ambrycrc_timing_collect_each", ctypes.c_int,
+     [ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     ("ambrycrc_grid_size", ctypes.c_int, [ctypes.c_int]),
     ("ambrycrc_fill_random_dev", ctypes.c_int,
      [_u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]),

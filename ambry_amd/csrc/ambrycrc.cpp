@@ -765,21 +765,39 @@ int ambrycrc_timing_enable(int device, int enable) {
   return AMBRYCRC_OK;
 }
 
-int ambrycrc_timing_collect(int device, double* total_ms, int* launches) {
+int ambrycrc_timing_collect_each(int device, float* ms_out, int cap, int* launches) {
   DevCtx* c = ctx_for(device);
   if (!c) return AMBRYCRC_ENOINIT;
+  if (cap < 0 || (cap > 0 && !ms_out)) return AMBRYCRC_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  double sum = 0;
   int cnt = 0;
   for (auto& e : c->pending) {
     if (hipEventSynchronize(e.b) != hipSuccess) return AMBRYCRC_EHIP;
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, e.a, e.b) != hipSuccess) return AMBRYCRC_EHIP;
-    sum += ms;
+    if (cnt < cap) ms_out[cnt] = ms;
     ++cnt;
     c->free_events.push_back(e);
   }
   c->pending.clear();
+  if (launches) *launches = cnt;
+  return AMBRYCRC_OK;
+}
+
+int ambrycrc_timing_collect(int device, double* total_ms, int* launches) {
+  DevCtx* c = ctx_for(device);
+  if (!c) return AMBRYCRC_ENOINIT;
+  std::vector<float> ms;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    ms.resize(c->pending.size() + 4096);  // room for launches recorded meanwhile
+  }
+  int cnt = 0;
+  const int rc = ambrycrc_timing_collect_each(device, ms.data(), (int)ms.size(), &cnt);
+  if (rc != AMBRYCRC_OK) return rc;
+  double sum = 0;
+  cnt = std::min(cnt, (int)ms.size());
+  for (int i = 0; i < cnt; ++i) sum += ms[i];
   if (total_ms) *total_ms = sum;
   if (launches) *launches = cnt;
   return AMBRYCRC_OK;

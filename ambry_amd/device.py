@@ -141,6 +141,14 @@ def timing_collect(device: int = 0):
     return ms.value, cnt.value
 
 
+def timing_collect_each(device: int = 0, cap: int = 4096):
+    """Per-launch sweep-kernel durations (ms, launch order) since the last collect."""
+    buf = (ctypes.c_float * cap)()
+    cnt = ctypes.c_int()
+    check(lib().ambrycrc_timing_collect_each(device, buf, cap, ctypes.byref(cnt)), "ambrycrc_timing_collect_each")
+    return [buf[i] for i in range(min(cap, cnt.value))]
+
+
 def workspace_bytes(n: int) -> int:
     """Bytes of caller workspace ambrycrc_batch_dev needs for n chunks."""
     return lib().ambrycrc_workspace_bytes(n)

@@ -328,7 +328,9 @@ def main():
         dist.barrier()
     wall = time.perf_counter() - t0
     D.timing_enable(dev.index, False)
-    kern_ms, launches = D.timing_collect(dev.index)
+    kern_each = D.timing_collect_each(dev.index)
+    kern_ms, launches = sum(kern_each), len(kern_each)
+    kern_median_ms = float(sorted(kern_each)[len(kern_each) // 2]) if kern_each else None
     ev_ms = ev0.elapsed_time(ev1)
 
     elapsed = wall
@@ -377,6 +379,7 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
             "traffic": None,
             "kernel_avg_ms": round(kern_avg_s * 1e3, 4),
+            "kernel_median_ms": round(kern_median_ms, 4) if kern_median_ms else None,
             "algorithmic_bytes_per_launch": alg_bytes,
             "value_frac_of_peak": round(value * 2**30 / 1e9 / world / HBM_PEAK_GBS, 4),
             "measured_read_roof": read_roof,

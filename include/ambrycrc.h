@@ -230,6 +230,9 @@ int ambrycrc_set_grid(int device, int workgroups);
  * and returns the sum and count of those durations since the last collect. */
 int ambrycrc_timing_enable(int device, int enable);
 int ambrycrc_timing_collect(int device, double* total_ms, int* launches);
+/* As ambrycrc_timing_collect, but writes each launch's duration (ms, launch order) to
+ * ms_out[0 .. min(cap, launches)) so a caller can report the median; *launches is the total. */
+int ambrycrc_timing_collect_each(int device, float* ms_out, int cap, int* launches);
 
 /* Number of workgroups the sweep kernel launches with on `device` (0 if unknown). */
 int ambrycrc_grid_size(int device);
