@@ -288,8 +288,20 @@ int ensure_ws(DevCtx* c, size_t need) {
   return AMBRYCRC_OK;
 }
 
+// Largest chunk the group phase takes whole for a batch of n chunks on c's variant (0: none).
+uint64_t batch_small_max(const DevCtx* c, size_t n) {
+  if (n < kGroupMinChunks) return 0;
+  const bool grouped = c->variant >= 14 && c->variant < 20;
+  const int group_mode = grouped ? c->variant - 13 : 0;
+  return c->variant == 20   ? group_small_max(4)
+         : c->variant == 21 ? group_small_max(2)
+         : c->variant >= 22 ? group_small_max(5)
+                            : group_small_max(group_mode);
+}
+
+// exp_fill: SweepArgs::exp_fill (message verify; honoured by variants 26-28 only).
 int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len, const uint32_t* crc_in,
-                  uint32_t* out, size_t n, void* ws, hipStream_t s) {
+                  uint32_t* out, size_t n, void* ws, hipStream_t s, uint32_t* exp_fill = nullptr) {
   if (n == 0) return AMBRYCRC_OK;
   PlanArgs p;
   p.off = off;
@@ -308,11 +320,7 @@ int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uin
   const bool grouped = c->variant >= 14 && c->variant < 20;
   const int sweep_variant = grouped ? 0 : c->variant;
   const int group_mode = grouped ? c->variant - 13 : 0;
-  p.small_max = c->variant == 20   ? group_small_max(4)
-                : c->variant == 21 ? group_small_max(2)
-                : c->variant >= 22 ? group_small_max(5)
-                                   : group_small_max(group_mode);
-  if (n < kGroupMinChunks) p.small_max = 0;
+  p.small_max = batch_small_max(c, n);
   hipError_t e = launch_plan(p, s);
   if (e != hipSuccess) return AMBRYCRC_EHIP;
   SweepArgs t;
@@ -328,6 +336,7 @@ int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uin
   t.small_total = p.small_total;
   t.claim = p.small_total + 4;
   t.small_idx = p.small_idx;
+  t.exp_fill = exp_fill;
   EventPair ev{nullptr, nullptr};
   if (c->timing) {
     std::lock_guard<std::mutex> g(c->mu);
@@ -856,9 +865,14 @@ int ambrycrc_verify_messages_dev(const uint8_t* d_region, uint64_t region_len, c
   a.mismatch = mism;
   a.status = d_status;
   a.msg_end = d_msg_end;
+  // The class-sized group phase (variants 26-28) reads the stored CRCs of the records it
+  // takes whole; the parse kernel reads the rest.
+  const bool inline_exp = c->variant >= 26 && c->variant <= 28;
+  a.inline_max = inline_exp ? batch_small_max(c, j) : 0;
   void* batch_ws = w + ((j * 2 * sizeof(uint64_t) + j * 2 * sizeof(uint32_t) + j + 255) & ~size_t(255));
   if (launch_msg_parse(a, stream) != hipSuccess) return AMBRYCRC_EHIP;
-  int rc = enqueue_batch(c, d_region, a.job_off, a.job_len, nullptr, crc, j, batch_ws, stream);
+  int rc = enqueue_batch(c, d_region, a.job_off, a.job_len, nullptr, crc, j, batch_ws, stream,
+                         a.inline_max ? a.expected : nullptr);
   if (rc) return rc;
   if (launch_verify(crc, a.expected, mism, nullptr, (uint32_t)j, stream) != hipSuccess) return AMBRYCRC_EHIP;
   return hip_err(launch_msg_reduce(a, stream));

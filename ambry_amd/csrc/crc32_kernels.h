@@ -38,6 +38,11 @@ struct SweepArgs {
   const uint64_t* small_total;  // [4] as PlanArgs
   uint64_t* claim;              // = PlanArgs small_total + 4 (dynamic shares, variant 27)
   const uint32_t* small_idx;
+  // Message verify (class-sized group phase only, variants 26-28): for every chunk the group
+  // phase takes, also read the big-endian 8-B CRC stored right after it (base + off + len)
+  // and write exp_fill[chunk] = its low word, or ~crc when the high word is not zero (a
+  // forced mismatch: a CRC-32 never has upper bits). Null otherwise.
+  uint32_t* exp_fill;
 };
 
 // Group kernel shapes (mode -> G lanes per chunk, NB blocks of 16G bytes): small_max = 16*G*NB.
@@ -99,6 +104,8 @@ struct MsgArgs {
   const uint8_t* mismatch;  // [5m]
   uint32_t* status;         // [m]
   uint64_t* msg_end;        // [m] or null
+  uint64_t inline_max;      // records of 1..inline_max bytes: stored CRC read by the sweep's
+                            // group phase (SweepArgs::exp_fill), not by the parse kernel
 };
 
 hipError_t launch_msg_parse(const MsgArgs& a, hipStream_t s);

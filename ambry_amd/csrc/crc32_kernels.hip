@@ -1001,10 +1001,19 @@ __device__ __forceinline__ void group_class(const SweepArgs& a, uint64_t lo, uin
       const uint32_t x = __builtin_amdgcn_readlane(nb, q * G);
       nbw = x > nbw ? x : nbw;
     }
+    const bool leader = (lane & (G - 1)) == 0 && act;
+    uint64_t stored = 0;
+    if (a.exp_fill && leader) {  // message verify: the record's stored CRC follows its bytes
+      __builtin_memcpy(&stored, a.base + off + len, 8);  // issued now, used after the chain
+      stored = __builtin_bswap64(stored);
+    }
     uint32_t crc;
     if constexpr (T4) crc = group_crc_t4<NT, G>(a.base, off, len, cin, nbw, lane, k);
     else crc = group_crc_g<G, NB, NT>(a.base, off, len, cin, nbw, lane, k);
-    if ((lane & (G - 1)) == 0 && act) a.out[ci] = crc;
+    if (leader) {
+      a.out[ci] = crc;
+      if (a.exp_fill) a.exp_fill[ci] = (stored >> 32) ? ~crc : (uint32_t)stored;
+    }
   }
 }
 
@@ -1246,21 +1255,46 @@ __global__ __launch_bounds__(TPB) void crc32_sweep_kernel(SweepArgs a) {
 // own kPlanPerBlock consecutive chunks, visited in rounds of 256 (coalesced). The scan
 // also initialises out[]: 0 for chunks the sweep will XOR into, crc_in (the CRC of
 // nothing continued from crc_in) for empty chunks.
-__device__ __forceinline__ uint64_t block_scan256(uint64_t v, uint64_t* total) {
-  __shared__ uint64_t wsum[4];
+// Inclusive wave scan of a 64-bit value with DPP: row_shr 1/2/4/8 inside 16-lane rows,
+// then row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3). VALU only -- a __shfl_up
+// ladder is 12 dependent ds_bpermute round trips per 64-bit scan.
+__device__ __forceinline__ uint64_t wave_scan64(uint64_t v) {
+#define AMBRY_SCAN_STEP(C, R)                                  \
+  {                                                            \
+    const uint32_t lo = dpp<C, R>((uint32_t)v);                \
+    const uint32_t hi = dpp<C, R>((uint32_t)(v >> 32));        \
+    v += ((uint64_t)hi << 32) | lo;                            \
+  }
+  AMBRY_SCAN_STEP(0x111, 0xf)
+  AMBRY_SCAN_STEP(0x112, 0xf)
+  AMBRY_SCAN_STEP(0x114, 0xf)
+  AMBRY_SCAN_STEP(0x118, 0xf)
+  AMBRY_SCAN_STEP(0x142, 0xa)
+  AMBRY_SCAN_STEP(0x143, 0xc)
+#undef AMBRY_SCAN_STEP
+  return v;
+}
+
+// Inclusive scans of N values across a 256-thread block, one pair of barriers for all N:
+// v[i] becomes the inclusive prefix, total[i] the block total.
+template <int N>
+__device__ __forceinline__ void block_scan256(uint64_t (&v)[N], uint64_t (&total)[N]) {
+  __shared__ uint64_t wsum[4][N];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint64_t o = __shfl_up(v, d);
-    if (lane >= (uint32_t)d) v += o;
+  for (int i = 0; i < N; ++i) {
+    v[i] = wave_scan64(v[i]);
+    if (lane == 63) wsum[wv][i] = v[i];
   }
-  if (lane == 63) wsum[wv] = v;
   __syncthreads();
-  uint64_t before = 0;
-  for (uint32_t i = 0; i < wv; ++i) before += wsum[i];
-  *total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    uint64_t before = 0;
+    for (uint32_t w = 0; w < wv; ++w) before += wsum[w][i];
+    total[i] = wsum[0][i] + wsum[1][i] + wsum[2][i] + wsum[3][i];
+    v[i] += before;
+  }
   __syncthreads();
-  return v + before;
 }
 
 // Bytes a chunk contributes to the sweep's byte shares: chunks the group kernel takes
@@ -1292,88 +1326,92 @@ __device__ __forceinline__ uint32_t plan_span(uint32_t n, uint32_t base) {
 
 __global__ __launch_bounds__(256) void crc32_plan_count_kernel(PlanArgs a) {
   const uint32_t base = blockIdx.x * kPlanPerBlock;
-  const uint32_t span = plan_span(a.n, base);
-  uint64_t sum = 0, cls = 0;
-  for (uint32_t r = 0; r < span; r += 256) {
-    const uint32_t c = base + r + threadIdx.x;
-    if (c < a.n) {
-      const uint64_t len = a.len[c];
-      sum += share_len(len, a.small_max);
-      cls += class_onehot(len, a.small_max);
-    }
+  uint64_t len[kPlanPerBlock / 256];  // every round's load in flight before the first use
+#pragma unroll
+  for (uint32_t r = 0; r < kPlanPerBlock / 256; ++r) {
+    const uint32_t c = base + r * 256 + threadIdx.x;
+    len[r] = c < a.n ? a.len[c] : 0u;
   }
-  uint64_t total, total_cls;
-  (void)block_scan256(sum, &total);
-  (void)block_scan256(cls, &total_cls);
+  uint64_t v[2] = {0, 0}, total[2];
+#pragma unroll
+  for (uint32_t r = 0; r < kPlanPerBlock / 256; ++r) {
+    v[0] += share_len(len[r], a.small_max);
+    v[1] += class_onehot(len[r], a.small_max);
+  }
+  block_scan256<2>(v, total);
   if (threadIdx.x == 0) {
-    a.block_sum[blockIdx.x] = total;
-    a.block_small[blockIdx.x] = total_cls;  // packed: 4 x 16-bit class counts
+    a.block_sum[blockIdx.x] = total[0];
+    a.block_small[blockIdx.x] = total[1];  // packed: 4 x 16-bit class counts
   }
-}
-
-// Per-class sum over plan blocks [0, nb) of the packed counts (64-bit per class).
-__device__ __forceinline__ void class_sums(const uint64_t* __restrict__ block_small, uint32_t nb, uint64_t (&out)[4]) {
-  uint64_t part[4] = {0, 0, 0, 0};
-  for (uint32_t i = threadIdx.x; i < nb; i += 256) {
-    const uint64_t v = block_small[i];
-#pragma unroll
-    for (uint32_t c = 0; c < 4; ++c) part[c] += field16(v, c);
-  }
-#pragma unroll
-  for (uint32_t c = 0; c < 4; ++c) (void)block_scan256(part[c], &out[c]);
 }
 
 __global__ __launch_bounds__(256) void crc32_plan_scan_kernel(PlanArgs a) {
   const uint32_t nblocks = gridDim.x;
-  uint64_t part = 0;
-  for (uint32_t i = threadIdx.x; i < blockIdx.x; i += 256) part += a.block_sum[i];
-  uint64_t carry;
-  (void)block_scan256(part, &carry);
-  // class c's list entries start at base[c] = chunks of classes < c; this block's at base[c] + earlier[c]
-  uint64_t cls_carry[4] = {0, 0, 0, 0}, cls_total[4] = {0, 0, 0, 0};
-  if (a.small_max) {
-    if (nblocks > 1) {
-      class_sums(a.block_small, blockIdx.x, cls_carry);
-      class_sums(a.block_small, nblocks, cls_total);
-    } else {  // no count launch: count this (only) block here
-      uint64_t cls = 0;
-      for (uint32_t r = 0; r < plan_span(a.n, 0); r += 256) {
-        const uint32_t c = r + threadIdx.x;
-        if (c < a.n) cls += class_onehot(a.len[c], a.small_max);
-      }
-      uint64_t t;
-      (void)block_scan256(cls, &t);
+  const uint32_t base = blockIdx.x * kPlanPerBlock;
+  const uint32_t span = plan_span(a.n, base);
+  constexpr uint32_t R = kPlanPerBlock / 256;
+  uint64_t len[R];  // every round's load in flight before the first scan
 #pragma unroll
-      for (uint32_t c = 0; c < 4; ++c) cls_total[c] = field16(t, c);
-    }
+  for (uint32_t r = 0; r < R; ++r) {
+    const uint32_t c = base + r * 256 + threadIdx.x;
+    len[r] = (r * 256 < span && c < a.n) ? a.len[c] : 0u;
   }
+  // One 9-value block reduction: the byte carry of earlier blocks, and per class the
+  // chunks of earlier blocks (carry) and of all blocks (total).
+  // cls[0] = byte carry, cls[1..4] = class carries, cls[5..8] = class totals
+  uint64_t red[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, tot[9];
+  if (nblocks > 1) {
+    for (uint32_t i = threadIdx.x; i < nblocks; i += 256) {
+      const bool earlier = i < blockIdx.x;
+      if (earlier) red[0] += a.block_sum[i];
+      if (a.small_max) {
+        const uint64_t v = a.block_small[i];
+#pragma unroll
+        for (uint32_t c = 0; c < 4; ++c) {
+          const uint64_t f = field16(v, c);
+          red[5 + c] += f;
+          if (earlier) red[1 + c] += f;
+        }
+      }
+    }
+  } else if (a.small_max) {  // no count launch: count this (only) block here
+    uint64_t cls = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < R; ++r) cls += class_onehot(len[r], a.small_max);
+#pragma unroll
+    for (uint32_t c = 0; c < 4; ++c) red[5 + c] = field16(cls, c);
+  }
+  block_scan256<9>(red, tot);
+  uint64_t carry = tot[0];
+  uint64_t cls_carry[4] = {tot[1], tot[2], tot[3], tot[4]};
+  const uint64_t cls_total[4] = {tot[5], tot[6], tot[7], tot[8]};
+  // class c's list entries start at base[c] = chunks of classes < c; this block's at base[c] + earlier[c]
   uint64_t cls_base[4];
   cls_base[0] = 0;
   cls_base[1] = cls_total[0];
   cls_base[2] = cls_base[1] + cls_total[1];
   cls_base[3] = cls_base[2] + cls_total[2];
-  const uint32_t base = blockIdx.x * kPlanPerBlock;
-  const uint32_t span = plan_span(a.n, base);
-  for (uint32_t r = 0; r < span; r += 256) {
-    const uint32_t c = base + r + threadIdx.x;
-    const uint64_t len = c < a.n ? a.len[c] : 0u;
-    const uint64_t v = share_len(len, a.small_max);
-    const uint64_t oh = c < a.n ? class_onehot(len, a.small_max) : 0ull;
-    uint64_t round_total, round_cls;
-    const uint64_t incl = block_scan256(v, &round_total);
-    const uint64_t incl_cls = block_scan256(oh, &round_cls);
-    if (c < a.n) {
-      a.byte_start[c] = carry + incl - v;
-      a.out[c] = len ? 0u : (a.crc_in ? a.crc_in[c] : 0u);
-      if (oh) {
-        const uint32_t k = small_class(len);
-        a.small_idx[cls_base[k] + cls_carry[k] + field16(incl_cls, k) - 1] = c;
-      }
-      if (c == a.n - 1) a.byte_start[a.n] = carry + incl;
-    }
-    carry += round_total;
 #pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) cls_carry[k] += field16(round_cls, k);
+  for (uint32_t r = 0; r < R; ++r) {
+    if (r * 256 >= span) break;
+    const uint32_t c = base + r * 256 + threadIdx.x;
+    const uint64_t ln = len[r];
+    const uint64_t sl = share_len(ln, a.small_max);
+    const uint64_t oh = c < a.n ? class_onehot(ln, a.small_max) : 0ull;
+    uint64_t sc[2] = {sl, oh}, round_tot[2];
+    block_scan256<2>(sc, round_tot);
+    if (c < a.n) {
+      a.byte_start[c] = carry + sc[0] - sl;
+      a.out[c] = ln ? 0u : (a.crc_in ? a.crc_in[c] : 0u);
+      if (oh) {
+        const uint32_t k = small_class(ln);
+        a.small_idx[cls_base[k] + cls_carry[k] + field16(sc[1], k) - 1] = c;
+      }
+      if (c == a.n - 1) a.byte_start[a.n] = carry + sc[0];
+    }
+    carry += round_tot[0];
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) cls_carry[k] += field16(round_tot[1], k);
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     a.small_total[4] = 0;  // the sweep's dynamic share counter

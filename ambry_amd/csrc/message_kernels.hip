@@ -9,7 +9,9 @@
 //                      slice-by-4 through LDS tables), header constraints, and up to five record
 //                      CRC jobs (enc key, properties, update, user metadata, blob) =
 //                      [record start, record end - 8) with the stored big-endian CRC; job
-//                      k*m + i is slot k of message i (slot-major: coalesced stores)
+//                      k*m + i is slot k of message i (slot-major: coalesced stores). The
+//                      stored CRC of a record the group phase takes whole (<= inline_max)
+//                      is left to the sweep, which streams that line anyway
 //   plan + sweep       the batch CRC engine over the 5m jobs (crc32_kernels.hip)
 //   verify             mismatch flags
 //   msg_reduce_kernel  per-message status bits
@@ -171,11 +173,15 @@ __global__ __launch_bounds__(256) void msg_parse_kernel(MsgArgs a) {
           e = (uint64_t)rel[j];
           break;
         }
-      const uint64_t stored = be64(p + e - 8);
-      if (stored >> 32) status |= kRecordBit[k];  // a CRC32 never has upper bits: mismatch regardless
       jo[k] = off + (uint64_t)rel[k];
       jl[k] = e - (uint64_t)rel[k] - 8;
-      ex[k] = (uint32_t)stored;
+      // Records the group phase takes whole have their stored CRC read there, from the line
+      // it is already streaming (SweepArgs::exp_fill); only the others cost a fetch here.
+      if (jl[k] == 0 || jl[k] > a.inline_max) {
+        const uint64_t stored = be64(p + e - 8);
+        if (stored >> 32) status |= kRecordBit[k];  // a CRC32 never has upper bits: mismatch regardless
+        ex[k] = (uint32_t)stored;
+      }
     }
   } while (false);
 #pragma unroll

@@ -77,3 +77,35 @@ def test_each_record_kind_flagged(gpu):
         region += b
     st, _ = run(gpu, bytes(region), offs)
     assert st == [bit for _, _, bit in cases]
+
+
+@pytest.mark.parametrize("variant", [22, 28])
+def test_stored_crc_bytes_corrupted_group_phase(gpu, variant):
+    """Flips inside the stored 8-B CRCs themselves, upper word (a CRC-32 has none: always a
+    mismatch) and lower word, on every record kind, in a batch large enough for the group
+    phase (4,000 messages). Variant 28 reads the stored CRCs of group-phase records inside the
+    sweep (SweepArgs::exp_fill); variant 22 reads all of them in the parse kernel."""
+    region, offs, expect = build_region(n=4000, seed=21, corrupt_frac=0.0, big_every=97)
+    assert all(s == 0 for s, _ in expect)
+    region = bytearray(region)
+    rng = np.random.default_rng(5)
+    for i in rng.choice(len(offs), size=400, replace=False):
+        off = offs[i]
+        v, total, rel = MF.parse_header(bytes(region[off:off + 64]), 0)
+        present = [r for r in rel if r != MF.INVALID]
+        end = present[0] + total
+        ends = present[1:] + [end]
+        e = ends[int(rng.integers(0, len(ends)))]
+        pos = off + e - 8 + int(rng.integers(0, 8))  # either word of the stored CRC
+        region[pos] ^= 1 << int(rng.integers(0, 8))
+    region = bytes(region)
+    expect = [MF.verify_message(region, o) for o in offs]
+    prev = gpu.get_variant(0)
+    gpu.set_variant(0, variant)
+    try:
+        st, end = run(gpu, region, offs)
+    finally:
+        gpu.set_variant(0, prev)
+    assert st == [s for s, _ in expect]
+    assert end == [e for _, e in expect]
+    assert sum(1 for s in st if s) == 400
