@@ -861,8 +861,7 @@ int ambrycrc_verify_messages_dev(const uint8_t* d_region, uint64_t region_len, c
   a.job_len = a.job_off + j;
   a.expected = reinterpret_cast<uint32_t*>(a.job_len + j);
   uint32_t* crc = a.expected + j;
-  uint8_t* mism = reinterpret_cast<uint8_t*>(crc + j);
-  a.mismatch = mism;
+  a.crc = crc;
   a.status = d_status;
   a.msg_end = d_msg_end;
   // The class-sized group phase (variants 26-28) reads the stored CRCs of the records it
@@ -874,7 +873,6 @@ int ambrycrc_verify_messages_dev(const uint8_t* d_region, uint64_t region_len, c
   int rc = enqueue_batch(c, d_region, a.job_off, a.job_len, nullptr, crc, j, batch_ws, stream,
                          a.inline_max ? a.expected : nullptr);
   if (rc) return rc;
-  if (launch_verify(crc, a.expected, mism, nullptr, (uint32_t)j, stream) != hipSuccess) return AMBRYCRC_EHIP;
   return hip_err(launch_msg_reduce(a, stream));
 }
 

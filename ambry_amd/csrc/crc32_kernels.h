@@ -101,7 +101,7 @@ struct MsgArgs {
   uint64_t* job_off;        // [5m], slot-major: job k*m + i = slot k of message i
   uint64_t* job_len;        // [5m]
   uint32_t* expected;       // [5m]
-  const uint8_t* mismatch;  // [5m]
+  const uint32_t* crc;      // [5m] computed record CRCs
   uint32_t* status;         // [m]
   uint64_t* msg_end;        // [m] or null
   uint64_t inline_max;      // records of 1..inline_max bytes: stored CRC read by the sweep's

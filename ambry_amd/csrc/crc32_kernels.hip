@@ -1361,6 +1361,7 @@ __global__ __launch_bounds__(256) void crc32_plan_scan_kernel(PlanArgs a) {
   // cls[0] = byte carry, cls[1..4] = class carries, cls[5..8] = class totals
   uint64_t red[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, tot[9];
   if (nblocks > 1) {
+#pragma unroll 4
     for (uint32_t i = threadIdx.x; i < nblocks; i += 256) {
       const bool earlier = i < blockIdx.x;
       if (earlier) red[0] += a.block_sum[i];
@@ -1391,6 +1392,23 @@ __global__ __launch_bounds__(256) void crc32_plan_scan_kernel(PlanArgs a) {
   cls_base[1] = cls_total[0];
   cls_base[2] = cls_base[1] + cls_total[1];
   cls_base[3] = cls_base[2] + cls_total[2];
+  // Rounds of 256 chunks: wave scans (DPP, no barrier) per round, then one barrier and each
+  // wave adds the totals of the waves before it -- earlier rounds, and earlier waves of its
+  // own round -- from LDS. Class counts stay packed (<= 256 per class per round: 16 bits).
+  __shared__ uint64_t wtot[R][4][2];
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  uint64_t incl_s[R], incl_c[R];
+#pragma unroll
+  for (uint32_t r = 0; r < R; ++r) {
+    const uint32_t c = base + r * 256 + threadIdx.x;
+    incl_s[r] = wave_scan64(share_len(len[r], a.small_max));
+    incl_c[r] = wave_scan64(c < a.n ? class_onehot(len[r], a.small_max) : 0ull);
+    if (lane == 63) {
+      wtot[r][wv][0] = incl_s[r];
+      wtot[r][wv][1] = incl_c[r];
+    }
+  }
+  __syncthreads();
 #pragma unroll
   for (uint32_t r = 0; r < R; ++r) {
     if (r * 256 >= span) break;
@@ -1398,20 +1416,30 @@ __global__ __launch_bounds__(256) void crc32_plan_scan_kernel(PlanArgs a) {
     const uint64_t ln = len[r];
     const uint64_t sl = share_len(ln, a.small_max);
     const uint64_t oh = c < a.n ? class_onehot(ln, a.small_max) : 0ull;
-    uint64_t sc[2] = {sl, oh}, round_tot[2];
-    block_scan256<2>(sc, round_tot);
+    uint64_t bs = 0, bc = 0, rs = 0, rc = 0;  // earlier waves of this round; whole round
+#pragma unroll
+    for (uint32_t w = 0; w < 4; ++w) {
+      const uint64_t ts = wtot[r][w][0], tc = wtot[r][w][1];
+      if (w < wv) {
+        bs += ts;
+        bc += tc;
+      }
+      rs += ts;
+      rc += tc;
+    }
     if (c < a.n) {
-      a.byte_start[c] = carry + sc[0] - sl;
+      const uint64_t incl = carry + bs + incl_s[r];
+      a.byte_start[c] = incl - sl;
       a.out[c] = ln ? 0u : (a.crc_in ? a.crc_in[c] : 0u);
       if (oh) {
         const uint32_t k = small_class(ln);
-        a.small_idx[cls_base[k] + cls_carry[k] + field16(sc[1], k) - 1] = c;
+        a.small_idx[cls_base[k] + cls_carry[k] + field16(bc + incl_c[r], k) - 1] = c;
       }
-      if (c == a.n - 1) a.byte_start[a.n] = carry + sc[0];
+      if (c == a.n - 1) a.byte_start[a.n] = incl;
     }
-    carry += round_tot[0];
+    carry += rs;
 #pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) cls_carry[k] += field16(round_tot[1], k);
+    for (uint32_t k = 0; k < 4; ++k) cls_carry[k] += field16(rc, k);
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     a.small_total[4] = 0;  // the sweep's dynamic share counter

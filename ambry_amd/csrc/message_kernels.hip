@@ -13,8 +13,7 @@
 //                      stored CRC of a record the group phase takes whole (<= inline_max)
 //                      is left to the sweep, which streams that line anyway
 //   plan + sweep       the batch CRC engine over the 5m jobs (crc32_kernels.hip)
-//   verify             mismatch flags
-//   msg_reduce_kernel  per-message status bits
+//   msg_reduce_kernel  per-message status bits: computed CRC vs expected, per record slot
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -42,11 +41,6 @@ __device__ __forceinline__ uint64_t be64(const uint8_t* p) {
   __builtin_memcpy(&v, p, 8);
   return __builtin_bswap64(v);
 }
-__device__ __forceinline__ uint32_t le32(const uint8_t* p) {
-  uint32_t v;
-  __builtin_memcpy(&v, p, 4);
-  return v;
-}
 
 // Slice-by-4 tables T0..T3 (T_j[b] = b advanced over j further zero bytes), 4 KiB, staged
 // into LDS per workgroup from the table image: T_j[b] sits at image byte
@@ -64,29 +58,73 @@ __device__ __forceinline__ void stage_slice_tables(uint32_t* __restrict__ t, con
   for (uint32_t r = 0; r < 4; ++r) t[threadIdx.x + 256u * r] = v[r];
 }
 
-// CRC-32 of n <= 32 header bytes: slice-by-4 over whole words (the loads are independent
-// of the register chain, so they issue together), byte-wise tail.
-__device__ __forceinline__ uint32_t crc_small(const uint8_t* p, uint32_t n, const uint32_t* __restrict__ t) {
-  uint32_t c = 0xFFFFFFFFu;
-  uint32_t i = 0;
-  for (; i + 4 <= n; i += 4) {
-    const uint32_t x = c ^ le32(p + i);
-    c = t[768 + (x & 0xffu)] ^ t[512 + ((x >> 8) & 0xffu)] ^ t[256 + ((x >> 16) & 0xffu)] ^ t[x >> 24];
-  }
-  for (; i < n; ++i) c = (c >> 8) ^ t[(c ^ p[i]) & 0xffu];
-  return ~c;
-}
-
 __constant__ uint32_t kRecordBit[5] = {AMBRYCRC_MSG_ENCKEY_CRC, AMBRYCRC_MSG_PROPS_CRC, AMBRYCRC_MSG_UPDATE_CRC,
                                        AMBRYCRC_MSG_USERMETA_CRC, AMBRYCRC_MSG_BLOB_CRC};
 
+// Header bytes [0, 40) of a message as ten little-endian words, one unaligned 16 + 16 + 8 B
+// load when the region holds 40 bytes past `off` (the longest header, V3), else byte loads
+// with zero fill. Issued before the table staging, so one memory round trip covers it.
+struct HeaderWords {
+  uint32_t w[10];
+};
+
+__device__ __forceinline__ HeaderWords load_header(const uint8_t* p, uint64_t rem) {
+  HeaderWords h;
+  if (rem >= 40) {
+    __builtin_memcpy(&h.w[0], p, 16);
+    __builtin_memcpy(&h.w[4], p + 16, 16);
+    __builtin_memcpy(&h.w[8], p + 32, 8);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        if ((uint64_t)(4 * i + b) < rem) v |= (uint32_t)p[4 * i + b] << (8 * b);
+      h.w[i] = v;
+    }
+  }
+  return h;
+}
+
+// Big-endian 32-bit field at byte 4k+2 (V1/V2 layouts) and at byte 4k (V3) of the header.
+__device__ __forceinline__ uint32_t be32_w2(const HeaderWords& h, int k) {
+  return __builtin_bswap32(__builtin_amdgcn_alignbyte(h.w[k + 1], h.w[k], 2));
+}
+__device__ __forceinline__ uint32_t be32_w0(const HeaderWords& h, int k) { return __builtin_bswap32(h.w[k]); }
+
+// CRC-32 of the first n = h - 8 header bytes (26, 30 or 32) from the words: slice-by-4 over
+// whole words, then the two trailing bytes of V1/V2.
+__device__ __forceinline__ uint32_t header_crc(const HeaderWords& h, uint32_t n, const uint32_t* __restrict__ t) {
+  uint32_t c = 0xFFFFFFFFu;
+  const uint32_t nw = n >> 2;
+#pragma unroll
+  for (uint32_t i = 0; i < 8; ++i) {
+    if (i < nw) {
+      const uint32_t x = c ^ h.w[i];
+      c = t[768 + (x & 0xffu)] ^ t[512 + ((x >> 8) & 0xffu)] ^ t[256 + ((x >> 16) & 0xffu)] ^ t[x >> 24];
+    }
+  }
+  if (n & 2u) {
+    const uint32_t tw = nw == 6 ? h.w[6] : h.w[7];
+    c = (c >> 8) ^ t[(c ^ tw) & 0xffu];
+    c = (c >> 8) ^ t[(c ^ (tw >> 8)) & 0xffu];
+  }
+  return ~c;
+}
+
 __global__ __launch_bounds__(256) void msg_parse_kernel(MsgArgs a) {
   __shared__ uint32_t tbl[1024];
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = i < a.m;
+  const uint64_t off = live ? a.msg_off[i] : 0;
+  const bool in_region = live && off <= a.region_len;
+  const uint64_t rem = in_region ? a.region_len - off : 0;
+  const uint8_t* p = a.region + (in_region ? off : 0);
+  const HeaderWords hw = load_header(p, rem);  // in flight across the table staging
   stage_slice_tables(tbl, a.img);
   __syncthreads();
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.m) return;
-  const uint64_t off = a.msg_off[i];
+  if (!live) return;
   // Jobs are slot-major (job k*m + i = slot k of message i), so each slot's store below is
   // one coalesced wave store; every slot is written exactly once.
   uint64_t jo[kMsgSlots] = {0, 0, 0, 0, 0}, jl[kMsgSlots] = {0, 0, 0, 0, 0};
@@ -94,41 +132,47 @@ __global__ __launch_bounds__(256) void msg_parse_kernel(MsgArgs a) {
   uint32_t status = 0;
   uint64_t end = 0;
   do {
-    if (off > a.region_len || a.region_len - off < 2) {
+    if (!in_region || rem < 2) {
       status = AMBRYCRC_MSG_BAD_LAYOUT;
       break;
     }
-    const uint8_t* p = a.region + off;
-    const int v = (int16_t)be16(p);
+    const int v = (int16_t)__builtin_bswap16((uint16_t)hw.w[0]);
     const uint32_t h = v == 1 ? 34u : v == 2 ? 38u : v == 3 ? 40u : 0u;
     if (h == 0) {
       status = AMBRYCRC_MSG_BAD_VERSION;
       break;
     }
-    if (a.region_len - off < h) {
+    if (rem < h) {
       status = AMBRYCRC_MSG_BAD_LAYOUT;
       break;
     }
-    if ((uint64_t)crc_small(p, h - 8, tbl) != be64(p + h - 8)) {  // verifyHeader: nothing else is read
+    // stored header CRC: bytes [h-8, h)
+    const uint32_t st_hi = v == 3 ? be32_w0(hw, 8) : v == 2 ? be32_w2(hw, 7) : be32_w2(hw, 6);
+    const uint32_t st_lo = v == 3 ? be32_w0(hw, 9) : v == 2 ? be32_w2(hw, 8) : be32_w2(hw, 7);
+    if (st_hi != 0 || header_crc(hw, h - 8, tbl) != st_lo) {  // verifyHeader: nothing else is read
       status = AMBRYCRC_MSG_HEADER_CRC;
       break;
     }
     int64_t total;
     int32_t rel[kMsgSlots];
-    if (v == 1) {
-      total = (int64_t)be64(p + 2);
-      rel[0] = -1;
-      for (int k = 0; k < 4; ++k) rel[k + 1] = (int32_t)be32(p + 10 + 4 * k);
-    } else if (v == 2) {
-      total = (int64_t)be64(p + 2);
-      for (int k = 0; k < 5; ++k) rel[k] = (int32_t)be32(p + 10 + 4 * k);
-    } else {
-      if ((int16_t)be16(p + 2) < 0) {  // lifeVersion >= 0
+    if (v == 3) {
+      if ((int16_t)__builtin_bswap16((uint16_t)(hw.w[0] >> 16)) < 0) {  // lifeVersion >= 0
         status = AMBRYCRC_MSG_BAD_LAYOUT;
         break;
       }
-      total = (int64_t)be64(p + 4);
-      for (int k = 0; k < 5; ++k) rel[k] = (int32_t)be32(p + 12 + 4 * k);
+      total = (int64_t)(((uint64_t)be32_w0(hw, 1) << 32) | be32_w0(hw, 2));
+#pragma unroll
+      for (int k = 0; k < 5; ++k) rel[k] = (int32_t)be32_w0(hw, 3 + k);
+    } else {
+      total = (int64_t)(((uint64_t)be32_w2(hw, 0) << 32) | be32_w2(hw, 1));
+      if (v == 1) {
+        rel[0] = -1;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) rel[k + 1] = (int32_t)be32_w2(hw, 2 + k);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) rel[k] = (int32_t)be32_w2(hw, 2 + k);
+      }
     }
     // checkHeaderConstraints (MessageFormatRecord.java:985-1030), exact put / update shapes
     const bool is_put = rel[1] != -1 && rel[2] == -1 && rel[3] != -1 && rel[4] != -1;
@@ -145,20 +189,20 @@ __global__ __launch_bounds__(256) void msg_parse_kernel(MsgArgs a) {
       if (first < 0) first = rel[k];
       prev = rel[k];
     }
-    if (!ok || (uint64_t)total > a.region_len - off || (uint64_t)first > a.region_len - off - (uint64_t)total) {
+    if (!ok || (uint64_t)total > rem || (uint64_t)first > rem - (uint64_t)total) {
       status = AMBRYCRC_MSG_BAD_LAYOUT;
       break;
     }
     end = (uint64_t)first + (uint64_t)total;
-    for (int k = 0; k < kMsgSlots && ok; ++k) {
-      if (rel[k] == -1) continue;
-      uint64_t e = end;
+    uint64_t rend[kMsgSlots];  // end of record k (its stored CRC's last byte + 1)
+    for (int k = 0; k < kMsgSlots; ++k) {
+      rend[k] = end;
       for (int j = k + 1; j < kMsgSlots; ++j)
         if (rel[j] != -1) {
-          e = (uint64_t)rel[j];
+          rend[k] = (uint64_t)rel[j];
           break;
         }
-      if (e < (uint64_t)rel[k] + 8) ok = false;
+      if (rel[k] != -1 && rend[k] < (uint64_t)rel[k] + 8) ok = false;
     }
     if (!ok) {
       status = AMBRYCRC_MSG_BAD_LAYOUT;
@@ -167,12 +211,7 @@ __global__ __launch_bounds__(256) void msg_parse_kernel(MsgArgs a) {
     }
     for (int k = 0; k < kMsgSlots; ++k) {
       if (rel[k] == -1) continue;
-      uint64_t e = end;
-      for (int j = k + 1; j < kMsgSlots; ++j)
-        if (rel[j] != -1) {
-          e = (uint64_t)rel[j];
-          break;
-        }
+      const uint64_t e = rend[k];
       jo[k] = off + (uint64_t)rel[k];
       jl[k] = e - (uint64_t)rel[k] - 8;
       // Records the group phase takes whole have their stored CRC read there, from the line
@@ -198,8 +237,11 @@ __global__ __launch_bounds__(256) void msg_reduce_kernel(MsgArgs a) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.m) return;
   uint32_t s = a.status[i];
-  for (int k = 0; k < kMsgSlots; ++k)
-    if (a.mismatch[(uint64_t)k * a.m + i]) s |= kRecordBit[k];
+#pragma unroll
+  for (int k = 0; k < kMsgSlots; ++k) {
+    const uint64_t j = (uint64_t)k * a.m + i;
+    if (a.crc[j] != a.expected[j]) s |= kRecordBit[k];
+  }
   a.status[i] = s;
 }
 
