@@ -293,8 +293,30 @@ def main():
     buf, off_t, len_t, n, total, chunk, desc = build_workload(torch, dev, args, rank)
     gathered = torch.empty(world * n, dtype=torch.int32, device=dev) if use_dist else None
 
+    verify = None
+    if args.config == "c4":
+        # C4 is the verify-on-read path: expected CRCs from a clean pass, then single-bit flips
+        # in 1 % of the chunks (seeded); each step recomputes and compares (ambrycrc_verify_dev).
+        import numpy as np
+
+        expected = D.crc32_batch(buf, off_t, len_t).clone()
+        rng = np.random.default_rng(20261016 + rank)
+        bad = np.sort(rng.choice(n, size=n // 100, replace=False))
+        lens_h = len_t.cpu().numpy()
+        offs_h = off_t.cpu().numpy()
+        pos = offs_h[bad] + (rng.random(len(bad)) * lens_h[bad]).astype(np.int64)
+        bits = torch.tensor(1 << rng.integers(0, 8, size=len(bad)), dtype=torch.uint8, device=dev)
+        pos_t = torch.tensor(pos, dtype=torch.int64, device=dev)
+        buf[pos_t] ^= bits
+        torch.cuda.synchronize()
+        verify = {"expected": expected, "bad": bad, "out": torch.empty(n, dtype=torch.int32, device=dev)}
+
     def step():
-        out = D.crc32_batch(buf, off_t, len_t)
+        if verify is not None:
+            out, mism, cnt = D.crc32_verify(buf, off_t, len_t, verify["expected"], out=verify["out"])
+            verify["mism"], verify["cnt"] = mism, cnt
+        else:
+            out = D.crc32_batch(buf, off_t, len_t)
         if use_dist:
             dist.all_gather_into_tensor(gathered, out)
         return out
@@ -347,6 +369,10 @@ def main():
         allgather_ok = bool(flag.item())
     read_roof = measure_read_roof(torch, D, buf, buf.numel(), dev.index) if args.config != "c4" else None
     crcs = out.cpu().numpy().view("uint32")
+    verify_ok = None
+    if verify is not None:  # the flags must name exactly the flipped chunks
+        flagged = np.nonzero(verify["mism"].cpu().numpy())[0]
+        verify_ok = bool(np.array_equal(flagged, verify["bad"]) and int(verify["cnt"].item()) == len(verify["bad"]))
     step_bytes = total  # per rank
     value = world * step_bytes * args.steps / elapsed / 2**30
     kern_avg_s = kern_ms / max(1, launches) / 1e3
@@ -388,6 +414,10 @@ def main():
         },
         "timing": {"wall_s": round(elapsed, 4), "stream_event_ms": round(ev_ms, 3), "kernel_launches": launches},
         "allgather_ok": allgather_ok,
+        "verify": (None if verify is None else
+                   {"flipped_chunks": int(len(verify["bad"])), "flags_exact": verify_ok,
+                    "what": "ambrycrc_verify_dev per step: CRCs recomputed and compared with the clean pass; "
+                            "single-bit flips in 1 % of chunks (seeded)"}),
     }
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc) and args.config == "c3":
