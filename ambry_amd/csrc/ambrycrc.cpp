@@ -98,6 +98,18 @@ struct HostSlab {
   hipEvent_t done = nullptr;
 };
 
+constexpr size_t kSlabMsgs = 1u << 16;  // messages per host-path staging slab
+
+struct MsgSlab {  // message verify staging per HostSlab, allocated on first use
+  uint64_t* h_off = nullptr;   // pinned [kSlabMsgs]: message offsets in the slab
+  uint32_t* h_status = nullptr;
+  uint64_t* h_end = nullptr;
+  uint64_t* d_off = nullptr;
+  uint32_t* d_status = nullptr;
+  uint64_t* d_end = nullptr;
+  void* d_ws = nullptr;
+};
+
 struct DevCtx {
   int device = -1;
   int num_cu = 0;
@@ -120,6 +132,8 @@ struct DevCtx {
   std::vector<EventPair> pending, free_events;
   bool slabs_ready = false;
   HostSlab slab[kSlabs];
+  bool msg_slabs_ready = false;
+  MsgSlab msg_slab[kSlabs];
   std::mutex mu;  // guards ws growth, events, slabs
 };
 
@@ -833,22 +847,12 @@ size_t ambrycrc_messages_workspace_bytes(size_t m) {
   return jobs + ws_need(j);
 }
 
-int ambrycrc_verify_messages_dev(const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off, size_t m,
-                                 uint32_t* d_status, uint64_t* d_msg_end, void* d_ws, size_t ws_bytes,
-                                 hipStream_t stream) {
-  if (m == 0) return AMBRYCRC_OK;
-  if (!d_region || !d_msg_off || !d_status || (size_t)kMsgSlots * m >= (1ull << 31)) return AMBRYCRC_EINVAL;
-  DevCtx* c = ctx_current();
-  if (!c) return AMBRYCRC_ENOINIT;
-  const size_t need = ambrycrc_messages_workspace_bytes(m);
-  if (d_ws) {
-    if (ws_bytes < need) return AMBRYCRC_EINVAL;
-  } else {
-    std::lock_guard<std::mutex> g(c->mu);
-    int rc = ensure_ws(c, need);
-    if (rc) return rc;
-    d_ws = c->d_ws;
-  }
+namespace {
+
+// The device message pipeline (parse -> plan + sweep -> reduce) on `stream`; d_ws holds
+// at least ambrycrc_messages_workspace_bytes(m).
+int enqueue_messages(DevCtx* c, const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off, size_t m,
+                     uint32_t* d_status, uint64_t* d_msg_end, void* d_ws, hipStream_t stream) {
   const size_t j = (size_t)kMsgSlots * m;
   uint8_t* w = static_cast<uint8_t*>(d_ws);
   MsgArgs a;
@@ -874,6 +878,231 @@ int ambrycrc_verify_messages_dev(const uint8_t* d_region, uint64_t region_len, c
                          a.inline_max ? a.expected : nullptr);
   if (rc) return rc;
   return hip_err(launch_msg_reduce(a, stream));
+}
+
+uint32_t rd_be32(const uint8_t* p) {
+  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+uint64_t rd_be64(const uint8_t* p) { return ((uint64_t)rd_be32(p) << 32) | rd_be32(p + 4); }
+
+// Bytes from a message's start that the device pipeline may read: the 40-B header window,
+// and, when the header's sizes fit the region, the whole message [0, first record + total).
+// Every early exit of msg_parse_kernel reads the header alone, so a staging copy of this
+// extent gives the same status bits as the whole region would.
+uint64_t message_extent(const uint8_t* p, uint64_t rem) {
+  const uint64_t hdr = std::min<uint64_t>(rem, 40);
+  if (rem < 2) return rem;
+  const int v = (int16_t)(((uint32_t)p[0] << 8) | p[1]);
+  const uint32_t h = v == 1 ? 34u : v == 2 ? 38u : v == 3 ? 40u : 0u;
+  if (h == 0 || rem < h) return hdr;
+  int64_t total;
+  int32_t rel[kMsgSlots];
+  if (v == 1) {
+    total = (int64_t)rd_be64(p + 2);
+    rel[0] = -1;
+    for (int k = 0; k < 4; ++k) rel[k + 1] = (int32_t)rd_be32(p + 10 + 4 * k);
+  } else if (v == 2) {
+    total = (int64_t)rd_be64(p + 2);
+    for (int k = 0; k < 5; ++k) rel[k] = (int32_t)rd_be32(p + 10 + 4 * k);
+  } else {
+    total = (int64_t)rd_be64(p + 4);
+    for (int k = 0; k < 5; ++k) rel[k] = (int32_t)rd_be32(p + 12 + 4 * k);
+  }
+  int64_t first = -1;
+  for (int k = 0; k < kMsgSlots; ++k)
+    if (rel[k] != -1) {
+      first = rel[k];
+      break;
+    }
+  if (total <= 0 || first < 0 || (uint64_t)total > rem || (uint64_t)first > rem - (uint64_t)total) return hdr;
+  return std::max<uint64_t>(hdr, (uint64_t)first + (uint64_t)total);
+}
+
+}  // namespace
+
+int ambrycrc_verify_messages_dev(const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off, size_t m,
+                                 uint32_t* d_status, uint64_t* d_msg_end, void* d_ws, size_t ws_bytes,
+                                 hipStream_t stream) {
+  if (m == 0) return AMBRYCRC_OK;
+  if (!d_region || !d_msg_off || !d_status || (size_t)kMsgSlots * m >= (1ull << 31)) return AMBRYCRC_EINVAL;
+  DevCtx* c = ctx_current();
+  if (!c) return AMBRYCRC_ENOINIT;
+  const size_t need = ambrycrc_messages_workspace_bytes(m);
+  if (d_ws) {
+    if (ws_bytes < need) return AMBRYCRC_EINVAL;
+  } else {
+    std::lock_guard<std::mutex> g(c->mu);
+    int rc = ensure_ws(c, need);
+    if (rc) return rc;
+    d_ws = c->d_ws;
+  }
+  return enqueue_messages(c, d_region, region_len, d_msg_off, m, d_status, d_msg_end, d_ws, stream);
+}
+
+int ambrycrc_verify_messages_host(const uint8_t* region, uint64_t region_len, const uint64_t* msg_off, size_t m,
+                                  uint32_t* status, uint64_t* msg_end, int device, int pinned) {
+  if (m == 0) return AMBRYCRC_OK;
+  if (!msg_off || !status || (!region && region_len)) return AMBRYCRC_EINVAL;
+  DevCtx* c = ctx_for(device);
+  if (!c) return AMBRYCRC_ENOINIT;
+  std::lock_guard<std::mutex> g(c->mu);
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  if (hipSetDevice(device) != hipSuccess) return AMBRYCRC_EHIP;
+  int rc = setup_slabs(c);
+  if (rc) return rc;
+  if (!c->msg_slabs_ready) {
+    for (int w = 0; w < kSlabs; ++w) {
+      MsgSlab& ms = c->msg_slab[w];
+      if (hipHostMalloc(reinterpret_cast<void**>(&ms.h_off), kSlabMsgs * sizeof(uint64_t), hipHostMallocDefault) !=
+              hipSuccess ||
+          hipHostMalloc(reinterpret_cast<void**>(&ms.h_status), kSlabMsgs * sizeof(uint32_t),
+                        hipHostMallocDefault) != hipSuccess ||
+          hipHostMalloc(reinterpret_cast<void**>(&ms.h_end), kSlabMsgs * sizeof(uint64_t), hipHostMallocDefault) !=
+              hipSuccess ||
+          hipMalloc(reinterpret_cast<void**>(&ms.d_off), kSlabMsgs * sizeof(uint64_t)) != hipSuccess ||
+          hipMalloc(reinterpret_cast<void**>(&ms.d_status), kSlabMsgs * sizeof(uint32_t)) != hipSuccess ||
+          hipMalloc(reinterpret_cast<void**>(&ms.d_end), kSlabMsgs * sizeof(uint64_t)) != hipSuccess ||
+          hipMalloc(&ms.d_ws, ambrycrc_messages_workspace_bytes(kSlabMsgs)) != hipSuccess) {
+        (void)hipSetDevice(prev);
+        return AMBRYCRC_ENOMEM;
+      }
+    }
+    c->msg_slabs_ready = true;
+  }
+
+  // Messages in offset order; each slab stages one contiguous span [lo, hi) of the region
+  // that covers every packed message's extent. A message whose extent exceeds a slab gets
+  // a staging buffer of its own.
+  std::vector<size_t> order(m);
+  for (size_t i = 0; i < m; ++i) order[i] = i;
+  if (!std::is_sorted(msg_off, msg_off + m))  // a recovery scan's offsets already are
+    std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) { return msg_off[x] < msg_off[y]; });
+  // Message extents: one header read each, scattered over the region (a cache and TLB miss
+  // apiece), so they are read by the copy pool's threads in parallel.
+  std::vector<uint64_t> ext(m);
+  {
+    CopyPool& pool = CopyPool::get();
+    const int parts = (int)std::min<size_t>((size_t)pool.threads(), std::max<size_t>(1, m / 4096));
+    pool.run(parts, [&](int p) {
+      for (size_t i = m * (size_t)p / (size_t)parts; i < m * (size_t)(p + 1) / (size_t)parts; ++i)
+        ext[i] = msg_off[i] > region_len ? 0 : message_extent(region + msg_off[i], region_len - msg_off[i]);
+    });
+  }
+  auto extent = [&](size_t i) -> uint64_t { return ext[i]; };
+
+  struct Span {
+    uint64_t lo;
+    std::vector<size_t> msgs;
+  };
+  Span inflight[kSlabs];
+  auto drain = [&](int which) -> int {
+    Span& sp = inflight[which];
+    if (sp.msgs.empty()) return AMBRYCRC_OK;
+    if (hipEventSynchronize(c->slab[which].done) != hipSuccess) return AMBRYCRC_EHIP;
+    const MsgSlab& ms = c->msg_slab[which];
+    for (size_t q = 0; q < sp.msgs.size(); ++q) {
+      status[sp.msgs[q]] = ms.h_status[q];
+      if (msg_end) msg_end[sp.msgs[q]] = ms.h_end[q] ? sp.lo + ms.h_end[q] : 0;
+    }
+    sp.msgs.clear();
+    return AMBRYCRC_OK;
+  };
+  std::vector<CopyJob> copies;
+  size_t oi = 0;
+  int k = 0;
+  while (oi < m && !rc) {
+    const size_t first = order[oi];
+    const uint64_t lo = std::min(msg_off[first], region_len);
+    if (extent(first) > kSlabBytes) {  // oversize: its own device buffer, synchronously
+      uint8_t* d_buf = nullptr;
+      uint64_t* d_o = nullptr;
+      uint32_t* d_s = nullptr;
+      uint64_t* d_e = nullptr;
+      void* d_w = nullptr;
+      const uint64_t zero = 0;
+      uint32_t st = 0;
+      uint64_t en = 0;
+      if (hipMalloc(reinterpret_cast<void**>(&d_buf), ext[first]) != hipSuccess ||
+          hipMalloc(reinterpret_cast<void**>(&d_o), 8) != hipSuccess ||
+          hipMalloc(reinterpret_cast<void**>(&d_s), 4) != hipSuccess ||
+          hipMalloc(reinterpret_cast<void**>(&d_e), 8) != hipSuccess ||
+          hipMalloc(&d_w, ambrycrc_messages_workspace_bytes(1)) != hipSuccess) {
+        rc = AMBRYCRC_ENOMEM;
+      } else if (hipMemcpy(d_buf, region + lo, ext[first], hipMemcpyHostToDevice) != hipSuccess ||
+                 hipMemcpy(d_o, &zero, 8, hipMemcpyHostToDevice) != hipSuccess) {
+        rc = AMBRYCRC_EHIP;
+      } else {
+        rc = enqueue_messages(c, d_buf, ext[first], d_o, 1, d_s, d_e, d_w, nullptr);
+        if (!rc && (hipMemcpy(&st, d_s, 4, hipMemcpyDeviceToHost) != hipSuccess ||
+                    hipMemcpy(&en, d_e, 8, hipMemcpyDeviceToHost) != hipSuccess))
+          rc = AMBRYCRC_EHIP;
+      }
+      (void)hipFree(d_buf);
+      (void)hipFree(d_o);
+      (void)hipFree(d_s);
+      (void)hipFree(d_e);
+      (void)hipFree(d_w);
+      status[first] = st;
+      if (msg_end) msg_end[first] = en ? lo + en : 0;
+      ++oi;
+      continue;
+    }
+    const int w = k % kSlabs;
+    rc = drain(w);
+    if (rc) break;
+    HostSlab& s = c->slab[w];
+    MsgSlab& ms = c->msg_slab[w];
+    Span& sp = inflight[w];
+    sp.lo = lo;
+    uint64_t hi = lo;
+    while (oi < m && sp.msgs.size() < kSlabMsgs) {
+      const size_t i = order[oi];
+      const uint64_t o = std::min(msg_off[i], region_len);
+      const uint64_t e = o + extent(i);
+      if (ext[i] > kSlabBytes || std::max(hi, e) - lo > kSlabBytes) break;
+      hi = std::max(hi, e);
+      ms.h_off[sp.msgs.size()] = o - lo;
+      sp.msgs.push_back(i);
+      ++oi;
+    }
+    const uint64_t span = hi - lo;
+    // an offset past the region end must stay past the slab end (BAD_LAYOUT either way)
+    for (size_t q = 0; q < sp.msgs.size(); ++q)
+      if (msg_off[sp.msgs[q]] > region_len) ms.h_off[q] = span + 1;
+    if (span) {
+      if (pinned) {
+        if (hipMemcpyAsync(s.d_data, region + lo, span, hipMemcpyHostToDevice, s.stream) != hipSuccess) rc = AMBRYCRC_EHIP;
+      } else {
+        copies.clear();
+        copies.push_back({s.h_data, region + lo, span});
+        parallel_copy(copies, span);  // overlaps the DMA of the slabs already issued
+        if (hipMemcpyAsync(s.d_data, s.h_data, span, hipMemcpyHostToDevice, s.stream) != hipSuccess) rc = AMBRYCRC_EHIP;
+      }
+    }
+    const size_t nm = sp.msgs.size();
+    if (!rc && hipMemcpyAsync(ms.d_off, ms.h_off, nm * sizeof(uint64_t), hipMemcpyHostToDevice, s.stream) != hipSuccess)
+      rc = AMBRYCRC_EHIP;
+    if (!rc) rc = enqueue_messages(c, s.d_data, span, ms.d_off, nm, ms.d_status, ms.d_end, ms.d_ws, s.stream);
+    if (!rc && (hipMemcpyAsync(ms.h_status, ms.d_status, nm * sizeof(uint32_t), hipMemcpyDeviceToHost, s.stream) !=
+                    hipSuccess ||
+                hipMemcpyAsync(ms.h_end, ms.d_end, nm * sizeof(uint64_t), hipMemcpyDeviceToHost, s.stream) !=
+                    hipSuccess ||
+                hipEventRecord(s.done, s.stream) != hipSuccess))
+      rc = AMBRYCRC_EHIP;
+    if (rc) {
+      sp.msgs.clear();
+      break;
+    }
+    ++k;
+  }
+  int rc2 = AMBRYCRC_OK;
+  for (int d = 0; d < kSlabs; ++d) {
+    const int r = drain((k + d) % kSlabs);
+    if (!rc2) rc2 = r;
+  }
+  (void)hipSetDevice(prev);
+  return rc ? rc : rc2;
 }
 
 size_t ambrycrc_chain_messages_host(const uint8_t* region, uint64_t region_len, uint64_t start, uint64_t* offs,

@@ -177,6 +177,30 @@ def verify_messages(region, msg_off, stream=None, want_end: bool = True):
     return status, end
 
 
+def verify_messages_host(region, msg_off, device: int = 0, pinned: bool = False):
+    """verify_messages for a region in host memory (bytes, numpy uint8, or a CPU uint8 tensor;
+    pinned=True for a hipHostMalloc'd / pin_memory() buffer). Returns (status uint32[m],
+    msg_end uint64[m]) as numpy arrays."""
+    import numpy as np
+
+    if hasattr(region, "data_ptr"):  # torch CPU tensor
+        ptr, nbytes, keep = region.data_ptr(), region.numel(), region
+    else:
+        arr = np.frombuffer(region, dtype=np.uint8) if isinstance(region, (bytes, bytearray)) else \
+            np.ascontiguousarray(region, dtype=np.uint8)
+        ptr, nbytes, keep = arr.ctypes.data, arr.nbytes, arr
+    offs = np.ascontiguousarray(np.asarray(msg_off, dtype=np.uint64))
+    m = len(offs)
+    status = np.zeros(m, dtype=np.uint32)
+    end = np.zeros(m, dtype=np.uint64)
+    check(lib().ambrycrc_verify_messages_host(
+        ctypes.c_void_p(ptr), nbytes, offs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), m,
+        status.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), end.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+        device, 1 if pinned else 0), "ambrycrc_verify_messages_host")
+    del keep
+    return status, end
+
+
 def chain_messages_host(region: bytes, start: int = 0, max_messages: int = 1 << 20):
     """Offsets of consecutive messages from `start` in a host buffer (BlobStoreRecovery's hop)."""
     buf = (ctypes.c_char * len(region)).from_buffer_copy(region)

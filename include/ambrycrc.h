@@ -147,6 +147,16 @@ int ambrycrc_verify_messages_dev(const uint8_t* d_region, uint64_t region_len, c
                                  uint32_t* d_status, uint64_t* d_msg_end, void* d_ws, size_t ws_bytes,
                                  hipStream_t stream);
 
+/* ambrycrc_verify_messages_dev for a region in HOST memory (a log segment read or mapped
+ * from disk: BlobStoreRecovery's scan, a GET of stored messages). Messages are staged in
+ * offset order through the context's pinned slabs (64 MiB, up to 65,536 messages each; a
+ * message larger than a slab gets its own staging buffer), each slab holding the span its
+ * messages cover, so the status bits and message ends equal those of the whole region.
+ * pinned != 0: region is hipHostMalloc'd / registered (copied by DMA directly). status[m],
+ * msg_end[m] (may be NULL): host arrays. Synchronous. */
+int ambrycrc_verify_messages_host(const uint8_t* region, uint64_t region_len, const uint64_t* msg_off, size_t m,
+                                  uint32_t* status, uint64_t* msg_end, int device, int pinned);
+
 /* Host-side message chain for a log region in host memory (the sequential hop of
  * BlobStoreRecovery.recover, BlobStoreRecovery.java:43-110): starting at `start`,
  * read each header (V1/V2/V3, header CRC checked) and follow its size to the next

@@ -109,3 +109,58 @@ def test_stored_crc_bytes_corrupted_group_phase(gpu, variant):
     assert st == [s for s, _ in expect]
     assert end == [e for _, e in expect]
     assert sum(1 for s in st if s) == 400
+
+
+def _host_case(n_msgs, seed):
+    """Region > one 64 MiB staging slab, messages listed out of order, with offsets at and past
+    the region end, a message truncated by the region end and one whose header claims a size
+    past it."""
+    region, offs, _ = build_region(n=n_msgs, seed=seed, corrupt_frac=0.05, big_every=3)
+    region = bytearray(region)
+    # a header whose total size runs past the region end (layout error, header-only read)
+    huge = bytearray(MF.put_message(MF.store_key("huge"), MF.blob_properties_bytes(10), b"u", bytes(10)))
+    offs.append(len(region))
+    region += huge
+    last = MF.put_message(MF.store_key("cut"), MF.blob_properties_bytes(3000), b"m" * 10, bytes(3000))
+    offs.append(len(region))
+    region += last[:-50]  # truncated by the region end
+    region = bytes(region)
+    offs += [len(region), len(region) + 7]
+    rng = np.random.default_rng(seed)
+    perm = rng.permutation(len(offs))
+    offs = [offs[i] for i in perm]
+    expect = [MF.verify_message(region, o) if o + 2 <= len(region) else (MF.BAD_LAYOUT, 0) for o in offs]
+    return region, offs, expect
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_verify_messages_host_matches_oracle(gpu, pinned):
+    """ambrycrc_verify_messages_host (host region staged through the pinned slabs) gives the
+    oracle's status and message end for every message, across slab boundaries."""
+    import torch
+
+    region, offs, expect = _host_case(1500, 31)
+    assert len(region) > (64 << 20)
+    if pinned:
+        host = torch.from_numpy(np.frombuffer(region, dtype=np.uint8).copy()).pin_memory()
+    else:
+        host = region
+    st, end = gpu.verify_messages_host(host, offs, device=0, pinned=pinned)
+    assert st.tolist() == [s for s, _ in expect]
+    assert end.tolist() == [e for _, e in expect]
+    assert sum(1 for s in st if s) >= 70
+
+
+def test_verify_messages_host_oversize_message(gpu):
+    """A message larger than a staging slab (a 70 MB blob) takes its own staging buffer."""
+    big = MF.put_message(MF.store_key("big"), MF.blob_properties_bytes(70 << 20), b"meta", bytes(70 << 20))
+    small = MF.put_message(MF.store_key("s"), MF.blob_properties_bytes(100), b"x", bytes(range(100)))
+    bad = bytearray(big)
+    bad[len(bad) // 2] ^= 4
+    region = small + big + bytes(bad) + small
+    offs = [0, len(small), len(small) + len(big), len(small) + 2 * len(big)]
+    expect = [MF.verify_message(region, o) for o in offs]
+    st, end = gpu.verify_messages_host(region, offs)
+    assert st.tolist() == [s for s, _ in expect]
+    assert end.tolist() == [e for _, e in expect]
+    assert st[2] == MF.BLOB_CRC and st[1] == 0

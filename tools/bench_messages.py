@@ -59,7 +59,7 @@ def c1_cpu(mf, reps=2000):
             "note": "oracle/crc32_ref.c via ctypes (includes ~1 us/record call overhead)"}
 
 
-def gpu_region(mf, m, blob_bytes, reps, variant=None):
+def gpu_region(mf, m, blob_bytes, reps, variant=None, host=False):
     import numpy as np
     import torch
 
@@ -115,9 +115,39 @@ def gpu_region(mf, m, blob_bytes, reps, variant=None):
         times.append(e0.elapsed_time(e1))
     times.sort()
     med = times[len(times) // 2]
-    return {"config": f"verify {m} x PUT({blob_bytes} B blob)", "variant": variant, "messages": m, "region_bytes": m * L,
-            "ms_median": round(med, 4), "GiBps": round(m * L / (med / 1e3) / 2**30, 1),
-            "messages_per_s": round(m / (med / 1e3)), "parity": "clean=0, 1% injected flips flagged exactly"}
+    res = {"config": f"verify {m} x PUT({blob_bytes} B blob)", "variant": variant, "messages": m, "region_bytes": m * L,
+           "ms_median": round(med, 4), "GiBps": round(m * L / (med / 1e3) / 2**30, 1),
+           "messages_per_s": round(m / (med / 1e3)), "parity": "clean=0, 1% injected flips flagged exactly"}
+    if host and m * L <= (5 << 30):
+        res["host"] = host_region_rate(D, region, base, m, L)
+    return res
+
+
+def host_region_rate(D, region, base, m, L):
+    """The same region from host memory through ambrycrc_verify_messages_host (PCIe-inclusive):
+    pageable (numpy) and pinned (pin_memory) sources, best of 3 after one untimed pass."""
+    import numpy as np
+
+    host = region.cpu().numpy()
+    offs = base.cpu().numpy().astype(np.uint64)
+    out = {}
+    for name, src, pinned in (("pageable", host, False), ("pinned", None, True)):
+        if pinned:
+            import torch
+
+            src = torch.from_numpy(host).pin_memory()
+        st, _ = D.verify_messages_host(src, offs, pinned=pinned)
+        assert int(st.sum()) == 0, "host verify of the clean region"
+        best = None
+        for _ in range(3):
+            t0 = time.perf_counter()
+            D.verify_messages_host(src, offs, pinned=pinned)
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+        out[name + "_GiBps"] = round(m * L / best / 2**30, 2)
+        del src
+    out["what"] = "ambrycrc_verify_messages_host, synchronous, host region staged through the pinned slabs"
+    return out
 
 
 def main():
@@ -126,6 +156,7 @@ def main():
     ap.add_argument("--no-gpu", action="store_true")
     ap.add_argument("--variants", default="0")
     ap.add_argument("--cases", default="64k,4m,4k", help="subset of 64k,4m,4k")
+    ap.add_argument("--host", action="store_true", help="also time the host-region path (regions <= 5 GiB)")
     args = ap.parse_args()
     mf = load_mf()
     print(json.dumps(c1_cpu(mf)), flush=True)
@@ -134,7 +165,7 @@ def main():
     cases = {"64k": (65536, 64 << 10), "4m": (4096, 4 << 20), "4k": (262144, 4 << 10)}
     for m, s in (cases[c] for c in args.cases.split(",")):
         for v in [int(x) for x in args.variants.split(",")]:
-            print(json.dumps(gpu_region(mf, m, s, args.reps, v)), flush=True)
+            print(json.dumps(gpu_region(mf, m, s, args.reps, v, args.host)), flush=True)
 
 
 if __name__ == "__main__":
