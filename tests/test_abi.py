@@ -126,6 +126,33 @@ def test_batch_dev_without_init_fails_loudly(ambry):
     assert rc == AMBRYCRC_ENOINIT
 
 
+def test_host_entry_points_without_init_fail_loudly(ambry):
+    """The host-resident entry points (batch, messages, file ranges) return ENOINIT without a
+    device context, and EINVAL for null arguments, before touching any memory."""
+    import ctypes
+
+    import numpy as np
+
+    from ambry_amd._lib import AMBRYCRC_EINVAL, AMBRYCRC_ENOINIT
+
+    lib = ambry.lib()
+    data = np.zeros(64, dtype=np.uint8)
+    offs = (ctypes.c_uint64 * 1)(0)
+    st = (ctypes.c_uint32 * 1)()
+    end = (ctypes.c_uint64 * 1)()
+    ptr = ctypes.c_void_p(data.ctypes.data)
+    assert lib.ambrycrc_verify_messages_host(ptr, 64, offs, 1, st, end, 0, 0) == AMBRYCRC_ENOINIT
+    assert lib.ambrycrc_verify_messages_host(ptr, 64, None, 1, st, end, 0, 0) == AMBRYCRC_EINVAL
+    assert lib.ambrycrc_verify_messages_host(ptr, 64, offs, 0, st, end, 0, 0) == 0  # nothing to do
+    ptrs = (ctypes.c_void_p * 1)(data.ctypes.data)
+    lens = (ctypes.c_uint64 * 1)(64)
+    out = (ctypes.c_uint32 * 1)()
+    assert lib.ambrycrc_batch_host(ptrs, lens, None, out, 1, 0, 0) == AMBRYCRC_ENOINIT
+    first = (ctypes.c_int64 * 1)(0)
+    second = (ctypes.c_int64 * 1)(-1)
+    assert lib.ambrycrc_range_checksums_host(ptr, 64, first, second, 1, out, 0) == AMBRYCRC_EINVAL
+
+
 def test_host_update_every_cpu_impl():
     """Each host implementation (slice-by-8, SSE PCLMULQDQ fold, AVX-512 VPCLMULQDQ fold) is
     bit-exact with zlib (java.util.zip.CRC32's function) at every length 0..1100 (crossing the
