@@ -124,7 +124,9 @@ struct DevCtx {
   // chunks from 0.51 to 1.6 TB/s, 1 KiB from 3.8 to 5.0 TB/s and the 4 KiB-blob message
   // verify from 1.96 to 3.1 TiB/s; the group runs took 4 KiB chunks from 5.5 to 5.9 TB/s
   // and 16 KiB from 5.9 to 6.5, and in the 8-lane groups 512 B - 1 KiB chunks by 3-4 %.
-  int variant = 28;
+  // 29 = 28 with s_setprio 3 while a wave issues its super-block loads: +0.2-0.5 % on C2,
+  // C3, C4 in interleaved sweeps (r01f).
+  int variant = 29;
   uint32_t* d_img = nullptr;
   void* d_ws = nullptr;
   size_t ws_bytes = 0;
@@ -313,7 +315,7 @@ uint64_t batch_small_max(const DevCtx* c, size_t n) {
                             : group_small_max(group_mode);
 }
 
-// exp_fill: SweepArgs::exp_fill (message verify; honoured by variants 26-28 only).
+// exp_fill: SweepArgs::exp_fill (message verify; honoured by variants 26-29 only).
 int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len, const uint32_t* crc_in,
                   uint32_t* out, size_t n, void* ws, hipStream_t s, uint32_t* exp_fill = nullptr) {
   if (n == 0) return AMBRYCRC_OK;
@@ -868,9 +870,9 @@ int enqueue_messages(DevCtx* c, const uint8_t* d_region, uint64_t region_len, co
   a.crc = crc;
   a.status = d_status;
   a.msg_end = d_msg_end;
-  // The class-sized group phase (variants 26-28) reads the stored CRCs of the records it
+  // The class-sized group phase (variants 26-29) reads the stored CRCs of the records it
   // takes whole; the parse kernel reads the rest.
-  const bool inline_exp = c->variant >= 26 && c->variant <= 28;
+  const bool inline_exp = c->variant >= 26 && c->variant <= 29;
   a.inline_max = inline_exp ? batch_small_max(c, j) : 0;
   void* batch_ws = w + ((j * 2 * sizeof(uint64_t) + j * 2 * sizeof(uint32_t) + j + 255) & ~size_t(255));
   if (launch_msg_parse(a, stream) != hipSuccess) return AMBRYCRC_EHIP;

@@ -38,7 +38,7 @@ struct SweepArgs {
   const uint64_t* small_total;  // [4] as PlanArgs
   uint64_t* claim;              // = PlanArgs small_total + 4 (dynamic shares, variant 27)
   const uint32_t* small_idx;
-  // Message verify (class-sized group phase only, variants 26-28): for every chunk the group
+  // Message verify (class-sized group phase only, variants 26-29): for every chunk the group
   // phase takes, also read the big-endian 8-B CRC stored right after it (base + off + len)
   // and write exp_fill[chunk] = its low word, or ~crc when the high word is not zero (a
   // forced mismatch: a CRC-32 never has upper bits). Null otherwise.
@@ -85,7 +85,7 @@ constexpr uint64_t group_small_max(int mode) {
 // 28 = 27 with 64-B lane runs in the 8-lane groups of class 1 (257 B - 1 KiB) too
 // (two super-blocks, 8 loads per lane, in flight in the sweep body: -6 % on C3, -4 % on C2
 // at the 128-VGPR cap)
-constexpr int kNumVariants = 29;
+constexpr int kNumVariants = 30;
 constexpr int kDiagNoFold = 100;  // diagnostic timing build, selectable via ambrycrc_set_variant only
 
 // Message verify (message_kernels.hip): kMsgSlots CRC jobs per message, slot order

@@ -500,7 +500,7 @@ __device__ __forceinline__ void qt(u32x4 (&x)[4], uint32_t lane) {
   else quad_transpose(x, lane);
 }
 
-template <int UB, bool NT, bool ASMT = false>
+template <int UB, bool NT, bool ASMT = false, bool PRIO = false>
 __device__ __forceinline__ uint32_t body_crc_t4(const uint8_t* __restrict__ base, uint64_t bs, uint64_t be,
                                                 uint32_t lane, const LaneConst& k) {
   constexpr uint64_t SB = 4 * (uint64_t)kBlockBytes;
@@ -540,11 +540,13 @@ __device__ __forceinline__ uint32_t body_crc_t4(const uint8_t* __restrict__ base
 #pragma unroll
       for (int u = 0; u < UB; ++u) {
         u32x4 cur[4];
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);  // loads first among the SIMD's waves
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           cur[i] = buf[u][i];
           buf[u][i] = ld16<NT>(q + (b + UB + u) * 256 + i * 64);
         }
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
         qt<ASMT>(cur, lane);
         s = run_crc<4>(cur, k, nib_mul(s, kFold));
       }
@@ -1142,7 +1144,7 @@ __global__ __launch_bounds__(TPB) void crc32_sweep_kernel(SweepArgs a) {
     uint32_t r = 0;
     if (sa < be) {
       if constexpr (LR < 0) {
-        r = body_crc_t4<(U >> 2) < 1 ? 1 : (U >> 2), NT, LR == -3>(a.base, sa, be, lane, k);
+        r = body_crc_t4<(U >> 2) < 1 ? 1 : (U >> 2), NT, LR <= -3, LR == -4>(a.base, sa, be, lane, k);
       } else if constexpr (LR > 0) {
         r = body_crc_runs<(U >> LR) < 1 ? 1 : (U >> LR), NT, LR>(a.base, sa, be, lane, k);
       } else {
@@ -1527,6 +1529,8 @@ hipError_t launch_sweep(const SweepArgs& a, int grid, int variant, hipStream_t s
     case 27: hipLaunchKernelGGL((crc32_sweep_kernel<4, true, true, false, true, 0, -3, 16, 64, 1024, 4>), dim3(grid), dim3(1024), 0, s, a); break;
     // 27 with 64-B lane runs in the 8-lane groups of class 1 (257 B - 1 KiB) too
     case 28: hipLaunchKernelGGL((crc32_sweep_kernel<4, true, true, false, true, 0, -3, 16, 64, 1024, 5>), dim3(grid), dim3(1024), 0, s, a); break;
+    // 29 (default): variant 28 with s_setprio 3 around each super-block's loads
+    case 29: hipLaunchKernelGGL((crc32_sweep_kernel<4, true, true, false, true, 0, -4, 16, 64, 1024, 5>), dim3(grid), dim3(1024), 0, s, a); break;
     // timing-only diagnostics (wrong CRCs): 100 FOLD lookups removed, 101 no per-segment
     // atomic, 102 no wave tree
     case kDiagNoFold: hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, true, true, 1>), dim3(grid), dim3(1024), 0, s, a); break;

@@ -219,15 +219,16 @@ int ambrycrc_range_checksums_host(const uint8_t* file, uint64_t file_len, const 
 
 /* ------------------------------------------------------- tuning / telemetry */
 
-/* Kernel variant (0..28; crc32_kernels.h lists them). 0..13: sweep-kernel shapes (blocks in
+/* Kernel variant (0..29; crc32_kernels.h lists them). 0..13: sweep-kernel shapes (blocks in
  * flight per lane, load policy, prefetch scheme, lane runs) for every chunk; 14..19: sweep
  * variant 0 plus a separate group kernel for whole chunks up to 2..16 KiB; 20..26: the
  * group phase fused into the sweep launch. Group modes engage for batches of >= 16384
  * chunks; smaller batches take the sweep for every chunk (latency).
- * Default 28 = 64-B lane runs (coalesced loads, quad transpose by v_cndmask_b32_dpp, one
+ * 28 = 64-B lane runs (coalesced loads, quad transpose by v_cndmask_b32_dpp, one
  * fold per 64 B) with the group phase for whole chunks <= 16 KiB sized per size class
  * (4 / 8 / 16 lanes per chunk, 64-B lane runs in the 8- and 16-lane groups) and spread over
- * all waves per class.
+ * all waves per class. Default 29 = 28 with the wave's priority raised (s_setprio 3)
+ * while it issues each super-block's loads.
  * 100..102 are timing diagnostics that produce wrong CRCs. ambrycrc_get_variant returns
  * the current one. */
 int ambrycrc_set_variant(int device, int variant);

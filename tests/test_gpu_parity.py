@@ -108,7 +108,7 @@ def test_ragged_batch_grid_sizes(gpu, oracle, grid):
     assert np.array_equal(got, oracle.batch(mem, off, ln, threads=8))
 
 
-@pytest.mark.parametrize("variant", list(range(29)))
+@pytest.mark.parametrize("variant", list(range(30)))
 def test_kernel_variants(gpu, oracle, variant):
     rng = np.random.default_rng(100 + variant)
     mem = stream_bytes(6, 0, 16 << 20)
@@ -123,7 +123,7 @@ def test_kernel_variants(gpu, oracle, variant):
     assert np.array_equal(got, oracle.batch(mem, off, ln, threads=8))
 
 
-@pytest.mark.parametrize("variant", [0, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28])
+@pytest.mark.parametrize("variant", [0, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29])
 @pytest.mark.parametrize("grid", [0, 3])
 def test_small_chunk_group_kernel(gpu, oracle, variant, grid):
     """Group phase (variants 14-24): whole chunks <= 2..16 KiB, G lanes each, init register
