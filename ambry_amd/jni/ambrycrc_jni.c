@@ -16,6 +16,8 @@
  *   static native int  nativeInit(int device);
  *   static native int  nativeBatchDirect(java.nio.ByteBuffer[] bufs, int[] pos, int[] len,
  *                                        int[] crcIn, int[] out, int device);
+ *   static native int  nativeVerifyMessages(java.nio.ByteBuffer region, long[] offsets,
+ *                                           int[] status, long[] ends, int device);
  * Errors are returned as negative ints (AMBRYCRC_E*); the Java wrapper maps them
  * to exceptions. CRC values travel as Java ints holding the uint32 bit pattern.
  */
@@ -106,5 +108,37 @@ done:
   free(lens);
   free(cin);
   free(res);
+  return rc;
+}
+
+/* Verify every CRC of the PUT / update messages at `offsets` in a direct ByteBuffer holding a
+ * log-segment region (BlobStoreRecovery.java:43-110 scan, MessageFormatSend.java:131-139 on
+ * GET, ValidatingTransformer.java:46-104 on replication) -> ambrycrc_verify_messages_host.
+ * status[i]: AMBRYCRC_MSG_* bits (0 = every CRC matches); ends[i]: message end or 0. */
+JNIEXPORT jint JNICALL JNI_FN(nativeVerifyMessages)(JNIEnv* env, jclass cls, jobject region, jlongArray offsets,
+                                                    jintArray status, jlongArray ends, jint device) {
+  (void)cls;
+  const jsize m = (*env)->GetArrayLength(env, offsets);
+  if (m <= 0) return AMBRYCRC_OK;
+  const uint8_t* base = (const uint8_t*)(*env)->GetDirectBufferAddress(env, region);
+  const jlong cap = (*env)->GetDirectBufferCapacity(env, region);
+  if (!base || cap < 0 || (*env)->GetArrayLength(env, status) < m ||
+      (ends && (*env)->GetArrayLength(env, ends) < m))
+    return AMBRYCRC_EINVAL;
+  uint64_t* offs = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)m);
+  uint32_t* st = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)m);
+  uint64_t* en = ends ? (uint64_t*)malloc(sizeof(uint64_t) * (size_t)m) : NULL;
+  jint rc = AMBRYCRC_ENOMEM;
+  if (offs && st && (!ends || en)) {
+    (*env)->GetLongArrayRegion(env, offsets, 0, m, (jlong*)offs);  /* jlong and uint64_t: same width */
+    rc = ambrycrc_verify_messages_host(base, (uint64_t)cap, offs, (size_t)m, st, en, device, 0);
+    if (rc == AMBRYCRC_OK) {
+      (*env)->SetIntArrayRegion(env, status, 0, m, (const jint*)st);
+      if (ends) (*env)->SetLongArrayRegion(env, ends, 0, m, (const jlong*)en);
+    }
+  }
+  free(offs);
+  free(st);
+  free(en);
   return rc;
 }
