@@ -62,6 +62,7 @@ _SIGNATURES = [
     ("ambrycrc_set_variant", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     ("ambrycrc_get_variant", ctypes.c_int, [ctypes.c_int]),
     ("ambrycrc_set_grid", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    ("ambrycrc_set_window", ctypes.c_int, [ctypes.c_int, ctypes.c_uint64]),
     ("ambrycrc_timing_enable", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     ("ambrycrc_timing_collect", ctypes.c_int,
      [ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),

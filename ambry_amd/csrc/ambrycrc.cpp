@@ -127,6 +127,8 @@ struct DevCtx {
   // 29 = 28 with s_setprio 3 while a wave issues its super-block loads: +0.2-0.5 % on C2,
   // C3, C4 in interleaved sweeps (r01f).
   int variant = 29;
+  // Sweep rounds of at most this many bytes (SweepArgs::window); 0 = one round.
+  uint64_t window = 32ull << 30;
   uint32_t* d_img = nullptr;
   void* d_ws = nullptr;
   size_t ws_bytes = 0;
@@ -353,6 +355,7 @@ int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uin
   t.claim = p.small_total + 4;
   t.small_idx = p.small_idx;
   t.exp_fill = exp_fill;
+  t.window = c->window;
   EventPair ev{nullptr, nullptr};
   if (c->timing) {
     std::lock_guard<std::mutex> g(c->mu);
@@ -781,6 +784,14 @@ int ambrycrc_set_grid(int device, int workgroups) {
 int ambrycrc_grid_size(int device) {
   DevCtx* c = ctx_for(device);
   return c ? c->grid : 0;
+}
+
+int ambrycrc_set_window(int device, uint64_t bytes) {
+  DevCtx* c = ctx_for(device);
+  if (!c) return AMBRYCRC_ENOINIT;
+  if (bytes != 0 && bytes < (1u << 20)) return AMBRYCRC_EINVAL;
+  c->window = bytes;
+  return AMBRYCRC_OK;
 }
 
 int ambrycrc_timing_enable(int device, int enable) {

@@ -43,6 +43,10 @@ struct SweepArgs {
   // and write exp_fill[chunk] = its low word, or ~crc when the high word is not zero (a
   // forced mismatch: a CRC-32 never has upper bits). Null otherwise.
   uint32_t* exp_fill;
+  // Byte-share rounds: a batch of more than `window` bytes is swept in R = ceil(total /
+  // window) rounds of nwaves shares each (share i -> wave i % nwaves), so at any time the
+  // waves read inside about one window, not across the whole batch. 0 = one round.
+  uint64_t window;
 };
 
 // Group kernel shapes (mode -> G lanes per chunk, NB blocks of 16G bytes): small_max = 16*G*NB.

@@ -125,6 +125,11 @@ def set_grid(device: int, workgroups: int) -> None:
     check(lib().ambrycrc_set_grid(device, workgroups), "ambrycrc_set_grid")
 
 
+def set_window(device: int, nbytes: int) -> None:
+    """Sweep rounds of at most nbytes (0 = one round); see ambrycrc_set_window."""
+    check(lib().ambrycrc_set_window(device, nbytes), "ambrycrc_set_window")
+
+
 def grid_size(device: int = 0) -> int:
     return lib().ambrycrc_grid_size(device)
 

@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS) + ["c4"])
     ap.add_argument("--variant", type=int, default=None)
     ap.add_argument("--grid", type=int, default=None, help="sweep-kernel workgroups (default: one per CU)")
+    ap.add_argument("--window", type=int, default=None,
+                    help="sweep rounds of at most this many bytes (default: the library's 32 GiB; 0 = one round)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-path", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -288,6 +290,8 @@ def main():
         D.set_variant(dev.index, args.variant)
     if args.grid is not None:
         D.set_grid(dev.index, args.grid)
+    if args.window is not None:
+        D.set_window(dev.index, args.window)
 
     log(args, f"rank {rank}/{world}: building workload {args.config}")
     buf, off_t, len_t, n, total, chunk, desc = build_workload(torch, dev, args, rank)
@@ -395,7 +399,8 @@ def main():
         "config": {"workload": desc, "chunks_per_gpu": n, "chunk_bytes": chunk, "bytes_per_gpu_step": total,
                    "parallelism": f"shard{world}" + ("+rccl_allgather" if use_dist else ""),
                    "kernel_variant": D.get_variant(dev.index),
-                   "grid_workgroups": D.grid_size(dev.index)},
+                   "grid_workgroups": D.grid_size(dev.index),
+                   "sweep_window_bytes": args.window if args.window is not None else 32 << 30},
         "roofline": {
             "bound": "hbm",
             "kernel": "crc32_sweep_kernel",

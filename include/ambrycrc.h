@@ -236,6 +236,11 @@ int ambrycrc_get_variant(int device);
 /* Grid size of the persistent sweep kernel (workgroups; 0 = one per CU). */
 int ambrycrc_set_grid(int device, int workgroups);
 
+/* Sweep rounds: a batch of more than `bytes` is swept in rounds of at most that many bytes,
+ * so the waves read inside one window at a time (default 32 GiB; 0 = one round over the
+ * whole batch; otherwise >= 1 MiB). Same results either way. */
+int ambrycrc_set_window(int device, uint64_t bytes);
+
 /* When enabled, every batch's CRC kernels (group kernel + sweep kernel, not the plan) are
  * bracketed by HIP events on the caller's stream; ambrycrc_timing_collect() waits for them
  * and returns the sum and count of those durations since the last collect. */

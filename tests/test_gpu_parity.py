@@ -256,6 +256,46 @@ def _full_size_check(gpu, oracle, n_chunks, chunk, seed, sample):
     del buf
 
 
+@pytest.mark.parametrize("window", [1 << 20, 3 << 20, 0])
+def test_sweep_rounds_window(gpu, oracle, window):
+    """Sweep rounds (ambrycrc_set_window): a 1 MiB or 3 MiB window turns a ~27 MiB ragged batch
+    into many rounds of shares, so chunks are cut at round as well as wave boundaries; 0 = one
+    round. Results equal the oracle either way, with crc_in and empty chunks mixed in."""
+    rng = np.random.default_rng(window + 3)
+    mem = stream_bytes(9, 0, 40 << 20)
+    n = 400
+    ln = rng.integers(0, 300000, size=n)
+    ln[:8] = [0, 1, 17, 4096, 1 << 20, (3 << 20) + 5, 16, 0]
+    off = rng.integers(0, (40 << 20) - (4 << 20), size=n)
+    cin = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32)
+    cin[::2] = 0
+    gpu.set_window(0, window)
+    try:
+        got = run_batch(gpu, mem, off, ln, crc_in=cin)
+    finally:
+        gpu.set_window(0, 32 << 30)
+    assert np.array_equal(got, oracle.batch(mem, off, ln, crc_in=cin, threads=8))
+
+
+def test_c3_full_size_rounds(gpu, oracle):
+    """C3 swept in 4 GiB rounds (8 rounds of 16,384 shares) gives the same CRCs as one round."""
+    torch = _torch()
+    total = 8192 * (4 << 20)
+    buf = torch.empty(total, dtype=torch.uint8, device="cuda")
+    gpu.fill_random(buf, 0xC3, 0)
+    off = dev_u64(np.arange(8192, dtype=np.int64) * (4 << 20))
+    ln = dev_u64(np.full(8192, 4 << 20, dtype=np.int64))
+    one = host_u32(gpu.crc32_batch(buf, off, ln))
+    gpu.set_window(0, 4 << 30)
+    try:
+        rounds = host_u32(gpu.crc32_batch(buf, off, ln))
+    finally:
+        gpu.set_window(0, 32 << 30)
+    assert np.array_equal(one, rounds)
+    assert oracle.crc32(buf[:4 << 20].cpu().numpy()) == int(one[0])
+    del buf
+
+
 def test_c2_full_size(gpu, oracle):
     """C2: 65,536 x 64 KiB."""
     _full_size_check(gpu, oracle, 65536, 64 << 10, 0xC2, sample=64)
