@@ -248,10 +248,12 @@ class KernelModel:
         return out
 
     def batch(self, mem: np.ndarray, off, length, crc_in=None, nwaves: int = 4096, quantum: int = 1024,
-              run: int = 1, group=None, min_share: int = 0):
+              run: int = 1, group=None, min_share: int = 0, window: int = 0):
         """Replays plan + sweep kernels with `nwaves` waves; returns the list of CRCs.
         group=(G, nbmax): runs of whole chunks of <= 16*G*nbmax bytes inside a 64-descriptor
-        window go through group_crc, up to 64/G at a time, as the kernel's group mode does."""
+        window go through group_crc, up to 64/G at a time, as the kernel's group mode does.
+        window: sweep rounds (SweepArgs::window) -- a batch of more than `window` bytes is cut
+        into R rounds of nwaves equal shares; wave w takes shares w, w + nwaves, ..."""
         n = len(off)
         off = [int(x) for x in off]
         length = [int(x) for x in length]
@@ -262,11 +264,21 @@ class KernelModel:
         out = [0 if length[c] else (0 if crc_in is None else int(crc_in[c])) for c in range(n)]
         share = ((total + nwaves - 1) // nwaves + quantum - 1) // quantum * quantum
         share = max(share, min_share)
+        step = 0
+        if window and total > window:
+            rounds = (total + window - 1) // window
+            share = ((total + rounds * nwaves - 1) // (rounds * nwaves) + quantum - 1) // quantum * quantum
+            share = max(share, min_share)
+            step = nwaves * share
+        shares = []
         for w in range(nwaves):
             g0 = w * share
-            if share == 0 or g0 >= total:
-                break
-            g1 = min(total, g0 + share)
+            while share and g0 < total:
+                shares.append((g0, min(total, g0 + share)))
+                if not step:
+                    break
+                g0 += step
+        for g0, g1 in shares:
             c = bisect.bisect_right(byte_start, g0, 0, n) - 1
             win_end = c + 64
             while c < n:

@@ -82,3 +82,15 @@ def test_model_group_mode(model, oracle, group):
     for nw, ms in ((1, 0), (3, 0), (7, 32768)):
         assert model.batch(mem, off, ln, crc_in=cin, nwaves=nw, group=group, min_share=ms) == exp
     assert model.batch(mem, off, ln, nwaves=2, group=group) == list(oracle.batch(mem, off, ln))
+
+
+@pytest.mark.parametrize("nwaves,window", [(3, 50000), (7, 100000), (64, 20000), (5, 300000)])
+def test_model_sweep_rounds(model, oracle, nwaves, window):
+    """Sweep rounds (SweepArgs::window): shares w, w + nwaves, ... over R rounds cut chunks at
+    round boundaries too; the XOR of the segment results is still each chunk's CRC."""
+    mem = stream_bytes(77, 0, 300000)
+    off = [c[0] for c in CASES]
+    ln = [c[1] for c in CASES]
+    exp = list(oracle.batch(mem, off, ln))
+    assert model.batch(mem, off, ln, nwaves=nwaves, window=window, run=-4) == exp
+    assert model.batch(mem, off, ln, nwaves=nwaves, window=window, min_share=16384) == exp
