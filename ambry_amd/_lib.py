@@ -44,6 +44,12 @@ _SIGNATURES = [
     ("ambrycrc_verify_messages_host", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t,
       ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint64), ctypes.c_int, ctypes.c_int]),
+    ("ambrycrc_trailed_workspace_bytes", ctypes.c_size_t, [ctypes.c_size_t]),
+    ("ambrycrc_verify_trailed_dev", ctypes.c_int,
+     [_u8p, _u8p, _u8p, _u8p, _u8p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    ("ambrycrc_verify_trailed_host", ctypes.c_int,
+     [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint8),
+      ctypes.c_size_t, ctypes.c_int, ctypes.c_int]),
     ("ambrycrc_chain_messages_host", ctypes.c_size_t,
      [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t]),
     ("ambrycrc_batch_host", ctypes.c_int,

@@ -1118,6 +1118,64 @@ int ambrycrc_verify_messages_host(const uint8_t* region, uint64_t region_len, co
   return rc ? rc : rc2;
 }
 
+size_t ambrycrc_trailed_workspace_bytes(size_t n) {
+  const size_t own = (n * (sizeof(uint64_t) + 2 * sizeof(uint32_t) + 1) + 255) & ~size_t(255);
+  return own + ws_need(n);
+}
+
+int ambrycrc_verify_trailed_dev(const uint8_t* d_base, const uint64_t* d_off, const uint64_t* d_len,
+                                uint8_t* d_mismatch, uint32_t* d_mismatch_count, size_t n, void* d_ws,
+                                size_t ws_bytes, hipStream_t stream) {
+  if (n == 0) return AMBRYCRC_OK;
+  if (!d_base || !d_off || !d_len || (n >> 32)) return AMBRYCRC_EINVAL;
+  DevCtx* c = ctx_current();
+  if (!c) return AMBRYCRC_ENOINIT;
+  const size_t need = ambrycrc_trailed_workspace_bytes(n);
+  if (d_ws) {
+    if (ws_bytes < need) return AMBRYCRC_EINVAL;
+  } else {
+    std::lock_guard<std::mutex> g(c->mu);
+    int rc = ensure_ws(c, need);
+    if (rc) return rc;
+    d_ws = c->d_ws;
+  }
+  uint8_t* w = static_cast<uint8_t*>(d_ws);
+  TrailerArgs a;
+  a.base = d_base;
+  a.off = d_off;
+  a.len = d_len;
+  a.n = n;
+  a.job_len = reinterpret_cast<uint64_t*>(w);
+  a.expected = reinterpret_cast<uint32_t*>(a.job_len + n);
+  uint32_t* crc = a.expected + n;
+  a.crc = crc;
+  a.force = reinterpret_cast<uint8_t*>(crc + n);
+  a.mismatch = d_mismatch;
+  a.count = d_mismatch_count;
+  const bool inline_exp = c->variant >= 26 && c->variant <= 29;
+  a.inline_max = inline_exp ? batch_small_max(c, n) : 0;
+  void* batch_ws = w + ((n * (sizeof(uint64_t) + 2 * sizeof(uint32_t) + 1) + 255) & ~size_t(255));
+  if (launch_trailer_parse(a, stream) != hipSuccess) return AMBRYCRC_EHIP;
+  int rc = enqueue_batch(c, d_base, d_off, a.job_len, nullptr, crc, n, batch_ws, stream,
+                         a.inline_max ? a.expected : nullptr);
+  if (rc) return rc;
+  return hip_err(launch_trailer_verify(a, stream));
+}
+
+int ambrycrc_verify_trailed_host(const void* const* ptrs, const uint64_t* lens, uint8_t* mismatch, size_t n,
+                                 int device, int pinned) {
+  if (n == 0) return AMBRYCRC_OK;
+  if (!ptrs || !lens || !mismatch) return AMBRYCRC_EINVAL;
+  std::vector<uint64_t> body(n);
+  for (size_t i = 0; i < n; ++i) body[i] = lens[i] >= 8 ? lens[i] - 8 : 0;
+  std::vector<uint32_t> crc(n);
+  const int rc = ambrycrc_batch_host(ptrs, body.data(), nullptr, crc.data(), n, device, pinned);
+  if (rc) return rc;
+  for (size_t i = 0; i < n; ++i)
+    mismatch[i] = lens[i] < 8 || rd_be64(static_cast<const uint8_t*>(ptrs[i]) + body[i]) != (uint64_t)crc[i];
+  return AMBRYCRC_OK;
+}
+
 size_t ambrycrc_chain_messages_host(const uint8_t* region, uint64_t region_len, uint64_t start, uint64_t* offs,
                                     size_t max) {
   if (!region || !offs) return 0;

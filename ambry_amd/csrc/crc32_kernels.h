@@ -112,6 +112,25 @@ struct MsgArgs {
                             // group phase (SweepArgs::exp_fill), not by the parse kernel
 };
 
+// CRC-trailered records (index segment files, log segment headers, user metadata, ...):
+// item i = [off[i], off[i] + len[i]) ends in its own big-endian 8-B CRC.
+struct TrailerArgs {
+  const uint8_t* base;
+  const uint64_t* off;      // [n]
+  const uint64_t* len;      // [n] including the 8-B trailer
+  uint64_t n;
+  uint64_t* job_len;        // [n] = len - 8 (0 when len < 8)
+  uint32_t* expected;       // [n] stored CRC (low word); left to the group phase for 1..inline_max
+  uint8_t* force;           // [n] 1 = mismatch whatever the CRC (len < 8, or a stored high word)
+  const uint32_t* crc;      // [n] computed
+  uint8_t* mismatch;        // [n] or null
+  uint32_t* count;          // or null
+  uint64_t inline_max;
+};
+
+hipError_t launch_trailer_parse(const TrailerArgs& a, hipStream_t s);
+hipError_t launch_trailer_verify(const TrailerArgs& a, hipStream_t s);
+
 hipError_t launch_msg_parse(const MsgArgs& a, hipStream_t s);
 hipError_t launch_msg_reduce(const MsgArgs& a, hipStream_t s);
 

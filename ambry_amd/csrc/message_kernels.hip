@@ -245,6 +245,52 @@ __global__ __launch_bounds__(256) void msg_reduce_kernel(MsgArgs a) {
   a.status[i] = s;
 }
 
+// ---- CRC-trailered records: IndexSegment.checkDataIntegrityInByteBufferWithCRC
+// (ambry-store/.../IndexSegment.java:727-735), the LogSegment header (LogSegment.java:130-140,
+// 603-607), RestUtils user metadata (RestUtils.java:775-776, 813-814): the CRC of bytes
+// [0, len - 8) compared, as a long, with the big-endian long in the last 8 bytes.
+__global__ __launch_bounds__(256) void trailer_parse_kernel(TrailerArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n) return;
+  const uint64_t len = a.len[i];
+  uint64_t jl = 0;
+  uint32_t ex = 0;
+  uint8_t force = 0;
+  if (len < 8) {
+    force = 1;  // the reference's limit(capacity - 8) throws: not intact
+  } else {
+    jl = len - 8;
+    if (jl == 0 || jl > a.inline_max) {  // else the group phase reads it (SweepArgs::exp_fill)
+      const uint64_t stored = be64(a.base + a.off[i] + jl);
+      ex = (uint32_t)stored;
+      force = (stored >> 32) ? 1 : 0;
+    }
+  }
+  a.job_len[i] = jl;
+  a.expected[i] = ex;
+  a.force[i] = force;
+}
+
+__global__ __launch_bounds__(256) void trailer_verify_kernel(TrailerArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n) return;
+  const bool bad = a.force[i] || a.crc[i] != a.expected[i];
+  if (a.mismatch) a.mismatch[i] = bad ? 1 : 0;
+  if (bad && a.count) atomicAdd(a.count, 1u);
+}
+
+hipError_t launch_trailer_parse(const TrailerArgs& a, hipStream_t s) {
+  if (a.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(trailer_parse_kernel, dim3((uint32_t)((a.n + 255) / 256)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_trailer_verify(const TrailerArgs& a, hipStream_t s) {
+  if (a.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(trailer_verify_kernel, dim3((uint32_t)((a.n + 255) / 256)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_msg_parse(const MsgArgs& a, hipStream_t s) {
   if (a.m == 0) return hipSuccess;
   hipLaunchKernelGGL(msg_parse_kernel, dim3((uint32_t)((a.m + 255) / 256)), dim3(256), 0, s, a);

@@ -182,6 +182,36 @@ def verify_messages(region, msg_off, stream=None, want_end: bool = True):
     return status, end
 
 
+def verify_trailed(base, off, length, stream=None):
+    """CRC-trailered items on the GPU: item i = base[off[i]:off[i]+len[i]] ends in the big-endian
+    8-B CRC of the bytes before it. Returns (mismatch uint8[n], count int32[1])."""
+    torch = _torch()
+    n = off.numel()
+    _check_batch(base, off, length, n)
+    mismatch = torch.empty(n, dtype=torch.uint8, device=base.device)
+    count = torch.zeros(1, dtype=torch.int32, device=base.device)
+    check(lib().ambrycrc_verify_trailed_dev(_ptr(base), _ptr(off), _ptr(length), _ptr(mismatch), _ptr(count), n,
+                                            None, 0, ctypes.c_void_p(_stream_handle(stream))),
+          "ambrycrc_verify_trailed_dev")
+    return mismatch, count
+
+
+def verify_trailed_host(buffers, device: int = 0, pinned: bool = False):
+    """The same over host buffers (bytes-likes, e.g. whole files): returns a list of bools, True =
+    the trailer does not match (IndexSegment.checkDataIntegrityInByteBufferWithCRC is False)."""
+    import numpy as np
+
+    arrs = [np.frombuffer(b, dtype=np.uint8) if isinstance(b, (bytes, bytearray, memoryview)) else
+            np.ascontiguousarray(b, dtype=np.uint8) for b in buffers]
+    n = len(arrs)
+    ptrs = (ctypes.c_void_p * n)(*[a.ctypes.data if a.nbytes else None for a in arrs])
+    lens = (ctypes.c_uint64 * n)(*[a.nbytes for a in arrs])
+    mism = (ctypes.c_uint8 * n)()
+    check(lib().ambrycrc_verify_trailed_host(ptrs, lens, mism, n, device, 1 if pinned else 0),
+          "ambrycrc_verify_trailed_host")
+    return [bool(x) for x in mism]
+
+
 def verify_messages_host(region, msg_off, device: int = 0, pinned: bool = False):
     """verify_messages for a region in host memory (bytes, numpy uint8, or a CPU uint8 tensor;
     pinned=True for a hipHostMalloc'd / pin_memory() buffer). Returns (status uint32[m],

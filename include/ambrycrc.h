@@ -147,6 +147,25 @@ int ambrycrc_verify_messages_dev(const uint8_t* d_region, uint64_t region_len, c
                                  uint32_t* d_status, uint64_t* d_msg_end, void* d_ws, size_t ws_bytes,
                                  hipStream_t stream);
 
+/* ------------------------------------- CRC-trailered records (store files, headers) */
+
+/* Item i = [off[i], off[i] + len[i]) ends in the big-endian 8-B CRC (a long, high word zero)
+ * of its first len[i] - 8 bytes. d_mismatch[i] = 1 iff the stored long differs from the
+ * computed CRC, or len[i] < 8 (where the reference throws). *d_mismatch_count (caller zeroes
+ * it) counts them. Either output may be NULL. Batch form of
+ * IndexSegment.checkDataIntegrityInByteBufferWithCRC (ambry-store/.../IndexSegment.java:727-735,
+ * every index segment file at store start-up), the LogSegment header check
+ * (LogSegment.java:130-140) and the user-metadata CRC of RestUtils.java:813-814. */
+size_t ambrycrc_trailed_workspace_bytes(size_t n);
+int ambrycrc_verify_trailed_dev(const uint8_t* d_base, const uint64_t* d_off, const uint64_t* d_len,
+                                uint8_t* d_mismatch, uint32_t* d_mismatch_count, size_t n, void* d_ws,
+                                size_t ws_bytes, hipStream_t stream);
+
+/* The same for n host buffers (whole files read or mapped from disk): mismatch[n] host array.
+ * The bodies go through ambrycrc_batch_host; synchronous. */
+int ambrycrc_verify_trailed_host(const void* const* ptrs, const uint64_t* lens, uint8_t* mismatch, size_t n,
+                                 int device, int pinned);
+
 /* ambrycrc_verify_messages_dev for a region in HOST memory (a log segment read or mapped
  * from disk: BlobStoreRecovery's scan, a GET of stored messages). Messages are staged in
  * offset order through the context's pinned slabs (64 MiB, up to 65,536 messages each; a
