@@ -1127,7 +1127,7 @@ int ambrycrc_verify_trailed_dev(const uint8_t* d_base, const uint64_t* d_off, co
                                 uint8_t* d_mismatch, uint32_t* d_mismatch_count, size_t n, void* d_ws,
                                 size_t ws_bytes, hipStream_t stream) {
   if (n == 0) return AMBRYCRC_OK;
-  if (!d_base || !d_off || !d_len || (n >> 32)) return AMBRYCRC_EINVAL;
+  if (!d_base || !d_off || !d_len || n >= (1ull << 31)) return AMBRYCRC_EINVAL;
   DevCtx* c = ctx_current();
   if (!c) return AMBRYCRC_ENOINIT;
   const size_t need = ambrycrc_trailed_workspace_bytes(n);
