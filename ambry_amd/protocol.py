@@ -87,3 +87,39 @@ def verify_chunks_device(base, off, length, stored_crcs):
     exp = torch.from_numpy(np.asarray(stored_crcs, dtype=np.uint32).view(np.int32)).to(base.device)
     _, mismatch, _ = D.crc32_verify(base, off, length, exp)
     return [not bool(x) for x in mismatch.cpu().tolist()]
+
+
+# ---- hard delete (HardDeleteMessageFormatInputStream, ambry-messageformat/.../
+# HardDeleteMessageFormatInputStream.java:58-124): the user-metadata record is rewritten with
+# `userMetadataSize` zero bytes and the blob record with `blobStreamSize` zero bytes
+# (ZeroBytesInputStream), each with a fresh CRC. The zero runs are never scanned: the CRC of
+# `prefix || 0^n` is ambrycrc_zeros(crc(prefix), n), a GF(2) shift (log2 n multiplies).
+
+
+def _crc_long(v: int) -> bytes:
+    return struct.pack(">q", v & 0xFFFFFFFF)
+
+
+def hard_delete_records(usermeta_size: int, blob_size: int, blob_version: int = 3, blob_type: int = 0,
+                        zero_fill: bool = True) -> tuple[bytes, bytes]:
+    """(user-metadata record, blob record) as the hard-delete stream writes them.
+
+    UserMetadata_Format_V1 (MessageFormatRecord.java:1603-1635): version(2) size(4) zeros crc(8).
+    Blob_Format_V2/V3 (:1717-1755, :1777-1795): prefix, zeros, crc(8); V3 isCompressed = false.
+    zero_fill=False returns the records without their zero bodies: (prefix || crc) pairs, for
+    callers that write the zeros themselves (a 4 MiB blob needs no 4 MiB buffer to get its CRC)."""
+    from .crc32 import zeros
+
+    um_prefix = struct.pack(">hi", 1, usermeta_size)
+    um_crc = zeros(crc32(um_prefix), usermeta_size)
+    if blob_version == 2:
+        bl_prefix = struct.pack(">hhq", 2, blob_type, blob_size)
+    elif blob_version == 3:
+        bl_prefix = struct.pack(">hhbq", 3, blob_type, 0, blob_size)
+    else:
+        raise ValueError(f"blob record version {blob_version}: the hard-delete stream writes V2 or V3 here")
+    bl_crc = zeros(crc32(bl_prefix), blob_size)
+    if not zero_fill:
+        return um_prefix + _crc_long(um_crc), bl_prefix + _crc_long(bl_crc)
+    return (um_prefix + bytes(usermeta_size) + _crc_long(um_crc),
+            bl_prefix + bytes(blob_size) + _crc_long(bl_crc))

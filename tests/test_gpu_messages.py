@@ -164,3 +164,28 @@ def test_verify_messages_host_oversize_message(gpu):
     assert st.tolist() == [s for s, _ in expect]
     assert end.tolist() == [e for _, e in expect]
     assert st[2] == MF.BLOB_CRC and st[1] == 0
+
+
+def test_hard_deleted_messages_verify_clean(gpu):
+    """Messages hard-deleted in place (HardDeleteMessageFormatInputStream.java:58-124: zeroed user
+    metadata and blob, CRCs from ambrycrc_zeros) verify clean on the device, group phase engaged."""
+    from ambry_amd.protocol import hard_delete_records
+
+    region, offs = bytearray(), []
+    rng = np.random.default_rng(13)
+    for i in range(4000):
+        size = int(rng.integers(0, 20000))
+        um_len = int(rng.integers(0, 1200))
+        msg = bytearray(MF.put_message(MF.store_key(f"hd{i}"), MF.blob_properties_bytes(size), bytes([7]) * um_len,
+                                       bytes([i & 255]) * size))
+        if i % 2:
+            v, total, rel = MF.parse_header(bytes(msg), 0)
+            um, bl = hard_delete_records(um_len, size)
+            msg[rel[3]:rel[3] + len(um)] = um
+            msg[rel[4]:rel[4] + len(bl)] = bl
+        offs.append(len(region))
+        region += msg
+    region = bytes(region)
+    st, end = run(gpu, region, offs)
+    assert st == [0] * len(offs)
+    assert end == [MF.verify_message(region, o)[1] for o in offs]

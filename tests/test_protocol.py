@@ -104,3 +104,34 @@ def test_verify_chunks_device(gpu):
     ln = torch.full((n,), size, dtype=torch.int64, device="cuda")
     ok = verify_chunks_device(base, off, ln, stored)
     assert [i for i, m in enumerate(ok) if not m] == [3, 17, 40]
+
+
+def test_hard_delete_records_match_oracle(ambry):
+    """HardDeleteMessageFormatInputStream.java:58-124: records rewritten with zero bytes and fresh
+    CRCs; ambrycrc_zeros gives the same CRCs as scanning the zeros (oracle layouts + zlib), and a
+    hard-deleted PUT message still verifies clean (oracle), as BlobStoreRecovery would see it."""
+    import importlib.util
+    import os
+
+    from ambry_amd.protocol import hard_delete_records
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("mf", os.path.join(root, "oracle", "message_format.py"))
+    mf = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mf)
+    for um_size, blob_size in ((0, 0), (1, 1), (1000, 65536), (7, 4 << 20), (4096, 1 << 20)):
+        for ver in (2, 3):
+            um, bl = hard_delete_records(um_size, blob_size, blob_version=ver)
+            assert um == mf.usermeta_record(bytes(um_size))
+            assert bl == mf.blob_record(bytes(blob_size), version=ver)
+            um2, bl2 = hard_delete_records(um_size, blob_size, blob_version=ver, zero_fill=False)
+            assert um2[-8:] == um[-8:] and bl2[-8:] == bl[-8:]
+    # a PUT message hard-deleted in place: same layout, zeroed user metadata and blob
+    key = mf.store_key("hd")
+    content = bytes(range(256)) * 300
+    msg = bytearray(mf.put_message(key, mf.blob_properties_bytes(len(content)), b"meta" * 50, content))
+    v, total, rel = mf.parse_header(bytes(msg), 0)
+    um, bl = hard_delete_records(200, len(content))
+    msg[rel[3]:rel[3] + len(um)] = um
+    msg[rel[4]:rel[4] + len(bl)] = bl
+    assert mf.verify_message(bytes(msg), 0) == (0, len(msg))
