@@ -435,3 +435,40 @@ def test_hip_graph_capture_and_replay(gpu, oracle):
         g.replay()
         torch.cuda.synchronize()
         assert np.array_equal(host_u32(out), oracle.batch(new, offs, lens)), seed
+
+
+def test_host_path_concurrent_threads(gpu, oracle):
+    """Host entry points called from several host threads at once (the reference calls Crc32
+    from the ChunkFiller, network and crypto threads): batch_host, verify_trailed_host and the
+    host streaming loop interleave and each thread gets its own exact results."""
+    import threading
+    import zlib
+
+    mem = stream_bytes(77, 0, 96 << 20)
+    errors = []
+
+    def worker(t):
+        try:
+            rng = np.random.default_rng(t)
+            for _ in range(3):
+                n = int(rng.integers(1, 40))
+                offs = rng.integers(0, (96 << 20) - (9 << 20), size=n)
+                lens = rng.integers(0, 3 << 20, size=n)
+                chunks = [(mem.ctypes.data + int(o), int(ln)) for o, ln in zip(offs, lens)]
+                got = gpu.crc32_batch_host(chunks)
+                exp = oracle.batch(mem, offs, lens)
+                if list(exp) != got:
+                    errors.append(("batch_host", t))
+                item = mem[int(offs[0]):int(offs[0]) + 100000].tobytes()
+                bad = gpu.verify_trailed_host([item + zlib.crc32(item).to_bytes(8, "big"), item[:7]])
+                if bad != [False, True]:
+                    errors.append(("trailed", t))
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append((repr(e), t))
+
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(6)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join()
+    assert not errors, errors
