@@ -5,6 +5,7 @@ import re
 import zlib
 
 import numpy as np
+import pytest
 from datagen import stream_bytes
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -164,6 +165,7 @@ def test_host_update_every_cpu_impl():
     code = r"""
 import sys, zlib
 import numpy as np
+import pytest
 sys.path.insert(0, sys.argv[1])
 import ambry_amd
 rng = np.random.default_rng(7)
@@ -184,3 +186,25 @@ print(ambry_amd.lib().ambrycrc_host_impl().decode())
     assert seen[0] == "slice8"
     # a CPU without the feature keeps the best it has; this image's Xeon has both
     assert seen[1] in ("slice8", "pclmul") and seen[2] in ("slice8", "pclmul", "vpclmul")
+
+
+def test_host_crc_loops_under_asan(tmp_path):
+    """The CLMUL and slice-by-8 host loops under AddressSanitizer/UBSan (host code only), each
+    implementation forced in turn: no out-of-bounds read at any length or alignment, and
+    bit-exact with zlib."""
+    import shutil
+    import subprocess
+
+    if not shutil.which("g++"):
+        pytest.skip("g++ not available")
+    exe = tmp_path / "host_crc_asan"
+    src = os.path.join(ROOT, "tests", "native", "host_crc_asan.cpp")
+    lib = os.path.join(ROOT, "ambry_amd", "csrc", "host_crc.cpp")
+    subprocess.run(["g++", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+                    "-fno-omit-frame-pointer", "-std=c++17", "-I" + os.path.join(ROOT, "ambry_amd", "csrc"),
+                    src, lib, "-lz", "-o", str(exe)], check=True, timeout=300)
+    for impl in ("slice8", "pclmul", "vpclmul"):
+        r = subprocess.run([str(exe)], env=dict(os.environ, AMBRYCRC_HOST_IMPL=impl), capture_output=True,
+                           text=True, timeout=300)
+        assert r.returncode == 0, r.stdout + r.stderr
+        assert "bad=0" in r.stdout
