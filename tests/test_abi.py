@@ -208,3 +208,35 @@ def test_host_crc_loops_under_asan(tmp_path):
                            text=True, timeout=300)
         assert r.returncode == 0, r.stdout + r.stderr
         assert "bad=0" in r.stdout
+
+
+def test_chain_messages_host_under_asan(tmp_path):
+    """ambrycrc_chain_messages_host parses untrusted log bytes: built with the library's host code
+    under AddressSanitizer/UBSan (-Xarch_host, device code untouched) and run from every start
+    offset and on every tail truncation of a region of mixed, partly corrupted messages."""
+    import shutil
+    import subprocess
+
+    from test_message_format import build_region
+
+    hipcc = "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc) or not shutil.which("g++"):
+        pytest.skip("hipcc/g++ not available")
+    region, _, _ = build_region(n=40, seed=5, corrupt_frac=0.2, big_every=10**9)
+    rf = tmp_path / "region.bin"
+    rf.write_bytes(region)
+    exe = tmp_path / "chain_asan"
+    csrc = os.path.join(ROOT, "ambry_amd", "csrc")
+    host_o = tmp_path / "host_crc.o"
+    subprocess.run(["g++", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=all", "-fPIC",
+                    "-std=c++17", "-c", os.path.join(csrc, "host_crc.cpp"), "-o", str(host_o)],
+                   check=True, timeout=300)
+    subprocess.run([hipcc, "-O1", "-g", "-std=c++17", "--offload-arch=gfx950",
+                    "-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
+                    "-Xarch_host", "-fno-sanitize-recover=all", str(host_o),
+                    os.path.join(ROOT, "tests", "native", "chain_asan.cpp"), os.path.join(csrc, "ambrycrc.cpp"),
+                    os.path.join(csrc, "crc32_kernels.hip"), os.path.join(csrc, "message_kernels.hip"),
+                    "-o", str(exe)], check=True, timeout=900)
+    r = subprocess.run([str(exe), str(rf)], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "runs=" in r.stdout
