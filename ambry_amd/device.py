@@ -55,15 +55,18 @@ def crc32_batch(base, off, length, crc_in=None, out=None, workspace=None, stream
     return out
 
 
-def crc32_verify(base, off, length, expected, crc_in=None, out=None, stream=None):
-    """Returns (crc int32[n], mismatch uint8[n], mismatch_count int32[1]) computed on the GPU."""
+def crc32_verify(base, off, length, expected, crc_in=None, out=None, stream=None, mismatch=None,
+                 count=True):
+    """Returns (crc int32[n], mismatch uint8[n], mismatch_count int32[1] or None) computed on the GPU.
+    mismatch: optional preallocated uint8[n]; count=False skips the counter (and its zeroing)."""
     torch = _torch()
     n = off.numel()
     _check_batch(base, off, length, n)
     if out is None:
         out = torch.empty(n, dtype=torch.int32, device=base.device)
-    mismatch = torch.empty(n, dtype=torch.uint8, device=base.device)
-    count = torch.zeros(1, dtype=torch.int32, device=base.device)
+    if mismatch is None:
+        mismatch = torch.empty(n, dtype=torch.uint8, device=base.device)
+    count = torch.zeros(1, dtype=torch.int32, device=base.device) if count else None
     check(lib().ambrycrc_verify_dev(_ptr(base), _ptr(off), _ptr(length), _ptr(crc_in), _ptr(expected), _ptr(out),
                                     _ptr(mismatch), _ptr(count), n, None, 0,
                                     ctypes.c_void_p(_stream_handle(stream))), "ambrycrc_verify_dev")
