@@ -63,6 +63,28 @@ __global__ void stride_kernel(const uint8_t* __restrict__ base, uint64_t nbytes,
   if (x == 0x12345678u) out[0] = x;
 }
 
+// Contiguous per-wave shares in 4 KiB super-blocks, lane l reading its own 64-B run
+// [64l, 64l + 64) of each super-block as 4 x 16 B (no cross-lane transpose needed to walk it);
+// U loads in flight per lane (U/4 super-blocks).
+template <int U, bool NT>
+__global__ void lanerun_kernel(const uint8_t* __restrict__ base, uint64_t nbytes, uint32_t* __restrict__ out) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * gridDim.x + blockIdx.x);
+  const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+  const uint64_t nsb = nbytes / 4096 / nwaves;
+  const u32x4* q = reinterpret_cast<const u32x4*>(base + (uint64_t)wave * nsb * 4096) + 4 * lane;
+  uint32_t x = 0;
+  constexpr int S = U / 4;
+  for (uint64_t b = 0; b + S <= nsb; b += S) {
+    u32x4 w[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) w[u] = ld<NT>(q + (b + u / 4) * 256 + (u & 3));
+#pragma unroll
+    for (int u = 0; u < U; ++u) x ^= w[u].x ^ w[u].y ^ w[u].z ^ w[u].w;
+  }
+  if (x == 0x12345678u) out[0] = x;
+}
+
 typedef void (*kfn)(const uint8_t*, uint64_t, uint32_t*);
 
 static double run(kfn f, int grid, int block, const uint8_t* d, uint64_t n, uint32_t* o) {
@@ -107,6 +129,9 @@ int main(int argc, char** argv) {
       {"share U8 NT 8w", share_kernel<8, true>, 1, 512},     {"share U16 NT 16w", share_kernel<16, true>, 1, 1024},
       {"stride U8 NT 16w", stride_kernel<8, true>, 1, 1024}, {"stride U8 T 16w", stride_kernel<8, false>, 1, 1024},
       {"stride U8 NT 32w", stride_kernel<8, true>, 2, 1024}, {"stride U16 NT 8w", stride_kernel<16, true>, 1, 512},
+      {"lanerun U4 NT 16w", lanerun_kernel<4, true>, 1, 1024}, {"lanerun U8 NT 16w", lanerun_kernel<8, true>, 1, 1024},
+      {"lanerun U16 NT 8w", lanerun_kernel<16, true>, 1, 512},
+      {"share U4 NT 16w (again)", share_kernel<4, true>, 1, 1024}, {"share U8 NT 16w (again)", share_kernel<8, true>, 1, 1024},
   };
   for (const Cfg& c : cfgs) {
     const double gbs = run(c.f, cus * c.wgs_per_cu, c.block, d, n, o);
