@@ -30,6 +30,8 @@ _SIGNATURES = [
     ("ambrycrc_update", ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]),
     ("ambrycrc_update_byte", ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_int]),
     ("ambrycrc_host_impl", ctypes.c_char_p, []),
+    ("ambrycrc_update_iov", ctypes.c_uint32,
+     [ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t), ctypes.c_size_t]),
     ("ambrycrc_combine", ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]),
     ("ambrycrc_zeros", ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint64]),
     ("ambrycrc_workspace_bytes", ctypes.c_size_t, [ctypes.c_size_t]),

@@ -58,6 +58,23 @@ class Crc32:
             self._value = lib().ambrycrc_update(self._value, ptr, length)
         del keep
 
+    def update_buffers(self, buffers) -> None:
+        """update(ByteBuffer) over every buffer in order (PutOperation.java:2041-2043), one native call."""
+        bufs = list(buffers)
+        n = len(bufs)
+        ptrs = (ctypes.c_void_p * n)()
+        lens = (ctypes.c_size_t * n)()
+        keep = []
+        for i, b in enumerate(bufs):
+            data = b.array_view()
+            ptr, k = _buffer_ptr(data, b.position, b.remaining())
+            keep.append(k)
+            ptrs[i], lens[i] = ptr, b.remaining()
+        self._value = lib().ambrycrc_update_iov(self._value, ptrs, lens, n)
+        for b in bufs:
+            b.position = b.limit  # each buffer is consumed, as update(ByteBuffer) does
+        del keep
+
     def update_buffer(self, buffer: "ByteBufferLike") -> None:
         """update(ByteBuffer) (Crc32.java:100-143): consumes position..limit."""
         if buffer.remaining() == 0:  # Crc32.java:101-103

@@ -471,6 +471,14 @@ uint32_t ambrycrc_update(uint32_t crc, const void* p, size_t n) {
 
 const char* ambrycrc_host_impl(void) { return host_impl_name(host_impl()); }
 
+uint32_t ambrycrc_update_iov(uint32_t crc, const void* const* ptrs, const size_t* lens, size_t n) {
+  if (!ptrs || !lens) return crc;
+  uint32_t reg = ~crc;
+  for (size_t i = 0; i < n; ++i)
+    if (ptrs[i] && lens[i]) reg = host_update_reg(reg, static_cast<const uint8_t*>(ptrs[i]), lens[i]);
+  return ~reg;
+}
+
 uint32_t ambrycrc_update_byte(uint32_t crc, int b) {
   const HostTables& h = host_tables();
   uint32_t c = ~crc;

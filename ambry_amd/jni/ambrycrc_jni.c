@@ -12,6 +12,7 @@
  *   static native int  nativeUpdateArray(int crc, byte[] b, int off, int len);
  *   static native int  nativeUpdateDirect(int crc, java.nio.ByteBuffer buf, int pos, int len);
  *   static native int  nativeUpdateByte(int crc, int b);
+ *   static native int  nativeUpdateDirectAll(int crc, java.nio.ByteBuffer[] bufs);
  *   static native int  nativeCombine(int crc1, int crc2, long len2);
  *   static native int  nativeInit(int device);
  *   static native int  nativeBatchDirect(java.nio.ByteBuffer[] bufs, int[] pos, int[] len,
@@ -141,4 +142,36 @@ JNIEXPORT jint JNICALL JNI_FN(nativeVerifyMessages)(JNIEnv* env, jclass cls, job
   free(st);
   free(en);
   return rc;
+}
+
+/* The loop of PutOperation.PutChunk.verifyCRC (PutOperation.java:2041-2043) over a Netty
+ * CompositeByteBuf's nioBuffers(), all direct: one JNI crossing for the whole gather list
+ * (ambrycrc_update_iov). Each buffer's position..limit is used; the Java side consumes them. */
+JNIEXPORT jint JNICALL JNI_FN(nativeUpdateDirectAll)(JNIEnv* env, jclass cls, jint crc, jobjectArray bufs) {
+  (void)cls;
+  const jsize n = (*env)->GetArrayLength(env, bufs);
+  if (n <= 0) return crc;
+  const void** ptrs = (const void**)malloc(sizeof(void*) * (size_t)n);
+  size_t* lens = (size_t*)malloc(sizeof(size_t) * (size_t)n);
+  if (!ptrs || !lens) {
+    free(ptrs);
+    free(lens);
+    return crc;  /* the Java wrapper checks isDirect() and sizes; allocation failure: unchanged */
+  }
+  jclass bbc = (*env)->FindClass(env, "java/nio/Buffer");
+  jmethodID mpos = bbc ? (*env)->GetMethodID(env, bbc, "position", "()I") : NULL;
+  jmethodID mlim = bbc ? (*env)->GetMethodID(env, bbc, "limit", "()I") : NULL;
+  for (jsize i = 0; i < n; ++i) {
+    jobject b = (*env)->GetObjectArrayElement(env, bufs, i);
+    const uint8_t* base = (const uint8_t*)(*env)->GetDirectBufferAddress(env, b);
+    const jint pos = mpos ? (*env)->CallIntMethod(env, b, mpos) : 0;
+    const jint lim = mlim ? (*env)->CallIntMethod(env, b, mlim) : 0;
+    ptrs[i] = base ? base + pos : NULL;
+    lens[i] = (base && lim > pos) ? (size_t)(lim - pos) : 0;
+    (*env)->DeleteLocalRef(env, b);
+  }
+  const jint out = (jint)ambrycrc_update_iov((uint32_t)crc, ptrs, lens, (size_t)n);
+  free(ptrs);
+  free(lens);
+  return out;
 }

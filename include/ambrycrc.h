@@ -70,6 +70,12 @@ const char* ambrycrc_version(void);
  * CrcInputStream.read/updateCrc (ambry-utils/.../utils/CrcInputStream.java:46-71). */
 uint32_t ambrycrc_update(uint32_t crc, const void* p, size_t n);
 
+/* Continue over a gather list of n buffers in order (one call for a Netty CompositeByteBuf's
+ * nioBuffers()): the loop of PutOperation.PutChunk.verifyCRC (ambry-router/.../
+ * PutOperation.java:2041-2043), `for (ByteBuffer b : buf.nioBuffers()) crc.update(b)`.
+ * Equals n successive ambrycrc_update calls; a NULL pointer with length 0 is allowed. */
+uint32_t ambrycrc_update_iov(uint32_t crc, const void* const* ptrs, const size_t* lens, size_t n);
+
 /* One byte: Crc32.update(int b) (Crc32.java:146-148). */
 uint32_t ambrycrc_update_byte(uint32_t crc, int b);
 

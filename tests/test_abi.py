@@ -240,3 +240,24 @@ def test_chain_messages_host_under_asan(tmp_path):
     r = subprocess.run([str(exe), str(rf)], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "runs=" in r.stdout
+
+
+def test_update_iov_gather_list(ambry):
+    """ambrycrc_update_iov == successive updates (PutChunk.verifyCRC over a CompositeByteBuf's
+    nioBuffers, PutOperation.java:2041-2043), empty and NULL entries included; the Crc32 mirror's
+    update_buffers consumes every buffer."""
+    from ambry_amd.crc32 import ByteBufferLike, Crc32
+
+    data = stream_bytes(21, 0, 300000).tobytes()
+    cuts = [0, 0, 1, 17, 4096, 4096, 100000, 299999, 300000]
+    slices = [ByteBufferLike(data[a:b]) for a, b in zip(cuts, cuts[1:])]
+    c = Crc32()
+    c.update(b"prefix", 0, 6)
+    c.update_buffers(slices)
+    assert c.getValue() == zlib.crc32(data, zlib.crc32(b"prefix"))
+    assert all(s.position == s.limit for s in slices)
+    import ctypes
+    lib = ambry.lib()
+    ptrs = (ctypes.c_void_p * 3)(None, None, None)
+    lens = (ctypes.c_size_t * 3)(0, 0, 0)
+    assert lib.ambrycrc_update_iov(0x1234, ptrs, lens, 3) == 0x1234
