@@ -472,3 +472,35 @@ def test_host_path_concurrent_threads(gpu, oracle):
     for th in threads:
         th.join()
     assert not errors, errors
+
+
+def test_randomized_batches(gpu, oracle):
+    """40 random batches against the oracle: chunk counts from 1 to 40,000 (either side of the
+    16,384-chunk group threshold), lengths from 0 to 2 MiB drawn per batch from different size
+    mixes, any offset, random crc_in, random grid sizes and sweep windows (rounds)."""
+    rng = np.random.default_rng(2026)
+    mem = stream_bytes(99, 0, 48 << 20)
+    for it in range(40):
+        n = int(rng.choice([1, 2, 7, 64, 500, 3000, 16383, 16384, 20000, 40000]))
+        mix = it % 4
+        if mix == 0:
+            ln = rng.integers(0, 300, size=n)
+        elif mix == 1:
+            ln = rng.integers(0, 20000, size=n)
+        elif mix == 2:
+            ln = (rng.pareto(1.2, size=n) * 2000).astype(np.int64).clip(0, 2 << 20)
+        else:
+            ln = rng.integers(0, 2 << 20, size=n) if n <= 64 else rng.integers(0, 5000, size=n)
+        off = rng.integers(0, (48 << 20) - int(ln.max()) - 1, size=n)
+        cin = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32) if it % 3 == 0 else None
+        grid = int(rng.choice([0, 0, 1, 5, 77]))
+        window = int(rng.choice([32 << 30, 1 << 20, 4 << 20]))
+        gpu.set_grid(0, grid)
+        gpu.set_window(0, window)
+        try:
+            got = run_batch(gpu, mem, off, ln, crc_in=cin)
+        finally:
+            gpu.set_grid(0, 0)
+            gpu.set_window(0, 32 << 30)
+        exp = oracle.batch(mem, off, ln, crc_in=cin, threads=8)
+        assert np.array_equal(got, exp), (it, n, mix, grid, window)
