@@ -397,19 +397,19 @@ int resolve(DevCtx** out_ctx, void** ws, size_t ws_bytes, size_t n) {
 
 int setup_slabs(DevCtx* c) {
   if (c->slabs_ready) return AMBRYCRC_OK;
+  // member by member, skipping what an earlier (failed) attempt already allocated
+  auto hhost = [](auto** p, size_t bytes) {
+    return *p || hipHostMalloc(reinterpret_cast<void**>(p), bytes, hipHostMallocDefault) == hipSuccess;
+  };
+  auto hdev = [](auto** p, size_t bytes) { return *p || hipMalloc(reinterpret_cast<void**>(p), bytes) == hipSuccess; };
   for (auto& s : c->slab) {
-    if (hipHostMalloc(reinterpret_cast<void**>(&s.h_data), kSlabBytes, hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc(reinterpret_cast<void**>(&s.h_meta), 2 * kSlabChunks * sizeof(uint64_t),
-                      hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc(reinterpret_cast<void**>(&s.h_out), kSlabChunks * sizeof(uint32_t), hipHostMallocDefault) !=
-            hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&s.d_data), kSlabBytes) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&s.d_meta), 2 * kSlabChunks * sizeof(uint64_t)) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&s.d_out), kSlabChunks * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(&s.d_ws, ws_need(kSlabChunks)) != hipSuccess)
+    if (!hhost(&s.h_data, kSlabBytes) || !hhost(&s.h_meta, 2 * kSlabChunks * sizeof(uint64_t)) ||
+        !hhost(&s.h_out, kSlabChunks * sizeof(uint32_t)) || !hdev(&s.d_data, kSlabBytes) ||
+        !hdev(&s.d_meta, 2 * kSlabChunks * sizeof(uint64_t)) || !hdev(&s.d_out, kSlabChunks * sizeof(uint32_t)) ||
+        !(s.d_ws || hipMalloc(&s.d_ws, ws_need(kSlabChunks)) == hipSuccess))
       return AMBRYCRC_ENOMEM;
-    if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess) return AMBRYCRC_EHIP;
-    if (hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess) return AMBRYCRC_EHIP;
+    if (!s.stream && hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess) return AMBRYCRC_EHIP;
+    if (!s.done && hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess) return AMBRYCRC_EHIP;
   }
   c->slabs_ready = true;
   return AMBRYCRC_OK;
@@ -429,18 +429,25 @@ void free_ctx(DevCtx* c) {
     (void)hipEventDestroy(e.a);
     (void)hipEventDestroy(e.b);
   }
-  if (c->slabs_ready) {
-    for (auto& s : c->slab) {
-      (void)hipHostFree(s.h_data);
-      (void)hipHostFree(s.h_meta);
-      (void)hipHostFree(s.h_out);
-      (void)hipFree(s.d_data);
-      (void)hipFree(s.d_meta);
-      (void)hipFree(s.d_out);
-      (void)hipFree(s.d_ws);
-      (void)hipStreamDestroy(s.stream);
-      (void)hipEventDestroy(s.done);
-    }
+  for (auto& ms : c->msg_slab) {  // allocated member by member on first use; free what exists
+    if (ms.h_off) (void)hipHostFree(ms.h_off);
+    if (ms.h_status) (void)hipHostFree(ms.h_status);
+    if (ms.h_end) (void)hipHostFree(ms.h_end);
+    if (ms.d_off) (void)hipFree(ms.d_off);
+    if (ms.d_status) (void)hipFree(ms.d_status);
+    if (ms.d_end) (void)hipFree(ms.d_end);
+    if (ms.d_ws) (void)hipFree(ms.d_ws);
+  }
+  for (auto& s : c->slab) {  // whatever setup_slabs got to, even if it failed part way
+    if (s.h_data) (void)hipHostFree(s.h_data);
+    if (s.h_meta) (void)hipHostFree(s.h_meta);
+    if (s.h_out) (void)hipHostFree(s.h_out);
+    if (s.d_data) (void)hipFree(s.d_data);
+    if (s.d_meta) (void)hipFree(s.d_meta);
+    if (s.d_out) (void)hipFree(s.d_out);
+    if (s.d_ws) (void)hipFree(s.d_ws);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+    if (s.done) (void)hipEventDestroy(s.done);
   }
   delete c;
 }
@@ -975,16 +982,17 @@ int ambrycrc_verify_messages_host(const uint8_t* region, uint64_t region_len, co
   if (!c->msg_slabs_ready) {
     for (int w = 0; w < kSlabs; ++w) {
       MsgSlab& ms = c->msg_slab[w];
-      if (hipHostMalloc(reinterpret_cast<void**>(&ms.h_off), kSlabMsgs * sizeof(uint64_t), hipHostMallocDefault) !=
-              hipSuccess ||
-          hipHostMalloc(reinterpret_cast<void**>(&ms.h_status), kSlabMsgs * sizeof(uint32_t),
-                        hipHostMallocDefault) != hipSuccess ||
-          hipHostMalloc(reinterpret_cast<void**>(&ms.h_end), kSlabMsgs * sizeof(uint64_t), hipHostMallocDefault) !=
-              hipSuccess ||
-          hipMalloc(reinterpret_cast<void**>(&ms.d_off), kSlabMsgs * sizeof(uint64_t)) != hipSuccess ||
-          hipMalloc(reinterpret_cast<void**>(&ms.d_status), kSlabMsgs * sizeof(uint32_t)) != hipSuccess ||
-          hipMalloc(reinterpret_cast<void**>(&ms.d_end), kSlabMsgs * sizeof(uint64_t)) != hipSuccess ||
-          hipMalloc(&ms.d_ws, ambrycrc_messages_workspace_bytes(kSlabMsgs)) != hipSuccess) {
+      // member by member, skipping what an earlier (failed) attempt already allocated
+      auto hhost = [](auto** p, size_t bytes) {
+        return *p || hipHostMalloc(reinterpret_cast<void**>(p), bytes, hipHostMallocDefault) == hipSuccess;
+      };
+      auto hdev = [](auto** p, size_t bytes) {
+        return *p || hipMalloc(reinterpret_cast<void**>(p), bytes) == hipSuccess;
+      };
+      if (!hhost(&ms.h_off, kSlabMsgs * sizeof(uint64_t)) || !hhost(&ms.h_status, kSlabMsgs * sizeof(uint32_t)) ||
+          !hhost(&ms.h_end, kSlabMsgs * sizeof(uint64_t)) || !hdev(&ms.d_off, kSlabMsgs * sizeof(uint64_t)) ||
+          !hdev(&ms.d_status, kSlabMsgs * sizeof(uint32_t)) || !hdev(&ms.d_end, kSlabMsgs * sizeof(uint64_t)) ||
+          !(ms.d_ws || hipMalloc(&ms.d_ws, ambrycrc_messages_workspace_bytes(kSlabMsgs)) == hipSuccess)) {
         (void)hipSetDevice(prev);
         return AMBRYCRC_ENOMEM;
       }

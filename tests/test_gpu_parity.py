@@ -4,6 +4,8 @@ Bit-exact comparisons only (integer path). Full-size configs (C2, C3) are checke
 through size-independent properties: per-chunk samples against the oracle, the
 whole region as one chunk vs the combine-fold of the per-chunk CRCs, determinism.
 """
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -504,3 +506,18 @@ def test_randomized_batches(gpu, oracle):
             gpu.set_window(0, 32 << 30)
         exp = oracle.batch(mem, off, ln, crc_in=cin, threads=8)
         assert np.array_equal(got, exp), (it, n, mix, grid, window)
+
+
+def test_shutdown_and_reinit(gpu, oracle):
+    """ambrycrc_shutdown releases every context (tables, workspace, staging and message slabs,
+    events); a new ambrycrc_init works as before."""
+    from ambry_amd import lib
+
+    mem = stream_bytes(31, 0, 4 << 20)
+    chunks = [(mem.ctypes.data + 5, 3 << 20), (mem.ctypes.data, 1000)]
+    before = gpu.crc32_batch_host(chunks)
+    assert lib().ambrycrc_shutdown() == 0
+    assert lib().ambrycrc_batch_host((ctypes.c_void_p * 1)(mem.ctypes.data), (ctypes.c_uint64 * 1)(10), None,
+                                     (ctypes.c_uint32 * 1)(), 1, 0, 0) == -4  # ENOINIT
+    gpu.init(0)
+    assert gpu.crc32_batch_host(chunks) == before == list(oracle.batch(mem, [5, 0], [3 << 20, 1000]))
