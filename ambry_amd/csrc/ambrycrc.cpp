@@ -138,7 +138,8 @@ struct DevCtx {
   HostSlab slab[kSlabs];
   bool msg_slabs_ready = false;
   MsgSlab msg_slab[kSlabs];
-  std::mutex mu;  // guards ws growth, events, slabs
+  std::mutex mu;     // guards ws growth and the slabs (held across a whole host-path call)
+  std::mutex ev_mu;  // guards the timing events (taken inside enqueue_batch, which host-path calls reach with mu held)
 };
 
 std::mutex g_mu;
@@ -358,7 +359,7 @@ int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uin
   t.window = c->window;
   EventPair ev{nullptr, nullptr};
   if (c->timing) {
-    std::lock_guard<std::mutex> g(c->mu);
+    std::lock_guard<std::mutex> g(c->ev_mu);
     if (!c->free_events.empty()) {
       ev = c->free_events.back();
       c->free_events.pop_back();
@@ -373,7 +374,7 @@ int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uin
   if (e != hipSuccess) return AMBRYCRC_EHIP;
   if (c->timing) {
     if (hipEventRecord(ev.b, s) != hipSuccess) return AMBRYCRC_EHIP;
-    std::lock_guard<std::mutex> g(c->mu);
+    std::lock_guard<std::mutex> g(c->ev_mu);
     c->pending.push_back(ev);
   }
   return AMBRYCRC_OK;
@@ -820,7 +821,7 @@ int ambrycrc_timing_collect_each(int device, float* ms_out, int cap, int* launch
   DevCtx* c = ctx_for(device);
   if (!c) return AMBRYCRC_ENOINIT;
   if (cap < 0 || (cap > 0 && !ms_out)) return AMBRYCRC_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
+  std::lock_guard<std::mutex> g(c->ev_mu);
   int cnt = 0;
   for (auto& e : c->pending) {
     if (hipEventSynchronize(e.b) != hipSuccess) return AMBRYCRC_EHIP;
@@ -840,7 +841,7 @@ int ambrycrc_timing_collect(int device, double* total_ms, int* launches) {
   if (!c) return AMBRYCRC_ENOINIT;
   std::vector<float> ms;
   {
-    std::lock_guard<std::mutex> g(c->mu);
+    std::lock_guard<std::mutex> g(c->ev_mu);
     ms.resize(c->pending.size() + 4096);  // room for launches recorded meanwhile
   }
   int cnt = 0;

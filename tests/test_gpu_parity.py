@@ -521,3 +521,22 @@ def test_shutdown_and_reinit(gpu, oracle):
                                      (ctypes.c_uint32 * 1)(), 1, 0, 0) == -4  # ENOINIT
     gpu.init(0)
     assert gpu.crc32_batch_host(chunks) == before == list(oracle.batch(mem, [5, 0], [3 << 20, 1000]))
+
+
+def test_timing_with_host_paths(gpu, oracle):
+    """Kernel timing stays usable while host-path calls run (they hold the context lock across the
+    call; the timing events have their own): batch_host and the device batch both record."""
+    torch = _torch()
+    mem = stream_bytes(41, 0, 8 << 20)
+    gpu.timing_collect(0)
+    gpu.timing_enable(0, True)
+    try:
+        got = gpu.crc32_batch_host([(mem.ctypes.data, 8 << 20)])
+        base = dev_bytes(mem)
+        out = gpu.crc32_batch(base, dev_u64([0]), dev_u64([8 << 20]))
+        torch.cuda.synchronize()
+    finally:
+        gpu.timing_enable(0, False)
+    each = gpu.timing_collect_each(0)
+    assert len(each) >= 2 and all(x > 0 for x in each)
+    assert got[0] == int(host_u32(out)[0]) == oracle.crc32(mem)
