@@ -12,6 +12,9 @@ Crc32Benchmark.java:43-44 times one buffer per call at sizes 100 B ... 4 MiB
               (the java.util.zip.CRC32 stand-in), one thread, µs per call and GB/s, over
               10 buffers x enough iterations for ~0.3 s
 One JSON line per size. --no-gpu runs the CPU columns only.
+
+The oracle appears here only as the CPU baseline being timed (and as the checker of the GPU
+results), the role bench.py's cpu_baseline leg gives it; nothing GPU-side calls it.
 """
 from __future__ import annotations
 

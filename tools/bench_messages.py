@@ -7,6 +7,10 @@ properties / user-metadata records (V3 header, 1000 B user metadata, as C1), blo
 contents are random device bytes, and each blob record's CRC is computed by the engine
 and stored big-endian, exactly as PutMessageFormatInputStream would have written it.
 Prints one JSON line per measurement.
+
+The oracle (oracle/message_format.py, oracle/crc32_ref.c) appears here only as the fixture
+builder, the checker and the C1 CPU baseline being timed -- the roles tests/ and bench.py's
+cpu_baseline leg give it; the GPU verify it measures is libambrycrc alone.
 """
 from __future__ import annotations
 
