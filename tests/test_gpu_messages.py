@@ -189,3 +189,22 @@ def test_hard_deleted_messages_verify_clean(gpu):
     st, end = run(gpu, region, offs)
     assert st == [0] * len(offs)
     assert end == [MF.verify_message(region, o)[1] for o in offs]
+
+
+def test_verify_messages_host_many_small_messages(gpu):
+    """70,000 update messages (~90 B each): more messages than one staging slab takes
+    (65,536), so the host path cuts slabs by count as well as by bytes."""
+    one = MF.update_message(MF.store_key("u"), version=3, kind="delete")
+    bad = bytearray(one)
+    bad[len(bad) - 12] ^= 0x40  # inside the update record
+    msgs = [bytes(bad) if i % 997 == 0 else one for i in range(70000)]
+    offs, pos = [], 0
+    for m in msgs:
+        offs.append(pos)
+        pos += len(m)
+    region = b"".join(msgs)
+    st, end = gpu.verify_messages_host(region, offs)
+    exp_one, exp_bad = MF.verify_message(one, 0)[0], MF.verify_message(bytes(bad), 0)[0]
+    assert exp_one == 0 and exp_bad != 0
+    assert st.tolist() == [exp_bad if i % 997 == 0 else 0 for i in range(70000)]
+    assert end.tolist() == [o + len(one) for o in offs]
