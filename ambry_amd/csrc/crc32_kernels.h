@@ -66,7 +66,7 @@ constexpr uint64_t group_small_max(int mode) {
 
 // sweep-kernel variants (U = loads in flight per lane, NT = nontemporal, PIPE = rolling prefetch,
 // IL = two pieces interleaved, WIN = descriptors fetched 64 per wave-load, else one-ahead scalar
-// prefetch): 0 U8/NT/PIPE/IL/WIN (default), 1 = 0 without WIN, 2 U8/NT/PIPE/WIN, 3 U4/NT/PIPE/WIN,
+// prefetch): 0 U8/NT/PIPE/IL/WIN (the round-1 base shape), 1 = 0 without WIN, 2 U8/NT/PIPE/WIN, 3 U4/NT/PIPE/WIN,
 // 4 U8/PIPE/IL/WIN (temporal loads), 5 U8/NT batch loads, 6 U4/NT/PIPE/IL/WIN, 7 U8 batch (temporal)
 // 8 R=2 strided lane runs (U8 loads in flight), 9 R=4 strided runs (U8), 10 R=4 strided (U4),
 // 11 R=2 strided (U4), 12 64-B runs by quad transpose of coalesced loads (U8), 13 same (U4)
@@ -89,6 +89,9 @@ constexpr uint64_t group_small_max(int mode) {
 // 28 = 27 with 64-B lane runs in the 8-lane groups of class 1 (257 B - 1 KiB) too
 // (two super-blocks, 8 loads per lane, in flight in the sweep body: -6 % on C3, -4 % on C2
 // at the 128-VGPR cap)
+// 29 (default) = 28 with s_setprio 3 while a wave issues its super-block loads (+0.2-0.5 %)
+// (measured and not kept, DESIGN.md §4: 12 waves per CU, 8-lane groups for 1-16 KiB, temporal
+// or prioritised group-phase loads, 128-B cut snapping, group caps of 8, 20 and 64 KiB)
 constexpr int kNumVariants = 30;
 constexpr int kDiagNoFold = 100;  // diagnostic timing build, selectable via ambrycrc_set_variant only
 
