@@ -241,7 +241,11 @@ def verify_messages_host(region, msg_off, device: int = 0, pinned: bool = False)
 
 def chain_messages_host(region: bytes, start: int = 0, max_messages: int = 1 << 20):
     """Offsets of consecutive messages from `start` in a host buffer (BlobStoreRecovery's hop)."""
-    buf = (ctypes.c_char * len(region)).from_buffer_copy(region)
-    offs = (ctypes.c_uint64 * max_messages)()
-    n = lib().ambrycrc_chain_messages_host(ctypes.cast(buf, ctypes.c_void_p), len(region), start, offs, max_messages)
-    return list(offs[:n])
+    import numpy as np
+
+    arr = np.frombuffer(region, dtype=np.uint8) if isinstance(region, (bytes, bytearray, memoryview)) else \
+        np.ascontiguousarray(region, dtype=np.uint8)  # no copy for bytes, mmaps and uint8 arrays
+    offs = np.zeros(max_messages, dtype=np.uint64)
+    n = lib().ambrycrc_chain_messages_host(ctypes.c_void_p(arr.ctypes.data if arr.nbytes else 0), arr.nbytes, start,
+                                           offs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), max_messages)
+    return [int(x) for x in offs[:n]]

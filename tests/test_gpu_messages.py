@@ -208,3 +208,37 @@ def test_verify_messages_host_many_small_messages(gpu):
     assert exp_one == 0 and exp_bad != 0
     assert st.tolist() == [exp_bad if i % 997 == 0 else 0 for i in range(70000)]
     assert end.tolist() == [o + len(one) for o in offs]
+
+
+def test_verify_log_tool(gpu, tmp_path):
+    """tools/verify_log.py over a log segment file (LogSegment header + messages): the chain, the
+    per-message status and the header check agree with the oracle; a corrupt header stops the
+    chain where BlobStoreRecovery would stop."""
+    import importlib.util
+    import os
+
+    from ambry_amd import store_files
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("verify_log", os.path.join(root, "tools", "verify_log.py"))
+    vl = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(vl)
+    region, offs, expect = build_region(n=300, seed=4, corrupt_frac=0.0, big_every=50)
+    region = bytearray(region)
+    for i in (7, 99, 200):  # record corruption: still chained, flagged
+        v, total, rel = MF.parse_header(bytes(region[offs[i]:offs[i] + 64]), 0)
+        region[offs[i] + rel[-1] + 3] ^= 0x08
+    hdr = store_files.log_segment_header(1 << 30)
+    path = tmp_path / "0_0_log"
+    path.write_bytes(hdr + bytes(region))
+    r = vl.verify_log(str(path))
+    assert r["log_header_intact"] and r["messages"] == 300
+    exp = [MF.verify_message(bytes(region), o)[0] for o in offs]
+    assert r["corrupt"] == sum(1 for s in exp if s) == 3
+    assert [x["offset"] for x in r["first_corrupt"]] == [len(hdr) + offs[i] for i in (7, 99, 200)]
+    assert r["unscanned_tail_bytes"] == 0
+    # a corrupt message header ends the chain there (BlobStoreRecovery stops at the first bad header)
+    region[offs[150] + 5] ^= 0x01
+    path.write_bytes(hdr + bytes(region))
+    r = vl.verify_log(str(path))
+    assert r["messages"] == 150 and r["chain_end"] == len(hdr) + offs[150]
