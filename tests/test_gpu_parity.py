@@ -298,6 +298,32 @@ def test_c3_full_size_rounds(gpu, oracle):
     del buf
 
 
+@pytest.mark.parametrize("window", [0, 1 << 30])
+def test_chunks_past_4gib(gpu, oracle, window):
+    """64-bit offsets and lengths: one 5 GiB + 3 B chunk starting at an odd offset (its length
+    and its end both past 2^32), a short chunk starting past 4 GiB, and a 4 GiB + 1 B chunk with
+    crc_in, in one batch, swept in one round or in 1 GiB rounds. The ABI takes uint64 lengths
+    (ambrycrc.h); Ambry's own chunks stop at 4 MiB, so this is the boundary's limit, not a
+    config. Every CRC is checked against the oracle over the same bytes copied to the host."""
+    torch = _torch()
+    total = (5 << 30) + 64
+    buf = torch.empty(total, dtype=torch.uint8, device="cuda")
+    gpu.fill_random(buf, 0x5C, 0)
+    off = [7, (4 << 30) + 13, 1]
+    ln = [(5 << 30) + 3, 4093, (4 << 30) + 1]
+    cin = np.array([0, 0x1234ABCD, 0xDEADBEEF], dtype=np.uint32)
+    cin_t = torch.from_numpy(cin.view(np.int32)).cuda()
+    gpu.set_window(0, window)
+    try:
+        got = host_u32(gpu.crc32_batch(buf, dev_u64(off), dev_u64(ln), crc_in=cin_t))
+    finally:
+        gpu.set_window(0, 32 << 30)
+    host = buf.cpu().numpy()
+    del buf
+    want = [oracle.crc32(host[o:o + n], int(c)) for o, n, c in zip(off, ln, cin)]
+    assert [int(x) for x in got] == want
+
+
 def test_c2_full_size(gpu, oracle):
     """C2: 65,536 x 64 KiB."""
     _full_size_check(gpu, oracle, 65536, 64 << 10, 0xC2, sample=64)
