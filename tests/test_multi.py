@@ -77,7 +77,7 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 4])
 def test_gloo_distributed_batch_and_blob(world, ambry):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
