@@ -114,31 +114,39 @@ struct DevCtx {
   int device = -1;
   int num_cu = 0;
   int grid = 0;
-  // 27: 64-B lane runs (four coalesced 1 KiB loads per 4 KiB super-block, quad transpose by
-  // v_cndmask_b32_dpp, one x^(8*4096) fold per 64 B), U4 loads in flight; plus, for batches
-  // of >= kGroupMinChunks chunks, whole chunks <= 16 KiB in the fused group phase, each size
-  // class spread over all waves with a class-sized group (G = 4 / 8 / 16 lanes), and 64-B
-  // lane runs inside the 8- and 16-lane groups (classes 1-3, 257 B - 16 KiB).
-  // Measured (tools/sweep.py, bench_ladder.py, bench_messages.py; profiles/r01d_*): the
-  // DPP-fused transpose beat 23 by 1.2-1.9 % on C3; the class-sized group phase took 100 B
-  // chunks from 0.51 to 1.6 TB/s, 1 KiB from 3.8 to 5.0 TB/s and the 4 KiB-blob message
-  // verify from 1.96 to 3.1 TiB/s; the group runs took 4 KiB chunks from 5.5 to 5.9 TB/s
-  // and 16 KiB from 5.9 to 6.5, and in the 8-lane groups 512 B - 1 KiB chunks by 3-4 %.
-  // 29 = 28 with s_setprio 3 while a wave issues its super-block loads: +0.2-0.5 % on C2,
-  // C3, C4 in interleaved sweeps (r01f).
-  int variant = 29;
+  // kVariantDefault (29): 64-B lane runs (four coalesced 1 KiB loads per 4 KiB super-block,
+  // quad transpose by v_cndmask_b32_dpp, one x^(8*4096) fold per 64 B), s_setprio 3 around
+  // the loads; plus, for batches of >= kGroupMinChunks chunks, whole chunks <= 16 KiB in the
+  // fused group phase, each size class spread over all waves with a class-sized group
+  // (G = 4 / 8 / 16 lanes). Measured against the round-1 alternatives in DESIGN.md §4-5.
+  int variant = kVariantDefault;
   // Sweep rounds of at most this many bytes (SweepArgs::window); 0 = one round.
   uint64_t window = 32ull << 30;
   uint32_t* d_img = nullptr;
-  void* d_ws = nullptr;
-  size_t ws_bytes = 0;
+  // Default workspaces (d_ws == NULL calls), one per stream: calls on one stream are ordered by
+  // it, so they may share a buffer; calls on different streams get different buffers. ws_mu is
+  // held from choosing the buffer until the call's work is enqueued, so a concurrent call that
+  // grows the same stream's buffer retires the old one only behind that work (an event on the
+  // stream; freed once it has completed, or at shutdown).
+  struct StreamWs {
+    hipStream_t stream;
+    void* ptr;
+    size_t bytes;
+  };
+  struct RetiredWs {
+    void* ptr;
+    hipEvent_t done;
+  };
+  std::mutex ws_mu;
+  std::vector<StreamWs> ws_list;
+  std::vector<RetiredWs> ws_retired;
   bool timing = false;
   std::vector<EventPair> pending, free_events;
   bool slabs_ready = false;
   HostSlab slab[kSlabs];
   bool msg_slabs_ready = false;
   MsgSlab msg_slab[kSlabs];
-  std::mutex mu;     // guards ws growth and the slabs (held across a whole host-path call)
+  std::mutex mu;     // guards the slabs (held across a whole host-path call)
   std::mutex ev_mu;  // guards the timing events (taken inside enqueue_batch, which host-path calls reach with mu held)
 };
 
@@ -286,39 +294,89 @@ DevCtx* ctx_current() {
 }
 
 // workspace: byte_start[n+1] | block_sum[B] | block_small[B] | small_total[5] (uint64:
-//            total, start of size classes 1..3 in small_idx, dynamic share counter) |
-//            small_idx[n] (uint32), B = ceil(n / kPlanPerBlock)
+//            total, start of size classes 1..3 in small_idx, spare) |
+//            small_idx[n] (uint32) | crc_stage[n] (uint32: crc_in as read by the plan),
+//            B = ceil(n / kPlanPerBlock)
 size_t ws_need(size_t n) {
   const size_t blocks = (n + kPlanPerBlock - 1) / kPlanPerBlock;
-  return ((n + 6 + 2 * blocks) * sizeof(uint64_t) + n * sizeof(uint32_t) + 255) & ~size_t(255);
+  return ((n + 6 + 2 * blocks) * sizeof(uint64_t) + 2 * n * sizeof(uint32_t) + 255) & ~size_t(255);
 }
 
-int ensure_ws(DevCtx* c, size_t need) {
-  if (c->ws_bytes >= need) return AMBRYCRC_OK;
-  const size_t sz = std::max(need, c->ws_bytes * 2);
-  if (c->d_ws) {
-    (void)hipDeviceSynchronize();  // the old workspace may still be in use by queued work
-    (void)hipFree(c->d_ws);
+// Frees retired default workspaces whose last user has completed. Caller holds c->ws_mu.
+void reap_retired_ws(DevCtx* c) {
+  auto& r = c->ws_retired;
+  for (size_t i = 0; i < r.size();) {
+    if (hipEventQuery(r[i].done) == hipSuccess) {
+      (void)hipFree(r[i].ptr);
+      (void)hipEventDestroy(r[i].done);
+      r[i] = r.back();
+      r.pop_back();
+    } else {
+      ++i;
+    }
   }
-  c->d_ws = nullptr;
-  c->ws_bytes = 0;
-  if (hipMalloc(&c->d_ws, sz) != hipSuccess) return AMBRYCRC_ENOMEM;
-  c->ws_bytes = sz;
+}
+
+// The default workspace of `stream` with at least `need` bytes. Caller holds c->ws_mu until the
+// work that uses it is enqueued on `stream`. A buffer that is too small is retired behind an
+// event on the stream (work already queued there may still read it), never freed in place.
+// (A destroyed stream's handle may be reused by a new stream; hipStreamDestroy drains the old
+// stream's work first, so the buffer is idle by then.)
+int stream_ws(DevCtx* c, hipStream_t s, size_t need, void** out) {
+  reap_retired_ws(c);
+  DevCtx::StreamWs* w = nullptr;
+  for (auto& e : c->ws_list)
+    if (e.stream == s) w = &e;
+  if (!w) {
+    c->ws_list.push_back({s, nullptr, 0});
+    w = &c->ws_list.back();
+  }
+  if (w->bytes >= need) {
+    *out = w->ptr;
+    return AMBRYCRC_OK;
+  }
+  if (w->ptr) {
+    hipEvent_t ev = nullptr;
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return AMBRYCRC_EHIP;
+    if (hipEventRecord(ev, s) != hipSuccess) {
+      (void)hipEventDestroy(ev);
+      return AMBRYCRC_EHIP;
+    }
+    c->ws_retired.push_back({w->ptr, ev});
+    w->ptr = nullptr;
+  }
+  const size_t sz = std::max(need, w->bytes * 2);
+  w->bytes = 0;
+  if (hipMalloc(&w->ptr, sz) != hipSuccess) {
+    w->ptr = nullptr;
+    return AMBRYCRC_ENOMEM;
+  }
+  w->bytes = sz;
+  *out = w->ptr;
   return AMBRYCRC_OK;
 }
 
+// Holds c->ws_mu for the lifetime of a *_dev call that uses the default workspace (d_ws ==
+// NULL); a call with its own workspace takes no lock.
+struct WsLease {
+  std::unique_lock<std::mutex> lk;
+  // On return *ws is the caller's buffer (checked against need) or the stream's default one.
+  int acquire(DevCtx* c, hipStream_t s, void** ws, size_t ws_bytes, size_t need) {
+    if (*ws) return ws_bytes < need ? AMBRYCRC_EINVAL : AMBRYCRC_OK;
+    lk = std::unique_lock<std::mutex>(c->ws_mu);
+    return stream_ws(c, s, need, ws);
+  }
+};
+
 // Largest chunk the group phase takes whole for a batch of n chunks on c's variant (0: none).
 uint64_t batch_small_max(const DevCtx* c, size_t n) {
-  if (n < kGroupMinChunks) return 0;
-  const bool grouped = c->variant >= 14 && c->variant < 20;
-  const int group_mode = grouped ? c->variant - 13 : 0;
-  return c->variant == 20   ? group_small_max(4)
-         : c->variant == 21 ? group_small_max(2)
-         : c->variant >= 22 ? group_small_max(5)
-                            : group_small_max(group_mode);
+  if (n < kGroupMinChunks || !variant_groups(c->variant)) return 0;
+  return kGroupSmallMax;
 }
 
-// exp_fill: SweepArgs::exp_fill (message verify; honoured by variants 26-29 only).
+// exp_fill: SweepArgs::exp_fill (message verify; honoured by the group phase of variant 29).
+// crc_in may equal out (an in-place continuation): the plan copies crc_in into the workspace
+// before it initialises out, and the CRC kernels read the copy.
 int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len, const uint32_t* crc_in,
                   uint32_t* out, size_t n, void* ws, hipStream_t s, uint32_t* exp_fill = nullptr) {
   if (n == 0) return AMBRYCRC_OK;
@@ -333,12 +391,8 @@ int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uin
   p.block_small = p.block_sum + blocks;
   p.small_total = p.block_small + blocks;
   p.small_idx = reinterpret_cast<uint32_t*>(p.small_total + 5);
+  p.crc_stage = crc_in ? p.small_idx + n : nullptr;
   p.out = out;
-  // variants >= 14: variant 0's sweep plus the group kernel for small whole chunks
-  // 20, 21: the group phase fused into the sweep launch (sweep variant = the variant itself)
-  const bool grouped = c->variant >= 14 && c->variant < 20;
-  const int sweep_variant = grouped ? 0 : c->variant;
-  const int group_mode = grouped ? c->variant - 13 : 0;
   p.small_max = batch_small_max(c, n);
   hipError_t e = launch_plan(p, s);
   if (e != hipSuccess) return AMBRYCRC_EHIP;
@@ -346,14 +400,13 @@ int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uin
   t.base = base;
   t.off = off;
   t.len = len;
-  t.crc_in = crc_in;
+  t.crc_in = p.crc_stage;
   t.n = (uint32_t)n;
   t.byte_start = p.byte_start;
   t.img = c->d_img;
   t.out = out;
   t.small_max = p.small_max;
   t.small_total = p.small_total;
-  t.claim = p.small_total + 4;
   t.small_idx = p.small_idx;
   t.exp_fill = exp_fill;
   t.window = c->window;
@@ -368,9 +421,7 @@ int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uin
     }
     if (hipEventRecord(ev.a, s) != hipSuccess) return AMBRYCRC_EHIP;
   }
-  e = launch_group(t, c->grid, group_mode, s);
-  if (e != hipSuccess) return AMBRYCRC_EHIP;
-  e = launch_sweep(t, c->grid, sweep_variant, s);
+  e = launch_sweep(t, c->grid, c->variant, s);
   if (e != hipSuccess) return AMBRYCRC_EHIP;
   if (c->timing) {
     if (hipEventRecord(ev.b, s) != hipSuccess) return AMBRYCRC_EHIP;
@@ -380,20 +431,12 @@ int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uin
   return AMBRYCRC_OK;
 }
 
-int resolve(DevCtx** out_ctx, void** ws, size_t ws_bytes, size_t n) {
-  DevCtx* c = ctx_current();
-  if (!c) return AMBRYCRC_ENOINIT;
-  const size_t need = ws_need(n);
-  if (*ws) {
-    if (ws_bytes < need) return AMBRYCRC_EINVAL;
-  } else {
-    std::lock_guard<std::mutex> g(c->mu);
-    int rc = ensure_ws(c, need);
-    if (rc) return rc;
-    *ws = c->d_ws;
-  }
-  *out_ctx = c;
-  return AMBRYCRC_OK;
+// Device pointers a and b of n uint32 each either coincide or do not overlap (in-place
+// continuation d_out == d_crc_in is supported; a shifted overlap is not).
+bool same_or_disjoint(const uint32_t* a, const uint32_t* b, size_t n) {
+  if (!a || !b || a == b) return true;
+  const uintptr_t x = reinterpret_cast<uintptr_t>(a), y = reinterpret_cast<uintptr_t>(b);
+  return x + 4 * n <= y || y + 4 * n <= x;
 }
 
 int setup_slabs(DevCtx* c) {
@@ -421,7 +464,12 @@ void free_ctx(DevCtx* c) {
   (void)hipSetDevice(c->device);
   (void)hipDeviceSynchronize();
   if (c->d_img) (void)hipFree(c->d_img);
-  if (c->d_ws) (void)hipFree(c->d_ws);
+  for (auto& w : c->ws_list)
+    if (w.ptr) (void)hipFree(w.ptr);
+  for (auto& r : c->ws_retired) {
+    (void)hipFree(r.ptr);
+    (void)hipEventDestroy(r.done);
+  }
   for (auto& e : c->pending) {
     (void)hipEventDestroy(e.a);
     (void)hipEventDestroy(e.b);
@@ -522,7 +570,13 @@ int ambrycrc_init(int device) {
   c->device = device;
   c->num_cu = prop.multiProcessorCount;
   c->grid = c->num_cu;
-  if (const char* v = getenv("AMBRYCRC_VARIANT")) c->variant = atoi(v);
+  // AMBRYCRC_VARIANT selects a built-in shape for A/B runs; anything else is ignored (a
+  // stray value must never change the checksums).
+  if (const char* v = getenv("AMBRYCRC_VARIANT")) {
+    char* end = nullptr;
+    const long x = strtol(v, &end, 10);
+    if (end != v && *end == '\0' && x >= 0 && x < 1000 && variant_supported((int)x)) c->variant = (int)x;
+  }
   std::vector<uint32_t> img = build_table_image();
   if (hipMalloc(reinterpret_cast<void**>(&c->d_img), img.size() * 4) != hipSuccess) {
     delete c;
@@ -531,10 +585,6 @@ int ambrycrc_init(int device) {
   if (hipMemcpy(c->d_img, img.data(), img.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
     free_ctx(c);
     return AMBRYCRC_EHIP;
-  }
-  if (ensure_ws(c, ws_need(1u << 16)) != AMBRYCRC_OK) {
-    free_ctx(c);
-    return AMBRYCRC_ENOMEM;
   }
   g_ctx[device] = c;
   (void)hipSetDevice(prev);
@@ -559,8 +609,11 @@ int ambrycrc_batch_dev(const uint8_t* d_base, const uint64_t* d_off, const uint6
                        uint32_t* d_out, size_t n, void* d_ws, size_t ws_bytes, hipStream_t stream) {
   if (n == 0) return AMBRYCRC_OK;
   if (!d_base || !d_off || !d_len || !d_out || n >= (1ull << 31)) return AMBRYCRC_EINVAL;
-  DevCtx* c = nullptr;
-  int rc = resolve(&c, &d_ws, ws_bytes, n);
+  if (!same_or_disjoint(d_crc_in, d_out, n)) return AMBRYCRC_EINVAL;
+  DevCtx* c = ctx_current();
+  if (!c) return AMBRYCRC_ENOINIT;
+  WsLease lease;
+  const int rc = lease.acquire(c, stream, &d_ws, ws_bytes, ws_need(n));
   if (rc) return rc;
   return enqueue_batch(c, d_base, d_off, d_len, d_crc_in, d_out, n, d_ws, stream);
 }
@@ -570,21 +623,15 @@ int ambrycrc_verify_dev(const uint8_t* d_base, const uint64_t* d_off, const uint
                         size_t n, void* d_ws, size_t ws_bytes, hipStream_t stream) {
   if (n == 0) return AMBRYCRC_OK;
   if (!d_base || !d_off || !d_len || !d_expected || n >= (1ull << 31)) return AMBRYCRC_EINVAL;
-  DevCtx* c = nullptr;
-  // Without a caller d_out, the CRCs live in the workspace right after tile_start.
+  if (!same_or_disjoint(d_crc_in, d_out, n)) return AMBRYCRC_EINVAL;
+  DevCtx* c = ctx_current();
+  if (!c) return AMBRYCRC_ENOINIT;
+  // Without a caller d_out, the CRCs live in the workspace after the batch's own part.
   const size_t extra = d_out ? 0 : ((n * sizeof(uint32_t) + 255) & ~size_t(255));
-  if (d_ws && ws_bytes < ws_need(n) + extra) return AMBRYCRC_EINVAL;
-  int rc = resolve(&c, &d_ws, d_ws ? ws_bytes : 0, n);
+  WsLease lease;
+  int rc = lease.acquire(c, stream, &d_ws, ws_bytes, ws_need(n) + extra);
   if (rc) return rc;
-  if (!d_out) {
-    std::lock_guard<std::mutex> g(c->mu);
-    if (d_ws == c->d_ws) {
-      rc = ensure_ws(c, ws_need(n) + extra);
-      if (rc) return rc;
-      d_ws = c->d_ws;
-    }
-    d_out = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(d_ws) + ws_need(n));
-  }
+  if (!d_out) d_out = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(d_ws) + ws_need(n));
   rc = enqueue_batch(c, d_base, d_off, d_len, d_crc_in, d_out, n, d_ws, stream);
   if (rc) return rc;
   return hip_err(launch_verify(d_out, d_expected, d_mismatch, d_mismatch_count, (uint32_t)n, stream));
@@ -778,8 +825,7 @@ int ambrycrc_range_checksums_host(const uint8_t* file, uint64_t file_len, const 
 int ambrycrc_set_variant(int device, int variant) {
   DevCtx* c = ctx_for(device);
   if (!c) return AMBRYCRC_ENOINIT;
-  if ((variant < 0 || variant >= kNumVariants) && (variant < kDiagNoFold || variant > kDiagNoFold + 2))
-    return AMBRYCRC_EINVAL;
+  if (!variant_supported(variant)) return AMBRYCRC_EINVAL;
   c->variant = variant;
   return AMBRYCRC_OK;
 }
@@ -897,9 +943,9 @@ int enqueue_messages(DevCtx* c, const uint8_t* d_region, uint64_t region_len, co
   a.crc = crc;
   a.status = d_status;
   a.msg_end = d_msg_end;
-  // The class-sized group phase (variants 26-29) reads the stored CRCs of the records it
+  // The class-sized group phase (variant 29) reads the stored CRCs of the records it
   // takes whole; the parse kernel reads the rest.
-  const bool inline_exp = c->variant >= 26 && c->variant <= 29;
+  const bool inline_exp = variant_groups(c->variant);
   a.inline_max = inline_exp ? batch_small_max(c, j) : 0;
   void* batch_ws = w + ((j * 2 * sizeof(uint64_t) + j * 2 * sizeof(uint32_t) + j + 255) & ~size_t(255));
   if (launch_msg_parse(a, stream) != hipSuccess) return AMBRYCRC_EHIP;
@@ -956,15 +1002,9 @@ int ambrycrc_verify_messages_dev(const uint8_t* d_region, uint64_t region_len, c
   if (!d_region || !d_msg_off || !d_status || (size_t)kMsgSlots * m >= (1ull << 31)) return AMBRYCRC_EINVAL;
   DevCtx* c = ctx_current();
   if (!c) return AMBRYCRC_ENOINIT;
-  const size_t need = ambrycrc_messages_workspace_bytes(m);
-  if (d_ws) {
-    if (ws_bytes < need) return AMBRYCRC_EINVAL;
-  } else {
-    std::lock_guard<std::mutex> g(c->mu);
-    int rc = ensure_ws(c, need);
-    if (rc) return rc;
-    d_ws = c->d_ws;
-  }
+  WsLease lease;
+  const int rc = lease.acquire(c, stream, &d_ws, ws_bytes, ambrycrc_messages_workspace_bytes(m));
+  if (rc) return rc;
   return enqueue_messages(c, d_region, region_len, d_msg_off, m, d_status, d_msg_end, d_ws, stream);
 }
 
@@ -1147,15 +1187,9 @@ int ambrycrc_verify_trailed_dev(const uint8_t* d_base, const uint64_t* d_off, co
   if (!d_base || !d_off || !d_len || n >= (1ull << 31)) return AMBRYCRC_EINVAL;
   DevCtx* c = ctx_current();
   if (!c) return AMBRYCRC_ENOINIT;
-  const size_t need = ambrycrc_trailed_workspace_bytes(n);
-  if (d_ws) {
-    if (ws_bytes < need) return AMBRYCRC_EINVAL;
-  } else {
-    std::lock_guard<std::mutex> g(c->mu);
-    int rc = ensure_ws(c, need);
-    if (rc) return rc;
-    d_ws = c->d_ws;
-  }
+  WsLease lease;
+  int rc = lease.acquire(c, stream, &d_ws, ws_bytes, ambrycrc_trailed_workspace_bytes(n));
+  if (rc) return rc;
   uint8_t* w = static_cast<uint8_t*>(d_ws);
   TrailerArgs a;
   a.base = d_base;
@@ -1169,11 +1203,11 @@ int ambrycrc_verify_trailed_dev(const uint8_t* d_base, const uint64_t* d_off, co
   a.force = reinterpret_cast<uint8_t*>(crc + n);
   a.mismatch = d_mismatch;
   a.count = d_mismatch_count;
-  const bool inline_exp = c->variant >= 26 && c->variant <= 29;
+  const bool inline_exp = variant_groups(c->variant);
   a.inline_max = inline_exp ? batch_small_max(c, n) : 0;
   void* batch_ws = w + ((n * (sizeof(uint64_t) + 2 * sizeof(uint32_t) + 1) + 255) & ~size_t(255));
   if (launch_trailer_parse(a, stream) != hipSuccess) return AMBRYCRC_EHIP;
-  int rc = enqueue_batch(c, d_base, d_off, a.job_len, nullptr, crc, n, batch_ws, stream,
+  rc = enqueue_batch(c, d_base, d_off, a.job_len, nullptr, crc, n, batch_ws, stream,
                          a.inline_max ? a.expected : nullptr);
   if (rc) return rc;
   return hip_err(launch_trailer_verify(a, stream));

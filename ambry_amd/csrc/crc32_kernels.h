@@ -17,8 +17,10 @@ struct PlanArgs {
   uint64_t small_max;      // chunks with 0 < len <= small_max go to the group kernel (0: none)
   uint64_t* block_small;   // [ceil(n / kPlanPerBlock)] scratch: 4 x 16-bit size-class counts
   uint64_t* small_total;   // [5] number of small chunks; start of size classes 1..3 in small_idx;
-                           // [4] the sweep's dynamic share counter (zeroed here)
+                           // [4] spare
   uint32_t* small_idx;     // [n] their indices, grouped by size class, ascending within a class
+  uint32_t* crc_stage;     // [n] copy of crc_in (null iff crc_in is): read before out[] is written,
+                           // so out may alias crc_in; the CRC kernels read this copy
 };
 
 constexpr uint32_t kPlanPerBlock = 2048;  // chunks per planning workgroup
@@ -36,9 +38,8 @@ struct SweepArgs {
   uint32_t* out;
   uint64_t small_max;      // sweep: skip chunks with len <= small_max; group kernel: take them
   const uint64_t* small_total;  // [4] as PlanArgs
-  uint64_t* claim;              // = PlanArgs small_total + 4 (dynamic shares, variant 27)
   const uint32_t* small_idx;
-  // Message verify (class-sized group phase only, variants 26-29): for every chunk the group
+  // Message verify (class-sized group phase only, variant 29): for every chunk the group
   // phase takes, also read the big-endian 8-B CRC stored right after it (base + off + len)
   // and write exp_fill[chunk] = its low word, or ~crc when the high word is not zero (a
   // forced mismatch: a CRC-32 never has upper bits). Null otherwise.
@@ -49,50 +50,32 @@ struct SweepArgs {
   uint64_t window;
 };
 
-// Group kernel shapes (mode -> G lanes per chunk, NB blocks of 16G bytes): small_max = 16*G*NB.
-// 0 = off, 1 = G16/NB8 (2 KiB), 2 = G16/NB16 (4 KiB), 3 = G32/NB8 (4 KiB), 4 = G16/NB32 (8 KiB),
-// 5 = G16/NB64 (16 KiB), 6 = G32/NB32 (16 KiB)
-constexpr int kNumGroupModes = 7;
-// Batches of fewer chunks than this take the sweep (wave mode) for every chunk: with idle
+// Chunks of 1 B .. kGroupSmallMax go to the group phase (variant 29) in batches of at least
+// kGroupMinChunks chunks; smaller batches take the sweep (wave mode) for every chunk: with idle
 // waves to spare, 64 lanes per chunk beat a 16-lane group's 4x longer chain on latency.
 constexpr size_t kGroupMinChunks = 16384;
-constexpr uint64_t group_small_max(int mode) {
-  return mode == 1 ? 2048u
-         : (mode == 2 || mode == 3) ? 4096u
-         : mode == 4 ? 8192u
-         : (mode == 5 || mode == 6) ? 16384u
-                                    : 0u;
-}
+constexpr uint64_t kGroupSmallMax = 16384;
 
-// sweep-kernel variants (U = loads in flight per lane, NT = nontemporal, PIPE = rolling prefetch,
-// IL = two pieces interleaved, WIN = descriptors fetched 64 per wave-load, else one-ahead scalar
-// prefetch): 0 U8/NT/PIPE/IL/WIN (the round-1 base shape), 1 = 0 without WIN, 2 U8/NT/PIPE/WIN, 3 U4/NT/PIPE/WIN,
-// 4 U8/PIPE/IL/WIN (temporal loads), 5 U8/NT batch loads, 6 U4/NT/PIPE/IL/WIN, 7 U8 batch (temporal)
-// 8 R=2 strided lane runs (U8 loads in flight), 9 R=4 strided runs (U8), 10 R=4 strided (U4),
-// 11 R=2 strided (U4), 12 64-B runs by quad transpose of coalesced loads (U8), 13 same (U4)
-// 14..19 = 0 plus the group kernel (modes 1..6) for small whole chunks; 20, 21, 22 = 0 with the
-// group phase (G16/NB32, G16/NB16, G16/NB64: chunks <= 8, 4, 16 KiB) fused into the sweep launch
-// 23 = 13 (quad-transposed 64-B lane runs, U4) with the G16/NB64 group phase fused in
-// 24 = 12 (quad-transposed 64-B lane runs, U8) with the G16/NB64 group phase fused in
-// (8 waves per CU with 256 VGPRs and U8/U16 prefetch lost 3-14 % to these at 16 waves: the
-// 4 waves per SIMD hide the LDS chains better; the TPB template parameter is kept)
-// 25 = 23 with the quad transposes' lane selects fused into DPP moves (v_cndmask_b32_dpp)
-// 26 = 25 with the group phase sized and balanced per size class (G = 4 for <= 256 B, 8 for
-// <= 1 KiB, 16 above; every class spread over all waves)
-// (prefetching the group rounds' list entries and descriptors two stages ahead measured no
-// gain over 26: the 16 waves per CU already hide that latency)
-// (dynamic shares -- share/8 bytes each, the rest claimed from an atomic counter after a
-// static first one; the DYN template parameter -- lost 0.6 % on C3, 1.3 % on C4 and 12 % on
-// C2: each claim pays a chunk search and a descriptor reload, and the tail it would
-// shorten was not there)
-// 27 = 26 with 64-B lane runs (quad transpose) in the 16-lane groups of classes 2-3
-// 28 = 27 with 64-B lane runs in the 8-lane groups of class 1 (257 B - 1 KiB) too
-// (two super-blocks, 8 loads per lane, in flight in the sweep body: -6 % on C3, -4 % on C2
-// at the 128-VGPR cap)
-// 29 (default) = 28 with s_setprio 3 while a wave issues its super-block loads (+0.2-0.5 %)
-// (measured and not kept, DESIGN.md §4: 12 waves per CU, 8-lane groups for 1-16 KiB, temporal
-// or prioritised group-phase loads, 128-B cut snapping, group caps of 8, 20 and 64 KiB)
-constexpr int kNumVariants = 30;
+// Sweep-kernel variants built into the library (round 1 measured 30 shapes; git history has
+// them, DESIGN.md §4 the results):
+//   0  (kVariantPieces): lane l owns bytes [16l, 16l+16) of every 1 KiB block, 8 blocks in
+//      flight, two pieces interleaved; every chunk in the sweep (no group phase). Fallback.
+//   29 (kVariantDefault): 64-B lane runs from coalesced 4 KiB super-blocks (quad transpose by
+//      v_cndmask_b32_dpp, one x^(8*4096) fold per 64 B), s_setprio 3 around the loads, plus
+//      the class-sized group phase (G = 4 / 8 / 16 lanes for <= 256 B / 1 KiB / 16 KiB) with
+//      the stored CRC read inline for message verify (SweepArgs::exp_fill).
+// 100..102: timing diagnostics that produce wrong CRCs, compiled only with
+// -DAMBRYCRC_DIAGNOSTICS (never in the product library).
+constexpr int kVariantPieces = 0;
+constexpr int kVariantDefault = 29;
+constexpr bool variant_supported(int v) {
+#ifdef AMBRYCRC_DIAGNOSTICS
+  if (v >= 100 && v <= 102) return true;
+#endif
+  return v == kVariantPieces || v == kVariantDefault;
+}
+// variant 29 reads group-phase records' stored CRCs inline
+constexpr bool variant_groups(int v) { return v == kVariantDefault; }
 constexpr int kDiagNoFold = 100;  // diagnostic timing build, selectable via ambrycrc_set_variant only
 
 // Message verify (message_kernels.hip): kMsgSlots CRC jobs per message, slot order
@@ -139,7 +122,6 @@ hipError_t launch_msg_reduce(const MsgArgs& a, hipStream_t s);
 
 hipError_t launch_plan(const PlanArgs& a, hipStream_t s);
 hipError_t launch_sweep(const SweepArgs& a, int grid, int variant, hipStream_t s);
-hipError_t launch_group(const SweepArgs& a, int grid, int mode, hipStream_t s);
 hipError_t launch_verify(const uint32_t* crc, const uint32_t* expected, uint8_t* mismatch, uint32_t* count,
                          uint32_t n, hipStream_t s);
 hipError_t launch_readbw(const uint8_t* base, uint64_t nbytes, uint32_t* out, int grid, int variant,

@@ -6,18 +6,19 @@
 // 1700-1703, 2033-2054) and per blob record (ambry-messageformat/.../
 // MessageFormatRecord.java:1797-1832). Results are bit-exact CRC-32/ISO-HDLC.
 //
-// Work decomposition
+// Work decomposition (default variant 29; variant 0 is the 16-B-piece fallback)
 //   batch  -> the chunks viewed as one concatenated byte stream; wave w of the
 //             persistent grid owns an equal share [w*S, (w+1)*S) of it (exact byte
-//             balance for any chunk-size mix), cut points snapped to 16 B in memory
-//   segment-> a (wave, chunk) intersection; the wave sweeps it in 1 KiB blocks,
-//             lane l owning bytes [16l, 16l+16) of every block (one coalesced
-//             global_load_dwordx4 per block per lane)
-//   lane   -> slice-by-4 over its 16-B piece using LDS byte tables that one
-//             v_perm_b32 addresses; the lane state hops one block with an
-//             x^(8*1024) nibble-table multiply (independent of the piece's own
-//             table walk, so consecutive pieces overlap)
-//   wave   -> 6-level xor-shuffle tree, level l shifting by 16*2^l bytes
+//             balance for any chunk-size mix), cut points snapped to 16 B in memory.
+//             Whole chunks <= 16 KiB (batches of >= 16,384 chunks) go to the group
+//             phase first: G = 4/8/16 lanes per chunk by size class, 64/G chunks per wave
+//   segment-> a (wave, chunk) intersection; the wave sweeps it in 4 KiB super-blocks:
+//             four coalesced 1 KiB global_load_dwordx4 per lane, a quad transpose
+//             leaving each lane a 64-B run
+//   lane   -> slice-by-4 over its run using LDS byte tables that one v_perm_b32
+//             addresses; the lane state hops one super-block with an x^(8*4096)
+//             nibble-table multiply (independent of the run's own table walk)
+//   wave   -> 6-level xor tree (DPP partners), shifts 64 B .. 2 KiB
 //   segment-> shifted by its distance to the chunk end and atomically XORed into
 //             out[chunk] (XOR is exact and order-free => deterministic)
 //
@@ -83,12 +84,6 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t lane) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-__device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src) {
-  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, (int)src);
-  const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), (int)src);
-  return ((uint64_t)hi << 32) | lo;
-}
-
 // Per-lane address constants for slice table j: region bit, (j&1)*128, lane column.
 struct LaneConst {
   uint32_t L0, L1, L2, L3;
@@ -123,10 +118,6 @@ __device__ __forceinline__ uint32_t rpiece(u32x4 w, const LaneConst& k, uint32_t
   return slice4(s, k, xin);
 }
 
-// Two pieces whose first three table steps are independent of the running state,
-// interleaved in source so a wave keeps two LDS dependency chains in flight.
-__device__ __forceinline__ uint32_t rpiece_pair(u32x4 w0, u32x4 w1, const LaneConst& k, uint32_t s);
-
 // v * C mod P where C's nibble tables sit at kNibBase + set_off (conflict-free, 8 lookups).
 __device__ __forceinline__ uint32_t nib_mul(uint32_t v, uint32_t set_off) {
   uint32_t t[8];
@@ -155,6 +146,8 @@ __device__ __forceinline__ uint32_t fold(uint32_t s) {
   }
 }
 
+// Two pieces whose first three table steps are independent of the running state,
+// interleaved in source so a wave keeps two LDS dependency chains in flight.
 template <int DIAG>
 __device__ __forceinline__ uint32_t rpiece_pair_d(u32x4 w0, u32x4 w1, const LaneConst& k, uint32_t s) {
   uint32_t x0 = slice4(w0.x, k, w0.y);
@@ -165,17 +158,6 @@ __device__ __forceinline__ uint32_t rpiece_pair_d(u32x4 w0, u32x4 w1, const Lane
   x1 = slice4(x1, k, w1.w);
   s = slice4(x0, k, fold<DIAG>(s));
   return slice4(x1, k, fold<DIAG>(s));
-}
-
-__device__ __forceinline__ uint32_t rpiece_pair(u32x4 w0, u32x4 w1, const LaneConst& k, uint32_t s) {
-  uint32_t x0 = slice4(w0.x, k, w0.y);
-  uint32_t x1 = slice4(w1.x, k, w1.y);
-  x0 = slice4(x0, k, w0.z);
-  x1 = slice4(x1, k, w1.z);
-  x0 = slice4(x0, k, w0.w);
-  x1 = slice4(x1, k, w1.w);
-  s = slice4(x0, k, nib_mul(s, kFoldOff));
-  return slice4(x1, k, nib_mul(s, kFoldOff));
 }
 
 template <bool NT>
@@ -239,7 +221,7 @@ __device__ __forceinline__ u32x4 load_block0(const uint8_t* __restrict__ base, i
 // Raw CRC of body [bs, be) (be 16-aligned, bs <= be arbitrary), returned in lane 63
 // (other lanes: junk). Bytes below bs are treated as zeros, which leave a zero
 // register unchanged, so the virtual range is aligned down to whole 1 KiB blocks.
-template <int U, bool NT, bool PIPE, bool IL, int DIAG = 0>
+template <int U, bool NT, int DIAG = 0>
 __device__ __forceinline__ uint32_t body_crc(const uint8_t* __restrict__ base, uint64_t bs, uint64_t be,
                                              uint32_t lane, const LaneConst& k) {
   const uint64_t nb = (be - bs + kBlockBytes - 1) / kBlockBytes;
@@ -250,7 +232,7 @@ __device__ __forceinline__ uint32_t body_crc(const uint8_t* __restrict__ base, u
   const u32x4* q = reinterpret_cast<const u32x4*>(base + v0) + lane;
 
   uint32_t s = 0u;  // fold(0) == 0, so block 0 takes the same step as every other block
-  if constexpr (PIPE) {
+  {
     // Prime: blocks 0..min(U,nb)-1 are all issued before the first is used, so a short
     // segment (a 4 KiB record = 4 blocks) costs one memory round trip, not one per block.
     u32x4 buf[U];
@@ -261,7 +243,6 @@ __device__ __forceinline__ uint32_t body_crc(const uint8_t* __restrict__ base, u
     // U blocks ahead, so each lane keeps U x 16 B loads in flight continuously.
     uint64_t b = 0;
     for (; b + 2 * U <= nb; b += U) {
-      if constexpr (IL) {
 #pragma unroll
         for (int u = 0; u < U; u += 2) {
           const u32x4 w0 = buf[u], w1 = buf[u + 1];
@@ -269,14 +250,6 @@ __device__ __forceinline__ uint32_t body_crc(const uint8_t* __restrict__ base, u
           buf[u + 1] = ld16<NT>(q + (b + U + u + 1) * (kBlockBytes / 16));
           s = rpiece_pair_d<DIAG>(w0, w1, k, s);
         }
-      } else {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const u32x4 w = buf[u];
-          buf[u] = ld16<NT>(q + (b + U + u) * (kBlockBytes / 16));
-          s = rpiece(w, k, nib_mul(s, kFoldOff));
-        }
-      }
     }
     // Drain (nb - b < 2U): consume the slots, refilling each with its block U ahead if
     // there is one, then consume the refills. Predicates are wave-uniform.
@@ -291,20 +264,6 @@ __device__ __forceinline__ uint32_t body_crc(const uint8_t* __restrict__ base, u
 #pragma unroll
     for (int u = 0; u < U; ++u)
       if (b + U + u < nb) s = rpiece(buf[u], k, nib_mul(s, kFoldOff));
-  } else {
-    s = rpiece(load_block0<NT>(base, v0, bs, lane), k, 0u);
-    uint64_t b = 1;
-    for (; b + U <= nb; b += U) {
-      u32x4 buf[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) buf[u] = ld16<NT>(q + (b + u) * (kBlockBytes / 16));
-#pragma unroll
-      for (int u = 0; u < U; ++u) s = rpiece(buf[u], k, nib_mul(s, kFoldOff));
-    }
-    for (; b < nb; ++b) {
-      const u32x4 x = ld16<NT>(q + b * (kBlockBytes / 16));
-      s = rpiece(x, k, nib_mul(s, kFoldOff));
-    }
   }
 
   // Lane l's stream ends 16(63-l) bytes before be: xor-tree with shifts 16*2^lvl,
@@ -319,11 +278,8 @@ __device__ __forceinline__ uint32_t body_crc(const uint8_t* __restrict__ base, u
   return s;
 }
 
-// Raw CRC of [bs, be) with R-piece lane runs: lane l owns bytes [16R*l, 16R*(l+1)) of every
-// super-block of 1024*R bytes (R strided dwordx4 loads per lane, 16R B apart across lanes), so
-// its state hops -- one x^(8*1024R) nibble multiply -- once per R pieces instead of once per
-// piece. Fold and tree constants are POW entries: x^(8*1024R) = POW[10+lg R], tree level l
-// shifts by 16R*2^l = POW[4+lg R+l]. UB super-blocks stay in flight (rolling prefetch).
+// Raw CRC of a lane's run of R consecutive 16-B pieces (R slice-by-4 chains of 4 steps, back
+// to back), xor xin into the last step.
 template <int R>
 __device__ __forceinline__ uint32_t run_crc(const u32x4 (&w)[R], const LaneConst& k, uint32_t xin) {
   uint32_t x = w[0].x;
@@ -337,81 +293,6 @@ __device__ __forceinline__ uint32_t run_crc(const u32x4 (&w)[R], const LaneConst
   return x;
 }
 
-template <int LR, int LVL>
-__device__ __forceinline__ uint32_t tree_level_pow(uint32_t s, uint32_t lane) {
-  const uint32_t sh = nib_mul(tree_partner<LVL>(s), kPowOff + kNibSetBytes * (4 + LR + LVL));
-  return (lane & (1u << LVL)) ? (s ^ sh) : s;
-}
-
-template <int UB, bool NT, int LR>
-__device__ __forceinline__ uint32_t body_crc_runs(const uint8_t* __restrict__ base, uint64_t bs, uint64_t be,
-                                                  uint32_t lane, const LaneConst& k) {
-  constexpr int R = 1 << LR;
-  constexpr uint64_t SB = (uint64_t)kBlockBytes * R;
-  constexpr uint32_t kFold = kPowOff + kNibSetBytes * (10 + LR);
-  const uint64_t nb = (be - bs + SB - 1) / SB;
-  if (nb == 0) return 0u;
-  const int64_t v0 = (int64_t)be - (int64_t)(nb * SB);  // may precede the allocation: signed
-  const int64_t lane0 = v0 + 16 * R * (int64_t)lane;
-  // super-block 0 carries the (possibly unaligned) start
-  u32x4 w[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    w[r] = u32x4{0u, 0u, 0u, 0u};
-    const int64_t p = lane0 + 16 * r;
-    if (p + 16 > (int64_t)bs) {  // => p >= floor16(bs) >= 0
-      w[r] = ld16<NT>(reinterpret_cast<const u32x4*>(base + p));
-      if (p < (int64_t)bs) {
-        const uint32_t cut = (uint32_t)(bs - p);
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-          const int lo = (int)cut - 4 * d;
-          const uint32_t m = lo <= 0 ? 0xFFFFFFFFu : (lo >= 4 ? 0u : (0xFFFFFFFFu << (8 * lo)));
-          w[r][d] &= m;
-        }
-      }
-    }
-  }
-  uint32_t s = run_crc<R>(w, k, 0u);
-  const u32x4* q = reinterpret_cast<const u32x4*>(base + lane0);  // super-block b, piece r: q[b*64R + r]
-  uint64_t b = 1;
-  if (nb >= 1 + 2 * (uint64_t)UB) {
-    u32x4 buf[UB][R];
-#pragma unroll
-    for (int u = 0; u < UB; ++u)
-#pragma unroll
-      for (int r = 0; r < R; ++r) buf[u][r] = ld16<NT>(q + (b + u) * (SB / 16) + r);
-    for (; b + 2 * UB <= nb; b += UB) {
-#pragma unroll
-      for (int u = 0; u < UB; ++u) {
-        u32x4 cur[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          cur[r] = buf[u][r];
-          buf[u][r] = ld16<NT>(q + (b + UB + u) * (SB / 16) + r);
-        }
-        s = run_crc<R>(cur, k, nib_mul(s, kFold));
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < UB; ++u) s = run_crc<R>(buf[u], k, nib_mul(s, kFold));
-    b += UB;
-  }
-  for (; b < nb; ++b) {
-    u32x4 cur[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) cur[r] = ld16<NT>(q + b * (SB / 16) + r);
-    s = run_crc<R>(cur, k, nib_mul(s, kFold));
-  }
-  s = tree_level_pow<LR, 0>(s, lane);
-  s = tree_level_pow<LR, 1>(s, lane);
-  s = tree_level_pow<LR, 2>(s, lane);
-  s = tree_level_pow<LR, 3>(s, lane);
-  s = tree_level_pow<LR, 4>(s, lane);
-  s = tree_level_pow<LR, 5>(s, lane);
-  return s;
-}
-
 // ---- 64-B lane runs from coalesced loads (variant 12 and up) ----
 // Per 4 KiB super-block each lane l = 4m+j issues 4 coalesced 1 KiB loads (block i, piece l),
 // then a 4x4 transpose of 16-B elements inside its quad (two DPP quad_perm butterfly stages)
@@ -423,27 +304,7 @@ __device__ __forceinline__ uint32_t dppq(uint32_t v) {  // quad_perm: every lane
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, true);
 }
 
-__device__ __forceinline__ void quad_transpose(u32x4 (&x)[4], uint32_t lane) {
-  // DPP is convergent: every move is issued in all lanes, then v_cndmask picks (no branches).
-  const bool t1 = lane & 1u, t2 = lane & 2u;
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    const uint32_t p0 = dppq<0xB1>(x[0][d]), p1 = dppq<0xB1>(x[1][d]);
-    const uint32_t p2 = dppq<0xB1>(x[2][d]), p3 = dppq<0xB1>(x[3][d]);
-    const uint32_t a0 = t1 ? p1 : x[0][d];
-    const uint32_t a1 = t1 ? x[1][d] : p0;
-    const uint32_t a2 = t1 ? p3 : x[2][d];
-    const uint32_t a3 = t1 ? x[3][d] : p2;
-    const uint32_t q0 = dppq<0x4E>(a0), q1 = dppq<0x4E>(a1);
-    const uint32_t q2 = dppq<0x4E>(a2), q3 = dppq<0x4E>(a3);
-    x[0][d] = t2 ? q2 : a0;
-    x[2][d] = t2 ? a2 : q0;
-    x[1][d] = t2 ? q3 : a1;
-    x[3][d] = t2 ? a3 : q1;
-  }
-}
-
-// The same transpose with the lane selects fused into the DPP moves: v_cndmask_b32_dpp
+// A 4x4 transpose of 16-B elements inside each lane quad, with the lane selects fused into the DPP moves: v_cndmask_b32_dpp
 // computes vcc ? src1 : dpp(src0), so each stage is 4 VALU ops per dword instead of 4 DPP
 // moves + 4 v_cndmask_b32_e64 (the compiler cannot fuse them: its selects take the lane
 // mask from an SGPR pair, the VOP3 form, which has no DPP encoding on gfx9). 8 VALU per
@@ -494,13 +355,7 @@ __device__ __forceinline__ uint32_t tree_level_t4(uint32_t s, uint32_t lane) {
   return (lane & (1u << BIT)) ? (s ^ sh) : s;
 }
 
-template <bool ASMT>
-__device__ __forceinline__ void qt(u32x4 (&x)[4], uint32_t lane) {
-  if constexpr (ASMT) quad_transpose_asm(x);
-  else quad_transpose(x, lane);
-}
-
-template <int UB, bool NT, bool ASMT = false, bool PRIO = false>
+template <int UB, bool NT, bool PRIO = false>
 __device__ __forceinline__ uint32_t body_crc_t4(const uint8_t* __restrict__ base, uint64_t bs, uint64_t be,
                                                 uint32_t lane, const LaneConst& k) {
   constexpr uint64_t SB = 4 * (uint64_t)kBlockBytes;
@@ -526,7 +381,7 @@ __device__ __forceinline__ uint32_t body_crc_t4(const uint8_t* __restrict__ base
       }
     }
   }
-  qt<ASMT>(x, lane);
+  quad_transpose_asm(x);
   uint32_t s = run_crc<4>(x, k, 0u);
   const u32x4* q = reinterpret_cast<const u32x4*>(base + v0) + lane;  // super-block b, block i: q[b*256 + i*64]
   uint64_t b = 1;
@@ -547,13 +402,13 @@ __device__ __forceinline__ uint32_t body_crc_t4(const uint8_t* __restrict__ base
           buf[u][i] = ld16<NT>(q + (b + UB + u) * 256 + i * 64);
         }
         if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
-        qt<ASMT>(cur, lane);
+        quad_transpose_asm(cur);
         s = run_crc<4>(cur, k, nib_mul(s, kFold));
       }
     }
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
-      qt<ASMT>(buf[u], lane);
+      quad_transpose_asm(buf[u]);
       s = run_crc<4>(buf[u], k, nib_mul(s, kFold));
     }
     b += UB;
@@ -562,7 +417,7 @@ __device__ __forceinline__ uint32_t body_crc_t4(const uint8_t* __restrict__ base
     u32x4 cur[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) cur[i] = ld16<NT>(q + b * 256 + i * 64);
-    qt<ASMT>(cur, lane);
+    quad_transpose_asm(cur);
     s = run_crc<4>(cur, k, nib_mul(s, kFold));
   }
   s = tree_level_t4<2, 6>(s, lane);
@@ -599,11 +454,6 @@ __device__ __forceinline__ u32x4 xor_init(u32x4 w, int64_t p, uint64_t cs, uint3
     else if (od < 0 && od > -4) w[d] ^= rinit >> (8 * (uint32_t)(-od));
   }
   return w;
-}
-
-template <int G>
-__device__ __forceinline__ constexpr uint32_t nib_fold_off() {  // x^(8*16G) = POW[log2 16G]
-  return kPowOff + kNibSetBytes * (G == 16 ? 8u : 9u);
 }
 
 // The blocks of a group chunk, block b at p0 + b*BB (BB = 16G), through a ring of P struct
@@ -670,104 +520,10 @@ struct GroupRingT<P, P, NT, BB> {
   }
 };
 
-// Finalized CRC of chunk [cs, cs+len) continued from cin, valid in the first lane of the
-// lane's group. nbw: wave-uniform block count (max over the groups); shorter chunks get
-// leading zero blocks, which leave a zero register unchanged and issue no loads.
-template <int G, int NB, bool NT>
-__device__ __forceinline__ uint32_t group_crc(const uint8_t* __restrict__ base, uint64_t cs, uint64_t len,
-                                              uint32_t cin, uint32_t nbw, uint32_t lane, const LaneConst& k) {
-  constexpr uint32_t BB = 16u * G;
-  const uint32_t gl = lane & (G - 1);
-  const uint32_t rinit = ~cin;
-  const uint64_t ce = cs + len;
-  const uint64_t cb = aligned_end(cs, ce);
-  const bool body = cb > cs;  // => cb is 16-B aligned
-  const int64_t p0 = (int64_t)cb - (int64_t)nbw * BB + 16 * (int64_t)gl;
-  // all NB blocks' loads in flight before the first is used (GroupBlocks: one member per
-  // block, so nothing becomes a promoted vector that predicated writes would copy whole)
-  const GroupCtx g{base, p0, cs, body, nbw, rinit};
-  constexpr int P = NB < 8 ? NB : 8;
-  GroupRingT<0, P, NT, (int)BB> ring;
-  ring.prime(g);
-  uint32_t s = 0;
-#pragma unroll 1
-  for (uint32_t b0 = 0; b0 < nbw; b0 += P) s = ring.step(g, k, b0, s, nib_fold_off<G>());
-  uint32_t r = s;
-  if (nbw) {
-    r = tree_level<0>(r, lane);
-    r = tree_level<1>(r, lane);
-    r = tree_level<2>(r, lane);
-    r = tree_level<3>(r, lane);
-    if constexpr (G == 32) r = tree_level<4>(r, lane);
-  }
-  r = __shfl(r, (int)(lane | (G - 1)));  // the group's body CRC, from its last lane
-  const uint32_t t = (uint32_t)(ce - cb);  // trailing < 16 bytes
-  if (t & 1u) r = nib_mul(r, kPowOff + kNibSetBytes * 0);
-  if (t & 2u) r = nib_mul(r, kPowOff + kNibSetBytes * 1);
-  if (t & 4u) r = nib_mul(r, kPowOff + kNibSetBytes * 2);
-  if (t & 8u) r = nib_mul(r, kPowOff + kNibSetBytes * 3);
-  uint32_t v = 0;
-  if (gl < t) {
-    const uint64_t a = cb + gl;
-    uint32_t byte = base[a];
-    if (a < cs + 4) byte ^= (rinit >> (8 * (uint32_t)(a - cs))) & 0xFFu;
-    const uint32_t kk = t - 1 - gl;
-    const uint32_t j = kk & 3;
-    v = lds_rd(((j >> 1) << 16) | (byte << 8) | ((j & 1) << 7) | ((lane & 31) << 2));
-    if (kk & 4) v = nib_mul(v, kPowOff + kNibSetBytes * 2);  // x^(8*4)
-    if (kk & 8) v = nib_mul(v, kPowOff + kNibSetBytes * 3);  // x^(8*8)
-  }
-  v ^= dpp<0x128, 0xf>(v);  // xor over the 16-lane row: row_ror 8, 4, 2, 1
-  v ^= dpp<0x124, 0xf>(v);
-  v ^= dpp<0x122, 0xf>(v);
-  v ^= dpp<0x121, 0xf>(v);
-  uint32_t crc = r ^ v ^ 0xFFFFFFFFu;
-  if (len < 4) crc ^= rinit >> (8 * (uint32_t)len);
-  return crc;
-}
-
-// Group kernel: every chunk with 0 < len <= a.small_max (= 16*G*NB), whole, from the
-// plan's compacted list small_idx[0..small_total). Wave w takes list entries
-// [w*K, (w+1)*K), K a multiple of 64/G, in rounds of 64/G chunks (one per group). The
-// sweep kernel skips these chunks (the plan gives them no byte share).
-// List entries of wave `wave` (wave-major numbering): [wave*K, (wave+1)*K), K a multiple of
-// 64/G so every round fills all groups.
+// List entries per wave for a class of ns chunks: a multiple of 64/G so every round fills all groups.
 template <int G>
 __device__ __forceinline__ uint64_t group_per(uint64_t ns, uint64_t nwaves) {
   return ((ns + nwaves - 1) / nwaves + 64 / G - 1) / (64 / G) * (64 / G);
-}
-
-template <int G, int NB, bool NT>
-__device__ __forceinline__ void group_phase(const SweepArgs& a, uint64_t ns, uint32_t wave, uint64_t nwaves,
-                                            uint32_t lane, const LaneConst& k) {
-  constexpr uint32_t S = 64 / G;
-  const uint64_t per = group_per<G>(ns, nwaves);
-  const uint64_t i0 = (uint64_t)wave * per;
-  if (i0 >= ns) return;
-  const uint64_t i1 = i0 + per < ns ? i0 + per : ns;
-  const uint32_t gi = lane / G;
-#pragma unroll 1
-  for (uint64_t i = i0; i < i1; i += S) {
-    const bool act = i + gi < i1;
-    const uint32_t ci = act ? a.small_idx[i + gi] : 0u;
-    uint64_t len = 0, off = 0;
-    uint32_t cin = 0;
-    if (act) {
-      len = a.len[ci];
-      off = a.off[ci];
-      cin = a.crc_in ? a.crc_in[ci] : 0u;
-    }
-    const uint64_t cb = aligned_end(off, off + len);
-    const uint32_t nb = (uint32_t)((cb - off + 16 * G - 1) / (16 * G));
-    uint32_t nbw = 0;
-#pragma unroll
-    for (uint32_t q = 0; q < S; ++q) {
-      const uint32_t x = __builtin_amdgcn_readlane(nb, q * G);
-      nbw = x > nbw ? x : nbw;
-    }
-    const uint32_t crc = group_crc<G, NB, NT>(a.base, off, len, cin, nbw, lane, k);
-    if ((lane & (G - 1)) == 0 && act) a.out[ci] = crc;  // whole chunks: plain stores
-  }
 }
 
 // ---- class-sized, class-balanced group phase (variant 26) ----
@@ -1029,29 +785,16 @@ __device__ __forceinline__ bool group_cls_has_work(const SweepArgs& a, uint32_t 
          (c4 > c3 && first_wave * group_per<16>(c4 - c3, nwaves) < c4 - c3);
 }
 
-template <bool NT, bool T4 = false, bool T4C1 = false>
+// Class 0 (<= 256 B) in 4-lane groups of 16-B pieces; classes 1-3 with 64-B lane runs in 8- and
+// 16-lane groups.
+template <bool NT>
 __device__ __forceinline__ void group_phase_cls(const SweepArgs& a, uint32_t wave, uint64_t nwaves, uint32_t lane,
                                                 const LaneConst& k) {
   const uint64_t c1 = a.small_total[1], c2 = a.small_total[2], c3 = a.small_total[3], c4 = a.small_total[0];
   group_class<4, 4, NT>(a, 0, c1, wave, nwaves, lane, k);
-  group_class<8, 8, NT, T4C1>(a, c1, c2, wave, nwaves, lane, k);
-  group_class<16, 16, NT, T4>(a, c2, c3, wave, nwaves, lane, k);
-  group_class<16, 64, NT, T4>(a, c3, c4, wave, nwaves, lane, k);
-}
-
-// Group kernel: every chunk with 0 < len <= a.small_max (= 16*G*NB), whole, from the
-// plan's compacted list small_idx[0..small_total), 64/G chunks per round (one per group).
-// The sweep kernel skips these chunks (the plan gives them no byte share).
-template <int G, int NB, bool NT>
-__global__ __launch_bounds__(1024) void crc32_group_kernel(SweepArgs a) {
-  const uint64_t ns = *a.small_total;
-  if (ns == 0) return;  // uniform: every wave leaves before the LDS fill
-  fill_lds(a.img);
-  const uint32_t lane = threadIdx.x & 63u;
-  // wave-major over workgroups: the first list ranges land on different CUs/XCDs
-  const uint32_t wave = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * gridDim.x + blockIdx.x);
-  const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-  group_phase<G, NB, NT>(a, ns, wave, nwaves, lane, make_lane_const(lane));
+  group_class<8, 8, NT, true>(a, c1, c2, wave, nwaves, lane, k);
+  group_class<16, 16, NT, true>(a, c2, c3, wave, nwaves, lane, k);
+  group_class<16, 64, NT, true>(a, c3, c4, wave, nwaves, lane, k);
 }
 
 // Largest c in [0, n) with byte_start[c] <= g (byte_start nondecreasing, byte_start[0] = 0).
@@ -1085,9 +828,12 @@ __device__ __forceinline__ uint64_t snap_cut(uint64_t cs, uint64_t len, uint64_t
 // as one concatenated stream (byte_start = exclusive scan of len), i.e. an equal share of
 // bytes whatever the chunk-size mix. Each (wave, chunk) intersection is a segment whose
 // raw CRC is shifted to the chunk end and XORed into out[chunk].
-template <int U, bool NT, bool PIPE, bool IL, bool WIN, int DIAG = 0, int LR = 0, int GG = 0, int GNB = 0,
-          int TPB = 1024, int GV = 1, int DYN = 0>
-__global__ __launch_bounds__(TPB) void crc32_sweep_kernel(SweepArgs a) {
+//   T4 = false (variant 0): 16-B pieces per lane, 8 blocks in flight, two pieces interleaved
+//   T4 = true  (variant 29): 64-B lane runs from coalesced 4 KiB super-blocks (quad transpose),
+//                one super-block prefetched, s_setprio 3 around its loads
+//   GROUP: whole chunks <= 16 KiB go to the class-sized group phase first (same launch)
+template <bool T4, bool GROUP, int DIAG = 0>
+__global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
   // Shares are wave-major over workgroups (share i -> wave i / gridDim.x of workgroup
   // i % gridDim.x), so when a batch has fewer shares than waves they spread over every
   // CU. A share is at least kMinShare bytes: a lone large chunk is cut into ~total/16 KiB
@@ -1097,41 +843,27 @@ __global__ __launch_bounds__(TPB) void crc32_sweep_kernel(SweepArgs a) {
   const uint64_t total = a.byte_start[a.n];
   uint64_t share = ((total + nwaves - 1) / nwaves + kShareQuantum - 1) & ~uint64_t(kShareQuantum - 1);
   share = share < kMinShare ? kMinShare : share;
-  // Fused group phase (GG > 0): the workgroup first takes its part of the small-chunk list.
-  const uint64_t ns = GG > 0 ? *a.small_total : 0;
-  const bool grp = GG > 0 && ns > 0 &&
-                   (GV >= 3 ? group_cls_has_work(a, blockIdx.x, nwaves)
-                            : (uint64_t)blockIdx.x * group_per<(GG > 0 ? GG : 16)>(ns, nwaves) < ns);
+  // Fused group phase: the workgroup first takes its part of each class of the small-chunk list.
+  const uint64_t ns = GROUP ? *a.small_total : 0;
+  const bool grp = GROUP && ns > 0 && group_cls_has_work(a, blockIdx.x, nwaves);
   if ((uint64_t)blockIdx.x * share >= total && !grp) return;  // uniform: no work for this workgroup
   fill_lds(a.img);
 
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * gridDim.x + blockIdx.x);
-  if constexpr (GG > 0) {
-    if (grp) {
-      if constexpr (GV >= 3) group_phase_cls<NT, GV >= 4, GV == 5>(a, wave, nwaves, lane, make_lane_const(lane));
-      else group_phase<GG, GNB, NT>(a, ns, wave, nwaves, lane, make_lane_const(lane));
-    }
-  }
-  // DYN > 0: shares of share/DYN bytes (>= kMinShare); wave w starts with share w, then
-  // claims share nwaves + atomicAdd(claim) until none is left, so waves that run fast (or
-  // start early) take more and the launch's tail shortens.
-  uint64_t S = share;
-  if constexpr (DYN > 0) {
-    S = (share / DYN + kShareQuantum - 1) & ~uint64_t(kShareQuantum - 1);
-    S = S < kMinShare ? kMinShare : S;
+  if constexpr (GROUP) {
+    if (grp) group_phase_cls<true>(a, wave, nwaves, lane, make_lane_const(lane));
   }
   // Rounds (SweepArgs::window): equal shares sized so R rounds of nwaves shares cover the
   // batch; wave w takes shares w, w + nwaves, ... A 256 GiB batch read as one round of
   // 16 MiB shares ran at 95.5 % of a 32 GiB batch's read rate (TLB reach of the spread).
+  uint64_t S = share;
   uint64_t round_step = 0;
-  if constexpr (DYN == 0) {
-    if (a.window && total > a.window) {
-      const uint64_t R = (total + a.window - 1) / a.window;
-      S = ((total + R * nwaves - 1) / (R * nwaves) + kShareQuantum - 1) & ~uint64_t(kShareQuantum - 1);
-      S = S < kMinShare ? kMinShare : S;
-      round_step = nwaves * S;
-    }
+  if (a.window && total > a.window) {
+    const uint64_t R = (total + a.window - 1) / a.window;
+    S = ((total + R * nwaves - 1) / (R * nwaves) + kShareQuantum - 1) & ~uint64_t(kShareQuantum - 1);
+    S = S < kMinShare ? kMinShare : S;
+    round_step = nwaves * S;
   }
   uint64_t g0 = (uint64_t)wave * S;
   if (g0 >= total) return;
@@ -1155,12 +887,10 @@ __global__ __launch_bounds__(TPB) void crc32_sweep_kernel(SweepArgs a) {
     const uint64_t be = se == ce ? cb : se;  // 16-B aligned body end
     uint32_t r = 0;
     if (sa < be) {
-      if constexpr (LR < 0) {
-        r = body_crc_t4<(U >> 2) < 1 ? 1 : (U >> 2), NT, LR <= -3, LR == -4>(a.base, sa, be, lane, k);
-      } else if constexpr (LR > 0) {
-        r = body_crc_runs<(U >> LR) < 1 ? 1 : (U >> LR), NT, LR>(a.base, sa, be, lane, k);
+      if constexpr (T4) {
+        r = body_crc_t4<1, true, true>(a.base, sa, be, lane, k);
       } else {
-        r = body_crc<U, NT, PIPE, IL, DIAG>(a.base, sa, be, lane, k);
+        r = body_crc<8, true, DIAG>(a.base, sa, be, lane, k);
       }
       r = __builtin_amdgcn_readlane(r, 63);
       r = shift_bytes(r, ce - be, xpow2);
@@ -1192,8 +922,7 @@ __global__ __launch_bounds__(TPB) void crc32_sweep_kernel(SweepArgs a) {
   };
 
   for (;;) {
-  uint32_t c = __builtin_amdgcn_readfirstlane(find_chunk(a.byte_start, a.n, g0, lane));
-  if constexpr (WIN) {
+    uint32_t c = __builtin_amdgcn_readfirstlane(find_chunk(a.byte_start, a.n, g0, lane));
     // Descriptors fetched 64 at a time (lane j <- chunk c+j), read back with readlane:
     // one load round trip per 64 chunks. byte_start only seeds a scalar running sum, so
     // 5 VGPRs stay live across the body.
@@ -1215,7 +944,7 @@ __global__ __launch_bounds__(TPB) void crc32_sweep_kernel(SweepArgs a) {
           break;
         }
         const uint64_t len = readlane64(w_len, j);
-        const uint64_t span = len > a.small_max ? len : 0;  // small chunks: group kernel
+        const uint64_t span = len > a.small_max ? len : 0;  // small chunks: group phase
         if (span != 0) {  // empty chunks are finished by the plan kernel
           bool whole;
           const uint32_t r = segment(bsc, len, readlane64(w_off, j), __builtin_amdgcn_readlane(w_cin, j), &whole);
@@ -1230,39 +959,10 @@ __global__ __launch_bounds__(TPB) void crc32_sweep_kernel(SweepArgs a) {
       }
       c += cnt;
     }
-  } else {
-    // One-ahead prefetch of the next descriptor into scalar registers while this chunk runs.
-    uint64_t n_bs = a.byte_start[c], n_len = a.len[c], n_off = a.off[c];
-    uint32_t n_cin = a.crc_in ? a.crc_in[c] : 0u;
-    while (c < a.n) {
-      const uint64_t bsc = n_bs, len = n_len, cs = n_off;
-      const uint32_t cin = n_cin;
-      if (bsc >= g1) break;
-      if (c + 1 < a.n) {
-        n_bs = a.byte_start[c + 1];
-        n_len = a.len[c + 1];
-        n_off = a.off[c + 1];
-        n_cin = a.crc_in ? a.crc_in[c + 1] : 0u;
-      }
-      if (len != 0 && len > a.small_max) {  // empty chunks: plan kernel; small ones: group kernel
-        bool whole;
-        emit_partial(c, segment(bsc, len, cs, cin, &whole));
-      }
-      ++c;
-    }
-  }
-  if constexpr (DYN == 0) {
     if (round_step == 0) break;
     g0 += round_step;
     if (g0 >= total) break;
     g1 = g0 + S < total ? g0 + S : total;
-  } else {
-    uint64_t nx = 0;
-    if (lane == 0) nx = atomicAdd(reinterpret_cast<unsigned long long*>(a.claim), 1ull);
-    g0 = (nwaves + readlane64(nx, 0)) * S;
-    if (g0 >= total) break;
-    g1 = g0 + S < total ? g0 + S : total;
-  }
   }
 }
 
@@ -1447,7 +1147,9 @@ __global__ __launch_bounds__(256) void crc32_plan_scan_kernel(PlanArgs a) {
     if (c < a.n) {
       const uint64_t incl = carry + bs + incl_s[r];
       a.byte_start[c] = incl - sl;
-      a.out[c] = ln ? 0u : (a.crc_in ? a.crc_in[c] : 0u);
+      const uint32_t cin = a.crc_in ? a.crc_in[c] : 0u;  // read before out[c] (may alias crc_in[c])
+      if (a.crc_stage) a.crc_stage[c] = cin;
+      a.out[c] = ln ? 0u : cin;
       if (oh) {
         const uint32_t k = small_class(ln);
         a.small_idx[cls_base[k] + cls_carry[k] + field16(bc + incl_c[r], k) - 1] = c;
@@ -1459,7 +1161,7 @@ __global__ __launch_bounds__(256) void crc32_plan_scan_kernel(PlanArgs a) {
     for (uint32_t k = 0; k < 4; ++k) cls_carry[k] += field16(rc, k);
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    a.small_total[4] = 0;  // the sweep's dynamic share counter
+    a.small_total[4] = 0;
     a.small_total[0] = cls_base[3] + cls_total[3];
     a.small_total[1] = cls_base[1];
     a.small_total[2] = cls_base[2];
@@ -1513,59 +1215,17 @@ hipError_t launch_plan(const PlanArgs& a, hipStream_t s) {
 
 hipError_t launch_sweep(const SweepArgs& a, int grid, int variant, hipStream_t s) {
   switch (variant) {
-#define AMBRY_TILES_CASE(V, U, NT, PIPE, IL, WIN) \
-  case V: hipLaunchKernelGGL((crc32_sweep_kernel<U, NT, PIPE, IL, WIN>), dim3(grid), dim3(1024), 0, s, a); break;
-    AMBRY_TILES_CASE(0, 8, true, true, true, true)
-    AMBRY_TILES_CASE(1, 8, true, true, true, false)
-    AMBRY_TILES_CASE(2, 8, true, true, false, true)
-    AMBRY_TILES_CASE(3, 4, true, true, false, true)
-    AMBRY_TILES_CASE(4, 8, false, true, true, true)
-    AMBRY_TILES_CASE(5, 8, true, false, false, true)
-    AMBRY_TILES_CASE(6, 4, true, true, true, true)
-    AMBRY_TILES_CASE(7, 8, false, false, false, true)
-    case 8: hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, false, true, 0, 1>), dim3(grid), dim3(1024), 0, s, a); break;
-    case 9: hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, false, true, 0, 2>), dim3(grid), dim3(1024), 0, s, a); break;
-    case 10: hipLaunchKernelGGL((crc32_sweep_kernel<4, true, true, false, true, 0, 2>), dim3(grid), dim3(1024), 0, s, a); break;
-    case 11: hipLaunchKernelGGL((crc32_sweep_kernel<4, true, true, false, true, 0, 1>), dim3(grid), dim3(1024), 0, s, a); break;
-    case 12: hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, false, true, 0, -2>), dim3(grid), dim3(1024), 0, s, a); break;
-    case 13: hipLaunchKernelGGL((crc32_sweep_kernel<4, true, true, false, true, 0, -2>), dim3(grid), dim3(1024), 0, s, a); break;
-    // 0 with the group phase fused in (small chunks first, same launch and LDS fill)
-    case 20: hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, true, true, 0, 0, 16, 32>), dim3(grid), dim3(1024), 0, s, a); break;
-    case 21: hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, true, true, 0, 0, 16, 16>), dim3(grid), dim3(1024), 0, s, a); break;
-    case 22: hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, true, true, 0, 0, 16, 64>), dim3(grid), dim3(1024), 0, s, a); break;
-    // 13 (64-B lane runs by quad transpose, U4) with the G16/NB64 group phase fused in
-    case 23: hipLaunchKernelGGL((crc32_sweep_kernel<4, true, true, false, true, 0, -2, 16, 64>), dim3(grid), dim3(1024), 0, s, a); break;
-    case 24: hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, false, true, 0, -2, 16, 64>), dim3(grid), dim3(1024), 0, s, a); break;
-    // 23 with the transposes' selects fused into the DPP moves (v_cndmask_b32_dpp)
-    case 25: hipLaunchKernelGGL((crc32_sweep_kernel<4, true, true, false, true, 0, -3, 16, 64>), dim3(grid), dim3(1024), 0, s, a); break;
-    // 25 with the class-sized (G = 4/8/16/16), class-balanced group phase
-    case 26: hipLaunchKernelGGL((crc32_sweep_kernel<4, true, true, false, true, 0, -3, 16, 64, 1024, 3>), dim3(grid), dim3(1024), 0, s, a); break;
-    // 26 with 64-B lane runs in the 16-lane groups of size classes 2-3 (4-16 KiB)
-    case 27: hipLaunchKernelGGL((crc32_sweep_kernel<4, true, true, false, true, 0, -3, 16, 64, 1024, 4>), dim3(grid), dim3(1024), 0, s, a); break;
-    // 27 with 64-B lane runs in the 8-lane groups of class 1 (257 B - 1 KiB) too
-    case 28: hipLaunchKernelGGL((crc32_sweep_kernel<4, true, true, false, true, 0, -3, 16, 64, 1024, 5>), dim3(grid), dim3(1024), 0, s, a); break;
-    // 29 (default): variant 28 with s_setprio 3 around each super-block's loads
-    case 29: hipLaunchKernelGGL((crc32_sweep_kernel<4, true, true, false, true, 0, -4, 16, 64, 1024, 5>), dim3(grid), dim3(1024), 0, s, a); break;
-    // timing-only diagnostics (wrong CRCs): 100 FOLD lookups removed, 101 no per-segment
-    // atomic, 102 no wave tree
-    case kDiagNoFold: hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, true, true, 1>), dim3(grid), dim3(1024), 0, s, a); break;
-    case kDiagNoFold + 1: hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, true, true, 2>), dim3(grid), dim3(1024), 0, s, a); break;
-    case kDiagNoFold + 2: hipLaunchKernelGGL((crc32_sweep_kernel<8, true, true, true, true, 3>), dim3(grid), dim3(1024), 0, s, a); break;
-#undef AMBRY_TILES_CASE
-    default: return hipErrorInvalidValue;
-  }
-  return hipGetLastError();
-}
-
-hipError_t launch_group(const SweepArgs& a, int grid, int mode, hipStream_t s) {
-  switch (mode) {
-    case 0: return hipSuccess;
-    case 1: hipLaunchKernelGGL((crc32_group_kernel<16, 8, true>), dim3(grid), dim3(1024), 0, s, a); break;
-    case 2: hipLaunchKernelGGL((crc32_group_kernel<16, 16, true>), dim3(grid), dim3(1024), 0, s, a); break;
-    case 3: hipLaunchKernelGGL((crc32_group_kernel<32, 8, true>), dim3(grid), dim3(1024), 0, s, a); break;
-    case 4: hipLaunchKernelGGL((crc32_group_kernel<16, 32, true>), dim3(grid), dim3(1024), 0, s, a); break;
-    case 5: hipLaunchKernelGGL((crc32_group_kernel<16, 64, true>), dim3(grid), dim3(1024), 0, s, a); break;
-    case 6: hipLaunchKernelGGL((crc32_group_kernel<32, 32, true>), dim3(grid), dim3(1024), 0, s, a); break;
+    // 0: 16-B pieces, every chunk in the sweep (no group phase): the fallback shape
+    case kVariantPieces: hipLaunchKernelGGL((crc32_sweep_kernel<false, false>), dim3(grid), dim3(1024), 0, s, a); break;
+    // 29 (default): 64-B lane runs + the class-sized group phase for whole chunks <= 16 KiB
+    case kVariantDefault: hipLaunchKernelGGL((crc32_sweep_kernel<true, true>), dim3(grid), dim3(1024), 0, s, a); break;
+#ifdef AMBRYCRC_DIAGNOSTICS
+    // timing-only diagnostics (wrong CRCs; debug builds only): 100 FOLD lookups removed, 101 no
+    // per-segment atomic, 102 no wave tree
+    case kDiagNoFold: hipLaunchKernelGGL((crc32_sweep_kernel<false, false, 1>), dim3(grid), dim3(1024), 0, s, a); break;
+    case kDiagNoFold + 1: hipLaunchKernelGGL((crc32_sweep_kernel<false, false, 2>), dim3(grid), dim3(1024), 0, s, a); break;
+    case kDiagNoFold + 2: hipLaunchKernelGGL((crc32_sweep_kernel<false, false, 3>), dim3(grid), dim3(1024), 0, s, a); break;
+#endif
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

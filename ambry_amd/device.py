@@ -40,16 +40,41 @@ def _check_batch(base, off, length, n):
     for name, t in (("off", off), ("len", length)):
         if t.dtype != torch.int64 or not t.is_cuda or t.numel() != n or not t.is_contiguous():
             raise TypeError(f"{name} must be a contiguous int64 CUDA tensor of {n} elements")
+        if t.device != base.device:
+            raise TypeError(f"{name} must be on {base.device}")
+
+
+def _check_u32(name, t, n, device):
+    """crc_in / out / expected: a contiguous int32 or uint32 CUDA tensor of n elements on `device`."""
+    torch = _torch()
+    if t is None:
+        return
+    if t.dtype not in (torch.int32, torch.uint32) or not t.is_cuda or t.numel() != n or not t.is_contiguous():
+        raise TypeError(f"{name} must be a contiguous int32/uint32 CUDA tensor of {n} elements")
+    if t.device != device:
+        raise TypeError(f"{name} must be on {device}")
+
+
+def _workspace(workspace, device):
+    """(pointer, byte size) of a caller workspace (any dtype: its byte size is what counts)."""
+    if workspace is None:
+        return None, 0
+    if not workspace.is_cuda or not workspace.is_contiguous() or workspace.device != device:
+        raise TypeError(f"workspace must be a contiguous CUDA tensor on {device}")
+    return _ptr(workspace), workspace.numel() * workspace.element_size()
 
 
 def crc32_batch(base, off, length, crc_in=None, out=None, workspace=None, stream=None):
-    """out[i] = crc32(crc_in[i] or 0, base[off[i]:off[i]+len[i]]) for every chunk i (on the GPU)."""
+    """out[i] = crc32(crc_in[i] or 0, base[off[i]:off[i]+len[i]]) for every chunk i (on the GPU).
+    out may be crc_in itself (an in-place continuation)."""
     torch = _torch()
     n = off.numel()
     _check_batch(base, off, length, n)
+    _check_u32("crc_in", crc_in, n, base.device)
+    _check_u32("out", out, n, base.device)
     if out is None:
         out = torch.empty(n, dtype=torch.int32, device=base.device)
-    ws, ws_bytes = (None, 0) if workspace is None else (_ptr(workspace), workspace.numel())
+    ws, ws_bytes = _workspace(workspace, base.device)
     check(lib().ambrycrc_batch_dev(_ptr(base), _ptr(off), _ptr(length), _ptr(crc_in), _ptr(out), n, ws, ws_bytes,
                                    ctypes.c_void_p(_stream_handle(stream))), "ambrycrc_batch_dev")
     return out
@@ -62,6 +87,13 @@ def crc32_verify(base, off, length, expected, crc_in=None, out=None, stream=None
     torch = _torch()
     n = off.numel()
     _check_batch(base, off, length, n)
+    for name, t in (("crc_in", crc_in), ("out", out), ("expected", expected)):
+        _check_u32(name, t, n, base.device)
+    if expected is None:
+        raise TypeError("expected is required")
+    if mismatch is not None and (mismatch.dtype != torch.uint8 or not mismatch.is_cuda or mismatch.numel() != n
+                                 or not mismatch.is_contiguous() or mismatch.device != base.device):
+        raise TypeError(f"mismatch must be a contiguous uint8 CUDA tensor of {n} elements on {base.device}")
     if out is None:
         out = torch.empty(n, dtype=torch.int32, device=base.device)
     if mismatch is None:
@@ -75,6 +107,9 @@ def crc32_verify(base, off, length, expected, crc_in=None, out=None, stream=None
 
 def fill_random(buf, seed: int, stream_off: int = 0, stream=None) -> None:
     """Deterministic splitmix64 bytes (same stream as oracle_fill_splitmix)."""
+    torch = _torch()
+    if buf.dtype != torch.uint8 or not buf.is_cuda or not buf.is_contiguous():
+        raise TypeError("buf must be a contiguous uint8 CUDA tensor")
     check(lib().ambrycrc_fill_random_dev(_ptr(buf), buf.numel(), seed & (2**64 - 1), stream_off,
                                          ctypes.c_void_p(_stream_handle(stream))), "ambrycrc_fill_random_dev")
 
@@ -174,8 +209,9 @@ def verify_messages(region, msg_off, stream=None, want_end: bool = True):
     torch = _torch()
     if region.dtype != torch.uint8 or not region.is_cuda:
         raise TypeError("region must be a uint8 CUDA tensor")
-    if msg_off.dtype != torch.int64 or not msg_off.is_cuda or not msg_off.is_contiguous():
-        raise TypeError("msg_off must be a contiguous int64 CUDA tensor")
+    if msg_off.dtype != torch.int64 or not msg_off.is_cuda or not msg_off.is_contiguous() or \
+            msg_off.device != region.device:
+        raise TypeError(f"msg_off must be a contiguous int64 CUDA tensor on {region.device}")
     m = msg_off.numel()
     status = torch.empty(m, dtype=torch.int32, device=region.device)
     end = torch.empty(m, dtype=torch.int64, device=region.device) if want_end else None

@@ -110,7 +110,10 @@ def test_ragged_batch_grid_sizes(gpu, oracle, grid):
     assert np.array_equal(got, oracle.batch(mem, off, ln, threads=8))
 
 
-@pytest.mark.parametrize("variant", list(range(30)))
+VARIANTS = (0, 29)  # built into the library: the 16-B-piece fallback and the default
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
 def test_kernel_variants(gpu, oracle, variant):
     rng = np.random.default_rng(100 + variant)
     mem = stream_bytes(6, 0, 16 << 20)
@@ -125,16 +128,16 @@ def test_kernel_variants(gpu, oracle, variant):
     assert np.array_equal(got, oracle.batch(mem, off, ln, threads=8))
 
 
-@pytest.mark.parametrize("variant", [0, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29])
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("grid", [0, 3])
 def test_small_chunk_group_kernel(gpu, oracle, variant, grid):
-    """Group phase (variants 14-24): whole chunks <= 2..16 KiB, G lanes each, init register
-    folded into the data, size-classed rounds. Lengths 0..20000 at every alignment, crc_in,
-    large chunks between; batches of >= 16384 chunks so the group modes engage."""
+    """Group phase (variant 29; variant 0 sweeps every chunk): whole chunks <= 16 KiB, G lanes
+    each, init register folded into the data, size-classed rounds. Lengths 0..20000 at every
+    alignment, crc_in, large chunks between; batches of >= 16384 chunks so the group phase engages."""
     rng = np.random.default_rng(700 + variant * 10 + grid)
     mem = stream_bytes(70 + variant, 0, 8 << 20)
     n = 20000  # >= kGroupMinChunks (16384): group modes engage
-    ln = rng.integers(0, 20000 if variant >= 17 else 5000, size=n)
+    ln = rng.integers(0, 20000, size=n)
     ln[:46] = list(range(0, 20)) + [255, 256, 257, 511, 512, 513, 2047, 2048, 2049, 4095, 4096, 4097,
                                     1 << 20, 3, 2, 1, 0, 16, 17, 33, 8191, 8192, 8193, 16383, 16384, 16385]
     ln[::397] = rng.integers(5000, 1 << 20, size=len(ln[::397]))  # large chunks mixed in
@@ -566,3 +569,132 @@ def test_timing_with_host_paths(gpu, oracle):
     each = gpu.timing_collect_each(0)
     assert len(each) >= 2 and all(x > 0 for x in each)
     assert got[0] == int(host_u32(out)[0]) == oracle.crc32(mem)
+
+
+def _mixed_batch(seed, n=20000):
+    rng = np.random.default_rng(seed)
+    mem = stream_bytes(seed, 0, 8 << 20)
+    ln = rng.integers(0, 20000, size=n)
+    ln[::397] = rng.integers(20000, 1 << 20, size=len(ln[::397]))  # sweep-mode chunks mixed in
+    ln[:8] = [0, 1, 3, 4, 5, 16, 17, 16385]
+    off = rng.integers(0, (8 << 20) - (1 << 20), size=n)
+    cin = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32)
+    cin[::5] = 0
+    return mem, off, ln, cin
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_in_place_continuation(gpu, oracle, variant):
+    """d_out == d_crc_in (a streaming update in place): the plan copies crc_in before it
+    initialises out, so every chunk continues from its own seed. 20,000 mixed chunks hit both
+    the group phase and the sweep (aliased buffers used to compute from 0)."""
+    torch = _torch()
+    mem, off, ln, cin = _mixed_batch(4242)
+    buf = torch.from_numpy(cin.view(np.int32).copy()).cuda()
+    default = gpu.get_variant(0)
+    gpu.set_variant(0, variant)
+    try:
+        out = gpu.crc32_batch(dev_bytes(mem), dev_u64(off), dev_u64(ln), crc_in=buf, out=buf)
+        torch.cuda.synchronize()
+    finally:
+        gpu.set_variant(0, default)
+    assert out.data_ptr() == buf.data_ptr()
+    assert np.array_equal(host_u32(buf), oracle.batch(mem, off, ln, crc_in=cin, threads=8))
+
+
+def test_partial_overlap_of_crc_in_and_out_rejected(gpu):
+    torch = _torch()
+    from ambry_amd._lib import AmbryCrcError
+
+    buf = torch.zeros(17, dtype=torch.int32, device="cuda")
+    mem = dev_bytes(stream_bytes(1, 0, 4096))
+    with pytest.raises(AmbryCrcError):
+        gpu.crc32_batch(mem, dev_u64([0] * 16), dev_u64([100] * 16), crc_in=buf[1:], out=buf[:16])
+
+
+def test_default_workspace_concurrent_threads(gpu, oracle):
+    """Six host threads call ambrycrc_batch_dev with ws = NULL and growing n, each on its own
+    stream and on the shared default stream: a growing workspace is retired behind the work
+    queued on it, never freed under it (ambrycrc.cpp resolve/ensure_ws)."""
+    import threading
+
+    torch = _torch()
+    mem = stream_bytes(77, 0, 4 << 20)
+    base = dev_bytes(mem)
+    errors, results = [], {}
+
+    def work(t):
+        try:
+            rng = np.random.default_rng(t)
+            s = torch.cuda.Stream() if t % 2 else torch.cuda.current_stream()
+            for it in range(12):
+                n = int(64 * (2 ** (it % 9)) + t)  # 65 .. 16,390 chunks: crosses the group threshold
+                ln = rng.integers(0, 9000, size=n)
+                off = rng.integers(0, (4 << 20) - 9000, size=n)
+                with torch.cuda.stream(s):
+                    o, l = dev_u64(off), dev_u64(ln)
+                    out = gpu.crc32_batch(base, o, l, stream=s)
+                    got = out.cpu().numpy().view(np.uint32)
+                results[(t, it)] = (off, ln, got)
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(repr(e))
+
+    ths = [threading.Thread(target=work, args=(t,)) for t in range(6)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    torch.cuda.synchronize()
+    assert not errors, errors
+    assert len(results) == 72
+    for off, ln, got in results.values():
+        assert np.array_equal(got, oracle.batch(mem, off, ln, threads=8))
+
+
+def test_diagnostic_variants_not_selectable(gpu):
+    """Variants 100-102 (timing builds that return wrong CRCs) are not in the product library."""
+    from ambry_amd._lib import AmbryCrcError
+
+    for v in (1, 22, 28, 30, 100, 101, 102, -1):
+        with pytest.raises(AmbryCrcError):
+            gpu.set_variant(0, v)
+    assert gpu.get_variant(0) == 29
+
+
+@pytest.mark.parametrize("value,expect", [("0", 0), ("29", 29), ("101", 29), ("abc", 29), ("29x", 29), ("-5", 29)])
+def test_variant_environment_validated(value, expect):
+    """AMBRYCRC_VARIANT selects only a built-in shape; anything else is ignored."""
+    import os
+    import subprocess
+    import sys
+
+    code = ("import sys; sys.path.insert(0, %r); from ambry_amd import device as D; D.init(0); "
+            "print(D.get_variant(0))" % os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    env = dict(os.environ, AMBRYCRC_VARIANT=value)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert int(r.stdout.strip().splitlines()[-1]) == expect
+
+
+def test_binding_rejects_bad_tensors(gpu):
+    """ambry_amd.device checks every tensor before the ABI sees it (device.py:45)."""
+    torch = _torch()
+    base = dev_bytes(stream_bytes(3, 0, 4096))
+    off, ln = dev_u64([0, 16]), dev_u64([10, 20])
+    bad = [
+        dict(crc_in=torch.zeros(2, dtype=torch.int32)),                       # CPU tensor
+        dict(crc_in=torch.zeros(2, dtype=torch.int64, device="cuda")),        # wrong dtype
+        dict(out=torch.zeros(3, dtype=torch.int32, device="cuda")),           # wrong size
+        dict(out=torch.zeros(4, dtype=torch.int32, device="cuda")[::2]),      # non-contiguous
+        dict(workspace=torch.zeros(16, dtype=torch.uint8)),                   # CPU workspace
+    ]
+    for kw in bad:
+        with pytest.raises(TypeError):
+            gpu.crc32_batch(base, off, ln, **kw)
+    with pytest.raises(TypeError):
+        gpu.crc32_verify(base, off, ln, torch.zeros(2, dtype=torch.int16, device="cuda"))
+    # a workspace is sized in bytes whatever its dtype
+    ws = torch.empty((gpu.workspace_bytes(2) + 7) // 8, dtype=torch.int64, device="cuda")
+    out = gpu.crc32_batch(base, off, ln, workspace=ws)
+    torch.cuda.synchronize()
+    assert out.numel() == 2
