@@ -19,6 +19,16 @@ AMBRYCRC_EHIP = -2
 AMBRYCRC_ENOMEM = -3
 AMBRYCRC_ENOINIT = -4
 AMBRYCRC_ENODEV = -5
+AMBRYCRC_ECOMM = -6
+UNIQUE_ID_BYTES = 128
+
+
+class Shard(ctypes.Structure):
+    """struct ambrycrc_shard (include/ambrycrc.h): one GPU's part of a multi-GPU batch."""
+    _fields_ = [("device", ctypes.c_int), ("d_base", ctypes.c_void_p), ("d_off", ctypes.c_void_p),
+                ("d_len", ctypes.c_void_p), ("d_crc_in", ctypes.c_void_p), ("n", ctypes.c_size_t),
+                ("d_gathered", ctypes.c_void_p), ("stream", ctypes.c_void_p)]
+
 
 # (name, restype, argtypes) for every symbol include/ambrycrc.h declares.
 _u8p = ctypes.c_void_p
@@ -60,6 +70,21 @@ _SIGNATURES = [
     ("ambrycrc_batch_multi", ctypes.c_int,
      [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32),
       ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t, ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_int]),
+    ("ambrycrc_batch_cpu", ctypes.c_int,
+     [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32),
+      ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t, ctypes.c_int]),
+    ("ambrycrc_shard_by_bytes", ctypes.c_int,
+     [ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]),
+    ("ambrycrc_unique_id", ctypes.c_int, [ctypes.POINTER(ctypes.c_uint8)]),
+    ("ambrycrc_comm_init_all", ctypes.c_int,
+     [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    ("ambrycrc_comm_init_rank", ctypes.c_int,
+     [ctypes.POINTER(ctypes.c_uint8), ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    ("ambrycrc_comm_destroy", ctypes.c_int, [ctypes.c_void_p]),
+    ("ambrycrc_comm_size", ctypes.c_int, [ctypes.c_void_p]),
+    ("ambrycrc_batch_dev_multi", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Shard), ctypes.c_int]),
+    ("ambrycrc_batch_dev_gather", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.POINTER(Shard), ctypes.POINTER(ctypes.c_uint64)]),
     ("ambrycrc_put_crcs", ctypes.c_int,
      [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_void_p),
       ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint64),

@@ -7,6 +7,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <sched.h>
+
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
@@ -514,6 +516,7 @@ const char* ambrycrc_strerror(int code) {
     case AMBRYCRC_ENOMEM: return "out of memory";
     case AMBRYCRC_ENOINIT: return "ambrycrc_init() not called for the current device";
     case AMBRYCRC_ENODEV: return "no usable gfx950 device";
+    case AMBRYCRC_ECOMM: return "RCCL unavailable or a collective call failed";
     default: return "unknown error";
   }
 }
@@ -533,6 +536,39 @@ uint32_t ambrycrc_update_iov(uint32_t crc, const void* const* ptrs, const size_t
   for (size_t i = 0; i < n; ++i)
     if (ptrs[i] && lens[i]) reg = host_update_reg(reg, static_cast<const uint8_t*>(ptrs[i]), lens[i]);
   return ~reg;
+}
+
+int ambrycrc_batch_cpu(const void* const* ptrs, const uint64_t* lens, const uint32_t* crc_in, uint32_t* out, size_t n,
+                       int threads) {
+  if (n == 0) return AMBRYCRC_OK;
+  if (!ptrs || !lens || !out || threads < 0) return AMBRYCRC_EINVAL;
+  for (size_t i = 0; i < n; ++i)
+    if (lens[i] && !ptrs[i]) return AMBRYCRC_EINVAL;
+  if (threads == 0) {
+    cpu_set_t set;
+    threads = sched_getaffinity(0, sizeof(set), &set) == 0 ? CPU_COUNT(&set) : 1;
+  }
+  threads = (int)std::min<size_t>((size_t)std::max(threads, 1), n);
+  auto run = [&](size_t a, size_t b) {
+    for (size_t i = a; i < b; ++i) {
+      const uint32_t c = crc_in ? crc_in[i] : 0u;
+      out[i] = lens[i] ? ~host_update_reg(~c, static_cast<const uint8_t*>(ptrs[i]), lens[i]) : c;
+    }
+  };
+  if (threads == 1) {
+    run(0, n);
+    return AMBRYCRC_OK;
+  }
+  std::vector<size_t> cut(threads + 1, n);
+  const int rc = ambrycrc_shard_by_bytes(lens, n, threads, cut.data());
+  if (rc) return rc;
+  std::vector<std::thread> th;
+  th.reserve(threads - 1);
+  for (int t = 1; t < threads; ++t)
+    if (cut[t] < cut[t + 1]) th.emplace_back(run, cut[t], cut[t + 1]);
+  run(cut[0], cut[1]);
+  for (auto& t : th) t.join();
+  return AMBRYCRC_OK;
 }
 
 uint32_t ambrycrc_update_byte(uint32_t crc, int b) {
@@ -763,17 +799,9 @@ int ambrycrc_batch_multi(const void* const* ptrs, const uint64_t* lens, const ui
     dev[g] = devices ? devices[g] : g;
     if (!ctx_for(dev[g])) return AMBRYCRC_ENOINIT;
   }
-  // Range g = [cut[g], cut[g+1]): the first chunk index whose byte prefix reaches g/ndev of the total.
-  uint64_t total = 0;
-  for (size_t i = 0; i < n; ++i) total += lens[i];
   std::vector<size_t> cut(ndev + 1, n);
-  cut[0] = 0;
-  uint64_t prefix = 0;
-  int g = 1;
-  for (size_t i = 0; i < n && g < ndev; ++i) {
-    while (g < ndev && (unsigned __int128)prefix * ndev >= (unsigned __int128)total * g) cut[g++] = i;
-    prefix += lens[i];
-  }
+  const int src = ambrycrc_shard_by_bytes(lens, n, ndev, cut.data());
+  if (src) return src;
   std::vector<int> rc(ndev, AMBRYCRC_OK);
   std::vector<std::thread> th;
   th.reserve(ndev);

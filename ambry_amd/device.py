@@ -10,7 +10,7 @@ from __future__ import annotations
 
 import ctypes
 
-from ._lib import check, lib
+from ._lib import UNIQUE_ID_BYTES, Shard, check, lib
 
 
 def _torch():
@@ -285,3 +285,102 @@ def chain_messages_host(region: bytes, start: int = 0, max_messages: int = 1 << 
     n = lib().ambrycrc_chain_messages_host(ctypes.c_void_p(arr.ctypes.data if arr.nbytes else 0), arr.nbytes, start,
                                            offs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), max_messages)
     return [int(x) for x in offs[:n]]
+
+
+# ------------------------------------------------ multi-GPU batch + RCCL all-gather (§8e)
+
+def shard_by_bytes(lengths, nshards: int):
+    """ambrycrc_shard_by_bytes: contiguous chunk ranges [lo, hi) of about equal bytes per shard."""
+    import numpy as np
+
+    lens = np.ascontiguousarray(np.asarray(lengths, dtype=np.uint64))
+    cuts = (ctypes.c_size_t * (nshards + 1))()
+    check(lib().ambrycrc_shard_by_bytes(lens.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), len(lens), nshards,
+                                        cuts), "ambrycrc_shard_by_bytes")
+    return [(int(cuts[g]), int(cuts[g + 1])) for g in range(nshards)]
+
+
+def crc32_batch_cpu(chunks, crc_in=None, threads: int = 0):
+    """ambrycrc_batch_cpu: per-chunk CRCs of host buffers on `threads` CPU threads (0 = all allowed)."""
+    n, ptrs, lens, cin = _host_chunks(chunks, crc_in)
+    out = (ctypes.c_uint32 * n)()
+    check(lib().ambrycrc_batch_cpu(ptrs, lens, cin, out, n, threads), "ambrycrc_batch_cpu")
+    return list(out)
+
+
+def unique_id() -> bytes:
+    """ambrycrc_unique_id: the 128-byte RCCL id rank 0 sends to every rank."""
+    buf = (ctypes.c_uint8 * UNIQUE_ID_BYTES)()
+    check(lib().ambrycrc_unique_id(buf), "ambrycrc_unique_id")
+    return bytes(buf)
+
+
+class Comm:
+    """An ambrycrc_comm (RCCL communicator): Comm.all_devices([0, 1, ...]) for one process driving
+    several GPUs, Comm.rank(uid, nranks, rank, device) for one process per GPU."""
+
+    def __init__(self, handle: int, devices):
+        self.handle = ctypes.c_void_p(handle)
+        self.devices = list(devices)
+
+    @classmethod
+    def all_devices(cls, devices):
+        devs = (ctypes.c_int * len(devices))(*devices)
+        h = ctypes.c_void_p()
+        check(lib().ambrycrc_comm_init_all(devs, len(devices), ctypes.byref(h)), "ambrycrc_comm_init_all")
+        return cls(h.value, devices)
+
+    @classmethod
+    def rank(cls, uid: bytes, nranks: int, rank: int, device: int):
+        if len(uid) != UNIQUE_ID_BYTES:
+            raise ValueError(f"unique id must be {UNIQUE_ID_BYTES} bytes")
+        buf = (ctypes.c_uint8 * UNIQUE_ID_BYTES).from_buffer_copy(uid)
+        h = ctypes.c_void_p()
+        check(lib().ambrycrc_comm_init_rank(buf, nranks, rank, device, ctypes.byref(h)), "ambrycrc_comm_init_rank")
+        c = cls(h.value, [device])
+        c.rank_id = rank
+        return c
+
+    def size(self) -> int:
+        return check(lib().ambrycrc_comm_size(self.handle), "ambrycrc_comm_size")
+
+    def destroy(self) -> None:
+        if self.handle.value:
+            check(lib().ambrycrc_comm_destroy(self.handle), "ambrycrc_comm_destroy")
+            self.handle = ctypes.c_void_p()
+
+
+def _shard(base, off, length, gathered, crc_in=None, stream=None):
+    torch = _torch()
+    n = off.numel()
+    _check_batch(base, off, length, n)
+    _check_u32("crc_in", crc_in, n, base.device)
+    if gathered.dtype not in (torch.int32, torch.uint32) or not gathered.is_cuda or not gathered.is_contiguous() \
+            or gathered.device != base.device:
+        raise TypeError(f"gathered must be a contiguous int32/uint32 CUDA tensor on {base.device}")
+    s = stream if stream is not None else torch.cuda.current_stream(base.device)
+    return Shard(base.device.index, base.data_ptr(), off.data_ptr(), length.data_ptr(),
+                 None if crc_in is None else crc_in.data_ptr(), n, gathered.data_ptr(), s.cuda_stream)
+
+
+def crc32_batch_multi_dev(comm: Comm, shards):
+    """ambrycrc_batch_dev_multi. shards: one dict per device of comm, in comm order, with keys
+    base, off, len, gathered (int32[total chunks] on that device), optional crc_in and stream.
+    Every device's `gathered` receives all CRCs (shard order). Asynchronous."""
+    arr = (Shard * len(shards))(*[_shard(s["base"], s["off"], s["len"], s["gathered"], s.get("crc_in"),
+                                         s.get("stream")) for s in shards])
+    total = sum(int(s["off"].numel()) for s in shards)
+    for s in shards:
+        if s["gathered"].numel() != total:
+            raise TypeError(f"gathered must hold all {total} CRCs")
+    check(lib().ambrycrc_batch_dev_multi(comm.handle, arr, len(shards)), "ambrycrc_batch_dev_multi")
+
+
+def crc32_batch_gather(comm: Comm, base, off, length, gathered, counts, crc_in=None, stream=None):
+    """ambrycrc_batch_dev_gather: this rank's shard, then the all-gather into `gathered`
+    (int32[sum(counts)]). counts: chunks per rank, the same on every rank. Asynchronous."""
+    if gathered.numel() != sum(int(c) for c in counts):
+        raise TypeError("gathered must hold sum(counts) CRCs")
+    sh = _shard(base, off, length, gathered, crc_in, stream)
+    cnt = (ctypes.c_uint64 * len(counts))(*[int(c) for c in counts])
+    check(lib().ambrycrc_batch_dev_gather(comm.handle, ctypes.byref(sh), cnt), "ambrycrc_batch_dev_gather")

@@ -20,8 +20,10 @@ from .crc32 import combine
 def shard_by_bytes(lengths: Sequence[int], world: int) -> list[tuple[int, int]]:
     """Contiguous chunk ranges [lo, hi) per rank with near-equal byte totals.
 
-    Rank r takes the chunks whose start byte falls in [r*T/world, (r+1)*T/world).
-    Every chunk belongs to exactly one rank; ranks may be empty when n < world.
+    Rank r takes the chunks whose start byte s satisfies r/world <= s/total < (r+1)/world
+    (exact rational comparison, the rule of ambrycrc_shard_by_bytes in the C ABI, which
+    tests/test_multi.py checks this against). Every chunk belongs to exactly one rank; ranks
+    may be empty when n < world; an all-empty batch is split by count.
     """
     lengths = np.asarray(lengths, dtype=np.int64)
     n = len(lengths)
@@ -34,9 +36,25 @@ def shard_by_bytes(lengths: Sequence[int], world: int) -> list[tuple[int, int]]:
         elif total == 0:
             bounds.append((n * r) // world)  # all-empty batch: split by count
         else:
-            cut = (total * r) // world
-            bounds.append(int(np.searchsorted(starts, cut, side="left")))
+            bounds.append(int(np.searchsorted(starts * world, total * r, side="left")))
     return [(bounds[r], bounds[r + 1]) for r in range(world)]
+
+
+SEG_ALIGN = 64  # CRCs per gather-segment quantum (256 B), as ambrycrc_multi.cpp kSegAlign
+
+
+def gather_layout(counts: Sequence[int]):
+    """Layout of the all-gather of per-rank CRCs, the rule ambrycrc_batch_dev_multi/_gather
+    use (ambrycrc_multi.cpp seg_width/enqueue_gather): every rank sends a segment of `width`
+    CRCs (the largest shard rounded up to 64); when every shard has exactly `width` chunks the
+    gather lands in place, otherwise rank r's CRCs are compacted from [r*width, r*width+counts[r])
+    to [starts[r], starts[r+1]). Returns (width, in_place, starts)."""
+    counts = [int(c) for c in counts]
+    width = -(-max(counts, default=0) // SEG_ALIGN) * SEG_ALIGN
+    starts = [0]
+    for c in counts:
+        starts.append(starts[-1] + c)
+    return width, width > 0 and all(c == width for c in counts), starts
 
 
 def gather_crcs(local, lo: int, hi: int, n: int, shards, dist, group=None, device=None):
@@ -44,15 +62,20 @@ def gather_crcs(local, lo: int, hi: int, n: int, shards, dist, group=None, devic
     import torch
 
     world = len(shards)
-    width = max(h - l for l, h in shards) if shards else 0
+    width, in_place, starts = gather_layout([h - l for l, h in shards])
     dev = local.device if device is None else device
-    padded = torch.zeros(max(width, 1), dtype=torch.int32, device=dev)
+    seg = max(width, 1)
+    padded = torch.zeros(seg, dtype=torch.int32, device=dev)
     if hi > lo:
         padded[: hi - lo] = local
-    gathered = torch.empty(world * max(width, 1), dtype=torch.int32, device=dev)
+    gathered = torch.empty(world * seg, dtype=torch.int32, device=dev)
     dist.all_gather_into_tensor(gathered, padded, group=group)
-    parts = [gathered[r * max(width, 1): r * max(width, 1) + (h - l)] for r, (l, h) in enumerate(shards)]
-    out = torch.cat(parts) if parts else gathered[:0]
+    if in_place:
+        out = gathered[:n]
+    else:
+        out = torch.empty(n, dtype=torch.int32, device=dev)
+        for r, (l, h) in enumerate(shards):
+            out[starts[r]:starts[r + 1]] = gathered[r * seg: r * seg + (h - l)]
     assert out.numel() == n
     return out
 

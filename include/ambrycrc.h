@@ -23,9 +23,10 @@
  *
  * Threading: the host functions are reentrant with no mutable global state.
  * The *_dev functions may be called from several host threads; each call
- * enqueues on the caller's stream. Calls that share the context's default
- * workspace (d_ws == NULL) must not overlap on different streams; pass a
- * per-stream workspace (ambrycrc_workspace_bytes) to run them concurrently.
+ * enqueues on the caller's stream. With d_ws == NULL a call uses the default
+ * workspace of its stream (one per stream, so calls on different streams never
+ * share one); a caller workspace (ambrycrc_workspace_bytes) must not be used by
+ * two calls whose work overlaps.
  */
 #ifndef AMBRYCRC_H
 #define AMBRYCRC_H
@@ -44,6 +45,7 @@ extern "C" {
 #define AMBRYCRC_ENOMEM (-3)   /* device or pinned-host allocation failed */
 #define AMBRYCRC_ENOINIT (-4)  /* ambrycrc_init() not called for the current device */
 #define AMBRYCRC_ENODEV (-5)   /* no usable gfx950 device */
+#define AMBRYCRC_ECOMM (-6)    /* RCCL unavailable, or a collective / communicator call failed */
 
 /* ---------------------------------------------------------------- lifecycle */
 
@@ -75,6 +77,14 @@ uint32_t ambrycrc_update(uint32_t crc, const void* p, size_t n);
  * PutOperation.java:2041-2043), `for (ByteBuffer b : buf.nioBuffers()) crc.update(b)`.
  * Equals n successive ambrycrc_update calls; a NULL pointer with length 0 is allowed. */
 uint32_t ambrycrc_update_iov(uint32_t crc, const void* const* ptrs, const size_t* lens, size_t n);
+
+/* n independent host chunks on `threads` CPU threads (0 = one per CPU this process may run on):
+ * out[i] = crc32(crc_in ? crc_in[i] : 0, ptrs[i], lens[i]), with the loop ambrycrc_update runs.
+ * The many-record CPU batch for bytes that live in host memory and are not going to the GPU
+ * anyway (a GET's FileChannel read, a PUT's Netty buffers: DESIGN.md §5 "the CPU wins"); the
+ * reference runs one Crc32 per record on the calling thread (Crc32.java:55-98). Synchronous. */
+int ambrycrc_batch_cpu(const void* const* ptrs, const uint64_t* lens, const uint32_t* crc_in, uint32_t* out, size_t n,
+                       int threads);
 
 /* One byte: Crc32.update(int b) (Crc32.java:146-148). */
 uint32_t ambrycrc_update_byte(uint32_t crc, int b);
@@ -205,8 +215,7 @@ int ambrycrc_batch_host(const void* const* ptrs, const uint64_t* lens, const uin
                         size_t n, int device, int pinned);
 
 /* ambrycrc_batch_host across several GPUs of this process: the n
- * chunks are split into ndev contiguous ranges of about equal BYTES (mixed sizes are
- * balanced by bytes, not by count), range g runs ambrycrc_batch_host on devices[g]
+ * chunks are split into ndev contiguous ranges by ambrycrc_shard_by_bytes, range g runs ambrycrc_batch_host on devices[g]
  * from its own host thread, and the calls are joined. devices == NULL means
  * 0..ndev-1; a device may appear more than once (its ranges then run one after the
  * other). Every listed device must have been ambrycrc_init'ed. Returns the first
@@ -215,6 +224,55 @@ int ambrycrc_batch_host(const void* const* ptrs, const uint64_t* lens, const uin
  * process per GPU: a storage node scanning many partitions in one process. */
 int ambrycrc_batch_multi(const void* const* ptrs, const uint64_t* lens, const uint32_t* crc_in, uint32_t* out,
                          size_t n, const int* devices, int ndev, int pinned);
+
+/* ------------------------------------- multi-GPU batch + RCCL all-gather */
+
+/* Shards of a batch: chunk ranges [cuts[g], cuts[g+1]) of about equal BYTES (mixed sizes are
+ * balanced by bytes, not by count): shard g takes the chunks whose start byte s (prefix sum of
+ * lens) satisfies g/nshards <= s/total < (g+1)/nshards; an all-empty batch is split by count.
+ * cuts[nshards + 1]. Host arithmetic, no device. */
+int ambrycrc_shard_by_bytes(const uint64_t* lens, size_t n, int nshards, size_t* cuts);
+
+/* An RCCL communicator over the GPUs that share one batch (opaque). RCCL (librccl.so.1) is
+ * loaded on first use; without it these calls return AMBRYCRC_ECOMM. */
+typedef struct ambrycrc_comm ambrycrc_comm;
+#define AMBRYCRC_UNIQUE_ID_BYTES 128
+
+/* One process driving ndev GPUs (devices == NULL: 0..ndev-1; no device twice). Every device
+ * must also be ambrycrc_init'ed before a batch runs on it. */
+int ambrycrc_comm_init_all(const int* devices, int ndev, ambrycrc_comm** comm);
+/* One process per GPU: rank 0 calls ambrycrc_unique_id and sends the 128 bytes to every rank
+ * (any channel); each rank then calls ambrycrc_comm_init_rank for its own device. */
+int ambrycrc_unique_id(uint8_t* id);
+int ambrycrc_comm_init_rank(const uint8_t* id, int nranks, int rank, int device, ambrycrc_comm** comm);
+/* Waits for the communicator's devices to go idle, then releases it. */
+int ambrycrc_comm_destroy(ambrycrc_comm* comm);
+int ambrycrc_comm_size(const ambrycrc_comm* comm);
+
+/* One GPU's part of a multi-GPU batch. */
+typedef struct ambrycrc_shard {
+  int device;
+  const uint8_t* d_base;    /* the shard's chunks: d_base + d_off[i], d_len[i] bytes (device arrays) */
+  const uint64_t* d_off;
+  const uint64_t* d_len;
+  const uint32_t* d_crc_in; /* nullable */
+  size_t n;                 /* chunks in this shard */
+  uint32_t* d_gathered;     /* on `device`: the CRCs of EVERY shard, shard order (sum of all n words) */
+  hipStream_t stream;       /* work is enqueued here (NULL: the device's null stream) */
+} ambrycrc_shard;
+
+/* Single process: shards[g] runs on comm's g-th device (shards[g].device must match); each
+ * shard's CRCs are computed on its GPU (ambrycrc_batch_dev), then one ncclAllGather of the
+ * uint32 CRCs over xGMI leaves the whole batch's CRCs in every shard's d_gathered.
+ * Asynchronous: enqueued on the shards' streams. The batch callers are replication verify
+ * (ambry-replication/.../ReplicaThread.java:1810-1815) and the recovery scan of a log
+ * (ambry-store/.../BlobStoreRecovery.java:43-110), run for many partitions in one server. */
+int ambrycrc_batch_dev_multi(ambrycrc_comm* comm, const ambrycrc_shard* shards, int nshards);
+
+/* One process per GPU: this rank's shard (`mine`, on the communicator's device) and the shard
+ * sizes of all ranks (counts[nranks], identical on every rank; counts[rank] == mine->n). Every
+ * rank must call it for the gather to complete. Asynchronous, as above. */
+int ambrycrc_batch_dev_gather(ambrycrc_comm* comm, const ambrycrc_shard* mine, const uint64_t* counts);
 
 /* One-pass PUT CRCs (§8f row 2). For each of n PUT requests whose blob CRC blob_crc[i]
  * (over blob_len[i] bytes, e.g. from ambrycrc_batch_dev/ambrycrc_batch_host) is known:

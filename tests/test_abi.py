@@ -28,7 +28,7 @@ def test_exports_every_declared_symbol(ambry):
 def test_version_and_errors(ambry):
     lib = ambry.lib()
     assert lib.ambrycrc_version().decode().startswith("ambrycrc")
-    for code in (0, -1, -2, -3, -4, -5):
+    for code in (0, -1, -2, -3, -4, -5, -6):
         assert lib.ambrycrc_strerror(code)
 
 
@@ -235,8 +235,8 @@ def test_chain_messages_host_under_asan(tmp_path):
                     "-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
                     "-Xarch_host", "-fno-sanitize-recover=all", str(host_o),
                     os.path.join(ROOT, "tests", "native", "chain_asan.cpp"), os.path.join(csrc, "ambrycrc.cpp"),
-                    os.path.join(csrc, "crc32_kernels.hip"), os.path.join(csrc, "message_kernels.hip"),
-                    "-o", str(exe)], check=True, timeout=900)
+                    os.path.join(csrc, "ambrycrc_multi.cpp"), os.path.join(csrc, "crc32_kernels.hip"),
+                    os.path.join(csrc, "message_kernels.hip"), "-ldl", "-o", str(exe)], check=True, timeout=900)
     r = subprocess.run([str(exe), str(rf)], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "runs=" in r.stdout
@@ -261,3 +261,37 @@ def test_update_iov_gather_list(ambry):
     ptrs = (ctypes.c_void_p * 3)(None, None, None)
     lens = (ctypes.c_size_t * 3)(0, 0, 0)
     assert lib.ambrycrc_update_iov(0x1234, ptrs, lens, 3) == 0x1234
+
+
+def test_batch_cpu_vs_oracle(ambry, oracle):
+    """ambrycrc_batch_cpu (the host-resident many-record batch) on 1, 3 and all threads."""
+    from ambry_amd import device as D
+
+    rng = np.random.default_rng(9)
+    mem = stream_bytes(31, 0, 3 << 20)
+    n = 500
+    ln = rng.integers(0, 20000, size=n)
+    ln[:6] = [0, 1, 63, 64, 65, 1 << 20]
+    off = rng.integers(0, (3 << 20) - (1 << 20), size=n)
+    cin = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32)
+    exp = oracle.batch(mem, off, ln, crc_in=cin)
+    base = mem.ctypes.data
+    chunks = [(base + int(o), int(l)) for o, l in zip(off, ln)]
+    for th in (1, 3, 0):
+        assert D.crc32_batch_cpu(chunks, crc_in=cin, threads=th) == exp.tolist()
+    assert D.crc32_batch_cpu([(0, 0), (base, 5)], threads=64) == [0, oracle.crc32(mem[:5])]
+
+
+def test_multi_gpu_entries_validate_without_gpu(ambry):
+    """The RCCL entry points reject bad arguments before touching a device or RCCL."""
+    import ctypes
+
+    lib = ambry.lib()
+    h = ctypes.c_void_p()
+    assert lib.ambrycrc_comm_init_all(None, 0, ctypes.byref(h)) == -1
+    assert lib.ambrycrc_comm_init_rank(None, 2, 0, 0, ctypes.byref(h)) == -1
+    assert lib.ambrycrc_batch_dev_multi(None, None, 1) == -1
+    assert lib.ambrycrc_batch_dev_gather(None, None, None) == -1
+    assert lib.ambrycrc_comm_destroy(None) == 0
+    assert lib.ambrycrc_comm_size(None) == -1
+    assert lib.ambrycrc_unique_id(None) == -1

@@ -39,6 +39,44 @@ def test_shard_by_bytes_covers_everything():
     assert shard_by_bytes([0, 0, 0, 0], 2) == [(0, 2), (2, 4)]
 
 
+def test_shard_by_bytes_matches_c_abi(ambry):
+    """The Python mirror and ambrycrc_shard_by_bytes (used by ambrycrc_batch_multi,
+    ambrycrc_batch_cpu and bench.py's multi-GPU shards) give the same cuts, including when a
+    chunk starts exactly on a shard boundary and for totals past 2^32."""
+    from ambry_amd import device as D
+    from ambry_amd.multi import shard_by_bytes
+
+    rng = np.random.default_rng(11)
+    cases = [[4] * 8, [4] * 9, [0, 0, 0], [], [1], [0, 5, 0, 5, 0], [1 << 40, 1, 1, 1 << 40],
+             [4 << 20] * 65536, [3, 3, 3, 3, 3, 3, 3]]
+    cases += [rng.integers(0, 1 << 22, size=int(rng.integers(1, 3000))).tolist() for _ in range(30)]
+    cases += [(rng.integers(0, 4, size=40) * 1024).tolist() for _ in range(30)]  # ties on boundaries
+    for lens in cases:
+        for world in (1, 2, 3, 4, 7, 8, 16):
+            assert D.shard_by_bytes(lens, world) == shard_by_bytes(lens, world), (lens[:10], world)
+
+
+def test_gather_layout_index_math():
+    """Segment width, in-place case and compaction offsets of the CRC all-gather."""
+    from ambry_amd.multi import gather_layout
+
+    assert gather_layout([64, 64, 64]) == (64, True, [0, 64, 128, 192])
+    assert gather_layout([8192] * 8)[:2] == (8192, True)
+    assert gather_layout([65536] * 8)[:2] == (65536, True)
+    w, inplace, starts = gather_layout([5, 0, 70, 64])
+    assert (w, inplace, starts) == (128, False, [0, 5, 5, 75, 139])
+    assert gather_layout([0, 0]) == (0, False, [0, 0, 0])
+    assert gather_layout([1]) == (64, False, [0, 1])
+    # the padded buffer holds world*width CRCs; each rank's segment fits its width
+    rng = np.random.default_rng(3)
+    for _ in range(100):
+        counts = rng.integers(0, 300, size=int(rng.integers(1, 9))).tolist()
+        w, inplace, starts = gather_layout(counts)
+        assert w % 64 == 0 and w >= max(counts) and w - max(counts) < 64
+        assert starts[-1] == sum(counts)
+        assert inplace == (w > 0 and all(c == w for c in counts))
+
+
 def _worker(rank, world, port, q):
     import torch
     import torch.distributed as dist
