@@ -1,16 +1,25 @@
 #!/usr/bin/env python3
-"""bench.py -- device-resident CRC-32 over 4 MiB blob chunks (BASELINE.json metric, config C3).
+"""bench.py -- device-resident CRC-32 over 4 MiB blob chunks (BASELINE.json metric).
 
-One step = one pass of the hot path (ambrycrc_batch_dev: plan + sweep kernels)
-over one batch of 8,192 x 4 MiB chunks (32 GiB) resident in HBM on every rank.
-N>1: one process per GPU (torchrun), each rank owns its own 8,192-chunk shard
-(weak scaling; C5 = 524,288 chunks = 8 such steps on 8 GPUs) and the 4-byte
-CRCs are all-gathered over RCCL once per step.
+One step = one pass of the hot path over one batch resident in HBM on every GPU:
+  N = 1  config C3 (8,192 x 4 MiB = 32 GiB): ambrycrc_batch_dev (plan + sweep kernels).
+  N > 1  config C5's per-GPU shard (65,536 x 4 MiB = 256 GiB per GPU; C5 = 524,288 chunks on
+         8 GPUs): every GPU CRCs its shard, then one RCCL all-gather of the 4-byte CRCs over
+         xGMI leaves the whole batch's CRCs on every GPU -- both inside libambrycrc's C ABI:
+           WORLD_SIZE set (torchrun, one process per GPU): ambrycrc_batch_dev_gather on a
+             communicator built from ambrycrc_unique_id (sent over a gloo control group);
+           WORLD_SIZE unset, --gpus N: one process drives N GPUs, ambrycrc_batch_dev_multi.
+         Weak scaling: the per-GPU shard is fixed as N grows.
+  --config c1   one 64 KiB PUT message on the CPU (BASELINE configs[0]): µs per message for the
+                product host path and for the oracle; not the headline metric.
 
 Prints ONE JSON line (rank 0). Besides the driver contract it carries:
-  roofline      sweep-kernel algorithmic bytes / its HIP-event-timed duration vs 8 TB/s
-  cpu_baseline  the oracle's restatement of Crc32.java (kind "port") on host cores, bounded sample
+  roofline      sweep-kernel algorithmic bytes / its HIP-event-timed duration vs 8 TB/s; traffic
+                from bench_data/pmc_traffic.json (rocprofv3 PMC, (2*FETCH_SIZE+WRITE_SIZE) KiB)
+  cpu_baseline  the oracle's restatement of Crc32.java (kind "port") on host cores, 1 thread and
+                the process's CPU share, over a DRAM-resident sample (> L3)
   host_path     pinned-host -> HBM -> CRC rate (PCIe-inclusive; never `value`)
+  rccl          N > 1: ranks RCCL saw and whether every GPU's gathered vector is right
 """
 from __future__ import annotations
 
@@ -26,6 +35,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 METRIC = "GiB/s device-resident CRC32 over 4 MiB blob chunks; % of HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+TRAFFIC_FILE = os.path.join(ROOT, "bench_data", "pmc_traffic.json")
 
 CONFIGS = {
     # name: (chunks per GPU, chunk bytes, description)
@@ -34,7 +44,7 @@ CONFIGS = {
     # 524,288 x 4 MiB over 8 GPUs = 65,536 x 4 MiB = 256 GiB resident per
     # GPU (of 268 GiB HBM). Every chunk is distinct: a reused buffer let waves that run at
     # the same time read the same bytes, and the caches then served ~4 % of the reads.
-    "c5": (65536, 4 << 20, "C5: 65,536 x 4 MiB chunks per GPU (256 GiB resident)"),
+    "c5": (65536, 4 << 20, "C5: 65,536 x 4 MiB chunks per GPU (256 GiB resident; 524,288 on 8 GPUs)"),
 }
 
 
@@ -43,7 +53,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS) + ["c4"])
+    ap.add_argument("--config", default=None, choices=sorted(CONFIGS) + ["c1", "c4"],
+                    help="default: c3 at one GPU, c5 (per-GPU shard) at N > 1")
     ap.add_argument("--variant", type=int, default=None)
     ap.add_argument("--grid", type=int, default=None, help="sweep-kernel workgroups (default: one per CU)")
     ap.add_argument("--window", type=int, default=None,
@@ -51,10 +62,14 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-path", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-sample-gib", type=float, default=2.0,
+                    help="CPU baseline sample (GiB): several times the host's L3, so it is a DRAM rate")
     ap.add_argument("--prewarm-s", type=float, default=0.3, help="untimed clock-ramp run before warmup")
     ap.add_argument("--quiet", action="store_true", help="no progress lines on stderr")
     ap.add_argument("--force-dist", action="store_true",
-                    help="init the RCCL process group and all-gather even at WORLD_SIZE=1 (exercises the N>1 path)")
+                    help="one-process-per-GPU form even at WORLD_SIZE=1 (gloo control group + RCCL gather)")
+    ap.add_argument("--inproc", action="store_true",
+                    help="one-process multi-GPU form (ambrycrc_batch_dev_multi) even at --gpus 1")
     return ap.parse_args()
 
 
@@ -63,10 +78,13 @@ def log(args, *msg):
         print("[bench]", *msg, file=sys.stderr, flush=True)
 
 
-def build_workload(torch, dev, args, rank):
+def build_workload(torch, dev, config, seed_rank):
+    """One GPU's batch in HBM: (buf, off, len, n, total bytes, chunk bytes or None, description)."""
+    import numpy as np
+
     from ambry_amd import device as D
 
-    if args.config == "c4":
+    if config == "c4":
         from datagen import zipf_sizes
 
         sizes = zipf_sizes(32768)
@@ -74,26 +92,77 @@ def build_workload(torch, dev, args, rank):
         for s in sizes[:-1]:
             off.append(off[-1] + ((int(s) + 15) // 16) * 16)
         total = off[-1] + int(sizes[-1])
-        import numpy as np
-
         off_t = torch.tensor(np.asarray(off, dtype=np.int64), device=dev)
         len_t = torch.tensor(sizes.astype(np.int64), device=dev)
         desc = "C4: 32,768 Zipf(1.2) chunks 4 KiB-4 MiB (verify-on-read sizes)"
         n = len(sizes)
         chunk = None
     else:
-        n, chunk, desc = CONFIGS[args.config]
+        n, chunk, desc = CONFIGS[config]
         total = n * chunk
         off_t = torch.arange(n, dtype=torch.int64, device=dev) * chunk
         len_t = torch.full((n,), chunk, dtype=torch.int64, device=dev)
     buf = torch.empty(total, dtype=torch.uint8, device=dev)
-    D.fill_random(buf, 0xA3B1C2D3 ^ (rank * 0x9E3779B97F4A7C15 & (2**64 - 1)), 0)
-    torch.cuda.synchronize()
+    D.fill_random(buf, 0xA3B1C2D3 ^ (seed_rank * 0x9E3779B97F4A7C15 & (2**64 - 1)), 0)
+    torch.cuda.synchronize(dev)
     return buf, off_t, len_t, n, total, chunk, desc
 
 
+# ------------------------------------------------------------------ CPU baseline
+
+def cpu_topology():
+    """CPUs this process may use: affinity set, cgroup quota, physical cores behind the set."""
+    aff = sorted(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()
+            if q != "max":
+                quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        pass
+    cores = set()
+    for c in aff:
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/core_id") as f:
+                core = f.read().strip()
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/physical_package_id") as f:
+                pkg = f.read().strip()
+            cores.add((pkg, core))
+        except OSError:
+            cores.add(("?", c))
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    usable = min(len(aff), quota) if quota else len(aff)
+    return {"cpu_model": model, "affinity_cpus": len(aff), "physical_cores_in_affinity": len(cores),
+            "cgroup_cpu_quota": quota, "usable_cpus": usable, "nproc": os.cpu_count()}
+
+
+def _timed(fn, nbytes, seconds):
+    """Repeat fn() for about `seconds`; GiB/s, passes, last result."""
+    t0 = time.perf_counter()
+    passes = 0
+    while True:
+        out = fn()
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or passes >= 1000:
+            return passes * nbytes / el / 2**30, passes, out
+
+
 def cpu_baseline(buf, off_t, len_t, n, args):
-    """Oracle (C restatement of Crc32.java slice-by-8) on host cores over a bounded sample."""
+    """The oracle (oracle/crc32_ref.c: C restatement of Crc32.java's slice-by-8, kind "port") on
+    the GPU box's host cores, over a sample of the same workload copied to host memory: at least
+    --cpu-sample-gib (default 2 GiB, several times the host's L3), so the rate is a DRAM rate.
+    1 thread, and the process's whole CPU share (min(affinity set, cgroup quota)); system zlib
+    (java.util.zip.CRC32's function) and the library's own CLMUL loop beside it."""
     import numpy as np
 
     from conftest import ORACLE_SO, Oracle
@@ -101,45 +170,51 @@ def cpu_baseline(buf, off_t, len_t, n, args):
     if not os.path.exists(ORACLE_SO):
         return None
     orc = Oracle()
-    sample_chunks = min(n, 64)
-    off = off_t[:sample_chunks].cpu().numpy()
-    ln = len_t[:sample_chunks].cpu().numpy()
+    import ambry_amd
+    from ambry_amd import device as D
+
+    ln_all = len_t.cpu().numpy()
+    want = int(args.cpu_sample_gib * 2**30)
+    cum = np.cumsum(ln_all)
+    k = int(min(n, np.searchsorted(cum, want) + 1))
+    off = off_t[:k].cpu().numpy()
+    ln = ln_all[:k]
     lo, hi = int(off[0]), int(off[-1] + ln[-1])
     host = buf[lo:hi].cpu().numpy()
     off = off - lo
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    nbytes = int(ln.sum())
+    topo = cpu_topology()
+    share = topo["usable_cpus"]
+    each = args.cpu_seconds / 7
     res = {}
     for zl in (False, True):
-        for th in (1, threads):
-            t0 = time.perf_counter()
-            passes = 0
-            while True:
-                out = orc.batch(host, off, ln, threads=th, zlib=zl)
-                passes += 1
-                el = time.perf_counter() - t0
-                if el >= args.cpu_seconds / 4 or passes >= 1000:
-                    break
-            res[(zl, th)] = (passes * int(ln.sum()) / el / 2**30, passes, out)
-    assert np.array_equal(res[(True, threads)][2], res[(False, threads)][2]), "zlib vs restatement"
-    gibs, passes, out = res[(False, threads)]
-    clmul = host_clmul_rate(host, off, ln, out, threads, args.cpu_seconds / 4)
-    cpu_model = None
-    try:
-        with open("/proc/cpuinfo") as f:
-            for line in f:
-                if line.startswith("model name"):
-                    cpu_model = line.split(":", 1)[1].strip()
-                    break
-    except OSError:
-        pass
+        for th in (1, share):
+            res[(zl, th)] = _timed(lambda: orc.batch(host, off, ln, threads=th, zlib=zl), nbytes, each)
+    assert np.array_equal(res[(True, share)][2], res[(False, share)][2]), "zlib vs restatement"
+    gibs, passes, out = res[(False, share)]
+    aff_run = None
+    if topo["affinity_cpus"] > share:  # the whole affinity set, throttled to the quota by the cgroup
+        aff_run = round(_timed(lambda: orc.batch(host, off, ln, threads=topo["affinity_cpus"]), nbytes, each)[0], 3)
+    base = host.ctypes.data
+    chunks = [(base + int(o), int(x)) for o, x in zip(off, ln)]
+    clmul_out = np.asarray(D.crc32_batch_cpu(chunks, threads=1), dtype=np.uint32)
+    clmul = {
+        "impl": ambry_amd.lib().ambrycrc_host_impl().decode(),
+        "single_thread_gibs": round(_timed(lambda: D.crc32_batch_cpu(chunks, threads=1), nbytes, each)[0], 3),
+        "gibs": round(_timed(lambda: D.crc32_batch_cpu(chunks, threads=share), nbytes, each)[0], 3),
+        "cores": share, "parity_vs_port": bool(np.array_equal(clmul_out, out)),
+        "what": "libambrycrc ambrycrc_batch_cpu (CLMUL fold, the class of HotSpot's CRC32 intrinsic), same sample",
+    }
     return {
-        "value": round(gibs, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-        "cpu_model": cpu_model, "nproc": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
-        "sample": f"{sample_chunks} chunks x {int(ln[0]) if len(set(ln.tolist())) == 1 else 'mixed'} B "
-                  f"(first chunks of the same workload, D2H-copied) x {passes} passes; oracle/crc32_ref.c "
-                  f"slice-by-8 restating Crc32.java:55-98, {threads} pthreads",
+        "value": round(gibs, 3), "unit": "GiB/s", "cores": share, "kind": "port",
+        **topo,
+        "sample": f"{k} chunks = {nbytes / 2**30:.2f} GiB (first chunks of the same workload, D2H-copied; "
+                  f"> the host L3) x {passes} passes; oracle/crc32_ref.c slice-by-8 restating Crc32.java:55-98, "
+                  f"{share} pthreads = the process's CPU share (cgroup quota {topo['cgroup_cpu_quota']}, "
+                  f"affinity {topo['affinity_cpus']} CPUs)",
         "single_thread_gibs": round(res[(False, 1)][0], 3),
-        "zlib": {"gibs": round(res[(True, threads)][0], 3), "cores": threads,
+        "all_affinity_threads_gibs": aff_run,
+        "zlib": {"gibs": round(res[(True, share)][0], 3), "cores": share,
                  "single_thread_gibs": round(res[(True, 1)][0], 3),
                  "what": "system zlib 1.2.11 crc32_z (the function java.util.zip.CRC32 wraps), same sample"},
         "host_clmul": clmul,
@@ -147,49 +222,7 @@ def cpu_baseline(buf, off_t, len_t, n, args):
     }
 
 
-def host_clmul_rate(host, off, ln, expect, threads, seconds):
-    """The library's own CPU path (ambrycrc_update: carry-less-multiply fold, the class of
-    HotSpot's CRC32 intrinsic) on the same sample, 1 thread and `threads` threads (ctypes
-    releases the GIL for the call). Not the baseline: a check on what the JVM could do."""
-    import ctypes
-    import threading
-
-    import numpy as np
-
-    import ambry_amd
-
-    lib = ambry_amd.lib()
-    base = host.ctypes.data
-    offs, lens = [int(o) for o in off], [int(x) for x in ln]
-    got = np.array([lib.ambrycrc_update(0, base + o, n) for o, n in zip(offs, lens)], dtype=np.uint32)
-    ok = bool(np.array_equal(got, np.asarray(expect, dtype=np.uint32)))
-
-    def run(th):
-        passes = [0] * th
-        stop = time.perf_counter() + seconds
-
-        def worker(t):
-            idx = list(range(t, len(offs), th))
-            while True:
-                for i in idx:
-                    lib.ambrycrc_update(0, ctypes.c_void_p(base + offs[i]), lens[i])
-                passes[t] += 1
-                if time.perf_counter() >= stop:
-                    break
-
-        t0 = time.perf_counter()
-        ws = [threading.Thread(target=worker, args=(t,)) for t in range(th)]
-        for w in ws:
-            w.start()
-        for w in ws:
-            w.join()
-        el = time.perf_counter() - t0
-        return sum(passes[t] * sum(lens[t::th]) for t in range(th)) / el / 2**30
-
-    return {"impl": lib.ambrycrc_host_impl().decode(), "single_thread_gibs": round(run(1), 3),
-            "gibs": round(run(threads), 3), "cores": threads, "parity_vs_port": ok,
-            "what": "libambrycrc ambrycrc_update on the host (CLMUL fold; HotSpot-intrinsic class), same sample"}
-
+# ------------------------------------------------------------------ probes
 
 def measure_read_roof(torch, D, buf, total, device):
     """Read-only probe (ambrycrc_debug_readbw_dev variant 1: the sweep kernel's grid and access
@@ -253,6 +286,93 @@ def host_path_rate(torch, args):
                       "pageable = malloc'd source staged by the library's copy threads"}
 
 
+def traffic_for(config):
+    """rocprofv3 PMC traffic per sweep launch for this config, if one was collected (bench_data/)."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            p = json.load(f).get(config)
+    except (OSError, ValueError):
+        return None, None
+    if not p:
+        return None, None
+    return p.get("hbm_bytes_per_launch"), p.get("source")
+
+
+# ------------------------------------------------------------------ C1 (CPU, one message)
+
+def run_c1(args, result_fd):
+    """BASELINE configs[0]: one 64 KiB-blob PUT message (V3 header, MockId("id1") key, BlobProperties,
+    1000 B user metadata, blob record) through the messageformat CRCs on the CPU. The product path
+    is libambrycrc's host entries (ambrycrc_update per record; the blob record's CRC derived from the
+    blob's with ambrycrc_put_crcs, PutMessageFormatInputStream.java:116-120); the oracle's
+    Crc32.java restatement is timed beside it. Both are checked against the committed fixture
+    (tests/golden/c1_message.json)."""
+    import ctypes
+
+    import numpy as np
+
+    from ambry_amd import lib
+    from c1_message import c1_message_bytes, c1_record_ranges
+    from conftest import Oracle
+
+    with open(os.path.join(ROOT, "tests", "golden", "c1_message.json")) as f:
+        fx = json.load(f)
+    msg = c1_message_bytes()
+    ranges = c1_record_ranges(msg)
+    L = lib()
+    arr = np.frombuffer(msg, dtype=np.uint8)
+    base = arr.ctypes.data
+    bl0, bl1 = ranges[-1]  # blob record: 13-B prefix + content
+    content_off, content_len = bl0 + 13, bl1 - bl0 - 13
+    pre = (ctypes.c_void_p * 1)(base + bl0)
+    pre_len = (ctypes.c_uint64 * 1)(13)
+    blen = (ctypes.c_uint64 * 1)(content_len)
+    bcrc = (ctypes.c_uint32 * 1)()
+    rec = (ctypes.c_uint32 * 1)()
+
+    def product():
+        crcs = [L.ambrycrc_update(0, base + a, b - a) for a, b in ranges[:-1]]
+        bcrc[0] = L.ambrycrc_update(0, base + content_off, content_len)
+        L.ambrycrc_put_crcs(None, None, pre, pre_len, bcrc, blen, 1, None, rec)
+        return crcs + [rec[0]]
+
+    orc = Oracle()
+
+    def oracle():
+        return [orc.crc32(arr[a:b]) for a, b in ranges]
+
+    expect = [int(x, 16) for x in fx["record_crcs"]]
+    ok_p, ok_o = product() == expect, oracle() == expect
+    reps = 20000
+    res = {}
+    for name, fn in (("product", product), ("oracle", oracle)):
+        fn()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        res[name] = (time.perf_counter() - t0) / reps * 1e6
+    crc_bytes = sum(b - a for a, b in ranges)
+    result = {
+        "metric": "us per 64 KiB PUT message, messageformat record CRCs on the CPU (C1)",
+        "value": round(res["product"], 3), "unit": "us", "n_gpus": 0, "steps": reps, "warmup": 1,
+        "ms_per_step": round(res["product"] / 1e3, 6), "higher_is_better": False, "scaling": "none",
+        "vs_baseline": None, "dtype": "u8", "data": "synthetic (splitmix64 bytes; the fixture's message)",
+        "config": {"workload": "C1: single 64 KiB blob PUT through messageformat on CPU",
+                   "message_bytes": len(msg), "crc_bytes": crc_bytes, "records": fx["records"]},
+        "product": {"us_per_message": round(res["product"], 3), "gibs": round(crc_bytes / res["product"] * 1e6 / 2**30, 2),
+                    "impl": L.ambrycrc_host_impl().decode(), "matches_fixture": ok_p,
+                    "what": "ambrycrc_update per record + ambrycrc_put_crcs for the blob record, one core"},
+        "cpu_baseline": {"value": round(res["oracle"], 3), "unit": "us per message", "cores": 1, "kind": "port",
+                         "matches_fixture": ok_o,
+                         "sample": "the C1 message, 20,000 repetitions; oracle/crc32_ref.c slice-by-8 restating "
+                                   "Crc32.java:55-98 per record"},
+        "note": "both legs pay ~0.3 us of Python->C call overhead per record (5 calls per message)",
+    }
+    os.write(result_fd, (json.dumps(result) + "\n").encode())
+
+
+# ------------------------------------------------------------------ main
+
 def main():
     args = parse()
     # stdout carries exactly one JSON line (rank 0). Native libraries print to fd 1 on their
@@ -261,130 +381,203 @@ def main():
     sys.stdout.flush()
     result_fd = os.dup(1)
     os.dup2(2, 1)
+    if args.config == "c1":
+        return run_c1(args, result_fd)
+    import numpy as np
     import torch
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(args, f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None or args.force_dist:
+        mode = "procs"  # one process per GPU (torchrun)
+        world = int(env_world or "1")
+        rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        if world != args.gpus:
+            log(args, f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+        devices = [local]
+    elif args.gpus > 1 or args.inproc:
+        mode = "inproc"  # this process drives every GPU
+        world, rank = args.gpus, 0
+        if torch.cuda.device_count() < world:
+            raise SystemExit(f"--gpus {world} but only {torch.cuda.device_count()} devices visible")
+        devices = list(range(world))
+    else:
+        mode, world, rank, devices = "single", 1, 0, [0]
+    config = args.config or ("c3" if world == 1 else "c5")
+    if config == "c4" and mode != "single":
+        raise SystemExit("c4 (verify-on-read) is a one-GPU config")
+
+    from ambry_amd import device as D
+
     dist = None
-    use_dist = world > 1 or args.force_dist
-    if use_dist:
+    if mode == "procs":
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
         os.environ.setdefault("RANK", "0")
         os.environ.setdefault("WORLD_SIZE", "1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", torch.cuda.current_device())
+        # gloo is only the control plane (unique id, barriers, max of the timings); the data path's
+        # collective is the RCCL all-gather inside libambrycrc
+        dist.init_process_group("gloo")
+    torch.cuda.set_device(devices[0])
+    for d in devices:
+        D.init(d)
+        if args.variant is not None:
+            D.set_variant(d, args.variant)
+        if args.grid is not None:
+            D.set_grid(d, args.grid)
+        if args.window is not None:
+            D.set_window(d, args.window)
 
-    from ambry_amd import device as D
+    work = []
+    for i, d in enumerate(devices):
+        dev = torch.device("cuda", d)
+        log(args, f"rank {rank + i}/{world} (device {d}): building workload {config}")
+        with torch.cuda.device(dev):
+            buf, off_t, len_t, n, total, chunk, desc = build_workload(torch, dev, config, rank + i)
+            w = {"dev": dev, "buf": buf, "off": off_t, "len": len_t, "n": n, "total": total,
+                 "stream": torch.cuda.current_stream(dev)}
+            if mode != "single":
+                w["gathered"] = torch.empty(world * n, dtype=torch.int32, device=dev)
+        work.append(w)
+    n, total = work[0]["n"], work[0]["total"]
 
-    D.init(dev.index)
-    if args.variant is not None:
-        D.set_variant(dev.index, args.variant)
-    if args.grid is not None:
-        D.set_grid(dev.index, args.grid)
-    if args.window is not None:
-        D.set_window(dev.index, args.window)
-
-    log(args, f"rank {rank}/{world}: building workload {args.config}")
-    buf, off_t, len_t, n, total, chunk, desc = build_workload(torch, dev, args, rank)
-    gathered = torch.empty(world * n, dtype=torch.int32, device=dev) if use_dist else None
+    comm = None
+    if mode == "procs":
+        uid = [D.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = D.Comm.rank(uid[0], world, rank, devices[0])
+    elif mode == "inproc":
+        comm = D.Comm.all_devices(devices)
+    counts = [n] * world
 
     verify = None
-    if args.config == "c4":
+    if config == "c4":
         # C4 is the verify-on-read path: expected CRCs from a clean pass, then single-bit flips
         # in 1 % of the chunks (seeded); each step recomputes and compares (ambrycrc_verify_dev).
-        import numpy as np
-
-        expected = D.crc32_batch(buf, off_t, len_t).clone()
+        w = work[0]
+        expected = D.crc32_batch(w["buf"], w["off"], w["len"]).clone()
         rng = np.random.default_rng(20261016 + rank)
         bad = np.sort(rng.choice(n, size=n // 100, replace=False))
-        lens_h = len_t.cpu().numpy()
-        offs_h = off_t.cpu().numpy()
+        lens_h = w["len"].cpu().numpy()
+        offs_h = w["off"].cpu().numpy()
         pos = offs_h[bad] + (rng.random(len(bad)) * lens_h[bad]).astype(np.int64)
-        bits = torch.tensor(1 << rng.integers(0, 8, size=len(bad)), dtype=torch.uint8, device=dev)
-        pos_t = torch.tensor(pos, dtype=torch.int64, device=dev)
-        buf[pos_t] ^= bits
+        bits = torch.tensor(1 << rng.integers(0, 8, size=len(bad)), dtype=torch.uint8, device=w["dev"])
+        pos_t = torch.tensor(pos, dtype=torch.int64, device=w["dev"])
+        w["buf"][pos_t] ^= bits
         torch.cuda.synchronize()
-        verify = {"expected": expected, "bad": bad, "out": torch.empty(n, dtype=torch.int32, device=dev),
-                  "mism": torch.empty(n, dtype=torch.uint8, device=dev)}
+        verify = {"expected": expected, "bad": bad, "out": torch.empty(n, dtype=torch.int32, device=w["dev"]),
+                  "mism": torch.empty(n, dtype=torch.uint8, device=w["dev"])}
 
     def step():
-        if verify is not None:
-            out, _, _ = D.crc32_verify(buf, off_t, len_t, verify["expected"], out=verify["out"],
-                                       mismatch=verify["mism"], count=False)
+        if mode == "single":
+            w = work[0]
+            if verify is not None:
+                D.crc32_verify(w["buf"], w["off"], w["len"], verify["expected"], out=verify["out"],
+                               mismatch=verify["mism"], count=False)
+            else:
+                w["out"] = D.crc32_batch(w["buf"], w["off"], w["len"])
+        elif mode == "inproc":
+            D.crc32_batch_multi_dev(comm, [dict(base=w["buf"], off=w["off"], len=w["len"], gathered=w["gathered"],
+                                                stream=w["stream"]) for w in work])
         else:
-            out = D.crc32_batch(buf, off_t, len_t)
-        if use_dist:
-            dist.all_gather_into_tensor(gathered, out)
-        return out
+            w = work[0]
+            D.crc32_batch_gather(comm, w["buf"], w["off"], w["len"], w["gathered"], counts, stream=w["stream"])
+
+    def sync_all():
+        for w in work:
+            torch.cuda.synchronize(w["dev"])
 
     # Clock ramp: the MI355X takes tens of ms of sustained load to reach its steady clocks
     # (a 0.7 ms C2 step measured 13 % slower over the first 20 steps than over 100). Run the
     # step untimed for >= --prewarm-s before the contract's W warmup steps.
     t_pre = time.perf_counter()
     while True:
-        out = step()
-        torch.cuda.synchronize()
+        step()
+        sync_all()
         if time.perf_counter() - t_pre >= args.prewarm_s:
             break
     for _ in range(args.warmup):
-        out = step()
-    torch.cuda.synchronize()
-    D.timing_collect(dev.index)  # drop warmup events
-    D.timing_enable(dev.index, True)
+        step()
+    sync_all()
+    for w in work:
+        D.timing_collect(w["dev"].index)  # drop warmup events
+        D.timing_enable(w["dev"].index, True)
     if dist:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync_all()
     t0 = time.perf_counter()
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
-    ev0.record()
-    for i in range(args.steps):
-        out = step()
-    ev1.record()
-    torch.cuda.synchronize()
+    ev0.record(work[0]["stream"])
+    for _ in range(args.steps):
+        step()
+    ev1.record(work[0]["stream"])
+    sync_all()
     if dist:
         dist.barrier()
     wall = time.perf_counter() - t0
-    D.timing_enable(dev.index, False)
-    kern_each = D.timing_collect_each(dev.index)
+    kern_each = []
+    for w in work:
+        D.timing_enable(w["dev"].index, False)
+        kern_each += D.timing_collect_each(w["dev"].index)
     kern_ms, launches = sum(kern_each), len(kern_each)
     kern_median_ms = float(sorted(kern_each)[len(kern_each) // 2]) if kern_each else None
     ev_ms = ev0.elapsed_time(ev1)
 
     elapsed = wall
     if dist:
-        t = torch.tensor([wall], dtype=torch.float64, device=dev)
+        t = torch.tensor([wall], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    allgather_ok = None
-    if use_dist:  # this rank's CRCs must sit at its slot of the gathered vector
-        allgather_ok = bool(torch.equal(gathered[rank * n:(rank + 1) * n], out))
-        flag = torch.tensor([1 if allgather_ok else 0], dtype=torch.int32, device=dev)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        allgather_ok = bool(flag.item())
-    read_roof = measure_read_roof(torch, D, buf, buf.numel(), dev.index) if args.config != "c4" else None
-    crcs = out.cpu().numpy().view("uint32")
+    rccl = None
+    if mode != "single":
+        # every GPU's gathered vector: its own slot equals its CRCs computed alone (untimed), and in
+        # one process all GPUs hold the same vector
+        ok = True
+        for i, w in enumerate(work):
+            with torch.cuda.device(w["dev"]):
+                mine = D.crc32_batch(w["buf"], w["off"], w["len"])
+                r = rank + i
+                ok = ok and bool(torch.equal(w["gathered"][r * n:(r + 1) * n], mine))
+                w["out"] = mine
+        if mode == "inproc":
+            g0 = work[0]["gathered"].cpu()
+            ok = ok and all(torch.equal(g0, w["gathered"].cpu()) for w in work[1:])
+        if dist:
+            flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            ok = bool(flag.item())
+        rccl = {"ranks": comm.size(), "allgather_ok": ok,
+                "form": ("one process per GPU: ambrycrc_unique_id + ambrycrc_comm_init_rank, "
+                         "ambrycrc_batch_dev_gather" if mode == "procs" else
+                         "one process, N GPUs: ambrycrc_comm_init_all, ambrycrc_batch_dev_multi"),
+                "gathered_crcs_per_gpu": world * n}
+    w0 = work[0]
+    with torch.cuda.device(w0["dev"]):
+        read_roof = measure_read_roof(torch, D, w0["buf"], w0["buf"].numel(), w0["dev"].index) \
+            if config != "c4" else None
     verify_ok = None
     if verify is not None:  # the flags must name exactly the flipped chunks
         flagged = np.nonzero(verify["mism"].cpu().numpy())[0]
-        _, _, cnt = D.crc32_verify(buf, off_t, len_t, verify["expected"])  # the counter form, once, untimed
+        _, _, cnt = D.crc32_verify(w0["buf"], w0["off"], w0["len"], verify["expected"])  # counter form, untimed
         verify_ok = bool(np.array_equal(flagged, verify["bad"]) and int(cnt.item()) == len(verify["bad"]))
-    step_bytes = total  # per rank
-    value = world * step_bytes * args.steps / elapsed / 2**30
+        w0["out"] = verify["out"]
+    crcs = w0["out"].cpu().numpy().view("uint32")
+    value = world * total * args.steps / elapsed / 2**30
     kern_avg_s = kern_ms / max(1, launches) / 1e3
     alg_bytes = total + 4 * n  # chunk bytes read + 4 B CRC written per chunk (offset/len arrays excluded)
     achieved = alg_bytes / kern_avg_s / 1e9 if kern_avg_s > 0 else None
+    traffic, traffic_src = traffic_for(config)
 
+    if mode == "single":
+        parallelism = "shard1"
+    elif mode == "procs":
+        parallelism = f"shard{world}+rccl_allgather (one process per GPU)"
+    else:
+        parallelism = f"shard{world}+rccl_allgather (one process, {world} GPUs)"
     result = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -398,10 +591,10 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (device splitmix64 bytes; no dataset)",
-        "config": {"workload": desc, "chunks_per_gpu": n, "chunk_bytes": chunk, "bytes_per_gpu_step": total,
-                   "parallelism": f"shard{world}" + ("+rccl_allgather" if use_dist else ""),
-                   "kernel_variant": D.get_variant(dev.index),
-                   "grid_workgroups": D.grid_size(dev.index),
+        "config": {"workload": desc, "chunks_per_gpu": n, "chunk_bytes": CONFIGS.get(config, (0, None))[1],
+                   "bytes_per_gpu_step": total, "parallelism": parallelism,
+                   "kernel_variant": D.get_variant(w0["dev"].index),
+                   "grid_workgroups": D.grid_size(w0["dev"].index),
                    "sweep_window_bytes": args.window if args.window is not None else 32 << 30},
         "roofline": {
             "bound": "hbm",
@@ -410,7 +603,9 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_source": traffic_src,
+            "traffic_over_algorithmic": round(traffic / alg_bytes, 5) if traffic else None,
             "kernel_avg_ms": round(kern_avg_s * 1e3, 4),
             "kernel_median_ms": round(kern_median_ms, 4) if kern_median_ms else None,
             "algorithmic_bytes_per_launch": alg_bytes,
@@ -420,38 +615,33 @@ def main():
                                            if achieved and read_roof else None),
         },
         "timing": {"wall_s": round(elapsed, 4), "stream_event_ms": round(ev_ms, 3), "kernel_launches": launches},
-        "allgather_ok": allgather_ok,
+        "allgather_ok": None if rccl is None else rccl["allgather_ok"],
+        "rccl": rccl,
         "verify": (None if verify is None else
                    {"flipped_chunks": int(len(verify["bad"])), "flags_exact": verify_ok,
                     "what": "ambrycrc_verify_dev per step: CRCs recomputed and compared with the clean pass; "
                             "single-bit flips in 1 % of chunks (seeded)"}),
     }
-    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc) and args.config == "c3":
-        try:
-            with open(pmc) as f:
-                p = json.load(f)
-            result["roofline"]["traffic"] = p.get("hbm_bytes_per_launch")
-            result["roofline"]["traffic_source"] = p.get("source")
-        except Exception:
-            pass
 
     if rank == 0 and world == 1:
         if not args.no_cpu_baseline:
             log(args, "cpu baseline")
-            cb = cpu_baseline(buf, off_t, len_t, n, args)
+            cb = cpu_baseline(w0["buf"], w0["off"], w0["len"], n, args)
             if cb is not None:
                 ref = cb.pop("_out")
                 cb["parity_vs_gpu"] = bool((ref == crcs[:len(ref)]).all())
                 result["cpu_baseline"] = cb
-        if not args.no_host_path and args.config == "c3":
+        if not args.no_host_path and config == "c3":
             log(args, "host-resident path")
-            del buf
+            for w in work:
+                del w["buf"]
             torch.cuda.empty_cache()
             result["host_path"] = host_path_rate(torch, args)
     if rank == 0:
         sys.stdout.flush()
         os.write(result_fd, (json.dumps(result) + "\n").encode())
+    if comm is not None:
+        comm.destroy()
     if dist:
         dist.destroy_process_group()
 

@@ -15,6 +15,12 @@ pinned by:
      MessageFormatSendTest.java:621-630 serialized per MessageFormatRecord.java
      :467-486 (V1), :696-725 (V2), :951-981 (V3), and seeded random vectors
      over tests/datagen.py's splitmix stream (seed, offset, length, crc only).
+  3. c1_message.bin + c1_message.json -- BASELINE.json configs[0] (C1): one PUT message with a
+     V3 header (MessageFormatRecord.java:951-981), MockId("id1") key (MockId.java:47-77),
+     BlobProperties VERSION_5 (BlobPropertiesSerDe.java:80-103), 1000 B user metadata and a
+     64 KiB blob record (Blob_Format_V3, :1777-1833), laid out by PutMessageFormatInputStream
+     (:76-124) through oracle/message_format.py; every record CRC from zlib.crc32 (the JDK
+     CRC32's function), with the record byte ranges. Shape of MessageFormatInputStreamTest.java:70-243.
 """
 from __future__ import annotations
 
@@ -98,7 +104,47 @@ def vectors():
             "known_answers": kat, "zero_runs": zero_runs, "message_headers": headers, "random": rnd}
 
 
+C1_SEED = 0xA3B1C2D3
+
+
+def c1_message():
+    """(message bytes, fixture dict) for config C1."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location(
+        "message_format", os.path.join(os.path.dirname(os.path.dirname(HERE)), "oracle", "message_format.py"))
+    mf = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mf)
+    content = stream_bytes(C1_SEED, 0, 64 << 10).tobytes()
+    usermeta = stream_bytes(C1_SEED, 1 << 20, 1000).tobytes()
+    key = mf.store_key("id1")
+    msg = mf.put_message(key, mf.blob_properties_bytes(len(content)), usermeta, content, version=3)
+    version, total, rel = mf.parse_header(msg, 0)
+    starts = [r for r in rel if r != -1]
+    ends = starts[1:] + [starts[0] + total]
+    ranges = [(0, mf.HEADER_SIZE[version] - 8)] + [(a, e - 8) for a, e in zip(starts, ends)]
+    crcs = [zlib.crc32(msg[a:b]) for a, b in ranges]
+    for (a, b), c in zip(ranges, crcs):  # the stored trailer of every record is that CRC
+        assert struct.unpack(">q", msg[b:b + 8])[0] == c
+    fx = {"generator": "tests/golden/make_golden.py (zlib %s)" % zlib.ZLIB_RUNTIME_VERSION,
+          "what": "C1: one 64 KiB-blob PUT message, V3 header, MockId(\"id1\") key, BlobProperties V5, "
+                  "1000 B user metadata, Blob_Format_V3 record",
+          "seed": f"0x{C1_SEED:x}", "content": "datagen.stream_bytes(seed, 0, 65536)",
+          "user_metadata": "datagen.stream_bytes(seed, 1 << 20, 1000)",
+          "message_bytes": len(msg), "sha256": hashlib.sha256(msg).hexdigest(),
+          "records": ["header", "blob_properties", "user_metadata", "blob"],
+          "record_ranges": [[a, b] for a, b in ranges],
+          "record_crcs": [f"0x{c:08x}" for c in crcs],
+          "blob_prefix_bytes": 13, "key_offset": mf.HEADER_SIZE[version], "key_bytes": len(key)}
+    return msg, fx
+
+
 def main():
+    msg, fx = c1_message()
+    with open(os.path.join(HERE, "c1_message.bin"), "wb") as f:
+        f.write(msg)
+    with open(os.path.join(HERE, "c1_message.json"), "w") as f:
+        json.dump(fx, f, indent=1)
     fp = table_fingerprint()
     if fp is not None:
         with open(os.path.join(HERE, "crc32_table_fingerprint.json"), "w") as f:

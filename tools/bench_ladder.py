@@ -186,7 +186,7 @@ def main():
     ap.add_argument("--reps", type=int, default=7)
     ap.add_argument("--no-gpu", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--variants", default="17", help="sweep variants (>= 100: timing diagnostics, no parity)")
+    ap.add_argument("--variants", default="29", help="sweep variants (0 or 29; 100-102 only in a -DAMBRYCRC_DIAGNOSTICS build)")
     ap.add_argument("--sizes", default=None, help="subset of the ladder, comma separated bytes")
     args = ap.parse_args()
     if not args.no_gpu:

@@ -158,7 +158,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--no-gpu", action="store_true")
-    ap.add_argument("--variants", default="0")
+    ap.add_argument("--variants", default="29")
     ap.add_argument("--cases", default="64k,4m,4k", help="subset of 64k,4m,4k")
     ap.add_argument("--host", action="store_true", help="also time the host-region path (regions <= 5 GiB)")
     args = ap.parse_args()

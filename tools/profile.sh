@@ -5,8 +5,8 @@
 #   prof_write  --pmc WRITE_SIZE            HBM write KiB
 #   prof_sq     --pmc SQ_* GRBM_GUI_ACTIVE  LDS / VALU issue and bank conflicts
 # Each counter set in its own pass, no trace domains combined with --pmc. Then
-#   python tools/summarize_profile.py --tag <round tag>
-# copies the summaries into profiles/.
+#   python tools/summarize_profile.py --tag <round tag> --config <c3|c2|c5>
+# copies the summaries into profiles/ and the traffic into bench_data/pmc_traffic.json.
 set -euo pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out

@@ -3,7 +3,8 @@
 
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (as emitted)
   profiles/<tag>_pmc_summary.json   per-dispatch averages of every PMC counter for the sweep kernel
-  profiles/pmc_traffic.json         HBM bytes per sweep-kernel launch, read by bench.py as roofline.traffic
+  bench_data/pmc_traffic.json       HBM bytes per sweep-kernel launch per config, read by bench.py as
+                                    roofline.traffic (bench_data/ travels to the GPU box; profiles/ does not)
 
 Traffic correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE and WRITE_SIZE are in KiB;
 on gfx950 FETCH_SIZE reads exactly half the bytes of a wide coalesced stream, so
@@ -46,8 +47,13 @@ def main():
     ap.add_argument("--src", default=os.path.join(ROOT, "gpurun_out"))
     ap.add_argument("--tag", required=True)
     ap.add_argument("--kernel", default="crc32_sweep_kernel")
-    ap.add_argument("--alg-bytes", type=int, default=8192 * (4 << 20) + 4 * 8192)
+    ap.add_argument("--config", default="c3", help="bench.py config the PMC passes ran (key in pmc_traffic.json)")
+    ap.add_argument("--alg-bytes", type=int, default=None,
+                    help="algorithmic bytes per launch (default: from --config: chunk bytes + 4 B per chunk)")
     args = ap.parse_args()
+    if args.alg_bytes is None:
+        n, chunk = {"c3": (8192, 4 << 20), "c2": (65536, 64 << 10), "c5": (65536, 4 << 20)}[args.config]
+        args.alg_bytes = n * chunk + 4 * n
     out = os.path.join(ROOT, "profiles")
     os.makedirs(out, exist_ok=True)
     shutil.copy(os.path.join(args.src, "prof_kt", "kt_kernel_stats.csv"),
@@ -81,11 +87,16 @@ def main():
         summary["hbm_bytes_per_launch"] = hbm
         summary["algorithmic_bytes_per_launch"] = args.alg_bytes
         summary["traffic_over_algorithmic"] = hbm / args.alg_bytes
-        with open(os.path.join(out, "pmc_traffic.json"), "w") as f:
-            json.dump({"hbm_bytes_per_launch": round(hbm),
-                       "source": f"profiles/{args.tag}_pmc_summary.json: (2*FETCH_SIZE + WRITE_SIZE) KiB, "
-                                 "separate rocprofv3 --pmc passes of bench.py (C3)",
-                       "kernel": args.kernel}, f, indent=1)
+        tf = os.path.join(ROOT, "bench_data", "pmc_traffic.json")
+        os.makedirs(os.path.dirname(tf), exist_ok=True)
+        table = json.load(open(tf)) if os.path.exists(tf) else {}
+        table[args.config] = {"hbm_bytes_per_launch": round(hbm), "algorithmic_bytes_per_launch": args.alg_bytes,
+                              "traffic_over_algorithmic": round(hbm / args.alg_bytes, 6),
+                              "source": f"profiles/{args.tag}_pmc_summary.json: (2*FETCH_SIZE + WRITE_SIZE) KiB, "
+                                        f"separate rocprofv3 --pmc passes of bench.py --config {args.config}",
+                              "kernel": args.kernel}
+        with open(tf, "w") as f:
+            json.dump(table, f, indent=1)
     if "GRBM_GUI_ACTIVE" in counters and "kernel_trace" in summary:
         summary["effective_clock_ghz_est"] = counters["GRBM_GUI_ACTIVE"] / 8 / (summary["kernel_trace"]["avg_ns"])
     with open(os.path.join(out, f"{args.tag}_pmc_summary.json"), "w") as f:

@@ -4,7 +4,7 @@
 Interleaved rounds (cdna_hip_programming.md §5.4 rule 24): every configuration is
 timed once per round, R rounds, and the median/min per configuration reported.
 Times are HIP-event kernel durations (ambrycrc timing hook) and stream wall time.
-Usage: python tools/sweep.py [--config c3|c2|c4] [--rounds 5] [--variants 0,1,...] [--grids 0,512]
+Usage: python tools/sweep.py [--config c3|c2|c4] [--rounds 5] [--variants 0,29] [--grids 0,512]
 """
 from __future__ import annotations
 
@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=3, help="launches per measurement")
-    ap.add_argument("--variants", default="0,1,2,3,4,5,6,7")
+    ap.add_argument("--variants", default="0,29")
     ap.add_argument("--grids", default="0")
     ap.add_argument("--readbw", action="store_true")
     ap.add_argument("--out", default=None)
