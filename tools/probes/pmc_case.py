@@ -1,0 +1,89 @@
+#!/usr/bin/env python3
+"""One small-record workload, launched `--reps` times back to back, for rocprofv3 passes
+(tools/pmc_cases.sh). Every case checks its first result against zlib, then repeats the call
+untimed; the profiler's per-dispatch counters are the measurement.
+
+  batch100   chunks of 100 B at 112-B stride (16-B aligned starts), 0.5 GiB   -- group class 0
+  batch1k    1 KiB chunks, aligned, 0.5 GiB                                     -- group class 1
+  batch4k    4 KiB chunks, aligned, 0.5 GiB                                     -- group class 2
+  batch4109  4109-B chunks at 16-B offsets (the blob records of 4 KiB PUTs)     -- group class 3
+  msg4k      ambrycrc_verify_messages_dev over 262,144 x PUT(4 KiB blob), 1.29 GiB
+  single100  one 100 B chunk per ambrycrc_batch_dev call
+  single4m   one 4 MiB chunk per ambrycrc_batch_dev call
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import zlib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+SIZES = {"batch100": (100, 112), "batch1k": (1024, 1024), "batch4k": (4096, 4096), "batch4109": (4109, 4112)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("case")
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--gib", type=float, default=0.5)
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+
+    from ambry_amd import device as D
+
+    torch.cuda.set_device(0)
+    D.init(0)
+    info = {"case": args.case}
+    if args.case in SIZES:
+        size, stride = SIZES[args.case]
+        n = int(args.gib * 2**30) // stride
+        buf = torch.empty(n * stride, dtype=torch.uint8, device="cuda")
+        D.fill_random(buf, 0xA1 + size, 0)
+        off = torch.arange(n, dtype=torch.int64, device="cuda") * stride
+        ln = torch.full((n,), size, dtype=torch.int64, device="cuda")
+        out = torch.empty(n, dtype=torch.int32, device="cuda")
+        ws = torch.empty(D.workspace_bytes(n), dtype=torch.uint8, device="cuda")
+        D.crc32_batch(buf, off, ln, out=out, workspace=ws)
+        torch.cuda.synchronize()
+        idx = [0, n // 2, n - 1]
+        host = buf.view(n, stride)[idx, :size].cpu().numpy()
+        assert [zlib.crc32(h.tobytes()) for h in host] == list(out[idx].cpu().numpy().view(np.uint32))
+        for _ in range(args.reps):
+            D.crc32_batch(buf, off, ln, out=out, workspace=ws)
+        info.update(chunks=n, chunk_bytes=size, alg_bytes_per_launch=n * size + 4 * n)
+    elif args.case in ("single100", "single4m"):
+        size = 100 if args.case == "single100" else 4 << 20
+        buf = torch.empty(size + 64, dtype=torch.uint8, device="cuda")
+        D.fill_random(buf, 7, 0)
+        off = torch.zeros(1, dtype=torch.int64, device="cuda")
+        ln = torch.full((1,), size, dtype=torch.int64, device="cuda")
+        out = torch.empty(1, dtype=torch.int32, device="cuda")
+        ws = torch.empty(D.workspace_bytes(1), dtype=torch.uint8, device="cuda")
+        D.crc32_batch(buf, off, ln, out=out, workspace=ws)
+        torch.cuda.synchronize()
+        assert zlib.crc32(buf[:size].cpu().numpy().tobytes()) == int(out.cpu().numpy().view(np.uint32)[0])
+        for _ in range(args.reps):
+            D.crc32_batch(buf, off, ln, out=out, workspace=ws)
+        info.update(chunks=1, chunk_bytes=size, alg_bytes_per_launch=size + 4)
+    elif args.case == "msg4k":
+        from bench_messages import gpu_region, load_mf
+
+        res = gpu_region(load_mf(), 262144, 4 << 10, args.reps)
+        info.update(res)
+        # CRC'd bytes per message: header 32 + props + usermeta 1006 + blob record 4109 (+ stored CRCs read)
+        info["alg_bytes_per_launch"] = res["region_bytes"]
+    else:
+        raise SystemExit(f"unknown case {args.case}")
+    torch.cuda.synchronize()
+    print(json.dumps(info), flush=True)
+
+
+if __name__ == "__main__":
+    main()
