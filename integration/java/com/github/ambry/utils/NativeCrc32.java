@@ -1,0 +1,152 @@
+/*
+ * NativeCrc32 -- drop-in java.util.zip.Checksum backed by libambrycrc (MI355X / gfx950 CRC-32
+ * engine), for ambry-utils. Bit-exact with com.github.ambry.utils.Crc32 and java.util.zip.CRC32
+ * (CRC-32/ISO-HDLC).
+ *
+ * Binding: libambrycrc_jni.so (ambry_amd/jni/ambrycrc_jni.c), which links libambrycrc.so and
+ * libambrycrc_jnicore.so. Native failures are thrown by the shim as exceptions
+ * (IndexOutOfBoundsException, IllegalArgumentException, NullPointerException,
+ * OutOfMemoryError, IllegalStateException); a CRC value is never a status code.
+ *
+ * Replaces: Crc32 (ambry-utils/.../utils/Crc32.java:34-149), and -- with
+ * ambry-utils-checksum-retype.patch applied -- the CRC32 instances of CrcInputStream
+ * (CrcInputStream.java:28,40) and CrcOutputStream (CrcOutputStream.java:25,36).
+ */
+package com.github.ambry.utils;
+
+import java.nio.ByteBuffer;
+import java.util.zip.Checksum;
+
+
+public final class NativeCrc32 implements Checksum {
+  static {
+    System.loadLibrary("ambrycrc_jni");
+  }
+
+  /** Finalized value (zlib convention, starts at 0); Crc32.java keeps the inverted register. */
+  private int crc;
+
+  /** Crc32.update(int), Crc32.java:146-148: the low 8 bits of b. */
+  @Override
+  public void update(int b) {
+    crc = nativeUpdateByte(crc, b);
+  }
+
+  /** Crc32.update(byte[], int, int), Crc32.java:55-98. Bounds as java.util.zip.CRC32. */
+  @Override
+  public void update(byte[] b, int off, int len) {
+    if (b == null) {
+      throw new NullPointerException();
+    }
+    if (off < 0 || len < 0 || off > b.length - len) {
+      throw new ArrayIndexOutOfBoundsException();
+    }
+    crc = nativeUpdateArray(crc, b, off, len);
+  }
+
+  /** Crc32.update(ByteBuffer), Crc32.java:100-143: consumes position..limit. */
+  @Override
+  public void update(ByteBuffer buffer) {
+    int pos = buffer.position();
+    int len = buffer.remaining();
+    if (len == 0) {
+      return;
+    }
+    if (buffer.isDirect()) {
+      crc = nativeUpdateDirect(crc, buffer, pos, len);
+    } else if (buffer.hasArray()) {
+      crc = nativeUpdateArray(crc, buffer.array(), buffer.arrayOffset() + pos, len);
+    } else {  // read-only heap buffer: copy out
+      byte[] tmp = new byte[len];
+      buffer.duplicate().get(tmp);
+      crc = nativeUpdateArray(crc, tmp, 0, len);
+    }
+    buffer.position(buffer.limit());
+  }
+
+  /** update(ByteBuffer) over a gather list, e.g. PutChunk.verifyCRC's nioBuffers() (PutOperation.java:2041-2043). */
+  public void updateAll(ByteBuffer[] buffers) {
+    boolean allDirect = true;
+    for (ByteBuffer b : buffers) {
+      allDirect &= b.isDirect();
+    }
+    if (!allDirect) {
+      for (ByteBuffer b : buffers) {
+        update(b);
+      }
+      return;
+    }
+    crc = nativeUpdateDirectAll(crc, buffers);  // one JNI crossing
+    for (ByteBuffer b : buffers) {
+      b.position(b.limit());
+    }
+  }
+
+  /** Crc32.getValue(), Crc32.java:44-47. */
+  @Override
+  public long getValue() {
+    return crc & 0xffffffffL;
+  }
+
+  /** Crc32.reset(), Crc32.java:49-52. */
+  @Override
+  public void reset() {
+    crc = 0;
+  }
+
+  /** CRC of A||B from crc(A), crc(B) and |B| (zlib crc32_combine). */
+  public static long combine(long crc1, long crc2, long len2) {
+    return nativeCombine((int) crc1, (int) crc2, len2) & 0xffffffffL;
+  }
+
+  /** Create the device context of GPU `device` (ambrycrc_init). Idempotent. */
+  public static void init(int device) {
+    nativeInit(device);
+  }
+
+  /**
+   * CRCs of many direct-buffer chunks on GPU `device` (ambrycrc_batch_host: pinned staging, PCIe
+   * copy, gfx950 kernels): out[i] = crc32(crcIn == null ? 0 : crcIn[i], bufs[i][pos[i], pos[i] + len[i])).
+   */
+  public static void batch(ByteBuffer[] bufs, int[] pos, int[] len, int[] crcIn, int[] out, int device) {
+    nativeBatchDirect(bufs, pos, len, crcIn, out, device);
+  }
+
+  /**
+   * Verify every CRC of the messages at `offsets` in a log-segment region held in a direct buffer
+   * (BlobStoreRecovery scan, GET, replication): status[i] = 0 when every CRC matches, else
+   * AMBRYCRC_MSG_* bits (the lowest set bit is the record deserializeBlobAll would throw on);
+   * ends[i] (may be null) = end offset of message i, 0 when its layout is invalid.
+   */
+  public static void verifyMessages(ByteBuffer region, long[] offsets, int[] status, long[] ends, int device) {
+    nativeVerifyMessages(region, offsets, status, ends, device);
+  }
+
+  /** AMBRYCRC_MSG_* status bits of verifyMessages (include/ambrycrc.h). */
+  public static final int MSG_HEADER_CRC = 1;
+  public static final int MSG_ENCKEY_CRC = 1 << 1;
+  public static final int MSG_PROPS_CRC = 1 << 2;
+  public static final int MSG_UPDATE_CRC = 1 << 3;
+  public static final int MSG_USERMETA_CRC = 1 << 4;
+  public static final int MSG_BLOB_CRC = 1 << 5;
+  public static final int MSG_BAD_VERSION = 1 << 8;
+  public static final int MSG_BAD_LAYOUT = 1 << 9;
+
+  private static native void nativeInit(int device);
+
+  private static native int nativeUpdateArray(int crc, byte[] b, int off, int len);
+
+  private static native int nativeUpdateDirect(int crc, ByteBuffer buf, int pos, int len);
+
+  private static native int nativeUpdateByte(int crc, int b);
+
+  private static native int nativeUpdateDirectAll(int crc, ByteBuffer[] bufs);
+
+  private static native int nativeCombine(int crc1, int crc2, long len2);
+
+  private static native void nativeBatchDirect(ByteBuffer[] bufs, int[] pos, int[] len, int[] crcIn, int[] out,
+      int device);
+
+  private static native void nativeVerifyMessages(ByteBuffer region, long[] offsets, int[] status, long[] ends,
+      int device);
+}

@@ -1,0 +1,120 @@
+"""The JNI shim's argument checks and marshalling (ambry_amd/jni/ambrycrc_jni_core.c), driven
+through ctypes: no JDK exists in this image, so ambrycrc_jni.c keeps only the JNI calls and every
+decision it makes is made by these functions. Bounds follow java.util.zip.CRC32.update(byte[],
+off, len) (ArrayIndexOutOfBoundsException unless 0 <= off, 0 <= len, off + len <= length) and
+Crc32.update(ByteBuffer) (position..limit, Crc32.java:100-143). Errors never come back in the
+CRC slot."""
+import ctypes
+import os
+import zlib
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CORE = os.path.join(ROOT, "ambry_amd", "libambrycrc_jnicore.so")
+
+AJC_OK, AJC_EBOUNDS, AJC_ENOTDIRECT, AJC_ESHORT, AJC_ENULL = 0, -100, -101, -102, -103
+
+
+@pytest.fixture(scope="module")
+def core(ambry):
+    if not os.path.exists(CORE):
+        import subprocess
+
+        subprocess.run(["make", "-C", os.path.join(ROOT, "ambry_amd")], check=True, capture_output=True)
+    L = ctypes.CDLL(CORE)
+    i64, i32, u32 = ctypes.c_int64, ctypes.c_int32, ctypes.c_uint32
+    L.ajc_range_ok.argtypes = [i64, i64, i64]
+    L.ajc_update.argtypes = [u32, ctypes.c_void_p, i64, i64, i64, ctypes.POINTER(u32)]
+    L.ajc_exception_class.restype = ctypes.c_char_p
+    L.ajc_message.restype = ctypes.c_char_p
+    L.ajc_batch_args.argtypes = [ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(i64),
+                                 ctypes.POINTER(i32), ctypes.POINTER(i32), ctypes.POINTER(ctypes.c_void_p),
+                                 ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_size_t)]
+    L.ajc_iov_args.argtypes = [ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(i64),
+                               ctypes.POINTER(i32), ctypes.POINTER(i32), ctypes.POINTER(ctypes.c_void_p),
+                               ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)]
+    L.ajc_batch_lengths.argtypes = [i64] * 5
+    L.ajc_verify_lengths.argtypes = [i64] * 3
+    return L
+
+
+def test_range_checks_follow_java(core):
+    ok = core.ajc_range_ok
+    assert ok(10, 0, 10) and ok(10, 10, 0) and ok(0, 0, 0) and ok(10, 3, 7)
+    for cap, off, ln in ((10, 0, 11), (10, -1, 1), (10, 1, -1), (10, 11, 0), (-1, 0, 0),
+                         (2**31 - 1, 2**31 - 1, 2**31 - 1), (100, 2**62, 2**62)):
+        assert not ok(cap, off, ln), (cap, off, ln)
+
+
+def test_update_reports_out_of_band(core):
+    data = np.frombuffer(os.urandom(1000), dtype=np.uint8)
+    out = ctypes.c_uint32(0xDEAD)
+    assert core.ajc_update(0, data.ctypes.data, 1000, 10, 500, ctypes.byref(out)) == AJC_OK
+    assert out.value == zlib.crc32(data[10:510].tobytes())
+    out.value = 0x1234
+    # a bad range is a status; the CRC slot keeps its value (never a status code)
+    assert core.ajc_update(7, data.ctypes.data, 1000, 900, 101, ctypes.byref(out)) == AJC_EBOUNDS
+    assert out.value == 0x1234
+    assert core.ajc_update(7, None, 0, 0, 0, ctypes.byref(out)) == AJC_OK and out.value == 7
+    assert core.ajc_update(7, None, 5, 0, 5, ctypes.byref(out)) == AJC_ENULL
+    # 0xFFFFFFFF is a legitimate CRC and comes back as a value
+    assert core.ajc_update(0xFFFFFFFF, data.ctypes.data, 1000, 0, 0, ctypes.byref(out)) == AJC_OK
+    assert out.value == 0xFFFFFFFF
+
+
+def test_batch_and_iov_marshalling(core):
+    bufs = [np.frombuffer(os.urandom(n), dtype=np.uint8) for n in (100, 4096, 1)]
+    n = len(bufs)
+    bases = (ctypes.c_void_p * n)(*[b.ctypes.data for b in bufs])
+    caps = (ctypes.c_int64 * n)(*[b.nbytes for b in bufs])
+    ptrs = (ctypes.c_void_p * n)()
+    lens = (ctypes.c_uint64 * n)()
+    bad = ctypes.c_size_t(99)
+    pos = (ctypes.c_int32 * n)(0, 96, 1)
+    ln = (ctypes.c_int32 * n)(100, 4000, 0)
+    assert core.ajc_batch_args(n, bases, caps, pos, ln, ptrs, lens, ctypes.byref(bad)) == AJC_OK
+    assert [ptrs[i] for i in range(n)] == [bufs[0].ctypes.data, bufs[1].ctypes.data + 96, bufs[2].ctypes.data + 1]
+    assert list(lens) == [100, 4000, 0]
+    ln[1] = 4001  # one byte past the capacity of buffer 1
+    assert core.ajc_batch_args(n, bases, caps, pos, ln, ptrs, lens, ctypes.byref(bad)) == AJC_EBOUNDS
+    assert bad.value == 1
+    ln[1] = 4000
+    bases[2] = None  # a heap buffer (no native address)
+    assert core.ajc_batch_args(n, bases, caps, pos, ln, ptrs, lens, ctypes.byref(bad)) == AJC_ENOTDIRECT
+    assert bad.value == 2
+    bases[2] = bufs[2].ctypes.data
+    szs = (ctypes.c_size_t * n)()
+    lim = (ctypes.c_int32 * n)(100, 4096, 1)
+    assert core.ajc_iov_args(n, bases, caps, pos, lim, ptrs, szs, ctypes.byref(bad)) == AJC_OK
+    assert list(szs) == [100, 4000, 0]
+    lim[0] = -1  # limit below position
+    assert core.ajc_iov_args(n, bases, caps, pos, lim, ptrs, szs, ctypes.byref(bad)) == AJC_EBOUNDS
+    lim[0] = 101  # limit past capacity
+    assert core.ajc_iov_args(n, bases, caps, pos, lim, ptrs, szs, ctypes.byref(bad)) == AJC_EBOUNDS
+    assert bad.value == 0
+
+
+def test_array_length_checks(core):
+    assert core.ajc_batch_lengths(3, 3, 3, -1, 3) == AJC_OK
+    assert core.ajc_batch_lengths(3, 3, 3, 3, 4) == AJC_OK
+    assert core.ajc_batch_lengths(3, 2, 3, -1, 3) == AJC_ESHORT
+    assert core.ajc_batch_lengths(3, 3, 3, 2, 3) == AJC_ESHORT
+    assert core.ajc_batch_lengths(3, 3, 3, 3, 2) == AJC_ESHORT
+    assert core.ajc_verify_lengths(5, 5, -1) == AJC_OK
+    assert core.ajc_verify_lengths(5, 4, -1) == AJC_ESHORT
+    assert core.ajc_verify_lengths(5, 5, 4) == AJC_ESHORT
+
+
+def test_exception_mapping(core):
+    cls = lambda s: core.ajc_exception_class(s)  # noqa: E731
+    assert cls(AJC_OK) is None
+    assert cls(AJC_EBOUNDS) == b"java/lang/IndexOutOfBoundsException"
+    assert cls(AJC_ENOTDIRECT) == b"java/lang/IllegalArgumentException"
+    assert cls(AJC_ENULL) == b"java/lang/NullPointerException"
+    assert cls(-1) == b"java/lang/IllegalArgumentException"
+    assert cls(-3) == b"java/lang/OutOfMemoryError"
+    for code in (-2, -4, -5, -6):
+        assert cls(code) == b"java/lang/IllegalStateException"
+    assert core.ajc_message(-4).decode().startswith("ambrycrc_init")
