@@ -30,6 +30,18 @@ class Shard(ctypes.Structure):
                 ("d_gathered", ctypes.c_void_p), ("stream", ctypes.c_void_p)]
 
 
+class PutDesc(ctypes.Structure):
+    """struct ambrycrc_put_desc (include/ambrycrc.h): one PUT message to serialize (80 bytes)."""
+    _fields_ = [("out_off", ctypes.c_uint64), ("key_src", ctypes.c_uint64), ("enckey_src", ctypes.c_uint64),
+                ("props_src", ctypes.c_uint64), ("usermeta_src", ctypes.c_uint64), ("blob_src", ctypes.c_uint64),
+                ("blob_len", ctypes.c_uint64), ("key_len", ctypes.c_uint32), ("enckey_len", ctypes.c_int32),
+                ("props_len", ctypes.c_uint32), ("usermeta_len", ctypes.c_uint32), ("life_version", ctypes.c_int16),
+                ("blob_type", ctypes.c_int16), ("compressed", ctypes.c_uint8), ("header_version", ctypes.c_uint8),
+                ("reserved", ctypes.c_uint8 * 2)]
+
+
+assert ctypes.sizeof(PutDesc) == 80
+
 # (name, restype, argtypes) for every symbol include/ambrycrc.h declares.
 _u8p = ctypes.c_void_p
 _SIGNATURES = [
@@ -56,6 +68,13 @@ _SIGNATURES = [
     ("ambrycrc_verify_messages_host", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t,
       ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint64), ctypes.c_int, ctypes.c_int]),
+    ("ambrycrc_put_layout", ctypes.c_uint64, [ctypes.POINTER(PutDesc), ctypes.POINTER(ctypes.c_uint64)]),
+    ("ambrycrc_serialize_put_host", ctypes.c_int,
+     [ctypes.POINTER(PutDesc), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+      ctypes.POINTER(ctypes.c_uint32)]),
+    ("ambrycrc_serialize_puts_workspace_bytes", ctypes.c_size_t, [ctypes.c_size_t]),
+    ("ambrycrc_serialize_puts_dev", ctypes.c_int,
+     [_u8p, ctypes.c_size_t, _u8p, _u8p, _u8p, _u8p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
     ("ambrycrc_trailed_workspace_bytes", ctypes.c_size_t, [ctypes.c_size_t]),
     ("ambrycrc_verify_trailed_dev", ctypes.c_int,
      [_u8p, _u8p, _u8p, _u8p, _u8p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),

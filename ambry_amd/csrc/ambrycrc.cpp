@@ -20,9 +20,11 @@
 #include "crc32_gf2.h"
 #include "crc32_kernels.h"
 #include "crc32_layout.h"
+#include "ambrycrc_ctx.h"
 #include "host_crc.h"
 
 using namespace ambrycrc;
+using namespace ambrycrc::detail;
 
 namespace {
 
@@ -75,82 +77,10 @@ std::vector<uint32_t> build_table_image() {
   return img;
 }
 
-// ------------------------------------------------------------ contexts
-constexpr int kMaxDevices = 64;
-// Host path: a ring of kSlabs staging slabs per device. Up to kSlabs-1 slabs are in
-// flight (H2D copy, kernels, D2H of CRCs on the slab's stream) while the host fills
-// the next one; 64 MiB keeps the pipeline's fill and drain short (1.2 ms at PCIe rate).
-constexpr int kSlabs = 4;
-constexpr size_t kSlabBytes = 64ull << 20;    // host-path staging slab
-constexpr size_t kSlabChunks = 1u << 14;      // max chunk pieces per slab
+}  // namespace
 
-struct EventPair {
-  hipEvent_t a, b;
-};
-
-struct HostSlab {
-  uint8_t* h_data = nullptr;   // pinned
-  uint64_t* h_meta = nullptr;  // pinned: off[kSlabChunks], len[kSlabChunks]
-  uint32_t* h_out = nullptr;   // pinned
-  uint8_t* d_data = nullptr;
-  uint64_t* d_meta = nullptr;
-  uint32_t* d_out = nullptr;
-  void* d_ws = nullptr;
-  hipStream_t stream = nullptr;
-  hipEvent_t done = nullptr;
-};
-
-constexpr size_t kSlabMsgs = 1u << 16;  // messages per host-path staging slab
-
-struct MsgSlab {  // message verify staging per HostSlab, allocated on first use
-  uint64_t* h_off = nullptr;   // pinned [kSlabMsgs]: message offsets in the slab
-  uint32_t* h_status = nullptr;
-  uint64_t* h_end = nullptr;
-  uint64_t* d_off = nullptr;
-  uint32_t* d_status = nullptr;
-  uint64_t* d_end = nullptr;
-  void* d_ws = nullptr;
-};
-
-struct DevCtx {
-  int device = -1;
-  int num_cu = 0;
-  int grid = 0;
-  // kVariantDefault (29): 64-B lane runs (four coalesced 1 KiB loads per 4 KiB super-block,
-  // quad transpose by v_cndmask_b32_dpp, one x^(8*4096) fold per 64 B), s_setprio 3 around
-  // the loads; plus, for batches of >= kGroupMinChunks chunks, whole chunks <= 16 KiB in the
-  // fused group phase, each size class spread over all waves with a class-sized group
-  // (G = 4 / 8 / 16 lanes). Measured against the round-1 alternatives in DESIGN.md §4-5.
-  int variant = kVariantDefault;
-  // Sweep rounds of at most this many bytes (SweepArgs::window); 0 = one round.
-  uint64_t window = 32ull << 30;
-  uint32_t* d_img = nullptr;
-  // Default workspaces (d_ws == NULL calls), one per stream: calls on one stream are ordered by
-  // it, so they may share a buffer; calls on different streams get different buffers. ws_mu is
-  // held from choosing the buffer until the call's work is enqueued, so a concurrent call that
-  // grows the same stream's buffer retires the old one only behind that work (an event on the
-  // stream; freed once it has completed, or at shutdown).
-  struct StreamWs {
-    hipStream_t stream;
-    void* ptr;
-    size_t bytes;
-  };
-  struct RetiredWs {
-    void* ptr;
-    hipEvent_t done;
-  };
-  std::mutex ws_mu;
-  std::vector<StreamWs> ws_list;
-  std::vector<RetiredWs> ws_retired;
-  bool timing = false;
-  std::vector<EventPair> pending, free_events;
-  bool slabs_ready = false;
-  HostSlab slab[kSlabs];
-  bool msg_slabs_ready = false;
-  MsgSlab msg_slab[kSlabs];
-  std::mutex mu;     // guards the slabs (held across a whole host-path call)
-  std::mutex ev_mu;  // guards the timing events (taken inside enqueue_batch, which host-path calls reach with mu held)
-};
+namespace ambrycrc {
+namespace detail {
 
 std::mutex g_mu;
 DevCtx* g_ctx[kMaxDevices] = {nullptr};
@@ -358,18 +288,6 @@ int stream_ws(DevCtx* c, hipStream_t s, size_t need, void** out) {
   return AMBRYCRC_OK;
 }
 
-// Holds c->ws_mu for the lifetime of a *_dev call that uses the default workspace (d_ws ==
-// NULL); a call with its own workspace takes no lock.
-struct WsLease {
-  std::unique_lock<std::mutex> lk;
-  // On return *ws is the caller's buffer (checked against need) or the stream's default one.
-  int acquire(DevCtx* c, hipStream_t s, void** ws, size_t ws_bytes, size_t need) {
-    if (*ws) return ws_bytes < need ? AMBRYCRC_EINVAL : AMBRYCRC_OK;
-    lk = std::unique_lock<std::mutex>(c->ws_mu);
-    return stream_ws(c, s, need, ws);
-  }
-};
-
 // Largest chunk the group phase takes whole for a batch of n chunks on c's variant (0: none).
 uint64_t batch_small_max(const DevCtx* c, size_t n) {
   if (n < kGroupMinChunks || !variant_groups(c->variant)) return 0;
@@ -380,7 +298,7 @@ uint64_t batch_small_max(const DevCtx* c, size_t n) {
 // crc_in may equal out (an in-place continuation): the plan copies crc_in into the workspace
 // before it initialises out, and the CRC kernels read the copy.
 int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len, const uint32_t* crc_in,
-                  uint32_t* out, size_t n, void* ws, hipStream_t s, uint32_t* exp_fill = nullptr) {
+                  uint32_t* out, size_t n, void* ws, hipStream_t s, uint32_t* exp_fill) {
   if (n == 0) return AMBRYCRC_OK;
   PlanArgs p;
   p.off = off;
@@ -503,7 +421,8 @@ void free_ctx(DevCtx* c) {
   delete c;
 }
 
-}  // namespace
+}  // namespace detail
+}  // namespace ambrycrc
 
 // ================================================================= C ABI
 extern "C" {

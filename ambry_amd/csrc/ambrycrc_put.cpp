@@ -1,0 +1,129 @@
+// ambrycrc_put.cpp -- write side of the message path: lay out PUT messages
+// and fill every CRC trailer, on the CPU for one message (ambrycrc_serialize_put_host) and on the
+// GPU for a batch (ambrycrc_serialize_puts_dev). Layout: put_layout.h.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include "../../include/ambrycrc.h"
+#include "ambrycrc_ctx.h"
+#include "crc32_kernels.h"
+#include "put_layout.h"
+
+using namespace ambrycrc;
+using namespace ambrycrc::detail;
+
+namespace {
+
+// Workspace of a device batch of m messages: copy jobs (src, dst, len) and CRC jobs (off, len,
+// crc) of 5 per message, then one batch workspace shared by the copy plan and the CRC batch
+// (both run on the same stream, one after the other).
+size_t put_jobs_bytes(size_t m) {
+  const size_t j = (size_t)kPutSlots * m;
+  return (j * (3 * sizeof(uint64_t) + 2 * sizeof(uint64_t) + sizeof(uint32_t)) + 255) & ~size_t(255);
+}
+
+}  // namespace
+
+extern "C" {
+
+uint64_t ambrycrc_put_layout(const ambrycrc_put_desc* d, uint64_t* offsets) {
+  if (!d) return 0;
+  PutLayout L;
+  if (!put_layout(*d, L)) return 0;
+  if (offsets) put_field_offsets(*d, L, offsets);
+  return L.length;
+}
+
+int ambrycrc_serialize_put_host(const ambrycrc_put_desc* d, const uint8_t* fields, const uint8_t* blobs, uint8_t* out,
+                                uint64_t out_cap, uint32_t* crcs) {
+  if (!d || !out) return AMBRYCRC_EINVAL;
+  PutLayout L;
+  if (!put_layout(*d, L)) return AMBRYCRC_EINVAL;
+  if (d->out_off > out_cap || L.length > out_cap - d->out_off) return AMBRYCRC_EINVAL;
+  uint8_t* m = out + d->out_off;
+  uint64_t fo[5];
+  put_field_offsets(*d, L, fo);
+  const uint64_t src[5] = {d->key_src, d->enckey_src, d->props_src, d->usermeta_src, d->blob_src};
+  const uint64_t len[5] = {d->key_len, L.enc_rec ? (uint64_t)d->enckey_len : 0, d->props_len, d->usermeta_len,
+                           d->blob_len};
+  for (int k = 0; k < 5; ++k) {
+    const uint8_t* base = k == 4 ? blobs : fields;
+    if (base && len[k]) memmove(m + fo[k], base + src[k], len[k]);
+  }
+  put_write_fixed(*d, L, m);
+  for (uint32_t k = 0; k < kPutSlots; ++k) {
+    uint64_t off, ln;
+    bool present;
+    put_crc_job(L, k, &off, &ln, &present);
+    const uint32_t c = present ? ambrycrc_update(0, m + off, ln) : 0u;
+    if (present) put_be64(m + off + ln, (uint64_t)c);
+    if (crcs) crcs[k] = c;
+  }
+  return AMBRYCRC_OK;
+}
+
+size_t ambrycrc_serialize_puts_workspace_bytes(size_t m) {
+  return put_jobs_bytes(m) + ws_need((size_t)kPutSlots * m);
+}
+
+int ambrycrc_serialize_puts_dev(const ambrycrc_put_desc* d_desc, size_t m, const uint8_t* d_fields,
+                                const uint8_t* d_blobs, uint8_t* d_out, uint64_t* d_msg_len, void* d_ws,
+                                size_t ws_bytes, hipStream_t stream) {
+  if (m == 0) return AMBRYCRC_OK;
+  if (!d_desc || !d_out || (size_t)kPutSlots * m >= (1ull << 31)) return AMBRYCRC_EINVAL;
+  DevCtx* c = ctx_current();
+  if (!c) return AMBRYCRC_ENOINIT;
+  WsLease lease;
+  int rc = lease.acquire(c, stream, &d_ws, ws_bytes, ambrycrc_serialize_puts_workspace_bytes(m));
+  if (rc) return rc;
+  const size_t j = (size_t)kPutSlots * m;
+  uint8_t* w = static_cast<uint8_t*>(d_ws);
+  PutArgs a;
+  a.desc = d_desc;
+  a.m = m;
+  a.out = d_out;
+  a.fields = d_fields;
+  a.blobs = d_blobs;
+  a.cp_src = reinterpret_cast<uint64_t*>(w);
+  a.cp_dst = a.cp_src + j;
+  a.cp_len = a.cp_dst + j;
+  a.crc_off = a.cp_len + j;
+  a.crc_len = a.crc_off + j;
+  uint32_t* crc = reinterpret_cast<uint32_t*>(a.crc_len + j);
+  a.crc = crc;
+  a.msg_len = d_msg_len;
+  void* batch_ws = w + put_jobs_bytes(m);
+  if (launch_put_layout(a, stream) != hipSuccess) return AMBRYCRC_EHIP;
+  if (d_fields || d_blobs) {
+    // byte offsets of the copy jobs: the plan kernel's exclusive scan (no small-chunk classes);
+    // its per-chunk output initialisation lands in `crc`, overwritten by the CRC batch below
+    PlanArgs p;
+    p.off = a.cp_dst;
+    p.len = a.cp_len;
+    p.crc_in = nullptr;
+    p.n = (uint32_t)j;
+    p.byte_start = static_cast<uint64_t*>(batch_ws);
+    const size_t blocks = (j + kPlanPerBlock - 1) / kPlanPerBlock;
+    p.block_sum = p.byte_start + j + 1;
+    p.block_small = p.block_sum + blocks;
+    p.small_total = p.block_small + blocks;
+    p.small_idx = reinterpret_cast<uint32_t*>(p.small_total + 5);
+    p.crc_stage = nullptr;
+    p.out = crc;
+    p.small_max = 0;
+    if (launch_plan(p, stream) != hipSuccess) return AMBRYCRC_EHIP;
+    CopyArgs ca;
+    ca.src = a.cp_src;
+    ca.dst_off = a.cp_dst;
+    ca.len = a.cp_len;
+    ca.start = p.byte_start;
+    ca.n = (uint32_t)j;
+    ca.dst = d_out;
+    if (launch_gather_copy(ca, c->num_cu * 8, stream) != hipSuccess) return AMBRYCRC_EHIP;
+  }
+  rc = enqueue_batch(c, d_out, a.crc_off, a.crc_len, nullptr, crc, j, batch_ws, stream);
+  if (rc) return rc;
+  return hip_err(launch_put_seal(a, stream));
+}
+
+}  // extern "C"

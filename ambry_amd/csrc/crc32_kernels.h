@@ -4,6 +4,8 @@
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
 
+#include "../../include/ambrycrc.h"
+
 namespace ambrycrc {
 
 struct PlanArgs {
@@ -113,6 +115,35 @@ struct TrailerArgs {
   uint32_t* count;          // or null
   uint64_t inline_max;
 };
+
+// PUT serialization (put_kernels.hip): job k of message i is entry k*m + i (slot-major).
+struct PutArgs {
+  const ::ambrycrc_put_desc* desc;  // [m]
+  uint64_t m;
+  uint8_t* out;
+  const uint8_t* fields;   // or null: key / encryption key / properties / user metadata already in place
+  const uint8_t* blobs;    // or null: blob contents already in place
+  uint64_t* cp_src;        // [5m] copy jobs: absolute source address, destination offset in out, length
+  uint64_t* cp_dst;
+  uint64_t* cp_len;
+  uint64_t* crc_off;       // [5m] CRC jobs in out (length 0: absent encryption-key record)
+  uint64_t* crc_len;
+  const uint32_t* crc;     // [5m] their CRCs (from the batch kernels)
+  uint64_t* msg_len;       // [m] or null
+};
+
+struct CopyArgs {
+  const uint64_t* src;      // [n] absolute source addresses
+  const uint64_t* dst_off;  // [n] destination offsets from dst
+  const uint64_t* len;      // [n]
+  const uint64_t* start;    // [n+1] exclusive scan of len
+  uint32_t n;
+  uint8_t* dst;
+};
+
+hipError_t launch_put_layout(const PutArgs& a, hipStream_t s);
+hipError_t launch_put_seal(const PutArgs& a, hipStream_t s);
+hipError_t launch_gather_copy(const CopyArgs& a, int grid, hipStream_t s);
 
 hipError_t launch_trailer_parse(const TrailerArgs& a, hipStream_t s);
 hipError_t launch_trailer_verify(const TrailerArgs& a, hipStream_t s);

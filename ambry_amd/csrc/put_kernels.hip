@@ -1,0 +1,217 @@
+// put_kernels.hip -- gfx950 kernels of the PUT-message write path (ambrycrc_serialize_puts_dev):
+// the batch form of PutMessageFormatInputStream (PutMessageFormatInputStream.java:76-124) +
+// MessageFormatInputStream.read* (MessageFormatInputStream.java:40-96), which Ambry's server runs
+// per PUT, computing every record CRC while it streams the message out.
+//
+//   put_layout_kernel   one thread per message: header fields and record prefixes (byte stores,
+//                       ~70 B per message), the copy jobs of the variable fields and the CRC jobs
+//   gather_copy_kernel  byte-balanced copy of every job (HBM read + write bound): each wave owns
+//                       an equal share of the concatenated job bytes; 16-B destination pieces are
+//                       built from two aligned source loads and v_alignbyte_b32, so loads and
+//                       stores stay coalesced whatever the source/destination misalignment
+//   (plan + sweep)      the batch CRC kernels over the CRC jobs, in the output buffer
+//   put_seal_kernel     one thread per CRC job: the big-endian 8-B trailer
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "crc32_kernels.h"
+#include "put_layout.h"
+
+namespace ambrycrc {
+
+typedef uint32_t u32x4p __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void put_layout_kernel(PutArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.m) return;
+  const ambrycrc_put_desc d = a.desc[i];
+  PutLayout L;
+  const uint64_t m = a.m;
+  if (!put_layout(d, L)) {  // the host checks descriptors it can see; a bad one here writes nothing
+    for (uint32_t k = 0; k < kPutSlots; ++k) {
+      a.cp_len[k * m + i] = 0;
+      a.crc_len[k * m + i] = 0;
+      a.crc_off[k * m + i] = 0;
+    }
+    if (a.msg_len) a.msg_len[i] = 0;
+    return;
+  }
+  uint8_t* msg = a.out + d.out_off;
+  put_write_fixed(d, L, msg);
+  uint64_t fo[5];
+  put_field_offsets(d, L, fo);
+  const uint64_t src[5] = {d.key_src, d.enckey_src, d.props_src, d.usermeta_src, d.blob_src};
+  const uint64_t len[5] = {d.key_len, L.enc_rec ? (uint64_t)d.enckey_len : 0, d.props_len, d.usermeta_len,
+                           d.blob_len};
+  for (uint32_t k = 0; k < kPutSlots; ++k) {
+    const uint8_t* base = k == 4 ? a.blobs : a.fields;
+    a.cp_src[k * m + i] = base ? (uint64_t)(uintptr_t)(base + src[k]) : 0;
+    a.cp_dst[k * m + i] = d.out_off + fo[k];
+    a.cp_len[k * m + i] = base ? len[k] : 0;
+    uint64_t off, ln;
+    bool present;
+    put_crc_job(L, k, &off, &ln, &present);
+    a.crc_off[k * m + i] = d.out_off + off;
+    a.crc_len[k * m + i] = present ? ln : 0;
+  }
+  if (a.msg_len) a.msg_len[i] = L.length;
+}
+
+__global__ __launch_bounds__(256) void put_seal_kernel(PutArgs a) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= kPutSlots * a.m) return;
+  const uint64_t len = a.crc_len[j];
+  if (len == 0) return;  // absent encryption-key record (every present record has >= 6 bytes)
+  put_be64(a.out + a.crc_off[j] + len, (uint64_t)a.crc[j]);
+}
+
+// ---------------------------------------------------------------- gather copy
+__device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t lane) {
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, lane);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), lane);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Largest c in [0, n) with start[c] <= g (start nondecreasing, start[0] = 0): 64-ary search.
+__device__ __forceinline__ uint32_t find_job(const uint64_t* __restrict__ start, uint32_t n, uint64_t g,
+                                             uint32_t lane) {
+  uint32_t lo = 0, hi = n;
+  while (hi - lo > 1) {
+    const uint32_t step = (hi - lo + 63) / 64;
+    const uint32_t idx = lo + lane * step;
+    const uint64_t m = __ballot(idx < hi && start[idx] <= g);
+    const uint32_t last = 63u - (uint32_t)__builtin_clzll(m);
+    const uint32_t nhi = lo + (last + 1) * step;
+    lo = lo + last * step;
+    hi = nhi < hi ? nhi : hi;
+  }
+  return lo;
+}
+
+// Dword k of bytes [4Q + r, 4Q + r + 16) of the 32-byte concatenation a||b (little endian).
+template <int Q>
+__device__ __forceinline__ u32x4p shift_pair(const u32x4p& a, const u32x4p& b, uint32_t r) {
+  const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  u32x4p o;
+  if (r == 0) {
+    o.x = w[Q];
+    o.y = w[Q + 1];
+    o.z = w[Q + 2];
+    o.w = w[Q + 3];
+  } else {
+    o.x = __builtin_amdgcn_alignbyte(w[Q + 1], w[Q], r);
+    o.y = __builtin_amdgcn_alignbyte(w[Q + 2], w[Q + 1], r);
+    o.z = __builtin_amdgcn_alignbyte(w[Q + 3], w[Q + 2], r);
+    o.w = __builtin_amdgcn_alignbyte(w[Q + 4], w[Q + 3], r);
+  }
+  return o;
+}
+
+// Copies n16 16-B pieces to the 16-B aligned dst from src (any alignment: shift = 4Q + r),
+// lane-strided, 4 pieces per lane in flight. The second aligned source block of a piece holds
+// bytes the piece needs whenever shift > 0, so every load touches the source range.
+template <int Q>
+__device__ __forceinline__ void copy_pieces(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint64_t n16,
+                                            uint32_t r, uint32_t lane) {
+  const uint32_t shift = 4 * Q + r;
+  const u32x4p* s0 = reinterpret_cast<const u32x4p*>(src - shift);
+  u32x4p* d0 = reinterpret_cast<u32x4p*>(dst);
+  constexpr int U = 4;
+  uint64_t p = lane;
+  for (; p + 64 * (U - 1) < n16; p += 64 * U) {
+    u32x4p a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      a[u] = __builtin_nontemporal_load(s0 + p + 64 * u);
+      b[u] = shift ? __builtin_nontemporal_load(s0 + p + 64 * u + 1) : u32x4p{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) __builtin_nontemporal_store(shift_pair<Q>(a[u], b[u], r), d0 + p + 64 * u);
+  }
+  for (; p < n16; p += 64) {
+    const u32x4p a = __builtin_nontemporal_load(s0 + p);
+    const u32x4p b = shift ? __builtin_nontemporal_load(s0 + p + 1) : u32x4p{0u, 0u, 0u, 0u};
+    __builtin_nontemporal_store(shift_pair<Q>(a, b, r), d0 + p);
+  }
+}
+
+// One wave copies n bytes src -> dst (wave-uniform arguments).
+__device__ __forceinline__ void copy_range(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint64_t n,
+                                           uint32_t lane) {
+  const uint64_t head0 = (16 - ((uintptr_t)dst & 15)) & 15;
+  const uint64_t head = head0 < n ? head0 : n;
+  if (lane < head) dst[lane] = src[lane];
+  const uint64_t body = n - head;
+  const uint64_t n16 = body >> 4;
+  uint8_t* d1 = dst + head;
+  const uint8_t* s1 = src + head;
+  if (n16) {
+    const uint32_t shift = (uint32_t)((uintptr_t)s1 & 15);
+    switch (shift >> 2) {
+      case 0: copy_pieces<0>(d1, s1, n16, shift & 3, lane); break;
+      case 1: copy_pieces<1>(d1, s1, n16, shift & 3, lane); break;
+      case 2: copy_pieces<2>(d1, s1, n16, shift & 3, lane); break;
+      default: copy_pieces<3>(d1, s1, n16, shift & 3, lane); break;
+    }
+  }
+  const uint64_t t = body & 15;
+  if (lane < t) d1[16 * n16 + lane] = s1[16 * n16 + lane];
+}
+
+// Persistent, byte-balanced: wave w copies bytes [w*S, (w+1)*S) of the jobs' concatenation
+// (start = exclusive scan of len, from the plan kernel). Descriptors 64 at a time per wave.
+__global__ __launch_bounds__(256) void gather_copy_kernel(CopyArgs a) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  const uint32_t wave = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * gridDim.x + blockIdx.x);
+  const uint64_t total = a.start[a.n];
+  uint64_t S = (total + nwaves - 1) / nwaves;
+  S = (S + 255) & ~uint64_t(255);
+  S = S < 4096 ? 4096 : S;
+  const uint64_t g0 = (uint64_t)wave * S;
+  if (g0 >= total) return;
+  const uint64_t g1 = g0 + S < total ? g0 + S : total;
+  uint32_t c = __builtin_amdgcn_readfirstlane(find_job(a.start, a.n, g0, lane));
+  while (c < a.n) {
+    const uint32_t cnt = a.n - c < 64u ? a.n - c : 64u;
+    uint64_t w_st = ~0ull, w_len = 0, w_src = 0, w_dst = 0;
+    if (lane < cnt) {
+      w_st = a.start[c + lane];
+      w_len = a.len[c + lane];
+      w_src = a.src[c + lane];
+      w_dst = a.dst_off[c + lane];
+    }
+    for (uint32_t j = 0; j < cnt; ++j) {
+      const uint64_t st = rl64(w_st, j);
+      if (st >= g1) return;
+      const uint64_t len = rl64(w_len, j);
+      if (len == 0) continue;
+      const uint64_t r0 = g0 > st ? g0 - st : 0;
+      const uint64_t r1 = g1 - st < len ? g1 - st : len;
+      if (r0 < r1)
+        copy_range(a.dst + rl64(w_dst, j) + r0,
+                   reinterpret_cast<const uint8_t*>((uintptr_t)rl64(w_src, j)) + r0, r1 - r0, lane);
+    }
+    c += cnt;
+  }
+}
+
+hipError_t launch_put_layout(const PutArgs& a, hipStream_t s) {
+  if (a.m == 0) return hipSuccess;
+  hipLaunchKernelGGL(put_layout_kernel, dim3((uint32_t)((a.m + 255) / 256)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_put_seal(const PutArgs& a, hipStream_t s) {
+  if (a.m == 0) return hipSuccess;
+  hipLaunchKernelGGL(put_seal_kernel, dim3((uint32_t)((kPutSlots * a.m + 255) / 256)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_copy(const CopyArgs& a, int grid, hipStream_t s) {
+  if (a.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(gather_copy_kernel, dim3(grid), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace ambrycrc

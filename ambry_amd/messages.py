@@ -1,0 +1,122 @@
+"""PUT message serialization (the write side of Ambry's message path).
+
+Mirrors PutMessageFormatInputStream (PutMessageFormatInputStream.java:60-124): a message is
+described by its store key, optional encryption key, BlobPropertiesSerDe bytes, user metadata
+and blob content, plus header version / life version / blob type / compression flag. The bytes
+and every CRC trailer are produced by libambrycrc -- on the CPU for one message
+(ambrycrc_serialize_put_host), on the GPU for a batch (ambrycrc_serialize_puts_dev).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from ._lib import PutDesc, check, lib
+
+# numpy mirror of struct ambrycrc_put_desc (80 bytes), for descriptor arrays copied to HBM
+PUT_DESC_DTYPE = np.dtype([
+    ("out_off", "<u8"), ("key_src", "<u8"), ("enckey_src", "<u8"), ("props_src", "<u8"), ("usermeta_src", "<u8"),
+    ("blob_src", "<u8"), ("blob_len", "<u8"), ("key_len", "<u4"), ("enckey_len", "<i4"), ("props_len", "<u4"),
+    ("usermeta_len", "<u4"), ("life_version", "<i2"), ("blob_type", "<i2"), ("compressed", "u1"),
+    ("header_version", "u1"), ("reserved", "u1", (2,))])
+assert PUT_DESC_DTYPE.itemsize == ctypes.sizeof(PutDesc) == 80
+
+FIELDS = ("key", "enckey", "props", "usermeta", "blob")
+
+
+@dataclass
+class PutMessage:
+    """One PUT: the arguments of PutMessageFormatInputStream's constructor, as bytes."""
+    key: bytes                # StoreKey.toBytes()
+    props: bytes              # BlobPropertiesSerDe bytes
+    usermeta: bytes
+    blob: bytes
+    enckey: bytes | None = None
+    header_version: int = 3   # MessageFormatRecord.headerVersionToUse
+    life_version: int = 0
+    blob_type: int = 0        # BlobType ordinal (0 = DataBlob)
+    compressed: bool = False
+
+    def desc(self, out_off: int = 0, src: dict | None = None) -> PutDesc:
+        src = src or {}
+        d = PutDesc()
+        d.out_off = out_off
+        d.key_src, d.enckey_src, d.props_src = src.get("key", 0), src.get("enckey", 0), src.get("props", 0)
+        d.usermeta_src, d.blob_src = src.get("usermeta", 0), src.get("blob", 0)
+        d.blob_len = len(self.blob)
+        d.key_len, d.props_len, d.usermeta_len = len(self.key), len(self.props), len(self.usermeta)
+        d.enckey_len = -1 if self.enckey is None else len(self.enckey)
+        d.life_version, d.blob_type = self.life_version, self.blob_type
+        d.compressed, d.header_version = 1 if self.compressed else 0, self.header_version
+        return d
+
+
+def layout(msg: PutMessage):
+    """(message length, {field: offset from the message start}) -- ambrycrc_put_layout."""
+    offs = (ctypes.c_uint64 * 5)()
+    n = lib().ambrycrc_put_layout(ctypes.byref(msg.desc()), offs)
+    if n == 0:
+        raise ValueError("invalid PUT descriptor")
+    return n, dict(zip(FIELDS, list(offs)))
+
+
+def serialize_host(msg: PutMessage):
+    """(message bytes, [header, enckey, props, usermeta, blob record CRCs]) on the CPU."""
+    fields = b"".join([msg.key, msg.enckey or b"", msg.props, msg.usermeta])
+    src = {"key": 0, "enckey": len(msg.key), "props": len(msg.key) + len(msg.enckey or b""),
+           "usermeta": len(msg.key) + len(msg.enckey or b"") + len(msg.props), "blob": 0}
+    n, _ = layout(msg)
+    out = ctypes.create_string_buffer(max(n, 1))
+    fb = ctypes.create_string_buffer(fields, max(len(fields), 1))
+    bb = ctypes.create_string_buffer(msg.blob, max(len(msg.blob), 1))
+    crcs = (ctypes.c_uint32 * 5)()
+    check(lib().ambrycrc_serialize_put_host(ctypes.byref(msg.desc(0, src)), fb, bb, out, n, crcs),
+          "ambrycrc_serialize_put_host")
+    return out.raw[:n], list(crcs)
+
+
+def pack_batch(msgs, out_align: int = 1, field_align: int = 1, gap: int = 0):
+    """Host-side packing for ambrycrc_serialize_puts_dev: (descriptor array, fields bytes, blobs
+    bytes, message offsets, total output bytes). Fields go back to back (each at field_align),
+    blobs likewise, messages at out_align with `gap` spare bytes between them."""
+    descs = np.zeros(len(msgs), dtype=PUT_DESC_DTYPE)
+    fields, blobs = bytearray(), bytearray()
+    offs, pos = [], 0
+    for i, m in enumerate(msgs):
+        src = {}
+        for name in FIELDS[:4]:
+            b = getattr(m, name) or b""
+            fields += bytes((-len(fields)) % field_align)
+            src[name] = len(fields)
+            fields += b
+        blobs += bytes((-len(blobs)) % field_align)
+        src["blob"] = len(blobs)
+        blobs += m.blob
+        pos += (-pos) % out_align
+        offs.append(pos)
+        d = m.desc(pos, src)
+        descs[i] = np.frombuffer(bytes(d), dtype=PUT_DESC_DTYPE)[0]
+        pos += layout(m)[0] + gap
+    return descs, bytes(fields), bytes(blobs), offs, pos
+
+
+def serialize_dev(descs, out, fields=None, blobs=None, msg_len=None, stream=None):
+    """ambrycrc_serialize_puts_dev: descs is a uint8 CUDA tensor holding the PUT_DESC_DTYPE array;
+    fields / blobs uint8 CUDA tensors or None (bytes already in place in `out`)."""
+    import torch
+
+    from .device import _stream_handle
+
+    if descs.dtype != torch.uint8 or not descs.is_cuda or descs.numel() % PUT_DESC_DTYPE.itemsize:
+        raise TypeError("descs must be a uint8 CUDA tensor of 80-byte descriptors")
+    m = descs.numel() // PUT_DESC_DTYPE.itemsize
+    for name, t in (("out", out), ("fields", fields), ("blobs", blobs)):
+        if t is not None and (t.dtype != torch.uint8 or not t.is_cuda or t.device != descs.device):
+            raise TypeError(f"{name} must be a uint8 CUDA tensor on {descs.device}")
+    if msg_len is not None and (msg_len.dtype != torch.int64 or msg_len.numel() != m or not msg_len.is_cuda):
+        raise TypeError("msg_len must be an int64 CUDA tensor of m elements")
+    ptr = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    check(lib().ambrycrc_serialize_puts_dev(ptr(descs), m, ptr(fields), ptr(blobs), ptr(out), ptr(msg_len), None, 0,
+                                            ctypes.c_void_p(_stream_handle(stream))), "ambrycrc_serialize_puts_dev")

@@ -163,6 +163,63 @@ int ambrycrc_verify_messages_dev(const uint8_t* d_region, uint64_t region_len, c
                                  uint32_t* d_status, uint64_t* d_msg_end, void* d_ws, size_t ws_bytes,
                                  hipStream_t stream);
 
+/* ------------------------------------------ PUT message serialization (write side, row a10) */
+
+/* One PUT message to lay out (PutMessageFormatInputStream.java:76-124 / :133-162 for header V1):
+ *   header (V1 34 B / V2 38 B / V3 40 B, MessageFormatRecord.java:467-486, :696-725, :951-981)
+ *   store key (its serialized bytes, e.g. MockId: short length + id)
+ *   [BlobEncryptionKey_Format_V1 record: version 1, int size, key, CRC]  (header V2/V3 only)
+ *   BlobProperties_Format_V1 record: version 1, BlobPropertiesSerDe bytes, CRC
+ *   UserMetadata_Format_V1 record: version 1, int size, metadata, CRC
+ *   Blob_Format_V3 record: version 3, short blobType, byte isCompressed, long size, content, CRC
+ * Every CRC is CRC-32 of its record (header: of its first size-8 bytes) stored as a big-endian
+ * long with the upper 32 bits zero; all integers big-endian. 80 bytes, no padding. */
+typedef struct ambrycrc_put_desc {
+  uint64_t out_off;      /* message start in the output buffer */
+  uint64_t key_src;      /* field offsets in the fields buffer (unused when fields == NULL) */
+  uint64_t enckey_src;
+  uint64_t props_src;
+  uint64_t usermeta_src;
+  uint64_t blob_src;     /* content offset in the blobs buffer (unused when blobs == NULL) */
+  uint64_t blob_len;
+  uint32_t key_len;
+  int32_t enckey_len;    /* -1: no encryption-key record */
+  uint32_t props_len;
+  uint32_t usermeta_len;
+  int16_t life_version;  /* header V3 */
+  int16_t blob_type;
+  uint8_t compressed;
+  uint8_t header_version; /* 1, 2 or 3 (MessageFormatRecord.headerVersionToUse) */
+  uint8_t reserved[2];
+} ambrycrc_put_desc;
+
+/* Where the variable fields of message d go, relative to its start: offsets[0..4] = key,
+ * encryption key (0 when absent), blob-properties bytes, user-metadata bytes, blob content.
+ * Returns the message length (header + key + records), or 0 for an invalid descriptor. A
+ * caller that receives the fields straight into the output at these offsets (a Netty buffer
+ * read into the log buffer) serializes in place: pass fields == NULL and blobs == NULL below. */
+uint64_t ambrycrc_put_layout(const ambrycrc_put_desc* d, uint64_t* offsets);
+
+/* One message on the CPU: header, key, records, every CRC trailer, at out + d->out_off
+ * (out_cap bytes in out). crcs[5] (nullable) = header, encryption key (0 if absent), properties,
+ * user metadata, blob record CRCs. The write side of MessageFormatInputStream.read*
+ * (MessageFormatInputStream.java:40-96) for one PUT. */
+int ambrycrc_serialize_put_host(const ambrycrc_put_desc* d, const uint8_t* fields, const uint8_t* blobs, uint8_t* out,
+                                uint64_t out_cap, uint32_t* crcs);
+
+/* m messages on the GPU (d_desc: device array): one thread per message writes the header and
+ * record prefixes, a byte-balanced copy kernel moves key / encryption key / properties /
+ * user metadata (from d_fields) and blob contents (from d_blobs) into place, the batch CRC
+ * kernels compute every record CRC (the group phase takes the small records, the sweep the
+ * blobs), and a last kernel writes the trailers. d_fields / d_blobs NULL: those bytes are
+ * already in place in d_out (ambrycrc_put_layout). d_msg_len[m] (nullable): message lengths.
+ * Descriptors must be valid (ambrycrc_put_layout != 0) and messages must not overlap.
+ * Asynchronous on `stream`; d_ws >= ambrycrc_serialize_puts_workspace_bytes(m) or NULL. */
+size_t ambrycrc_serialize_puts_workspace_bytes(size_t m);
+int ambrycrc_serialize_puts_dev(const ambrycrc_put_desc* d_desc, size_t m, const uint8_t* d_fields,
+                                const uint8_t* d_blobs, uint8_t* d_out, uint64_t* d_msg_len, void* d_ws,
+                                size_t ws_bytes, hipStream_t stream);
+
 /* ------------------------------------- CRC-trailered records (store files, headers) */
 
 /* Item i = [off[i], off[i] + len[i]) ends in the big-endian 8-B CRC (a long, high word zero)

@@ -1,0 +1,85 @@
+"""GPU write path (ambrycrc_serialize_puts_dev): batches of PUT messages laid out in HBM with every
+CRC trailer filled, byte-exact against oracle/message_format.py's layouts (zlib CRCs), then
+verified by ambrycrc_verify_messages_dev (round trip). Copy mode (fields and blobs gathered from
+their own buffers, at any alignment) and in-place mode (bytes already at ambrycrc_put_layout's
+offsets); batches under and over the group-phase threshold; 4 MiB blobs."""
+import numpy as np
+import pytest
+
+from test_put_serialize import expected, random_messages
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def mf():
+    import importlib.util
+    import os
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("message_format", os.path.join(root, "oracle", "message_format.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def _dev(b):
+    import torch
+
+    return torch.frombuffer(bytearray(b if len(b) else b"\0"), dtype=torch.uint8).cuda()
+
+
+def _run(gpu, mf, msgs, out_align, field_align, gap, in_place=False):
+    import torch
+
+    from ambry_amd.messages import layout, pack_batch, serialize_dev
+
+    descs, fields, blobs, offs, total = pack_batch(msgs, out_align=out_align, field_align=field_align, gap=gap)
+    host_out = bytearray(b"\xAA" * total)  # filler: gaps must stay untouched
+    if in_place:
+        for m, o in zip(msgs, offs):
+            _, fo = layout(m)
+            for name in ("key", "enckey", "props", "usermeta", "blob"):
+                b = getattr(m, name)
+                if b:
+                    host_out[o + fo[name]:o + fo[name] + len(b)] = b
+    out = _dev(bytes(host_out))
+    mlen = torch.empty(len(msgs), dtype=torch.int64, device="cuda")
+    serialize_dev(_dev(descs.tobytes()), out, None if in_place else _dev(fields), None if in_place else _dev(blobs),
+                  msg_len=mlen)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().tobytes()
+    exp = bytearray(b"\xAA" * total)
+    for m, o in zip(msgs, offs):
+        e = expected(mf, m)
+        exp[o:o + len(e)] = e
+    assert got == bytes(exp)
+    assert mlen.cpu().numpy().tolist() == [len(expected(mf, m)) for m in msgs]
+    status, end = gpu.verify_messages(out, torch.tensor(offs, dtype=torch.int64, device="cuda"))
+    torch.cuda.synchronize()
+    assert int(status.abs().sum().item()) == 0
+    assert end.cpu().numpy().tolist() == [o + len(expected(mf, m)) for o, m in zip(offs, msgs)]
+
+
+@pytest.mark.parametrize("out_align,field_align,gap", [(1, 1, 0), (16, 16, 0), (1, 7, 3), (4096, 1, 0)])
+def test_serialize_batch_copy_mode(gpu, mf, out_align, field_align, gap):
+    _run(gpu, mf, random_messages(mf, 400, seed=100 + out_align + field_align), out_align, field_align, gap)
+
+
+def test_serialize_batch_in_place(gpu, mf):
+    _run(gpu, mf, random_messages(mf, 300, seed=7), 1, 1, 5, in_place=True)
+
+
+def test_serialize_group_phase_batch(gpu, mf):
+    """4,000 messages = 20,000 CRC jobs (>= 16,384: the group phase takes the small records)."""
+    _run(gpu, mf, random_messages(mf, 4000, seed=9, max_blob=9000), 1, 3, 0)
+
+
+def test_serialize_large_blobs(gpu, mf):
+    from ambry_amd.messages import PutMessage
+    from datagen import stream_bytes
+
+    msgs = [PutMessage(key=mf.store_key("big%d" % i), props=mf.blob_properties_bytes(4 << 20),
+                       usermeta=b"m" * 1000, blob=stream_bytes(50 + i, 0, (4 << 20) - (i % 3)).tobytes(),
+                       header_version=3) for i in range(12)]
+    _run(gpu, mf, msgs, 1, 1, 0)
