@@ -14,12 +14,12 @@ using namespace ambrycrc::detail;
 
 namespace {
 
-// Workspace of a device batch of m messages: copy jobs (src, dst, len) and CRC jobs (off, len,
+// Workspace of a device batch of m messages: copy jobs (src, dst, len, cost) and CRC jobs (off, len,
 // crc) of 5 per message, then one batch workspace shared by the copy plan and the CRC batch
 // (both run on the same stream, one after the other).
 size_t put_jobs_bytes(size_t m) {
   const size_t j = (size_t)kPutSlots * m;
-  return (j * (3 * sizeof(uint64_t) + 2 * sizeof(uint64_t) + sizeof(uint32_t)) + 255) & ~size_t(255);
+  return (j * (4 * sizeof(uint64_t) + 2 * sizeof(uint64_t) + sizeof(uint32_t)) + 255) & ~size_t(255);
 }
 
 }  // namespace
@@ -87,7 +87,8 @@ int ambrycrc_serialize_puts_dev(const ambrycrc_put_desc* d_desc, size_t m, const
   a.cp_src = reinterpret_cast<uint64_t*>(w);
   a.cp_dst = a.cp_src + j;
   a.cp_len = a.cp_dst + j;
-  a.crc_off = a.cp_len + j;
+  a.cp_cost = a.cp_len + j;
+  a.crc_off = a.cp_cost + j;
   a.crc_len = a.crc_off + j;
   uint32_t* crc = reinterpret_cast<uint32_t*>(a.crc_len + j);
   a.crc = crc;
@@ -95,11 +96,11 @@ int ambrycrc_serialize_puts_dev(const ambrycrc_put_desc* d_desc, size_t m, const
   void* batch_ws = w + put_jobs_bytes(m);
   if (launch_put_layout(a, stream) != hipSuccess) return AMBRYCRC_EHIP;
   if (d_fields || d_blobs) {
-    // byte offsets of the copy jobs: the plan kernel's exclusive scan (no small-chunk classes);
+    // cost offsets of the copy jobs: the plan kernel's exclusive scan (no small-chunk classes);
     // its per-chunk output initialisation lands in `crc`, overwritten by the CRC batch below
     PlanArgs p;
     p.off = a.cp_dst;
-    p.len = a.cp_len;
+    p.len = a.cp_cost;
     p.crc_in = nullptr;
     p.n = (uint32_t)j;
     p.byte_start = static_cast<uint64_t*>(batch_ws);

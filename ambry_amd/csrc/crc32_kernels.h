@@ -126,17 +126,23 @@ struct PutArgs {
   uint64_t* cp_src;        // [5m] copy jobs: absolute source address, destination offset in out, length
   uint64_t* cp_dst;
   uint64_t* cp_len;
+  uint64_t* cp_cost;       // [5m] len + kCopyJobCost (0 for an empty job): what the copy balances
   uint64_t* crc_off;       // [5m] CRC jobs in out (length 0: absent encryption-key record)
   uint64_t* crc_len;
   const uint32_t* crc;     // [5m] their CRCs (from the batch kernels)
   uint64_t* msg_len;       // [m] or null
 };
 
+// Each copy job costs its bytes plus kCopyJobCost: a wave pays about one memory round trip
+// (~2 us, ~1.6 KB of its share of HBM bandwidth) per job whatever its size, so balancing bytes
+// alone put 22,000 24-B key copies on one wave (a 28 ms kernel for 4 GiB of 64 KiB PUTs).
+constexpr uint64_t kCopyJobCost = 2048;
+
 struct CopyArgs {
   const uint64_t* src;      // [n] absolute source addresses
   const uint64_t* dst_off;  // [n] destination offsets from dst
   const uint64_t* len;      // [n]
-  const uint64_t* start;    // [n+1] exclusive scan of len
+  const uint64_t* start;    // [n+1] exclusive scan of the job costs (len + kCopyJobCost)
   uint32_t n;
   uint8_t* dst;
 };

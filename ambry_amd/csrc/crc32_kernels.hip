@@ -938,6 +938,7 @@ __global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
         w_cin = a.crc_in ? a.crc_in[c + lane] : 0u;
       }
       uint64_t bsc = readlane64(w_bs, 0);
+      bool work = false;
       for (uint32_t j = 0; j < cnt;) {
         if (bsc >= g1) {
           done = true;
@@ -946,6 +947,7 @@ __global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
         const uint64_t len = readlane64(w_len, j);
         const uint64_t span = len > a.small_max ? len : 0;  // small chunks: group phase
         if (span != 0) {  // empty chunks are finished by the plan kernel
+          work = true;
           bool whole;
           const uint32_t r = segment(bsc, len, readlane64(w_off, j), __builtin_amdgcn_readlane(w_cin, j), &whole);
           if (whole && DIAG != 2) {
@@ -957,7 +959,15 @@ __global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
         bsc += span;
         ++j;
       }
-      c += cnt;
+      // A window with no byte share (empty chunks, or small ones the group phase took) may head a
+      // long run of them at one byte position: jump to the run's end (the chunk holding byte bsc)
+      // instead of walking it 64 descriptors at a time.
+      uint32_t next = c + cnt;
+      if (!work && !done && next < a.n) {
+        const uint32_t far = __builtin_amdgcn_readfirstlane(find_chunk(a.byte_start, a.n, bsc, lane));
+        next = far > next ? far : next;
+      }
+      c = next;
     }
     if (round_step == 0) break;
     g0 += round_step;

@@ -30,6 +30,7 @@ __global__ __launch_bounds__(256) void put_layout_kernel(PutArgs a) {
   if (!put_layout(d, L)) {  // the host checks descriptors it can see; a bad one here writes nothing
     for (uint32_t k = 0; k < kPutSlots; ++k) {
       a.cp_len[k * m + i] = 0;
+      a.cp_cost[k * m + i] = 0;
       a.crc_len[k * m + i] = 0;
       a.crc_off[k * m + i] = 0;
     }
@@ -48,6 +49,7 @@ __global__ __launch_bounds__(256) void put_layout_kernel(PutArgs a) {
     a.cp_src[k * m + i] = base ? (uint64_t)(uintptr_t)(base + src[k]) : 0;
     a.cp_dst[k * m + i] = d.out_off + fo[k];
     a.cp_len[k * m + i] = base ? len[k] : 0;
+    a.cp_cost[k * m + i] = base && len[k] ? len[k] + kCopyJobCost : 0;
     uint64_t off, ln;
     bool present;
     put_crc_job(L, k, &off, &ln, &present);
@@ -158,8 +160,9 @@ __device__ __forceinline__ void copy_range(uint8_t* __restrict__ dst, const uint
   if (lane < t) d1[16 * n16 + lane] = s1[16 * n16 + lane];
 }
 
-// Persistent, byte-balanced: wave w copies bytes [w*S, (w+1)*S) of the jobs' concatenation
-// (start = exclusive scan of len, from the plan kernel). Descriptors 64 at a time per wave.
+// Persistent, cost-balanced: wave w takes [w*S, (w+1)*S) of the jobs' concatenated costs (start =
+// exclusive scan of len + kCopyJobCost, from the plan kernel); job j's bytes are the first len[j]
+// units of its cost range, so every byte is copied by exactly one wave. Descriptors 64 at a time.
 __global__ __launch_bounds__(256) void gather_copy_kernel(CopyArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
@@ -181,18 +184,27 @@ __global__ __launch_bounds__(256) void gather_copy_kernel(CopyArgs a) {
       w_src = a.src[c + lane];
       w_dst = a.dst_off[c + lane];
     }
+    bool work = false;
     for (uint32_t j = 0; j < cnt; ++j) {
       const uint64_t st = rl64(w_st, j);
       if (st >= g1) return;
       const uint64_t len = rl64(w_len, j);
       if (len == 0) continue;
+      work = true;
       const uint64_t r0 = g0 > st ? g0 - st : 0;
       const uint64_t r1 = g1 - st < len ? g1 - st : len;
       if (r0 < r1)
         copy_range(a.dst + rl64(w_dst, j) + r0,
                    reinterpret_cast<const uint8_t*>((uintptr_t)rl64(w_src, j)) + r0, r1 - r0, lane);
     }
-    c += cnt;
+    // A window of empty jobs (e.g. the encryption-key slot of messages without one: cost 0, all
+    // at one start) may be the head of a long run; jump to its end instead of walking it 64 at a time.
+    uint32_t next = c + cnt;
+    if (!work && next < a.n) {
+      const uint32_t far = __builtin_amdgcn_readfirstlane(find_job(a.start, a.n, rl64(w_st, cnt - 1), lane));
+      next = far > next ? far : next;
+    }
+    c = next;
   }
 }
 
