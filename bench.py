@@ -302,26 +302,50 @@ def traffic_for(config):
 
 def run_c1(args, result_fd):
     """BASELINE configs[0]: one 64 KiB-blob PUT message (V3 header, MockId("id1") key, BlobProperties,
-    1000 B user metadata, blob record) through the messageformat CRCs on the CPU. The product path
-    is libambrycrc's host entries (ambrycrc_update per record; the blob record's CRC derived from the
-    blob's with ambrycrc_put_crcs, PutMessageFormatInputStream.java:116-120); the oracle's
-    Crc32.java restatement is timed beside it. Both are checked against the committed fixture
-    (tests/golden/c1_message.json)."""
+    1000 B user metadata, blob record) through messageformat on the CPU.
+      product (write)   ambrycrc_serialize_put_host: the whole message laid out and every CRC
+                        trailer filled (PutMessageFormatInputStream + MessageFormatInputStream.read*,
+                        PutMessageFormatInputStream.java:76-124); must equal the fixture's bytes
+      product (verify)  ambrycrc_update per record, the blob record's CRC derived from the blob's
+                        by ambrycrc_put_crcs (PutMessageFormatInputStream.java:116-120)
+      cpu_baseline      the oracle's Crc32.java restatement over the same four records
+    All checked against the committed fixture (tests/golden/c1_message.*)."""
     import ctypes
 
     import numpy as np
 
     from ambry_amd import lib
-    from c1_message import c1_message_bytes, c1_record_ranges
+    from ambry_amd.messages import PutMessage
+    from c1_message import c1_fixture, c1_message_bytes, c1_record_ranges
     from conftest import Oracle
 
-    with open(os.path.join(ROOT, "tests", "golden", "c1_message.json")) as f:
-        fx = json.load(f)
+    fx = c1_fixture()
     msg = c1_message_bytes()
-    ranges = c1_record_ranges(msg)
+    ranges = c1_record_ranges()
     L = lib()
     arr = np.frombuffer(msg, dtype=np.uint8)
     base = arr.ctypes.data
+    expect = [int(x, 16) for x in fx["record_crcs"]]
+
+    # write side: the C1 fields (sliced from the fixture) serialized by the product
+    ko, kl = fx["key_offset"], fx["key_bytes"]
+    (p0, p1), (u0, u1), (b0, b1) = ranges[1], ranges[2], ranges[3]
+    m = PutMessage(key=msg[ko:ko + kl], props=msg[p0 + 2:p1], usermeta=msg[u0 + 6:u1], blob=msg[b0 + 13:b1])
+    fields = m.key + m.props + m.usermeta
+    src = {"key": 0, "props": len(m.key), "usermeta": len(m.key) + len(m.props), "blob": 0}
+    desc = m.desc(0, src)
+    fbuf = ctypes.create_string_buffer(fields, len(fields))
+    bbuf = ctypes.create_string_buffer(m.blob, len(m.blob))
+    out = ctypes.create_string_buffer(len(msg))
+    crcs = (ctypes.c_uint32 * 5)()
+    dref = ctypes.byref(desc)
+
+    def write():
+        L.ambrycrc_serialize_put_host(dref, fbuf, bbuf, out, len(msg), crcs)
+
+    write()
+    ok_w = out.raw == msg and [crcs[0], crcs[2], crcs[3], crcs[4]] == expect
+
     bl0, bl1 = ranges[-1]  # blob record: 13-B prefix + content
     content_off, content_len = bl0 + 13, bl1 - bl0 - 13
     pre = (ctypes.c_void_p * 1)(base + bl0)
@@ -330,22 +354,21 @@ def run_c1(args, result_fd):
     bcrc = (ctypes.c_uint32 * 1)()
     rec = (ctypes.c_uint32 * 1)()
 
-    def product():
-        crcs = [L.ambrycrc_update(0, base + a, b - a) for a, b in ranges[:-1]]
+    def verify():
+        got = [L.ambrycrc_update(0, base + a, b - a) for a, b in ranges[:-1]]
         bcrc[0] = L.ambrycrc_update(0, base + content_off, content_len)
         L.ambrycrc_put_crcs(None, None, pre, pre_len, bcrc, blen, 1, None, rec)
-        return crcs + [rec[0]]
+        return got + [rec[0]]
 
     orc = Oracle()
 
     def oracle():
         return [orc.crc32(arr[a:b]) for a, b in ranges]
 
-    expect = [int(x, 16) for x in fx["record_crcs"]]
-    ok_p, ok_o = product() == expect, oracle() == expect
+    ok_v, ok_o = verify() == expect, oracle() == expect
     reps = 20000
     res = {}
-    for name, fn in (("product", product), ("oracle", oracle)):
+    for name, fn in (("write", write), ("verify", verify), ("oracle", oracle)):
         fn()
         t0 = time.perf_counter()
         for _ in range(reps):
@@ -353,20 +376,23 @@ def run_c1(args, result_fd):
         res[name] = (time.perf_counter() - t0) / reps * 1e6
     crc_bytes = sum(b - a for a, b in ranges)
     result = {
-        "metric": "us per 64 KiB PUT message, messageformat record CRCs on the CPU (C1)",
-        "value": round(res["product"], 3), "unit": "us", "n_gpus": 0, "steps": reps, "warmup": 1,
-        "ms_per_step": round(res["product"] / 1e3, 6), "higher_is_better": False, "scaling": "none",
-        "vs_baseline": None, "dtype": "u8", "data": "synthetic (splitmix64 bytes; the fixture's message)",
+        "metric": "us per 64 KiB PUT message through messageformat on the CPU (C1)",
+        "value": round(res["write"], 3), "unit": "us", "n_gpus": 0, "steps": reps, "warmup": 1,
+        "ms_per_step": round(res["write"] / 1e3, 6), "higher_is_better": False, "scaling": "none",
+        "vs_baseline": None, "dtype": "u8", "data": "synthetic (splitmix64 bytes; the committed C1 fixture)",
         "config": {"workload": "C1: single 64 KiB blob PUT through messageformat on CPU",
                    "message_bytes": len(msg), "crc_bytes": crc_bytes, "records": fx["records"]},
-        "product": {"us_per_message": round(res["product"], 3), "gibs": round(crc_bytes / res["product"] * 1e6 / 2**30, 2),
-                    "impl": L.ambrycrc_host_impl().decode(), "matches_fixture": ok_p,
-                    "what": "ambrycrc_update per record + ambrycrc_put_crcs for the blob record, one core"},
+        "product_write": {"us_per_message": round(res["write"], 3), "matches_fixture": ok_w,
+                          "impl": L.ambrycrc_host_impl().decode(),
+                          "what": "ambrycrc_serialize_put_host: header, key, records laid out, 4 CRC trailers, one core"},
+        "product_verify": {"us_per_message": round(res["verify"], 3), "matches_fixture": ok_v,
+                           "GiBps": round(crc_bytes / res["verify"] * 1e6 / 2**30, 2),
+                           "what": "ambrycrc_update per record + ambrycrc_put_crcs for the blob record, one core"},
         "cpu_baseline": {"value": round(res["oracle"], 3), "unit": "us per message", "cores": 1, "kind": "port",
                          "matches_fixture": ok_o,
-                         "sample": "the C1 message, 20,000 repetitions; oracle/crc32_ref.c slice-by-8 restating "
-                                   "Crc32.java:55-98 per record"},
-        "note": "both legs pay ~0.3 us of Python->C call overhead per record (5 calls per message)",
+                         "sample": "the C1 message's four record CRCs, 20,000 repetitions; oracle/crc32_ref.c "
+                                   "slice-by-8 restating Crc32.java:55-98"},
+        "note": "every leg pays ~0.3 us of Python->C call overhead per call (write: 1 call; verify: 5; oracle: 4)",
     }
     os.write(result_fd, (json.dumps(result) + "\n").encode())
 
