@@ -19,6 +19,11 @@ for c in $CASES; do
   d=gpurun_out/pmc_cases/$c
   mkdir -p $d
   timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $d/kt -o kt -- python3 tools/probes/pmc_case.py $c --reps $REPS > $d/kt.log 2>&1
+  if [ -n "${KT_ONLY:-}" ]; then
+    find $d/kt -mindepth 2 -name '*.csv' -exec cp {} $d/kt/ \;
+    echo "case $c done (kernel trace only)"
+    continue
+  fi
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $d/fetch -o pmc -- python3 tools/probes/pmc_case.py $c --reps $REPS > $d/fetch.log 2>&1
   timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $d/write -o pmc -- python3 tools/probes/pmc_case.py $c --reps $REPS > $d/write.log 2>&1
   timeout -s KILL 120 rocprofv3 --pmc $SQ GRBM_GUI_ACTIVE --output-format csv -d $d/sq -o pmc -- python3 tools/probes/pmc_case.py $c --reps $REPS > $d/sq.log 2>&1
