@@ -1340,7 +1340,47 @@ __global__ __launch_bounds__(256) void readbw_stream_kernel(const u32x4* __restr
   out[blockIdx.x * blockDim.x + threadIdx.x] = x;
 }
 
+// The group phase's access shape without its arithmetic: chunks of `chunk` bytes back to back,
+// 64/G per wave round (one per G-lane group), wave w taking an equal run of the chunk list; each
+// lane loads its 16 B of four 16G-byte blocks per 64G-byte super-block (group_load_sb), one
+// super-block prefetched. The read roof the 4 KiB records' group rounds are compared against.
+template <int G>
+__global__ __launch_bounds__(1024) void readbw_group_kernel(const uint8_t* __restrict__ base, uint64_t nbytes,
+                                                            uint32_t chunk, uint32_t* __restrict__ out) {
+  constexpr uint32_t S = 64 / G;
+  const uint32_t lane = threadIdx.x & 63u, gl = lane & (G - 1), gi = lane / G;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * gridDim.x + blockIdx.x);
+  const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  const uint64_t n = nbytes / chunk;
+  const uint64_t per = ((n + nwaves - 1) / nwaves + S - 1) / S * S;
+  const uint64_t i0 = wave * per, i1 = i0 + per < n ? i0 + per : n;
+  const uint32_t nsb = (chunk + 64 * G - 1) / (64 * G);
+  uint32_t x = 0;
+  for (uint64_t i = i0; i < i1; i += S) {
+    const uint64_t c = i + gi < i1 ? i + gi : i;
+    const u32x4* q = reinterpret_cast<const u32x4*>(base + c * chunk) + gl;
+    u32x4 nx[4], cur[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) nx[j] = ld16<true>(q + G * j);
+    for (uint32_t sb = 0; sb < nsb; ++sb) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        cur[j] = nx[j];
+        if (sb + 1 < nsb) nx[j] = ld16<true>(q + (sb + 1) * 4 * G + G * j);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) x ^= cur[j].x ^ cur[j].y ^ cur[j].z ^ cur[j].w;
+    }
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = x;
+}
+
 hipError_t launch_readbw(const uint8_t* base, uint64_t nbytes, uint32_t* out, int grid, int variant, hipStream_t s) {
+  if (variant >= 16) {  // group shape: variant = 16 + log2(chunk bytes / 1024) for G = 16 (4 KiB: 18)
+    const uint32_t chunk = 1024u << (variant - 16);
+    hipLaunchKernelGGL(readbw_group_kernel<16>, dim3(grid), dim3(1024), 0, s, base, nbytes, chunk, out);
+    return hipGetLastError();
+  }
   switch (variant) {
     case 0: hipLaunchKernelGGL(readbw_tiles_kernel<false>, dim3(grid), dim3(1024), 0, s, base, nbytes, out); break;
     case 1: hipLaunchKernelGGL(readbw_tiles_kernel<true>, dim3(grid), dim3(1024), 0, s, base, nbytes, out); break;

@@ -404,8 +404,9 @@ int ambrycrc_fill_random_dev(uint8_t* d_dst, uint64_t nbytes, uint64_t seed, uin
 /* Read-bandwidth probe (no CRC arithmetic) over [d_base, d_base+nbytes) with the
  * sweep kernel's grid and access pattern (variant 0: 256 KiB tiles; 1 = the same with
  * nontemporal loads; 2 = plain grid-stride stream; 3 = contiguous per-wave shares, NT;
- * 4 = shares entered at a per-wave rotation, NT). d_out needs grid*1024 words. Measures the achievable HBM
- * read roof the CRC sweep kernel is compared against. */
+ * 4 = shares entered at a per-wave rotation, NT; 16 + k = the group phase's shape for chunks of 1 KiB << k,
+ * 16-lane groups, 4 chunks per wave round, one 1 KiB super-block per group prefetched). d_out needs grid*1024
+ * words. Measures the achievable HBM read roof the CRC kernels are compared against. */
 int ambrycrc_debug_readbw_dev(const uint8_t* d_base, uint64_t nbytes, uint32_t* d_out, int variant,
                               hipStream_t stream);
 
