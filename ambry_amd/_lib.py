@@ -75,6 +75,10 @@ _SIGNATURES = [
     ("ambrycrc_serialize_puts_workspace_bytes", ctypes.c_size_t, [ctypes.c_size_t]),
     ("ambrycrc_serialize_puts_dev", ctypes.c_int,
      [_u8p, ctypes.c_size_t, _u8p, _u8p, _u8p, _u8p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    ("ambrycrc_transform_workspace_bytes", ctypes.c_size_t, [ctypes.c_size_t]),
+    ("ambrycrc_transform_messages_dev", ctypes.c_int,
+     [_u8p, ctypes.c_uint64, _u8p, ctypes.c_size_t, _u8p, ctypes.c_int, _u8p, ctypes.c_uint64, _u8p, _u8p, _u8p,
+      ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
     ("ambrycrc_trailed_workspace_bytes", ctypes.c_size_t, [ctypes.c_size_t]),
     ("ambrycrc_verify_trailed_dev", ctypes.c_int,
      [_u8p, _u8p, _u8p, _u8p, _u8p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),

@@ -869,7 +869,10 @@ size_t ambrycrc_messages_workspace_bytes(size_t m) {
   return jobs + ws_need(j);
 }
 
-namespace {
+}  // extern "C"
+
+namespace ambrycrc {
+namespace detail {
 
 // The device message pipeline (parse -> plan + sweep -> reduce) on `stream`; d_ws holds
 // at least ambrycrc_messages_workspace_bytes(m).
@@ -901,6 +904,11 @@ int enqueue_messages(DevCtx* c, const uint8_t* d_region, uint64_t region_len, co
   if (rc) return rc;
   return hip_err(launch_msg_reduce(a, stream));
 }
+
+}  // namespace detail
+}  // namespace ambrycrc
+
+namespace {
 
 uint32_t rd_be32(const uint8_t* p) {
   return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
@@ -941,6 +949,8 @@ uint64_t message_extent(const uint8_t* p, uint64_t rem) {
 }
 
 }  // namespace
+
+extern "C" {
 
 int ambrycrc_verify_messages_dev(const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off, size_t m,
                                  uint32_t* d_status, uint64_t* d_msg_end, void* d_ws, size_t ws_bytes,

@@ -102,6 +102,15 @@ uint64_t batch_small_max(const DevCtx* c, size_t n);
 int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len, const uint32_t* crc_in,
                   uint32_t* out, size_t n, void* ws, hipStream_t s, uint32_t* exp_fill = nullptr);
 
+// The device message-verify pipeline (parse -> plan + sweep -> reduce) on `stream`; d_ws holds at
+// least ambrycrc_messages_workspace_bytes(m). d_msg_end may be null.
+int enqueue_messages(DevCtx* c, const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off, size_t m,
+                     uint32_t* d_status, uint64_t* d_msg_end, void* d_ws, hipStream_t stream);
+// The PUT serialization pipeline (layout -> copy -> plan + CRC -> seal); d_ws holds at least
+// ambrycrc_serialize_puts_workspace_bytes(m).
+int enqueue_serialize(DevCtx* c, const ::ambrycrc_put_desc* d_desc, size_t m, const uint8_t* d_fields,
+                      const uint8_t* d_blobs, uint8_t* d_out, uint64_t* d_msg_len, void* d_ws, hipStream_t stream);
+
 // Holds c->ws_mu for the lifetime of a *_dev call that uses the default workspace (d_ws ==
 // NULL); a call with its own workspace takes no lock.
 struct WsLease {

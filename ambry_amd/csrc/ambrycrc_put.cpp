@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 
+#include <algorithm>
+
 #include "../../include/ambrycrc.h"
 #include "ambrycrc_ctx.h"
 #include "crc32_kernels.h"
@@ -23,6 +25,65 @@ size_t put_jobs_bytes(size_t m) {
 }
 
 }  // namespace
+
+namespace ambrycrc {
+namespace detail {
+
+int enqueue_serialize(DevCtx* c, const ::ambrycrc_put_desc* d_desc, size_t m, const uint8_t* d_fields,
+                      const uint8_t* d_blobs, uint8_t* d_out, uint64_t* d_msg_len, void* d_ws, hipStream_t stream) {
+  const size_t j = (size_t)kPutSlots * m;
+  uint8_t* w = static_cast<uint8_t*>(d_ws);
+  PutArgs a;
+  a.desc = d_desc;
+  a.m = m;
+  a.out = d_out;
+  a.fields = d_fields;
+  a.blobs = d_blobs;
+  a.cp_src = reinterpret_cast<uint64_t*>(w);
+  a.cp_dst = a.cp_src + j;
+  a.cp_len = a.cp_dst + j;
+  a.cp_cost = a.cp_len + j;
+  a.crc_off = a.cp_cost + j;
+  a.crc_len = a.crc_off + j;
+  uint32_t* crc = reinterpret_cast<uint32_t*>(a.crc_len + j);
+  a.crc = crc;
+  a.msg_len = d_msg_len;
+  void* batch_ws = w + put_jobs_bytes(m);
+  if (launch_put_layout(a, stream) != hipSuccess) return AMBRYCRC_EHIP;
+  if (d_fields || d_blobs) {
+    // cost offsets of the copy jobs: the plan kernel's exclusive scan (no small-chunk classes);
+    // its per-chunk output initialisation lands in `crc`, overwritten by the CRC batch below
+    PlanArgs p;
+    p.off = a.cp_dst;
+    p.len = a.cp_cost;
+    p.crc_in = nullptr;
+    p.n = (uint32_t)j;
+    p.byte_start = static_cast<uint64_t*>(batch_ws);
+    const size_t blocks = (j + kPlanPerBlock - 1) / kPlanPerBlock;
+    p.block_sum = p.byte_start + j + 1;
+    p.block_small = p.block_sum + blocks;
+    p.small_total = p.block_small + blocks;
+    p.small_idx = reinterpret_cast<uint32_t*>(p.small_total + 5);
+    p.crc_stage = nullptr;
+    p.out = crc;
+    p.small_max = 0;
+    if (launch_plan(p, stream) != hipSuccess) return AMBRYCRC_EHIP;
+    CopyArgs ca;
+    ca.src = a.cp_src;
+    ca.dst_off = a.cp_dst;
+    ca.len = a.cp_len;
+    ca.start = p.byte_start;
+    ca.n = (uint32_t)j;
+    ca.dst = d_out;
+    if (launch_gather_copy(ca, c->num_cu * 8, stream) != hipSuccess) return AMBRYCRC_EHIP;
+  }
+  const int rc = enqueue_batch(c, d_out, a.crc_off, a.crc_len, nullptr, crc, j, batch_ws, stream);
+  if (rc) return rc;
+  return hip_err(launch_put_seal(a, stream));
+}
+
+}  // namespace detail
+}  // namespace ambrycrc
 
 extern "C" {
 
@@ -74,57 +135,68 @@ int ambrycrc_serialize_puts_dev(const ambrycrc_put_desc* d_desc, size_t m, const
   DevCtx* c = ctx_current();
   if (!c) return AMBRYCRC_ENOINIT;
   WsLease lease;
-  int rc = lease.acquire(c, stream, &d_ws, ws_bytes, ambrycrc_serialize_puts_workspace_bytes(m));
+  const int rc = lease.acquire(c, stream, &d_ws, ws_bytes, ambrycrc_serialize_puts_workspace_bytes(m));
   if (rc) return rc;
-  const size_t j = (size_t)kPutSlots * m;
+  return enqueue_serialize(c, d_desc, m, d_fields, d_blobs, d_out, d_msg_len, d_ws, stream);
+}
+
+size_t ambrycrc_transform_workspace_bytes(size_t m) {
+  const size_t own = (m * (sizeof(ambrycrc_put_desc) + sizeof(uint32_t)) + 255) & ~size_t(255);
+  return own + ws_need(m) + std::max(ambrycrc_messages_workspace_bytes(m), ambrycrc_serialize_puts_workspace_bytes(m));
+}
+
+int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off, size_t m,
+                                    const int16_t* d_life_version, int header_version, uint8_t* d_out,
+                                    uint64_t out_cap, uint64_t* d_out_off, uint64_t* d_out_len, uint32_t* d_status,
+                                    void* d_ws, size_t ws_bytes, hipStream_t stream) {
+  if (m == 0) return AMBRYCRC_OK;
+  if (!d_region || !d_msg_off || !d_out || !d_out_len || !d_status || header_version < 1 || header_version > 3 ||
+      (size_t)kPutSlots * m >= (1ull << 31))
+    return AMBRYCRC_EINVAL;
+  DevCtx* c = ctx_current();
+  if (!c) return AMBRYCRC_ENOINIT;
+  WsLease lease;
+  int rc = lease.acquire(c, stream, &d_ws, ws_bytes, ambrycrc_transform_workspace_bytes(m));
+  if (rc) return rc;
+  // workspace: desc[m] | scan scratch (uint32 per message) | plan workspace for the m lengths |
+  //            the verify pipeline's, then the serializer's (one after the other on the stream)
   uint8_t* w = static_cast<uint8_t*>(d_ws);
-  PutArgs a;
-  a.desc = d_desc;
-  a.m = m;
-  a.out = d_out;
-  a.fields = d_fields;
-  a.blobs = d_blobs;
-  a.cp_src = reinterpret_cast<uint64_t*>(w);
-  a.cp_dst = a.cp_src + j;
-  a.cp_len = a.cp_dst + j;
-  a.cp_cost = a.cp_len + j;
-  a.crc_off = a.cp_cost + j;
-  a.crc_len = a.crc_off + j;
-  uint32_t* crc = reinterpret_cast<uint32_t*>(a.crc_len + j);
-  a.crc = crc;
-  a.msg_len = d_msg_len;
-  void* batch_ws = w + put_jobs_bytes(m);
-  if (launch_put_layout(a, stream) != hipSuccess) return AMBRYCRC_EHIP;
-  if (d_fields || d_blobs) {
-    // cost offsets of the copy jobs: the plan kernel's exclusive scan (no small-chunk classes);
-    // its per-chunk output initialisation lands in `crc`, overwritten by the CRC batch below
-    PlanArgs p;
-    p.off = a.cp_dst;
-    p.len = a.cp_cost;
-    p.crc_in = nullptr;
-    p.n = (uint32_t)j;
-    p.byte_start = static_cast<uint64_t*>(batch_ws);
-    const size_t blocks = (j + kPlanPerBlock - 1) / kPlanPerBlock;
-    p.block_sum = p.byte_start + j + 1;
-    p.block_small = p.block_sum + blocks;
-    p.small_total = p.block_small + blocks;
-    p.small_idx = reinterpret_cast<uint32_t*>(p.small_total + 5);
-    p.crc_stage = nullptr;
-    p.out = crc;
-    p.small_max = 0;
-    if (launch_plan(p, stream) != hipSuccess) return AMBRYCRC_EHIP;
-    CopyArgs ca;
-    ca.src = a.cp_src;
-    ca.dst_off = a.cp_dst;
-    ca.len = a.cp_len;
-    ca.start = p.byte_start;
-    ca.n = (uint32_t)j;
-    ca.dst = d_out;
-    if (launch_gather_copy(ca, c->num_cu * 8, stream) != hipSuccess) return AMBRYCRC_EHIP;
-  }
-  rc = enqueue_batch(c, d_out, a.crc_off, a.crc_len, nullptr, crc, j, batch_ws, stream);
+  TransformArgs t;
+  t.region = d_region;
+  t.region_len = region_len;
+  t.msg_off = d_msg_off;
+  t.m = m;
+  t.life = d_life_version;
+  t.header_version = header_version;
+  t.desc = reinterpret_cast<ambrycrc_put_desc*>(w);
+  t.out_len = d_out_len;
+  t.out_off = d_out_off;
+  t.status = d_status;
+  t.out_cap = out_cap;
+  uint32_t* scan_out = reinterpret_cast<uint32_t*>(w + m * sizeof(ambrycrc_put_desc));
+  uint8_t* plan_ws = w + ((m * (sizeof(ambrycrc_put_desc) + sizeof(uint32_t)) + 255) & ~size_t(255));
+  void* shared = plan_ws + ws_need(m);
+  rc = enqueue_messages(c, d_region, region_len, d_msg_off, m, d_status, nullptr, shared, stream);
   if (rc) return rc;
-  return hip_err(launch_put_seal(a, stream));
+  if (launch_transform_desc(t, stream) != hipSuccess) return AMBRYCRC_EHIP;
+  // packed output offsets: the plan kernel's exclusive scan of the output lengths
+  PlanArgs p;
+  p.off = d_msg_off;
+  p.len = d_out_len;
+  p.crc_in = nullptr;
+  p.n = (uint32_t)m;
+  p.byte_start = reinterpret_cast<uint64_t*>(plan_ws);
+  const size_t blocks = (m + kPlanPerBlock - 1) / kPlanPerBlock;
+  p.block_sum = p.byte_start + m + 1;
+  p.block_small = p.block_sum + blocks;
+  p.small_total = p.block_small + blocks;
+  p.small_idx = reinterpret_cast<uint32_t*>(p.small_total + 5);
+  p.crc_stage = nullptr;
+  p.out = scan_out;
+  p.small_max = 0;
+  if (launch_plan(p, stream) != hipSuccess) return AMBRYCRC_EHIP;
+  if (launch_transform_place(t, p.byte_start, stream) != hipSuccess) return AMBRYCRC_EHIP;
+  return enqueue_serialize(c, t.desc, m, d_region, d_region, d_out, nullptr, shared, stream);
 }
 
 }  // extern "C"

@@ -147,6 +147,24 @@ struct CopyArgs {
   uint8_t* dst;
 };
 
+// ValidatingTransformer (message_kernels.hip): stored messages -> put descriptors -> serialization.
+struct TransformArgs {
+  const uint8_t* region;
+  uint64_t region_len;
+  const uint64_t* msg_off;        // [m]
+  uint64_t m;
+  const int16_t* life;            // [m] or null
+  int header_version;             // of the output
+  ::ambrycrc_put_desc* desc;      // [m] built here (header_version 0: not transformed)
+  uint64_t* out_len;              // [m]
+  uint64_t* out_off;              // [m] or null
+  uint32_t* status;               // [m] in: verify bits; out: + NOT_PUT / BAD_RECORD / NO_ROOM
+  uint64_t out_cap;
+};
+
+hipError_t launch_transform_desc(const TransformArgs& a, hipStream_t s);
+hipError_t launch_transform_place(const TransformArgs& a, const uint64_t* start, hipStream_t s);
+
 hipError_t launch_put_layout(const PutArgs& a, hipStream_t s);
 hipError_t launch_put_seal(const PutArgs& a, hipStream_t s);
 hipError_t launch_gather_copy(const CopyArgs& a, int grid, hipStream_t s);

@@ -20,6 +20,7 @@
 #include "../../include/ambrycrc.h"
 #include "crc32_kernels.h"
 #include "crc32_layout.h"
+#include "put_layout.h"
 
 namespace ambrycrc {
 
@@ -277,6 +278,138 @@ __global__ __launch_bounds__(256) void trailer_verify_kernel(TrailerArgs a) {
   const bool bad = a.force[i] || a.crc[i] != a.expected[i];
   if (a.mismatch) a.mismatch[i] = bad ? 1 : 0;
   if (bad && a.count) atomicAdd(a.count, 1u);
+}
+
+// ---------------------------------------------------------------- transform
+// ValidatingTransformer.transform (ValidatingTransformer.java:46-104), after the verify pipeline
+// set each message's status: one thread per message deserializes a clean PUT's fields the way
+// deserializeBlobEncryptionKey / deserializeBlobProperties / deserializeUserMetadata /
+// deserializeBlob read them (MessageFormatRecord.java:1568-1833) and describes the message
+// PutMessageFormatInputStream would write from them (the fields stay in the region: the
+// serializer copies them from there).
+__global__ __launch_bounds__(256) void transform_desc_kernel(TransformArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.m) return;
+  uint32_t st = a.status[i];
+  ambrycrc_put_desc d;
+  __builtin_memset(&d, 0, sizeof(d));  // header_version 0: nothing to write
+  uint64_t out_len = 0;
+  if (st == 0) {  // verified: the header and every record lie inside the region
+    const uint64_t off = a.msg_off[i];
+    const uint8_t* p = a.region + off;
+    const uint32_t v = be16(p);
+    const uint32_t hs = v == 1 ? 34u : v == 2 ? 38u : 40u;
+    int32_t rel[5];
+    int64_t total;
+    uint32_t life = 0;
+    if (v == 1) {
+      total = (int64_t)be64(p + 2);
+      rel[0] = -1;
+      for (int k = 0; k < 4; ++k) rel[k + 1] = (int32_t)be32(p + 10 + 4 * k);
+    } else if (v == 2) {
+      total = (int64_t)be64(p + 2);
+      for (int k = 0; k < 5; ++k) rel[k] = (int32_t)be32(p + 10 + 4 * k);
+    } else {
+      life = be16(p + 2);
+      total = (int64_t)be64(p + 4);
+      for (int k = 0; k < 5; ++k) rel[k] = (int32_t)be32(p + 12 + 4 * k);
+    }
+    const int32_t enc = rel[0], bp = rel[1], upd = rel[2], um = rel[3], blob = rel[4];
+    if (upd != -1 || bp == -1 || um == -1 || blob == -1) {
+      st |= AMBRYCRC_MSG_NOT_PUT;
+    } else {
+      const int64_t first = enc != -1 ? enc : bp;
+      const int64_t end = first + total;  // message end, relative
+      bool ok = first >= (int64_t)hs;
+      uint32_t enc_len = 0;
+      if (enc != -1) {  // BlobEncryptionKey_Format_V1: version, int size, key, CRC
+        enc_len = be32(p + enc + 2);
+        ok = ok && (int64_t)enc + 6 + enc_len + 8 == bp;
+      }
+      const int64_t props_len = (int64_t)um - bp - 2 - 8;  // BlobProperties_Format_V1: version, props, CRC
+      const uint32_t um_len = be32(p + um + 2);             // UserMetadata_Format_V1: version, int size, ..., CRC
+      ok = ok && props_len >= 0 && (int64_t)um + 6 + um_len + 8 == blob;
+      const uint32_t bv = be16(p + blob);  // Blob_Format_V1 / V2 / V3 (:1668-1833)
+      uint32_t head = 0, type = 0, comp = 0;
+      uint64_t size = 0;
+      if (bv == 1) {
+        size = be64(p + blob + 2);
+        head = 10;
+      } else if (bv == 2) {
+        type = be16(p + blob + 2);
+        size = be64(p + blob + 4);
+        head = 12;
+      } else if (bv == 3) {
+        type = be16(p + blob + 2);
+        comp = p[blob + 4] == 1 ? 1u : 0u;  // `readByte() == 1`
+        size = be64(p + blob + 5);
+        head = 13;
+      } else {
+        ok = false;
+      }
+      // BlobType has two values (DataBlob, MetadataBlob); sizes above Integer.MAX_VALUE throw
+      ok = ok && type < 2 && size <= 0x7FFFFFFFull && (int64_t)blob + head + (int64_t)size + 8 == end;
+      if (!ok) {
+        st |= AMBRYCRC_MSG_BAD_RECORD;
+      } else {
+        d.key_src = off + hs;
+        d.key_len = (uint32_t)(first - hs);
+        const bool keep_enc = enc != -1 && a.header_version >= 2;
+        d.enckey_src = keep_enc ? off + enc + 6 : 0;
+        d.enckey_len = keep_enc ? (int32_t)enc_len : -1;
+        d.props_src = off + bp + 2;
+        d.props_len = (uint32_t)props_len;
+        d.usermeta_src = off + um + 6;
+        d.usermeta_len = um_len;
+        d.blob_src = off + blob + head;
+        d.blob_len = size;
+        d.life_version = a.life ? a.life[i] : (int16_t)life;
+        d.blob_type = (int16_t)type;
+        d.compressed = (uint8_t)comp;
+        d.header_version = (uint8_t)a.header_version;
+        PutLayout L;
+        out_len = put_layout(d, L) ? L.length : 0;
+        if (!out_len) {
+          d.header_version = 0;
+          st |= AMBRYCRC_MSG_BAD_RECORD;
+        }
+      }
+    }
+  }
+  a.desc[i] = d;
+  a.out_len[i] = out_len;
+  a.status[i] = st;
+}
+
+// Packed placement: message i goes to start[i] (exclusive scan of out_len), if it fits.
+__global__ __launch_bounds__(256) void transform_place_kernel(TransformArgs a, const uint64_t* __restrict__ start) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.m) return;
+  const uint64_t len = a.out_len[i];
+  uint64_t at = ~0ull;
+  if (len) {
+    if (start[i] + len <= a.out_cap) {
+      at = start[i];
+      a.desc[i].out_off = at;
+    } else {
+      a.desc[i].header_version = 0;
+      a.out_len[i] = 0;
+      a.status[i] |= AMBRYCRC_MSG_NO_ROOM;
+    }
+  }
+  if (a.out_off) a.out_off[i] = at;
+}
+
+hipError_t launch_transform_desc(const TransformArgs& a, hipStream_t s) {
+  if (a.m == 0) return hipSuccess;
+  hipLaunchKernelGGL(transform_desc_kernel, dim3((uint32_t)((a.m + 255) / 256)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_transform_place(const TransformArgs& a, const uint64_t* start, hipStream_t s) {
+  if (a.m == 0) return hipSuccess;
+  hipLaunchKernelGGL(transform_place_kernel, dim3((uint32_t)((a.m + 255) / 256)), dim3(256), 0, s, a, start);
+  return hipGetLastError();
 }
 
 hipError_t launch_trailer_parse(const TrailerArgs& a, hipStream_t s) {

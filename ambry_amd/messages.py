@@ -120,3 +120,43 @@ def serialize_dev(descs, out, fields=None, blobs=None, msg_len=None, stream=None
     ptr = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
     check(lib().ambrycrc_serialize_puts_dev(ptr(descs), m, ptr(fields), ptr(blobs), ptr(out), ptr(msg_len), None, 0,
                                             ctypes.c_void_p(_stream_handle(stream))), "ambrycrc_serialize_puts_dev")
+
+
+# status bits added by the transform (include/ambrycrc.h)
+MSG_NOT_PUT = 1 << 10
+MSG_BAD_RECORD = 1 << 11
+MSG_NO_ROOM = 1 << 12
+
+
+def transform_dev(region, msg_off, header_version: int = 3, life_version=None, out=None, stream=None):
+    """ambrycrc_transform_messages_dev -- ValidatingTransformer.transform for a batch of stored
+    messages in HBM: every clean PUT re-serialized at `header_version` (and life version
+    life_version[i], an int16 CUDA tensor, or the stored one), packed in order into `out` (a uint8
+    CUDA tensor; default: region bytes + 6 per message, enough for any header change).
+    Returns (out, out_off int64[m], out_len int64[m], status int32[m])."""
+    import torch
+
+    from .device import _stream_handle
+
+    if region.dtype != torch.uint8 or not region.is_cuda:
+        raise TypeError("region must be a uint8 CUDA tensor")
+    if msg_off.dtype != torch.int64 or not msg_off.is_cuda or not msg_off.is_contiguous() or \
+            msg_off.device != region.device:
+        raise TypeError("msg_off must be a contiguous int64 CUDA tensor on the region's device")
+    m = msg_off.numel()
+    if life_version is not None and (life_version.dtype != torch.int16 or life_version.numel() != m
+                                     or not life_version.is_cuda or not life_version.is_contiguous()):
+        raise TypeError("life_version must be a contiguous int16 CUDA tensor of m elements")
+    if out is None:
+        out = torch.empty(region.numel() + 6 * m, dtype=torch.uint8, device=region.device)
+    elif out.dtype != torch.uint8 or not out.is_cuda or not out.is_contiguous() or out.device != region.device:
+        raise TypeError("out must be a contiguous uint8 CUDA tensor on the region's device")
+    out_off = torch.empty(m, dtype=torch.int64, device=region.device)
+    out_len = torch.empty(m, dtype=torch.int64, device=region.device)
+    status = torch.empty(m, dtype=torch.int32, device=region.device)
+    ptr = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    check(lib().ambrycrc_transform_messages_dev(ptr(region), region.numel(), ptr(msg_off), m, ptr(life_version),
+                                                header_version, ptr(out), out.numel(), ptr(out_off), ptr(out_len),
+                                                ptr(status), None, 0, ctypes.c_void_p(_stream_handle(stream))),
+          "ambrycrc_transform_messages_dev")
+    return out, out_off, out_len, status

@@ -220,6 +220,31 @@ int ambrycrc_serialize_puts_dev(const ambrycrc_put_desc* d_desc, size_t m, const
                                 const uint8_t* d_blobs, uint8_t* d_out, uint64_t* d_msg_len, void* d_ws,
                                 size_t ws_bytes, hipStream_t stream);
 
+/* Status bits ambrycrc_transform_messages_dev adds to the AMBRYCRC_MSG_* verify bits. */
+#define AMBRYCRC_MSG_NOT_PUT (1u << 10)     /* an update record: "Message cannot be anything rather than put record" */
+#define AMBRYCRC_MSG_BAD_RECORD (1u << 11)  /* a record's own fields disagree with its span, an unknown blob record
+                                               version, a blob type ordinal >= 2 or a size > Integer.MAX_VALUE
+                                               (the DataCorrupt / IOException cases of deserializeBlob*) */
+#define AMBRYCRC_MSG_NO_ROOM (1u << 12)     /* the re-serialized message did not fit in out_cap */
+
+/* Replication's ValidatingTransformer.transform (ambry-messageformat/.../ValidatingTransformer.java:46-104)
+ * for m stored messages at d_msg_off[i] in [d_region, d_region + region_len): every CRC is verified
+ * (ambrycrc_verify_messages_dev), update records are refused, the fields are deserialized
+ * (key, encryption key, properties, user metadata, blob content / type / compression), and every
+ * clean PUT is re-serialized by PutMessageFormatInputStream's layout with header version
+ * `header_version` (1, 2 or 3: MessageFormatRecord.headerVersionToUse; V1 drops the encryption key,
+ * as createStreamWithMessageHeaderV1 does) and life version d_life_version[i] (nullable: the
+ * stored header's, 0 for V1/V2) -- all CRCs recomputed -- packed in message order into
+ * [d_out, d_out + out_cap). Outputs (device arrays of m): d_status (AMBRYCRC_MSG_* bits, 0 =
+ * transformed), d_out_len (0 when not transformed), d_out_off (nullable; the message's offset in
+ * d_out). Asynchronous on `stream`; d_ws >= ambrycrc_transform_workspace_bytes(m) or NULL. The
+ * store-key comparison with the index entry stays with the caller (it owns the StoreKey type). */
+size_t ambrycrc_transform_workspace_bytes(size_t m);
+int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off, size_t m,
+                                    const int16_t* d_life_version, int header_version, uint8_t* d_out,
+                                    uint64_t out_cap, uint64_t* d_out_off, uint64_t* d_out_len, uint32_t* d_status,
+                                    void* d_ws, size_t ws_bytes, hipStream_t stream);
+
 /* ------------------------------------- CRC-trailered records (store files, headers) */
 
 /* Item i = [off[i], off[i] + len[i]) ends in the big-endian 8-B CRC (a long, high word zero)

@@ -23,6 +23,7 @@ Restated from ambry-messageformat/src/main/java/com/github/ambry/messageformat/:
     :257-303   deserializeBlobAll: header verified first (corrupt header -> no record parsed),
                then encryption key (if present), blob properties, user metadata, blob.
   PutMessageFormatInputStream.java:76-124,133-162 (record order and relative offsets)
+  ValidatingTransformer.java:46-104 (transform: verify, deserialize, re-serialize a PUT)
   BlobPropertiesSerDe.java:43-103 (VERSION_5 layout)
 Every record's CRC covers [record start, record end - 8) and is stored as a
 big-endian long with the upper 32 bits zero. CRCs come from zlib.crc32, the
@@ -46,6 +47,8 @@ USERMETA_CRC = 1 << 4
 BLOB_CRC = 1 << 5
 BAD_VERSION = 1 << 8
 BAD_LAYOUT = 1 << 9
+NOT_PUT = 1 << 10      # transform only: an update record
+BAD_RECORD = 1 << 11   # transform only: record fields disagree with the span, bad blob version/type/size
 
 RECORD_BITS = (ENCKEY_CRC, PROPS_CRC, UPDATE_CRC, USERMETA_CRC, BLOB_CRC)  # slot order enc, bp, upd, um, blob
 
@@ -123,13 +126,14 @@ def update_record_v3(account=101, container=5, update_ms=1_700_000_000_123, kind
 
 
 def put_message(key: bytes, props: bytes, usermeta: bytes, content: bytes, version=3, enc_key=None, life=0,
-                blob_version=None, compressed=False) -> bytes:
+                blob_version=None, compressed=False, blob_type=0) -> bytes:
     """PutMessageFormatInputStream: header, key, [encryption key], properties, user metadata, blob."""
     h = HEADER_SIZE[version]
     enc = enckey_record(enc_key) if (enc_key is not None and version >= 2) else b""
     pr = props_record(props)
     um = usermeta_record(usermeta)
-    bl = blob_record(content, version=blob_version or (3 if version != 1 else 3), compressed=compressed)
+    bl = blob_record(content, version=blob_version or (3 if version != 1 else 3), blob_type=blob_type,
+                     compressed=compressed)
     total = len(enc) + len(pr) + len(um) + len(bl)
     enc_off = h + len(key) if enc else INVALID
     bp_off = h + len(key) + len(enc)
@@ -210,3 +214,63 @@ def verify_message(region: bytes, off: int):
         if zlib.crc32(region[off + s:off + e - CRC_SIZE]) != stored:
             status |= RECORD_BITS[k]
     return status, off + end
+
+
+def blob_record_v1(content: bytes) -> bytes:
+    """Blob_Format_V1 (MessageFormatRecord.java:1668-1716): short 1, long size, content, CRC."""
+    body = struct.pack(">hq", 1, len(content)) + content
+    return body + _crc_long(body)
+
+
+def transform_message(region: bytes, off: int, life=None, version: int = 3):
+    """ValidatingTransformer.transform (ValidatingTransformer.java:46-104): (status, bytes or None).
+
+    Verify every CRC (verify_message); refuse update records ("Message cannot be anything rather
+    than put record"); deserialize the encryption key, properties, user metadata and blob
+    (deserializeBlob* :1568-1833: blob record V1/V2/V3, type ordinal < 2, size <= MAX_INT, the
+    fields consistent with the record spans); re-serialize with PutMessageFormatInputStream at
+    header `version` (V1 drops the encryption key) and lifeVersion `life` (msgInfo's; None: the
+    stored header's, 0 for V1/V2)."""
+    status, end = verify_message(region, off)
+    if status:
+        return status, None
+    v, total, rel = parse_header(region, off)
+    enc, bp, upd, um, blob = rel
+    if upd != INVALID or bp == INVALID or um == INVALID or blob == INVALID:
+        return NOT_PUT, None
+    h = HEADER_SIZE[v]
+    first = enc if enc != INVALID else bp
+    key = region[off + h:off + first]
+    enc_key = None
+    if enc != INVALID:
+        n = _be32(region, off + enc + 2)
+        if n < 0 or enc + 6 + n + 8 != bp:
+            return BAD_RECORD, None
+        enc_key = region[off + enc + 6:off + enc + 6 + n]
+    if um - 8 < bp + 2:
+        return BAD_RECORD, None
+    props = region[off + bp + 2:off + um - 8]
+    n = _be32(region, off + um + 2)
+    if n < 0 or um + 6 + n + 8 != blob:
+        return BAD_RECORD, None
+    usermeta = region[off + um + 6:off + um + 6 + n]
+    bv = _be16(region, off + blob)
+    btype, comp = 0, False
+    if bv == 1:
+        size, head = _be64(region, off + blob + 2), 10
+    elif bv == 2:
+        btype, size, head = _be16(region, off + blob + 2), _be64(region, off + blob + 4), 12
+    elif bv == 3:
+        btype = _be16(region, off + blob + 2)
+        comp = region[off + blob + 4] == 1
+        size, head = _be64(region, off + blob + 5), 13
+    else:
+        return BAD_RECORD, None
+    if not (0 <= btype < 2) or not (0 <= size <= 0x7FFFFFFF) or blob + head + size + 8 != first + total:
+        return BAD_RECORD, None
+    content = region[off + blob + head:off + blob + head + size]
+    stored_life = _be16(region, off + 2) if v == 3 else 0
+    out = put_message(key, props, usermeta, content, version=version,
+                      enc_key=enc_key if version >= 2 else None, life=stored_life if life is None else life,
+                      compressed=comp, blob_type=btype)
+    return 0, out

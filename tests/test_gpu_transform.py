@@ -1,0 +1,133 @@
+"""Replication's ValidatingTransformer on the GPU (ambrycrc_transform_messages_dev): stored
+messages of every header version, with and without encryption keys, blob records V1/V2/V3,
+corrupted ones, update records and bad blob types, re-serialized at header V3, V2 and V1 with
+every CRC recomputed. Byte-exact against oracle/message_format.py's transform_message, which
+restates ValidatingTransformer.java:46-104; outputs packed in message order; every output
+verifies clean."""
+import struct
+
+import numpy as np
+import pytest
+
+from datagen import stream_bytes
+from test_gpu_put import mf  # noqa: F401  (fixture)
+
+pytestmark = pytest.mark.gpu
+
+
+def _blob_v1_message(mf, key, props, um, content, version):
+    """A PUT whose blob record is Blob_Format_V1 (stored by old servers)."""
+    h = mf.HEADER_SIZE[version]
+    pr, ur, bl = mf.props_record(props), mf.usermeta_record(um), mf.blob_record_v1(content)
+    bp = h + len(key)
+    return mf.header(version, len(pr) + len(ur) + len(bl), mf.INVALID, bp, mf.INVALID, bp + len(pr),
+                     bp + len(pr) + len(ur), 0) + key + pr + ur + bl
+
+
+def build_region(mf, n, seed):
+    rng = np.random.default_rng(seed)
+    msgs = []
+    for i in range(n):
+        kind = rng.random()
+        v = int(rng.choice([1, 2, 3]))
+        key = mf.store_key("rep-%d" % i)
+        blen = int(rng.choice([0, 1, 100, 4096, 4109, 70000]))
+        content = stream_bytes(seed + i, 0, blen).tobytes()
+        um = stream_bytes(seed + i, 1 << 20, int(rng.choice([0, 7, 1000]))).tobytes()
+        props = mf.blob_properties_bytes(blen, service_id="s%d" % (i % 7))
+        if kind < 0.08:
+            m = mf.update_message(key, version=3)
+        elif kind < 0.14:
+            m = _blob_v1_message(mf, key, props, um, content, 1 if v == 1 else 2)
+        else:
+            enc = stream_bytes(seed, 9, 32).tobytes() if (v >= 2 and rng.random() < 0.4) else None
+            bt = int(rng.choice([0, 1, 2], p=[0.6, 0.35, 0.05]))
+            m = mf.put_message(key, props, um, content, version=v, enc_key=enc, life=int(rng.integers(0, 4)) if v == 3
+                               else 0, blob_version=int(rng.choice([2, 3])), compressed=bool(rng.random() < 0.3),
+                               blob_type=bt)
+        m = bytearray(m)
+        if rng.random() < 0.07:  # corrupt a byte somewhere
+            m[int(rng.integers(0, len(m)))] ^= 0x40
+        msgs.append(bytes(m))
+    region, offs = bytearray(), []
+    for m in msgs:
+        region += bytes(int(rng.integers(0, 5)))  # gaps and odd alignment between messages
+        offs.append(len(region))
+        region += m
+    return bytes(region), offs
+
+
+@pytest.mark.parametrize("version", [3, 2, 1])
+def test_transform_matches_oracle(gpu, mf, version):
+    import torch
+
+    from ambry_amd.messages import transform_dev
+
+    region, offs = build_region(mf, 600, seed=31 + version)
+    m = len(offs)
+    life = np.random.default_rng(version).integers(0, 9, size=m).astype(np.int16)
+    use_life = version != 2  # V2 run: the stored life versions
+    dev = torch.frombuffer(bytearray(region), dtype=torch.uint8).cuda()
+    out, out_off, out_len, status = transform_dev(
+        dev, torch.tensor(offs, dtype=torch.int64, device="cuda"), header_version=version,
+        life_version=torch.from_numpy(life).cuda() if use_life else None)
+    torch.cuda.synchronize()
+    out_h = out.cpu().numpy().tobytes()
+    st, oo, ol = status.cpu().numpy().view(np.uint32), out_off.cpu().numpy(), out_len.cpu().numpy()
+    pos, kinds = 0, set()
+    for i, o in enumerate(offs):
+        exp_st, exp = mf.transform_message(region, o, life=int(life[i]) if use_life else None, version=version)
+        assert int(st[i]) == exp_st, i
+        kinds.add(exp_st)
+        if exp is None:
+            assert ol[i] == 0 and oo[i] == -1
+            continue
+        assert oo[i] == pos and ol[i] == len(exp), i
+        assert out_h[pos:pos + len(exp)] == exp, i
+        assert mf.verify_message(out_h, pos) == (0, pos + len(exp))
+        pos += len(exp)
+    assert 0 in kinds and mf.NOT_PUT in kinds and mf.BAD_RECORD in kinds and len(kinds) >= 4
+
+
+def test_transform_out_of_room(gpu, mf):
+    import torch
+
+    from ambry_amd.messages import MSG_NO_ROOM, transform_dev
+
+    msgs = [mf.put_message(mf.store_key("k%d" % i), mf.blob_properties_bytes(1000), b"u", bytes(1000))
+            for i in range(10)]
+    region = b"".join(msgs)
+    offs = np.cumsum([0] + [len(x) for x in msgs[:-1]]).tolist()
+    cap = len(msgs[0]) * 4 + 10  # room for four
+    dev = torch.frombuffer(bytearray(region), dtype=torch.uint8).cuda()
+    out = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+    _, out_off, out_len, status = transform_dev(dev, torch.tensor(offs, dtype=torch.int64, device="cuda"), out=out)
+    torch.cuda.synchronize()
+    st = status.cpu().numpy().tolist()
+    assert st[:4] == [0] * 4 and all(s == MSG_NO_ROOM for s in st[4:])
+    assert out_len.cpu().numpy().tolist() == [len(msgs[0])] * 4 + [0] * 6
+    assert out.cpu().numpy().tobytes()[:4 * len(msgs[0])] == b"".join(msgs[:4])
+
+
+def test_transform_large_batch_group_phase(gpu, mf):
+    """3,500 messages: 17,500 CRC jobs engage the group phase in both the verify and the re-serialize."""
+    import torch
+
+    from ambry_amd.messages import transform_dev
+
+    region, offs = build_region(mf, 3500, seed=77)
+    dev = torch.frombuffer(bytearray(region), dtype=torch.uint8).cuda()
+    out, out_off, out_len, status = transform_dev(dev, torch.tensor(offs, dtype=torch.int64, device="cuda"))
+    torch.cuda.synchronize()
+    st = status.cpu().numpy().view(np.uint32)
+    oo, ol = out_off.cpu().numpy(), out_len.cpu().numpy()
+    out_h = out.cpu().numpy().tobytes()
+    for i in range(0, len(offs), 7):
+        exp_st, exp = mf.transform_message(region, offs[i], version=3)
+        assert int(st[i]) == exp_st
+        if exp is not None:
+            assert out_h[oo[i]:oo[i] + ol[i]] == exp
+    good = np.nonzero(st == 0)[0]
+    status2, _ = gpu.verify_messages(out, torch.from_numpy(oo[good]).cuda())
+    torch.cuda.synchronize()
+    assert int(status2.abs().sum().item()) == 0
