@@ -93,10 +93,59 @@ def run(m, blob_bytes, reps, in_place):
             "parity": "3 sampled messages byte-exact vs ambrycrc_serialize_put_host; all verify clean on the GPU"}
 
 
+def run_transform(m, blob_bytes, reps):
+    """ValidatingTransformer (ambrycrc_transform_messages_dev) over a region of m stored V3 PUTs (made by
+    the serializer), re-serialized at V3: verify + deserialize + copy + CRC, 4 passes over the bytes."""
+    import numpy as np
+    import torch
+
+    from ambry_amd import device as D
+    from ambry_amd.messages import PUT_DESC_DTYPE, PutMessage, layout, serialize_dev, transform_dev
+
+    key_len, props_len, um_len = 24, 94, 1000
+    L, _ = layout(PutMessage(key=bytes(key_len), props=bytes(props_len), usermeta=bytes(um_len),
+                             blob=bytes(blob_bytes)))
+    descs = np.zeros(m, dtype=PUT_DESC_DTYPE)
+    idx = np.arange(m, dtype=np.uint64)
+    descs["out_off"] = idx * L
+    descs["blob_len"] = blob_bytes
+    descs["key_len"], descs["props_len"], descs["usermeta_len"] = key_len, props_len, um_len
+    descs["enckey_len"] = -1
+    descs["header_version"] = 3
+    region = torch.empty(m * L, dtype=torch.uint8, device="cuda")
+    D.fill_random(region[: (m * L) // 16 * 16], 3, 0)
+    serialize_dev(torch.from_numpy(descs.view(np.uint8).copy()).cuda(), region)  # in place: random fields
+    offs = torch.from_numpy((idx * L).astype(np.int64)).cuda()
+    out = torch.empty(m * L + 6 * m, dtype=torch.uint8, device="cuda")
+    _, oo, ol, st = transform_dev(region, offs, out=out)
+    torch.cuda.synchronize()
+    assert int(st.abs().sum().item()) == 0 and bool(torch.equal(out[: m * L], region))  # V3 -> V3: identical
+    t_pre = time.perf_counter()
+    while time.perf_counter() - t_pre < 0.3:
+        transform_dev(region, offs, out=out)
+        torch.cuda.synchronize()
+    times = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        transform_dev(region, offs, out=out)
+        e1.record()
+        torch.cuda.synchronize()
+        times.append(e0.elapsed_time(e1))
+    times.sort()
+    ms = times[len(times) // 2]
+    nbytes = m * L
+    return {"case": f"transform {m} x PUT({blob_bytes} B blob) V3 -> V3", "messages": m, "message_bytes": nbytes,
+            "ms_median": round(ms, 4), "GiBps_messages": round(nbytes / (ms / 1e3) / 2**30, 1),
+            "messages_per_s": round(m / (ms / 1e3)), "GBps_hbm_min": round(4 * nbytes / (ms / 1e3) / 1e9, 1),
+            "parity": "every message verifies and the V3 -> V3 output equals the input region byte for byte"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--cases", default="64k,4k,4m")
+    ap.add_argument("--transform", default="64k,4k,4m", help="ValidatingTransformer cases ('' for none)")
     args = ap.parse_args()
     import torch
 
@@ -105,11 +154,15 @@ def main():
     torch.cuda.set_device(0)
     D.init(0)
     cases = {"64k": (65536, 64 << 10), "4k": (262144, 4 << 10), "4m": (4096, 4 << 20)}
-    for c in args.cases.split(","):
+    for c in [x for x in args.cases.split(",") if x]:
         m, s = cases[c]
         for in_place in (False, True):
             print(json.dumps(run(m, s, args.reps, in_place)), flush=True)
             torch.cuda.empty_cache()
+    for c in [x for x in args.transform.split(",") if x]:
+        m, s = cases[c]
+        print(json.dumps(run_transform(m, s, args.reps)), flush=True)
+        torch.cuda.empty_cache()
 
 
 if __name__ == "__main__":
