@@ -11,7 +11,9 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libambrycrc.so")
+# AMBRYCRC_LIBRARY names another build of the same library (A/B timing of two kernel builds on
+# one box, tools/ab_cases.sh); default: the in-tree build.
+LIB_PATH = os.environ.get("AMBRYCRC_LIBRARY") or os.path.join(_HERE, "libambrycrc.so")
 
 AMBRYCRC_OK = 0
 AMBRYCRC_EINVAL = -1

@@ -620,16 +620,18 @@ __device__ __forceinline__ uint32_t group_crc_g(const uint8_t* __restrict__ base
   return crc;
 }
 
-// Group body with 64-B lane runs (G = 16, classes 2-3 of variant 26): the wave-mode
-// transpose inside each 16-lane group. A 1 KiB super-block is 4 loads per lane (load i:
+// Group body with 64-B lane runs (G = 8 for class 1, G = 16 for classes 2-3): the wave-mode
+// transpose inside each G-lane group (G = 16 shown). A 1 KiB super-block is 4 loads per lane (load i:
 // lane gl <- bytes [16gl, 16gl+16) of 256-B block i, 256 B contiguous per group); the quad
 // transpose leaves lane gl = 4m + j holding the 64-B run [64m, 64m+64) of block j, which
 // it walks as one 16-step slice-by-4 chain; the lane state hops one super-block with
 // FOLD = x^(8*1024). Tree: gl bits 2, 3 merge the runs of a block (64, 128 B = POW[6, 7]),
 // bits 0, 1 the blocks (256, 512 B = POW[8, 9]). 18 LDS reads per 16 B-lane piece... per
-// KiB of chunk, against 24 for the 16-B-piece body; one super-block prefetched.
+// KiB of chunk, against 24 for the 16-B-piece body; one super-block prefetched
+// (group_class_t4s below).
 template <bool NT>
 __device__ __forceinline__ void group_fix_piece(u32x4& w, int64_t p, uint64_t cs, uint32_t rinit) {
+  if (p + 16 <= (int64_t)cs) w = u32x4{0u, 0u, 0u, 0u};  // loaded from the dummy address (t4_load)
   if (p < (int64_t)cs + 4 && p + 16 > (int64_t)cs) {
     w = xor_init(w, p, cs, rinit);
     if (p < (int64_t)cs) {
@@ -641,17 +643,6 @@ __device__ __forceinline__ void group_fix_piece(u32x4& w, int64_t p, uint64_t cs
         w[d] &= m;
       }
     }
-  }
-}
-
-template <bool NT, int G>
-__device__ __forceinline__ void group_load_sb(const GroupCtx& g, uint32_t sb, u32x4 (&x)[4]) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int64_t p = g.p0 + (int64_t)sb * (64 * G) + (16 * G) * i;
-    x[i] = u32x4{0u, 0u, 0u, 0u};
-    if (sb < g.nbw && g.body && p + 16 > (int64_t)g.cs)  // => floor16(cs) <= p < cb
-      x[i] = ld16<NT>(reinterpret_cast<const u32x4*>(g.base + p));
   }
 }
 
@@ -667,52 +658,106 @@ __device__ __forceinline__ uint32_t group_tree_t4(uint32_t r, uint32_t lane) {
   return r;
 }
 
-template <bool NT, int G>
-__device__ __forceinline__ uint32_t group_crc_t4(const uint8_t* __restrict__ base, uint64_t cs, uint64_t len,
-                                                 uint32_t cin, uint32_t nbw, uint32_t lane, const LaneConst& k) {
-  static_assert(G == 8 || G == 16, "64-B run groups are 8 or 16 lanes");
-  constexpr uint32_t BPL = 16u / G;  // trailing bytes per lane
-  constexpr uint32_t kFold = G == 16 ? kFoldOff : kPowOff + kNibSetBytes * 9;  // x^(8*64G)
-  const uint32_t gl = lane & (G - 1);
-  const uint32_t rinit = ~cin;
-  const uint64_t ce = cs + len;
-  const uint64_t cb = aligned_end(cs, ce);
-  const bool body = cb > cs;
-  const int64_t p0 = (int64_t)cb - (int64_t)nbw * (64 * G) + 16 * (int64_t)gl;
-  const GroupCtx g{base, p0, cs, body, nbw, rinit};
-  const uint32_t t = (uint32_t)(ce - cb);
-  const uint32_t k0 = BPL * (G - 1 - gl);
-  uint32_t tb[BPL];
+// ---- streamed 64-B-run group path (classes 1-3) ----
+// Run per round (descriptors, first super-block, steps, tree), a wave pays a bubble at every
+// round start: the round's first super-block is only issued once the round begins, after two
+// dependent descriptor loads, so a wave whose rounds are 1-4 steps long spends up to three
+// memory round trips per round with nothing in flight. Here a wave's rounds form one stream
+// of steps: the step that ends round r issues round r+1's first super-block (and its trailing
+// bytes and stored CRC), so one super-block per group is always in flight, across round
+// boundaries as within a round. Chunk descriptors are loaded a round ahead and list entries
+// two rounds ahead (an entry past the wave's range re-reads its first: always loaded, never
+// used).
+// Every load here is issued unconditionally: a lane whose piece lies outside its chunk reads
+// 16 B of the (cache-resident) table image instead, zeroed in group_fix_piece. A load under a
+// lane-divergent branch is skipped when no lane takes it, so the number of loads in flight
+// would depend on the path and the compiler would wait for all of them (vmcnt(0)) before
+// using any: the prefetched super-block would be waited for before the current one is used.
+struct T4Round {
+  int64_t p0;        // this lane's first piece address (virtual start + 16 gl)
+  uint64_t cs, ce, cb;
+  uint32_t nbw;      // super-blocks this round (max over the wave's groups)
+  uint32_t rinit, t, ci;
+  bool act;
+};
+
+template <int G>
+__device__ __forceinline__ T4Round t4_round(uint32_t ci, uint64_t len, uint64_t off, uint32_t cin, bool act,
+                                            uint32_t lane) {
+  T4Round r;
+  len = act ? len : 0;
+  off = act ? off : 0;
+  r.cs = off;
+  r.ce = off + len;
+  r.cb = aligned_end(off, r.ce);
+  const uint32_t nb = (uint32_t)((r.cb - off + 64 * G - 1) / (64 * G));
+  uint32_t nbw = 0;
 #pragma unroll
-  for (uint32_t i = 0; i < BPL; ++i) tb[i] = k0 + i < t ? base[ce - 1 - (k0 + i)] : 0u;
-  u32x4 nx[4];
-  group_load_sb<NT, G>(g, 0, nx);
-  uint32_t s = 0;
-#pragma unroll 1
-  for (uint32_t sb = 0; sb < nbw; ++sb) {
-    u32x4 x[4] = {nx[0], nx[1], nx[2], nx[3]};
-    group_load_sb<NT, G>(g, sb + 1, nx);  // none past nbw
-#pragma unroll
-    for (int i = 0; i < 4; ++i) group_fix_piece<NT>(x[i], p0 + (int64_t)sb * (64 * G) + (16 * G) * i, cs, rinit);
-    quad_transpose_asm(x);
-    s = run_crc<4>(x, k, sb ? nib_mul(s, kFold) : 0u);
+  for (uint32_t q = 0; q < 64 / G; ++q) {
+    const uint32_t x = __builtin_amdgcn_readlane(nb, q * G);
+    nbw = x > nbw ? x : nbw;
   }
-  uint32_t r = s;
-  if (nbw) r = group_tree_t4<G>(r, lane);
-  r = __shfl(r, (int)(lane | (G - 1)));
-  if (t & 1u) r = nib_mul(r, kPowOff + kNibSetBytes * 0);
-  if (t & 2u) r = nib_mul(r, kPowOff + kNibSetBytes * 1);
-  if (t & 4u) r = nib_mul(r, kPowOff + kNibSetBytes * 2);
-  if (t & 8u) r = nib_mul(r, kPowOff + kNibSetBytes * 3);
+  r.nbw = nbw;
+  r.p0 = (int64_t)r.cb - (int64_t)nbw * (64 * G) + 16 * (int64_t)(lane & (G - 1));
+  r.rinit = ~(act ? cin : 0u);
+  r.t = (uint32_t)(r.ce - r.cb);
+  r.ci = ci;
+  r.act = act;
+  return r;
+}
+
+// Super-block sb of a round given by its fields (passed by value: a select between two rounds'
+// structs through a reference would put both on the stack).
+template <bool NT, int G>
+__device__ __forceinline__ void t4_load(const uint8_t* __restrict__ base, const uint8_t* __restrict__ dummy,
+                                        int64_t p0, uint64_t cs, uint64_t cb, uint32_t nbw, uint32_t sb,
+                                        u32x4 (&x)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t p = p0 + (int64_t)sb * (64 * G) + (16 * G) * i;
+    const bool in = sb < nbw && cb > cs && p + 16 > (int64_t)cs;  // => floor16(cs) <= p < cb
+    x[i] = ld16<NT>(reinterpret_cast<const u32x4*>(in ? base + p : dummy));
+  }
+}
+
+// The round's trailing bytes (16/G per lane) and, for message verify, its stored CRC.
+template <int G>
+__device__ __forceinline__ uint64_t t4_aux(const SweepArgs& a, const uint8_t* __restrict__ dummy, const T4Round& r,
+                                           uint32_t lane, uint32_t (&tb)[16 / G]) {
+  constexpr uint32_t BPL = 16u / G;
+  const uint32_t k0 = BPL * (G - 1 - (lane & (G - 1)));
+#pragma unroll
+  for (uint32_t i = 0; i < BPL; ++i) tb[i] = *(k0 + i < r.t ? a.base + (r.ce - 1 - (k0 + i)) : dummy);
+  uint64_t stored = 0;
+  if (a.exp_fill) {
+    const bool leader = (lane & (G - 1)) == 0 && r.act;
+    __builtin_memcpy(&stored, leader ? a.base + r.ce : dummy, 8);
+  }
+  return stored;
+}
+
+// The round's CRCs from the lanes' chain states: tree over the group, trailing bytes, xor-out.
+template <int G>
+__device__ __forceinline__ uint32_t t4_finish(const T4Round& r, uint32_t s, const uint32_t (&tb)[16 / G],
+                                              uint32_t lane) {
+  constexpr uint32_t BPL = 16u / G;
+  const uint32_t k0 = BPL * (G - 1 - (lane & (G - 1)));
+  uint32_t rr = r.nbw ? group_tree_t4<G>(s, lane) : 0u;
+  rr = __shfl(rr, (int)(lane | (G - 1)));
+  const uint32_t t = r.t;
+  if (t & 1u) rr = nib_mul(rr, kPowOff + kNibSetBytes * 0);
+  if (t & 2u) rr = nib_mul(rr, kPowOff + kNibSetBytes * 1);
+  if (t & 4u) rr = nib_mul(rr, kPowOff + kNibSetBytes * 2);
+  if (t & 8u) rr = nib_mul(rr, kPowOff + kNibSetBytes * 3);
   uint32_t v = 0;
   if (k0 < t) {
 #pragma unroll
     for (uint32_t i = 0; i < BPL; ++i) {
       const uint32_t kk = k0 + i;
       if (kk < t) {
-        const uint64_t at = ce - 1 - kk;
+        const uint64_t at = r.ce - 1 - kk;
         uint32_t byte = tb[i];
-        if (at < cs + 4) byte ^= (rinit >> (8 * (uint32_t)(at - cs))) & 0xFFu;
+        if (at < r.cs + 4) byte ^= (r.rinit >> (8 * (uint32_t)(at - r.cs))) & 0xFFu;
         const uint32_t j = kk & 3;
         v ^= lds_rd(((j >> 1) << 16) | (byte << 8) | ((j & 1) << 7) | ((lane & 31) << 2));
       }
@@ -721,17 +766,90 @@ __device__ __forceinline__ uint32_t group_crc_t4(const uint8_t* __restrict__ bas
     if (k0 & 8) v = nib_mul(v, kPowOff + kNibSetBytes * 3);
   }
   v = group_xor<G>(v);
-  uint32_t crc = r ^ v ^ 0xFFFFFFFFu;
-  if (len < 4) crc ^= rinit >> (8 * (uint32_t)len);
+  uint32_t crc = rr ^ v ^ 0xFFFFFFFFu;
+  const uint64_t len = r.ce - r.cs;
+  if (len < 4) crc ^= r.rinit >> (8 * (uint32_t)len);
   return crc;
+}
+
+template <int G, bool NT>
+__device__ __forceinline__ void group_class_t4s(const SweepArgs& a, uint64_t lo, uint64_t hi, uint32_t wave,
+                                                uint64_t nwaves, uint32_t lane, const LaneConst& k) {
+  static_assert(G == 8 || G == 16, "64-B run groups are 8 or 16 lanes");
+  constexpr uint32_t S = 64 / G;
+  constexpr uint32_t BPL = 16u / G;
+  constexpr uint32_t kFold = G == 16 ? kFoldOff : kPowOff + kNibSetBytes * 9;  // x^(8*64G)
+  if (hi <= lo) return;
+  const uint64_t per = group_per<G>(hi - lo, nwaves);
+  const uint64_t i0 = lo + (uint64_t)wave * per;
+  if (i0 >= hi) return;
+  const uint64_t i1 = i0 + per < hi ? i0 + per : hi;
+  const uint32_t gi = lane / G;
+  const uint8_t* dummy = reinterpret_cast<const uint8_t*>(a.img);
+  auto idx_at = [&](uint64_t i) -> uint32_t { return a.small_idx[i + gi < i1 ? i + gi : i0]; };
+  const uint32_t ci0 = idx_at(i0);
+  uint32_t ci_n = idx_at(i0 + S);
+  T4Round r = t4_round<G>(ci0, a.len[ci0], a.off[ci0], a.crc_in ? a.crc_in[ci0] : 0u, i0 + gi < i1, lane);
+  uint32_t tb[BPL];
+  uint64_t stored = t4_aux<G>(a, dummy, r, lane, tb);
+  uint64_t len_n = a.len[ci_n], off_n = a.off[ci_n];
+  uint32_t cin_n = a.crc_in ? a.crc_in[ci_n] : 0u;
+  uint32_t ci_nn = idx_at(i0 + 2 * S);
+  u32x4 nx[4];
+  t4_load<NT, G>(a.base, dummy, r.p0, r.cs, r.cb, r.nbw, 0, nx);
+  T4Round rn = r;
+  uint32_t tbn[BPL];
+  uint64_t stored_n = 0;
+  uint64_t i = i0;
+  uint32_t sb = 0, s = 0;
+#pragma unroll 1
+  while (true) {
+    u32x4 x[4] = {nx[0], nx[1], nx[2], nx[3]};
+    const bool last = sb + 1 >= r.nbw;  // wave-uniform
+    if (last) {  // descriptors of round r+1 (loaded a round ago); start loading r+2's and r+3's entry
+      rn = t4_round<G>(ci_n, len_n, off_n, cin_n, i + S + gi < i1, lane);
+      stored_n = t4_aux<G>(a, dummy, rn, lane, tbn);
+      ci_n = ci_nn;
+      len_n = a.len[ci_n];
+      off_n = a.off[ci_n];
+      cin_n = a.crc_in ? a.crc_in[ci_n] : 0u;
+      ci_nn = idx_at(i + 3 * S);
+    }
+    // the next step, whichever round it is in
+    t4_load<NT, G>(a.base, dummy, last ? rn.p0 : r.p0, last ? rn.cs : r.cs, last ? rn.cb : r.cb,
+                   last ? rn.nbw : r.nbw, last ? 0u : sb + 1, nx);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      group_fix_piece<NT>(x[q], r.p0 + (int64_t)sb * (64 * G) + (16 * G) * q, r.cs, r.rinit);
+    quad_transpose_asm(x);
+    s = run_crc<4>(x, k, sb ? nib_mul(s, kFold) : 0u);
+    if (!last) {
+      ++sb;
+      continue;
+    }
+    const uint32_t crc = t4_finish<G>(r, r.nbw ? s : 0u, tb, lane);
+    if ((lane & (G - 1)) == 0 && r.act) {
+      a.out[r.ci] = crc;
+      if (a.exp_fill) {
+        const uint64_t st = __builtin_bswap64(stored);
+        a.exp_fill[r.ci] = (st >> 32) ? ~crc : (uint32_t)st;
+      }
+    }
+    i += S;
+    if (i >= i1) break;
+    r = rn;
+    stored = stored_n;
+#pragma unroll
+    for (uint32_t q = 0; q < BPL; ++q) tb[q] = tbn[q];
+    sb = 0;
+  }
 }
 
 // One size class [lo, hi) of the list, spread over all waves: wave w takes entries
 // [lo + w*per, lo + (w+1)*per), per a multiple of 64/G.
-template <int G, int NB, bool NT, bool T4 = false>
+template <int G, int NB, bool NT>
 __device__ __forceinline__ void group_class(const SweepArgs& a, uint64_t lo, uint64_t hi, uint32_t wave,
                                             uint64_t nwaves, uint32_t lane, const LaneConst& k) {
-  static_assert(!T4 || G == 8 || G == 16, "64-B run group body needs 8- or 16-lane groups");
   constexpr uint32_t S = 64 / G;
   if (hi <= lo) return;
   const uint64_t per = group_per<G>(hi - lo, nwaves);
@@ -751,7 +869,7 @@ __device__ __forceinline__ void group_class(const SweepArgs& a, uint64_t lo, uin
       cin = a.crc_in ? a.crc_in[ci] : 0u;
     }
     const uint64_t cb = aligned_end(off, off + len);
-    constexpr uint32_t BLK = T4 ? 64 * G : 16 * G;  // bytes per chain step
+    constexpr uint32_t BLK = 16 * G;  // bytes per chain step
     const uint32_t nb = (uint32_t)((cb - off + BLK - 1) / BLK);
     uint32_t nbw = 0;
 #pragma unroll
@@ -766,8 +884,7 @@ __device__ __forceinline__ void group_class(const SweepArgs& a, uint64_t lo, uin
       stored = __builtin_bswap64(stored);
     }
     uint32_t crc;
-    if constexpr (T4) crc = group_crc_t4<NT, G>(a.base, off, len, cin, nbw, lane, k);
-    else crc = group_crc_g<G, NB, NT>(a.base, off, len, cin, nbw, lane, k);
+    crc = group_crc_g<G, NB, NT>(a.base, off, len, cin, nbw, lane, k);
     if (leader) {
       a.out[ci] = crc;
       if (a.exp_fill) a.exp_fill[ci] = (stored >> 32) ? ~crc : (uint32_t)stored;
@@ -792,9 +909,9 @@ __device__ __forceinline__ void group_phase_cls(const SweepArgs& a, uint32_t wav
                                                 const LaneConst& k) {
   const uint64_t c1 = a.small_total[1], c2 = a.small_total[2], c3 = a.small_total[3], c4 = a.small_total[0];
   group_class<4, 4, NT>(a, 0, c1, wave, nwaves, lane, k);
-  group_class<8, 8, NT, true>(a, c1, c2, wave, nwaves, lane, k);
-  group_class<16, 16, NT, true>(a, c2, c3, wave, nwaves, lane, k);
-  group_class<16, 64, NT, true>(a, c3, c4, wave, nwaves, lane, k);
+  group_class_t4s<8, NT>(a, c1, c2, wave, nwaves, lane, k);
+  group_class_t4s<16, NT>(a, c2, c3, wave, nwaves, lane, k);
+  group_class_t4s<16, NT>(a, c3, c4, wave, nwaves, lane, k);
 }
 
 // Largest c in [0, n) with byte_start[c] <= g (byte_start nondecreasing, byte_start[0] = 0).
@@ -1342,7 +1459,7 @@ __global__ __launch_bounds__(256) void readbw_stream_kernel(const u32x4* __restr
 
 // The group phase's access shape without its arithmetic: chunks of `chunk` bytes back to back,
 // 64/G per wave round (one per G-lane group), wave w taking an equal run of the chunk list; each
-// lane loads its 16 B of four 16G-byte blocks per 64G-byte super-block (group_load_sb), one
+// lane loads its 16 B of four 16G-byte blocks per 64G-byte super-block (t4_load), one
 // super-block prefetched. The read roof the 4 KiB records' group rounds are compared against.
 template <int G>
 __global__ __launch_bounds__(1024) void readbw_group_kernel(const uint8_t* __restrict__ base, uint64_t nbytes,

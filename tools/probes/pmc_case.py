@@ -31,6 +31,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("case")
     ap.add_argument("--reps", type=int, default=5)
+    # timing probes of deliberately wrong kernels (tools/ab_cases.sh with a probe build) skip the check
+    ap.add_argument("--no-check", action="store_true", default=bool(os.environ.get("AB_NO_CHECK")))
     ap.add_argument("--gib", type=float, default=0.5)
     args = ap.parse_args()
     import numpy as np
@@ -54,7 +56,7 @@ def main():
         torch.cuda.synchronize()
         idx = [0, n // 2, n - 1]
         host = buf.view(n, stride)[idx, :size].cpu().numpy()
-        assert [zlib.crc32(h.tobytes()) for h in host] == list(out[idx].cpu().numpy().view(np.uint32))
+        assert args.no_check or [zlib.crc32(h.tobytes()) for h in host] == list(out[idx].cpu().numpy().view(np.uint32))
         for _ in range(args.reps):
             D.crc32_batch(buf, off, ln, out=out, workspace=ws)
         info.update(chunks=n, chunk_bytes=size, alg_bytes_per_launch=n * size + 4 * n)
@@ -68,7 +70,7 @@ def main():
         ws = torch.empty(D.workspace_bytes(1), dtype=torch.uint8, device="cuda")
         D.crc32_batch(buf, off, ln, out=out, workspace=ws)
         torch.cuda.synchronize()
-        assert zlib.crc32(buf[:size].cpu().numpy().tobytes()) == int(out.cpu().numpy().view(np.uint32)[0])
+        assert args.no_check or zlib.crc32(buf[:size].cpu().numpy().tobytes()) == int(out.cpu().numpy().view(np.uint32)[0])
         for _ in range(args.reps):
             D.crc32_batch(buf, off, ln, out=out, workspace=ws)
         info.update(chunks=1, chunk_bytes=size, alg_bytes_per_launch=size + 4)
