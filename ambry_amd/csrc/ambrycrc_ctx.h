@@ -107,9 +107,12 @@ int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uin
 int enqueue_messages(DevCtx* c, const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off, size_t m,
                      uint32_t* d_status, uint64_t* d_msg_end, void* d_ws, hipStream_t stream);
 // The PUT serialization pipeline (layout -> copy -> plan + CRC -> seal); d_ws holds at least
-// ambrycrc_serialize_puts_workspace_bytes(m).
+// ambrycrc_serialize_puts_workspace_bytes(m). d_in_crc (transform): the CRCs of records 1-4,
+// 4 per message (PutArgs::in_crc); the layout kernel then writes every trailer and the CRC pass
+// over the output is skipped.
 int enqueue_serialize(DevCtx* c, const ::ambrycrc_put_desc* d_desc, size_t m, const uint8_t* d_fields,
-                      const uint8_t* d_blobs, uint8_t* d_out, uint64_t* d_msg_len, void* d_ws, hipStream_t stream);
+                      const uint8_t* d_blobs, uint8_t* d_out, uint64_t* d_msg_len, void* d_ws, hipStream_t stream,
+                      const uint32_t* d_in_crc = nullptr);
 
 // Holds c->ws_mu for the lifetime of a *_dev call that uses the default workspace (d_ws ==
 // NULL); a call with its own workspace takes no lock.

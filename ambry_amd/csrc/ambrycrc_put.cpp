@@ -24,13 +24,19 @@ size_t put_jobs_bytes(size_t m) {
   return (j * (4 * sizeof(uint64_t) + 2 * sizeof(uint64_t) + sizeof(uint32_t)) + 255) & ~size_t(255);
 }
 
+// A transform's own workspace: descriptors, the scan's per-message output, in_crc (4 per message).
+size_t transform_own_bytes(size_t m) {
+  return (m * (sizeof(ambrycrc_put_desc) + sizeof(uint32_t) + 4 * sizeof(uint32_t)) + 255) & ~size_t(255);
+}
+
 }  // namespace
 
 namespace ambrycrc {
 namespace detail {
 
 int enqueue_serialize(DevCtx* c, const ::ambrycrc_put_desc* d_desc, size_t m, const uint8_t* d_fields,
-                      const uint8_t* d_blobs, uint8_t* d_out, uint64_t* d_msg_len, void* d_ws, hipStream_t stream) {
+                      const uint8_t* d_blobs, uint8_t* d_out, uint64_t* d_msg_len, void* d_ws, hipStream_t stream,
+                      const uint32_t* d_in_crc) {
   const size_t j = (size_t)kPutSlots * m;
   uint8_t* w = static_cast<uint8_t*>(d_ws);
   PutArgs a;
@@ -48,6 +54,8 @@ int enqueue_serialize(DevCtx* c, const ::ambrycrc_put_desc* d_desc, size_t m, co
   uint32_t* crc = reinterpret_cast<uint32_t*>(a.crc_len + j);
   a.crc = crc;
   a.msg_len = d_msg_len;
+  a.in_crc = d_in_crc;
+  a.img = c->d_img;
   void* batch_ws = w + put_jobs_bytes(m);
   if (launch_put_layout(a, stream) != hipSuccess) return AMBRYCRC_EHIP;
   if (d_fields || d_blobs) {
@@ -77,6 +85,7 @@ int enqueue_serialize(DevCtx* c, const ::ambrycrc_put_desc* d_desc, size_t m, co
     ca.dst = d_out;
     if (launch_gather_copy(ca, c->num_cu * 8, stream) != hipSuccess) return AMBRYCRC_EHIP;
   }
+  if (d_in_crc) return AMBRYCRC_OK;  // the layout kernel wrote every trailer
   const int rc = enqueue_batch(c, d_out, a.crc_off, a.crc_len, nullptr, crc, j, batch_ws, stream);
   if (rc) return rc;
   return hip_err(launch_put_seal(a, stream));
@@ -141,8 +150,8 @@ int ambrycrc_serialize_puts_dev(const ambrycrc_put_desc* d_desc, size_t m, const
 }
 
 size_t ambrycrc_transform_workspace_bytes(size_t m) {
-  const size_t own = (m * (sizeof(ambrycrc_put_desc) + sizeof(uint32_t)) + 255) & ~size_t(255);
-  return own + ws_need(m) + std::max(ambrycrc_messages_workspace_bytes(m), ambrycrc_serialize_puts_workspace_bytes(m));
+  return transform_own_bytes(m) + ws_need(m) +
+         std::max(ambrycrc_messages_workspace_bytes(m), ambrycrc_serialize_puts_workspace_bytes(m));
 }
 
 int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off, size_t m,
@@ -158,8 +167,8 @@ int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len
   WsLease lease;
   int rc = lease.acquire(c, stream, &d_ws, ws_bytes, ambrycrc_transform_workspace_bytes(m));
   if (rc) return rc;
-  // workspace: desc[m] | scan scratch (uint32 per message) | plan workspace for the m lengths |
-  //            the verify pipeline's, then the serializer's (one after the other on the stream)
+  // workspace: desc[m] | scan scratch (uint32 per message) | in_crc[4m] | plan workspace for the
+  //            m lengths | the verify pipeline's, then the serializer's (one after the other)
   uint8_t* w = static_cast<uint8_t*>(d_ws);
   TransformArgs t;
   t.region = d_region;
@@ -174,7 +183,9 @@ int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len
   t.status = d_status;
   t.out_cap = out_cap;
   uint32_t* scan_out = reinterpret_cast<uint32_t*>(w + m * sizeof(ambrycrc_put_desc));
-  uint8_t* plan_ws = w + ((m * (sizeof(ambrycrc_put_desc) + sizeof(uint32_t)) + 255) & ~size_t(255));
+  t.in_crc = scan_out + m;
+  t.img = c->d_img;
+  uint8_t* plan_ws = w + transform_own_bytes(m);
   void* shared = plan_ws + ws_need(m);
   rc = enqueue_messages(c, d_region, region_len, d_msg_off, m, d_status, nullptr, shared, stream);
   if (rc) return rc;
@@ -196,7 +207,7 @@ int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len
   p.small_max = 0;
   if (launch_plan(p, stream) != hipSuccess) return AMBRYCRC_EHIP;
   if (launch_transform_place(t, p.byte_start, stream) != hipSuccess) return AMBRYCRC_EHIP;
-  return enqueue_serialize(c, t.desc, m, d_region, d_region, d_out, nullptr, shared, stream);
+  return enqueue_serialize(c, t.desc, m, d_region, d_region, d_out, nullptr, shared, stream, t.in_crc);
 }
 
 }  // extern "C"

@@ -131,6 +131,12 @@ struct PutArgs {
   uint64_t* crc_len;
   const uint32_t* crc;     // [5m] their CRCs (from the batch kernels)
   uint64_t* msg_len;       // [m] or null
+  // Transform only: the CRCs of records 1-4 (encryption key, properties, user metadata, blob)
+  // known from the input message ([4m], message-major; see TransformArgs::in_crc). When set,
+  // put_layout_kernel hashes the new header itself and writes every trailer, and no CRC pass
+  // over the output runs. img: the table image (crc_img.h).
+  const uint32_t* in_crc;
+  const uint32_t* img;
 };
 
 // Each copy job costs its bytes plus kCopyJobCost: a wave pays about one memory round trip
@@ -160,6 +166,12 @@ struct TransformArgs {
   uint64_t* out_off;              // [m] or null
   uint32_t* status;               // [m] in: verify bits; out: + NOT_PUT / BAD_RECORD / NO_ROOM
   uint64_t out_cap;
+  // [4m] out: per transformed message, the CRCs its encryption-key, properties, user-metadata
+  // and blob records will have in the output. The input verified, so each is the stored trailer
+  // of the same bytes, except a Blob_Format_V1/V2 record re-written as V3, whose CRC follows by
+  // linearity (crc_img.h). Null: the serializer recomputes them.
+  uint32_t* in_crc;
+  const uint32_t* img;
 };
 
 hipError_t launch_transform_desc(const TransformArgs& a, hipStream_t s);

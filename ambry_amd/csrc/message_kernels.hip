@@ -20,6 +20,7 @@
 #include "../../include/ambrycrc.h"
 #include "crc32_kernels.h"
 #include "crc32_layout.h"
+#include "crc_img.h"
 #include "put_layout.h"
 
 namespace ambrycrc {
@@ -372,6 +373,25 @@ __global__ __launch_bounds__(256) void transform_desc_kernel(TransformArgs a) {
         if (!out_len) {
           d.header_version = 0;
           st |= AMBRYCRC_MSG_BAD_RECORD;
+        } else if (a.in_crc) {
+          // every record of the input verified: its CRC is the low word of its 8-B trailer
+          uint32_t* ic = a.in_crc + 4 * i;
+          ic[0] = keep_enc ? be32(p + bp - 4) : 0u;
+          ic[1] = be32(p + um - 4);
+          ic[2] = be32(p + blob - 4);
+          uint32_t cblob = be32(p + end - 4);
+          if (bv != 3) {  // the V3 head (version 3, type, compressed, size) replaces a V1/V2 head
+            // crc(B||C) = crc(A||C) ^ (crc(A) ^ crc(B)) * x^(8|C|)  (zlib's crc32_combine)
+            uint8_t h3[13];
+            put_be16(h3, 3u);
+            put_be16(h3 + 2, type);
+            h3[4] = (uint8_t)comp;
+            put_be64(h3 + 5, size);
+            const uint32_t ca = crc_bytes_img(a.img, 0u, p + blob, head);
+            const uint32_t cb = crc_bytes_img(a.img, 0u, h3, 13);
+            cblob ^= mul_xpow8_img(a.img, ca ^ cb, size);
+          }
+          ic[3] = cblob;
         }
       }
     }

@@ -15,6 +15,7 @@
 #include <stdint.h>
 
 #include "crc32_kernels.h"
+#include "crc_img.h"
 #include "put_layout.h"
 
 namespace ambrycrc {
@@ -55,6 +56,10 @@ __global__ __launch_bounds__(256) void put_layout_kernel(PutArgs a) {
     put_crc_job(L, k, &off, &ln, &present);
     a.crc_off[k * m + i] = d.out_off + off;
     a.crc_len[k * m + i] = present ? ln : 0;
+    if (a.in_crc && present) {  // transform: every CRC known but the header's (hashed here)
+      const uint32_t crc = k == 0 ? crc_bytes_img(a.img, 0u, msg, (uint32_t)ln) : a.in_crc[4 * i + k - 1];
+      put_be64(msg + off + ln, (uint64_t)crc);
+    }
   }
   if (a.msg_len) a.msg_len[i] = L.length;
 }
