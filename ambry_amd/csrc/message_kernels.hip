@@ -115,6 +115,41 @@ __device__ __forceinline__ uint32_t header_crc(const HeaderWords& h, uint32_t n,
   return ~c;
 }
 
+// What each record's deserializer reads before its CRC (MessageFormatRecord.java), for a record
+// of `span` bytes at q (its stored CRC the last 8): the record version (an unknown one throws
+// UnknownFormatVersion, :147-239) and the size fields that decide where the stream looks for
+// the CRC. BlobEncryptionKey_Format_V1 (:1588-1600) and UserMetadata_Format_V1 (:1637-1649): an
+// int size, then that many bytes, then the CRC; Blob_Format_V1/V2/V3 (:1681-1833): blob type
+// ordinal < 2, a long size <= Integer.MAX_VALUE, then the content and the CRC. A size that
+// disagrees with the header's record span, or a bad type, is AMBRYCRC_MSG_BAD_RECORD (the
+// reference reads the CRC at a different place, or throws). BlobProperties_Format_V1 and
+// Update_Format_V1..V3: the version only.
+__device__ __forceinline__ uint32_t record_check(int k, const uint8_t* q, uint64_t span) {
+  if (span < 10) return AMBRYCRC_MSG_BAD_RECORD;  // a version and a CRC at least
+  const uint32_t v = be16(q);
+  switch (k) {
+    case 0:    // encryption key
+    case 3: {  // user metadata
+      if (v != 1) return AMBRYCRC_MSG_BAD_VERSION;
+      if (span < 14) return AMBRYCRC_MSG_BAD_RECORD;
+      const int32_t n = (int32_t)be32(q + 2);
+      return n >= 0 && (uint64_t)n + 14 == span ? 0u : AMBRYCRC_MSG_BAD_RECORD;
+    }
+    case 1:  // properties
+      return v == 1 ? 0u : AMBRYCRC_MSG_BAD_VERSION;
+    case 2:  // update
+      return v >= 1 && v <= 3 ? 0u : AMBRYCRC_MSG_BAD_VERSION;
+    default: {  // blob
+      if (v < 1 || v > 3) return AMBRYCRC_MSG_BAD_VERSION;
+      const uint32_t head = v == 1 ? 10u : v == 2 ? 12u : 13u;
+      if (span < head + 8) return AMBRYCRC_MSG_BAD_RECORD;
+      const uint32_t type = v == 1 ? 0u : be16(q + 2);
+      const uint64_t size = be64(q + (v == 1 ? 2 : v == 2 ? 4 : 5));
+      return type < 2 && size <= 0x7FFFFFFFull && size + head + 8 == span ? 0u : AMBRYCRC_MSG_BAD_RECORD;
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void msg_parse_kernel(MsgArgs a) {
   __shared__ uint32_t tbl[1024];
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -214,6 +249,7 @@ __global__ __launch_bounds__(256) void msg_parse_kernel(MsgArgs a) {
     for (int k = 0; k < kMsgSlots; ++k) {
       if (rel[k] == -1) continue;
       const uint64_t e = rend[k];
+      status |= record_check(k, p + rel[k], e - (uint64_t)rel[k]);
       jo[k] = off + (uint64_t)rel[k];
       jl[k] = e - (uint64_t)rel[k] - 8;
       // Records the group phase takes whole have their stored CRC read there, from the line

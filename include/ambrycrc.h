@@ -143,8 +143,14 @@ int ambrycrc_verify_dev(const uint8_t* d_base, const uint64_t* d_off, const uint
 #define AMBRYCRC_MSG_UPDATE_CRC (1u << 3)   /* Update_Format_V1..V3 (:1215-1420) */
 #define AMBRYCRC_MSG_USERMETA_CRC (1u << 4) /* UserMetadata_Format_V1 (:1637-1649) */
 #define AMBRYCRC_MSG_BLOB_CRC (1u << 5)     /* Blob_Format_V1..V3 (:1668-1833) */
-#define AMBRYCRC_MSG_BAD_VERSION (1u << 8)  /* MessageFormatErrorCodes.UnknownFormatVersion */
+#define AMBRYCRC_MSG_BAD_VERSION (1u << 8)  /* MessageFormatErrorCodes.UnknownFormatVersion: the header's, or a
+                                               record's version (MessageFormatRecord.java:147-239) */
 #define AMBRYCRC_MSG_BAD_LAYOUT (1u << 9)   /* HeaderConstraintError, or the message overruns the region */
+#define AMBRYCRC_MSG_BAD_RECORD (1u << 11)  /* a record's own size field disagrees with its span in the header
+                                               (encryption key, user metadata, blob: the stream would look for
+                                               the CRC elsewhere), a blob type ordinal >= 2, a blob size >
+                                               Integer.MAX_VALUE (the DataCorrupt / IOException cases of
+                                               deserializeBlob*), or a record too short for its fields */
 
 /* Bytes of device workspace ambrycrc_verify_messages_dev needs for m messages. */
 size_t ambrycrc_messages_workspace_bytes(size_t m);
@@ -153,7 +159,9 @@ size_t ambrycrc_messages_workspace_bytes(size_t m);
  * [d_region, d_region + region_len): header (V1/V2/V3), encryption key, blob
  * properties, update, user metadata and blob records. d_status[i] gets the
  * AMBRYCRC_MSG_* bits (all corrupt records, not just the first: the reference's
- * deserializeBlobAll throws at the first, which is the lowest record bit set).
+ * deserializeBlobAll throws at the first, which is the lowest record bit set, with
+ * UnknownFormatVersion when AMBRYCRC_MSG_BAD_VERSION is set for it). Besides the CRCs, each
+ * record's version and size fields are checked against the header's record spans.
  * A corrupt header stops the message there, as verifyHeader does. d_msg_end[i]
  * (nullable) gets the offset one past the message, or 0 when unparseable.
  * Batch form of deserializeBlobAll's checks (MessageFormatRecord.java:257-303),
@@ -222,9 +230,6 @@ int ambrycrc_serialize_puts_dev(const ambrycrc_put_desc* d_desc, size_t m, const
 
 /* Status bits ambrycrc_transform_messages_dev adds to the AMBRYCRC_MSG_* verify bits. */
 #define AMBRYCRC_MSG_NOT_PUT (1u << 10)     /* an update record: "Message cannot be anything rather than put record" */
-#define AMBRYCRC_MSG_BAD_RECORD (1u << 11)  /* a record's own fields disagree with its span, an unknown blob record
-                                               version, a blob type ordinal >= 2 or a size > Integer.MAX_VALUE
-                                               (the DataCorrupt / IOException cases of deserializeBlob*) */
 #define AMBRYCRC_MSG_NO_ROOM (1u << 12)     /* the re-serialized message did not fit in out_cap */
 
 /* Replication's ValidatingTransformer.transform (ambry-messageformat/.../ValidatingTransformer.java:46-104)

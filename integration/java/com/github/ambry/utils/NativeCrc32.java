@@ -131,6 +131,7 @@ public final class NativeCrc32 implements Checksum {
   public static final int MSG_BLOB_CRC = 1 << 5;
   public static final int MSG_BAD_VERSION = 1 << 8;
   public static final int MSG_BAD_LAYOUT = 1 << 9;
+  public static final int MSG_BAD_RECORD = 1 << 11;
 
   private static native void nativeInit(int device);
 

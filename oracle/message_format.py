@@ -48,7 +48,7 @@ BLOB_CRC = 1 << 5
 BAD_VERSION = 1 << 8
 BAD_LAYOUT = 1 << 9
 NOT_PUT = 1 << 10      # transform only: an update record
-BAD_RECORD = 1 << 11   # transform only: record fields disagree with the span, bad blob version/type/size
+BAD_RECORD = 1 << 11   # a record's size field disagrees with its span, bad blob type/size, record too short
 
 RECORD_BITS = (ENCKEY_CRC, PROPS_CRC, UPDATE_CRC, USERMETA_CRC, BLOB_CRC)  # slot order enc, bp, upd, um, blob
 
@@ -177,6 +177,37 @@ def parse_header(region: bytes, off: int):
     return v, total, rel
 
 
+def _record_check(k: int, rec: bytes) -> int:
+    """What record k's deserializer reads before its CRC (MessageFormatRecord.java): the version
+    (deserializeAndGet*WithVersion :147-239 throw UnknownFormatVersion), then the size fields that
+    decide where the stream reads the CRC -- BlobEncryptionKey_Format_V1 (:1588-1600) and
+    UserMetadata_Format_V1 (:1637-1649): int size + bytes; Blob_Format_V1..V3 (:1681-1833): type
+    ordinal < 2, long size <= Integer.MAX_VALUE. `rec` is the record's span from the header,
+    stored CRC included. BlobProperties / Update records: the version only."""
+    if len(rec) < 10:
+        return BAD_RECORD
+    v = _be16(rec, 0)
+    if k in (0, 3):
+        if v != 1:
+            return BAD_VERSION
+        if len(rec) < 14:
+            return BAD_RECORD
+        n = _be32(rec, 2)
+        return 0 if n >= 0 and n + 14 == len(rec) else BAD_RECORD
+    if k == 1:
+        return 0 if v == 1 else BAD_VERSION
+    if k == 2:
+        return 0 if 1 <= v <= 3 else BAD_VERSION
+    if not 1 <= v <= 3:
+        return BAD_VERSION
+    head = {1: 10, 2: 12, 3: 13}[v]
+    if len(rec) < head + 8:
+        return BAD_RECORD
+    btype = 0 if v == 1 else struct.unpack_from(">H", rec, 2)[0]  # a negative ordinal fails too (index error)
+    size = struct.unpack_from(">Q", rec, {1: 2, 2: 4, 3: 5}[v])[0]
+    return 0 if btype < 2 and size <= 0x7FFFFFFF and size + head + 8 == len(rec) else BAD_RECORD
+
+
 def verify_message(region: bytes, off: int):
     """(status bits, message end offset or 0) -- deserializeBlobAll / update-record semantics."""
     if off + 2 > len(region):
@@ -213,6 +244,7 @@ def verify_message(region: bytes, off: int):
         stored = _be64(region, off + e - CRC_SIZE)
         if zlib.crc32(region[off + s:off + e - CRC_SIZE]) != stored:
             status |= RECORD_BITS[k]
+        status |= _record_check(k, region[off + s:off + e])
     return status, off + end
 
 

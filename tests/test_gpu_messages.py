@@ -242,3 +242,19 @@ def test_verify_log_tool(gpu, tmp_path):
     path.write_bytes(hdr + bytes(region))
     r = vl.verify_log(str(path))
     assert r["messages"] == 150 and r["chain_end"] == len(hdr) + offs[150]
+
+
+def test_record_level_checks(gpu):
+    """Messages whose CRCs are all valid but whose record versions / size fields / blob type are
+    not what the reference's deserializers accept: BAD_VERSION / BAD_RECORD, as the oracle says."""
+    from test_message_format import record_level_cases
+
+    cases = record_level_cases()
+    region, offs = bytearray(), []
+    for msg, _ in cases:
+        region += bytes(3)  # odd alignment
+        offs.append(len(region))
+        region += msg
+    st, end = run(gpu, bytes(region), offs)
+    assert st == [want for _, want in cases]
+    assert end == [o + len(m) for o, (m, _) in zip(offs, cases)]

@@ -57,7 +57,8 @@ def _run(gpu, mf, msgs, out_align, field_align, gap, in_place=False):
     assert mlen.cpu().numpy().tolist() == [len(expected(mf, m)) for m in msgs]
     status, end = gpu.verify_messages(out, torch.tensor(offs, dtype=torch.int64, device="cuda"))
     torch.cuda.synchronize()
-    assert int(status.abs().sum().item()) == 0
+    # BlobType has two values: a type-2 blob record fails the reader's check (AMBRYCRC_MSG_BAD_RECORD)
+    assert status.cpu().numpy().tolist() == [mf.BAD_RECORD if m.blob_type >= 2 else 0 for m in msgs]
     assert end.cpu().numpy().tolist() == [o + len(expected(mf, m)) for o, m in zip(offs, msgs)]
 
 

@@ -95,3 +95,63 @@ def test_chain_stops_at_corrupt_header(ambry):
     from ambry_amd.device import chain_messages_host
 
     assert chain_messages_host(bytes(bad), 0) == offs[:25]
+
+
+def _seal(body: bytes) -> bytes:
+    return body + struct.pack(">q", zlib.crc32(body))
+
+
+def _assemble(version, key, enc, pr, um, bl, upd=None):
+    """A message from already-sealed records (header offsets from their lengths, header CRC valid)."""
+    h = MF.HEADER_SIZE[version]
+    if upd is not None:
+        return MF.header(version, len(upd), MF.INVALID, MF.INVALID, h + len(key), MF.INVALID, MF.INVALID) + key + upd
+    enc = enc or b""
+    bp = h + len(key) + len(enc)
+    total = len(enc) + len(pr) + len(um) + len(bl)
+    return MF.header(version, total, h + len(key) if enc else MF.INVALID, bp, MF.INVALID, bp + len(pr),
+                     bp + len(pr) + len(um)) + key + enc + pr + um + bl
+
+
+def record_level_cases():
+    """(message, expected status) pairs whose every CRC is valid but whose record fields are not
+    what the reference's deserializers accept (MessageFormatRecord.java:147-239, 1588-1833):
+    unknown record versions -> BAD_VERSION; size fields that disagree with the header's record
+    span, blob type ordinals >= 2, blob sizes > Integer.MAX_VALUE -> BAD_RECORD."""
+    key = MF.store_key("rec-level")
+    props = MF.blob_properties_bytes(300)
+    content = bytes(range(200)) + bytes(100)
+    ek = b"e" * 32
+    pr, um = MF.props_record(props), MF.usermeta_record(b"meta" * 5)
+    bl, enc = MF.blob_record(content), MF.enckey_record(ek)
+    cases = [
+        (_assemble(3, key, enc, pr, um, bl), 0),
+        (_assemble(2, key, None, pr, um, MF.blob_record_v1(content)), 0),
+        (_assemble(3, key, None, pr, um, MF.blob_record(content, version=2, blob_type=1)), 0),
+        (_assemble(3, key, _seal(struct.pack(">hi", 2, len(ek)) + ek), pr, um, bl), MF.BAD_VERSION),
+        (_assemble(3, key, _seal(struct.pack(">hi", 1, len(ek) + 1) + ek), pr, um, bl), MF.BAD_RECORD),
+        (_assemble(3, key, None, _seal(struct.pack(">h", 2) + props), um, bl), MF.BAD_VERSION),
+        (_assemble(3, key, None, pr, _seal(struct.pack(">hi", 0, 20) + b"meta" * 5), bl), MF.BAD_VERSION),
+        (_assemble(3, key, None, pr, _seal(struct.pack(">hi", 1, 19) + b"meta" * 5), bl), MF.BAD_RECORD),
+        (_assemble(3, key, None, pr, _seal(struct.pack(">hi", 1, -4) + b"meta" * 5), bl), MF.BAD_RECORD),
+        (_assemble(3, key, None, pr, um, _seal(struct.pack(">hhbq", 3, 2, 0, len(content)) + content)),
+         MF.BAD_RECORD),
+        (_assemble(3, key, None, pr, um, _seal(struct.pack(">hhbq", 4, 0, 0, len(content)) + content)),
+         MF.BAD_VERSION),
+        (_assemble(3, key, None, pr, um, _seal(struct.pack(">hhbq", 3, 0, 0, len(content) - 1) + content)),
+         MF.BAD_RECORD),
+        (_assemble(3, key, None, pr, um, _seal(struct.pack(">hhbq", 3, 0, 0, len(content) + (1 << 32)) + content)),
+         MF.BAD_RECORD),
+        (_assemble(1, key, None, pr, um, _seal(struct.pack(">hq", 1, len(content) + 3) + content)), MF.BAD_RECORD),
+        (_assemble(3, key, None, pr, um, _seal(struct.pack(">hhq", 2, 7, len(content)) + content)), MF.BAD_RECORD),
+    ]
+    upd = bytearray(MF.update_record_v3())
+    upd[0:2] = struct.pack(">h", 4)
+    cases.append((_assemble(3, key, None, None, None, None, upd=_seal(bytes(upd[:-8]))), MF.BAD_VERSION))
+    cases.append((_assemble(3, key, None, None, None, None, upd=MF.update_record_v3(kind="delete")), 0))
+    return cases
+
+
+def test_oracle_record_level_checks():
+    for i, (msg, want) in enumerate(record_level_cases()):
+        assert MF.verify_message(msg, 0) == (want, len(msg)), i

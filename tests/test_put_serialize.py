@@ -67,7 +67,8 @@ def test_host_serializer_matches_layout_oracle(ambry, mf):
         got, crcs = serialize_host(m)
         exp = expected(mf, m)
         assert got == exp
-        assert mf.verify_message(got, 0) == (0, len(got))
+        # BlobType has two values (DataBlob, MetadataBlob): a type-2 record fails the reader's check
+        assert mf.verify_message(got, 0) == (mf.BAD_RECORD if m.blob_type >= 2 else 0, len(got))
         n, offs = layout(m)
         assert n == len(got)
         assert got[offs["key"]:offs["key"] + len(m.key)] == m.key
