@@ -7,6 +7,7 @@ untimed; the profiler's per-dispatch counters are the measurement.
   batch1k    1 KiB chunks, aligned, 0.5 GiB                                     -- group class 1
   batch4k    4 KiB chunks, aligned, 0.5 GiB                                     -- group class 2
   batch4109  4109-B chunks at 16-B offsets (the blob records of 4 KiB PUTs)     -- group class 3
+  batch2000  2000-B chunks, packed (8-B offsets); batch3000: 3000 B at 16-B offsets -- class 2
   msg4k      ambrycrc_verify_messages_dev over 262,144 x PUT(4 KiB blob), 1.29 GiB
   single100  one 100 B chunk per ambrycrc_batch_dev call
   single4m   one 4 MiB chunk per ambrycrc_batch_dev call
@@ -24,7 +25,8 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
-SIZES = {"batch100": (100, 112), "batch1k": (1024, 1024), "batch4k": (4096, 4096), "batch4109": (4109, 4112)}
+SIZES = {"batch100": (100, 112), "batch1k": (1024, 1024), "batch4k": (4096, 4096), "batch4109": (4109, 4112),
+         "batch2000": (2000, 2000), "batch3000": (3000, 3008)}
 
 
 def main():
