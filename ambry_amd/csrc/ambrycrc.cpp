@@ -298,7 +298,8 @@ uint64_t batch_small_max(const DevCtx* c, size_t n) {
 // crc_in may equal out (an in-place continuation): the plan copies crc_in into the workspace
 // before it initialises out, and the CRC kernels read the copy.
 int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len, const uint32_t* crc_in,
-                  uint32_t* out, size_t n, void* ws, hipStream_t s, uint32_t* exp_fill) {
+                  uint32_t* out, size_t n, void* ws, hipStream_t s, uint32_t* exp_fill, uint8_t* copy_dst,
+                  const uint64_t* copy_off) {
   if (n == 0) return AMBRYCRC_OK;
   PlanArgs p;
   p.off = off;
@@ -313,7 +314,7 @@ int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uin
   p.small_idx = reinterpret_cast<uint32_t*>(p.small_total + 5);
   p.crc_stage = crc_in ? p.small_idx + n : nullptr;
   p.out = out;
-  p.small_max = batch_small_max(c, n);
+  p.small_max = copy_dst ? (n >= kGroupMinChunks ? kGroupSmallMax : 0) : batch_small_max(c, n);
   hipError_t e = launch_plan(p, s);
   if (e != hipSuccess) return AMBRYCRC_EHIP;
   SweepArgs t;
@@ -330,6 +331,8 @@ int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uin
   t.small_idx = p.small_idx;
   t.exp_fill = exp_fill;
   t.window = c->window;
+  t.copy_dst = copy_dst;
+  t.copy_off = copy_off;
   EventPair ev{nullptr, nullptr};
   if (c->timing) {
     std::lock_guard<std::mutex> g(c->ev_mu);
@@ -341,7 +344,7 @@ int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uin
     }
     if (hipEventRecord(ev.a, s) != hipSuccess) return AMBRYCRC_EHIP;
   }
-  e = launch_sweep(t, c->grid, c->variant, s);
+  e = copy_dst ? launch_sweep_copy(t, c->grid, s) : launch_sweep(t, c->grid, c->variant, s);
   if (e != hipSuccess) return AMBRYCRC_EHIP;
   if (c->timing) {
     if (hipEventRecord(ev.b, s) != hipSuccess) return AMBRYCRC_EHIP;

@@ -98,9 +98,11 @@ size_t ws_need(size_t n);
 int stream_ws(DevCtx* c, hipStream_t s, size_t need, void** out);
 // Largest chunk the group phase takes whole for a batch of n chunks on c's variant (0: none).
 uint64_t batch_small_max(const DevCtx* c, size_t n);
-// Plan + CRC kernels for n chunks on stream s (ws: >= ws_need(n) bytes). exp_fill: see SweepArgs.
+// Plan + CRC kernels for n chunks on stream s (ws: >= ws_need(n) bytes). exp_fill, copy_dst,
+// copy_off: see SweepArgs (copy_dst set: the copy-through kernel, whatever c's variant).
 int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len, const uint32_t* crc_in,
-                  uint32_t* out, size_t n, void* ws, hipStream_t s, uint32_t* exp_fill = nullptr);
+                  uint32_t* out, size_t n, void* ws, hipStream_t s, uint32_t* exp_fill = nullptr,
+                  uint8_t* copy_dst = nullptr, const uint64_t* copy_off = nullptr);
 
 // The device message-verify pipeline (parse -> plan + sweep -> reduce) on `stream`; d_ws holds at
 // least ambrycrc_messages_workspace_bytes(m). d_msg_end may be null.

@@ -56,8 +56,17 @@ int enqueue_serialize(DevCtx* c, const ::ambrycrc_put_desc* d_desc, size_t m, co
   a.msg_len = d_msg_len;
   a.in_crc = d_in_crc;
   a.img = c->d_img;
+  a.copy_through = (d_fields || d_blobs) && !d_in_crc;
   void* batch_ws = w + put_jobs_bytes(m);
   if (launch_put_layout(a, stream) != hipSuccess) return AMBRYCRC_EHIP;
+  if (a.copy_through) {
+    // one pass over the fields: the copy-through sweep reads each from its source, writes it into
+    // the message and CRCs it (job k*m+i = slot k of message i, as the CRC jobs)
+    const int rc = enqueue_batch(c, nullptr, a.cp_src, a.cp_len, nullptr, crc, j, batch_ws, stream, nullptr, d_out,
+                                 a.cp_dst);
+    if (rc) return rc;
+    return hip_err(launch_put_seal_combine(a, stream));
+  }
   if (d_fields || d_blobs) {
     // cost offsets of the copy jobs: the plan kernel's exclusive scan (no small-chunk classes);
     // its per-chunk output initialisation lands in `crc`, overwritten by the CRC batch below

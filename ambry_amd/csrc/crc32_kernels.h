@@ -50,6 +50,11 @@ struct SweepArgs {
   // window) rounds of nwaves shares each (share i -> wave i % nwaves), so at any time the
   // waves read inside about one window, not across the whole batch. 0 = one round.
   uint64_t window;
+  // Copy-through (launch_sweep_copy only): every byte read for chunk c is also written to
+  // copy_dst + copy_off[c] + (its offset in the chunk). The PUT serializer's copy mode uses it so a
+  // field is read once for both its copy and its CRC. Null for every other launch.
+  uint8_t* copy_dst;
+  const uint64_t* copy_off;
 };
 
 // Chunks of 1 B .. kGroupSmallMax go to the group phase (variant 29) in batches of at least
@@ -137,6 +142,11 @@ struct PutArgs {
   // over the output runs. img: the table image (crc_img.h).
   const uint32_t* in_crc;
   const uint32_t* img;
+  // Copy-through mode (copy mode without in_crc): the copy jobs become the CRC batch itself --
+  // the sweep reads each field once, writes it to the message and CRCs it; put_seal_combine_kernel
+  // then extends each content CRC over its record prefix. A slot with no source buffer (fields
+  // or blobs null) re-reads its bytes in place (src = dst).
+  bool copy_through;
 };
 
 // Each copy job costs its bytes plus kCopyJobCost: a wave pays about one memory round trip
@@ -179,6 +189,7 @@ hipError_t launch_transform_place(const TransformArgs& a, const uint64_t* start,
 
 hipError_t launch_put_layout(const PutArgs& a, hipStream_t s);
 hipError_t launch_put_seal(const PutArgs& a, hipStream_t s);
+hipError_t launch_put_seal_combine(const PutArgs& a, hipStream_t s);
 hipError_t launch_gather_copy(const CopyArgs& a, int grid, hipStream_t s);
 
 hipError_t launch_trailer_parse(const TrailerArgs& a, hipStream_t s);
@@ -189,6 +200,7 @@ hipError_t launch_msg_reduce(const MsgArgs& a, hipStream_t s);
 
 hipError_t launch_plan(const PlanArgs& a, hipStream_t s);
 hipError_t launch_sweep(const SweepArgs& a, int grid, int variant, hipStream_t s);
+hipError_t launch_sweep_copy(const SweepArgs& a, int grid, hipStream_t s);
 hipError_t launch_verify(const uint32_t* crc, const uint32_t* expected, uint8_t* mismatch, uint32_t* count,
                          uint32_t n, hipStream_t s);
 hipError_t launch_readbw(const uint8_t* base, uint64_t nbytes, uint32_t* out, int grid, int variant,

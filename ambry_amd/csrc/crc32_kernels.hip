@@ -169,6 +169,24 @@ __device__ __forceinline__ u32x4 ld16(const u32x4* p) {
   }
 }
 
+// ---- copy-through (SweepArgs::copy_dst): every byte read for a chunk is also stored to the
+// chunk's destination, dbase + (its source offset), so a serialization moves each field once.
+// 16-B stores at any destination alignment (gfx9 global memory runs in unaligned mode; the
+// memcpy becomes one global_store_dwordx4); a piece that starts before the chunk stores only
+// its bytes from `lo` on.
+__device__ __forceinline__ void st16u(uint8_t* d, const u32x4& v) { __builtin_memcpy(d, &v, 16); }
+
+__device__ __forceinline__ void copy_piece(uint8_t* dbase, int64_t p, const u32x4& v, int64_t lo) {
+  if (p + 16 <= lo) return;
+  if (p >= lo) {
+    st16u(dbase + p, v);
+    return;
+  }
+#pragma unroll
+  for (int b = 0; b < 16; ++b)
+    if (p + b >= lo) dbase[p + b] = (uint8_t)(v[b >> 2] >> (8 * (b & 3)));
+}
+
 template <int LVL>
 __device__ __forceinline__ uint32_t tree_level(uint32_t s, uint32_t lane) {
   const uint32_t sh = nib_mul(tree_partner<LVL>(s), kTreeOff + kNibSetBytes * LVL);
@@ -355,9 +373,9 @@ __device__ __forceinline__ uint32_t tree_level_t4(uint32_t s, uint32_t lane) {
   return (lane & (1u << BIT)) ? (s ^ sh) : s;
 }
 
-template <int UB, bool NT, bool PRIO = false>
+template <int UB, bool NT, bool PRIO = false, bool COPY = false>
 __device__ __forceinline__ uint32_t body_crc_t4(const uint8_t* __restrict__ base, uint64_t bs, uint64_t be,
-                                                uint32_t lane, const LaneConst& k) {
+                                                uint32_t lane, const LaneConst& k, uint8_t* dbase = nullptr) {
   constexpr uint64_t SB = 4 * (uint64_t)kBlockBytes;
   constexpr uint32_t kFold = kPowOff + kNibSetBytes * 12;
   const uint64_t nb = (be - bs + SB - 1) / SB;
@@ -370,6 +388,7 @@ __device__ __forceinline__ uint32_t body_crc_t4(const uint8_t* __restrict__ base
     const int64_t p = v0 + (int64_t)kBlockBytes * i + 16 * (int64_t)lane;
     if (p + 16 > (int64_t)bs) {  // => p >= floor16(bs) >= 0
       x[i] = ld16<NT>(reinterpret_cast<const u32x4*>(base + p));
+      if constexpr (COPY) copy_piece(dbase, p, x[i], (int64_t)bs);
       if (p < (int64_t)bs) {
         const uint32_t cut = (uint32_t)(bs - p);
 #pragma unroll
@@ -402,12 +421,20 @@ __device__ __forceinline__ uint32_t body_crc_t4(const uint8_t* __restrict__ base
           buf[u][i] = ld16<NT>(q + (b + UB + u) * 256 + i * 64);
         }
         if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+        if constexpr (COPY) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) st16u(dbase + v0 + (int64_t)((b + u) * SB) + 1024 * i + 16 * lane, cur[i]);
+        }
         quad_transpose_asm(cur);
         s = run_crc<4>(cur, k, nib_mul(s, kFold));
       }
     }
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
+      if constexpr (COPY) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) st16u(dbase + v0 + (int64_t)((b + u) * SB) + 1024 * i + 16 * lane, buf[u][i]);
+      }
       quad_transpose_asm(buf[u]);
       s = run_crc<4>(buf[u], k, nib_mul(s, kFold));
     }
@@ -417,6 +444,10 @@ __device__ __forceinline__ uint32_t body_crc_t4(const uint8_t* __restrict__ base
     u32x4 cur[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) cur[i] = ld16<NT>(q + b * 256 + i * 64);
+    if constexpr (COPY) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) st16u(dbase + v0 + (int64_t)(b * SB) + 1024 * i + 16 * lane, cur[i]);
+    }
     quad_transpose_asm(cur);
     s = run_crc<4>(cur, k, nib_mul(s, kFold));
   }
@@ -464,6 +495,7 @@ __device__ __forceinline__ u32x4 xor_init(u32x4 w, int64_t p, uint64_t cs, uint3
 // piece holding [cs, cs+4) gets the initial register XORed in.
 struct GroupCtx {
   const uint8_t* __restrict__ base;
+  uint8_t* dbase;  // copy-through destination base (COPY builds)
   int64_t p0;
   uint64_t cs;
   bool body;
@@ -480,10 +512,10 @@ __device__ __forceinline__ u32x4 group_load(const GroupCtx& g, int b) {
   return w;
 }
 
-template <int U, int P, bool NT, int BB>
+template <int U, int P, bool NT, int BB, bool COPY = false>
 struct GroupRingT {
   u32x4 w;
-  GroupRingT<U + 1, P, NT, BB> next;
+  GroupRingT<U + 1, P, NT, BB, COPY> next;
   __device__ __forceinline__ void prime(const GroupCtx& g) {
     w = group_load<NT, BB>(g, U);
     next.prime(g);
@@ -496,6 +528,9 @@ struct GroupRingT {
     u32x4 x = w;
     w = group_load<NT, BB>(g, (int)(b + P));
     const int64_t p = g.p0 + (int64_t)b * BB;
+    if constexpr (COPY) {
+      if (g.body) copy_piece(g.dbase, p, x, (int64_t)g.cs);
+    }
     if (p < (int64_t)g.cs + 4 && p + 16 > (int64_t)g.cs) {
       x = xor_init(x, p, g.cs, g.rinit);
       if (p < (int64_t)g.cs) {
@@ -512,8 +547,8 @@ struct GroupRingT {
     return next.step(g, k, b0, s, fold_off);
   }
 };
-template <int P, bool NT, int BB>
-struct GroupRingT<P, P, NT, BB> {
+template <int P, bool NT, int BB, bool COPY>
+struct GroupRingT<P, P, NT, BB, COPY> {
   __device__ __forceinline__ void prime(const GroupCtx&) {}
   __device__ __forceinline__ uint32_t step(const GroupCtx&, const LaneConst&, uint32_t, uint32_t s, uint32_t) {
     return s;
@@ -561,9 +596,10 @@ __device__ __forceinline__ uint32_t group_xor(uint32_t v) {
   return v;
 }
 
-template <int G, int NB, bool NT>
+template <int G, int NB, bool NT, bool COPY = false>
 __device__ __forceinline__ uint32_t group_crc_g(const uint8_t* __restrict__ base, uint64_t cs, uint64_t len,
-                                                uint32_t cin, uint32_t nbw, uint32_t lane, const LaneConst& k) {
+                                                uint32_t cin, uint32_t nbw, uint32_t lane, const LaneConst& k,
+                                                uint8_t* dbase = nullptr) {
   constexpr uint32_t BB = 16u * G;
   constexpr uint32_t BPL = 16u / G;  // trailing bytes per lane
   const uint32_t gl = lane & (G - 1);
@@ -572,15 +608,20 @@ __device__ __forceinline__ uint32_t group_crc_g(const uint8_t* __restrict__ base
   const uint64_t cb = aligned_end(cs, ce);
   const bool body = cb > cs;
   const int64_t p0 = (int64_t)cb - (int64_t)nbw * BB + 16 * (int64_t)gl;
-  const GroupCtx g{base, p0, cs, body, nbw, rinit};
+  const GroupCtx g{base, dbase, p0, cs, body, nbw, rinit};
   const uint32_t t = (uint32_t)(ce - cb);  // trailing < 16 bytes
   const uint32_t k0 = BPL * (G - 1 - gl);  // this lane's bytes sit at distance k0..k0+BPL-1 from the end
   // the trailing bytes are loaded with the blocks, not after the chain (one round trip)
   uint32_t tb[BPL];
 #pragma unroll
   for (uint32_t i = 0; i < BPL; ++i) tb[i] = k0 + i < t ? base[ce - 1 - (k0 + i)] : 0u;
+  if constexpr (COPY) {
+#pragma unroll
+    for (uint32_t i = 0; i < BPL; ++i)
+      if (k0 + i < t) dbase[ce - 1 - (k0 + i)] = (uint8_t)tb[i];
+  }
   constexpr int P = NB < 8 ? NB : 8;
-  GroupRingT<0, P, NT, (int)BB> ring;
+  GroupRingT<0, P, NT, (int)BB, COPY> ring;
   ring.prime(g);
   uint32_t s = 0;
 #pragma unroll 1
@@ -679,6 +720,7 @@ struct T4Round {
   uint32_t nbw;      // super-blocks this round (max over the wave's groups)
   uint32_t rinit, t, ci;
   bool act;
+  uint64_t dsh;      // copy-through: the destination of source offset p is (uint8_t*)dsh + p
 };
 
 template <int G>
@@ -703,6 +745,7 @@ __device__ __forceinline__ T4Round t4_round(uint32_t ci, uint64_t len, uint64_t 
   r.t = (uint32_t)(r.ce - r.cb);
   r.ci = ci;
   r.act = act;
+  r.dsh = 0;
   return r;
 }
 
@@ -772,7 +815,7 @@ __device__ __forceinline__ uint32_t t4_finish(const T4Round& r, uint32_t s, cons
   return crc;
 }
 
-template <int G, bool NT>
+template <int G, bool NT, bool COPY = false>
 __device__ __forceinline__ void group_class_t4s(const SweepArgs& a, uint64_t lo, uint64_t hi, uint32_t wave,
                                                 uint64_t nwaves, uint32_t lane, const LaneConst& k) {
   static_assert(G == 8 || G == 16, "64-B run groups are 8 or 16 lanes");
@@ -790,10 +833,12 @@ __device__ __forceinline__ void group_class_t4s(const SweepArgs& a, uint64_t lo,
   const uint32_t ci0 = idx_at(i0);
   uint32_t ci_n = idx_at(i0 + S);
   T4Round r = t4_round<G>(ci0, a.len[ci0], a.off[ci0], a.crc_in ? a.crc_in[ci0] : 0u, i0 + gi < i1, lane);
+  if constexpr (COPY) r.dsh = (uint64_t)(uintptr_t)a.copy_dst + a.copy_off[ci0] - r.cs;
   uint32_t tb[BPL];
   uint64_t stored = t4_aux<G>(a, dummy, r, lane, tb);
   uint64_t len_n = a.len[ci_n], off_n = a.off[ci_n];
   uint32_t cin_n = a.crc_in ? a.crc_in[ci_n] : 0u;
+  uint64_t dst_n = COPY ? a.copy_off[ci_n] : 0;
   uint32_t ci_nn = idx_at(i0 + 2 * S);
   u32x4 nx[4];
   t4_load<NT, G>(a.base, dummy, r.p0, r.cs, r.cb, r.nbw, 0, nx);
@@ -808,16 +853,26 @@ __device__ __forceinline__ void group_class_t4s(const SweepArgs& a, uint64_t lo,
     const bool last = sb + 1 >= r.nbw;  // wave-uniform
     if (last) {  // descriptors of round r+1 (loaded a round ago); start loading r+2's and r+3's entry
       rn = t4_round<G>(ci_n, len_n, off_n, cin_n, i + S + gi < i1, lane);
+      if constexpr (COPY) rn.dsh = (uint64_t)(uintptr_t)a.copy_dst + dst_n - rn.cs;
       stored_n = t4_aux<G>(a, dummy, rn, lane, tbn);
       ci_n = ci_nn;
       len_n = a.len[ci_n];
       off_n = a.off[ci_n];
       cin_n = a.crc_in ? a.crc_in[ci_n] : 0u;
+      if constexpr (COPY) dst_n = a.copy_off[ci_n];
       ci_nn = idx_at(i + 3 * S);
     }
     // the next step, whichever round it is in
     t4_load<NT, G>(a.base, dummy, last ? rn.p0 : r.p0, last ? rn.cs : r.cs, last ? rn.cb : r.cb,
                    last ? rn.nbw : r.nbw, last ? 0u : sb + 1, nx);
+    if constexpr (COPY) {
+      if (r.cb > r.cs) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          copy_piece(reinterpret_cast<uint8_t*>(r.dsh), r.p0 + (int64_t)sb * (64 * G) + (16 * G) * q, x[q],
+                     (int64_t)r.cs);
+      }
+    }
 #pragma unroll
     for (int q = 0; q < 4; ++q)
       group_fix_piece<NT>(x[q], r.p0 + (int64_t)sb * (64 * G) + (16 * G) * q, r.cs, r.rinit);
@@ -828,6 +883,12 @@ __device__ __forceinline__ void group_class_t4s(const SweepArgs& a, uint64_t lo,
       continue;
     }
     const uint32_t crc = t4_finish<G>(r, r.nbw ? s : 0u, tb, lane);
+    if constexpr (COPY) {  // the round's trailing bytes
+      const uint32_t k0 = BPL * (G - 1 - (lane & (G - 1)));
+#pragma unroll
+      for (uint32_t q = 0; q < BPL; ++q)
+        if (k0 + q < r.t) reinterpret_cast<uint8_t*>(r.dsh)[r.ce - 1 - (k0 + q)] = (uint8_t)tb[q];
+    }
     if ((lane & (G - 1)) == 0 && r.act) {
       a.out[r.ci] = crc;
       if (a.exp_fill) {
@@ -847,7 +908,7 @@ __device__ __forceinline__ void group_class_t4s(const SweepArgs& a, uint64_t lo,
 
 // One size class [lo, hi) of the list, spread over all waves: wave w takes entries
 // [lo + w*per, lo + (w+1)*per), per a multiple of 64/G.
-template <int G, int NB, bool NT>
+template <int G, int NB, bool NT, bool COPY = false>
 __device__ __forceinline__ void group_class(const SweepArgs& a, uint64_t lo, uint64_t hi, uint32_t wave,
                                             uint64_t nwaves, uint32_t lane, const LaneConst& k) {
   constexpr uint32_t S = 64 / G;
@@ -883,8 +944,9 @@ __device__ __forceinline__ void group_class(const SweepArgs& a, uint64_t lo, uin
       __builtin_memcpy(&stored, a.base + off + len, 8);  // issued now, used after the chain
       stored = __builtin_bswap64(stored);
     }
-    uint32_t crc;
-    crc = group_crc_g<G, NB, NT>(a.base, off, len, cin, nbw, lane, k);
+    uint8_t* dbase = nullptr;
+    if constexpr (COPY) dbase = a.copy_dst + (a.copy_off[ci] - off);  // dst of source offset p: dbase + p
+    const uint32_t crc = group_crc_g<G, NB, NT, COPY>(a.base, off, len, cin, nbw, lane, k, dbase);
     if (leader) {
       a.out[ci] = crc;
       if (a.exp_fill) a.exp_fill[ci] = (stored >> 32) ? ~crc : (uint32_t)stored;
@@ -904,14 +966,14 @@ __device__ __forceinline__ bool group_cls_has_work(const SweepArgs& a, uint32_t 
 
 // Class 0 (<= 256 B) in 4-lane groups of 16-B pieces; classes 1-3 with 64-B lane runs in 8- and
 // 16-lane groups.
-template <bool NT>
+template <bool NT, bool COPY = false>
 __device__ __forceinline__ void group_phase_cls(const SweepArgs& a, uint32_t wave, uint64_t nwaves, uint32_t lane,
                                                 const LaneConst& k) {
   const uint64_t c1 = a.small_total[1], c2 = a.small_total[2], c3 = a.small_total[3], c4 = a.small_total[0];
-  group_class<4, 4, NT>(a, 0, c1, wave, nwaves, lane, k);
-  group_class_t4s<8, NT>(a, c1, c2, wave, nwaves, lane, k);
-  group_class_t4s<16, NT>(a, c2, c3, wave, nwaves, lane, k);
-  group_class_t4s<16, NT>(a, c3, c4, wave, nwaves, lane, k);
+  group_class<4, 4, NT, COPY>(a, 0, c1, wave, nwaves, lane, k);
+  group_class_t4s<8, NT, COPY>(a, c1, c2, wave, nwaves, lane, k);
+  group_class_t4s<16, NT, COPY>(a, c2, c3, wave, nwaves, lane, k);
+  group_class_t4s<16, NT, COPY>(a, c3, c4, wave, nwaves, lane, k);
 }
 
 // Largest c in [0, n) with byte_start[c] <= g (byte_start nondecreasing, byte_start[0] = 0).
@@ -949,8 +1011,10 @@ __device__ __forceinline__ uint64_t snap_cut(uint64_t cs, uint64_t len, uint64_t
 //   T4 = true  (variant 29): 64-B lane runs from coalesced 4 KiB super-blocks (quad transpose),
 //                one super-block prefetched, s_setprio 3 around its loads
 //   GROUP: whole chunks <= 16 KiB go to the class-sized group phase first (same launch)
-template <bool T4, bool GROUP, int DIAG = 0>
+//   COPY: copy-through (SweepArgs::copy_dst), T4 and GROUP only
+template <bool T4, bool GROUP, int DIAG = 0, bool COPY = false>
 __global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
+  static_assert(!COPY || (T4 && GROUP && DIAG == 0), "copy-through is built for the default kernel only");
   // Shares are wave-major over workgroups (share i -> wave i / gridDim.x of workgroup
   // i % gridDim.x), so when a batch has fewer shares than waves they spread over every
   // CU. A share is at least kMinShare bytes: a lone large chunk is cut into ~total/16 KiB
@@ -969,7 +1033,7 @@ __global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * gridDim.x + blockIdx.x);
   if constexpr (GROUP) {
-    if (grp) group_phase_cls<true>(a, wave, nwaves, lane, make_lane_const(lane));
+    if (grp) group_phase_cls<true, COPY>(a, wave, nwaves, lane, make_lane_const(lane));
   }
   // Rounds (SweepArgs::window): equal shares sized so R rounds of nwaves shares cover the
   // batch; wave w takes shares w, w + nwaves, ... A 256 GiB batch read as one round of
@@ -993,7 +1057,8 @@ __global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
 
   // One segment: raw CRC of its body, shifted to the chunk end, + tail + init (wave-uniform).
   // *whole: the segment is the entire chunk, so no other wave contributes to out[ci].
-  auto segment = [&](uint64_t bsc, uint64_t len, uint64_t cs, uint32_t cin, bool* whole) -> uint32_t {
+  // dsh (COPY): the destination of source offset p is (uint8_t*)dsh + p
+  auto segment = [&](uint64_t bsc, uint64_t len, uint64_t cs, uint32_t cin, uint64_t dsh, bool* whole) -> uint32_t {
     const uint64_t ce = cs + len;
     const uint64_t cb = aligned_end(cs, ce);
     const uint64_t r0 = g0 > bsc ? snap_cut(cs, len, g0 - bsc) : 0;
@@ -1005,7 +1070,7 @@ __global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
     uint32_t r = 0;
     if (sa < be) {
       if constexpr (T4) {
-        r = body_crc_t4<1, true, true>(a.base, sa, be, lane, k);
+        r = body_crc_t4<1, true, true, COPY>(a.base, sa, be, lane, k, reinterpret_cast<uint8_t*>(dsh));
       } else {
         r = body_crc<8, true, DIAG>(a.base, sa, be, lane, k);
       }
@@ -1015,6 +1080,9 @@ __global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
     if (se == ce && ce > cb) {  // trailing < 16 bytes, lane-parallel
       const uint64_t t0 = sa > cb ? sa : cb;
       r ^= __builtin_amdgcn_readlane(tail_crc(a.base + t0, (uint32_t)(ce - t0), lane), 0);
+      if constexpr (COPY) {
+        if (lane < ce - t0) reinterpret_cast<uint8_t*>(dsh)[t0 + lane] = a.base[t0 + lane];
+      }
     }
     if (r0 == 0) {  // initial register ~crc_in advanced over the chunk, plus xor-out
       if (cin == 0) {
@@ -1046,13 +1114,14 @@ __global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
     bool done = false;
     while (!done && c < a.n) {
       const uint32_t cnt = a.n - c < 64u ? a.n - c : 64u;
-      uint64_t w_bs = ~0ull, w_len = 0, w_off = 0;
+      uint64_t w_bs = ~0ull, w_len = 0, w_off = 0, w_dst = 0;
       uint32_t w_cin = 0;
       if (lane < cnt) {
         w_bs = a.byte_start[c + lane];
         w_len = a.len[c + lane];
         w_off = a.off[c + lane];
         w_cin = a.crc_in ? a.crc_in[c + lane] : 0u;
+        if constexpr (COPY) w_dst = (uint64_t)(uintptr_t)a.copy_dst + a.copy_off[c + lane] - w_off;
       }
       uint64_t bsc = readlane64(w_bs, 0);
       bool work = false;
@@ -1066,7 +1135,8 @@ __global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
         if (span != 0) {  // empty chunks are finished by the plan kernel
           work = true;
           bool whole;
-          const uint32_t r = segment(bsc, len, readlane64(w_off, j), __builtin_amdgcn_readlane(w_cin, j), &whole);
+          const uint32_t r = segment(bsc, len, readlane64(w_off, j), __builtin_amdgcn_readlane(w_cin, j),
+                                     COPY ? readlane64(w_dst, j) : 0, &whole);
           if (whole && DIAG != 2) {
             if (lane == 0) a.out[c + j] = r;  // no other wave contributes to this chunk
           } else {
@@ -1337,6 +1407,11 @@ hipError_t launch_plan(const PlanArgs& a, hipStream_t s) {
   // one planning block needs no per-block sums (its carry is 0)
   if (blocks > 1) hipLaunchKernelGGL(crc32_plan_count_kernel, dim3(blocks), dim3(256), 0, s, a);
   hipLaunchKernelGGL(crc32_plan_scan_kernel, dim3(blocks), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_sweep_copy(const SweepArgs& a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL((crc32_sweep_kernel<true, true, 0, true>), dim3(grid), dim3(1024), 0, s, a);
   return hipGetLastError();
 }
 

@@ -47,9 +47,10 @@ __global__ __launch_bounds__(256) void put_layout_kernel(PutArgs a) {
                            d.blob_len};
   for (uint32_t k = 0; k < kPutSlots; ++k) {
     const uint8_t* base = k == 4 ? a.blobs : a.fields;
-    a.cp_src[k * m + i] = base ? (uint64_t)(uintptr_t)(base + src[k]) : 0;
+    a.cp_src[k * m + i] = base ? (uint64_t)(uintptr_t)(base + src[k])
+                               : (a.copy_through ? (uint64_t)(uintptr_t)(msg + fo[k]) : 0);
     a.cp_dst[k * m + i] = d.out_off + fo[k];
-    a.cp_len[k * m + i] = base ? len[k] : 0;
+    a.cp_len[k * m + i] = base || a.copy_through ? len[k] : 0;
     a.cp_cost[k * m + i] = base && len[k] ? len[k] + kCopyJobCost : 0;
     uint64_t off, ln;
     bool present;
@@ -62,6 +63,26 @@ __global__ __launch_bounds__(256) void put_layout_kernel(PutArgs a) {
     }
   }
   if (a.msg_len) a.msg_len[i] = L.length;
+}
+
+// Copy-through mode: crc[j] holds the CRC of job j's content (the field bytes after the record
+// prefix); the record CRC follows by combine, crc(prefix || content) = crc(prefix) * x^(8|content|)
+// ^ crc(content), with the prefix (<= 13 B: version, size fields) hashed here from the message.
+// Slot 0's copy job is the key, which no CRC covers: the header CRC is hashed whole.
+__global__ __launch_bounds__(256) void put_seal_combine_kernel(PutArgs a) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= kPutSlots * a.m) return;
+  const uint64_t len = a.crc_len[j];
+  if (len == 0) return;  // absent encryption-key record
+  uint8_t* rec = a.out + a.crc_off[j];
+  uint32_t crc;
+  if (j < a.m) {
+    crc = crc_bytes_img(a.img, 0u, rec, (uint32_t)len);
+  } else {
+    const uint64_t cl = a.cp_len[j];
+    crc = mul_xpow8_img(a.img, crc_bytes_img(a.img, 0u, rec, (uint32_t)(len - cl)), cl) ^ a.crc[j];
+  }
+  put_be64(rec + len, (uint64_t)crc);
 }
 
 __global__ __launch_bounds__(256) void put_seal_kernel(PutArgs a) {
@@ -222,6 +243,12 @@ hipError_t launch_put_layout(const PutArgs& a, hipStream_t s) {
 hipError_t launch_put_seal(const PutArgs& a, hipStream_t s) {
   if (a.m == 0) return hipSuccess;
   hipLaunchKernelGGL(put_seal_kernel, dim3((uint32_t)((kPutSlots * a.m + 255) / 256)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_put_seal_combine(const PutArgs& a, hipStream_t s) {
+  if (a.m == 0) return hipSuccess;
+  hipLaunchKernelGGL(put_seal_combine_kernel, dim3((uint32_t)((kPutSlots * a.m + 255) / 256)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
