@@ -175,6 +175,11 @@ __device__ __forceinline__ u32x4 ld16(const u32x4* p) {
 // memcpy becomes one global_store_dwordx4); a piece that starts before the chunk stores only
 // its bytes from `lo` on.
 __device__ __forceinline__ void st16u(uint8_t* d, const u32x4& v) { __builtin_memcpy(d, &v, 16); }
+// Wave-mode bodies (large chunks) stream their stores nontemporal: 3-5 % faster there, 18 %
+// slower in the group phase's short records (r02x A/B), which keep the plain store.
+__device__ __forceinline__ void st16u_nt(uint8_t* d, const u32x4& v) {
+  __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(d));
+}
 
 __device__ __forceinline__ void copy_piece(uint8_t* dbase, int64_t p, const u32x4& v, int64_t lo) {
   if (p + 16 <= lo) return;
@@ -423,7 +428,7 @@ __device__ __forceinline__ uint32_t body_crc_t4(const uint8_t* __restrict__ base
         if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
         if constexpr (COPY) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) st16u(dbase + v0 + (int64_t)((b + u) * SB) + 1024 * i + 16 * lane, cur[i]);
+          for (int i = 0; i < 4; ++i) st16u_nt(dbase + v0 + (int64_t)((b + u) * SB) + 1024 * i + 16 * lane, cur[i]);
         }
         quad_transpose_asm(cur);
         s = run_crc<4>(cur, k, nib_mul(s, kFold));
@@ -433,7 +438,7 @@ __device__ __forceinline__ uint32_t body_crc_t4(const uint8_t* __restrict__ base
     for (int u = 0; u < UB; ++u) {
       if constexpr (COPY) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) st16u(dbase + v0 + (int64_t)((b + u) * SB) + 1024 * i + 16 * lane, buf[u][i]);
+        for (int i = 0; i < 4; ++i) st16u_nt(dbase + v0 + (int64_t)((b + u) * SB) + 1024 * i + 16 * lane, buf[u][i]);
       }
       quad_transpose_asm(buf[u]);
       s = run_crc<4>(buf[u], k, nib_mul(s, kFold));
@@ -446,7 +451,7 @@ __device__ __forceinline__ uint32_t body_crc_t4(const uint8_t* __restrict__ base
     for (int i = 0; i < 4; ++i) cur[i] = ld16<NT>(q + b * 256 + i * 64);
     if constexpr (COPY) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) st16u(dbase + v0 + (int64_t)(b * SB) + 1024 * i + 16 * lane, cur[i]);
+      for (int i = 0; i < 4; ++i) st16u_nt(dbase + v0 + (int64_t)(b * SB) + 1024 * i + 16 * lane, cur[i]);
     }
     quad_transpose_asm(cur);
     s = run_crc<4>(cur, k, nib_mul(s, kFold));

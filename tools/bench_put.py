@@ -20,14 +20,17 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def run(m, blob_bytes, reps, in_place):
+def run(m, blob_bytes, reps, in_place, um_len=1000):
     import numpy as np
     import torch
 
     from ambry_amd import device as D
     from ambry_amd.messages import PUT_DESC_DTYPE, PutMessage, layout, serialize_dev, serialize_host
 
-    key_len, props_len, um_len = 24, 94, 1000
+    # blob content at message offset 40 + 24 + 104 + (um_len + 14) + 13: 1195 = 11 mod 16 for the
+    # default 1000-B user metadata (the copy's stores then sit 11 B off the loads); --um-len 1005
+    # aligns them
+    key_len, props_len = 24, 94
     tmpl = PutMessage(key=bytes(key_len), props=bytes(props_len), usermeta=bytes(um_len), blob=bytes(blob_bytes))
     L, fo = layout(tmpl)
     stride = (L + 15) // 16 * 16
@@ -105,7 +108,10 @@ def run_transform(m, blob_bytes, reps):
     from ambry_amd import device as D
     from ambry_amd.messages import PUT_DESC_DTYPE, PutMessage, layout, serialize_dev, transform_dev
 
-    key_len, props_len, um_len = 24, 94, 1000
+    # blob content at message offset 40 + 24 + 104 + (um_len + 14) + 13: 1195 = 11 mod 16 for the
+    # default 1000-B user metadata (the copy's stores then sit 11 B off the loads); --um-len 1005
+    # aligns them
+    key_len, props_len = 24, 94
     L, _ = layout(PutMessage(key=bytes(key_len), props=bytes(props_len), usermeta=bytes(um_len),
                              blob=bytes(blob_bytes)))
     descs = np.zeros(m, dtype=PUT_DESC_DTYPE)
@@ -148,6 +154,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--cases", default="64k,4k,4m")
+    ap.add_argument("--um-len", type=int, default=1000, help="user metadata bytes per PUT (1005: blob stores aligned)")
+    ap.add_argument("--copy-only", action="store_true", help="skip the in-place mode")
     ap.add_argument("--transform", default="64k,4k,4m", help="ValidatingTransformer cases ('' for none)")
     args = ap.parse_args()
     import torch
@@ -160,7 +168,11 @@ def main():
     for c in [x for x in args.cases.split(",") if x]:
         m, s = cases[c]
         for in_place in (False, True):
-            print(json.dumps(run(m, s, args.reps, in_place)), flush=True)
+            if in_place and args.copy_only:
+                continue
+            r = run(m, s, args.reps, in_place, args.um_len)
+            r["usermeta_bytes"] = args.um_len
+            print(json.dumps(r), flush=True)
             torch.cuda.empty_cache()
     for c in [x for x in args.transform.split(",") if x]:
         m, s = cases[c]
