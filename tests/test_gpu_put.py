@@ -29,7 +29,8 @@ def _dev(b):
     return torch.frombuffer(bytearray(b if len(b) else b"\0"), dtype=torch.uint8).cuda()
 
 
-def _run(gpu, mf, msgs, out_align, field_align, gap, in_place=False):
+def _run(gpu, mf, msgs, out_align, field_align, gap, in_place=False, place=("key", "enckey", "props", "usermeta",
+                                                                           "blob")):
     import torch
 
     from ambry_amd.messages import layout, pack_batch, serialize_dev
@@ -39,14 +40,15 @@ def _run(gpu, mf, msgs, out_align, field_align, gap, in_place=False):
     if in_place:
         for m, o in zip(msgs, offs):
             _, fo = layout(m)
-            for name in ("key", "enckey", "props", "usermeta", "blob"):
+            for name in place:
                 b = getattr(m, name)
                 if b:
                     host_out[o + fo[name]:o + fo[name] + len(b)] = b
     out = _dev(bytes(host_out))
     mlen = torch.empty(len(msgs), dtype=torch.int64, device="cuda")
-    serialize_dev(_dev(descs.tobytes()), out, None if in_place else _dev(fields), None if in_place else _dev(blobs),
-                  msg_len=mlen)
+    fields_in = None if in_place and "key" in place else _dev(fields)
+    blobs_in = None if in_place and "blob" in place else _dev(blobs)
+    serialize_dev(_dev(descs.tobytes()), out, fields_in, blobs_in, msg_len=mlen)
     torch.cuda.synchronize()
     got = out.cpu().numpy().tobytes()
     exp = bytearray(b"\xAA" * total)
@@ -84,3 +86,10 @@ def test_serialize_large_blobs(gpu, mf):
                        usermeta=b"m" * 1000, blob=stream_bytes(50 + i, 0, (4 << 20) - (i % 3)).tobytes(),
                        header_version=3) for i in range(12)]
     _run(gpu, mf, msgs, 1, 1, 0)
+
+
+@pytest.mark.parametrize("place", [("blob",), ("key", "enckey", "props", "usermeta")])
+def test_serialize_batch_mixed(gpu, mf, place):
+    """One source buffer given, the other slots already in place: the copy-through sweep copies
+    the given fields and re-reads the in-place ones where they lie."""
+    _run(gpu, mf, random_messages(mf, 300, seed=13), 1, 5, 2, in_place=True, place=place)
