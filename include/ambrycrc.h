@@ -216,12 +216,14 @@ int ambrycrc_serialize_put_host(const ambrycrc_put_desc* d, const uint8_t* field
                                 uint64_t out_cap, uint32_t* crcs);
 
 /* m messages on the GPU (d_desc: device array): one thread per message writes the header and
- * record prefixes, a byte-balanced copy kernel moves key / encryption key / properties /
- * user metadata (from d_fields) and blob contents (from d_blobs) into place, the batch CRC
- * kernels compute every record CRC (the group phase takes the small records, the sweep the
- * blobs), and a last kernel writes the trailers. d_fields / d_blobs NULL: those bytes are
- * already in place in d_out (ambrycrc_put_layout). d_msg_len[m] (nullable): message lengths.
- * Descriptors must be valid (ambrycrc_put_layout != 0) and messages must not overlap.
+ * record prefixes. With d_fields or d_blobs given, the batch CRC kernels read key / encryption
+ * key / properties / user metadata (from d_fields) and blob contents (from d_blobs) once, write
+ * them into place and CRC them in the same pass (copy-through); a last kernel extends those CRCs
+ * over the record prefixes and writes the trailers. d_fields / d_blobs NULL: those bytes are
+ * already in place in d_out (ambrycrc_put_layout) and are CRC'd there; both NULL is a single
+ * read pass. d_msg_len[m] (nullable): message lengths. Descriptors must be valid
+ * (ambrycrc_put_layout != 0), messages must not overlap, and the source buffers must not
+ * overlap d_out.
  * Asynchronous on `stream`; d_ws >= ambrycrc_serialize_puts_workspace_bytes(m) or NULL. */
 size_t ambrycrc_serialize_puts_workspace_bytes(size_t m);
 int ambrycrc_serialize_puts_dev(const ambrycrc_put_desc* d_desc, size_t m, const uint8_t* d_fields,
