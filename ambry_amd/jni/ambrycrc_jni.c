@@ -3,10 +3,11 @@
  * (integration/java/com/github/ambry/utils/NativeCrc32.java) to libambrycrc's C ABI
  * (include/ambrycrc.h).
  *
- * Built only where a JDK provides jni.h (`make -C ambry_amd jni JAVA_HOME=...`); this build
- * image has no JDK, so the shim is source-only here. Its argument checks and
- * marshalling live in ambrycrc_jni_core.c (plain C, built and tested without a JDK:
- * tests/test_jni_core.py); this file only moves Java values in and out.
+ * Built for a JVM where a JDK provides jni.h (`make -C ambry_amd jni JAVA_HOME=...`). This build
+ * image has no JDK: tests/test_jni_core.py compiles this file against a test-only
+ * JNI subset (tests/native/jni_stub/jni.h) and runs it in a fake JVM (tests/native/jni_harness.c).
+ * Its argument checks and marshalling live in ambrycrc_jni_core.c (plain C, tested through
+ * ctypes); this file only moves Java values in and out.
  *
  * Errors never travel in the CRC slot: a failed check or a native error throws (the matching
  * java.lang exception from ajc_exception_class) and the native method returns; the Java

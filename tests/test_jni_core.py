@@ -118,3 +118,38 @@ def test_exception_mapping(core):
     for code in (-2, -4, -5, -6):
         assert cls(code) == b"java/lang/IllegalStateException"
     assert core.ajc_message(-4).decode().startswith("ambrycrc_init")
+
+
+def test_jni_shim_against_fake_jvm(core, tmp_path):
+    """ambrycrc_jni.c itself, compiled (-Wall -Wextra -Werror) against the JNI subset in
+    tests/native/jni_stub/jni.h and run inside the fake JVM of tests/native/jni_harness.c: the
+    exported Java_com_github_ambry_utils_NativeCrc32_* entries return zlib's CRCs, leave the CRC
+    argument unchanged when they throw, and throw the exception class the core maps."""
+    import subprocess
+
+    amd = os.path.join(ROOT, "ambry_amd")
+    exe = str(tmp_path / "jni_harness")
+    subprocess.run(["gcc", "-std=c11", "-O1", "-Wall", "-Wextra", "-Werror",
+                    "-I", os.path.join(ROOT, "tests", "native", "jni_stub"), "-I/opt/rocm/include",
+                    "-D__HIP_PLATFORM_AMD__", "-o", exe, os.path.join(ROOT, "tests", "native", "jni_harness.c"),
+                    os.path.join(amd, "jni", "ambrycrc_jni.c"), "-L", amd, "-lambrycrc_jnicore", "-lambrycrc",
+                    "-Wl,-rpath," + amd], check=True, capture_output=True)
+    out = subprocess.run([exe], check=True, capture_output=True, text=True, timeout=120).stdout
+    got = {name: (int(val, 16), exc) for name, val, exc in (line.split() for line in out.splitlines())}
+    crc = lambda b: zlib.crc32(b)  # noqa: E731
+    NPE, IOOBE = "java/lang/NullPointerException", "java/lang/IndexOutOfBoundsException"
+    IAE = "java/lang/IllegalArgumentException"
+    expect = {
+        "array_full": (crc(b"123456789"), "-"), "array_tail": (crc(b"56789"), "-"),
+        "array_bounds": (0x1234, IOOBE), "array_negative": (0x1234, IOOBE), "array_null": (0x1234, NPE),
+        "direct_full": (crc(b"123456789"), "-"), "direct_bounds": (7, IOOBE), "direct_heap": (7, IAE),
+        "direct_null": (7, NPE), "byte": (crc(b"1"), "-"), "combine": (crc(b"123456789"), "-"),
+        "combine_negative": (0, IAE), "direct_all": (crc(b"123456789"), "-"), "direct_all_bounds": (0, IOOBE),
+        "direct_all_heap": (0, IAE), "batch_short_out": (0, IAE), "batch_null": (0, NPE),
+        "batch_bounds": (0, IOOBE), "verify_short_status": (0, IAE), "verify_heap": (0, IAE),
+        "verify_null": (0, NPE),
+    }
+    for name, want in expect.items():
+        assert got[name] == want, name
+    # without a GPU ambrycrc_init fails and nativeInit throws; with one it succeeds
+    assert got["init_no_gpu"] in ((0, "java/lang/IllegalStateException"), (0, "-"))
