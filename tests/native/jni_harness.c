@@ -149,7 +149,34 @@ static struct _jobject arr(enum Kind k, void* data, jsize len) {
   return o;
 }
 
-int main(void) {
+/* With a GPU (argv[1] == "gpu"): the device entries on valid arguments. */
+static int gpu_cases(void) {
+  FN(nativeInit)(&g_env, NULL, 0);
+  report("gpu_init", 0);
+  static uint8_t s1[] = "123", s2[] = "xx456", s3[] = "789yy", region[] = "123456789";
+  struct _jobject g1 = arr(K_BUFFER, s1, 3), g2 = arr(K_BUFFER, s2, 5), g3 = arr(K_BUFFER, s3, 5);
+  jobject list[3] = {&g1, &g2, &g3};
+  struct _jobject lst = arr(K_OBJS, list, 3);
+  jint pos[3] = {0, 2, 1}, len[3] = {3, 3, 4}, cin[3] = {0, 0, 0}, out[3] = {0, 0, 0};
+  struct _jobject jpos = arr(K_INTS, pos, 3), jlen = arr(K_INTS, len, 3), jcin = arr(K_INTS, cin, 3);
+  struct _jobject jout = arr(K_INTS, out, 3);
+  FN(nativeBatchDirect)(&g_env, NULL, &lst, &jpos, &jlen, &jcin, &jout, 0);
+  report("gpu_batch_0", out[0]);
+  report("gpu_batch_1", out[1]);
+  report("gpu_batch_2", out[2]);
+  struct _jobject reg = arr(K_BUFFER, region, 9);
+  jlong offs[2] = {0, 4}, ends[2] = {7, 7};
+  jint st[2] = {0, 0};
+  struct _jobject joffs = arr(K_LONGS, offs, 2), jst = arr(K_INTS, st, 2), jends = arr(K_LONGS, ends, 2);
+  FN(nativeVerifyMessages)(&g_env, NULL, &reg, &joffs, &jst, &jends, 0);
+  report("gpu_verify_0", st[0]);
+  report("gpu_verify_1", st[1]);
+  report("gpu_verify_end", (jint)(ends[0] + ends[1]));
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  if (argc > 1 && strcmp(argv[1], "gpu") == 0) return gpu_cases();
   static uint8_t digits[] = "123456789";
   struct _jobject b9 = arr(K_BYTES, digits, 9);
   report("array_full", FN(nativeUpdateArray)(&g_env, NULL, 0, &b9, 0, 9));

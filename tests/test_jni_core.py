@@ -120,11 +120,7 @@ def test_exception_mapping(core):
     assert core.ajc_message(-4).decode().startswith("ambrycrc_init")
 
 
-def test_jni_shim_against_fake_jvm(core, tmp_path):
-    """ambrycrc_jni.c itself, compiled (-Wall -Wextra -Werror) against the JNI subset in
-    tests/native/jni_stub/jni.h and run inside the fake JVM of tests/native/jni_harness.c: the
-    exported Java_com_github_ambry_utils_NativeCrc32_* entries return zlib's CRCs, leave the CRC
-    argument unchanged when they throw, and throw the exception class the core maps."""
+def _run_harness(tmp_path, *args):
     import subprocess
 
     amd = os.path.join(ROOT, "ambry_amd")
@@ -134,8 +130,16 @@ def test_jni_shim_against_fake_jvm(core, tmp_path):
                     "-D__HIP_PLATFORM_AMD__", "-o", exe, os.path.join(ROOT, "tests", "native", "jni_harness.c"),
                     os.path.join(amd, "jni", "ambrycrc_jni.c"), "-L", amd, "-lambrycrc_jnicore", "-lambrycrc",
                     "-Wl,-rpath," + amd], check=True, capture_output=True)
-    out = subprocess.run([exe], check=True, capture_output=True, text=True, timeout=120).stdout
-    got = {name: (int(val, 16), exc) for name, val, exc in (line.split() for line in out.splitlines())}
+    out = subprocess.run([exe, *args], check=True, capture_output=True, text=True, timeout=120).stdout
+    return {name: (int(val, 16), exc) for name, val, exc in (line.split() for line in out.splitlines())}
+
+
+def test_jni_shim_against_fake_jvm(core, tmp_path):
+    """ambrycrc_jni.c itself, compiled (-Wall -Wextra -Werror) against the JNI subset in
+    tests/native/jni_stub/jni.h and run inside the fake JVM of tests/native/jni_harness.c: the
+    exported Java_com_github_ambry_utils_NativeCrc32_* entries return zlib's CRCs, leave the CRC
+    argument unchanged when they throw, and throw the exception class the core maps."""
+    got = _run_harness(tmp_path)
     crc = lambda b: zlib.crc32(b)  # noqa: E731
     NPE, IOOBE = "java/lang/NullPointerException", "java/lang/IndexOutOfBoundsException"
     IAE = "java/lang/IllegalArgumentException"
@@ -153,3 +157,17 @@ def test_jni_shim_against_fake_jvm(core, tmp_path):
         assert got[name] == want, name
     # without a GPU ambrycrc_init fails and nativeInit throws; with one it succeeds
     assert got["init_no_gpu"] in ((0, "java/lang/IllegalStateException"), (0, "-"))
+
+
+@pytest.mark.gpu
+def test_jni_shim_device_entries(core, tmp_path):
+    """The shim's device entries on a GPU, in the fake JVM: nativeBatchDirect over three direct
+    buffers at positions 0 / 2 / 1 (ambrycrc_batch_host), nativeVerifyMessages over a region
+    holding no message (AMBRYCRC_MSG_BAD_VERSION at both offsets, ends 0)."""
+    got = _run_harness(tmp_path, "gpu")
+    assert got["gpu_init"] == (0, "-")
+    assert got["gpu_batch_0"] == (zlib.crc32(b"123"), "-")
+    assert got["gpu_batch_1"] == (zlib.crc32(b"456"), "-")
+    assert got["gpu_batch_2"] == (zlib.crc32(b"89yy"), "-")
+    assert got["gpu_verify_0"] == (1 << 8, "-") and got["gpu_verify_1"] == (1 << 8, "-")
+    assert got["gpu_verify_end"] == (0, "-")
