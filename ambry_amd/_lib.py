@@ -89,6 +89,12 @@ _SIGNATURES = [
       ctypes.c_size_t, ctypes.c_int, ctypes.c_int]),
     ("ambrycrc_chain_messages_host", ctypes.c_size_t,
      [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t]),
+    ("ambrycrc_verify_message_cpu", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint32),
+      ctypes.POINTER(ctypes.c_uint64)]),
+    ("ambrycrc_transform_message_cpu", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+      ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32)]),
     ("ambrycrc_batch_host", ctypes.c_int,
      [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32),
       ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t, ctypes.c_int, ctypes.c_int]),

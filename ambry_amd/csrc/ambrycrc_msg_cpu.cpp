@@ -1,0 +1,190 @@
+// ambrycrc_msg_cpu.cpp -- one stored message on the CPU: deserializeBlobAll's checks
+// (MessageFormatRecord.java:257-303) and ValidatingTransformer.transform
+// (ValidatingTransformer.java:46-104), for the per-message callers (a GET of one blob, a
+// replication thread transforming one message) that a device batch does not fit. The
+// semantics and status bits are ambrycrc_verify_messages_dev's and
+// ambrycrc_transform_messages_dev's (message_kernels.hip); the CRCs run through the CLMUL
+// host loop (ambrycrc_update).
+#include "../../include/ambrycrc.h"
+
+#include <string.h>
+
+#include "put_layout.h"
+
+namespace {
+
+uint32_t rd16(const uint8_t* p) { return (uint32_t)p[0] << 8 | p[1]; }
+uint32_t rd32(const uint8_t* p) { return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3]; }
+uint64_t rd64(const uint8_t* p) { return (uint64_t)rd32(p) << 32 | rd32(p + 4); }
+
+constexpr uint32_t kRecordBit[5] = {AMBRYCRC_MSG_ENCKEY_CRC, AMBRYCRC_MSG_PROPS_CRC, AMBRYCRC_MSG_UPDATE_CRC,
+                                    AMBRYCRC_MSG_USERMETA_CRC, AMBRYCRC_MSG_BLOB_CRC};
+
+// The record-level reads of each deserializer before its CRC (message_kernels.hip record_check).
+uint32_t record_check(int k, const uint8_t* q, uint64_t span) {
+  if (span < 10) return AMBRYCRC_MSG_BAD_RECORD;
+  const uint32_t v = rd16(q);
+  switch (k) {
+    case 0:
+    case 3: {
+      if (v != 1) return AMBRYCRC_MSG_BAD_VERSION;
+      if (span < 14) return AMBRYCRC_MSG_BAD_RECORD;
+      const int32_t n = (int32_t)rd32(q + 2);
+      return n >= 0 && (uint64_t)n + 14 == span ? 0u : AMBRYCRC_MSG_BAD_RECORD;
+    }
+    case 1:
+      return v == 1 ? 0u : AMBRYCRC_MSG_BAD_VERSION;
+    case 2:
+      return v >= 1 && v <= 3 ? 0u : AMBRYCRC_MSG_BAD_VERSION;
+    default: {
+      if (v < 1 || v > 3) return AMBRYCRC_MSG_BAD_VERSION;
+      const uint32_t head = v == 1 ? 10u : v == 2 ? 12u : 13u;
+      if (span < head + 8) return AMBRYCRC_MSG_BAD_RECORD;
+      const uint32_t type = v == 1 ? 0u : rd16(q + 2);
+      const uint64_t size = rd64(q + (v == 1 ? 2 : v == 2 ? 4 : 5));
+      return type < 2 && size <= 0x7FFFFFFFull && size + head + 8 == span ? 0u : AMBRYCRC_MSG_BAD_RECORD;
+    }
+  }
+}
+
+struct Parsed {
+  uint32_t version, hsize, life;
+  int64_t total;
+  int32_t rel[5];  // encryption key, properties, update, user metadata, blob; -1 absent
+  uint64_t end;    // message end, relative
+};
+
+// Header and every record of the message at p (rem bytes available): status bits.
+uint32_t verify(const uint8_t* p, uint64_t rem, Parsed* m) {
+  m->end = 0;
+  if (rem < 2) return AMBRYCRC_MSG_BAD_LAYOUT;
+  const int v = (int16_t)rd16(p);
+  const uint32_t h = v == 1 ? 34u : v == 2 ? 38u : v == 3 ? 40u : 0u;
+  if (h == 0) return AMBRYCRC_MSG_BAD_VERSION;
+  if (rem < h) return AMBRYCRC_MSG_BAD_LAYOUT;
+  if ((uint64_t)ambrycrc_update(0, p, h - 8) != rd64(p + h - 8)) return AMBRYCRC_MSG_HEADER_CRC;  // verifyHeader
+  m->version = (uint32_t)v;
+  m->hsize = h;
+  m->life = 0;
+  if (v == 3) {
+    if ((int16_t)rd16(p + 2) < 0) return AMBRYCRC_MSG_BAD_LAYOUT;  // checkHeaderConstraints
+    m->life = rd16(p + 2);
+    m->total = (int64_t)rd64(p + 4);
+    for (int k = 0; k < 5; ++k) m->rel[k] = (int32_t)rd32(p + 12 + 4 * k);
+  } else {
+    m->total = (int64_t)rd64(p + 2);
+    const uint8_t* q = p + 10;
+    if (v == 1) {
+      m->rel[0] = -1;
+      for (int k = 0; k < 4; ++k) m->rel[k + 1] = (int32_t)rd32(q + 4 * k);
+    } else {
+      for (int k = 0; k < 5; ++k) m->rel[k] = (int32_t)rd32(q + 4 * k);
+    }
+  }
+  const int32_t* rel = m->rel;
+  const bool is_put = rel[1] != -1 && rel[2] == -1 && rel[3] != -1 && rel[4] != -1;
+  const bool is_upd = rel[2] != -1 && rel[0] == -1 && rel[1] == -1 && rel[3] == -1 && rel[4] == -1;
+  if (m->total <= 0 || !(is_put || is_upd)) return AMBRYCRC_MSG_BAD_LAYOUT;
+  int64_t prev = -1, first = -1;
+  for (int k = 0; k < 5; ++k) {
+    if (rel[k] == -1) continue;
+    if (rel[k] <= prev || rel[k] < (int32_t)h) return AMBRYCRC_MSG_BAD_LAYOUT;
+    if (first < 0) first = rel[k];
+    prev = rel[k];
+  }
+  if ((uint64_t)m->total > rem || (uint64_t)first > rem - (uint64_t)m->total) return AMBRYCRC_MSG_BAD_LAYOUT;
+  const uint64_t end = (uint64_t)first + (uint64_t)m->total;
+  uint64_t rend[5];
+  for (int k = 0; k < 5; ++k) {
+    rend[k] = end;
+    for (int j = k + 1; j < 5; ++j)
+      if (rel[j] != -1) {
+        rend[k] = (uint64_t)rel[j];
+        break;
+      }
+    if (rel[k] != -1 && rend[k] < (uint64_t)rel[k] + 8) return AMBRYCRC_MSG_BAD_LAYOUT;
+  }
+  uint32_t status = 0;
+  for (int k = 0; k < 5; ++k) {
+    if (rel[k] == -1) continue;
+    const uint8_t* q = p + rel[k];
+    const uint64_t span = rend[k] - (uint64_t)rel[k];
+    if ((uint64_t)ambrycrc_update(0, q, span - 8) != rd64(q + span - 8)) status |= kRecordBit[k];
+    status |= record_check(k, q, span);
+  }
+  m->end = end;
+  return status;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ambrycrc_verify_message_cpu(const uint8_t* region, uint64_t region_len, uint64_t off, uint32_t* status,
+                                uint64_t* msg_end) {
+  if (!region || !status) return AMBRYCRC_EINVAL;
+  Parsed m;
+  *status = off <= region_len ? verify(region + off, region_len - off, &m) : (uint32_t)AMBRYCRC_MSG_BAD_LAYOUT;
+  if (msg_end) *msg_end = off <= region_len && m.end ? off + m.end : 0;
+  return AMBRYCRC_OK;
+}
+
+int ambrycrc_transform_message_cpu(const uint8_t* region, uint64_t region_len, uint64_t off, int life_version,
+                                   int header_version, uint8_t* out, uint64_t out_cap, uint64_t* out_len,
+                                   uint32_t* status) {
+  if (!region || !out_len || !status || header_version < 1 || header_version > 3 || life_version > 32767)
+    return AMBRYCRC_EINVAL;
+  *out_len = 0;
+  Parsed m;
+  m.end = 0;
+  uint32_t st = off <= region_len ? verify(region + off, region_len - off, &m) : (uint32_t)AMBRYCRC_MSG_BAD_LAYOUT;
+  if (st) {
+    *status = st;
+    return AMBRYCRC_OK;
+  }
+  const uint8_t* p = region + off;
+  const int32_t enc = m.rel[0], bp = m.rel[1], upd = m.rel[2], um = m.rel[3], blob = m.rel[4];
+  if (upd != -1 || bp == -1 || um == -1 || blob == -1) {  // "cannot be anything rather than put record"
+    *status = AMBRYCRC_MSG_NOT_PUT;
+    return AMBRYCRC_OK;
+  }
+  // the deserializers' field reads (deserializeBlobEncryptionKey / Properties / UserMetadata / Blob,
+  // MessageFormatRecord.java:1568-1833); verify's record checks already hold for them
+  const int64_t first = enc != -1 ? enc : bp;
+  const uint32_t bv = rd16(p + blob);
+  const uint32_t head = bv == 1 ? 10u : bv == 2 ? 12u : 13u;
+  ambrycrc_put_desc d;
+  memset(&d, 0, sizeof d);
+  const bool keep_enc = enc != -1 && header_version >= 2;
+  d.out_off = 0;
+  d.key_src = off + m.hsize;
+  d.key_len = (uint32_t)(first - m.hsize);
+  d.enckey_src = keep_enc ? off + enc + 6 : 0;
+  d.enckey_len = keep_enc ? (int32_t)rd32(p + enc + 2) : -1;
+  d.props_src = off + bp + 2;
+  d.props_len = (uint32_t)(um - bp - 2 - 8);
+  d.usermeta_src = off + um + 6;
+  d.usermeta_len = rd32(p + um + 2);
+  d.blob_src = off + blob + head;
+  d.blob_len = rd64(p + blob + (bv == 1 ? 2 : bv == 2 ? 4 : 5));
+  d.life_version = (int16_t)(life_version >= 0 ? life_version : (int)m.life);
+  d.blob_type = (int16_t)(bv == 1 ? 0u : rd16(p + blob + 2));
+  d.compressed = (uint8_t)(bv == 3 && p[blob + 4] == 1 ? 1 : 0);
+  d.header_version = (uint8_t)header_version;
+  const uint64_t n = ambrycrc_put_layout(&d, nullptr);
+  if (n == 0) {
+    *status = AMBRYCRC_MSG_BAD_RECORD;
+    return AMBRYCRC_OK;
+  }
+  if (!out || n > out_cap) {
+    *status = AMBRYCRC_MSG_NO_ROOM;
+    return AMBRYCRC_OK;
+  }
+  const int rc = ambrycrc_serialize_put_host(&d, region, region, out, out_cap, nullptr);
+  if (rc) return rc;
+  *out_len = n;
+  *status = 0;
+  return AMBRYCRC_OK;
+}
+
+}  // extern "C"

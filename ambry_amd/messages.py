@@ -122,6 +122,29 @@ def serialize_dev(descs, out, fields=None, blobs=None, msg_len=None, stream=None
                                             ctypes.c_void_p(_stream_handle(stream))), "ambrycrc_serialize_puts_dev")
 
 
+def verify_message_cpu(region, off: int):
+    """ambrycrc_verify_message_cpu: (AMBRYCRC_MSG_* status bits, message end or 0) for the message
+    at `off` in a host buffer (bytes / bytearray / uint8 numpy array)."""
+    buf = np.frombuffer(region, dtype=np.uint8) if not isinstance(region, np.ndarray) else region
+    st, end = ctypes.c_uint32(0), ctypes.c_uint64(0)
+    check(lib().ambrycrc_verify_message_cpu(buf.ctypes.data_as(ctypes.c_void_p), buf.size, off, ctypes.byref(st),
+                                            ctypes.byref(end)), "ambrycrc_verify_message_cpu")
+    return st.value, end.value
+
+
+def transform_message_cpu(region, off: int, header_version: int = 3, life=None, out_cap=None):
+    """ambrycrc_transform_message_cpu: (status bits, the re-serialized message or None)."""
+    buf = np.frombuffer(region, dtype=np.uint8) if not isinstance(region, np.ndarray) else region
+    cap = out_cap if out_cap is not None else buf.size + 64  # a transform grows a message by <= 9 B
+    out = np.zeros(max(cap, 1), dtype=np.uint8)
+    st, n = ctypes.c_uint32(0), ctypes.c_uint64(0)
+    check(lib().ambrycrc_transform_message_cpu(buf.ctypes.data_as(ctypes.c_void_p), buf.size, off,
+                                               -1 if life is None else int(life), header_version,
+                                               out.ctypes.data_as(ctypes.c_void_p), cap, ctypes.byref(n),
+                                               ctypes.byref(st)), "ambrycrc_transform_message_cpu")
+    return st.value, (out[:n.value].tobytes() if st.value == 0 else None)
+
+
 # status bits added by the transform (include/ambrycrc.h)
 MSG_NOT_PUT = 1 << 10
 MSG_BAD_RECORD = 1 << 11

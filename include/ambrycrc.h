@@ -289,6 +289,24 @@ int ambrycrc_verify_messages_host(const uint8_t* region, uint64_t region_len, co
 size_t ambrycrc_chain_messages_host(const uint8_t* region, uint64_t region_len, uint64_t start, uint64_t* offs,
                                     size_t max);
 
+/* One message on the CPU, for per-message callers (a GET of one blob through
+ * MessageFormatSend.java:131-139, BlobStoreRecovery's per-message read): the checks of
+ * ambrycrc_verify_messages_dev (header, every record CRC, record versions and size fields) for
+ * the message at region + off, with the CLMUL host loop. *status = AMBRYCRC_MSG_* bits;
+ * *msg_end (nullable) = offset one past the message, or 0 when unparseable. */
+int ambrycrc_verify_message_cpu(const uint8_t* region, uint64_t region_len, uint64_t off, uint32_t* status,
+                                uint64_t* msg_end);
+
+/* ValidatingTransformer.transform (ValidatingTransformer.java:46-104) for one stored message on
+ * the CPU, as ambrycrc_transform_messages_dev does it for a batch: verify, refuse update records,
+ * deserialize, re-serialize at header_version (1..3) with life_version (< 0: the stored one;
+ * V1/V2 headers carry none) into out[0 .. *out_len). *status = AMBRYCRC_MSG_* verify bits |
+ * AMBRYCRC_MSG_NOT_PUT / _BAD_RECORD / _NO_ROOM (out_cap too small; *out_len 0); 0 = transformed.
+ * out must not overlap the region. */
+int ambrycrc_transform_message_cpu(const uint8_t* region, uint64_t region_len, uint64_t off, int life_version,
+                                   int header_version, uint8_t* out, uint64_t out_cap, uint64_t* out_len,
+                                   uint32_t* status);
+
 /* ------------------------------------------------------- host-resident batch */
 
 /* CRC-32 of n host chunks (ptrs[i], lens[i]) on `device`: chunks are packed into

@@ -242,6 +242,38 @@ def test_chain_messages_host_under_asan(tmp_path):
     assert "runs=" in r.stdout
 
 
+def test_message_cpu_under_asan(ambry, tmp_path):
+    """ambrycrc_verify_message_cpu / ambrycrc_transform_message_cpu parse untrusted bytes: built with
+    ASan + UBSan (host side) and run over every message of a region, its truncations and byte
+    flips in its header and record heads (tests/native/msg_cpu_asan.cpp)."""
+    import shutil
+    import subprocess
+
+    from test_message_format import build_region
+
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    region, _, _ = build_region(n=30, seed=8, corrupt_frac=0.0, big_every=10**9)
+    rf = tmp_path / "region.bin"
+    rf.write_bytes(region)
+    exe = tmp_path / "msg_cpu_asan"
+    csrc = os.path.join(ROOT, "ambry_amd", "csrc")
+    host_o = tmp_path / "host_crc.o"
+    subprocess.run(["g++", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=all", "-fPIC",
+                    "-std=c++17", "-c", os.path.join(csrc, "host_crc.cpp"), "-o", str(host_o)],
+                   check=True, timeout=300)
+    subprocess.run([hipcc, "-O1", "-g", "-std=c++17", "--offload-arch=gfx950",
+                    "-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
+                    "-Xarch_host", "-fno-sanitize-recover=all", str(host_o),
+                    os.path.join(ROOT, "tests", "native", "msg_cpu_asan.cpp"), os.path.join(csrc, "ambrycrc.cpp"),
+                    os.path.join(csrc, "ambrycrc_multi.cpp"), os.path.join(csrc, "ambrycrc_put.cpp"),
+                    os.path.join(csrc, "ambrycrc_msg_cpu.cpp"), os.path.join(csrc, "crc32_kernels.hip"),
+                    os.path.join(csrc, "message_kernels.hip"), os.path.join(csrc, "put_kernels.hip"), "-ldl",
+                    "-o", str(exe)], check=True, timeout=900)
+    r = subprocess.run([str(exe), str(rf)], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "runs=" in r.stdout
+
+
 def test_update_iov_gather_list(ambry):
     """ambrycrc_update_iov == successive updates (PutChunk.verifyCRC over a CompositeByteBuf's
     nioBuffers, PutOperation.java:2041-2043), empty and NULL entries included; the Crc32 mirror's

@@ -1,0 +1,63 @@
+"""One message on the CPU (ambrycrc_verify_message_cpu / ambrycrc_transform_message_cpu): the
+per-message form of the device verify and ValidatingTransformer paths, byte- and bit-exact
+against oracle/message_format.py (verify_message restating deserializeBlobAll,
+MessageFormatRecord.java:257-303; transform_message restating ValidatingTransformer.java:46-104)
+on corrupted regions, the record-level cases, every header version and life version."""
+import numpy as np
+import pytest
+
+from test_message_format import MF, build_region, record_level_cases
+
+
+def test_verify_matches_oracle(ambry):
+    from ambry_amd.messages import verify_message_cpu
+
+    for seed in (1, 2, 3):
+        region, offs, expect = build_region(n=300, seed=seed, corrupt_frac=0.15)
+        for o, e in zip(offs, expect):
+            assert verify_message_cpu(region, o) == e, (seed, o)
+    for msg, want in record_level_cases():
+        region = bytes(5) + msg
+        assert verify_message_cpu(region, 5) == (want, len(region))
+
+
+def test_verify_truncated_and_out_of_range(ambry):
+    from ambry_amd.messages import verify_message_cpu
+
+    region, offs, _ = build_region(n=40, seed=9, corrupt_frac=0.0)
+    cut = region[:offs[-1] + 57]  # the last message cut inside its records
+    for o in offs:
+        assert verify_message_cpu(cut, o) == MF.verify_message(cut, o), o
+    assert verify_message_cpu(region, len(region)) == (MF.BAD_LAYOUT, 0)
+    assert verify_message_cpu(region, len(region) + 10) == (MF.BAD_LAYOUT, 0)
+    assert verify_message_cpu(region, len(region) - 1) == (MF.BAD_LAYOUT, 0)
+
+
+@pytest.mark.parametrize("version", [3, 2, 1])
+@pytest.mark.parametrize("life", [None, 5])
+def test_transform_matches_oracle(ambry, version, life):
+    from test_gpu_transform import build_region as transform_region
+
+    from ambry_amd.messages import transform_message_cpu
+
+    region, offs = transform_region(MF, 300, seed=50 + version)
+    kinds = set()
+    for o in offs:
+        exp_st, exp = MF.transform_message(region, o, life=life, version=version)
+        st, got = transform_message_cpu(region, o, header_version=version, life=life)
+        assert st == exp_st, o
+        assert got == exp, o
+        kinds.add(st)
+    assert 0 in kinds and MF.NOT_PUT in kinds and MF.BAD_RECORD in kinds
+
+
+def test_transform_no_room_and_args(ambry):
+    from ambry_amd._lib import AmbryCrcError
+    from ambry_amd.messages import MSG_NO_ROOM, transform_message_cpu
+
+    msg = MF.put_message(MF.store_key("k"), MF.blob_properties_bytes(100), b"um", bytes(100))
+    st, out = transform_message_cpu(msg, 0, out_cap=len(msg) - 1)
+    assert st == MSG_NO_ROOM and out is None
+    assert transform_message_cpu(msg, 0, out_cap=len(msg)) == (0, msg)
+    with pytest.raises(AmbryCrcError):
+        transform_message_cpu(msg, 0, header_version=4)
