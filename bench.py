@@ -308,6 +308,8 @@ def run_c1(args, result_fd):
                         PutMessageFormatInputStream.java:76-124); must equal the fixture's bytes
       product (verify)  ambrycrc_update per record, the blob record's CRC derived from the blob's
                         by ambrycrc_put_crcs (PutMessageFormatInputStream.java:116-120)
+      product (read)    ambrycrc_verify_message_cpu: deserializeBlobAll's checks on the whole
+                        message in one call (header, record versions / sizes, every CRC)
       cpu_baseline      the oracle's Crc32.java restatement over the same four records
     All checked against the committed fixture (tests/golden/c1_message.*)."""
     import ctypes
@@ -360,6 +362,13 @@ def run_c1(args, result_fd):
         L.ambrycrc_put_crcs(None, None, pre, pre_len, bcrc, blen, 1, None, rec)
         return got + [rec[0]]
 
+    vst, vend = ctypes.c_uint32(1), ctypes.c_uint64(0)
+
+    def read():
+        L.ambrycrc_verify_message_cpu(base, len(msg), 0, ctypes.byref(vst), ctypes.byref(vend))
+
+    read()
+    ok_r = vst.value == 0 and vend.value == len(msg)
     orc = Oracle()
 
     def oracle():
@@ -368,7 +377,7 @@ def run_c1(args, result_fd):
     ok_v, ok_o = verify() == expect, oracle() == expect
     reps = 20000
     res = {}
-    for name, fn in (("write", write), ("verify", verify), ("oracle", oracle)):
+    for name, fn in (("write", write), ("verify", verify), ("read", read), ("oracle", oracle)):
         fn()
         t0 = time.perf_counter()
         for _ in range(reps):
@@ -388,11 +397,13 @@ def run_c1(args, result_fd):
         "product_verify": {"us_per_message": round(res["verify"], 3), "matches_fixture": ok_v,
                            "GiBps": round(crc_bytes / res["verify"] * 1e6 / 2**30, 2),
                            "what": "ambrycrc_update per record + ambrycrc_put_crcs for the blob record, one core"},
+        "product_read": {"us_per_message": round(res["read"], 3), "clean": ok_r,
+                         "what": "ambrycrc_verify_message_cpu: header, record versions and sizes, every CRC, one call"},
         "cpu_baseline": {"value": round(res["oracle"], 3), "unit": "us per message", "cores": 1, "kind": "port",
                          "matches_fixture": ok_o,
                          "sample": "the C1 message's four record CRCs, 20,000 repetitions; oracle/crc32_ref.c "
                                    "slice-by-8 restating Crc32.java:55-98"},
-        "note": "every leg pays ~0.3 us of Python->C call overhead per call (write: 1 call; verify: 5; oracle: 4)",
+        "note": "every leg pays ~0.3 us of Python->C call overhead per call (write: 1; verify: 5; read: 1; oracle: 4)",
     }
     os.write(result_fd, (json.dumps(result) + "\n").encode())
 
