@@ -23,6 +23,9 @@
  *   void nativeInit(int device)
  *   void nativeBatchDirect(ByteBuffer[] bufs, int[] pos, int[] len, int[] crcIn, int[] out, int device)
  *   void nativeVerifyMessages(ByteBuffer region, long[] offsets, int[] status, long[] ends, int device)
+ *   int  nativeVerifyMessage(ByteBuffer region, long offset, long[] end)
+ *   int  nativeTransformMessage(ByteBuffer region, long offset, int lifeVersion, int headerVersion,
+ *                               ByteBuffer out, long[] outLen)
  * CRC values travel as Java ints holding the uint32 bit pattern.
  */
 #include <jni.h>
@@ -238,4 +241,48 @@ JNIEXPORT jint JNICALL JNI_FN(nativeUpdateDirectAll)(JNIEnv* env, jclass cls, ji
   free(lens);
   raise(env, st);
   return result;
+}
+
+/* One message on the CPU (ambrycrc_verify_message_cpu): MessageFormatSend / BlobStoreRecovery's
+ * per-message read. Returns the status bits; end[0] = the message end (0: unparseable). */
+JNIEXPORT jint JNICALL JNI_FN(nativeVerifyMessage)(JNIEnv* env, jclass cls, jobject region, jlong offset,
+                                                   jlongArray end) {
+  (void)cls;
+  if (!region) return raise(env, AJC_ENULL), 0;
+  if (end && (*env)->GetArrayLength(env, end) < 1) return raise(env, AJC_ESHORT), 0;
+  if (offset < 0) return raise(env, AJC_EBOUNDS), 0;
+  int64_t cap;
+  const uint8_t* base = direct(env, region, &cap);
+  if (!base) return raise(env, AJC_ENOTDIRECT), 0;
+  uint32_t st = 0;
+  uint64_t e = 0;
+  if (raise(env, ambrycrc_verify_message_cpu(base, (uint64_t)cap, (uint64_t)offset, &st, &e))) return 0;
+  if (end) {
+    const jlong je = (jlong)e;
+    (*env)->SetLongArrayRegion(env, end, 0, 1, &je);
+  }
+  return (jint)st;
+}
+
+/* ValidatingTransformer.transform for one message (ambrycrc_transform_message_cpu) into the direct
+ * buffer `out` from its position 0. Returns the status bits; outLen[0] = bytes written. */
+JNIEXPORT jint JNICALL JNI_FN(nativeTransformMessage)(JNIEnv* env, jclass cls, jobject region, jlong offset,
+                                                      jint life_version, jint header_version, jobject out,
+                                                      jlongArray out_len) {
+  (void)cls;
+  if (!region || !out || !out_len) return raise(env, AJC_ENULL), 0;
+  if ((*env)->GetArrayLength(env, out_len) < 1) return raise(env, AJC_ESHORT), 0;
+  if (offset < 0) return raise(env, AJC_EBOUNDS), 0;
+  int64_t cap, ocap;
+  const uint8_t* base = direct(env, region, &cap);
+  uint8_t* dst = (uint8_t*)direct(env, out, &ocap);
+  if (!base || !dst) return raise(env, AJC_ENOTDIRECT), 0;
+  uint32_t st = 0;
+  uint64_t n = 0;
+  if (raise(env, ambrycrc_transform_message_cpu(base, (uint64_t)cap, (uint64_t)offset, life_version, header_version,
+                                                dst, (uint64_t)ocap, &n, &st)))
+    return 0;
+  const jlong jn = (jlong)n;
+  (*env)->SetLongArrayRegion(env, out_len, 0, 1, &jn);
+  return (jint)st;
 }

@@ -122,6 +122,27 @@ public final class NativeCrc32 implements Checksum {
     nativeVerifyMessages(region, offsets, status, ends, device);
   }
 
+  /**
+   * One message on the CPU (ambrycrc_verify_message_cpu): deserializeBlobAll's checks (header, record
+   * versions and sizes, every CRC) for the message at `offset` in a direct buffer. Returns the
+   * AMBRYCRC_MSG_* bits (0: intact); end[0] (if end is non-null) = the message's end offset, 0 when
+   * its layout is invalid.
+   */
+  public static int verifyMessage(ByteBuffer region, long offset, long[] end) {
+    return nativeVerifyMessage(region, offset, end);
+  }
+
+  /**
+   * ValidatingTransformer.transform for one stored message on the CPU (ambrycrc_transform_message_cpu):
+   * verify, refuse update records, re-serialize at `headerVersion` (1..3) with `lifeVersion` (< 0:
+   * the stored one) into `out` from position 0. Returns the status bits (0: transformed; MSG_NOT_PUT,
+   * MSG_BAD_RECORD, MSG_NO_ROOM or verify bits otherwise); outLen[0] = bytes written.
+   */
+  public static int transformMessage(ByteBuffer region, long offset, int lifeVersion, int headerVersion,
+      ByteBuffer out, long[] outLen) {
+    return nativeTransformMessage(region, offset, lifeVersion, headerVersion, out, outLen);
+  }
+
   /** AMBRYCRC_MSG_* status bits of verifyMessages (include/ambrycrc.h). */
   public static final int MSG_HEADER_CRC = 1;
   public static final int MSG_ENCKEY_CRC = 1 << 1;
@@ -131,7 +152,9 @@ public final class NativeCrc32 implements Checksum {
   public static final int MSG_BLOB_CRC = 1 << 5;
   public static final int MSG_BAD_VERSION = 1 << 8;
   public static final int MSG_BAD_LAYOUT = 1 << 9;
+  public static final int MSG_NOT_PUT = 1 << 10;
   public static final int MSG_BAD_RECORD = 1 << 11;
+  public static final int MSG_NO_ROOM = 1 << 12;
 
   private static native void nativeInit(int device);
 
@@ -150,4 +173,9 @@ public final class NativeCrc32 implements Checksum {
 
   private static native void nativeVerifyMessages(ByteBuffer region, long[] offsets, int[] status, long[] ends,
       int device);
+
+  private static native int nativeVerifyMessage(ByteBuffer region, long offset, long[] end);
+
+  private static native int nativeTransformMessage(ByteBuffer region, long offset, int lifeVersion,
+      int headerVersion, ByteBuffer out, long[] outLen);
 }

@@ -149,6 +149,40 @@ static struct _jobject arr(enum Kind k, void* data, jsize len) {
   return o;
 }
 
+JNIEXPORT jint JNICALL FN(nativeVerifyMessage)(JNIEnv*, jclass, jobject, jlong, jlongArray);
+JNIEXPORT jint JNICALL FN(nativeTransformMessage)(JNIEnv*, jclass, jobject, jlong, jint, jint, jobject, jlongArray);
+
+/* argv[1] == "msg", argv[2] = a file holding one PUT message: the per-message CPU entries. */
+static int msg_cases(const char* path) {
+  FILE* f = fopen(path, "rb");
+  if (!f) return 2;
+  static uint8_t msg[1 << 20], out[1 << 20];
+  const size_t n = fread(msg, 1, sizeof msg, f);
+  fclose(f);
+  struct _jobject reg = arr(K_BUFFER, msg, (jsize)n), heap = arr(K_BUFFER, NULL, (jsize)n);
+  struct _jobject dst = arr(K_BUFFER, out, (jsize)sizeof out), small = arr(K_BUFFER, out, 16);
+  jlong end[1] = {-1}, olen[1] = {-1};
+  struct _jobject jend = arr(K_LONGS, end, 1), jolen = arr(K_LONGS, olen, 1), jnone = arr(K_LONGS, end, 0);
+  report("msg_verify", FN(nativeVerifyMessage)(&g_env, NULL, &reg, 0, &jend));
+  report("msg_verify_end", (jint)end[0]);
+  report("msg_verify_heap", FN(nativeVerifyMessage)(&g_env, NULL, &heap, 0, &jend));
+  report("msg_verify_null", FN(nativeVerifyMessage)(&g_env, NULL, NULL, 0, &jend));
+  report("msg_verify_short", FN(nativeVerifyMessage)(&g_env, NULL, &reg, 0, &jnone));
+  report("msg_verify_past", FN(nativeVerifyMessage)(&g_env, NULL, &reg, (jlong)n + 5, NULL));
+  report("msg_transform_v3", FN(nativeTransformMessage)(&g_env, NULL, &reg, 0, -1, 3, &dst, &jolen));
+  report("msg_transform_v3_len", (jint)olen[0]);
+  report("msg_transform_v3_same", (jint)(olen[0] == (jlong)n && memcmp(out, msg, n) == 0));
+  report("msg_transform_v1", FN(nativeTransformMessage)(&g_env, NULL, &reg, 0, -1, 1, &dst, &jolen));
+  report("msg_transform_v1_len", (jint)olen[0]);
+  report("msg_transform_small", FN(nativeTransformMessage)(&g_env, NULL, &reg, 0, -1, 3, &small, &jolen));
+  report("msg_transform_small_len", (jint)olen[0]);
+  report("msg_transform_badver", FN(nativeTransformMessage)(&g_env, NULL, &reg, 0, -1, 7, &dst, &jolen));
+  msg[n / 2] ^= 0x20; /* inside the blob content */
+  report("msg_verify_corrupt", FN(nativeVerifyMessage)(&g_env, NULL, &reg, 0, &jend));
+  report("msg_transform_corrupt", FN(nativeTransformMessage)(&g_env, NULL, &reg, 0, -1, 3, &dst, &jolen));
+  return 0;
+}
+
 /* With a GPU (argv[1] == "gpu"): the device entries on valid arguments. */
 static int gpu_cases(void) {
   FN(nativeInit)(&g_env, NULL, 0);
@@ -177,6 +211,7 @@ static int gpu_cases(void) {
 
 int main(int argc, char** argv) {
   if (argc > 1 && strcmp(argv[1], "gpu") == 0) return gpu_cases();
+  if (argc > 2 && strcmp(argv[1], "msg") == 0) return msg_cases(argv[2]);
   static uint8_t digits[] = "123456789";
   struct _jobject b9 = arr(K_BYTES, digits, 9);
   report("array_full", FN(nativeUpdateArray)(&g_env, NULL, 0, &b9, 0, 9));

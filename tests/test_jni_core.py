@@ -171,3 +171,28 @@ def test_jni_shim_device_entries(core, tmp_path):
     assert got["gpu_batch_2"] == (zlib.crc32(b"89yy"), "-")
     assert got["gpu_verify_0"] == (1 << 8, "-") and got["gpu_verify_1"] == (1 << 8, "-")
     assert got["gpu_verify_end"] == (0, "-")
+
+
+def test_jni_shim_message_entries(core, tmp_path):
+    """nativeVerifyMessage / nativeTransformMessage (ambrycrc_verify_message_cpu /
+    ambrycrc_transform_message_cpu) in the fake JVM on the C1 message: clean verify with its end,
+    V3 -> V3 reproducing it, V1 re-serialized 6 B shorter (34-B header), NO_ROOM into 16 B, a
+    blob flip flagged, and the argument errors thrown."""
+    from c1_message import c1_message_bytes
+
+    msg = c1_message_bytes()
+    path = tmp_path / "msg.bin"
+    path.write_bytes(msg)
+    got = _run_harness(tmp_path, "msg", str(path))
+    NPE = "java/lang/NullPointerException"
+    IAE, ISE = "java/lang/IllegalArgumentException", "java/lang/IllegalStateException"
+    assert got["msg_verify"] == (0, "-") and got["msg_verify_end"] == (len(msg), "-")
+    assert got["msg_verify_heap"] == (0, IAE) and got["msg_verify_null"] == (0, NPE)
+    assert got["msg_verify_short"] == (0, IAE)
+    assert got["msg_verify_past"] == (1 << 9, "-")  # BAD_LAYOUT is data, not an error
+    assert got["msg_transform_v3"] == (0, "-") and got["msg_transform_v3_len"] == (len(msg), "-")
+    assert got["msg_transform_v3_same"] == (1, "-")
+    assert got["msg_transform_v1"] == (0, "-") and got["msg_transform_v1_len"] == (len(msg) - 6, "-")
+    assert got["msg_transform_small"] == (1 << 12, "-") and got["msg_transform_small_len"] == (0, "-")
+    assert got["msg_transform_badver"][1] in (IAE, ISE)
+    assert got["msg_verify_corrupt"] == (1 << 5, "-") and got["msg_transform_corrupt"] == (1 << 5, "-")
