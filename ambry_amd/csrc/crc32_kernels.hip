@@ -174,12 +174,17 @@ __device__ __forceinline__ u32x4 ld16(const u32x4* p) {
 // 16-B stores at any destination alignment (gfx9 global memory runs in unaligned mode; the
 // memcpy becomes one global_store_dwordx4); a piece that starts before the chunk stores only
 // its bytes from `lo` on.
-__device__ __forceinline__ void st16u(uint8_t* d, const u32x4& v) { __builtin_memcpy(d, &v, 16); }
+// The destination pointers are built from integers (SweepArgs::copy_off), which leaves them in
+// the generic address space: a store through one is a flat_store, which counts on lgkmcnt as well
+// as vmcnt, so every LDS wait of the CRC chain would also wait for the outstanding stores. The
+// casts keep them global_store.
+typedef __attribute__((address_space(1))) u32x4 gu32x4;
+typedef __attribute__((address_space(1))) uint8_t gu8;
+__device__ __forceinline__ void st8g(uint8_t* d, uint32_t v) { *(gu8*)d = (uint8_t)v; }
+__device__ __forceinline__ void st16u(uint8_t* d, const u32x4& v) { *(gu32x4*)d = v; }
 // Wave-mode bodies (large chunks) stream their stores nontemporal: 3-5 % faster there, 18 %
 // slower in the group phase's short records (r02x A/B), which keep the plain store.
-__device__ __forceinline__ void st16u_nt(uint8_t* d, const u32x4& v) {
-  __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(d));
-}
+__device__ __forceinline__ void st16u_nt(uint8_t* d, const u32x4& v) { __builtin_nontemporal_store(v, (gu32x4*)d); }
 
 __device__ __forceinline__ void copy_piece(uint8_t* dbase, int64_t p, const u32x4& v, int64_t lo) {
   if (p + 16 <= lo) return;
@@ -189,7 +194,7 @@ __device__ __forceinline__ void copy_piece(uint8_t* dbase, int64_t p, const u32x
   }
 #pragma unroll
   for (int b = 0; b < 16; ++b)
-    if (p + b >= lo) dbase[p + b] = (uint8_t)(v[b >> 2] >> (8 * (b & 3)));
+    if (p + b >= lo) st8g(dbase + p + b, v[b >> 2] >> (8 * (b & 3)));
 }
 
 template <int LVL>
@@ -623,7 +628,7 @@ __device__ __forceinline__ uint32_t group_crc_g(const uint8_t* __restrict__ base
   if constexpr (COPY) {
 #pragma unroll
     for (uint32_t i = 0; i < BPL; ++i)
-      if (k0 + i < t) dbase[ce - 1 - (k0 + i)] = (uint8_t)tb[i];
+      if (k0 + i < t) st8g(dbase + (ce - 1 - (k0 + i)), tb[i]);
   }
   constexpr int P = NB < 8 ? NB : 8;
   GroupRingT<0, P, NT, (int)BB, COPY> ring;
@@ -892,7 +897,7 @@ __device__ __forceinline__ void group_class_t4s(const SweepArgs& a, uint64_t lo,
       const uint32_t k0 = BPL * (G - 1 - (lane & (G - 1)));
 #pragma unroll
       for (uint32_t q = 0; q < BPL; ++q)
-        if (k0 + q < r.t) reinterpret_cast<uint8_t*>(r.dsh)[r.ce - 1 - (k0 + q)] = (uint8_t)tb[q];
+        if (k0 + q < r.t) st8g(reinterpret_cast<uint8_t*>(r.dsh) + (r.ce - 1 - (k0 + q)), tb[q]);
     }
     if ((lane & (G - 1)) == 0 && r.act) {
       a.out[r.ci] = crc;
@@ -1086,7 +1091,7 @@ __global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
       const uint64_t t0 = sa > cb ? sa : cb;
       r ^= __builtin_amdgcn_readlane(tail_crc(a.base + t0, (uint32_t)(ce - t0), lane), 0);
       if constexpr (COPY) {
-        if (lane < ce - t0) reinterpret_cast<uint8_t*>(dsh)[t0 + lane] = a.base[t0 + lane];
+        if (lane < ce - t0) st8g(reinterpret_cast<uint8_t*>(dsh) + t0 + lane, a.base[t0 + lane]);
       }
     }
     if (r0 == 0) {  // initial register ~crc_in advanced over the chunk, plus xor-out
