@@ -881,9 +881,17 @@ namespace detail {
 // at least ambrycrc_messages_workspace_bytes(m).
 int enqueue_messages(DevCtx* c, const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off, size_t m,
                      uint32_t* d_status, uint64_t* d_msg_end, void* d_ws, hipStream_t stream) {
+  MsgStage st;
+  const int rc = enqueue_messages_parse(c, d_region, region_len, d_msg_off, m, d_status, d_msg_end, d_ws, stream, &st);
+  return rc ? rc : enqueue_messages_check(c, st, stream);
+}
+
+int enqueue_messages_parse(DevCtx* c, const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off,
+                           size_t m, uint32_t* d_status, uint64_t* d_msg_end, void* d_ws, hipStream_t stream,
+                           MsgStage* st) {
   const size_t j = (size_t)kMsgSlots * m;
   uint8_t* w = static_cast<uint8_t*>(d_ws);
-  MsgArgs a;
+  MsgArgs& a = st->a;
   a.region = d_region;
   a.region_len = region_len;
   a.msg_off = d_msg_off;
@@ -900,10 +908,19 @@ int enqueue_messages(DevCtx* c, const uint8_t* d_region, uint64_t region_len, co
   // takes whole; the parse kernel reads the rest.
   const bool inline_exp = variant_groups(c->variant);
   a.inline_max = inline_exp ? batch_small_max(c, j) : 0;
-  void* batch_ws = w + ((j * 2 * sizeof(uint64_t) + j * 2 * sizeof(uint32_t) + j + 255) & ~size_t(255));
-  if (launch_msg_parse(a, stream) != hipSuccess) return AMBRYCRC_EHIP;
-  int rc = enqueue_batch(c, d_region, a.job_off, a.job_len, nullptr, crc, j, batch_ws, stream,
-                         a.inline_max ? a.expected : nullptr);
+  st->batch_ws = w + ((j * 2 * sizeof(uint64_t) + j * 2 * sizeof(uint32_t) + j + 255) & ~size_t(255));
+  st->crc = crc;
+  st->j = j;
+  return hip_err(launch_msg_parse(a, stream));
+}
+
+int enqueue_messages_check(DevCtx* c, const MsgStage& st, hipStream_t stream, uint8_t* copy_dst,
+                           const uint64_t* copy_off) {
+  const MsgArgs& a = st.a;
+  // copy-through runs the group-phase kernel whatever c's variant, so the stored CRCs of the records
+  // it takes are read there exactly when the parse kernel left them to it (inline_max)
+  const int rc = enqueue_batch(c, a.region, a.job_off, a.job_len, nullptr, st.crc, st.j, st.batch_ws, stream,
+                               a.inline_max ? a.expected : nullptr, copy_dst, copy_off);
   if (rc) return rc;
   return hip_err(launch_msg_reduce(a, stream));
 }

@@ -108,13 +108,29 @@ int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uin
 // least ambrycrc_messages_workspace_bytes(m). d_msg_end may be null.
 int enqueue_messages(DevCtx* c, const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off, size_t m,
                      uint32_t* d_status, uint64_t* d_msg_end, void* d_ws, hipStream_t stream);
+// The same in two halves: the parse kernel (jobs and their stored CRCs in st->a), then the CRC
+// batch and the reduce -- with copy_dst / copy_off, the batch is the copy-through kernel
+// (SweepArgs::copy_dst), which the transform uses to copy the records while verifying them.
+struct MsgStage {
+  MsgArgs a;
+  uint32_t* crc;  // a.crc, writable: the batch's output
+  void* batch_ws;
+  size_t j;
+};
+int enqueue_messages_parse(DevCtx* c, const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off,
+                           size_t m, uint32_t* d_status, uint64_t* d_msg_end, void* d_ws, hipStream_t stream,
+                           MsgStage* st);
+int enqueue_messages_check(DevCtx* c, const MsgStage& st, hipStream_t stream, uint8_t* copy_dst = nullptr,
+                           const uint64_t* copy_off = nullptr);
 // The PUT serialization pipeline (layout -> copy -> plan + CRC -> seal); d_ws holds at least
 // ambrycrc_serialize_puts_workspace_bytes(m). d_in_crc (transform): the CRCs of records 1-4,
 // 4 per message (PutArgs::in_crc); the layout kernel then writes every trailer and the CRC pass
 // over the output is skipped.
+// layout_only: the layout kernel alone (the transform's speculative pass, whose fields the
+// verify already copied); gate: run the layout and copy kernels only when *gate != 0.
 int enqueue_serialize(DevCtx* c, const ::ambrycrc_put_desc* d_desc, size_t m, const uint8_t* d_fields,
                       const uint8_t* d_blobs, uint8_t* d_out, uint64_t* d_msg_len, void* d_ws, hipStream_t stream,
-                      const uint32_t* d_in_crc = nullptr);
+                      const uint32_t* d_in_crc = nullptr, bool layout_only = false, const uint32_t* gate = nullptr);
 
 // Holds c->ws_mu for the lifetime of a *_dev call that uses the default workspace (d_ws ==
 // NULL); a call with its own workspace takes no lock.

@@ -24,9 +24,11 @@ size_t put_jobs_bytes(size_t m) {
   return (j * (4 * sizeof(uint64_t) + 2 * sizeof(uint64_t) + sizeof(uint32_t)) + 255) & ~size_t(255);
 }
 
-// A transform's own workspace: descriptors, the scan's per-message output, in_crc (4 per message).
+// A transform's own workspace: descriptors, the scan's per-message output, in_crc (4 per message),
+// the speculative pass's xstatus, its fail flag and the verify jobs' copy destinations (5 per message).
 size_t transform_own_bytes(size_t m) {
-  return (m * (sizeof(ambrycrc_put_desc) + sizeof(uint32_t) + 4 * sizeof(uint32_t)) + 255) & ~size_t(255);
+  const size_t head = (m * (sizeof(ambrycrc_put_desc) + 6 * sizeof(uint32_t)) + 8 + 7) & ~size_t(7);
+  return (head + (size_t)kPutSlots * m * sizeof(uint64_t) + 255) & ~size_t(255);
 }
 
 }  // namespace
@@ -36,7 +38,7 @@ namespace detail {
 
 int enqueue_serialize(DevCtx* c, const ::ambrycrc_put_desc* d_desc, size_t m, const uint8_t* d_fields,
                       const uint8_t* d_blobs, uint8_t* d_out, uint64_t* d_msg_len, void* d_ws, hipStream_t stream,
-                      const uint32_t* d_in_crc) {
+                      const uint32_t* d_in_crc, bool layout_only, const uint32_t* gate) {
   const size_t j = (size_t)kPutSlots * m;
   uint8_t* w = static_cast<uint8_t*>(d_ws);
   PutArgs a;
@@ -57,8 +59,10 @@ int enqueue_serialize(DevCtx* c, const ::ambrycrc_put_desc* d_desc, size_t m, co
   a.in_crc = d_in_crc;
   a.img = c->d_img;
   a.copy_through = (d_fields || d_blobs) && !d_in_crc;
+  a.gate = gate;
   void* batch_ws = w + put_jobs_bytes(m);
   if (launch_put_layout(a, stream) != hipSuccess) return AMBRYCRC_EHIP;
+  if (layout_only) return AMBRYCRC_OK;
   if (a.copy_through) {
     // one pass over the fields: the copy-through sweep reads each from its source, writes it into
     // the message and CRCs it (job k*m+i = slot k of message i, as the CRC jobs)
@@ -92,6 +96,7 @@ int enqueue_serialize(DevCtx* c, const ::ambrycrc_put_desc* d_desc, size_t m, co
     ca.start = p.byte_start;
     ca.n = (uint32_t)j;
     ca.dst = d_out;
+    ca.gate = gate;
     if (launch_gather_copy(ca, c->num_cu * 8, stream) != hipSuccess) return AMBRYCRC_EHIP;
   }
   if (d_in_crc) return AMBRYCRC_OK;  // the layout kernel wrote every trailer
@@ -176,10 +181,12 @@ int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len
   WsLease lease;
   int rc = lease.acquire(c, stream, &d_ws, ws_bytes, ambrycrc_transform_workspace_bytes(m));
   if (rc) return rc;
-  // workspace: desc[m] | scan scratch (uint32 per message) | in_crc[4m] | plan workspace for the
-  //            m lengths | the verify pipeline's, then the serializer's (one after the other)
+  // workspace: desc[m] | scan scratch (uint32 per message) | in_crc[4m] | xstatus[m] | fail |
+  //            copy_off[5m] | plan workspace for the m lengths | the verify pipeline's, then the
+  //            serializer's (one after the other on the stream)
   uint8_t* w = static_cast<uint8_t*>(d_ws);
   TransformArgs t;
+  memset(&t, 0, sizeof t);
   t.region = d_region;
   t.region_len = region_len;
   t.msg_off = d_msg_off;
@@ -193,12 +200,15 @@ int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len
   t.out_cap = out_cap;
   uint32_t* scan_out = reinterpret_cast<uint32_t*>(w + m * sizeof(ambrycrc_put_desc));
   t.in_crc = scan_out + m;
+  uint32_t* xstatus = t.in_crc + 4 * m;
+  uint32_t* fail = xstatus + m;
+  uint64_t* copy_off = reinterpret_cast<uint64_t*>(w + ((m * (sizeof(ambrycrc_put_desc) + 6 * sizeof(uint32_t)) + 8 +
+                                                         7) & ~size_t(7)));
   t.img = c->d_img;
+  t.out = d_out;
+  t.fail = fail;
   uint8_t* plan_ws = w + transform_own_bytes(m);
   void* shared = plan_ws + ws_need(m);
-  rc = enqueue_messages(c, d_region, region_len, d_msg_off, m, d_status, nullptr, shared, stream);
-  if (rc) return rc;
-  if (launch_transform_desc(t, stream) != hipSuccess) return AMBRYCRC_EHIP;
   // packed output offsets: the plan kernel's exclusive scan of the output lengths
   PlanArgs p;
   p.off = d_msg_off;
@@ -214,9 +224,40 @@ int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len
   p.crc_stage = nullptr;
   p.out = scan_out;
   p.small_max = 0;
+
+  // Speculative pass (two HBM passes: the verify reads every record once and writes the ones the
+  // output keeps into place). The descriptors and the packed placement come from the parse alone,
+  // before the CRCs are known; the verify's CRC batch is the copy-through kernel. A message that
+  // then fails verification sets `fail`, and the fallback pass below rebuilds the output exactly as
+  // the three-pass form did (verify bits first, then the transform's own, then the placement).
+  if (hipMemsetAsync(fail, 0, sizeof(uint32_t), stream) != hipSuccess) return AMBRYCRC_EHIP;
+  MsgStage ms;
+  rc = enqueue_messages_parse(c, d_region, region_len, d_msg_off, m, d_status, nullptr, shared, stream, &ms);
+  if (rc) return rc;
+  t.xstatus = xstatus;
+  t.job_off = ms.a.job_off;
+  t.copy_off = copy_off;
+  if (launch_transform_desc(t, stream) != hipSuccess) return AMBRYCRC_EHIP;
   if (launch_plan(p, stream) != hipSuccess) return AMBRYCRC_EHIP;
   if (launch_transform_place(t, p.byte_start, stream) != hipSuccess) return AMBRYCRC_EHIP;
-  return enqueue_serialize(c, t.desc, m, d_region, d_region, d_out, nullptr, shared, stream, t.in_crc);
+  if (launch_transform_jobs(t, stream) != hipSuccess) return AMBRYCRC_EHIP;
+  rc = enqueue_messages_check(c, ms, stream, d_out, copy_off);
+  if (rc) return rc;
+  if (launch_transform_finish(t, stream) != hipSuccess) return AMBRYCRC_EHIP;
+  rc = enqueue_serialize(c, t.desc, m, d_region, d_region, d_out, nullptr, shared, stream, t.in_crc, true);
+  if (rc) return rc;
+  t.gate = fail;
+  t.gate_when = 0;  // no failure: the final status is the verify's bits, else the transform's own
+  if (launch_transform_merge(t, stream) != hipSuccess) return AMBRYCRC_EHIP;
+
+  // Fallback pass (only when `fail` is set; every kernel checks it): descriptors from the final
+  // verify status, packed placement, layout and a gather copy of the fields from the region.
+  t.xstatus = nullptr;
+  t.gate_when = 1;
+  if (launch_transform_desc(t, stream) != hipSuccess) return AMBRYCRC_EHIP;
+  if (launch_plan(p, stream) != hipSuccess) return AMBRYCRC_EHIP;
+  if (launch_transform_place(t, p.byte_start, stream) != hipSuccess) return AMBRYCRC_EHIP;
+  return enqueue_serialize(c, t.desc, m, d_region, d_region, d_out, nullptr, shared, stream, t.in_crc, false, fail);
 }
 
 }  // extern "C"

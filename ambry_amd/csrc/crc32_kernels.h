@@ -54,8 +54,9 @@ struct SweepArgs {
   // copy_dst + copy_off[c] + (its offset in the chunk). The PUT serializer's copy mode uses it so a
   // field is read once for both its copy and its CRC. Null for every other launch.
   uint8_t* copy_dst;
-  const uint64_t* copy_off;
+  const uint64_t* copy_off;  // kCopySkip: chunk c is read (CRC'd) but not copied
 };
+constexpr uint64_t kCopySkip = ~0ull;
 
 // Chunks of 1 B .. kGroupSmallMax go to the group phase (variant 29) in batches of at least
 // kGroupMinChunks chunks; smaller batches take the sweep (wave mode) for every chunk: with idle
@@ -142,6 +143,8 @@ struct PutArgs {
   // over the output runs. img: the table image (crc_img.h).
   const uint32_t* in_crc;
   const uint32_t* img;
+  // Run only when *gate != 0 (null: always). The transform's fallback pass.
+  const uint32_t* gate;
   // Copy-through mode (copy mode without in_crc): the copy jobs become the CRC batch itself --
   // the sweep reads each field once, writes it to the message and CRCs it; put_seal_combine_kernel
   // then extends each content CRC over its record prefix. A slot with no source buffer (fields
@@ -161,6 +164,7 @@ struct CopyArgs {
   const uint64_t* start;    // [n+1] exclusive scan of the job costs (len + kCopyJobCost)
   uint32_t n;
   uint8_t* dst;
+  const uint32_t* gate;  // run only when *gate != 0 (null: always)
 };
 
 // ValidatingTransformer (message_kernels.hip): stored messages -> put descriptors -> serialization.
@@ -182,10 +186,25 @@ struct TransformArgs {
   // linearity (crc_img.h). Null: the serializer recomputes them.
   uint32_t* in_crc;
   const uint32_t* img;
+  // Speculative pass (transform_spec_*): the output is placed and the verify pass copies the
+  // records into it before the CRCs are known. xstatus (nullable) takes the transform's own bits
+  // (NOT_PUT / BAD_RECORD / NO_ROOM) instead of status; job_off / copy_off are the verify jobs
+  // (5m, slot-major) and their copy destinations; fail is set when a placed message then fails
+  // verification, which gates the fallback pass (gate: run only when (*gate != 0) == gate_when).
+  uint32_t* xstatus;
+  const uint64_t* job_off;
+  uint64_t* copy_off;
+  uint32_t* fail;
+  uint8_t* out;
+  const uint32_t* gate;
+  int gate_when;
 };
 
 hipError_t launch_transform_desc(const TransformArgs& a, hipStream_t s);
 hipError_t launch_transform_place(const TransformArgs& a, const uint64_t* start, hipStream_t s);
+hipError_t launch_transform_jobs(const TransformArgs& a, hipStream_t s);
+hipError_t launch_transform_finish(const TransformArgs& a, hipStream_t s);
+hipError_t launch_transform_merge(const TransformArgs& a, hipStream_t s);
 
 hipError_t launch_put_layout(const PutArgs& a, hipStream_t s);
 hipError_t launch_put_seal(const PutArgs& a, hipStream_t s);

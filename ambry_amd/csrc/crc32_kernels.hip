@@ -187,7 +187,7 @@ __device__ __forceinline__ void st16u(uint8_t* d, const u32x4& v) { *(gu32x4*)d 
 __device__ __forceinline__ void st16u_nt(uint8_t* d, const u32x4& v) { __builtin_nontemporal_store(v, (gu32x4*)d); }
 
 __device__ __forceinline__ void copy_piece(uint8_t* dbase, int64_t p, const u32x4& v, int64_t lo) {
-  if (p + 16 <= lo) return;
+  if (!dbase || p + 16 <= lo) return;  // null: a chunk read but not copied (kCopySkip)
   if (p >= lo) {
     st16u(dbase + p, v);
     return;
@@ -432,8 +432,11 @@ __device__ __forceinline__ uint32_t body_crc_t4(const uint8_t* __restrict__ base
         }
         if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
         if constexpr (COPY) {
+          if (dbase) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) st16u_nt(dbase + v0 + (int64_t)((b + u) * SB) + 1024 * i + 16 * lane, cur[i]);
+            for (int i = 0; i < 4; ++i)
+              st16u_nt(dbase + v0 + (int64_t)((b + u) * SB) + 1024 * i + 16 * lane, cur[i]);
+          }
         }
         quad_transpose_asm(cur);
         s = run_crc<4>(cur, k, nib_mul(s, kFold));
@@ -442,8 +445,11 @@ __device__ __forceinline__ uint32_t body_crc_t4(const uint8_t* __restrict__ base
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
       if constexpr (COPY) {
+        if (dbase) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) st16u_nt(dbase + v0 + (int64_t)((b + u) * SB) + 1024 * i + 16 * lane, buf[u][i]);
+          for (int i = 0; i < 4; ++i)
+            st16u_nt(dbase + v0 + (int64_t)((b + u) * SB) + 1024 * i + 16 * lane, buf[u][i]);
+        }
       }
       quad_transpose_asm(buf[u]);
       s = run_crc<4>(buf[u], k, nib_mul(s, kFold));
@@ -455,8 +461,10 @@ __device__ __forceinline__ uint32_t body_crc_t4(const uint8_t* __restrict__ base
 #pragma unroll
     for (int i = 0; i < 4; ++i) cur[i] = ld16<NT>(q + b * 256 + i * 64);
     if constexpr (COPY) {
+      if (dbase) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) st16u_nt(dbase + v0 + (int64_t)(b * SB) + 1024 * i + 16 * lane, cur[i]);
+        for (int i = 0; i < 4; ++i) st16u_nt(dbase + v0 + (int64_t)(b * SB) + 1024 * i + 16 * lane, cur[i]);
+      }
     }
     quad_transpose_asm(cur);
     s = run_crc<4>(cur, k, nib_mul(s, kFold));
@@ -628,7 +636,7 @@ __device__ __forceinline__ uint32_t group_crc_g(const uint8_t* __restrict__ base
   if constexpr (COPY) {
 #pragma unroll
     for (uint32_t i = 0; i < BPL; ++i)
-      if (k0 + i < t) st8g(dbase + (ce - 1 - (k0 + i)), tb[i]);
+      if (dbase && k0 + i < t) st8g(dbase + (ce - 1 - (k0 + i)), tb[i]);
   }
   constexpr int P = NB < 8 ? NB : 8;
   GroupRingT<0, P, NT, (int)BB, COPY> ring;
@@ -843,7 +851,10 @@ __device__ __forceinline__ void group_class_t4s(const SweepArgs& a, uint64_t lo,
   const uint32_t ci0 = idx_at(i0);
   uint32_t ci_n = idx_at(i0 + S);
   T4Round r = t4_round<G>(ci0, a.len[ci0], a.off[ci0], a.crc_in ? a.crc_in[ci0] : 0u, i0 + gi < i1, lane);
-  if constexpr (COPY) r.dsh = (uint64_t)(uintptr_t)a.copy_dst + a.copy_off[ci0] - r.cs;
+  if constexpr (COPY) {
+    const uint64_t co = a.copy_off[ci0];
+    r.dsh = co == kCopySkip ? 0 : (uint64_t)(uintptr_t)a.copy_dst + co - r.cs;
+  }
   uint32_t tb[BPL];
   uint64_t stored = t4_aux<G>(a, dummy, r, lane, tb);
   uint64_t len_n = a.len[ci_n], off_n = a.off[ci_n];
@@ -863,7 +874,7 @@ __device__ __forceinline__ void group_class_t4s(const SweepArgs& a, uint64_t lo,
     const bool last = sb + 1 >= r.nbw;  // wave-uniform
     if (last) {  // descriptors of round r+1 (loaded a round ago); start loading r+2's and r+3's entry
       rn = t4_round<G>(ci_n, len_n, off_n, cin_n, i + S + gi < i1, lane);
-      if constexpr (COPY) rn.dsh = (uint64_t)(uintptr_t)a.copy_dst + dst_n - rn.cs;
+      if constexpr (COPY) rn.dsh = dst_n == kCopySkip ? 0 : (uint64_t)(uintptr_t)a.copy_dst + dst_n - rn.cs;
       stored_n = t4_aux<G>(a, dummy, rn, lane, tbn);
       ci_n = ci_nn;
       len_n = a.len[ci_n];
@@ -897,7 +908,7 @@ __device__ __forceinline__ void group_class_t4s(const SweepArgs& a, uint64_t lo,
       const uint32_t k0 = BPL * (G - 1 - (lane & (G - 1)));
 #pragma unroll
       for (uint32_t q = 0; q < BPL; ++q)
-        if (k0 + q < r.t) st8g(reinterpret_cast<uint8_t*>(r.dsh) + (r.ce - 1 - (k0 + q)), tb[q]);
+        if (r.dsh && k0 + q < r.t) st8g(reinterpret_cast<uint8_t*>(r.dsh) + (r.ce - 1 - (k0 + q)), tb[q]);
     }
     if ((lane & (G - 1)) == 0 && r.act) {
       a.out[r.ci] = crc;
@@ -955,7 +966,10 @@ __device__ __forceinline__ void group_class(const SweepArgs& a, uint64_t lo, uin
       stored = __builtin_bswap64(stored);
     }
     uint8_t* dbase = nullptr;
-    if constexpr (COPY) dbase = a.copy_dst + (a.copy_off[ci] - off);  // dst of source offset p: dbase + p
+    if constexpr (COPY) {  // dst of source offset p: dbase + p
+      const uint64_t co = a.copy_off[ci];
+      dbase = act && co != kCopySkip ? a.copy_dst + (co - off) : nullptr;
+    }
     const uint32_t crc = group_crc_g<G, NB, NT, COPY>(a.base, off, len, cin, nbw, lane, k, dbase);
     if (leader) {
       a.out[ci] = crc;
@@ -1091,7 +1105,7 @@ __global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
       const uint64_t t0 = sa > cb ? sa : cb;
       r ^= __builtin_amdgcn_readlane(tail_crc(a.base + t0, (uint32_t)(ce - t0), lane), 0);
       if constexpr (COPY) {
-        if (lane < ce - t0) st8g(reinterpret_cast<uint8_t*>(dsh) + t0 + lane, a.base[t0 + lane]);
+        if (dsh && lane < ce - t0) st8g(reinterpret_cast<uint8_t*>(dsh) + t0 + lane, a.base[t0 + lane]);
       }
     }
     if (r0 == 0) {  // initial register ~crc_in advanced over the chunk, plus xor-out
@@ -1131,7 +1145,10 @@ __global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
         w_len = a.len[c + lane];
         w_off = a.off[c + lane];
         w_cin = a.crc_in ? a.crc_in[c + lane] : 0u;
-        if constexpr (COPY) w_dst = (uint64_t)(uintptr_t)a.copy_dst + a.copy_off[c + lane] - w_off;
+        if constexpr (COPY) {
+          const uint64_t co = a.copy_off[c + lane];
+          w_dst = co == kCopySkip ? 0 : (uint64_t)(uintptr_t)a.copy_dst + co - w_off;
+        }
       }
       uint64_t bsc = readlane64(w_bs, 0);
       bool work = false;

@@ -324,10 +324,15 @@ __global__ __launch_bounds__(256) void trailer_verify_kernel(TrailerArgs a) {
 // deserializeBlob read them (MessageFormatRecord.java:1568-1833) and describes the message
 // PutMessageFormatInputStream would write from them (the fields stay in the region: the
 // serializer copies them from there).
+__device__ __forceinline__ bool gated_off(const uint32_t* gate, int when) {
+  return gate && ((*gate != 0) != (when != 0));
+}
+
 __global__ __launch_bounds__(256) void transform_desc_kernel(TransformArgs a) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.m) return;
-  uint32_t st = a.status[i];
+  if (i >= a.m || gated_off(a.gate, a.gate_when)) return;
+  const uint32_t st0 = a.status[i];
+  uint32_t st = st0;
   ambrycrc_put_desc d;
   __builtin_memset(&d, 0, sizeof(d));  // header_version 0: nothing to write
   uint64_t out_len = 0;
@@ -434,13 +439,14 @@ __global__ __launch_bounds__(256) void transform_desc_kernel(TransformArgs a) {
   }
   a.desc[i] = d;
   a.out_len[i] = out_len;
-  a.status[i] = st;
+  if (a.xstatus) a.xstatus[i] = st & ~st0;  // speculative: the transform's own bits, kept apart
+  else a.status[i] = st;
 }
 
 // Packed placement: message i goes to start[i] (exclusive scan of out_len), if it fits.
 __global__ __launch_bounds__(256) void transform_place_kernel(TransformArgs a, const uint64_t* __restrict__ start) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.m) return;
+  if (i >= a.m || gated_off(a.gate, a.gate_when)) return;
   const uint64_t len = a.out_len[i];
   uint64_t at = ~0ull;
   if (len) {
@@ -450,10 +456,75 @@ __global__ __launch_bounds__(256) void transform_place_kernel(TransformArgs a, c
     } else {
       a.desc[i].header_version = 0;
       a.out_len[i] = 0;
-      a.status[i] |= AMBRYCRC_MSG_NO_ROOM;
+      if (a.xstatus) a.xstatus[i] |= AMBRYCRC_MSG_NO_ROOM;
+      else a.status[i] |= AMBRYCRC_MSG_NO_ROOM;
     }
   }
   if (a.out_off) a.out_off[i] = at;
+}
+
+// Speculative pass: where the verify pass's copy-through puts each verify job (slot k of message
+// i at k*m + i: encryption key, properties, update, user metadata, blob record) in the output.
+// Records the output keeps byte for byte go to their output record start; the blob record goes
+// so that its content lands at the output's content offset (a V1/V2 head, 10/12 B, lands inside
+// the V3 head put_layout_kernel writes afterwards); the rest is read but not copied.
+__global__ __launch_bounds__(256) void transform_jobs_kernel(TransformArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.m) return;
+  const ambrycrc_put_desc d = a.desc[i];
+  uint64_t co[kMsgSlots] = {kCopySkip, kCopySkip, kCopySkip, kCopySkip, kCopySkip};
+  PutLayout L;
+  if (d.header_version != 0 && put_layout(d, L)) {
+    if (L.enc_rec) co[0] = d.out_off + (uint64_t)L.enc_rel;
+    co[1] = d.out_off + (uint64_t)L.bp_rel;
+    co[3] = d.out_off + (uint64_t)L.um_rel;
+    const uint64_t in_head = d.blob_src - a.job_off[4 * a.m + i];  // both region offsets
+    co[4] = d.out_off + (uint64_t)L.blob_rel + 13 - in_head;
+  }
+#pragma unroll
+  for (int k = 0; k < kMsgSlots; ++k) a.copy_off[(uint64_t)k * a.m + i] = co[k];
+}
+
+// Speculative pass, after the verify: a placed message that failed verification sets `fail`
+// (the fallback pass then rebuilds the output); a clean one gets its store key, the one field
+// no verify job covers.
+__global__ __launch_bounds__(256) void transform_finish_kernel(TransformArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.m) return;
+  const ambrycrc_put_desc d = a.desc[i];
+  if (d.header_version == 0) return;
+  if (a.status[i] != 0) {
+    atomicOr(a.fail, 1u);
+    return;
+  }
+  const uint8_t* src = a.region + d.key_src;
+  uint8_t* dst = a.out + d.out_off + (d.header_version == 1 ? 34u : d.header_version == 2 ? 38u : 40u);
+  for (uint32_t b = 0; b < d.key_len; ++b) dst[b] = src[b];
+}
+
+// No fallback: the final status is the verify's bits, or else the transform's own.
+__global__ __launch_bounds__(256) void transform_merge_kernel(TransformArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.m || gated_off(a.gate, a.gate_when)) return;
+  if (a.status[i] == 0) a.status[i] = a.xstatus[i];
+}
+
+hipError_t launch_transform_jobs(const TransformArgs& a, hipStream_t s) {
+  if (a.m == 0) return hipSuccess;
+  hipLaunchKernelGGL(transform_jobs_kernel, dim3((uint32_t)((a.m + 255) / 256)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_transform_finish(const TransformArgs& a, hipStream_t s) {
+  if (a.m == 0) return hipSuccess;
+  hipLaunchKernelGGL(transform_finish_kernel, dim3((uint32_t)((a.m + 255) / 256)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_transform_merge(const TransformArgs& a, hipStream_t s) {
+  if (a.m == 0) return hipSuccess;
+  hipLaunchKernelGGL(transform_merge_kernel, dim3((uint32_t)((a.m + 255) / 256)), dim3(256), 0, s, a);
+  return hipGetLastError();
 }
 
 hipError_t launch_transform_desc(const TransformArgs& a, hipStream_t s) {

@@ -24,7 +24,7 @@ typedef uint32_t u32x4p __attribute__((ext_vector_type(4)));
 
 __global__ __launch_bounds__(256) void put_layout_kernel(PutArgs a) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.m) return;
+  if (i >= a.m || (a.gate && *a.gate == 0)) return;
   const ambrycrc_put_desc d = a.desc[i];
   PutLayout L;
   const uint64_t m = a.m;
@@ -190,6 +190,7 @@ __device__ __forceinline__ void copy_range(uint8_t* __restrict__ dst, const uint
 // exclusive scan of len + kCopyJobCost, from the plan kernel); job j's bytes are the first len[j]
 // units of its cost range, so every byte is copied by exactly one wave. Descriptors 64 at a time.
 __global__ __launch_bounds__(256) void gather_copy_kernel(CopyArgs a) {
+  if (a.gate && *a.gate == 0) return;  // uniform
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
   const uint32_t wave = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * gridDim.x + blockIdx.x);

@@ -244,7 +244,9 @@ int ambrycrc_serialize_puts_dev(const ambrycrc_put_desc* d_desc, size_t m, const
  * stored header's, 0 for V1/V2) -- all CRCs recomputed -- packed in message order into
  * [d_out, d_out + out_cap). Outputs (device arrays of m): d_status (AMBRYCRC_MSG_* bits, 0 =
  * transformed), d_out_len (0 when not transformed), d_out_off (nullable; the message's offset in
- * d_out). Asynchronous on `stream`; d_ws >= ambrycrc_transform_workspace_bytes(m) or NULL. The
+ * d_out). Bytes of d_out outside the returned spans are unspecified (a clean batch is copied while
+ * it is verified; a batch with a failing message is then rebuilt). d_out must not overlap the
+ * region. Asynchronous on `stream`; d_ws >= ambrycrc_transform_workspace_bytes(m) or NULL. The
  * store-key comparison with the index entry stays with the caller (it owns the StoreKey type). */
 size_t ambrycrc_transform_workspace_bytes(size_t m);
 int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off, size_t m,

@@ -93,3 +93,20 @@ def test_serialize_batch_mixed(gpu, mf, place):
     """One source buffer given, the other slots already in place: the copy-through sweep copies
     the given fields and re-reads the in-place ones where they lie."""
     _run(gpu, mf, random_messages(mf, 300, seed=13), 1, 5, 2, in_place=True, place=place)
+
+
+def test_serialize_large_blobs_copy_through(gpu, mf):
+    """Blobs of 4-17 MiB at ragged lengths: the copy-through sweep splits each over several waves'
+    byte shares (segments that start mid-blob, nontemporal body stores, the trailing bytes), so
+    every segment boundary's head piece and tail must land exactly."""
+    from ambry_amd.messages import PutMessage
+
+    from datagen import stream_bytes
+
+    sizes = [4 << 20, (4 << 20) + 13, (17 << 20) + 5, 3, (1 << 20) + 4109, 65536 + 1, 9 << 20]
+    msgs = []
+    for i, blen in enumerate(sizes * 2):
+        msgs.append(PutMessage(key=mf.store_key("big-%d" % i), props=mf.blob_properties_bytes(blen),
+                               usermeta=stream_bytes(i, 3 << 20, 1000 + i).tobytes(),
+                               blob=stream_bytes(i, 0, blen).tobytes(), header_version=3, life_version=i % 3))
+    _run(gpu, mf, msgs, 1, 7, 5)

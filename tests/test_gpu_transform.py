@@ -24,7 +24,7 @@ def _blob_v1_message(mf, key, props, um, content, version):
                      bp + len(pr) + len(ur), 0) + key + pr + ur + bl
 
 
-def build_region(mf, n, seed):
+def build_region(mf, n, seed, corrupt=True):
     rng = np.random.default_rng(seed)
     msgs = []
     for i in range(n):
@@ -46,7 +46,7 @@ def build_region(mf, n, seed):
                                else 0, blob_version=int(rng.choice([2, 3])), compressed=bool(rng.random() < 0.3),
                                blob_type=bt)
         m = bytearray(m)
-        if rng.random() < 0.07:  # corrupt a byte somewhere
+        if rng.random() < 0.07 and corrupt:  # corrupt a byte somewhere
             m[int(rng.integers(0, len(m)))] ^= 0x40
         msgs.append(bytes(m))
     region, offs = bytearray(), []
@@ -131,3 +131,42 @@ def test_transform_large_batch_group_phase(gpu, mf):
     status2, _ = gpu.verify_messages(out, torch.from_numpy(oo[good]).cuda())
     torch.cuda.synchronize()
     assert int(status2.abs().sum().item()) == 0
+
+
+@pytest.mark.parametrize("version", [3, 1])
+def test_transform_speculative_pass(gpu, mf, version):
+    """No message fails its CRCs (update records and bad blob types still do not transform): the
+    two-pass speculative path alone produces the output -- the verify's copy-through places every
+    kept record, the blob V1/V2 heads are rewritten as V3, the keys are copied -- packed and
+    byte-exact against the oracle; then one flipped byte sends the same batch through the
+    fallback pass, with the same result for every other message."""
+    import torch
+
+    from ambry_amd.messages import transform_dev
+
+    region, offs = build_region(mf, 400, seed=90 + version, corrupt=False)
+    life = np.random.default_rng(7).integers(0, 9, size=len(offs)).astype(np.int16)
+
+    def run(reg):
+        dev = torch.frombuffer(bytearray(reg), dtype=torch.uint8).cuda()
+        out, oo, ol, st = transform_dev(dev, torch.tensor(offs, dtype=torch.int64, device="cuda"),
+                                        header_version=version, life_version=torch.from_numpy(life).cuda())
+        torch.cuda.synchronize()
+        return out.cpu().numpy().tobytes(), oo.cpu().numpy(), ol.cpu().numpy(), st.cpu().numpy().view(np.uint32)
+
+    for reg in (region, None):
+        if reg is None:  # one stored-CRC failure: the fallback pass
+            reg = bytearray(region)
+            reg[offs[len(offs) // 2] + 60] ^= 0x01
+            reg = bytes(reg)
+        out, oo, ol, st = run(reg)
+        pos = 0
+        for i, o in enumerate(offs):
+            exp_st, exp = mf.transform_message(reg, o, life=int(life[i]), version=version)
+            assert int(st[i]) == exp_st, i
+            if exp is None:
+                assert ol[i] == 0 and oo[i] == -1
+                continue
+            assert oo[i] == pos and ol[i] == len(exp), i
+            assert out[pos:pos + len(exp)] == exp, i
+            pos += len(exp)

@@ -100,18 +100,16 @@ def run(m, blob_bytes, reps, in_place, um_len=1000):
 
 def run_transform(m, blob_bytes, reps):
     """ValidatingTransformer (ambrycrc_transform_messages_dev) over a region of m stored V3 PUTs (made by
-    the serializer), re-serialized at V3: verify (one read) + deserialize + copy (a read and a write);
-    the output CRCs come from the verified input trailers, so 3 passes over the bytes."""
+    the serializer), re-serialized at V3. Clean messages take the speculative pass: the verify reads
+    each message once and its copy-through writes the output once, the CRCs coming from the
+    verified input trailers: 2 passes over the bytes."""
     import numpy as np
     import torch
 
     from ambry_amd import device as D
     from ambry_amd.messages import PUT_DESC_DTYPE, PutMessage, layout, serialize_dev, transform_dev
 
-    # blob content at message offset 40 + 24 + 104 + (um_len + 14) + 13: 1195 = 11 mod 16 for the
-    # default 1000-B user metadata (the copy's stores then sit 11 B off the loads); --um-len 1005
-    # aligns them
-    key_len, props_len = 24, 94
+    key_len, props_len, um_len = 24, 94, 1000
     L, _ = layout(PutMessage(key=bytes(key_len), props=bytes(props_len), usermeta=bytes(um_len),
                              blob=bytes(blob_bytes)))
     descs = np.zeros(m, dtype=PUT_DESC_DTYPE)
@@ -146,7 +144,7 @@ def run_transform(m, blob_bytes, reps):
     nbytes = m * L
     return {"case": f"transform {m} x PUT({blob_bytes} B blob) V3 -> V3", "messages": m, "message_bytes": nbytes,
             "ms_median": round(ms, 4), "GiBps_messages": round(nbytes / (ms / 1e3) / 2**30, 1),
-            "messages_per_s": round(m / (ms / 1e3)), "GBps_hbm_min": round(3 * nbytes / (ms / 1e3) / 1e9, 1),
+            "messages_per_s": round(m / (ms / 1e3)), "GBps_hbm_min": round(2 * nbytes / (ms / 1e3) / 1e9, 1),
             "parity": "every message verifies and the V3 -> V3 output equals the input region byte for byte"}
 
 
