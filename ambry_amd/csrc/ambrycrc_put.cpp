@@ -17,11 +17,11 @@ using namespace ambrycrc::detail;
 namespace {
 
 // Workspace of a device batch of m messages: copy jobs (src, dst, len, cost) and CRC jobs (off, len,
-// crc) of 5 per message, then one batch workspace shared by the copy plan and the CRC batch
+// crc, crc_in) of 5 per message, then one batch workspace shared by the copy plan and the CRC batch
 // (both run on the same stream, one after the other).
 size_t put_jobs_bytes(size_t m) {
   const size_t j = (size_t)kPutSlots * m;
-  return (j * (4 * sizeof(uint64_t) + 2 * sizeof(uint64_t) + sizeof(uint32_t)) + 255) & ~size_t(255);
+  return (j * (4 * sizeof(uint64_t) + 2 * sizeof(uint64_t) + 2 * sizeof(uint32_t)) + 255) & ~size_t(255);
 }
 
 // A transform's own workspace: descriptors, the scan's per-message output, in_crc (4 per message),
@@ -55,6 +55,7 @@ int enqueue_serialize(DevCtx* c, const ::ambrycrc_put_desc* d_desc, size_t m, co
   a.crc_len = a.crc_off + j;
   uint32_t* crc = reinterpret_cast<uint32_t*>(a.crc_len + j);
   a.crc = crc;
+  a.crc_in = crc + j;
   a.msg_len = d_msg_len;
   a.in_crc = d_in_crc;
   a.img = c->d_img;
@@ -66,10 +67,10 @@ int enqueue_serialize(DevCtx* c, const ::ambrycrc_put_desc* d_desc, size_t m, co
   if (a.copy_through) {
     // one pass over the fields: the copy-through sweep reads each from its source, writes it into
     // the message and CRCs it (job k*m+i = slot k of message i, as the CRC jobs)
-    const int rc = enqueue_batch(c, nullptr, a.cp_src, a.cp_len, nullptr, crc, j, batch_ws, stream, nullptr, d_out,
+    const int rc = enqueue_batch(c, nullptr, a.cp_src, a.cp_len, a.crc_in, crc, j, batch_ws, stream, nullptr, d_out,
                                  a.cp_dst);
     if (rc) return rc;
-    return hip_err(launch_put_seal_combine(a, stream));
+    return hip_err(launch_put_seal(a, stream));
   }
   if (d_fields || d_blobs) {
     // cost offsets of the copy jobs: the plan kernel's exclusive scan (no small-chunk classes);

@@ -136,6 +136,7 @@ struct PutArgs {
   uint64_t* crc_off;       // [5m] CRC jobs in out (length 0: absent encryption-key record)
   uint64_t* crc_len;
   const uint32_t* crc;     // [5m] their CRCs (from the batch kernels)
+  uint32_t* crc_in;        // [5m] copy-through: the CRC of each record's prefix, the batch's seed
   uint64_t* msg_len;       // [m] or null
   // Transform only: the CRCs of records 1-4 (encryption key, properties, user metadata, blob)
   // known from the input message ([4m], message-major; see TransformArgs::in_crc). When set,
@@ -146,9 +147,10 @@ struct PutArgs {
   // Run only when *gate != 0 (null: always). The transform's fallback pass.
   const uint32_t* gate;
   // Copy-through mode (copy mode without in_crc): the copy jobs become the CRC batch itself --
-  // the sweep reads each field once, writes it to the message and CRCs it; put_seal_combine_kernel
-  // then extends each content CRC over its record prefix. A slot with no source buffer (fields
-  // or blobs null) re-reads its bytes in place (src = dst).
+  // the sweep reads each field once, writes it to the message and CRCs it, seeded (crc_in) with
+  // the CRC of the record's prefix (<= 13 B, hashed by the layout kernel), so the batch's result
+  // is the record CRC; the layout kernel writes the header trailer itself. A slot with no source
+  // buffer (fields or blobs null) re-reads its bytes in place (src = dst).
   bool copy_through;
 };
 
@@ -208,7 +210,6 @@ hipError_t launch_transform_merge(const TransformArgs& a, hipStream_t s);
 
 hipError_t launch_put_layout(const PutArgs& a, hipStream_t s);
 hipError_t launch_put_seal(const PutArgs& a, hipStream_t s);
-hipError_t launch_put_seal_combine(const PutArgs& a, hipStream_t s);
 hipError_t launch_gather_copy(const CopyArgs& a, int grid, hipStream_t s);
 
 hipError_t launch_trailer_parse(const TrailerArgs& a, hipStream_t s);

@@ -499,7 +499,13 @@ __global__ __launch_bounds__(256) void transform_finish_kernel(TransformArgs a) 
   }
   const uint8_t* src = a.region + d.key_src;
   uint8_t* dst = a.out + d.out_off + (d.header_version == 1 ? 34u : d.header_version == 2 ? 38u : 40u);
-  for (uint32_t b = 0; b < d.key_len; ++b) dst[b] = src[b];
+  uint32_t b = 0;
+  for (; b + 8 <= d.key_len; b += 8) {  // 8-B moves at any alignment (unaligned global access)
+    uint64_t v;
+    __builtin_memcpy(&v, src + b, 8);
+    __builtin_memcpy(dst + b, &v, 8);
+  }
+  for (; b < d.key_len; ++b) dst[b] = src[b];
 }
 
 // No fallback: the final status is the verify's bits, or else the transform's own.

@@ -34,6 +34,7 @@ __global__ __launch_bounds__(256) void put_layout_kernel(PutArgs a) {
       a.cp_cost[k * m + i] = 0;
       a.crc_len[k * m + i] = 0;
       a.crc_off[k * m + i] = 0;
+      if (a.copy_through) a.crc_in[k * m + i] = 0;
     }
     if (a.msg_len) a.msg_len[i] = 0;
     return;
@@ -61,33 +62,20 @@ __global__ __launch_bounds__(256) void put_layout_kernel(PutArgs a) {
       const uint32_t crc = k == 0 ? crc_bytes_img(a.img, 0u, msg, (uint32_t)ln) : a.in_crc[4 * i + k - 1];
       put_be64(msg + off + ln, (uint64_t)crc);
     }
+    if (a.copy_through) {  // the batch's seeds: each record's prefix CRC; the header is hashed whole
+      uint32_t seed = 0;
+      if (k == 0) put_be64(msg + ln, (uint64_t)crc_bytes_img(a.img, 0u, msg, (uint32_t)ln));
+      else if (present) seed = crc_bytes_img(a.img, 0u, msg + off, (uint32_t)(ln - len[k]));
+      a.crc_in[k * m + i] = seed;
+    }
   }
   if (a.msg_len) a.msg_len[i] = L.length;
-}
-
-// Copy-through mode: crc[j] holds the CRC of job j's content (the field bytes after the record
-// prefix); the record CRC follows by combine, crc(prefix || content) = crc(prefix) * x^(8|content|)
-// ^ crc(content), with the prefix (<= 13 B: version, size fields) hashed here from the message.
-// Slot 0's copy job is the key, which no CRC covers: the header CRC is hashed whole.
-__global__ __launch_bounds__(256) void put_seal_combine_kernel(PutArgs a) {
-  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= kPutSlots * a.m) return;
-  const uint64_t len = a.crc_len[j];
-  if (len == 0) return;  // absent encryption-key record
-  uint8_t* rec = a.out + a.crc_off[j];
-  uint32_t crc;
-  if (j < a.m) {
-    crc = crc_bytes_img(a.img, 0u, rec, (uint32_t)len);
-  } else {
-    const uint64_t cl = a.cp_len[j];
-    crc = mul_xpow8_img(a.img, crc_bytes_img(a.img, 0u, rec, (uint32_t)(len - cl)), cl) ^ a.crc[j];
-  }
-  put_be64(rec + len, (uint64_t)crc);
 }
 
 __global__ __launch_bounds__(256) void put_seal_kernel(PutArgs a) {
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= kPutSlots * a.m) return;
+  if (a.copy_through && j < a.m) return;  // slot 0's job is the key; the layout kernel sealed the header
   const uint64_t len = a.crc_len[j];
   if (len == 0) return;  // absent encryption-key record (every present record has >= 6 bytes)
   put_be64(a.out + a.crc_off[j] + len, (uint64_t)a.crc[j]);
@@ -244,12 +232,6 @@ hipError_t launch_put_layout(const PutArgs& a, hipStream_t s) {
 hipError_t launch_put_seal(const PutArgs& a, hipStream_t s) {
   if (a.m == 0) return hipSuccess;
   hipLaunchKernelGGL(put_seal_kernel, dim3((uint32_t)((kPutSlots * a.m + 255) / 256)), dim3(256), 0, s, a);
-  return hipGetLastError();
-}
-
-hipError_t launch_put_seal_combine(const PutArgs& a, hipStream_t s) {
-  if (a.m == 0) return hipSuccess;
-  hipLaunchKernelGGL(put_seal_combine_kernel, dim3((uint32_t)((kPutSlots * a.m + 255) / 256)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
