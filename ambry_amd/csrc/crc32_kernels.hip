@@ -11,7 +11,7 @@
 //             persistent grid owns an equal share [w*S, (w+1)*S) of it (exact byte
 //             balance for any chunk-size mix), cut points snapped to 16 B in memory.
 //             Whole chunks <= 16 KiB (batches of >= 16,384 chunks) go to the group
-//             phase first: G = 4/8/16 lanes per chunk by size class, 64/G chunks per wave
+//             phase first: G = 2/8/16 lanes per chunk by size class, 64/G chunks per wave
 //   segment-> a (wave, chunk) intersection; the wave sweeps it in 4 KiB super-blocks:
 //             four coalesced 1 KiB global_load_dwordx4 per lane, a quad transpose
 //             leaving each lane a 64-B run
@@ -585,7 +585,8 @@ __device__ __forceinline__ uint64_t group_per(uint64_t ns, uint64_t nwaves) {
 // metadata, 4 KiB blob) puts all the 4 KiB records on a third of the waves; and it runs
 // every class with G = 16, so a 100 B chunk pays a 256 B block and a 4-level tree. Here
 // each class is spread over all waves separately, with a group width sized to the class:
-//   class 0 (<= 256 B): G = 4,  64 B blocks, 16 chunks per round
+//   class 0 (<= 256 B): G = 2,  32 B blocks, 32 chunks per round (was G = 4: a round is
+//                       latency-bound, so twice the chunks per round wins over a shorter chain)
 //   class 1 (<= 1 KiB): G = 8, 128 B blocks,  8 chunks per round
 //   class 2 (<= 4 KiB): G = 16, 256 B blocks, 4 chunks per round; class 3 (<= 16 KiB) too.
 // The trailing t < 16 bytes go 16/G per lane: lane gl takes the bytes at distance
@@ -594,7 +595,7 @@ __device__ __forceinline__ uint64_t group_per(uint64_t ns, uint64_t nwaves) {
 
 template <int G>
 __device__ __forceinline__ constexpr uint32_t group_fold_off() {  // x^(8*16G) = POW[log2 16G]
-  return kPowOff + kNibSetBytes * (G == 4 ? 6u : G == 8 ? 7u : G == 16 ? 8u : 9u);
+  return kPowOff + kNibSetBytes * (G == 1 ? 4u : G == 2 ? 5u : G == 4 ? 6u : G == 8 ? 7u : G == 16 ? 8u : 9u);
 }
 
 // xor over the G lanes of each group; result in every lane of the group
@@ -606,9 +607,9 @@ __device__ __forceinline__ uint32_t group_xor(uint32_t v) {
     v ^= dpp<0x122, 0xf>(v);
     v ^= dpp<0x121, 0xf>(v);
   } else {
-    static_assert(G == 4 || G == 8, "group width");
-    v ^= dppq<0xB1>(v);  // lane ^ 1
-    v ^= dppq<0x4E>(v);  // lane ^ 2
+    static_assert(G == 1 || G == 2 || G == 4 || G == 8, "group width");
+    if constexpr (G >= 2) v ^= dppq<0xB1>(v);  // lane ^ 1
+    if constexpr (G >= 4) v ^= dppq<0x4E>(v);  // lane ^ 2
     if constexpr (G == 8) v ^= (uint32_t)__shfl_xor((int)v, 4);
   }
   return v;
@@ -646,8 +647,8 @@ __device__ __forceinline__ uint32_t group_crc_g(const uint8_t* __restrict__ base
   for (uint32_t b0 = 0; b0 < nbw; b0 += P) s = ring.step(g, k, b0, s, group_fold_off<G>());
   uint32_t r = s;
   if (nbw) {
-    r = tree_level<0>(r, lane);
-    r = tree_level<1>(r, lane);
+    if constexpr (G >= 2) r = tree_level<0>(r, lane);
+    if constexpr (G >= 4) r = tree_level<1>(r, lane);
     if constexpr (G >= 8) r = tree_level<2>(r, lane);
     if constexpr (G >= 16) r = tree_level<3>(r, lane);
     if constexpr (G >= 32) r = tree_level<4>(r, lane);
@@ -657,6 +658,11 @@ __device__ __forceinline__ uint32_t group_crc_g(const uint8_t* __restrict__ base
   if (t & 2u) r = nib_mul(r, kPowOff + kNibSetBytes * 1);
   if (t & 4u) r = nib_mul(r, kPowOff + kNibSetBytes * 2);
   if (t & 8u) r = nib_mul(r, kPowOff + kNibSetBytes * 3);
+  // vq[q]: the lane's bytes 4q..4q+3 (16/G > 4 for G < 4), each quad one x^(8*4) further
+  constexpr uint32_t NQ = (BPL + 3) / 4;
+  uint32_t vq[NQ];
+#pragma unroll
+  for (uint32_t q = 0; q < NQ; ++q) vq[q] = 0;
   uint32_t v = 0;
   if (k0 < t) {
 #pragma unroll
@@ -667,9 +673,12 @@ __device__ __forceinline__ uint32_t group_crc_g(const uint8_t* __restrict__ base
         uint32_t byte = tb[i];
         if (at < cs + 4) byte ^= (rinit >> (8 * (uint32_t)(at - cs))) & 0xFFu;
         const uint32_t j = kk & 3;
-        v ^= lds_rd(((j >> 1) << 16) | (byte << 8) | ((j & 1) << 7) | ((lane & 31) << 2));
+        vq[i / 4] ^= lds_rd(((j >> 1) << 16) | (byte << 8) | ((j & 1) << 7) | ((lane & 31) << 2));
       }
     }
+    v = vq[NQ - 1];
+#pragma unroll
+    for (int q = (int)NQ - 2; q >= 0; --q) v = vq[q] ^ nib_mul(v, kPowOff + kNibSetBytes * 2);
     if (k0 & 4) v = nib_mul(v, kPowOff + kNibSetBytes * 2);  // x^(8*4)
     if (k0 & 8) v = nib_mul(v, kPowOff + kNibSetBytes * 3);  // x^(8*8)
   }
@@ -978,23 +987,33 @@ __device__ __forceinline__ void group_class(const SweepArgs& a, uint64_t lo, uin
   }
 }
 
+// Class 0's group width and ring depth (A/B knobs for tools/ab_build.sh AB_FLAGS): 2-lane groups,
+// 8 blocks in flight, 32 chunks per round -- measured 1.57x faster than 4-lane groups on 100 B
+// records. Class 1 at G = 4 or 2 measured slower (1.1x, 1.75x).
+#ifndef AMBRY_C0_G
+#define AMBRY_C0_G 2
+#endif
+#ifndef AMBRY_C0_NB
+#define AMBRY_C0_NB 8
+#endif
+
 // class bounds from the plan: small_total = {total, start of class 1, 2, 3}
 __device__ __forceinline__ bool group_cls_has_work(const SweepArgs& a, uint32_t first_wave, uint64_t nwaves) {
   const uint64_t c0 = 0, c1 = a.small_total[1], c2 = a.small_total[2], c3 = a.small_total[3];
   const uint64_t c4 = a.small_total[0];
-  return (c1 > c0 && first_wave * group_per<4>(c1 - c0, nwaves) < c1 - c0) ||
+  return (c1 > c0 && first_wave * group_per<AMBRY_C0_G>(c1 - c0, nwaves) < c1 - c0) ||
          (c2 > c1 && first_wave * group_per<8>(c2 - c1, nwaves) < c2 - c1) ||
          (c3 > c2 && first_wave * group_per<16>(c3 - c2, nwaves) < c3 - c2) ||
          (c4 > c3 && first_wave * group_per<16>(c4 - c3, nwaves) < c4 - c3);
 }
 
-// Class 0 (<= 256 B) in 4-lane groups of 16-B pieces; classes 1-3 with 64-B lane runs in 8- and
+// Class 0 (<= 256 B) in 2-lane groups of 16-B pieces; classes 1-3 with 64-B lane runs in 8- and
 // 16-lane groups.
 template <bool NT, bool COPY = false>
 __device__ __forceinline__ void group_phase_cls(const SweepArgs& a, uint32_t wave, uint64_t nwaves, uint32_t lane,
                                                 const LaneConst& k) {
   const uint64_t c1 = a.small_total[1], c2 = a.small_total[2], c3 = a.small_total[3], c4 = a.small_total[0];
-  group_class<4, 4, NT, COPY>(a, 0, c1, wave, nwaves, lane, k);
+  group_class<AMBRY_C0_G, AMBRY_C0_NB, NT, COPY>(a, 0, c1, wave, nwaves, lane, k);
   group_class_t4s<8, NT, COPY>(a, c1, c2, wave, nwaves, lane, k);
   group_class_t4s<16, NT, COPY>(a, c2, c3, wave, nwaves, lane, k);
   group_class_t4s<16, NT, COPY>(a, c3, c4, wave, nwaves, lane, k);
