@@ -44,22 +44,6 @@ __device__ __forceinline__ uint64_t be64(const uint8_t* p) {
   return __builtin_bswap64(v);
 }
 
-// Slice-by-4 tables T0..T3 (T_j[b] = b advanced over j further zero bytes), 4 KiB, staged
-// into LDS per workgroup from the table image: T_j[b] sits at image byte
-// (j>>1)<<16 | b<<8 | (j&1)<<7 (lane column 0), crc32_layout.h.
-// 256-thread blocks: each thread issues its 4 loads before its 4 LDS stores (one memory
-// round trip, not four).
-__device__ __forceinline__ void stage_slice_tables(uint32_t* __restrict__ t, const uint32_t* __restrict__ img) {
-  uint32_t v[4];
-#pragma unroll
-  for (uint32_t r = 0; r < 4; ++r) {
-    const uint32_t i = threadIdx.x + 256u * r, j = i >> 8, b = i & 255u;
-    v[r] = img[(((j >> 1) << 16) | (b << 8) | ((j & 1) << 7)) >> 2];
-  }
-#pragma unroll
-  for (uint32_t r = 0; r < 4; ++r) t[threadIdx.x + 256u * r] = v[r];
-}
-
 __constant__ uint32_t kRecordBit[5] = {AMBRYCRC_MSG_ENCKEY_CRC, AMBRYCRC_MSG_PROPS_CRC, AMBRYCRC_MSG_UPDATE_CRC,
                                        AMBRYCRC_MSG_USERMETA_CRC, AMBRYCRC_MSG_BLOB_CRC};
 

@@ -23,6 +23,15 @@ namespace ambrycrc {
 typedef uint32_t u32x4p __attribute__((ext_vector_type(4)));
 
 __global__ __launch_bounds__(256) void put_layout_kernel(PutArgs a) {
+  // The CRCs this kernel takes itself (the header's; copy-through's record-prefix seeds) run over
+  // bytes it builds in registers, through LDS tables: not over bytes it just stored, read back
+  // one dependent global load per byte.
+  __shared__ uint32_t tbl[1024];
+  const bool hashes = a.copy_through || a.in_crc;  // kernel-uniform
+  if (hashes) {
+    stage_slice_tables(tbl, a.img);
+    __syncthreads();
+  }
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.m || (a.gate && *a.gate == 0)) return;
   const ambrycrc_put_desc d = a.desc[i];
@@ -41,11 +50,18 @@ __global__ __launch_bounds__(256) void put_layout_kernel(PutArgs a) {
   }
   uint8_t* msg = a.out + d.out_off;
   put_write_fixed(d, L, msg);
+  uint32_t head_crc = 0;
+  if (hashes) {
+    uint8_t h[32];
+    const uint32_t hn = put_header_bytes(d, L, h);
+    head_crc = crc_regs_lds(tbl, 0u, h, hn);
+  }
   uint64_t fo[5];
   put_field_offsets(d, L, fo);
   const uint64_t src[5] = {d.key_src, d.enckey_src, d.props_src, d.usermeta_src, d.blob_src};
   const uint64_t len[5] = {d.key_len, L.enc_rec ? (uint64_t)d.enckey_len : 0, d.props_len, d.usermeta_len,
                            d.blob_len};
+#pragma unroll
   for (uint32_t k = 0; k < kPutSlots; ++k) {
     const uint8_t* base = k == 4 ? a.blobs : a.fields;
     a.cp_src[k * m + i] = base ? (uint64_t)(uintptr_t)(base + src[k])
@@ -59,13 +75,18 @@ __global__ __launch_bounds__(256) void put_layout_kernel(PutArgs a) {
     a.crc_off[k * m + i] = d.out_off + off;
     a.crc_len[k * m + i] = present ? ln : 0;
     if (a.in_crc && present) {  // transform: every CRC known but the header's (hashed here)
-      const uint32_t crc = k == 0 ? crc_bytes_img(a.img, 0u, msg, (uint32_t)ln) : a.in_crc[4 * i + k - 1];
+      const uint32_t crc = k == 0 ? head_crc : a.in_crc[4 * i + k - 1];
       put_be64(msg + off + ln, (uint64_t)crc);
     }
     if (a.copy_through) {  // the batch's seeds: each record's prefix CRC; the header is hashed whole
       uint32_t seed = 0;
-      if (k == 0) put_be64(msg + ln, (uint64_t)crc_bytes_img(a.img, 0u, msg, (uint32_t)ln));
-      else if (present) seed = crc_bytes_img(a.img, 0u, msg + off, (uint32_t)(ln - len[k]));
+      if (k == 0) {
+        put_be64(msg + ln, (uint64_t)head_crc);
+      } else if (present) {
+        uint8_t b[16];
+        const uint32_t pl = put_prefix_bytes(d, k, b);
+        seed = crc_regs_lds(tbl, 0u, b, pl);
+      }
       a.crc_in[k * m + i] = seed;
     }
   }

@@ -55,52 +55,100 @@ __host__ __device__ inline bool put_layout(const ambrycrc_put_desc& d, PutLayout
   return true;
 }
 
+// Big-endian stores at any alignment (one unaligned store each on the device and the host).
 __host__ __device__ inline void put_be16(uint8_t* p, uint32_t v) {
-  p[0] = (uint8_t)(v >> 8);
-  p[1] = (uint8_t)v;
+  const uint16_t x = __builtin_bswap16((uint16_t)v);
+  __builtin_memcpy(p, &x, 2);
 }
 __host__ __device__ inline void put_be32(uint8_t* p, uint32_t v) {
-  p[0] = (uint8_t)(v >> 24);
-  p[1] = (uint8_t)(v >> 16);
-  p[2] = (uint8_t)(v >> 8);
-  p[3] = (uint8_t)v;
+  const uint32_t x = __builtin_bswap32(v);
+  __builtin_memcpy(p, &x, 4);
 }
 __host__ __device__ inline void put_be64(uint8_t* p, uint64_t v) {
-  put_be32(p, (uint32_t)(v >> 32));
-  put_be32(p + 4, (uint32_t)v);
+  const uint64_t x = __builtin_bswap64(v);
+  __builtin_memcpy(p, &x, 8);
 }
 
-// Header (without its CRC) and the fixed prefixes of every record, at message start m.
-__host__ __device__ inline void put_write_fixed(const ambrycrc_put_desc& d, const PutLayout& L, uint8_t* m) {
+// The header's CRC'd bytes [0, hsize - 8) (26, 30 or 32) into h; returns their count.
+__host__ __device__ inline uint32_t put_header_bytes(const ambrycrc_put_desc& d, const PutLayout& L, uint8_t (&h)[32]) {
   const int v = d.header_version;
-  put_be16(m, (uint32_t)v);
-  uint8_t* q = m + 2;
+  h[30] = h[31] = 0;
+  put_be16(h, (uint32_t)v);
   if (v == 3) {
-    put_be16(q, (uint32_t)(uint16_t)d.life_version);
-    q += 2;
+    put_be16(h + 2, (uint32_t)(uint16_t)d.life_version);
+    put_be64(h + 4, L.total);
+    put_be32(h + 12, (uint32_t)L.enc_rel);
+    put_be32(h + 16, (uint32_t)L.bp_rel);
+    put_be32(h + 20, 0xFFFFFFFFu);  // update record: Message_Header_Invalid_Relative_Offset
+    put_be32(h + 24, (uint32_t)L.um_rel);
+    put_be32(h + 28, (uint32_t)L.blob_rel);
+    return 32;
   }
-  put_be64(q, L.total);
-  q += 8;
-  if (v >= 2) {
-    put_be32(q, (uint32_t)L.enc_rel);
-    q += 4;
+  put_be64(h + 2, L.total);
+  if (v == 2) {
+    put_be32(h + 10, (uint32_t)L.enc_rel);
+    put_be32(h + 14, (uint32_t)L.bp_rel);
+    put_be32(h + 18, 0xFFFFFFFFu);
+    put_be32(h + 22, (uint32_t)L.um_rel);
+    put_be32(h + 26, (uint32_t)L.blob_rel);
+    return 30;
   }
-  put_be32(q, (uint32_t)L.bp_rel);
-  put_be32(q + 4, 0xFFFFFFFFu);  // update record: Message_Header_Invalid_Relative_Offset
-  put_be32(q + 8, (uint32_t)L.um_rel);
-  put_be32(q + 12, (uint32_t)L.blob_rel);
+  put_be32(h + 10, (uint32_t)L.bp_rel);
+  put_be32(h + 14, 0xFFFFFFFFu);
+  put_be32(h + 18, (uint32_t)L.um_rel);
+  put_be32(h + 22, (uint32_t)L.blob_rel);
+  return 26;
+}
+
+// Record k's prefix (k = 1 encryption key, 2 properties, 3 user metadata, 4 blob): the bytes
+// before its variable field that its CRC covers -- version, and the size (key, metadata) or
+// type, isCompressed and size (blob) fields. Into b; returns the count (6, 2, 6, 13).
+__host__ __device__ inline uint32_t put_prefix_bytes(const ambrycrc_put_desc& d, uint32_t k, uint8_t (&b)[16]) {
+  switch (k) {
+    case 1:
+      put_be16(b, 1);
+      put_be32(b + 2, (uint32_t)d.enckey_len);
+      return 6;
+    case 2:
+      put_be16(b, 1);
+      return 2;
+    case 3:
+      put_be16(b, 1);
+      put_be32(b + 2, d.usermeta_len);
+      return 6;
+    default:
+      put_be16(b, 3);
+      put_be16(b + 2, (uint32_t)(uint16_t)d.blob_type);
+      b[4] = d.compressed ? 1 : 0;
+      put_be64(b + 5, d.blob_len);
+      return 13;
+  }
+}
+
+// Record k's offset from the message start (k as put_prefix_bytes).
+__host__ __device__ inline int32_t put_record_rel(const PutLayout& L, uint32_t k) {
+  return k == 1 ? L.enc_rel : k == 2 ? L.bp_rel : k == 3 ? L.um_rel : L.blob_rel;
+}
+
+// Header (without its CRC) and the fixed prefixes of every record, at message start m
+// (constant-size copies: on the device one wide unaligned store per 16 B, not a store per byte).
+__host__ __device__ inline void put_write_fixed(const ambrycrc_put_desc& d, const PutLayout& L, uint8_t* m) {
+  uint8_t h[32];
+  const uint32_t n = put_header_bytes(d, L, h);
+  if (n == 32) __builtin_memcpy(m, h, 32);
+  else if (n == 30) __builtin_memcpy(m, h, 30);
+  else __builtin_memcpy(m, h, 26);
+  uint8_t b[16];
   if (L.enc_rec) {
-    put_be16(m + L.enc_rel, 1);
-    put_be32(m + L.enc_rel + 2, (uint32_t)d.enckey_len);
+    put_prefix_bytes(d, 1, b);
+    __builtin_memcpy(m + L.enc_rel, b, 6);
   }
-  put_be16(m + L.bp_rel, 1);
-  put_be16(m + L.um_rel, 1);
-  put_be32(m + L.um_rel + 2, d.usermeta_len);
-  uint8_t* b = m + L.blob_rel;
-  put_be16(b, 3);
-  put_be16(b + 2, (uint32_t)(uint16_t)d.blob_type);
-  b[4] = d.compressed ? 1 : 0;
-  put_be64(b + 5, d.blob_len);
+  put_prefix_bytes(d, 2, b);
+  __builtin_memcpy(m + L.bp_rel, b, 2);
+  put_prefix_bytes(d, 3, b);
+  __builtin_memcpy(m + L.um_rel, b, 6);
+  put_prefix_bytes(d, 4, b);
+  __builtin_memcpy(m + L.blob_rel, b, 13);
 }
 
 // Offsets (from the message start) of the variable fields: key, encryption key, properties,
