@@ -1582,9 +1582,12 @@ __global__ __launch_bounds__(256) void readbw_stream_kernel(const u32x4* __restr
 // 64/G per wave round (one per G-lane group), wave w taking an equal run of the chunk list; each
 // lane loads its 16 B of four 16G-byte blocks per 64G-byte super-block (t4_load), one
 // super-block prefetched. The read roof the 4 KiB records' group rounds are compared against.
-template <int G>
+// COPY: also store every piece at dst + (its source offset) -- the group phase's copy-through
+// store shape, for the copy roof of that shape (variants 32+ of launch_readbw).
+template <int G, bool COPY = false>
 __global__ __launch_bounds__(1024) void readbw_group_kernel(const uint8_t* __restrict__ base, uint64_t nbytes,
-                                                            uint32_t chunk, uint32_t* __restrict__ out) {
+                                                            uint32_t chunk, uint32_t* __restrict__ out,
+                                                            uint8_t* __restrict__ dst = nullptr) {
   constexpr uint32_t S = 64 / G;
   const uint32_t lane = threadIdx.x & 63u, gl = lane & (G - 1), gi = lane / G;
   const uint32_t wave = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * gridDim.x + blockIdx.x);
@@ -1607,13 +1610,51 @@ __global__ __launch_bounds__(1024) void readbw_group_kernel(const uint8_t* __res
         if (sb + 1 < nsb) nx[j] = ld16<true>(q + (sb + 1) * 4 * G + G * j);
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) x ^= cur[j].x ^ cur[j].y ^ cur[j].z ^ cur[j].w;
+      for (int j = 0; j < 4; ++j) {
+        if constexpr (COPY) {
+          if (sb * 4 * G + G * j + gl < chunk / 16)
+            st16u(dst + c * chunk + 16 * ((uint64_t)sb * 4 * G + G * j + gl), cur[j]);
+        }
+        x ^= cur[j].x ^ cur[j].y ^ cur[j].z ^ cur[j].w;
+      }
     }
   }
   out[blockIdx.x * blockDim.x + threadIdx.x] = x;
 }
 
+// Contiguous copy: each wave copies an equal contiguous share of [0, n16) 16-B pieces, four per
+// lane in flight (the plain copy roof of launch_readbw variant 48).
+__global__ __launch_bounds__(1024) void copybw_stream_kernel(const u32x4* __restrict__ src, uint64_t n16,
+                                                             uint8_t* __restrict__ dst) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t wave = (threadIdx.x >> 6) * (uint64_t)gridDim.x + blockIdx.x;
+  const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  const uint64_t per = ((n16 + nwaves - 1) / nwaves + 255) / 256 * 256;
+  const uint64_t i0 = wave * per, i1 = i0 + per < n16 ? i0 + per : n16;
+  for (uint64_t i = i0 + lane; i < i1; i += 256) {
+    u32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = ld16<true>(src + (i + 64 * u < i1 ? i + 64 * u : i));
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i + 64 * u < i1) st16u(dst + 16 * (i + 64 * u), v[u]);
+  }
+}
+
 hipError_t launch_readbw(const uint8_t* base, uint64_t nbytes, uint32_t* out, int grid, int variant, hipStream_t s) {
+  if (variant >= 32) {  // copy probes: read [0, nbytes/2), write from nbytes/2 (+ 11 B for 40..44)
+    const uint64_t half = nbytes / 2 - 4096;
+    uint8_t* dst = const_cast<uint8_t*>(base) + nbytes / 2 + (variant >= 40 && variant < 48 ? 11 : 0);
+    if (variant == 48) {
+      hipLaunchKernelGGL(copybw_stream_kernel, dim3(grid), dim3(1024), 0, s, reinterpret_cast<const u32x4*>(base),
+                         half / 16, dst);
+      return hipGetLastError();
+    }
+    if (variant > 44) return hipErrorInvalidValue;
+    const uint32_t chunk = 1024u << ((variant - 32) & 7);
+    hipLaunchKernelGGL((readbw_group_kernel<16, true>), dim3(grid), dim3(1024), 0, s, base, half, chunk, out, dst);
+    return hipGetLastError();
+  }
   if (variant >= 16) {  // group shape: variant = 16 + log2(chunk bytes / 1024) for G = 16 (4 KiB: 18)
     const uint32_t chunk = 1024u << (variant - 16);
     hipLaunchKernelGGL(readbw_group_kernel<16>, dim3(grid), dim3(1024), 0, s, base, nbytes, chunk, out);

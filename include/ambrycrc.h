@@ -458,7 +458,11 @@ int ambrycrc_fill_random_dev(uint8_t* d_dst, uint64_t nbytes, uint64_t seed, uin
  * nontemporal loads; 2 = plain grid-stride stream; 3 = contiguous per-wave shares, NT;
  * 4 = shares entered at a per-wave rotation, NT; 16 + k = the group phase's shape for chunks of 1 KiB << k,
  * 16-lane groups, 4 chunks per wave round, one 1 KiB super-block per group prefetched). d_out needs grid*1024
- * words. Measures the achievable HBM read roof the CRC kernels are compared against. */
+ * words. Measures the achievable HBM read roof the CRC kernels are compared against.
+ * Copy probes (they WRITE the buffer's upper half): 32 + k = the group shape above reading
+ * [0, nbytes/2 - 4096) and storing each piece at the same offset from d_base + nbytes/2;
+ * 40 + k = the same with the destination 11 B further (unaligned stores); 48 = contiguous
+ * per-wave shares, the plain copy roof. */
 int ambrycrc_debug_readbw_dev(const uint8_t* d_base, uint64_t nbytes, uint32_t* d_out, int variant,
                               hipStream_t stream);
 
