@@ -888,7 +888,7 @@ int enqueue_messages(DevCtx* c, const uint8_t* d_region, uint64_t region_len, co
 
 int enqueue_messages_parse(DevCtx* c, const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off,
                            size_t m, uint32_t* d_status, uint64_t* d_msg_end, void* d_ws, hipStream_t stream,
-                           MsgStage* st) {
+                           MsgStage* st, const TransformArgs* desc) {
   const size_t j = (size_t)kMsgSlots * m;
   uint8_t* w = static_cast<uint8_t*>(d_ws);
   MsgArgs& a = st->a;
@@ -911,7 +911,7 @@ int enqueue_messages_parse(DevCtx* c, const uint8_t* d_region, uint64_t region_l
   st->batch_ws = w + ((j * 2 * sizeof(uint64_t) + j * 2 * sizeof(uint32_t) + j + 255) & ~size_t(255));
   st->crc = crc;
   st->j = j;
-  return hip_err(launch_msg_parse(a, stream));
+  return hip_err(desc ? launch_msg_parse_desc(a, *desc, stream) : launch_msg_parse(a, stream));
 }
 
 int enqueue_messages_check(DevCtx* c, const MsgStage& st, hipStream_t stream, uint8_t* copy_dst,

@@ -58,7 +58,7 @@ struct DevCtx {
   // quad transpose by v_cndmask_b32_dpp, one x^(8*4096) fold per 64 B), s_setprio 3 around
   // the loads; plus, for batches of >= kGroupMinChunks chunks, whole chunks <= 16 KiB in the
   // fused group phase, each size class spread over all waves with a class-sized group
-  // (G = 4 / 8 / 16 lanes). Measured against the round-1 alternatives in DESIGN.md §4-5.
+  // (G = 2 / 8 / 16 lanes). Measured against the round-1 alternatives in DESIGN.md §4-5.
   int variant = kVariantDefault;
   // Sweep rounds of at most this many bytes (SweepArgs::window); 0 = one round.
   uint64_t window = 32ull << 30;
@@ -119,7 +119,7 @@ struct MsgStage {
 };
 int enqueue_messages_parse(DevCtx* c, const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off,
                            size_t m, uint32_t* d_status, uint64_t* d_msg_end, void* d_ws, hipStream_t stream,
-                           MsgStage* st);
+                           MsgStage* st, const TransformArgs* desc = nullptr);
 int enqueue_messages_check(DevCtx* c, const MsgStage& st, hipStream_t stream, uint8_t* copy_dst = nullptr,
                            const uint64_t* copy_off = nullptr);
 // The PUT serialization pipeline (layout -> copy -> plan + CRC -> seal); d_ws holds at least

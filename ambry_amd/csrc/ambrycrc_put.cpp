@@ -233,12 +233,12 @@ int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len
   // the three-pass form did (verify bits first, then the transform's own, then the placement).
   if (hipMemsetAsync(fail, 0, sizeof(uint32_t), stream) != hipSuccess) return AMBRYCRC_EHIP;
   MsgStage ms;
-  rc = enqueue_messages_parse(c, d_region, region_len, d_msg_off, m, d_status, nullptr, shared, stream, &ms);
-  if (rc) return rc;
   t.xstatus = xstatus;
-  t.job_off = ms.a.job_off;
   t.copy_off = copy_off;
-  if (launch_transform_desc(t, stream) != hipSuccess) return AMBRYCRC_EHIP;
+  // the parse kernel describes each message as it parses it (transform_desc_kernel fused)
+  rc = enqueue_messages_parse(c, d_region, region_len, d_msg_off, m, d_status, nullptr, shared, stream, &ms, &t);
+  if (rc) return rc;
+  t.job_off = ms.a.job_off;
   if (launch_plan(p, stream) != hipSuccess) return AMBRYCRC_EHIP;
   if (launch_transform_place(t, p.byte_start, stream) != hipSuccess) return AMBRYCRC_EHIP;
   if (launch_transform_jobs(t, stream) != hipSuccess) return AMBRYCRC_EHIP;

@@ -203,6 +203,9 @@ struct TransformArgs {
 };
 
 hipError_t launch_transform_desc(const TransformArgs& a, hipStream_t s);
+// msg_parse_kernel fused with transform_desc_kernel (the speculative pass): a and t describe the
+// same messages.
+hipError_t launch_msg_parse_desc(const MsgArgs& a, const TransformArgs& t, hipStream_t s);
 hipError_t launch_transform_place(const TransformArgs& a, const uint64_t* start, hipStream_t s);
 hipError_t launch_transform_jobs(const TransformArgs& a, hipStream_t s);
 hipError_t launch_transform_finish(const TransformArgs& a, hipStream_t s);

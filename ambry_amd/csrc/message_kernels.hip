@@ -134,7 +134,12 @@ __device__ __forceinline__ uint32_t record_check(int k, const uint8_t* q, uint64
   }
 }
 
-__global__ __launch_bounds__(256) void msg_parse_kernel(MsgArgs a) {
+__device__ __forceinline__ void transform_describe(const TransformArgs& a, uint64_t i, uint32_t st0);
+
+// DESC: the transform's speculative pass -- describe each message right after parsing it, from
+// the header and record heads this thread just loaded (transform_describe's reads hit the cache).
+template <bool DESC>
+__global__ __launch_bounds__(256) void msg_parse_kernel(MsgArgs a, TransformArgs t) {
   __shared__ uint32_t tbl[1024];
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = i < a.m;
@@ -253,6 +258,7 @@ __global__ __launch_bounds__(256) void msg_parse_kernel(MsgArgs a) {
   }
   a.status[i] = status;
   if (a.msg_end) a.msg_end[i] = end ? off + end : 0;
+  if constexpr (DESC) transform_describe(t, i, status);
 }
 
 __global__ __launch_bounds__(256) void msg_reduce_kernel(MsgArgs a) {
@@ -312,10 +318,7 @@ __device__ __forceinline__ bool gated_off(const uint32_t* gate, int when) {
   return gate && ((*gate != 0) != (when != 0));
 }
 
-__global__ __launch_bounds__(256) void transform_desc_kernel(TransformArgs a) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.m || gated_off(a.gate, a.gate_when)) return;
-  const uint32_t st0 = a.status[i];
+__device__ __forceinline__ void transform_describe(const TransformArgs& a, uint64_t i, uint32_t st0) {
   uint32_t st = st0;
   ambrycrc_put_desc d;
   __builtin_memset(&d, 0, sizeof(d));  // header_version 0: nothing to write
@@ -427,6 +430,12 @@ __global__ __launch_bounds__(256) void transform_desc_kernel(TransformArgs a) {
   else a.status[i] = st;
 }
 
+__global__ __launch_bounds__(256) void transform_desc_kernel(TransformArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.m || gated_off(a.gate, a.gate_when)) return;
+  transform_describe(a, i, a.status[i]);
+}
+
 // Packed placement: message i goes to start[i] (exclusive scan of out_len), if it fits.
 __global__ __launch_bounds__(256) void transform_place_kernel(TransformArgs a, const uint64_t* __restrict__ start) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -481,15 +490,27 @@ __global__ __launch_bounds__(256) void transform_finish_kernel(TransformArgs a) 
     atomicOr(a.fail, 1u);
     return;
   }
-  const uint8_t* src = a.region + d.key_src;
-  uint8_t* dst = a.out + d.out_off + (d.header_version == 1 ? 34u : d.header_version == 2 ? 38u : 40u);
-  uint32_t b = 0;
-  for (; b + 8 <= d.key_len; b += 8) {  // 8-B moves at any alignment (unaligned global access)
-    uint64_t v;
-    __builtin_memcpy(&v, src + b, 8);
-    __builtin_memcpy(dst + b, &v, 8);
+  const uint8_t* __restrict__ src = a.region + d.key_src;
+  uint8_t* __restrict__ dst = a.out + d.out_off + (d.header_version == 1 ? 34u : d.header_version == 2 ? 38u : 40u);
+  const uint32_t n = d.key_len;
+  if (n < 8) {
+    uint8_t t[8];
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) t[j] = j < n ? src[j] : 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j)
+      if (j < n) dst[j] = t[j];
+    return;
   }
-  for (; b < d.key_len; ++b) dst[b] = src[b];
+  // 8-B moves at any alignment (unaligned global access), four loads in flight before their
+  // stores; the last piece is [n - 8, n), overlapping the one before (one round trip per 32 B)
+  for (uint32_t b0 = 0; b0 < n; b0 += 32) {
+    uint64_t v[4];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) __builtin_memcpy(&v[u], src + min(b0 + 8 * u, n - 8), 8);
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) __builtin_memcpy(dst + min(b0 + 8 * u, n - 8), &v[u], 8);
+  }
 }
 
 // No fallback: the final status is the verify's bits, or else the transform's own.
@@ -543,7 +564,15 @@ hipError_t launch_trailer_verify(const TrailerArgs& a, hipStream_t s) {
 
 hipError_t launch_msg_parse(const MsgArgs& a, hipStream_t s) {
   if (a.m == 0) return hipSuccess;
-  hipLaunchKernelGGL(msg_parse_kernel, dim3((uint32_t)((a.m + 255) / 256)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(msg_parse_kernel<false>, dim3((uint32_t)((a.m + 255) / 256)), dim3(256), 0, s, a,
+                     TransformArgs{});
+  return hipGetLastError();
+}
+
+hipError_t launch_msg_parse_desc(const MsgArgs& a, const TransformArgs& t, hipStream_t s) {
+  if (a.m == 0) return hipSuccess;
+  if (t.m != a.m || t.region != a.region || t.msg_off != a.msg_off) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(msg_parse_kernel<true>, dim3((uint32_t)((a.m + 255) / 256)), dim3(256), 0, s, a, t);
   return hipGetLastError();
 }
 
