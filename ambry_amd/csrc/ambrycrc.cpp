@@ -302,6 +302,7 @@ int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uin
                   const uint64_t* copy_off) {
   if (n == 0) return AMBRYCRC_OK;
   PlanArgs p;
+  p.gate = nullptr;
   p.off = off;
   p.len = len;
   p.crc_in = crc_in;

@@ -76,6 +76,7 @@ int enqueue_serialize(DevCtx* c, const ::ambrycrc_put_desc* d_desc, size_t m, co
     // cost offsets of the copy jobs: the plan kernel's exclusive scan (no small-chunk classes);
     // its per-chunk output initialisation lands in `crc`, overwritten by the CRC batch below
     PlanArgs p;
+    p.gate = gate;  // the transform's fallback pass: only when a placed message failed
     p.off = a.cp_dst;
     p.len = a.cp_cost;
     p.crc_in = nullptr;
@@ -212,6 +213,7 @@ int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len
   void* shared = plan_ws + ws_need(m);
   // packed output offsets: the plan kernel's exclusive scan of the output lengths
   PlanArgs p;
+  p.gate = nullptr;
   p.off = d_msg_off;
   p.len = d_out_len;
   p.crc_in = nullptr;
@@ -255,6 +257,7 @@ int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len
   // verify status, packed placement, layout and a gather copy of the fields from the region.
   t.xstatus = nullptr;
   t.gate_when = 1;
+  p.gate = fail;
   if (launch_transform_desc(t, stream) != hipSuccess) return AMBRYCRC_EHIP;
   if (launch_plan(p, stream) != hipSuccess) return AMBRYCRC_EHIP;
   if (launch_transform_place(t, p.byte_start, stream) != hipSuccess) return AMBRYCRC_EHIP;

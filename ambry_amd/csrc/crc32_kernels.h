@@ -23,6 +23,7 @@ struct PlanArgs {
   uint32_t* small_idx;     // [n] their indices, grouped by size class, ascending within a class
   uint32_t* crc_stage;     // [n] copy of crc_in (null iff crc_in is): read before out[] is written,
                            // so out may alias crc_in; the CRC kernels read this copy
+  const uint32_t* gate;    // run only when *gate != 0 (null: always): the transform's fallback pass
 };
 
 constexpr uint32_t kPlanPerBlock = 2048;  // chunks per planning workgroup

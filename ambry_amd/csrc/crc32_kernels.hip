@@ -1285,6 +1285,7 @@ __device__ __forceinline__ uint32_t plan_span(uint32_t n, uint32_t base) {
 }
 
 __global__ __launch_bounds__(256) void crc32_plan_count_kernel(PlanArgs a) {
+  if (a.gate && *a.gate == 0) return;
   const uint32_t base = blockIdx.x * kPlanPerBlock;
   uint64_t len[kPlanPerBlock / 256];  // every round's load in flight before the first use
 #pragma unroll
@@ -1306,6 +1307,7 @@ __global__ __launch_bounds__(256) void crc32_plan_count_kernel(PlanArgs a) {
 }
 
 __global__ __launch_bounds__(256) void crc32_plan_scan_kernel(PlanArgs a) {
+  if (a.gate && *a.gate == 0) return;
   const uint32_t nblocks = gridDim.x;
   const uint32_t base = blockIdx.x * kPlanPerBlock;
   const uint32_t span = plan_span(a.n, base);
