@@ -156,6 +156,25 @@ def test_small_chunk_group_kernel(gpu, oracle, variant, grid):
     assert np.array_equal(got, oracle.batch(mem, off, ln, crc_in=cin, threads=8))
 
 
+def test_class0_small_records(gpu, oracle):
+    """Group class 0 (<= 256 B, 2-lane groups, 32 chunks per round): every length 1..256 at every
+    offset mod 16 with and without a seed, a batch whose class-0 count is not a multiple of 32
+    (idle groups in a wave's last round), and chunks ending at the buffer's last byte."""
+    rng = np.random.default_rng(4242)
+    size = 4 << 20
+    mem = stream_bytes(77, 0, size)
+    n = 16384 + 4133  # >= kGroupMinChunks; odd count
+    ln = rng.integers(1, 257, size=n)
+    ln[:256] = np.arange(1, 257)
+    off = rng.integers(0, size - 256, size=n)
+    off[:256] = (np.arange(256) * 4099) % (size - 256)  # all 16 alignments
+    off[256:512] = size - ln[256:512]  # ends at the last byte
+    cin = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32)
+    cin[1::2] = 0
+    got = run_batch(gpu, mem, off, ln, crc_in=cin)
+    assert np.array_equal(got, oracle.batch(mem, off, ln, crc_in=cin, threads=8))
+
+
 def test_crc_in_streaming_composition(gpu, oracle):
     """update(A) then update(B) == update(A||B): PutOperation's slice-by-slice fill (PutOperation.java:1700-1703)."""
     torch = _torch()
