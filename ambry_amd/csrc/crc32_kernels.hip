@@ -1313,27 +1313,40 @@ __global__ __launch_bounds__(256) void crc32_plan_scan_kernel(PlanArgs a) {
   const uint32_t span = plan_span(a.n, base);
   constexpr uint32_t R = kPlanPerBlock / 256;
   uint64_t len[R];  // every round's load in flight before the first scan
+  uint32_t cin[R];
 #pragma unroll
-  for (uint32_t r = 0; r < R; ++r) {
+  for (uint32_t r = 0; r < R; ++r) {  // clamped index: unconditional loads, masked after
     const uint32_t c = base + r * 256 + threadIdx.x;
-    len[r] = (r * 256 < span && c < a.n) ? a.len[c] : 0u;
+    const uint32_t cc = c < a.n ? c : a.n - 1;
+    const uint64_t v = a.len[cc];
+    cin[r] = a.crc_in ? a.crc_in[cc] : 0u;  // read before out[c] is written (out may alias crc_in)
+    len[r] = (r * 256 < span && c < a.n) ? v : 0u;
   }
   // One 9-value block reduction: the byte carry of earlier blocks, and per class the
   // chunks of earlier blocks (carry) and of all blocks (total).
   // cls[0] = byte carry, cls[1..4] = class carries, cls[5..8] = class totals
   uint64_t red[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, tot[9];
   if (nblocks > 1) {
-#pragma unroll 4
-    for (uint32_t i = threadIdx.x; i < nblocks; i += 256) {
-      const bool earlier = i < blockIdx.x;
-      if (earlier) red[0] += a.block_sum[i];
-      if (a.small_max) {
-        const uint64_t v = a.block_small[i];
+    // four entries per thread per pass, every load issued (clamped index) before any is used
+    for (uint32_t i0 = threadIdx.x; i0 < nblocks; i0 += 1024) {
+      uint64_t bs[4], bm[4];
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u) {
+        const uint32_t i = i0 + 256 * u;
+        const uint32_t ic = i < nblocks ? i : 0u;
+        bs[u] = a.block_sum[ic];
+        bm[u] = a.small_max ? a.block_small[ic] : 0u;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u) {
+        const uint32_t i = i0 + 256 * u;
+        const bool in = i < nblocks, earlier = i < blockIdx.x;  // earlier implies in
+        red[0] += earlier ? bs[u] : 0u;
 #pragma unroll
         for (uint32_t c = 0; c < 4; ++c) {
-          const uint64_t f = field16(v, c);
-          red[5 + c] += f;
-          if (earlier) red[1 + c] += f;
+          const uint64_t f = field16(bm[u], c);
+          red[5 + c] += in ? f : 0u;
+          red[1 + c] += earlier ? f : 0u;
         }
       }
     }
@@ -1392,9 +1405,8 @@ __global__ __launch_bounds__(256) void crc32_plan_scan_kernel(PlanArgs a) {
     if (c < a.n) {
       const uint64_t incl = carry + bs + incl_s[r];
       a.byte_start[c] = incl - sl;
-      const uint32_t cin = a.crc_in ? a.crc_in[c] : 0u;  // read before out[c] (may alias crc_in[c])
-      if (a.crc_stage) a.crc_stage[c] = cin;
-      a.out[c] = ln ? 0u : cin;
+      if (a.crc_stage) a.crc_stage[c] = cin[r];
+      a.out[c] = ln ? 0u : cin[r];
       if (oh) {
         const uint32_t k = small_class(ln);
         a.small_idx[cls_base[k] + cls_carry[k] + field16(bc + incl_c[r], k) - 1] = c;
