@@ -1636,6 +1636,19 @@ __global__ __launch_bounds__(1024) void readbw_group_kernel(const uint8_t* __res
   out[blockIdx.x * blockDim.x + threadIdx.x] = x;
 }
 
+// Grid-stride copy over many small blocks (the guide's float4-copy shape): variant 49 plain
+// stores, 50 nontemporal stores.
+template <bool NTS>
+__global__ __launch_bounds__(256) void copybw_gridstride_kernel(const u32x4* __restrict__ src, uint64_t n16,
+                                                               uint8_t* __restrict__ dst) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) {
+    const u32x4 v = ld16<true>(src + i);
+    if constexpr (NTS) st16u_nt(dst + 16 * i, v);
+    else st16u(dst + 16 * i, v);
+  }
+}
+
 // Contiguous copy: each wave copies an equal contiguous share of [0, n16) 16-B pieces, four per
 // lane in flight (the plain copy roof of launch_readbw variant 48).
 __global__ __launch_bounds__(1024) void copybw_stream_kernel(const u32x4* __restrict__ src, uint64_t n16,
@@ -1659,12 +1672,21 @@ hipError_t launch_readbw(const uint8_t* base, uint64_t nbytes, uint32_t* out, in
   if (variant >= 32) {  // copy probes: read [0, nbytes/2), write from nbytes/2 (+ 11 B for 40..44)
     const uint64_t half = nbytes / 2 - 4096;
     uint8_t* dst = const_cast<uint8_t*>(base) + nbytes / 2 + (variant >= 40 && variant < 48 ? 11 : 0);
+    if (variant == 49 || variant == 50) {
+      if (variant == 49)
+        hipLaunchKernelGGL(copybw_gridstride_kernel<false>, dim3(grid * 32), dim3(256), 0, s,
+                           reinterpret_cast<const u32x4*>(base), half / 16, dst);
+      else
+        hipLaunchKernelGGL(copybw_gridstride_kernel<true>, dim3(grid * 32), dim3(256), 0, s,
+                           reinterpret_cast<const u32x4*>(base), half / 16, dst);
+      return hipGetLastError();
+    }
     if (variant == 48) {
       hipLaunchKernelGGL(copybw_stream_kernel, dim3(grid), dim3(1024), 0, s, reinterpret_cast<const u32x4*>(base),
                          half / 16, dst);
       return hipGetLastError();
     }
-    if (variant > 44) return hipErrorInvalidValue;
+    if (variant > 44) return hipErrorInvalidValue;  // 45..47, 51+: none
     const uint32_t chunk = 1024u << ((variant - 32) & 7);
     hipLaunchKernelGGL((readbw_group_kernel<16, true>), dim3(grid), dim3(1024), 0, s, base, half, chunk, out, dst);
     return hipGetLastError();

@@ -27,7 +27,7 @@ def main():
     buf = torch.zeros(nbytes, dtype=torch.uint8, device="cuda")
     scratch = torch.zeros(256 * 1024 * 4, dtype=torch.int32, device="cuda")
     moved = 2 * (nbytes // 2 - 4096)
-    for v, name in [(48, "contiguous"), (32, "group 1 KiB"), (34, "group 4 KiB"), (36, "group 16 KiB"),
+    for v, name in [(49, "grid-stride"), (50, "grid-stride, nt stores"), (48, "contiguous"), (32, "group 1 KiB"), (34, "group 4 KiB"), (36, "group 16 KiB"),
                     (42, "group 4 KiB, dst +11 B")]:
         s = torch.cuda.current_stream()
         times = []
