@@ -26,7 +26,12 @@ struct PlanArgs {
   const uint32_t* gate;    // run only when *gate != 0 (null: always): the transform's fallback pass
 };
 
-constexpr uint32_t kPlanPerBlock = 2048;  // chunks per planning workgroup
+#ifndef AMBRY_PLAN_PER_BLOCK
+#define AMBRY_PLAN_PER_BLOCK 2048
+#endif
+// chunks per planning workgroup (a multiple of 256, <= 65535 so per-block class counts fit 16 bits)
+constexpr uint32_t kPlanPerBlock = AMBRY_PLAN_PER_BLOCK;
+static_assert(kPlanPerBlock % 256 == 0 && kPlanPerBlock <= 65535, "plan block size");
 constexpr uint64_t kShareQuantum = 1024;  // per-wave byte shares are multiples of this
 constexpr uint64_t kMinShare = 16384;     // ... and at least this (see crc32_sweep_kernel)
 

@@ -1212,7 +1212,7 @@ __global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
 // ------------------------------------------------------------------ planning
 // byte_start = exclusive scan of len (64-bit), in two small launches: count (per-block
 // sums) and scan (block-local scans + carry of earlier blocks). Blocks of 256 threads
-// own kPlanPerBlock consecutive chunks, visited in rounds of 256 (coalesced). The scan
+// own kPlanPerBlock consecutive chunks, loaded in rounds of 256 (coalesced). The scan
 // also initialises out[]: 0 for chunks the sweep will XOR into, crc_in (the CRC of
 // nothing continued from crc_in) for empty chunks.
 // Inclusive wave scan of a 64-bit value with DPP: row_shr 1/2/4/8 inside 16-lane rows,
@@ -1271,18 +1271,11 @@ __device__ __forceinline__ bool is_small(uint64_t len, uint64_t small_max) { ret
 __device__ __forceinline__ uint32_t small_class(uint64_t len) {
   return len <= 256 ? 0u : len <= 1024 ? 1u : len <= 4096 ? 2u : 3u;
 }
-// Per-chunk class indicator packed as 16-bit fields (a plan block has <= 2048 chunks).
+// Per-chunk class indicator packed as 16-bit fields (a plan block has <= kPlanPerBlock <= 65535 chunks).
 __device__ __forceinline__ uint64_t class_onehot(uint64_t len, uint64_t small_max) {
   return is_small(len, small_max) ? (1ull << (16 * small_class(len))) : 0ull;
 }
 __device__ __forceinline__ uint64_t field16(uint64_t v, uint32_t c) { return (v >> (16 * c)) & 0xFFFFu; }
-
-// Chunks of plan block `base` rounded up to whole 256-chunk rounds: the last block (and a
-// one-block batch) stops at n instead of running all kPlanPerBlock / 256 scan rounds.
-__device__ __forceinline__ uint32_t plan_span(uint32_t n, uint32_t base) {
-  const uint32_t left = n - base;
-  return left < kPlanPerBlock ? (left + 255u) & ~255u : kPlanPerBlock;
-}
 
 __global__ __launch_bounds__(256) void crc32_plan_count_kernel(PlanArgs a) {
   if (a.gate && *a.gate == 0) return;
@@ -1306,29 +1299,57 @@ __global__ __launch_bounds__(256) void crc32_plan_count_kernel(PlanArgs a) {
   }
 }
 
-__global__ __launch_bounds__(256) void crc32_plan_scan_kernel(PlanArgs a) {
+// Scan: a thread owns R = kPlanPerBlock / 256 consecutive chunks. Lengths arrive in coalesced
+// rounds of 256 (with crc_in; out[] is initialised right there, it needs no scan), are transposed
+// through LDS (runs padded to R + 1 words: conflict-free strided reads), summed serially per
+// thread and scanned once across the block; byte_start goes back through the same LDS slots to
+// coalesced stores. One block scan per block instead of two wave scans per round: ~60 VGPRs
+// (8 waves per SIMD) against 164 (3 waves) for the round-by-round form.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void crc32_plan_scan_kernel(PlanArgs a) {
   if (a.gate && *a.gate == 0) return;
+  constexpr uint32_t R = kPlanPerBlock / 256;
+  constexpr uint32_t P = R + 1;
+  __shared__ uint64_t lds[256 * P];
   const uint32_t nblocks = gridDim.x;
   const uint32_t base = blockIdx.x * kPlanPerBlock;
-  const uint32_t span = plan_span(a.n, base);
-  constexpr uint32_t R = kPlanPerBlock / 256;
-  uint64_t len[R];  // every round's load in flight before the first scan
-  uint32_t cin[R];
+  const uint32_t tid = threadIdx.x;
+  {
+    uint64_t len[R];  // every round's load in flight before the first use (clamped index)
+    uint32_t cin[R];
 #pragma unroll
-  for (uint32_t r = 0; r < R; ++r) {  // clamped index: unconditional loads, masked after
-    const uint32_t c = base + r * 256 + threadIdx.x;
-    const uint32_t cc = c < a.n ? c : a.n - 1;
-    const uint64_t v = a.len[cc];
-    cin[r] = a.crc_in ? a.crc_in[cc] : 0u;  // read before out[c] is written (out may alias crc_in)
-    len[r] = (r * 256 < span && c < a.n) ? v : 0u;
+    for (uint32_t r = 0; r < R; ++r) {
+      const uint32_t c = base + r * 256 + tid;
+      const uint32_t cc = c < a.n ? c : a.n - 1;
+      len[r] = a.len[cc];
+      cin[r] = a.crc_in ? a.crc_in[cc] : 0u;  // read before out[c] is written (out may alias crc_in)
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < R; ++r) {
+      const uint32_t i = r * 256 + tid, c = base + i;
+      const bool in = c < a.n;
+      lds[(i / R) * P + i % R] = in ? len[r] : 0u;  // chunks past n: length 0 (no share, no class)
+      if (in) {
+        if (a.crc_stage) a.crc_stage[c] = cin[r];
+        a.out[c] = len[r] ? 0u : cin[r];
+      }
+    }
   }
-  // One 9-value block reduction: the byte carry of earlier blocks, and per class the
-  // chunks of earlier blocks (carry) and of all blocks (total).
-  // cls[0] = byte carry, cls[1..4] = class carries, cls[5..8] = class totals
-  uint64_t red[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, tot[9];
+  __syncthreads();
+  uint64_t tsum = 0, tcls = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < R; ++j) {
+    const uint64_t ln = lds[tid * P + j];
+    tsum += share_len(ln, a.small_max);
+    tcls += class_onehot(ln, a.small_max);
+  }
+  // One 7-value block scan: v[0] = byte carry of earlier blocks; v[1], v[2] class counts of earlier
+  // blocks and v[3], v[4] of all blocks, two 32-bit fields each (classes 0|1, 2|3; their totals are
+  // what is used); v[5] / v[6] this thread's bytes / packed 16-bit class counts (their prefixes
+  // place the thread's run).
+  uint64_t v[7] = {0, 0, 0, 0, 0, 0, 0}, tot[7];
   if (nblocks > 1) {
     // four entries per thread per pass, every load issued (clamped index) before any is used
-    for (uint32_t i0 = threadIdx.x; i0 < nblocks; i0 += 1024) {
+    for (uint32_t i0 = tid; i0 < nblocks; i0 += 1024) {
       uint64_t bs[4], bm[4];
 #pragma unroll
       for (uint32_t u = 0; u < 4; ++u) {
@@ -1341,83 +1362,59 @@ __global__ __launch_bounds__(256) void crc32_plan_scan_kernel(PlanArgs a) {
       for (uint32_t u = 0; u < 4; ++u) {
         const uint32_t i = i0 + 256 * u;
         const bool in = i < nblocks, earlier = i < blockIdx.x;  // earlier implies in
-        red[0] += earlier ? bs[u] : 0u;
-#pragma unroll
-        for (uint32_t c = 0; c < 4; ++c) {
-          const uint64_t f = field16(bm[u], c);
-          red[5 + c] += in ? f : 0u;
-          red[1 + c] += earlier ? f : 0u;
-        }
+        const uint64_t lo = field16(bm[u], 0) | (field16(bm[u], 1) << 32);
+        const uint64_t hi = field16(bm[u], 2) | (field16(bm[u], 3) << 32);
+        v[0] += earlier ? bs[u] : 0u;
+        v[1] += earlier ? lo : 0u;
+        v[2] += earlier ? hi : 0u;
+        v[3] += in ? lo : 0u;
+        v[4] += in ? hi : 0u;
       }
     }
-  } else if (a.small_max) {  // no count launch: count this (only) block here
-    uint64_t cls = 0;
-#pragma unroll
-    for (uint32_t r = 0; r < R; ++r) cls += class_onehot(len[r], a.small_max);
-#pragma unroll
-    for (uint32_t c = 0; c < 4; ++c) red[5 + c] = field16(cls, c);
   }
-  block_scan256<9>(red, tot);
-  uint64_t carry = tot[0];
-  uint64_t cls_carry[4] = {tot[1], tot[2], tot[3], tot[4]};
-  const uint64_t cls_total[4] = {tot[5], tot[6], tot[7], tot[8]};
-  // class c's list entries start at base[c] = chunks of classes < c; this block's at base[c] + earlier[c]
+  v[5] = tsum;
+  v[6] = tcls;
+  block_scan256<7>(v, tot);
+  uint64_t cls_total[4], cls_carry[4];
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k) {
+    const uint32_t sh = 32 * (k & 1);
+    cls_total[k] = nblocks > 1 ? (tot[3 + (k >> 1)] >> sh) & 0xFFFFFFFFu : field16(tot[6], k);  // one block: its own
+    cls_carry[k] = nblocks > 1 ? (tot[1 + (k >> 1)] >> sh) & 0xFFFFFFFFu : 0u;
+  }
+  // class c's list entries start at base[c] = chunks of classes < c
   uint64_t cls_base[4];
   cls_base[0] = 0;
   cls_base[1] = cls_total[0];
   cls_base[2] = cls_base[1] + cls_total[1];
   cls_base[3] = cls_base[2] + cls_total[2];
-  // Rounds of 256 chunks: wave scans (DPP, no barrier) per round, then one barrier and each
-  // wave adds the totals of the waves before it -- earlier rounds, and earlier waves of its
-  // own round -- from LDS. Class counts stay packed (<= 256 per class per round: 16 bits).
-  __shared__ uint64_t wtot[R][4][2];
-  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  uint64_t incl_s[R], incl_c[R];
+  const uint64_t before_cls = v[6] - tcls;  // earlier threads of this block, packed
+  uint64_t pos[4];
 #pragma unroll
-  for (uint32_t r = 0; r < R; ++r) {
-    const uint32_t c = base + r * 256 + threadIdx.x;
-    incl_s[r] = wave_scan64(share_len(len[r], a.small_max));
-    incl_c[r] = wave_scan64(c < a.n ? class_onehot(len[r], a.small_max) : 0ull);
-    if (lane == 63) {
-      wtot[r][wv][0] = incl_s[r];
-      wtot[r][wv][1] = incl_c[r];
+  for (uint32_t k = 0; k < 4; ++k) pos[k] = cls_base[k] + cls_carry[k] + field16(before_cls, k);
+  uint64_t b = tot[0] + v[5] - tsum;  // bytes of earlier blocks and of earlier threads
+#pragma unroll
+  for (uint32_t j = 0; j < R; ++j) {
+    const uint64_t ln = lds[tid * P + j];  // the thread's own slots: read, then reused for byte_start
+    const uint32_t c = base + tid * R + j;
+    lds[tid * P + j] = b;
+    b += share_len(ln, a.small_max);
+    if (is_small(ln, a.small_max)) {  // implies c < n (lengths past n are 0)
+      const uint32_t k = small_class(ln);
+      const uint64_t p = k == 0 ? pos[0] : k == 1 ? pos[1] : k == 2 ? pos[2] : pos[3];
+      a.small_idx[p] = c;
+#pragma unroll
+      for (uint32_t q = 0; q < 4; ++q) pos[q] += q == k ? 1u : 0u;
     }
+    if (c == a.n - 1) a.byte_start[a.n] = b;
   }
   __syncthreads();
 #pragma unroll
   for (uint32_t r = 0; r < R; ++r) {
-    if (r * 256 >= span) break;
-    const uint32_t c = base + r * 256 + threadIdx.x;
-    const uint64_t ln = len[r];
-    const uint64_t sl = share_len(ln, a.small_max);
-    const uint64_t oh = c < a.n ? class_onehot(ln, a.small_max) : 0ull;
-    uint64_t bs = 0, bc = 0, rs = 0, rc = 0;  // earlier waves of this round; whole round
-#pragma unroll
-    for (uint32_t w = 0; w < 4; ++w) {
-      const uint64_t ts = wtot[r][w][0], tc = wtot[r][w][1];
-      if (w < wv) {
-        bs += ts;
-        bc += tc;
-      }
-      rs += ts;
-      rc += tc;
-    }
-    if (c < a.n) {
-      const uint64_t incl = carry + bs + incl_s[r];
-      a.byte_start[c] = incl - sl;
-      if (a.crc_stage) a.crc_stage[c] = cin[r];
-      a.out[c] = ln ? 0u : cin[r];
-      if (oh) {
-        const uint32_t k = small_class(ln);
-        a.small_idx[cls_base[k] + cls_carry[k] + field16(bc + incl_c[r], k) - 1] = c;
-      }
-      if (c == a.n - 1) a.byte_start[a.n] = incl;
-    }
-    carry += rs;
-#pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) cls_carry[k] += field16(rc, k);
+    const uint32_t i = r * 256 + tid, c = base + i;
+    if (c < a.n) a.byte_start[c] = lds[(i / R) * P + i % R];
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  if (blockIdx.x == 0 && tid == 0) {
     a.small_total[4] = 0;
     a.small_total[0] = cls_base[3] + cls_total[3];
     a.small_total[1] = cls_base[1];

@@ -175,6 +175,31 @@ def test_class0_small_records(gpu, oracle):
     assert np.array_equal(got, oracle.batch(mem, off, ln, crc_in=cin, threads=8))
 
 
+@pytest.mark.parametrize("n", [2048 * 1024 + 777, 2048 * 3 + 1])
+def test_plan_many_blocks(gpu, oracle, n):
+    """The plan's scan across planning blocks (2048 chunks each): more blocks than one pass of the
+    block-sum loop covers (1024), every size class in every block, empty chunks, seeds, in place."""
+    torch = _torch()
+    rng = np.random.default_rng(n)
+    size = 64 << 20
+    mem = stream_bytes(78, 0, size)
+    ln = rng.integers(0, 600, size=n)
+    mid = rng.random(n) < 0.02
+    ln[mid] = rng.integers(600, 20000, size=int(mid.sum()))
+    big = rng.random(n) < 0.001
+    ln[big] = rng.integers(20000, 1 << 20, size=int(big.sum()))
+    ln[rng.random(n) < 0.05] = 0
+    off = rng.integers(0, size - (1 << 20), size=n)
+    cin = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32)
+    expect = oracle.batch(mem, off, ln, crc_in=cin, threads=8)
+    assert np.array_equal(run_batch(gpu, mem, off, ln, crc_in=cin), expect)
+    base = dev_bytes(mem)
+    io = torch.from_numpy(cin.view(np.int32).copy()).cuda()
+    gpu.crc32_batch(base, dev_u64(off), dev_u64(ln), crc_in=io, out=io)  # in place
+    torch.cuda.synchronize()
+    assert np.array_equal(host_u32(io), expect)
+
+
 def test_crc_in_streaming_composition(gpu, oracle):
     """update(A) then update(B) == update(A||B): PutOperation's slice-by-slice fill (PutOperation.java:1700-1703)."""
     torch = _torch()
