@@ -15,7 +15,8 @@ struct PlanArgs {
   uint32_t n;
   uint64_t* byte_start;    // [n+1] exclusive scan of len; [n] = total bytes
   uint64_t* block_sum;     // [ceil(n / kPlanPerBlock)] scratch
-  uint32_t* out;           // [n] initialised here, XOR-accumulated by the sweep kernel
+  uint32_t* out;           // [n] initialised here, XOR-accumulated by the sweep kernel (small chunks:
+                           // stored whole by the group phase, not initialised here)
   uint64_t small_max;      // chunks with 0 < len <= small_max go to the group kernel (0: none)
   uint64_t* block_small;   // [ceil(n / kPlanPerBlock)] scratch: 4 x 16-bit size-class counts
   uint64_t* small_total;   // [5] number of small chunks; start of size classes 1..3 in small_idx;

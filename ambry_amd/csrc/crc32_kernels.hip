@@ -1214,7 +1214,8 @@ __global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
 // sums) and scan (block-local scans + carry of earlier blocks). Blocks of 256 threads
 // own kPlanPerBlock consecutive chunks, loaded in rounds of 256 (coalesced). The scan
 // also initialises out[]: 0 for chunks the sweep will XOR into, crc_in (the CRC of
-// nothing continued from crc_in) for empty chunks.
+// nothing continued from crc_in) for empty chunks; chunks the group phase takes whole
+// (small) are left alone, it stores their CRC.
 // Inclusive wave scan of a 64-bit value with DPP: row_shr 1/2/4/8 inside 16-lane rows,
 // then row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3). VALU only -- a __shfl_up
 // ladder is 12 dependent ds_bpermute round trips per 64-bit scan.
@@ -1305,7 +1306,7 @@ __global__ __launch_bounds__(256) void crc32_plan_count_kernel(PlanArgs a) {
 // thread and scanned once across the block; byte_start goes back through the same LDS slots to
 // coalesced stores. One block scan per block instead of two wave scans per round: ~60 VGPRs
 // (8 waves per SIMD) against 164 (3 waves) for the round-by-round form.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void crc32_plan_scan_kernel(PlanArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void crc32_plan_scan_kernel(PlanArgs a) {
   if (a.gate && *a.gate == 0) return;
   constexpr uint32_t R = kPlanPerBlock / 256;
   constexpr uint32_t P = R + 1;
@@ -1330,7 +1331,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void c
       lds[(i / R) * P + i % R] = in ? len[r] : 0u;  // chunks past n: length 0 (no share, no class)
       if (in) {
         if (a.crc_stage) a.crc_stage[c] = cin[r];
-        a.out[c] = len[r] ? 0u : cin[r];
+        // small chunks: the group phase stores their CRC whole (no XOR into out), so no init
+        if (!is_small(len[r], a.small_max)) a.out[c] = len[r] ? 0u : cin[r];
       }
     }
   }
@@ -1347,6 +1349,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void c
   // what is used); v[5] / v[6] this thread's bytes / packed 16-bit class counts (their prefixes
   // place the thread's run).
   uint64_t v[7] = {0, 0, 0, 0, 0, 0, 0}, tot[7];
+  int any_share = 0;  // some block has share bytes
   if (nblocks > 1) {
     // four entries per thread per pass, every load issued (clamped index) before any is used
     for (uint32_t i0 = tid; i0 < nblocks; i0 += 1024) {
@@ -1369,6 +1372,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void c
         v[2] += earlier ? hi : 0u;
         v[3] += in ? lo : 0u;
         v[4] += in ? hi : 0u;
+        any_share |= in && bs[u] != 0;
       }
     }
   }
@@ -1408,11 +1412,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void c
     }
     if (c == a.n - 1) a.byte_start[a.n] = b;
   }
+  // A batch the group phase takes whole (no share bytes at all): the sweep reads byte_start[n]
+  // (total 0) and nothing below it, so the per-chunk starts are not stored -- 8 of the 20 B per
+  // chunk this kernel moves for small records. (small_max == 0: byte_start is a plain scan that
+  // the PUT and transform paths read.)
+  const bool store_starts = a.small_max == 0 || (nblocks > 1 ? __syncthreads_or(any_share) != 0 : tot[5] != 0);
   __syncthreads();
+  if (store_starts) {
 #pragma unroll
-  for (uint32_t r = 0; r < R; ++r) {
-    const uint32_t i = r * 256 + tid, c = base + i;
-    if (c < a.n) a.byte_start[c] = lds[(i / R) * P + i % R];
+    for (uint32_t r = 0; r < R; ++r) {
+      const uint32_t i = r * 256 + tid, c = base + i;
+      if (c < a.n) a.byte_start[c] = lds[(i / R) * P + i % R];
+    }
   }
   if (blockIdx.x == 0 && tid == 0) {
     a.small_total[4] = 0;
