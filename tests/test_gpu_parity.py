@@ -200,6 +200,31 @@ def test_plan_many_blocks(gpu, oracle, n):
     assert np.array_equal(host_u32(io), expect)
 
 
+@pytest.mark.parametrize("with_large", [False, True])
+def test_all_small_batch_garbage_workspace(gpu, oracle, with_large):
+    """A batch the group phase takes whole stores no per-chunk byte_start and leaves its chunks'
+    out[] words to the group phase: a workspace and an out buffer full of garbage must not leak
+    into the CRCs. with_large: one 1 MiB chunk, so the batch has share bytes and the starts are stored."""
+    torch = _torch()
+    rng = np.random.default_rng(808 + with_large)
+    size = 16 << 20
+    mem = stream_bytes(79, 0, size)
+    n = 20000
+    ln = rng.integers(0, 16385, size=n)
+    ln[::7] = 0
+    ln[:300] = rng.integers(1, 257, size=300)
+    if with_large:
+        ln[n // 2] = 1 << 20
+    off = rng.integers(0, size - (1 << 20), size=n)
+    cin = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32)
+    ws = torch.full((gpu.workspace_bytes(n),), 0xA5, dtype=torch.uint8, device="cuda")
+    out = torch.full((n,), -0x5A5A5A5B, dtype=torch.int32, device="cuda")
+    c_in = torch.from_numpy(cin.view(np.int32).copy()).cuda()
+    gpu.crc32_batch(dev_bytes(mem), dev_u64(off), dev_u64(ln), crc_in=c_in, out=out, workspace=ws)
+    torch.cuda.synchronize()
+    assert np.array_equal(host_u32(out), oracle.batch(mem, off, ln, crc_in=cin, threads=8))
+
+
 def test_crc_in_streaming_composition(gpu, oracle):
     """update(A) then update(B) == update(A||B): PutOperation's slice-by-slice fill (PutOperation.java:1700-1703)."""
     torch = _torch()
