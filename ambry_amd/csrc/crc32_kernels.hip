@@ -948,20 +948,16 @@ __device__ __forceinline__ void group_class(const SweepArgs& a, uint64_t lo, uin
   if (i0 >= hi) return;
   const uint64_t i1 = i0 + per < hi ? i0 + per : hi;
   const uint32_t gi = lane / G;
-  // list entries a round ahead (one VGPR); every list and descriptor load unconditional (clamped
-  // index, masked after), so no load sits under a lane-divergent branch
-  uint32_t ci_next = a.small_idx[i0 + gi < i1 ? i0 + gi : i0];
 #pragma unroll 1
   for (uint64_t i = i0; i < i1; i += S) {
     const bool act = i + gi < i1;
-    const uint32_t ci = ci_next;
-    ci_next = a.small_idx[i + S + gi < i1 ? i + S + gi : i0];
-    uint64_t len = a.len[ci], off = a.off[ci];
-    uint32_t cin = a.crc_in ? a.crc_in[ci] : 0u;
-    if (!act) {
-      len = 0;
-      off = 0;
-      cin = 0;
+    const uint32_t ci = act ? a.small_idx[i + gi] : 0u;
+    uint64_t len = 0, off = 0;
+    uint32_t cin = 0;
+    if (act) {
+      len = a.len[ci];
+      off = a.off[ci];
+      cin = a.crc_in ? a.crc_in[ci] : 0u;
     }
     const uint64_t cb = aligned_end(off, off + len);
     constexpr uint32_t BLK = 16 * G;  // bytes per chain step
