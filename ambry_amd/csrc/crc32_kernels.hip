@@ -1304,8 +1304,8 @@ __global__ __launch_bounds__(256) void crc32_plan_count_kernel(PlanArgs a) {
 // rounds of 256 (with crc_in; out[] is initialised right there, it needs no scan), are transposed
 // through LDS (runs padded to R + 1 words: conflict-free strided reads), summed serially per
 // thread and scanned once across the block; byte_start goes back through the same LDS slots to
-// coalesced stores. One block scan per block instead of two wave scans per round: ~60 VGPRs
-// (8 waves per SIMD) against 164 (3 waves) for the round-by-round form.
+// coalesced stores. One block scan per block instead of two wave scans per round: 94 VGPRs
+// (5 waves per SIMD) against 164 (3 waves) for the round-by-round form.
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void crc32_plan_scan_kernel(PlanArgs a) {
   if (a.gate && *a.gate == 0) return;
   constexpr uint32_t R = kPlanPerBlock / 256;
