@@ -106,6 +106,11 @@ _SIGNATURES = [
       ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t, ctypes.c_int]),
     ("ambrycrc_shard_by_bytes", ctypes.c_int,
      [ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]),
+    ("ambrycrc_gather_layout", ctypes.c_int,
+     [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int),
+      ctypes.POINTER(ctypes.c_uint64)]),
+    ("ambrycrc_gather_compact_host", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int, ctypes.c_void_p]),
     ("ambrycrc_unique_id", ctypes.c_int, [ctypes.POINTER(ctypes.c_uint8)]),
     ("ambrycrc_comm_init_all", ctypes.c_int,
      [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),

@@ -130,7 +130,8 @@ int enqueue_messages_check(DevCtx* c, const MsgStage& st, hipStream_t stream, ui
 // verify already copied); gate: run the layout and copy kernels only when *gate != 0.
 int enqueue_serialize(DevCtx* c, const ::ambrycrc_put_desc* d_desc, size_t m, const uint8_t* d_fields,
                       const uint8_t* d_blobs, uint8_t* d_out, uint64_t* d_msg_len, void* d_ws, hipStream_t stream,
-                      const uint32_t* d_in_crc = nullptr, bool layout_only = false, const uint32_t* gate = nullptr);
+                      const uint32_t* d_in_crc = nullptr, bool layout_only = false, const uint32_t* gate = nullptr,
+                      const PropsFix* pfix = nullptr);
 
 // Holds c->ws_mu for the lifetime of a *_dev call that uses the default workspace (d_ws ==
 // NULL); a call with its own workspace takes no lock.

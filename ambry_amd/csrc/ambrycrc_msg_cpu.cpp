@@ -10,6 +10,7 @@
 #include <string.h>
 
 #include "put_layout.h"
+#include "record_fields.h"
 
 namespace {
 
@@ -33,9 +34,9 @@ uint32_t record_check(int k, const uint8_t* q, uint64_t span) {
       return n >= 0 && (uint64_t)n + 14 == span ? 0u : AMBRYCRC_MSG_BAD_RECORD;
     }
     case 1:
-      return v == 1 ? 0u : AMBRYCRC_MSG_BAD_VERSION;
+      return ambrycrc::props_record_check(q, span);
     case 2:
-      return v >= 1 && v <= 3 ? 0u : AMBRYCRC_MSG_BAD_VERSION;
+      return ambrycrc::update_record_check(q, span);
     default: {
       if (v < 1 || v > 3) return AMBRYCRC_MSG_BAD_VERSION;
       const uint32_t head = v == 1 ? 10u : v == 2 ? 12u : 13u;
@@ -161,8 +162,20 @@ int ambrycrc_transform_message_cpu(const uint8_t* region, uint64_t region_len, u
   d.key_len = (uint32_t)(first - m.hsize);
   d.enckey_src = keep_enc ? off + enc + 6 : 0;
   d.enckey_len = keep_enc ? (int32_t)rd32(p + enc + 2) : -1;
+  // deserializeBlobProperties, re-serialized at VERSION_5 (record_fields.h; verify parsed it)
+  const uint32_t stored = (uint32_t)(um - bp - 2 - 8);
+  ambrycrc::PropsFields pf;
+  if (ambrycrc::props_parse<true>(p + bp + 2, stored, &pf) != 0) {
+    *status = AMBRYCRC_MSG_BAD_RECORD;
+    return AMBRYCRC_OK;
+  }
+  if (!pf.ascii) {
+    *status = AMBRYCRC_MSG_NOT_ENCODABLE;
+    return AMBRYCRC_OK;
+  }
+  const ambrycrc::PropsFix fx = ambrycrc::props_fix_of(pf, stored);
   d.props_src = off + bp + 2;
-  d.props_len = (uint32_t)(um - bp - 2 - 8);
+  d.props_len = ambrycrc::props_v5_len(fx);
   d.usermeta_src = off + um + 6;
   d.usermeta_len = rd32(p + um + 2);
   d.blob_src = off + blob + head;
@@ -180,8 +193,18 @@ int ambrycrc_transform_message_cpu(const uint8_t* region, uint64_t region_len, u
     *status = AMBRYCRC_MSG_NO_ROOM;
     return AMBRYCRC_OK;
   }
+  // the stored payload is copied (props_len bytes from props_src: the appendix's share of them comes
+  // from the user-metadata record that follows, inside the message), then rewritten as V5 and its
+  // record CRC recomputed
   const int rc = ambrycrc_serialize_put_host(&d, region, region, out, out_cap, nullptr);
   if (rc) return rc;
+  if (fx.version) {
+    uint64_t fo[5];
+    ambrycrc_put_layout(&d, fo);
+    uint8_t* rec = out + fo[2] - 2;
+    ambrycrc::props_apply_fix(rec + 2, fx);
+    ambrycrc::put_be64(rec + 2 + d.props_len, (uint64_t)ambrycrc_update(0, rec, 2ull + d.props_len));
+  }
   *out_len = n;
   *status = 0;
   return AMBRYCRC_OK;

@@ -53,26 +53,53 @@ const Rccl& rccl() {
 // Per-rank segment of the gather buffer: a multiple of 64 CRCs (256 B), so RCCL moves aligned
 // blocks; a batch whose shards all have exactly that many chunks is gathered in place in the
 // caller's d_gathered, any other goes through a padded scratch buffer and is compacted after.
+// The arithmetic is ambrycrc_gather_layout's; the compaction copies are gather_copies' (the host
+// executor ambrycrc_gather_compact_host runs the same list, so the CPU multi-rank tests drive it).
 constexpr uint64_t kSegAlign = 64;
 
-uint64_t seg_width(const uint64_t* counts, int nranks) {
-  uint64_t w = 0;
-  for (int r = 0; r < nranks; ++r) w = std::max(w, counts[r]);
-  return (w + kSegAlign - 1) / kSegAlign * kSegAlign;
-}
-
-struct DevScratch {
-  int device = -1;
-  uint32_t* ptr = nullptr;
-  size_t words = 0;
+struct GatherLayout {
+  uint64_t width = 0;  // CRCs per rank segment
+  bool in_place = false;
+  std::vector<uint64_t> start;  // [nranks + 1]: shard r's CRCs end at d_gathered[start[r] .. start[r+1])
 };
 
-// Prefix sums of the shard counts: shard r's CRCs land at d_gathered[start[r] .. start[r+1]).
-std::vector<uint64_t> count_starts(const uint64_t* counts, int nranks) {
-  std::vector<uint64_t> s(nranks + 1, 0);
-  for (int r = 0; r < nranks; ++r) s[r + 1] = s[r] + counts[r];
-  return s;
+GatherLayout gather_layout(const uint64_t* counts, int nranks) {
+  GatherLayout g;
+  uint64_t w = 0;
+  for (int r = 0; r < nranks; ++r) w = std::max(w, counts[r]);
+  g.width = (w + kSegAlign - 1) / kSegAlign * kSegAlign;
+  g.in_place = g.width > 0;
+  g.start.assign(nranks + 1, 0);
+  for (int r = 0; r < nranks; ++r) {
+    g.start[r + 1] = g.start[r] + counts[r];
+    g.in_place = g.in_place && counts[r] == g.width;
+  }
+  return g;
 }
+
+// The padded layout's compaction: fn(dst word, src word, words) for each non-empty shard.
+template <class Fn>
+int gather_copies(const GatherLayout& g, const uint64_t* counts, int nranks, Fn fn) {
+  for (int r = 0; r < nranks; ++r)
+    if (counts[r]) {
+      const int rc = fn(g.start[r], (uint64_t)r * g.width, counts[r]);
+      if (rc) return rc;
+    }
+  return AMBRYCRC_OK;
+}
+
+// Padded gather buffers, one per (local device, stream): a batch on another stream never shares
+// one with a batch still queued (its kernels, all-gather and compaction run in stream order).
+// `done` is recorded after the compaction; a buffer is reused for another stream, or regrown,
+// only after it has fired. At most kScratchPerDevice streams keep one (least recent evicted).
+struct DevScratch {
+  hipStream_t stream = nullptr;
+  uint32_t* ptr = nullptr;
+  size_t words = 0;
+  hipEvent_t done = nullptr;
+  uint64_t last_use = 0;
+};
+constexpr size_t kScratchPerDevice = 8;
 
 }  // namespace
 
@@ -81,39 +108,66 @@ struct ambrycrc_comm {
   std::vector<int> devices;
   int nranks = 0;
   int rank = 0;  // rank of comms[0] (0 for ambrycrc_comm_init_all)
-  std::vector<DevScratch> scratch;
-  std::mutex mu;  // one batch enqueues at a time (RCCL group semantics, scratch growth)
+  std::vector<std::vector<DevScratch>> scratch;  // per local device
+  uint64_t uses = 0;
+  std::mutex mu;  // one batch enqueues at a time (RCCL group semantics, scratch bookkeeping)
 };
 
 namespace {
 
-int scratch_for(ambrycrc_comm* c, size_t i, size_t words, uint32_t** out) {
-  DevScratch& s = c->scratch[i];
-  if (s.words < words) {
-    if (s.ptr) {
-      (void)hipDeviceSynchronize();  // queued gathers may still use it (rare: growth only)
-      (void)hipFree(s.ptr);
-    }
-    s.ptr = nullptr;
-    s.words = 0;
-    if (hipMalloc(reinterpret_cast<void**>(&s.ptr), words * sizeof(uint32_t)) != hipSuccess) return AMBRYCRC_ENOMEM;
-    s.words = words;
+// The padded buffer of local device i for `stream` (current device: that device). *entry is where
+// the caller records the buffer's `done` event after its last use.
+int scratch_for(ambrycrc_comm* c, size_t i, hipStream_t stream, size_t words, uint32_t** out, DevScratch** entry) {
+  std::vector<DevScratch>& list = c->scratch[i];
+  DevScratch* s = nullptr;
+  for (DevScratch& x : list)
+    if (x.ptr && x.stream == stream) s = &x;
+  if (!s && list.size() < kScratchPerDevice) {
+    list.emplace_back();
+    s = &list.back();
   }
-  *out = s.ptr;
+  if (!s) {  // evict the least recently used stream's buffer
+    s = &list[0];
+    for (DevScratch& x : list)
+      if (x.last_use < s->last_use) s = &x;
+  }
+  if (s->stream != stream || s->words < words) {
+    if (s->done && hipEventSynchronize(s->done) != hipSuccess) return AMBRYCRC_EHIP;  // its last gather
+    s->stream = stream;
+  }
+  if (s->words < words) {
+    if (s->ptr) (void)hipFree(s->ptr);
+    s->ptr = nullptr;
+    s->words = 0;
+    if (hipMalloc(reinterpret_cast<void**>(&s->ptr), words * sizeof(uint32_t)) != hipSuccess) return AMBRYCRC_ENOMEM;
+    s->words = words;
+  }
+  if (!s->done && hipEventCreateWithFlags(&s->done, hipEventDisableTiming) != hipSuccess) return AMBRYCRC_EHIP;
+  s->last_use = ++c->uses;
+  *out = s->ptr;
+  *entry = s;
   return AMBRYCRC_OK;
+}
+
+void free_scratch(std::vector<DevScratch>& list) {
+  for (DevScratch& x : list) {
+    if (x.ptr) (void)hipFree(x.ptr);
+    if (x.done) (void)hipEventDestroy(x.done);
+  }
+  list.clear();
 }
 
 // Enqueues shard i's CRCs into its segment, for every local shard, then one grouped all-gather,
 // then (padded layout) the compaction copies. Caller holds c->mu; device restored by the caller.
 int enqueue_gather(ambrycrc_comm* c, const ambrycrc_shard* shards, const uint64_t* counts) {
   const int nranks = c->nranks;
-  const uint64_t width = seg_width(counts, nranks);
+  const GatherLayout g = gather_layout(counts, nranks);
+  const uint64_t width = g.width;
   if (width == 0) return AMBRYCRC_OK;
-  bool in_place = true;
-  for (int r = 0; r < nranks; ++r) in_place = in_place && counts[r] == width;
-  const std::vector<uint64_t> start = count_starts(counts, nranks);
+  const bool in_place = g.in_place;
   const size_t local = c->comms.size();
   std::vector<uint32_t*> recv(local, nullptr);
+  std::vector<DevScratch*> entry(local, nullptr);
   for (size_t i = 0; i < local; ++i) {
     const ambrycrc_shard& s = shards[i];
     const int rank = c->rank + (int)i;
@@ -121,7 +175,7 @@ int enqueue_gather(ambrycrc_comm* c, const ambrycrc_shard* shards, const uint64_
     if (in_place) {
       recv[i] = s.d_gathered;
     } else {
-      const int rc = scratch_for(c, i, (size_t)width * nranks, &recv[i]);
+      const int rc = scratch_for(c, i, s.stream, (size_t)width * nranks, &recv[i], &entry[i]);
       if (rc) return rc;
     }
     const int rc = ambrycrc_batch_dev(s.d_base, s.d_off, s.d_len, s.d_crc_in, recv[i] + (size_t)rank * width, s.n,
@@ -139,11 +193,15 @@ int enqueue_gather(ambrycrc_comm* c, const ambrycrc_shard* shards, const uint64_
   if (rc || in_place) return rc;
   for (size_t i = 0; i < local; ++i) {
     if (hipSetDevice(shards[i].device) != hipSuccess) return AMBRYCRC_EHIP;
-    for (int r = 0; r < nranks; ++r)
-      if (counts[r] &&
-          hipMemcpyAsync(shards[i].d_gathered + start[r], recv[i] + (size_t)r * width, counts[r] * sizeof(uint32_t),
-                         hipMemcpyDeviceToDevice, shards[i].stream) != hipSuccess)
-        return AMBRYCRC_EHIP;
+    const hipStream_t st = shards[i].stream;
+    rc = gather_copies(g, counts, nranks, [&](uint64_t dst, uint64_t src, uint64_t words) {
+      return hipMemcpyAsync(shards[i].d_gathered + dst, recv[i] + src, words * sizeof(uint32_t), hipMemcpyDeviceToDevice,
+                            st) == hipSuccess
+                 ? AMBRYCRC_OK
+                 : AMBRYCRC_EHIP;
+    });
+    if (rc) return rc;
+    if (hipEventRecord(entry[i]->done, st) != hipSuccess) return AMBRYCRC_EHIP;
   }
   return AMBRYCRC_OK;
 }
@@ -156,6 +214,28 @@ bool shard_ok(const ambrycrc_shard& s) {
 }  // namespace
 
 extern "C" {
+
+int ambrycrc_gather_layout(const uint64_t* counts, int nranks, uint64_t* width, int* in_place, uint64_t* starts) {
+  if (nranks <= 0 || !counts) return AMBRYCRC_EINVAL;
+  const GatherLayout g = gather_layout(counts, nranks);
+  if (width) *width = g.width;
+  if (in_place) *in_place = g.in_place ? 1 : 0;
+  if (starts) memcpy(starts, g.start.data(), sizeof(uint64_t) * (nranks + 1));
+  return AMBRYCRC_OK;
+}
+
+int ambrycrc_gather_compact_host(const uint32_t* padded, const uint64_t* counts, int nranks, uint32_t* out) {
+  if (nranks <= 0 || !counts || !out || !padded) return AMBRYCRC_EINVAL;
+  const GatherLayout g = gather_layout(counts, nranks);
+  if (g.in_place) {  // the gather buffer is the result
+    if (out != padded) memmove(out, padded, sizeof(uint32_t) * g.start[nranks]);
+    return AMBRYCRC_OK;
+  }
+  return gather_copies(g, counts, nranks, [&](uint64_t dst, uint64_t src, uint64_t words) {
+    memmove(out + dst, padded + src, words * sizeof(uint32_t));
+    return AMBRYCRC_OK;
+  });
+}
 
 int ambrycrc_shard_by_bytes(const uint64_t* lens, size_t n, int nshards, size_t* cuts) {
   if (nshards <= 0 || !cuts || (n && !lens)) return AMBRYCRC_EINVAL;
@@ -246,7 +326,7 @@ int ambrycrc_comm_destroy(ambrycrc_comm* c) {
   for (size_t i = 0; i < c->comms.size(); ++i) {
     (void)hipSetDevice(c->devices[i]);
     (void)hipDeviceSynchronize();
-    if (c->scratch[i].ptr) (void)hipFree(c->scratch[i].ptr);
+    free_scratch(c->scratch[i]);
     if (c->comms[i] && R.comm_destroy(c->comms[i]) != ncclSuccess) rc = AMBRYCRC_ECOMM;
   }
   (void)hipSetDevice(prev);

@@ -10,6 +10,7 @@
 #include "ambrycrc_ctx.h"
 #include "crc32_kernels.h"
 #include "put_layout.h"
+#include "record_fields.h"
 
 using namespace ambrycrc;
 using namespace ambrycrc::detail;
@@ -25,10 +26,14 @@ size_t put_jobs_bytes(size_t m) {
 }
 
 // A transform's own workspace: descriptors, the scan's per-message output, in_crc (4 per message),
-// the speculative pass's xstatus, its fail flag and the verify jobs' copy destinations (5 per message).
+// the speculative pass's xstatus, its fail flag, the verify jobs' copy destinations (5 per message)
+// and the properties re-encodings (one PropsFix per message).
+size_t transform_head_bytes(size_t m) {
+  return (m * (sizeof(ambrycrc_put_desc) + 6 * sizeof(uint32_t)) + 8 + 15) & ~size_t(15);
+}
 size_t transform_own_bytes(size_t m) {
-  const size_t head = (m * (sizeof(ambrycrc_put_desc) + 6 * sizeof(uint32_t)) + 8 + 7) & ~size_t(7);
-  return (head + (size_t)kPutSlots * m * sizeof(uint64_t) + 255) & ~size_t(255);
+  return (transform_head_bytes(m) + (size_t)kPutSlots * m * sizeof(uint64_t) + m * sizeof(PropsFix) + 255) &
+         ~size_t(255);
 }
 
 }  // namespace
@@ -38,7 +43,7 @@ namespace detail {
 
 int enqueue_serialize(DevCtx* c, const ::ambrycrc_put_desc* d_desc, size_t m, const uint8_t* d_fields,
                       const uint8_t* d_blobs, uint8_t* d_out, uint64_t* d_msg_len, void* d_ws, hipStream_t stream,
-                      const uint32_t* d_in_crc, bool layout_only, const uint32_t* gate) {
+                      const uint32_t* d_in_crc, bool layout_only, const uint32_t* gate, const PropsFix* pfix) {
   const size_t j = (size_t)kPutSlots * m;
   uint8_t* w = static_cast<uint8_t*>(d_ws);
   PutArgs a;
@@ -61,14 +66,23 @@ int enqueue_serialize(DevCtx* c, const ::ambrycrc_put_desc* d_desc, size_t m, co
   a.img = c->d_img;
   a.copy_through = (d_fields || d_blobs) && !d_in_crc;
   a.gate = gate;
+  a.src_base = 0;
+  if (a.copy_through) {  // every source lies in fields, blobs or (a slot in place) the output
+    uintptr_t lo = UINTPTR_MAX;
+    if (d_fields) lo = std::min(lo, (uintptr_t)d_fields);
+    if (d_blobs) lo = std::min(lo, (uintptr_t)d_blobs);
+    if (!d_fields || !d_blobs) lo = std::min(lo, (uintptr_t)d_out);
+    a.src_base = (uint64_t)lo;
+  }
+  a.pfix = pfix;
   void* batch_ws = w + put_jobs_bytes(m);
   if (launch_put_layout(a, stream) != hipSuccess) return AMBRYCRC_EHIP;
   if (layout_only) return AMBRYCRC_OK;
   if (a.copy_through) {
     // one pass over the fields: the copy-through sweep reads each from its source, writes it into
     // the message and CRCs it (job k*m+i = slot k of message i, as the CRC jobs)
-    const int rc = enqueue_batch(c, nullptr, a.cp_src, a.cp_len, a.crc_in, crc, j, batch_ws, stream, nullptr, d_out,
-                                 a.cp_dst);
+    const int rc = enqueue_batch(c, reinterpret_cast<const uint8_t*>((uintptr_t)a.src_base), a.cp_src, a.cp_len,
+                                 a.crc_in, crc, j, batch_ws, stream, nullptr, d_out, a.cp_dst);
     if (rc) return rc;
     return hip_err(launch_put_seal(a, stream));
   }
@@ -184,7 +198,7 @@ int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len
   int rc = lease.acquire(c, stream, &d_ws, ws_bytes, ambrycrc_transform_workspace_bytes(m));
   if (rc) return rc;
   // workspace: desc[m] | scan scratch (uint32 per message) | in_crc[4m] | xstatus[m] | fail |
-  //            copy_off[5m] | plan workspace for the m lengths | the verify pipeline's, then the
+  //            copy_off[5m] | pfix[m] | plan workspace for the m lengths | the verify pipeline's, then the
   //            serializer's (one after the other on the stream)
   uint8_t* w = static_cast<uint8_t*>(d_ws);
   TransformArgs t;
@@ -204,8 +218,8 @@ int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len
   t.in_crc = scan_out + m;
   uint32_t* xstatus = t.in_crc + 4 * m;
   uint32_t* fail = xstatus + m;
-  uint64_t* copy_off = reinterpret_cast<uint64_t*>(w + ((m * (sizeof(ambrycrc_put_desc) + 6 * sizeof(uint32_t)) + 8 +
-                                                         7) & ~size_t(7)));
+  uint64_t* copy_off = reinterpret_cast<uint64_t*>(w + transform_head_bytes(m));
+  t.pfix = reinterpret_cast<PropsFix*>(copy_off + (size_t)kPutSlots * m);
   t.img = c->d_img;
   t.out = d_out;
   t.fail = fail;
@@ -249,6 +263,7 @@ int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len
   if (launch_transform_finish(t, stream) != hipSuccess) return AMBRYCRC_EHIP;
   rc = enqueue_serialize(c, t.desc, m, d_region, d_region, d_out, nullptr, shared, stream, t.in_crc, true);
   if (rc) return rc;
+  if (launch_props_fix(t, stream) != hipSuccess) return AMBRYCRC_EHIP;  // after the copy-through
   t.gate = fail;
   t.gate_when = 0;  // no failure: the final status is the verify's bits, else the transform's own
   if (launch_transform_merge(t, stream) != hipSuccess) return AMBRYCRC_EHIP;
@@ -261,7 +276,10 @@ int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len
   if (launch_transform_desc(t, stream) != hipSuccess) return AMBRYCRC_EHIP;
   if (launch_plan(p, stream) != hipSuccess) return AMBRYCRC_EHIP;
   if (launch_transform_place(t, p.byte_start, stream) != hipSuccess) return AMBRYCRC_EHIP;
-  return enqueue_serialize(c, t.desc, m, d_region, d_region, d_out, nullptr, shared, stream, t.in_crc, false, fail);
+  rc = enqueue_serialize(c, t.desc, m, d_region, d_region, d_out, nullptr, shared, stream, t.in_crc, false, fail,
+                         t.pfix);
+  if (rc) return rc;
+  return hip_err(launch_props_fix(t, stream));  // after the gather copy (gated as the pass)
 }
 
 }  // extern "C"

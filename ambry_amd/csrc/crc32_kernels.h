@@ -8,6 +8,8 @@
 
 namespace ambrycrc {
 
+struct PropsFix;  // record_fields.h
+
 struct PlanArgs {
   const uint64_t* off;     // [n] byte offsets of chunks from base
   const uint64_t* len;     // [n] chunk lengths
@@ -36,6 +38,12 @@ static_assert(kPlanPerBlock % 256 == 0 && kPlanPerBlock <= 65535, "plan block si
 constexpr uint64_t kShareQuantum = 1024;  // per-wave byte shares are multiples of this
 constexpr uint64_t kMinShare = 16384;     // ... and at least this (see crc32_sweep_kernel)
 
+// Load invariant of every CRC kernel (plan, sweep, group phase, copy-through): the only global
+// bytes read through `base` are chunk bytes, [base + off[c], base + off[c] + len[c]) for c < n,
+// plus -- with exp_fill -- the 8 stored-CRC bytes after a group-phase chunk. An empty chunk reads
+// nothing. So base must be a real device pointer that every chunk's bytes lie at or after (it is
+// never dereferenced by itself); the serializer's copy-through passes the lowest of its source
+// buffers (PutArgs::src_base), not null.
 struct SweepArgs {
   const uint8_t* base;
   const uint64_t* off;
@@ -136,7 +144,7 @@ struct PutArgs {
   uint8_t* out;
   const uint8_t* fields;   // or null: key / encryption key / properties / user metadata already in place
   const uint8_t* blobs;    // or null: blob contents already in place
-  uint64_t* cp_src;        // [5m] copy jobs: absolute source address, destination offset in out, length
+  uint64_t* cp_src;        // [5m] copy jobs: source address - src_base, destination offset in out, length
   uint64_t* cp_dst;
   uint64_t* cp_len;
   uint64_t* cp_cost;       // [5m] len + kCopyJobCost (0 for an empty job): what the copy balances
@@ -153,6 +161,12 @@ struct PutArgs {
   const uint32_t* img;
   // Run only when *gate != 0 (null: always). The transform's fallback pass.
   const uint32_t* gate;
+  // Transform only ([m] or null): properties re-encoded at V5 -- the copy job moves the stored
+  // payload (stored_len bytes), props_fix_kernel then rewrites it in place (record_fields.h).
+  const PropsFix* pfix;
+  // Subtracted from every cp_src: 0 for the gather copy (absolute addresses); in copy-through mode the
+  // lowest of the source buffers, and the CRC batch's base (SweepArgs load invariant).
+  uint64_t src_base;
   // Copy-through mode (copy mode without in_crc): the copy jobs become the CRC batch itself --
   // the sweep reads each field once, writes it to the message and CRCs it, seeded (crc_in) with
   // the CRC of the record's prefix (<= 13 B, hashed by the layout kernel), so the batch's result
@@ -207,6 +221,10 @@ struct TransformArgs {
   uint8_t* out;
   const uint32_t* gate;
   int gate_when;
+  // [m] how each transformed message's stored BlobProperties payload becomes its V5 bytes
+  // (record_fields.h): written by transform_describe, applied by props_fix_kernel after the
+  // payload is copied into place.
+  PropsFix* pfix;
 };
 
 hipError_t launch_transform_desc(const TransformArgs& a, hipStream_t s);
@@ -217,6 +235,7 @@ hipError_t launch_transform_place(const TransformArgs& a, const uint64_t* start,
 hipError_t launch_transform_jobs(const TransformArgs& a, hipStream_t s);
 hipError_t launch_transform_finish(const TransformArgs& a, hipStream_t s);
 hipError_t launch_transform_merge(const TransformArgs& a, hipStream_t s);
+hipError_t launch_props_fix(const TransformArgs& a, hipStream_t s);
 
 hipError_t launch_put_layout(const PutArgs& a, hipStream_t s);
 hipError_t launch_put_seal(const PutArgs& a, hipStream_t s);

@@ -22,6 +22,7 @@
 #include "crc32_layout.h"
 #include "crc_img.h"
 #include "put_layout.h"
+#include "record_fields.h"
 
 namespace ambrycrc {
 
@@ -107,7 +108,7 @@ __device__ __forceinline__ uint32_t header_crc(const HeaderWords& h, uint32_t n,
 // ordinal < 2, a long size <= Integer.MAX_VALUE, then the content and the CRC. A size that
 // disagrees with the header's record span, or a bad type, is AMBRYCRC_MSG_BAD_RECORD (the
 // reference reads the CRC at a different place, or throws). BlobProperties_Format_V1 and
-// Update_Format_V1..V3: the version only.
+// Update_Format_V1..V3: their fields, to the CRC (record_fields.h).
 __device__ __forceinline__ uint32_t record_check(int k, const uint8_t* q, uint64_t span) {
   if (span < 10) return AMBRYCRC_MSG_BAD_RECORD;  // a version and a CRC at least
   const uint32_t v = be16(q);
@@ -120,9 +121,9 @@ __device__ __forceinline__ uint32_t record_check(int k, const uint8_t* q, uint64
       return n >= 0 && (uint64_t)n + 14 == span ? 0u : AMBRYCRC_MSG_BAD_RECORD;
     }
     case 1:  // properties
-      return v == 1 ? 0u : AMBRYCRC_MSG_BAD_VERSION;
+      return props_record_check(q, span);
     case 2:  // update
-      return v >= 1 && v <= 3 ? 0u : AMBRYCRC_MSG_BAD_VERSION;
+      return update_record_check(q, span);
     default: {  // blob
       if (v < 1 || v > 3) return AMBRYCRC_MSG_BAD_VERSION;
       const uint32_t head = v == 1 ? 10u : v == 2 ? 12u : 13u;
@@ -318,6 +319,44 @@ __device__ __forceinline__ bool gated_off(const uint32_t* gate, int when) {
   return gate && ((*gate != 0) != (when != 0));
 }
 
+// CRC of the V5 properties record from the stored record's CRC `c` (its bytes at rec, verified):
+// the edits are XOR patterns at fixed places of an equal-length record, so each adds
+// (crc(old window) ^ crc(new window)) * x^(8 * bytes after the window); the appended fields
+// continue the CRC. No pass over the payload.
+__device__ __forceinline__ uint32_t props_v5_crc(const uint32_t* __restrict__ img, const uint8_t* rec,
+                                                 const PropsFix& x, uint32_t c) {
+  if (!x.version) return c;
+  const uint64_t L = 2ull + x.stored_len;  // record bytes the CRC covers
+  uint8_t o[11], n[11];                    // record bytes [2, 13): SerDe version, ttl, private
+#pragma unroll
+  for (int k = 0; k < 11; ++k) o[k] = n[k] = rec[2 + k];
+  n[0] = 0;
+  n[1] = 5;
+  n[kSerdePrivate] = x.priv;
+  c ^= mul_xpow8_img(img, crc_bytes_img(img, 0u, o, 11) ^ crc_bytes_img(img, 0u, n, 11), L - 13);
+  if (x.enc_pos) {
+    const uint8_t eo = rec[2 + x.enc_pos], en = x.enc;
+    if (eo != en)
+      c ^= mul_xpow8_img(img, crc_bytes_img(img, 0u, &eo, 1) ^ crc_bytes_img(img, 0u, &en, 1),
+                         L - (2ull + x.enc_pos + 1));
+  }
+  uint8_t app[kPropsAppendixMax];
+  const uint32_t na = props_appendix(x.version, app);
+  return crc_bytes_img(img, c, app, na);
+}
+
+// After the stored payloads are in place in the output: rewrite the re-encoded ones as V5.
+__global__ __launch_bounds__(256) void props_fix_kernel(TransformArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.m || gated_off(a.gate, a.gate_when)) return;
+  const ambrycrc_put_desc d = a.desc[i];
+  if (d.header_version == 0) return;
+  const PropsFix x = a.pfix[i];
+  PutLayout L;
+  if (!x.version || !put_layout(d, L)) return;
+  props_apply_fix(a.out + d.out_off + (uint64_t)L.bp_rel + 2, x);
+}
+
 __device__ __forceinline__ void transform_describe(const TransformArgs& a, uint64_t i, uint32_t st0) {
   uint32_t st = st0;
   ambrycrc_put_desc d;
@@ -358,6 +397,11 @@ __device__ __forceinline__ void transform_describe(const TransformArgs& a, uint6
       const int64_t props_len = (int64_t)um - bp - 2 - 8;  // BlobProperties_Format_V1: version, props, CRC
       const uint32_t um_len = be32(p + um + 2);             // UserMetadata_Format_V1: version, int size, ..., CRC
       ok = ok && props_len >= 0 && (int64_t)um + 6 + um_len + 8 == blob;
+      // deserializeBlobProperties -> serializeBlobProperties at VERSION_5 (record_fields.h)
+      PropsFields pf;
+      ok = ok && props_parse<true>(p + bp + 2, (uint64_t)props_len, &pf) == 0;
+      const bool encodable = !ok || pf.ascii;
+      const PropsFix fx = ok ? props_fix_of(pf, (uint32_t)props_len) : PropsFix{};
       const uint32_t bv = be16(p + blob);  // Blob_Format_V1 / V2 / V3 (:1668-1833)
       uint32_t head = 0, type = 0, comp = 0;
       uint64_t size = 0;
@@ -380,6 +424,8 @@ __device__ __forceinline__ void transform_describe(const TransformArgs& a, uint6
       ok = ok && type < 2 && size <= 0x7FFFFFFFull && (int64_t)blob + head + (int64_t)size + 8 == end;
       if (!ok) {
         st |= AMBRYCRC_MSG_BAD_RECORD;
+      } else if (!encodable) {
+        st |= AMBRYCRC_MSG_NOT_ENCODABLE;
       } else {
         d.key_src = off + hs;
         d.key_len = (uint32_t)(first - hs);
@@ -387,7 +433,8 @@ __device__ __forceinline__ void transform_describe(const TransformArgs& a, uint6
         d.enckey_src = keep_enc ? off + enc + 6 : 0;
         d.enckey_len = keep_enc ? (int32_t)enc_len : -1;
         d.props_src = off + bp + 2;
-        d.props_len = (uint32_t)props_len;
+        d.props_len = props_v5_len(fx);
+        a.pfix[i] = fx;
         d.usermeta_src = off + um + 6;
         d.usermeta_len = um_len;
         d.blob_src = off + blob + head;
@@ -405,7 +452,7 @@ __device__ __forceinline__ void transform_describe(const TransformArgs& a, uint6
           // every record of the input verified: its CRC is the low word of its 8-B trailer
           uint32_t* ic = a.in_crc + 4 * i;
           ic[0] = keep_enc ? be32(p + bp - 4) : 0u;
-          ic[1] = be32(p + um - 4);
+          ic[1] = props_v5_crc(a.img, p + bp, fx, be32(p + um - 4));
           ic[2] = be32(p + blob - 4);
           uint32_t cblob = be32(p + end - 4);
           if (bv != 3) {  // the V3 head (version 3, type, compressed, size) replaces a V1/V2 head
@@ -535,6 +582,12 @@ hipError_t launch_transform_finish(const TransformArgs& a, hipStream_t s) {
 hipError_t launch_transform_merge(const TransformArgs& a, hipStream_t s) {
   if (a.m == 0) return hipSuccess;
   hipLaunchKernelGGL(transform_merge_kernel, dim3((uint32_t)((a.m + 255) / 256)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_props_fix(const TransformArgs& a, hipStream_t s) {
+  if (a.m == 0) return hipSuccess;
+  hipLaunchKernelGGL(props_fix_kernel, dim3((uint32_t)((a.m + 255) / 256)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

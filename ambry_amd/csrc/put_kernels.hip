@@ -17,6 +17,7 @@
 #include "crc32_kernels.h"
 #include "crc_img.h"
 #include "put_layout.h"
+#include "record_fields.h"
 
 namespace ambrycrc {
 
@@ -59,13 +60,15 @@ __global__ __launch_bounds__(256) void put_layout_kernel(PutArgs a) {
   uint64_t fo[5];
   put_field_offsets(d, L, fo);
   const uint64_t src[5] = {d.key_src, d.enckey_src, d.props_src, d.usermeta_src, d.blob_src};
-  const uint64_t len[5] = {d.key_len, L.enc_rec ? (uint64_t)d.enckey_len : 0, d.props_len, d.usermeta_len,
+  // a transform's V5 re-encoding copies the stored payload; props_fix_kernel completes it
+  const uint64_t props_copy = a.pfix && a.pfix[i].version ? a.pfix[i].stored_len : d.props_len;
+  const uint64_t len[5] = {d.key_len, L.enc_rec ? (uint64_t)d.enckey_len : 0, props_copy, d.usermeta_len,
                            d.blob_len};
 #pragma unroll
   for (uint32_t k = 0; k < kPutSlots; ++k) {
     const uint8_t* base = k == 4 ? a.blobs : a.fields;
-    a.cp_src[k * m + i] = base ? (uint64_t)(uintptr_t)(base + src[k])
-                               : (a.copy_through ? (uint64_t)(uintptr_t)(msg + fo[k]) : 0);
+    a.cp_src[k * m + i] = base ? (uint64_t)(uintptr_t)(base + src[k]) - a.src_base
+                               : (a.copy_through ? (uint64_t)(uintptr_t)(msg + fo[k]) - a.src_base : 0);
     a.cp_dst[k * m + i] = d.out_off + fo[k];
     a.cp_len[k * m + i] = base || a.copy_through ? len[k] : 0;
     a.cp_cost[k * m + i] = base && len[k] ? len[k] + kCopyJobCost : 0;

@@ -1,87 +1,82 @@
 """One-process-per-GPU sharding of a CRC batch, with the 4-byte results exchanged by all-gather.
 
-The batch path shards trivially: chunk CRCs are independent, so
-rank r computes a contiguous block of chunks balanced by bytes and the only
-exchange is one all-gather of uint32 CRCs (RCCL over xGMI on MI355X; gloo in
-the CPU tests). A single blob larger than one GPU is split by byte range and
-the per-rank CRCs are folded with the GF(2) combine after an all-gather of
-(crc, length) pairs. There is no Ambry counterpart: the reference never splits
-one blob's CRC across workers (CrcInputStream streams it serially).
+The batch path shards trivially: chunk CRCs are independent, so rank r computes
+a contiguous block of chunks balanced by bytes and the only exchange is one all-gather of uint32
+CRCs. On MI355X that all-gather is RCCL over xGMI inside libambrycrc (ambrycrc_batch_dev_gather);
+here any torch.distributed group (gloo in the CPU tests) carries the padded segments, and every
+other step is libambrycrc's own C code through ctypes -- the shard cuts
+(ambrycrc_shard_by_bytes), the segment layout (ambrycrc_gather_layout) and the compaction
+(ambrycrc_gather_compact_host, the copy list the device path enqueues) -- so the multi-rank CPU
+tests run the arithmetic the GPU path runs, not a restatement of it.
+
+A single blob larger than one GPU is split by byte range and the per-rank CRCs are folded with
+the GF(2) combine after an all-gather of (crc, length) pairs. There is no Ambry counterpart: the
+reference never splits one blob's CRC across workers (CrcInputStream streams it serially).
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Callable, Sequence
 
 import numpy as np
 
+from ._lib import check, lib
 from .crc32 import combine
 
 
 def shard_by_bytes(lengths: Sequence[int], world: int) -> list[tuple[int, int]]:
-    """Contiguous chunk ranges [lo, hi) per rank with near-equal byte totals.
+    """ambrycrc_shard_by_bytes: contiguous chunk ranges [lo, hi) per rank with near-equal bytes."""
+    from .device import shard_by_bytes as c_shard
 
-    Rank r takes the chunks whose start byte s satisfies r/world <= s/total < (r+1)/world
-    (exact rational comparison, the rule of ambrycrc_shard_by_bytes in the C ABI, which
-    tests/test_multi.py checks this against). Every chunk belongs to exactly one rank; ranks
-    may be empty when n < world; an all-empty batch is split by count.
-    """
-    lengths = np.asarray(lengths, dtype=np.int64)
-    n = len(lengths)
-    starts = np.concatenate([[0], np.cumsum(lengths)[:-1]]) if n else np.zeros(0, dtype=np.int64)
-    total = int(lengths.sum()) if n else 0
-    bounds = []
-    for r in range(world + 1):
-        if r == world:
-            bounds.append(n)
-        elif total == 0:
-            bounds.append((n * r) // world)  # all-empty batch: split by count
-        else:
-            bounds.append(int(np.searchsorted(starts * world, total * r, side="left")))
-    return [(bounds[r], bounds[r + 1]) for r in range(world)]
-
-
-SEG_ALIGN = 64  # CRCs per gather-segment quantum (256 B), as ambrycrc_multi.cpp kSegAlign
+    return c_shard(lengths, world)
 
 
 def gather_layout(counts: Sequence[int]):
-    """Layout of the all-gather of per-rank CRCs, the rule ambrycrc_batch_dev_multi/_gather
-    use (ambrycrc_multi.cpp seg_width/enqueue_gather): every rank sends a segment of `width`
-    CRCs (the largest shard rounded up to 64); when every shard has exactly `width` chunks the
-    gather lands in place, otherwise rank r's CRCs are compacted from [r*width, r*width+counts[r])
-    to [starts[r], starts[r+1]). Returns (width, in_place, starts)."""
-    counts = [int(c) for c in counts]
-    width = -(-max(counts, default=0) // SEG_ALIGN) * SEG_ALIGN
-    starts = [0]
-    for c in counts:
-        starts.append(starts[-1] + c)
-    return width, width > 0 and all(c == width for c in counts), starts
+    """ambrycrc_gather_layout: (width, in_place, starts) of the CRC all-gather for shard sizes
+    `counts` -- every rank sends `width` CRCs, rank r's at [r*width, r*width + counts[r]); unless
+    in_place they are compacted to [starts[r], starts[r+1])."""
+    c = np.ascontiguousarray(np.asarray(counts, dtype=np.uint64))
+    nr = len(c)
+    width, in_place = ctypes.c_uint64(0), ctypes.c_int(0)
+    starts = (ctypes.c_uint64 * (nr + 1))()
+    check(lib().ambrycrc_gather_layout(c.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), nr, ctypes.byref(width),
+                                       ctypes.byref(in_place), starts), "ambrycrc_gather_layout")
+    return int(width.value), bool(in_place.value), [int(x) for x in starts]
 
 
-def gather_crcs(local, lo: int, hi: int, n: int, shards, dist, group=None, device=None):
-    """All-gather each rank's CRCs (int32 tensor of hi-lo) into the full int32[n] on every rank."""
-    import torch
-
-    world = len(shards)
-    width, in_place, starts = gather_layout([h - l for l, h in shards])
-    dev = local.device if device is None else device
-    seg = max(width, 1)
-    padded = torch.zeros(seg, dtype=torch.int32, device=dev)
-    if hi > lo:
-        padded[: hi - lo] = local
-    gathered = torch.empty(world * seg, dtype=torch.int32, device=dev)
-    dist.all_gather_into_tensor(gathered, padded, group=group)
-    if in_place:
-        out = gathered[:n]
-    else:
-        out = torch.empty(n, dtype=torch.int32, device=dev)
-        for r, (l, h) in enumerate(shards):
-            out[starts[r]:starts[r + 1]] = gathered[r * seg: r * seg + (h - l)]
-    assert out.numel() == n
+def gather_compact(padded: np.ndarray, counts: Sequence[int]) -> np.ndarray:
+    """ambrycrc_gather_compact_host: the shard-order CRC vector from the padded gather buffer."""
+    c = np.ascontiguousarray(np.asarray(counts, dtype=np.uint64))
+    src = np.ascontiguousarray(padded, dtype=np.uint32)
+    out = np.empty(int(c.sum()), dtype=np.uint32)
+    if out.size == 0:
+        return out
+    check(lib().ambrycrc_gather_compact_host(src.ctypes.data, c.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                             len(c), out.ctypes.data), "ambrycrc_gather_compact_host")
     return out
 
 
-def distributed_batch(lengths: Sequence[int], compute: Callable[[int, int], "object"], dist, group=None,
-                      device=None):
+def gather_crcs(local, lo: int, hi: int, n: int, shards, dist, group=None):
+    """All-gather each rank's CRCs (int32 CPU tensor of hi-lo) into the full int32[n] on every rank:
+    the padded segment layout of ambrycrc_gather_layout, one all_gather_into_tensor, then the C
+    compaction."""
+    import torch
+
+    counts = [h - l for l, h in shards]
+    world = len(shards)
+    width, _, _ = gather_layout(counts)
+    seg = max(width, 1)
+    padded = torch.zeros(seg, dtype=torch.int32)
+    if hi > lo:
+        padded[: hi - lo] = local
+    gathered = torch.empty(world * seg, dtype=torch.int32)
+    dist.all_gather_into_tensor(gathered, padded, group=group)
+    out = gather_compact(gathered.numpy().view(np.uint32), counts)
+    assert out.size == n
+    return torch.from_numpy(out.view(np.int32).copy())
+
+
+def distributed_batch(lengths: Sequence[int], compute: Callable[[int, int], "object"], dist, group=None):
     """Shard chunks by bytes, run `compute(lo, hi)` (-> int32 tensor of hi-lo CRCs) on this rank, all-gather.
 
     Returns (all CRCs as int32[n] tensor, (lo, hi) of this rank).
@@ -91,7 +86,7 @@ def distributed_batch(lengths: Sequence[int], compute: Callable[[int, int], "obj
     shards = shard_by_bytes(lengths, world)
     lo, hi = shards[rank]
     local = compute(lo, hi)
-    return gather_crcs(local, lo, hi, len(lengths), shards, dist, group=group, device=device), (lo, hi)
+    return gather_crcs(local, lo, hi, len(lengths), shards, dist, group=group), (lo, hi)
 
 
 def split_blob(total: int, world: int) -> list[tuple[int, int]]:

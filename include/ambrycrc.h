@@ -150,7 +150,13 @@ int ambrycrc_verify_dev(const uint8_t* d_base, const uint64_t* d_off, const uint
                                                (encryption key, user metadata, blob: the stream would look for
                                                the CRC elsewhere), a blob type ordinal >= 2, a blob size >
                                                Integer.MAX_VALUE (the DataCorrupt / IOException cases of
-                                               deserializeBlob*), or a record too short for its fields */
+                                               deserializeBlob*), or a record too short for its fields;
+                                               BlobProperties: a SerDe version outside 1..5, a negative
+                                               string size, a field past the span, or fields that end
+                                               before it (BlobPropertiesSerDe.java:56-77 under
+                                               MessageFormatRecord.java:1179-1195); Update: an unknown
+                                               SubRecord.Type or fields that do not end at the CRC
+                                               (:1217-1228, 1253-1266, 1388-1413) */
 
 /* Bytes of device workspace ambrycrc_verify_messages_dev needs for m messages. */
 size_t ambrycrc_messages_workspace_bytes(size_t m);
@@ -233,12 +239,19 @@ int ambrycrc_serialize_puts_dev(const ambrycrc_put_desc* d_desc, size_t m, const
 /* Status bits ambrycrc_transform_messages_dev adds to the AMBRYCRC_MSG_* verify bits. */
 #define AMBRYCRC_MSG_NOT_PUT (1u << 10)     /* an update record: "Message cannot be anything rather than put record" */
 #define AMBRYCRC_MSG_NO_ROOM (1u << 12)     /* the re-serialized message did not fit in out_cap */
+#define AMBRYCRC_MSG_NOT_ENCODABLE (1u << 13) /* a BlobProperties string holds a non-ASCII byte: the
+                                               reference's V5 re-serialization overruns its buffer,
+                                               whose size counts String.length() (BlobPropertiesSerDe
+                                               .java:43-54 vs :83-103; PutMessageFormatInputStream.java
+                                               :83-90), and the transform throws */
 
 /* Replication's ValidatingTransformer.transform (ambry-messageformat/.../ValidatingTransformer.java:46-104)
  * for m stored messages at d_msg_off[i] in [d_region, d_region + region_len): every CRC is verified
  * (ambrycrc_verify_messages_dev), update records are refused, the fields are deserialized
  * (key, encryption key, properties, user metadata, blob content / type / compression), and every
- * clean PUT is re-serialized by PutMessageFormatInputStream's layout with header version
+ * clean PUT is re-serialized by PutMessageFormatInputStream's layout -- blob properties at
+ * BlobPropertiesSerDe VERSION_5 (ValidatingTransformer.java:77,87-89; AMBRYCRC_MSG_NOT_ENCODABLE
+ * when a property string is not ASCII), blob record at Blob_Format_V3 -- with header version
  * `header_version` (1, 2 or 3: MessageFormatRecord.headerVersionToUse; V1 drops the encryption key,
  * as createStreamWithMessageHeaderV1 does) and life version d_life_version[i] (nullable: the
  * stored header's, 0 for V1/V2) -- all CRCs recomputed -- packed in message order into
@@ -302,8 +315,10 @@ int ambrycrc_verify_message_cpu(const uint8_t* region, uint64_t region_len, uint
 /* ValidatingTransformer.transform (ValidatingTransformer.java:46-104) for one stored message on
  * the CPU, as ambrycrc_transform_messages_dev does it for a batch: verify, refuse update records,
  * deserialize, re-serialize at header_version (1..3) with life_version (< 0: the stored one;
- * V1/V2 headers carry none) into out[0 .. *out_len). *status = AMBRYCRC_MSG_* verify bits |
- * AMBRYCRC_MSG_NOT_PUT / _BAD_RECORD / _NO_ROOM (out_cap too small; *out_len 0); 0 = transformed.
+ * V1/V2 headers carry none) into out[0 .. *out_len); the blob properties are re-encoded at
+ * BlobPropertiesSerDe VERSION_5 whatever version they were stored at. *status = AMBRYCRC_MSG_*
+ * verify bits | AMBRYCRC_MSG_NOT_PUT / _BAD_RECORD / _NOT_ENCODABLE / _NO_ROOM (out_cap too
+ * small; *out_len 0); 0 = transformed.
  * out must not overlap the region. */
 int ambrycrc_transform_message_cpu(const uint8_t* region, uint64_t region_len, uint64_t off, int life_version,
                                    int header_version, uint8_t* out, uint64_t out_cap, uint64_t* out_len,
@@ -382,6 +397,19 @@ int ambrycrc_batch_dev_multi(ambrycrc_comm* comm, const ambrycrc_shard* shards, 
  * sizes of all ranks (counts[nranks], identical on every rank; counts[rank] == mine->n). Every
  * rank must call it for the gather to complete. Asynchronous, as above. */
 int ambrycrc_batch_dev_gather(ambrycrc_comm* comm, const ambrycrc_shard* mine, const uint64_t* counts);
+
+/* The all-gather layout both entries above use, for shard sizes counts[nranks]: every rank sends
+ * a segment of *width CRCs (the largest count rounded up to 64); rank r's CRCs sit at
+ * [r * width, r * width + counts[r]) of the nranks * width gather buffer. *in_place (every count
+ * == width, width > 0): that buffer is d_gathered itself; otherwise a padded scratch buffer,
+ * whose segments are then copied to d_gathered[starts[r] .. starts[r + 1]) (starts[nranks + 1],
+ * prefix sums of counts). Any output pointer may be NULL. Host arithmetic, no device. */
+int ambrycrc_gather_layout(const uint64_t* counts, int nranks, uint64_t* width, int* in_place, uint64_t* starts);
+
+/* The compaction step of that layout on host memory: out[starts[r] ..] = padded[r * width ..]
+ * for every rank (the same copy list the device path enqueues; a gloo / host-side gather of the
+ * padded segments finishes here). padded holds nranks * width words, out sum(counts). */
+int ambrycrc_gather_compact_host(const uint32_t* padded, const uint64_t* counts, int nranks, uint32_t* out);
 
 /* One-pass PUT CRCs (§8f row 2). For each of n PUT requests whose blob CRC blob_crc[i]
  * (over blob_len[i] bytes, e.g. from ambrycrc_batch_dev/ambrycrc_batch_host) is known:

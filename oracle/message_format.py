@@ -24,7 +24,8 @@ Restated from ambry-messageformat/src/main/java/com/github/ambry/messageformat/:
                then encryption key (if present), blob properties, user metadata, blob.
   PutMessageFormatInputStream.java:76-124,133-162 (record order and relative offsets)
   ValidatingTransformer.java:46-104 (transform: verify, deserialize, re-serialize a PUT)
-  BlobPropertiesSerDe.java:43-103 (VERSION_5 layout)
+  BlobPropertiesSerDe.java:43-103 (VERSION_1..5 read, VERSION_5 written)
+  Utils.java:233-283,860-892 (int-length strings)
 Every record's CRC covers [record start, record end - 8) and is stored as a
 big-endian long with the upper 32 bits zero. CRCs come from zlib.crc32, the
 function java.util.zip.CRC32 computes.
@@ -49,6 +50,7 @@ BAD_VERSION = 1 << 8
 BAD_LAYOUT = 1 << 9
 NOT_PUT = 1 << 10      # transform only: an update record
 BAD_RECORD = 1 << 11   # a record's size field disagrees with its span, bad blob type/size, record too short
+NOT_ENCODABLE = 1 << 13  # transform only: the properties cannot be re-serialized (serialize_blob_properties_v5)
 
 RECORD_BITS = (ENCKEY_CRC, PROPS_CRC, UPDATE_CRC, USERMETA_CRC, BLOB_CRC)  # slot order enc, bp, upd, um, blob
 
@@ -76,19 +78,140 @@ def store_key(blob_id: str) -> bytes:
 def _int_string(s):
     if s is None:
         return struct.pack(">i", 0)
-    raw = s.encode()
+    raw = s if isinstance(s, bytes) else s.encode()
     return struct.pack(">i", len(raw)) + raw
 
 
 def blob_properties_bytes(blob_size, service_id="servid", owner_id="owner", content_type="application/octet",
                           ttl=-1, private=False, creation_ms=1_700_000_000_000, account=101, container=5,
-                          encrypted=False, content_encoding=None, filename=None, reserved=None):
-    """BlobPropertiesSerDe.serializeBlobProperties, VERSION_5 (BlobPropertiesSerDe.java:80-103)."""
-    out = struct.pack(">hqbqq", 5, ttl, 1 if private else 0, creation_ms, blob_size)
+                          encrypted=False, content_encoding=None, filename=None, reserved=None, serde_version=5):
+    """BlobPropertiesSerDe bytes at `serde_version` 1..5: serializeBlobProperties writes VERSION_5
+    (BlobPropertiesSerDe.java:83-103); versions 1..4 are the layouts getBlobPropertiesFromStream
+    still reads (:56-77) -- older servers wrote them: V1 has no account/container, V1-V2 no
+    `encrypted` byte, V1-V3 no contentEncoding/filename, V1-V4 no reservedMetadataBlobId.
+    `private` / `encrypted` may be an int to store a non-canonical byte (the reader tests `== 1`)."""
+    v = serde_version
+    out = struct.pack(">hqbqq", v, ttl, int(private), creation_ms, blob_size)
     out += _int_string(content_type) + _int_string(owner_id) + _int_string(service_id)
-    out += struct.pack(">hhb", account, container, 1 if encrypted else 0)
-    out += _int_string(content_encoding) + _int_string(filename) + _int_string(reserved)
+    if v > 1:
+        out += struct.pack(">hh", account, container)
+    if v > 2:
+        out += struct.pack(">b", int(encrypted))
+    if v > 3:
+        out += _int_string(content_encoding) + _int_string(filename)
+    if v > 4:
+        out += _int_string(reserved)
     return out
+
+
+class PropsParseError(Exception):
+    """getBlobPropertiesFromStream threw (IllegalArgumentException / EOFException): the record
+    deserializer maps every such exception to DataCorrupt (MessageFormatRecord.java:1192-1195)."""
+
+
+class NotEncodable(Exception):
+    """serializeBlobProperties cannot re-write these properties: see serialize_blob_properties_v5."""
+
+
+UNKNOWN_ACCOUNT_ID = -1    # Account.UNKNOWN_ACCOUNT_ID (ambry-api/.../account/Account.java:111)
+UNKNOWN_CONTAINER_ID = -1  # Container.UNKNOWN_CONTAINER_ID (Container.java:97)
+
+
+def parse_blob_properties(b: bytes, pos: int, end: int):
+    """BlobPropertiesSerDe.getBlobPropertiesFromStream (BlobPropertiesSerDe.java:56-77) over
+    b[pos:end): (fields dict, parsed end). Big-endian DataInputStream reads; a read past `end`
+    is the EOFException; strings are Utils.readIntString (Utils.java:265-283: a negative size
+    throws) and, from V4, readNullableIntString (:253-256: empty -> null). Strings are kept as
+    their raw bytes (decoding is a separate question: serialize_blob_properties_v5)."""
+    def take(n):
+        nonlocal pos
+        if n < 0 or pos + n > end:
+            raise PropsParseError("EOF")
+        s = b[pos:pos + n]
+        pos += n
+        return s
+
+    def int_string(nullable=False):
+        n = struct.unpack(">i", take(4))[0]
+        if n < 0:
+            raise PropsParseError("readIntString: the size cannot be negative")
+        s = take(n)
+        return None if (nullable and n == 0) else s
+
+    v = struct.unpack(">h", take(2))[0]
+    if v < 1 or v > 5:
+        raise PropsParseError("stream has unknown blob property version %d" % v)
+    ttl, priv, ctime, size = struct.unpack(">qbqq", take(25))
+    f = {"version": v, "ttl": ttl, "private": priv == 1, "creation": ctime, "size": size}
+    f["content_type"] = int_string()
+    f["owner"] = int_string()
+    f["service"] = int_string()
+    f["account"], f["container"] = (struct.unpack(">hh", take(4)) if v > 1
+                                    else (UNKNOWN_ACCOUNT_ID, UNKNOWN_CONTAINER_ID))
+    f["encrypted"] = v > 2 and struct.unpack(">b", take(1))[0] == 1
+    f["content_encoding"] = int_string(True) if v > 3 else None
+    f["filename"] = int_string(True) if v > 3 else None
+    f["reserved"] = int_string(True) if v > 4 else None
+    return f, pos
+
+
+_PROPS_STRINGS = ("content_type", "owner", "service", "content_encoding", "filename", "reserved")
+
+
+def serialize_blob_properties_v5(f) -> bytes:
+    """BlobPropertiesSerDe.serializeBlobProperties at CURRENT_VERSION = VERSION_5
+    (BlobPropertiesSerDe.java:41,83-103), of properties parse_blob_properties read.
+
+    Each string was decoded as UTF-8 (Utils.readIntString, Utils.java:265-283) and is re-encoded
+    with Charset.defaultCharset() (Utils.serializeNullableString / serializeString, :860-866,
+    888-892) -- UTF-8 assumed (the JDK 18+ default, JEP 400; a UTF-8 locale before). ASCII bytes
+    round-trip unchanged. Any other byte makes the encoded string longer than String.length(),
+    which is what getBlobPropertiesSerDeSize (:43-54, Utils.getIntStringLength :233-235) budgets:
+    PutMessageFormatInputStream sizes its buffer from that budget (PutMessageFormatInputStream.java
+    :83-90), so the extra bytes overrun it (BufferOverflowException) and the transform fails
+    (ValidatingTransformer.java:100-102). NotEncodable models that."""
+    for k in _PROPS_STRINGS:
+        s = f[k]
+        if s is not None and any(c >= 0x80 for c in s):
+            raise NotEncodable(k)
+    out = struct.pack(">hqbqq", 5, f["ttl"], 1 if f["private"] else 0, f["creation"], f["size"])
+    for k in _PROPS_STRINGS[:3]:
+        out += struct.pack(">i", len(f[k])) + f[k]
+    out += struct.pack(">hhb", f["account"], f["container"], 1 if f["encrypted"] else 0)
+    for k in _PROPS_STRINGS[3:]:
+        s = f[k] or b""  # serializeNullableString: null -> int 0
+        out += struct.pack(">i", len(s)) + s
+    return out
+
+
+UPDATE_TYPES = 3  # SubRecord.Type: DELETE, TTL_UPDATE, UNDELETE (SubRecord.java:26-28)
+
+
+def _update_check(rec: bytes) -> int:
+    """deserializeUpdateRecord (MessageFormatRecord.java:158-172) over a record span, stored CRC
+    included: Update_Format_V1 (:1217-1228) reads a byte, V2 (:1253-1266) account, container and
+    update time, V3 (:1388-1413) those, a short type indexing SubRecord.Type.values() (out of range
+    throws), then the sub-record -- a short version that must be 1 (:1422-1464, UnknownFormatVersion
+    otherwise) and, for TTL_UPDATE, a long expiry -- before the CRC. The parsed end must be the span's
+    CRC position (else the reference reads its CRC elsewhere)."""
+    v = _be16(rec, 0)
+    body = len(rec) - CRC_SIZE
+    if v == 1:
+        return 0 if body == 3 else BAD_RECORD
+    if v == 2:
+        return 0 if body == 14 else BAD_RECORD
+    if v != 3:
+        return BAD_VERSION
+    if body < 16:
+        return BAD_RECORD
+    t = _be16(rec, 14)
+    if not 0 <= t < UPDATE_TYPES:
+        return BAD_RECORD
+    if body < 18:
+        return BAD_RECORD
+    if _be16(rec, 16) != 1:
+        return BAD_VERSION
+    return 0 if body == (26 if t == 1 else 18) else BAD_RECORD
 
 
 def props_record(props: bytes) -> bytes:
@@ -182,8 +305,11 @@ def _record_check(k: int, rec: bytes) -> int:
     (deserializeAndGet*WithVersion :147-239 throw UnknownFormatVersion), then the size fields that
     decide where the stream reads the CRC -- BlobEncryptionKey_Format_V1 (:1588-1600) and
     UserMetadata_Format_V1 (:1637-1649): int size + bytes; Blob_Format_V1..V3 (:1681-1833): type
-    ordinal < 2, long size <= Integer.MAX_VALUE. `rec` is the record's span from the header,
-    stored CRC included. BlobProperties / Update records: the version only."""
+    ordinal < 2, long size <= Integer.MAX_VALUE. BlobProperties_Format_V1 (:1179-1195): the
+    BlobPropertiesSerDe fields (parse_blob_properties), any exception -> DataCorrupt. Update
+    records: _update_check. `rec` is the record's span from the header, stored CRC included; a
+    parsed end other than the span's CRC position is BAD_RECORD (the reference would read its CRC
+    from other bytes)."""
     if len(rec) < 10:
         return BAD_RECORD
     v = _be16(rec, 0)
@@ -195,9 +321,15 @@ def _record_check(k: int, rec: bytes) -> int:
         n = _be32(rec, 2)
         return 0 if n >= 0 and n + 14 == len(rec) else BAD_RECORD
     if k == 1:
-        return 0 if v == 1 else BAD_VERSION
+        if v != 1:
+            return BAD_VERSION
+        try:
+            _, end = parse_blob_properties(rec, 2, len(rec) - CRC_SIZE)
+        except PropsParseError:
+            return BAD_RECORD
+        return 0 if end == len(rec) - CRC_SIZE else BAD_RECORD
     if k == 2:
-        return 0 if 1 <= v <= 3 else BAD_VERSION
+        return _update_check(rec)
     if not 1 <= v <= 3:
         return BAD_VERSION
     head = {1: 10, 2: 12, 3: 13}[v]
@@ -281,7 +413,13 @@ def transform_message(region: bytes, off: int, life=None, version: int = 3):
         enc_key = region[off + enc + 6:off + enc + 6 + n]
     if um - 8 < bp + 2:
         return BAD_RECORD, None
-    props = region[off + bp + 2:off + um - 8]
+    # deserializeBlobProperties, then serializeBlobProperties at VERSION_5 (ValidatingTransformer.java
+    # :77,87-89 -> PutMessageFormatInputStream.java:114 -> BlobPropertiesSerDe.java:83-103)
+    fields, _ = parse_blob_properties(region, off + bp + 2, off + um - 8)  # verify_message parsed it
+    try:
+        props = serialize_blob_properties_v5(fields)
+    except NotEncodable:
+        return NOT_ENCODABLE, None
     n = _be32(region, off + um + 2)
     if n < 0 or um + 6 + n + 8 != blob:
         return BAD_RECORD, None

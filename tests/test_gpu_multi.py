@@ -72,6 +72,49 @@ def test_batch_dev_gather_rank_form(gpu, oracle):
         comm.destroy()
 
 
+def test_padded_gather_two_streams(gpu, oracle):
+    """Two padded-layout batches in flight at once on two streams (unequal counts, neither a
+    multiple of 64), then the first stream again with a larger count (its scratch regrows): each
+    stream has its own gather scratch, so the second batch's CRC kernel cannot overwrite the
+    first's segment before its all-gather and compaction ran. Then nine more streams, past the
+    per-device scratch cap (the least recently used buffer is reused after its event fired)."""
+    torch = _torch()
+    comm = gpu.Comm.all_devices([0])
+    try:
+        streams = [torch.cuda.Stream() for _ in range(2)]
+        jobs = []
+        for k, (n, max_len, s) in enumerate(((5000, 400000, streams[0]), (70, 3000, streams[1]),
+                                             (9000, 100000, streams[0]))):
+            mem, off, ln = _batch(900 + k, n, max_len, mem_bytes=32 << 20)
+            base, o, l = _dev(torch, mem, off, ln)
+            jobs.append((mem, off, ln, base, o, l, s))
+        torch.cuda.synchronize()
+        outs = []
+        for mem, off, ln, base, o, l, s in jobs:  # no sync between the launches
+            g = torch.full((len(off),), -1, dtype=torch.int32, device="cuda")
+            with torch.cuda.stream(s):
+                gpu.crc32_batch_multi_dev(comm, [dict(base=base, off=o, len=l, gathered=g, stream=s)])
+            outs.append(g)
+        torch.cuda.synchronize()
+        for (mem, off, ln, *_), g in zip(jobs, outs):
+            assert np.array_equal(g.cpu().numpy().view(np.uint32), oracle.batch(mem, off, ln, threads=8)), len(off)
+        mem, off, ln = _batch(990, 333, 5000)
+        base, o, l = _dev(torch, mem, off, ln)
+        exp = oracle.batch(mem, off, ln, threads=8)
+        extra = [torch.cuda.Stream() for _ in range(9)]
+        gs = []
+        for s in extra:
+            g = torch.full((333,), -1, dtype=torch.int32, device="cuda")
+            with torch.cuda.stream(s):
+                gpu.crc32_batch_multi_dev(comm, [dict(base=base, off=o, len=l, gathered=g, stream=s)])
+            gs.append(g)
+        torch.cuda.synchronize()
+        for g in gs:
+            assert np.array_equal(g.cpu().numpy().view(np.uint32), exp)
+    finally:
+        comm.destroy()
+
+
 def test_multi_entry_argument_checks(gpu):
     torch = _torch()
     from ambry_amd._lib import AmbryCrcError

@@ -29,8 +29,18 @@ def _dev(b):
     return torch.frombuffer(bytearray(b if len(b) else b"\0"), dtype=torch.uint8).cuda()
 
 
+def _far(b, at):
+    """b in device memory `at` bytes into a larger allocation (a view whose buffer starts lower)."""
+    import torch
+
+    d = _dev(b)
+    big = torch.full((d.numel() + at,), 0x5A, dtype=torch.uint8, device="cuda")
+    big[at:] = d
+    return big[at:]
+
+
 def _run(gpu, mf, msgs, out_align, field_align, gap, in_place=False, place=("key", "enckey", "props", "usermeta",
-                                                                           "blob")):
+                                                                           "blob"), far=0):
     import torch
 
     from ambry_amd.messages import layout, pack_batch, serialize_dev
@@ -46,8 +56,9 @@ def _run(gpu, mf, msgs, out_align, field_align, gap, in_place=False, place=("key
                     host_out[o + fo[name]:o + fo[name] + len(b)] = b
     out = _dev(bytes(host_out))
     mlen = torch.empty(len(msgs), dtype=torch.int64, device="cuda")
-    fields_in = None if in_place and "key" in place else _dev(fields)
-    blobs_in = None if in_place and "blob" in place else _dev(blobs)
+    dev_in = (lambda b: _far(b, far)) if far else _dev
+    fields_in = None if in_place and "key" in place else dev_in(fields)
+    blobs_in = None if in_place and "blob" in place else dev_in(blobs)
     serialize_dev(_dev(descs.tobytes()), out, fields_in, blobs_in, msg_len=mlen)
     torch.cuda.synchronize()
     got = out.cpu().numpy().tobytes()
@@ -76,6 +87,28 @@ def test_serialize_batch_in_place(gpu, mf):
 def test_serialize_group_phase_batch(gpu, mf):
     """4,000 messages = 20,000 CRC jobs (>= 16,384: the group phase takes the small records)."""
     _run(gpu, mf, random_messages(mf, 4000, seed=9, max_blob=9000), 1, 3, 0)
+
+
+@pytest.mark.parametrize("far", [(64 << 20) + 3, (1 << 30) + 11])
+def test_serialize_class0_heavy_far_sources(gpu, mf, far):
+    """Round-2 fault regression (an experimental class-0 tail load read the sweep's base block, and the
+    copy-through then passed base = null): 6,000 PUTs whose every field is <= 256 B (30,000 jobs, all
+    in group class 0 of the copy-through sweep), sources placed `far` bytes into their allocations.
+    The copy-through's base is now the lowest source buffer (PutArgs::src_base)."""
+    from ambry_amd.messages import PutMessage
+
+    from datagen import stream_bytes
+
+    rng = np.random.default_rng(far & 0xFFFF)
+    msgs = []
+    for i in range(6000):
+        blen = int(rng.integers(0, 200))
+        enc = stream_bytes(i, 5, int(rng.integers(0, 64))).tobytes() if i % 3 else None
+        msgs.append(PutMessage(key=mf.store_key("c0-%d" % i), props=mf.blob_properties_bytes(blen, service_id="s%d" % i),
+                               usermeta=stream_bytes(i, 7 << 20, int(rng.integers(0, 120))).tobytes(),
+                               blob=stream_bytes(i ^ 77, 0, blen).tobytes(), enckey=enc, header_version=3,
+                               life_version=i % 4))
+    _run(gpu, mf, msgs, 1, 1, 0, far=far)
 
 
 def test_serialize_large_blobs(gpu, mf):

@@ -24,6 +24,23 @@ def _blob_v1_message(mf, key, props, um, content, version):
                      bp + len(pr) + len(ur), 0) + key + pr + ur + bl
 
 
+def stored_props(mf, rng, blen, i):
+    """BlobPropertiesSerDe bytes as servers of every version stored them (V1..V5), some with
+    non-canonical private / encrypted bytes (read as `== 1`), a few with a non-ASCII string
+    (the transform cannot re-encode those: NOT_ENCODABLE)."""
+    v = int(rng.choice([1, 2, 3, 4, 5], p=[0.15, 0.15, 0.15, 0.15, 0.4]))
+    odd = rng.random() < 0.15
+    s = rng.random()
+    owner = b"own\xc3\xa9r" if s < 0.03 else ("o%d" % (i % 5) if s < 0.8 else None)
+    return mf.blob_properties_bytes(
+        blen, service_id="s%d" % (i % 7), owner_id=owner, content_type=None if i % 9 == 0 else "application/x",
+        ttl=int(rng.integers(-1, 10**6)), private=int(rng.choice([0, 1, 2])) if odd else bool(i % 2),
+        encrypted=int(rng.choice([0, 1, 5])) if odd else bool(i % 3 == 0),
+        content_encoding="gzip" if i % 4 == 0 else None, filename="file-%d.bin" % i if i % 5 else None,
+        reserved="res%d" % i if i % 6 == 0 else None, account=int(rng.integers(-5, 30000)), container=i % 300,
+        serde_version=v)
+
+
 def build_region(mf, n, seed, corrupt=True):
     rng = np.random.default_rng(seed)
     msgs = []
@@ -34,7 +51,7 @@ def build_region(mf, n, seed, corrupt=True):
         blen = int(rng.choice([0, 1, 100, 4096, 4109, 70000]))
         content = stream_bytes(seed + i, 0, blen).tobytes()
         um = stream_bytes(seed + i, 1 << 20, int(rng.choice([0, 7, 1000]))).tobytes()
-        props = mf.blob_properties_bytes(blen, service_id="s%d" % (i % 7))
+        props = stored_props(mf, rng, blen, i)
         if kind < 0.08:
             m = mf.update_message(key, version=3)
         elif kind < 0.14:
@@ -86,7 +103,8 @@ def test_transform_matches_oracle(gpu, mf, version):
         assert out_h[pos:pos + len(exp)] == exp, i
         assert mf.verify_message(out_h, pos) == (0, pos + len(exp))
         pos += len(exp)
-    assert 0 in kinds and mf.NOT_PUT in kinds and mf.BAD_RECORD in kinds and len(kinds) >= 4
+    assert 0 in kinds and mf.NOT_PUT in kinds and mf.BAD_RECORD in kinds and mf.NOT_ENCODABLE in kinds
+    assert len(kinds) >= 5
 
 
 def test_transform_out_of_room(gpu, mf):

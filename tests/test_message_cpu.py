@@ -48,7 +48,7 @@ def test_transform_matches_oracle(ambry, version, life):
         assert st == exp_st, o
         assert got == exp, o
         kinds.add(st)
-    assert 0 in kinds and MF.NOT_PUT in kinds and MF.BAD_RECORD in kinds
+    assert 0 in kinds and MF.NOT_PUT in kinds and MF.BAD_RECORD in kinds and MF.NOT_ENCODABLE in kinds
 
 
 def test_transform_no_room_and_args(ambry):
@@ -61,3 +61,26 @@ def test_transform_no_room_and_args(ambry):
     assert transform_message_cpu(msg, 0, out_cap=len(msg)) == (0, msg)
     with pytest.raises(AmbryCrcError):
         transform_message_cpu(msg, 0, header_version=4)
+
+
+def test_verdict_probes_props(ambry):
+    """Round-2 review probes: a CRC-valid properties record at SerDe version 9 is DataCorrupt
+    (BlobPropertiesSerDe.java:58-60 under MessageFormatRecord.java:1192-1195), and a message whose
+    properties are stored at SerDe V1 comes out of the transform re-encoded at V5
+    (ValidatingTransformer.java:77,87-89 -> BlobPropertiesSerDe.java:83-103): new bytes, new CRC."""
+    import struct
+
+    from ambry_amd.messages import transform_message_cpu, verify_message_cpu
+
+    key, um, content = MF.store_key("probe"), b"meta", bytes(range(50))
+    v5 = MF.blob_properties_bytes(50, content_encoding="gzip")
+    bad = MF.put_message(key, struct.pack(">h", 9) + v5[2:], um, content)
+    assert verify_message_cpu(bad, 0) == (MF.BAD_RECORD, len(bad))
+    v1 = MF.blob_properties_bytes(50, serde_version=1, private=True)
+    msg = MF.put_message(key, v1, um, content)
+    st, out = transform_message_cpu(msg, 0)
+    assert st == 0 and out != msg
+    want = MF.put_message(key, MF.blob_properties_bytes(50, serde_version=5, private=True, account=-1, container=-1),
+                          um, content)
+    assert out == want and MF.transform_message(msg, 0) == (0, want)
+    assert verify_message_cpu(out, 0) == (0, len(out))

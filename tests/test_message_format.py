@@ -149,7 +149,112 @@ def record_level_cases():
     upd[0:2] = struct.pack(">h", 4)
     cases.append((_assemble(3, key, None, None, None, None, upd=_seal(bytes(upd[:-8]))), MF.BAD_VERSION))
     cases.append((_assemble(3, key, None, None, None, None, upd=MF.update_record_v3(kind="delete")), 0))
+    cases += props_level_cases(key, um, bl) + update_level_cases(key)
     return cases
+
+
+def _props_msg(key, um, bl, serde: bytes, version=3):
+    return _assemble(version, key, None, _seal(struct.pack(">h", 1) + serde), um, bl)
+
+
+def props_level_cases(key, um, bl):
+    """CRC-valid BlobProperties records through BlobPropertiesSerDe.getBlobPropertiesFromStream
+    (BlobPropertiesSerDe.java:56-77) under deserializeBlobPropertiesRecord's catch-all
+    (MessageFormatRecord.java:1179-1195: any exception -> DataCorrupt = BAD_RECORD)."""
+    cases = []
+    for v in (1, 2, 3, 4, 5):  # every stored version reads clean
+        cases.append((_props_msg(key, um, bl, MF.blob_properties_bytes(
+            300, serde_version=v, content_encoding="gzip", filename="f", reserved="r")), 0))
+    good = MF.blob_properties_bytes(300, content_encoding="gzip", filename="name.bin")
+    for bad_v in (0, 6, 9, -1):  # "stream has unknown blob property version"
+        cases.append((_props_msg(key, um, bl, struct.pack(">h", bad_v) + good[2:]), MF.BAD_RECORD))
+    # contentType's int size: past the span / negative / one short (the fields end early)
+    ct = 27
+    for n, want in ((1 << 20, MF.BAD_RECORD), (-2, MF.BAD_RECORD), (0x7FFFFFFF, MF.BAD_RECORD)):
+        b = bytearray(good)
+        b[ct:ct + 4] = struct.pack(">i", n)
+        cases.append((_props_msg(key, um, bl, bytes(b)), want))
+    cases.append((_props_msg(key, um, bl, good + b"\0"), MF.BAD_RECORD))  # trailing byte: CRC read early
+    cases.append((_props_msg(key, um, bl, good[:-1]), MF.BAD_RECORD))      # last string cut: EOF
+    cases.append((_props_msg(key, um, bl, good[:20]), MF.BAD_RECORD))      # inside the fixed fields
+    v4 = MF.blob_properties_bytes(300, serde_version=4, filename="abc")
+    cases.append((_props_msg(key, um, bl, v4[:-7] + struct.pack(">i", -1) + b"abc"), MF.BAD_RECORD))
+    # non-canonical private / encrypted bytes and non-ASCII strings still verify (decoding never throws)
+    cases.append((_props_msg(key, um, bl, MF.blob_properties_bytes(300, private=7, encrypted=2)), 0))
+    cases.append((_props_msg(key, um, bl, MF.blob_properties_bytes(300, owner_id=b"\xc3\xa9t\xff")), 0))
+    return cases
+
+
+def update_level_cases(key):
+    """CRC-valid update records through deserializeUpdateRecord (MessageFormatRecord.java:158-172,
+    1217-1228, 1253-1266, 1388-1464)."""
+    def upd_msg(body):
+        return _assemble(3, key, None, None, None, None, upd=_seal(body))
+
+    base = struct.pack(">hhhq", 3, 101, 5, 1_700_000_000_123)
+    return [
+        (upd_msg(struct.pack(">hb", 1, 1)), 0),                                  # V1: a delete flag
+        (upd_msg(struct.pack(">hb", 1, 1) + b"x"), MF.BAD_RECORD),
+        (upd_msg(struct.pack(">hhhq", 2, 101, 5, 7)), 0),                          # V2
+        (upd_msg(struct.pack(">hhhq", 2, 101, 5, 7)[:-1]), MF.BAD_RECORD),
+        (upd_msg(base + struct.pack(">hhq", 1, 1, 99)), 0),                        # V3 TTL_UPDATE
+        (upd_msg(base + struct.pack(">hh", 2, 1)), 0),                             # V3 UNDELETE
+        (upd_msg(base + struct.pack(">hh", 3, 1)), MF.BAD_RECORD),                 # Type.values()[3]
+        (upd_msg(base + struct.pack(">hh", -1, 1)), MF.BAD_RECORD),
+        (upd_msg(base + struct.pack(">hh", 0, 2)), MF.BAD_VERSION),                # delete sub-record v2
+        (upd_msg(base + struct.pack(">hhq", 1, 0, 99)), MF.BAD_VERSION),           # ttl sub-record v0
+        (upd_msg(base + struct.pack(">hh", 0, 1) + bytes(8)), MF.BAD_RECORD),      # delete + 8 stray bytes
+        (upd_msg(base + struct.pack(">hh", 1, 1)), MF.BAD_RECORD),                 # TTL without its expiry
+        (upd_msg(base), MF.BAD_RECORD),                                          # no type
+        (upd_msg(struct.pack(">hhhq", 0, 1, 1, 1) + bytes(2)), MF.BAD_VERSION),
+    ]
+
+
+def test_blob_properties_versions_match_reference_test():
+    """BlobPropertiesTest.basicTest (ambry-messageformat/src/test/.../BlobPropertiesTest.java:68-202)
+    restated over the layouts its serializeBlobPropertiesInVersion writes (:209-275): what
+    getBlobPropertiesFromStream must return at each version -- account/container UNKNOWN (-1) at
+    V1, `encrypted` only from V3, contentEncoding/filename only from V4, the reserved metadata id
+    only at V5, null owner/contentType read back as "" (readIntString) and null nullable strings
+    as null -- and the V5 re-serialization (serializeBlobProperties, BlobPropertiesSerDe.java:83-103)."""
+    acct, cont, ttl, ctime = 1234, -77, 144, 1_700_000_000_555
+    for v in (1, 2, 3, 4, 5):
+        for enc in (False, True):
+            ce, fn = ("gzip", "filename") if v >= 4 else (None, None)
+            raw = MF.blob_properties_bytes(100, service_id="ServiceId", owner_id="OwnerId", content_type="ContentType",
+                                           ttl=ttl, private=True, creation_ms=ctime, account=acct, container=cont,
+                                           encrypted=enc, content_encoding=ce, filename=fn, reserved="blobid",
+                                           serde_version=v)
+            f, end = MF.parse_blob_properties(raw, 0, len(raw))
+            assert end == len(raw)
+            assert (f["size"], f["service"], f["owner"], f["content_type"]) == (100, b"ServiceId", b"OwnerId",
+                                                                                b"ContentType")
+            assert (f["private"], f["ttl"], f["creation"]) == (True, ttl, ctime)
+            assert (f["account"], f["container"]) == ((acct, cont) if v > 1 else (-1, -1))
+            assert f["encrypted"] == (v >= 3 and enc)
+            assert (f["content_encoding"], f["filename"]) == ((b"gzip", b"filename") if v >= 4 else (None, None))
+            assert f["reserved"] == (b"blobid" if v == 5 else None)
+            v5 = MF.serialize_blob_properties_v5(f)
+            g, _ = MF.parse_blob_properties(v5, 0, len(v5))
+            assert {k: x for k, x in g.items() if k != "version"} == {k: x for k, x in f.items() if k != "version"}
+            assert v5 == MF.blob_properties_bytes(100, service_id="ServiceId", owner_id="OwnerId",
+                                                  content_type="ContentType", ttl=ttl, private=True, creation_ms=ctime,
+                                                  account=f["account"], container=f["container"],
+                                                  encrypted=f["encrypted"], content_encoding=ce, filename=fn,
+                                                  reserved="blobid" if v == 5 else None)
+    # null owner / contentType serialize as int 0 and read back as "" (not null): the same bytes
+    raw = MF.blob_properties_bytes(100, owner_id=None, content_type=None, serde_version=2)
+    f, _ = MF.parse_blob_properties(raw, 0, len(raw))
+    assert f["owner"] == b"" and f["content_type"] == b""
+    assert MF.serialize_blob_properties_v5(f)[27:35] == bytes(8)
+
+
+def test_props_not_encodable():
+    for s in (b"\x80", b"caf\xc3\xa9", b"\xf0\x9f\x98\x80"):
+        raw = MF.blob_properties_bytes(1, filename=s)
+        f, _ = MF.parse_blob_properties(raw, 0, len(raw))
+        with pytest.raises(MF.NotEncodable):
+            MF.serialize_blob_properties_v5(f)
 
 
 def test_oracle_record_level_checks():

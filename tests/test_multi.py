@@ -3,6 +3,7 @@
 On MI355X the same code runs one process per GPU over RCCL (bench.py --gpus N);
 here the per-rank compute is libambrycrc's host primitive, so the sharding,
 padding and gather logic is what is under test."""
+import bisect
 import os
 import socket
 import zlib
@@ -39,13 +40,31 @@ def test_shard_by_bytes_covers_everything():
     assert shard_by_bytes([0, 0, 0, 0], 2) == [(0, 2), (2, 4)]
 
 
-def test_shard_by_bytes_matches_c_abi(ambry):
-    """The Python mirror and ambrycrc_shard_by_bytes (used by ambrycrc_batch_multi,
-    ambrycrc_batch_cpu and bench.py's multi-GPU shards) give the same cuts, including when a
-    chunk starts exactly on a shard boundary and for totals past 2^32."""
-    from ambry_amd import device as D
-    from ambry_amd.multi import shard_by_bytes
+def _ref_shard_by_bytes(lengths, world):
+    """The cut rule, stated independently for the test: rank r takes the chunks whose start byte s
+    satisfies r/world <= s/total < (r+1)/world (exact integers); an all-empty batch splits by count."""
+    lengths = np.asarray(lengths, dtype=object)
+    n = len(lengths)
+    starts, acc = [], 0
+    for x in lengths:
+        starts.append(acc)
+        acc += int(x)
+    total = acc
+    scaled = [s * world for s in starts]
+    bounds = []
+    for r in range(world):
+        bounds.append((n * r) // world if total == 0 else bisect.bisect_left(scaled, total * r))
+    bounds.append(n)
+    return [(bounds[r], bounds[r + 1]) for r in range(world)]
 
+
+def test_shard_by_bytes_matches_rule(ambry):
+    """ambrycrc_shard_by_bytes (used by ambrycrc_batch_multi, ambrycrc_batch_cpu, bench.py's
+    multi-GPU shards and ambry_amd.multi) against the rule restated above, including chunks that
+    start exactly on a shard boundary and totals past 2^32."""
+    from ambry_amd import device as D
+
+    shard_by_bytes = _ref_shard_by_bytes
     rng = np.random.default_rng(11)
     cases = [[4] * 8, [4] * 9, [0, 0, 0], [], [1], [0, 5, 0, 5, 0], [1 << 40, 1, 1, 1 << 40],
              [4 << 20] * 65536, [3, 3, 3, 3, 3, 3, 3]]
@@ -56,8 +75,9 @@ def test_shard_by_bytes_matches_c_abi(ambry):
             assert D.shard_by_bytes(lens, world) == shard_by_bytes(lens, world), (lens[:10], world)
 
 
-def test_gather_layout_index_math():
-    """Segment width, in-place case and compaction offsets of the CRC all-gather."""
+def test_gather_layout_index_math(ambry):
+    """Segment width, in-place case and compaction offsets of the CRC all-gather: the C arithmetic
+    ambrycrc_batch_dev_multi / _gather run (ambrycrc_gather_layout), through ctypes."""
     from ambry_amd.multi import gather_layout
 
     assert gather_layout([64, 64, 64]) == (64, True, [0, 64, 128, 192])
@@ -74,7 +94,28 @@ def test_gather_layout_index_math():
         w, inplace, starts = gather_layout(counts)
         assert w % 64 == 0 and w >= max(counts) and w - max(counts) < 64
         assert starts[-1] == sum(counts)
+        assert starts == [0] + np.cumsum(counts).tolist()
         assert inplace == (w > 0 and all(c == w for c in counts))
+
+
+def test_gather_compact_host(ambry):
+    """ambrycrc_gather_compact_host runs the device path's copy list on host memory: rank r's
+    segment [r*width, r*width + counts[r]) of the padded buffer lands at starts[r]; the in-place
+    layout is the identity."""
+    from ambry_amd.multi import gather_compact, gather_layout
+
+    rng = np.random.default_rng(4)
+    for trial in range(100):
+        counts = rng.integers(0, 300, size=int(rng.integers(1, 9))).tolist()
+        if trial % 10 == 0:
+            counts = [128] * len(counts)
+        w, inplace, starts = gather_layout(counts)
+        padded = rng.integers(0, 1 << 32, size=max(w, 1) * len(counts), dtype=np.uint64).astype(np.uint32)
+        got = gather_compact(padded, counts)
+        exp = np.concatenate([padded[r * w:r * w + c] for r, c in enumerate(counts)] + [np.zeros(0, np.uint32)])
+        assert np.array_equal(got, exp), counts
+        if inplace:
+            assert np.array_equal(got, padded[:sum(counts)])
 
 
 def _worker(rank, world, port, q):
