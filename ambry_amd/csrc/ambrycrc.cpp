@@ -345,7 +345,8 @@ int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uin
     }
     if (hipEventRecord(ev.a, s) != hipSuccess) return AMBRYCRC_EHIP;
   }
-  e = copy_dst ? launch_sweep_copy(t, c->grid, s) : launch_sweep(t, c->grid, c->variant, s);
+  e = copy_dst ? launch_sweep_copy(t, c->grid, c->variant == kVariantSplit ? kVariantSplit : kVariantDefault, s)
+               : launch_sweep(t, c->grid, c->variant, s);
   if (e != hipSuccess) return AMBRYCRC_EHIP;
   if (c->timing) {
     if (hipEventRecord(ev.b, s) != hipSuccess) return AMBRYCRC_EHIP;

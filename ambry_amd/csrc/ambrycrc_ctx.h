@@ -59,7 +59,10 @@ struct DevCtx {
   // the loads; plus, for batches of >= kGroupMinChunks chunks, whole chunks <= 16 KiB in the
   // fused group phase, each size class spread over all waves with a class-sized group
   // (G = 2 / 8 / 16 lanes). Measured against the round-1 alternatives in DESIGN.md §4-5.
-  int variant = kVariantDefault;
+#ifndef AMBRY_DEFAULT_VARIANT
+#define AMBRY_DEFAULT_VARIANT kVariantDefault
+#endif
+  int variant = AMBRY_DEFAULT_VARIANT;  // (A/B builds: -DAMBRY_DEFAULT_VARIANT=...)
   // Sweep rounds of at most this many bytes (SweepArgs::window); 0 = one round.
   uint64_t window = 32ull << 30;
   uint32_t* d_img = nullptr;

@@ -72,7 +72,7 @@ int enqueue_serialize(DevCtx* c, const ::ambrycrc_put_desc* d_desc, size_t m, co
     if (d_fields) lo = std::min(lo, (uintptr_t)d_fields);
     if (d_blobs) lo = std::min(lo, (uintptr_t)d_blobs);
     if (!d_fields || !d_blobs) lo = std::min(lo, (uintptr_t)d_out);
-    a.src_base = (uint64_t)lo;
+    a.src_base = (uint64_t)lo & ~uint64_t(255);  // offsets keep their addresses' alignment
   }
   a.pfix = pfix;
   void* batch_ws = w + put_jobs_bytes(m);

@@ -89,16 +89,20 @@ constexpr uint64_t kGroupSmallMax = 16384;
 //      the stored CRC read inline for message verify (SweepArgs::exp_fill).
 // 100..102: timing diagnostics that produce wrong CRCs, compiled only with
 // -DAMBRYCRC_DIAGNOSTICS (never in the product library).
+//   32 (kVariantSplit): the group phase as a kernel of its own (group_kernels.hip: 72.5 KiB LDS
+//      image, <= 64 VGPRs, two 1024-thread workgroups = 32 waves per CU), then variant 29's
+//      sweep kernel without its fused group phase.
 constexpr int kVariantPieces = 0;
 constexpr int kVariantDefault = 29;
+constexpr int kVariantSplit = 32;
 constexpr bool variant_supported(int v) {
 #ifdef AMBRYCRC_DIAGNOSTICS
   if (v >= 100 && v <= 102) return true;
 #endif
-  return v == kVariantPieces || v == kVariantDefault;
+  return v == kVariantPieces || v == kVariantDefault || v == kVariantSplit;
 }
-// variant 29 reads group-phase records' stored CRCs inline
-constexpr bool variant_groups(int v) { return v == kVariantDefault; }
+// variants 29 and 32 read group-phase records' stored CRCs inline
+constexpr bool variant_groups(int v) { return v == kVariantDefault || v == kVariantSplit; }
 constexpr int kDiagNoFold = 100;  // diagnostic timing build, selectable via ambrycrc_set_variant only
 
 // Message verify (message_kernels.hip): kMsgSlots CRC jobs per message, slot order
@@ -249,7 +253,9 @@ hipError_t launch_msg_reduce(const MsgArgs& a, hipStream_t s);
 
 hipError_t launch_plan(const PlanArgs& a, hipStream_t s);
 hipError_t launch_sweep(const SweepArgs& a, int grid, int variant, hipStream_t s);
-hipError_t launch_sweep_copy(const SweepArgs& a, int grid, hipStream_t s);
+hipError_t launch_sweep_copy(const SweepArgs& a, int grid, int variant, hipStream_t s);
+// The separate group kernel (group_kernels.hip) on num_cu CUs (it sizes its own grid).
+hipError_t launch_group(const SweepArgs& a, int num_cu, hipStream_t s);
 hipError_t launch_verify(const uint32_t* crc, const uint32_t* expected, uint8_t* mismatch, uint32_t* count,
                          uint32_t n, hipStream_t s);
 hipError_t launch_readbw(const uint8_t* base, uint64_t nbytes, uint32_t* out, int grid, int variant,

@@ -1057,7 +1057,7 @@ __device__ __forceinline__ uint64_t snap_cut(uint64_t cs, uint64_t len, uint64_t
 //   COPY: copy-through (SweepArgs::copy_dst), T4 and GROUP only
 template <bool T4, bool GROUP, int DIAG = 0, bool COPY = false>
 __global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
-  static_assert(!COPY || (T4 && GROUP && DIAG == 0), "copy-through is built for the default kernel only");
+  static_assert(!COPY || (T4 && DIAG == 0), "copy-through is built for the 64-B-run sweep only");
   // Shares are wave-major over workgroups (share i -> wave i / gridDim.x of workgroup
   // i % gridDim.x), so when a batch has fewer shares than waves they spread over every
   // CU. A share is at least kMinShare bytes: a lone large chunk is cut into ~total/16 KiB
@@ -1478,8 +1478,13 @@ hipError_t launch_plan(const PlanArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_sweep_copy(const SweepArgs& a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((crc32_sweep_kernel<true, true, 0, true>), dim3(grid), dim3(1024), 0, s, a);
+hipError_t launch_sweep_copy(const SweepArgs& a, int grid, int variant, hipStream_t s) {
+  if (variant == kVariantSplit) {
+    if (a.small_max && launch_group(a, grid, s) != hipSuccess) return hipGetLastError();
+    hipLaunchKernelGGL((crc32_sweep_kernel<true, false, 0, true>), dim3(grid), dim3(1024), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((crc32_sweep_kernel<true, true, 0, true>), dim3(grid), dim3(1024), 0, s, a);
+  }
   return hipGetLastError();
 }
 
@@ -1489,6 +1494,11 @@ hipError_t launch_sweep(const SweepArgs& a, int grid, int variant, hipStream_t s
     case kVariantPieces: hipLaunchKernelGGL((crc32_sweep_kernel<false, false>), dim3(grid), dim3(1024), 0, s, a); break;
     // 29 (default): 64-B lane runs + the class-sized group phase for whole chunks <= 16 KiB
     case kVariantDefault: hipLaunchKernelGGL((crc32_sweep_kernel<true, true>), dim3(grid), dim3(1024), 0, s, a); break;
+    // 32: the group kernel (two workgroups per CU), then the sweep without its group phase
+    case kVariantSplit:
+      if (a.small_max && launch_group(a, grid, s) != hipSuccess) return hipGetLastError();
+      hipLaunchKernelGGL((crc32_sweep_kernel<true, false>), dim3(grid), dim3(1024), 0, s, a);
+      break;
 #ifdef AMBRYCRC_DIAGNOSTICS
     // timing-only diagnostics (wrong CRCs; debug builds only): 100 FOLD lookups removed, 101 no
     // per-segment atomic, 102 no wave tree

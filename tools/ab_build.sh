@@ -14,6 +14,6 @@ cd $tree/ambry_amd
 g++ -O3 -std=c++17 -fPIC -Wall -c -o host_crc.o csrc/host_crc.cpp
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 ${AB_FLAGS:-} -shared -o $ROOT/build/ab/$name/libambrycrc.so host_crc.o \
   csrc/ambrycrc.cpp csrc/ambrycrc_multi.cpp csrc/ambrycrc_put.cpp csrc/crc32_kernels.hip csrc/message_kernels.hip \
-  csrc/put_kernels.hip csrc/ambrycrc_msg_cpu.cpp -ldl
+  csrc/put_kernels.hip csrc/ambrycrc_msg_cpu.cpp csrc/group_kernels.hip -ldl
 rm -rf $tree
 echo "built build/ab/$name/libambrycrc.so"

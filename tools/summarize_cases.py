@@ -115,8 +115,11 @@ def main():
                                ("SQ_INSTS_VMEM_RD", "vmem_rd_per_kib")):
                     if cn in c:
                         row[nm] = round(c[cn] / data_kib, 2)
+            # no clock estimate: GRBM_GUI_ACTIVE counts over the counter window, which for dispatches
+            # shorter than it (plan, reduce, single-call sweeps) exceeds the kernel time (round-2 review
+            # found 4.0-7.6 "GHz" that way); GRBM_GUI_ACTIVE is kept raw only
             if "GRBM_GUI_ACTIVE" in c:
-                row["clock_ghz_est"] = round(c["GRBM_GUI_ACTIVE"] / 8 / ns, 3)
+                row["grbm_gui_active"] = c["GRBM_GUI_ACTIVE"]
             kern[k] = row
         res["cases"][case] = {"info": info, "kernels": kern}
     out = os.path.join(ROOT, "profiles", f"{args.tag}_small_cases.json")
@@ -125,8 +128,7 @@ def main():
     for case, v in res["cases"].items():
         sw = v["kernels"].get("crc32_sweep_kernel", {})
         print(case, {k: sw.get(k) for k in ("achieved_GBps", "traffic_over_alg", "valu_per_kib", "lds_per_kib",
-                                            "wait_any_frac", "wait_inst_lds_frac", "active_inst_frac",
-                                            "clock_ghz_est")}, sw.get("trace", {}).get("median_ns"))
+                                            "wait_any_frac", "wait_inst_lds_frac", "active_inst_frac")}, sw.get("trace", {}).get("median_ns"))
 
 
 if __name__ == "__main__":
