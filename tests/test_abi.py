@@ -235,7 +235,7 @@ def test_chain_messages_host_under_asan(tmp_path):
                     "-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
                     "-Xarch_host", "-fno-sanitize-recover=all", str(host_o),
                     os.path.join(ROOT, "tests", "native", "chain_asan.cpp"), os.path.join(csrc, "ambrycrc.cpp"),
-                    os.path.join(csrc, "ambrycrc_multi.cpp"), os.path.join(csrc, "crc32_kernels.hip"),
+                    os.path.join(csrc, "ambrycrc_multi.cpp"), os.path.join(csrc, "crc32_kernels.hip"), os.path.join(csrc, "group_kernels.hip"),
                     os.path.join(csrc, "message_kernels.hip"), "-ldl", "-o", str(exe)], check=True, timeout=900)
     r = subprocess.run([str(exe), str(rf)], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
@@ -266,7 +266,7 @@ def test_message_cpu_under_asan(ambry, tmp_path):
                     "-Xarch_host", "-fno-sanitize-recover=all", str(host_o),
                     os.path.join(ROOT, "tests", "native", "msg_cpu_asan.cpp"), os.path.join(csrc, "ambrycrc.cpp"),
                     os.path.join(csrc, "ambrycrc_multi.cpp"), os.path.join(csrc, "ambrycrc_put.cpp"),
-                    os.path.join(csrc, "ambrycrc_msg_cpu.cpp"), os.path.join(csrc, "crc32_kernels.hip"),
+                    os.path.join(csrc, "ambrycrc_msg_cpu.cpp"), os.path.join(csrc, "crc32_kernels.hip"), os.path.join(csrc, "group_kernels.hip"),
                     os.path.join(csrc, "message_kernels.hip"), os.path.join(csrc, "put_kernels.hip"), "-ldl",
                     "-o", str(exe)], check=True, timeout=900)
     r = subprocess.run([str(exe), str(rf)], capture_output=True, text=True, timeout=600)
