@@ -31,6 +31,11 @@
 #include "crc32_layout.h"
 #include "crc32_kernels.h"
 
+// A/B knob: s_setprio 3 around the streamed group path's loads, as the wave-mode body has it.
+#ifndef AMBRY_GRP_PRIO
+#define AMBRY_GRP_PRIO 0
+#endif
+
 namespace ambrycrc {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -796,8 +801,13 @@ __device__ __forceinline__ uint64_t t4_aux(const SweepArgs& a, const uint8_t* __
                                            uint32_t lane, uint32_t (&tb)[16 / G]) {
   constexpr uint32_t BPL = 16u / G;
   const uint32_t k0 = BPL * (G - 1 - (lane & (G - 1)));
+#if AMBRY_PROBE_TAIL  // timing probe (chunks without trailing bytes only)
+#pragma unroll
+  for (uint32_t i = 0; i < BPL; ++i) tb[i] = 0;
+#else
 #pragma unroll
   for (uint32_t i = 0; i < BPL; ++i) tb[i] = *(k0 + i < r.t ? a.base + (r.ce - 1 - (k0 + i)) : dummy);
+#endif
   uint64_t stored = 0;
   if (a.exp_fill) {
     const bool leader = (lane & (G - 1)) == 0 && r.act;
@@ -856,17 +866,25 @@ __device__ __forceinline__ void group_class_t4s(const SweepArgs& a, uint64_t lo,
   const uint64_t i1 = i0 + per < hi ? i0 + per : hi;
   const uint32_t gi = lane / G;
   const uint8_t* dummy = reinterpret_cast<const uint8_t*>(a.img);
+#if AMBRY_PROBE_DESC  // timing probe (batch4k only): no descriptor loads
+  auto idx_at = [&](uint64_t i) -> uint32_t { return (uint32_t)(i + gi < i1 ? i + gi : i0); };
+#define PLEN(c) ((uint64_t)4096)
+#define POFF(c) ((uint64_t)(c) * 4096)
+#else
   auto idx_at = [&](uint64_t i) -> uint32_t { return a.small_idx[i + gi < i1 ? i + gi : i0]; };
+#define PLEN(c) a.len[c]
+#define POFF(c) a.off[c]
+#endif
   const uint32_t ci0 = idx_at(i0);
   uint32_t ci_n = idx_at(i0 + S);
-  T4Round r = t4_round<G>(ci0, a.len[ci0], a.off[ci0], a.crc_in ? a.crc_in[ci0] : 0u, i0 + gi < i1, lane);
+  T4Round r = t4_round<G>(ci0, PLEN(ci0), POFF(ci0), a.crc_in ? a.crc_in[ci0] : 0u, i0 + gi < i1, lane);
   if constexpr (COPY) {
     const uint64_t co = a.copy_off[ci0];
     r.dsh = co == kCopySkip ? 0 : (uint64_t)(uintptr_t)a.copy_dst + co - r.cs;
   }
   uint32_t tb[BPL];
   uint64_t stored = t4_aux<G>(a, dummy, r, lane, tb);
-  uint64_t len_n = a.len[ci_n], off_n = a.off[ci_n];
+  uint64_t len_n = PLEN(ci_n), off_n = POFF(ci_n);
   uint32_t cin_n = a.crc_in ? a.crc_in[ci_n] : 0u;
   uint64_t dst_n = COPY ? a.copy_off[ci_n] : 0;
   uint32_t ci_nn = idx_at(i0 + 2 * S);
@@ -886,15 +904,21 @@ __device__ __forceinline__ void group_class_t4s(const SweepArgs& a, uint64_t lo,
       if constexpr (COPY) rn.dsh = dst_n == kCopySkip ? 0 : (uint64_t)(uintptr_t)a.copy_dst + dst_n - rn.cs;
       stored_n = t4_aux<G>(a, dummy, rn, lane, tbn);
       ci_n = ci_nn;
-      len_n = a.len[ci_n];
-      off_n = a.off[ci_n];
+      len_n = PLEN(ci_n);
+      off_n = POFF(ci_n);
       cin_n = a.crc_in ? a.crc_in[ci_n] : 0u;
       if constexpr (COPY) dst_n = a.copy_off[ci_n];
       ci_nn = idx_at(i + 3 * S);
     }
     // the next step, whichever round it is in
+#if AMBRY_GRP_PRIO
+    __builtin_amdgcn_s_setprio(3);
+#endif
     t4_load<NT, G>(a.base, dummy, last ? rn.p0 : r.p0, last ? rn.cs : r.cs, last ? rn.cb : r.cb,
                    last ? rn.nbw : r.nbw, last ? 0u : sb + 1, nx);
+#if AMBRY_GRP_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
     if constexpr (COPY) {
       if (r.cb > r.cs) {
 #pragma unroll

@@ -20,6 +20,27 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def props94() -> bytes:
+    """94 bytes of valid BlobPropertiesSerDe V5 (BlobPropertiesSerDe.java:83-103): ttl -1, public,
+    fixed creation time, contentType / ownerId / serviceId strings, account 101, container 5, not
+    encrypted, three null strings. The message verify parses the properties (deserializeBlobAll),
+    so the fields buffer must hold real ones, not random bytes."""
+    import struct
+
+    out = struct.pack(">hqbqq", 5, -1, 0, 1_700_000_000_000, 4096)
+    for s in (b"application/octet-stream", b"owner-01", b"svc001"):
+        out += struct.pack(">i", len(s)) + s
+    out += struct.pack(">hhb", 101, 5, 0) + struct.pack(">iii", 0, 0, 0)
+    assert len(out) == 94
+    return out
+
+
+def _props_tensor(torch):
+    import numpy as np
+
+    return torch.from_numpy(np.frombuffer(props94(), dtype=np.uint8).copy()).cuda()
+
+
 def run(m, blob_bytes, reps, in_place, um_len=1000):
     import numpy as np
     import torch
@@ -51,6 +72,7 @@ def run(m, blob_bytes, reps, in_place, um_len=1000):
     blobs = torch.empty(max(1, m * blob_bytes), dtype=torch.uint8, device="cuda")
     D.fill_random(fields, 1, 0)
     D.fill_random(blobs, 2, 0)
+    fields[: m * fstride].view(m, fstride)[:, key_len:key_len + props_len] = _props_tensor(torch)
     out = torch.zeros(m * stride, dtype=torch.uint8, device="cuda")
     serialize_dev(d_desc, out, fields, blobs)  # copy mode fills `out`; in-place mode then reuses its bytes
     torch.cuda.synchronize()
@@ -110,8 +132,8 @@ def run_transform(m, blob_bytes, reps):
     from ambry_amd.messages import PUT_DESC_DTYPE, PutMessage, layout, serialize_dev, transform_dev
 
     key_len, props_len, um_len = 24, 94, 1000
-    L, _ = layout(PutMessage(key=bytes(key_len), props=bytes(props_len), usermeta=bytes(um_len),
-                             blob=bytes(blob_bytes)))
+    L, fo = layout(PutMessage(key=bytes(key_len), props=bytes(props_len), usermeta=bytes(um_len),
+                              blob=bytes(blob_bytes)))
     descs = np.zeros(m, dtype=PUT_DESC_DTYPE)
     idx = np.arange(m, dtype=np.uint64)
     descs["out_off"] = idx * L
@@ -121,6 +143,8 @@ def run_transform(m, blob_bytes, reps):
     descs["header_version"] = 3
     region = torch.empty(m * L, dtype=torch.uint8, device="cuda")
     D.fill_random(region[: (m * L) // 16 * 16], 3, 0)
+    p0 = fo["props"]
+    region.view(m, L)[:, p0:p0 + props_len] = _props_tensor(torch)
     serialize_dev(torch.from_numpy(descs.view(np.uint8).copy()).cuda(), region)  # in place: random fields
     offs = torch.from_numpy((idx * L).astype(np.int64)).cuda()
     out = torch.empty(m * L + 6 * m, dtype=torch.uint8, device="cuda")

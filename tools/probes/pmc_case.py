@@ -9,6 +9,8 @@ untimed; the profiler's per-dispatch counters are the measurement.
   batch4109  4109-B chunks at 16-B offsets (the blob records of 4 KiB PUTs)     -- group class 3
   batch2000  2000-B chunks, packed (8-B offsets); batch3000: 3000 B at 16-B offsets -- class 2
   msg4k      ambrycrc_verify_messages_dev over 262,144 x PUT(4 KiB blob), 1.29 GiB
+  put4k      ambrycrc_serialize_puts_dev, copy mode, 262,144 x PUT(4 KiB blob); put4k_inplace in place
+  xform4k    ambrycrc_transform_messages_dev over 262,144 stored PUT(4 KiB blob) messages
   single100  one 100 B chunk per ambrycrc_batch_dev call
   single4m   one 4 MiB chunk per ambrycrc_batch_dev call
 """
@@ -83,6 +85,22 @@ def main():
         info.update(res)
         # CRC'd bytes per message: header 32 + props + usermeta 1006 + blob record 4109 (+ stored CRCs read)
         info["alg_bytes_per_launch"] = res["region_bytes"]
+    elif args.case in ("put4k", "put4k_inplace"):
+        # ambrycrc_serialize_puts_dev, 262,144 PUTs with a 4 KiB blob: copy mode (fields and blobs in their
+        # own buffers; the copy-through sweep reads, writes and CRCs each field) or in place
+        from bench_put import run
+
+        res = run(262144, 4096, args.reps, args.case == "put4k_inplace")
+        info.update(res)
+        info["alg_bytes_per_launch"] = res["hbm_bytes_min"]  # fields + blobs read, messages written (copy)
+    elif args.case == "xform4k":
+        # ambrycrc_transform_messages_dev over 262,144 stored 4 KiB-blob PUTs (the speculative pass: the
+        # verify's copy-through reads each record once and writes it into the output)
+        from bench_put import run_transform
+
+        res = run_transform(262144, 4096, args.reps)
+        info.update(res)
+        info["alg_bytes_per_launch"] = 2 * res["message_bytes"]
     else:
         raise SystemExit(f"unknown case {args.case}")
     torch.cuda.synchronize()
