@@ -254,15 +254,35 @@ void reap_retired_ws(DevCtx* c) {
 // event on the stream (work already queued there may still read it), never freed in place.
 // (A destroyed stream's handle may be reused by a new stream; hipStreamDestroy drains the old
 // stream's work first, so the buffer is idle by then.)
-int stream_ws(DevCtx* c, hipStream_t s, size_t need, void** out) {
+int stream_ws(DevCtx* c, hipStream_t s, size_t need, void** out, size_t* entry) {
   reap_retired_ws(c);
   DevCtx::StreamWs* w = nullptr;
   for (auto& e : c->ws_list)
     if (e.stream == s) w = &e;
+  if (!w && c->ws_list.size() >= kMaxStreamWs) {
+    // evict the least recently used stream's buffer: retired behind its last call's event
+    // (the entry's event moves with it), the entry reused for s
+    w = &c->ws_list[0];
+    for (auto& e : c->ws_list)
+      if (e.tick < w->tick) w = &e;
+    if (w->ptr) {
+      if (w->last) {
+        c->ws_retired.push_back({w->ptr, w->last});
+      } else {
+        (void)hipDeviceSynchronize();  // no event to wait on (its creation failed): drain, then free
+        (void)hipFree(w->ptr);
+      }
+    } else if (w->last) {
+      (void)hipEventDestroy(w->last);
+    }
+    *w = {s, nullptr, 0, nullptr, 0};
+  }
   if (!w) {
-    c->ws_list.push_back({s, nullptr, 0});
+    c->ws_list.push_back({s, nullptr, 0, nullptr, 0});
     w = &c->ws_list.back();
   }
+  w->tick = ++c->ws_tick;
+  *entry = (size_t)(w - c->ws_list.data());
   if (w->bytes >= need) {
     *out = w->ptr;
     return AMBRYCRC_OK;
@@ -389,8 +409,10 @@ void free_ctx(DevCtx* c) {
   (void)hipSetDevice(c->device);
   (void)hipDeviceSynchronize();
   if (c->d_img) (void)hipFree(c->d_img);
-  for (auto& w : c->ws_list)
+  for (auto& w : c->ws_list) {
     if (w.ptr) (void)hipFree(w.ptr);
+    if (w.last) (void)hipEventDestroy(w.last);
+  }
   for (auto& r : c->ws_retired) {
     (void)hipFree(r.ptr);
     (void)hipEventDestroy(r.done);

@@ -75,14 +75,17 @@ struct DevCtx {
     hipStream_t stream;
     void* ptr;
     size_t bytes;
+    hipEvent_t last;  // recorded on `stream` after each call's work (WsLease), null before the first
+    uint64_t tick;    // last use, for eviction
   };
   struct RetiredWs {
     void* ptr;
     hipEvent_t done;
   };
   std::mutex ws_mu;
-  std::vector<StreamWs> ws_list;
+  std::vector<StreamWs> ws_list;  // at most kMaxStreamWs: the least recently used is evicted
   std::vector<RetiredWs> ws_retired;
+  uint64_t ws_tick = 0;
   bool timing = false;
   std::vector<EventPair> pending, free_events;
   bool slabs_ready = false;
@@ -98,7 +101,11 @@ DevCtx* ctx_for(int device);
 DevCtx* ctx_current();
 // Bytes of batch workspace for n chunks (ambrycrc_workspace_bytes).
 size_t ws_need(size_t n);
-int stream_ws(DevCtx* c, hipStream_t s, size_t need, void** out);
+// Default workspaces kept per device: a caller cycling through many short-lived streams (one per
+// request) holds at most this many buffers; the least recently used one is retired behind its
+// last call's event and freed once that work has completed.
+constexpr size_t kMaxStreamWs = 16;
+int stream_ws(DevCtx* c, hipStream_t s, size_t need, void** out, size_t* entry);
 // Largest chunk the group phase takes whole for a batch of n chunks on c's variant (0: none).
 uint64_t batch_small_max(const DevCtx* c, size_t n);
 // Plan + CRC kernels for n chunks on stream s (ws: >= ws_need(n) bytes). exp_fill, copy_dst,
@@ -140,11 +147,26 @@ int enqueue_serialize(DevCtx* c, const ::ambrycrc_put_desc* d_desc, size_t m, co
 // NULL); a call with its own workspace takes no lock.
 struct WsLease {
   std::unique_lock<std::mutex> lk;
+  DevCtx* ctx = nullptr;
+  hipStream_t stream = nullptr;
+  size_t entry = ~size_t(0);
   // On return *ws is the caller's buffer (checked against need) or the stream's default one.
   int acquire(DevCtx* c, hipStream_t s, void** ws, size_t ws_bytes, size_t need) {
     if (*ws) return ws_bytes < need ? AMBRYCRC_EINVAL : AMBRYCRC_OK;
     lk = std::unique_lock<std::mutex>(c->ws_mu);
-    return stream_ws(c, s, need, ws);
+    const int rc = stream_ws(c, s, need, ws, &entry);
+    if (rc == AMBRYCRC_OK) {
+      ctx = c;
+      stream = s;
+    }
+    return rc;
+  }
+  // The call's work is enqueued: mark the buffer's last use on its stream (still under ws_mu).
+  ~WsLease() {
+    if (!ctx || entry >= ctx->ws_list.size()) return;
+    DevCtx::StreamWs& w = ctx->ws_list[entry];
+    if (!w.last && hipEventCreateWithFlags(&w.last, hipEventDisableTiming) != hipSuccess) w.last = nullptr;
+    if (w.last) (void)hipEventRecord(w.last, stream);
   }
 };
 

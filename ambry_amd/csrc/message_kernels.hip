@@ -120,7 +120,7 @@ __device__ __forceinline__ uint32_t record_check(int k, const uint8_t* q, uint64
       const int32_t n = (int32_t)be32(q + 2);
       return n >= 0 && (uint64_t)n + 14 == span ? 0u : AMBRYCRC_MSG_BAD_RECORD;
     }
-    case 1:  // properties
+    case 1:  // properties (msg_parse_kernel parses them from its LDS window instead)
       return props_record_check(q, span);
     case 2:  // update
       return update_record_check(q, span);
@@ -135,15 +135,45 @@ __device__ __forceinline__ uint32_t record_check(int k, const uint8_t* q, uint64
   }
 }
 
-__device__ __forceinline__ void transform_describe(const TransformArgs& a, uint64_t i, uint32_t st0);
+__device__ __forceinline__ void transform_describe(const TransformArgs& a, uint64_t i, uint32_t st0,
+                                                   const PropsFields* pre = nullptr);
+
+// The first bytes of a record staged in this thread's LDS slot, the rest read from global memory:
+// the properties parse walks int-length strings, one dependent read per field, which from LDS
+// costs an LDS round trip instead of a memory one.
+#ifndef AMBRY_PROPS_WIN
+#define AMBRY_PROPS_WIN 128
+#endif
+constexpr uint32_t kPropsWin = AMBRY_PROPS_WIN;        // bytes staged per thread (a multiple of 16)
+constexpr uint32_t kPropsSlotWords = kPropsWin / 4 + 1;  // +1 word: consecutive slots start on consecutive banks
+struct WinBytes {
+  const uint8_t* w;  // LDS copy of [0, n)
+  const uint8_t* g;  // the same bytes in global memory
+  uint32_t n;
+  __device__ uint32_t u8(uint64_t i) const { return i < n ? w[i] : g[i]; }
+  __device__ uint32_t be16(uint64_t i) const { return i + 2 <= n ? (uint32_t)w[i] << 8 | w[i + 1] : ld_be16(g + i); }
+  __device__ uint32_t be32(uint64_t i) const {
+    return i + 4 <= n ? (uint32_t)w[i] << 24 | (uint32_t)w[i + 1] << 16 | (uint32_t)w[i + 2] << 8 | w[i + 3]
+                      : ld_be32(g + i);
+  }
+  __device__ bool ascii(uint64_t i, uint64_t len) const {
+    if (i + len > n) return bytes_ascii(g + i, len);
+    uint32_t acc = 0;
+    for (uint64_t j = 0; j < len; ++j) acc |= w[i + j];
+    return acc < 0x80u;
+  }
+};
 
 // DESC: the transform's speculative pass -- describe each message right after parsing it, from
 // the header and record heads this thread just loaded (transform_describe's reads hit the cache).
 template <bool DESC>
 __global__ __launch_bounds__(256) void msg_parse_kernel(MsgArgs a, TransformArgs t) {
   __shared__ uint32_t tbl[1024];
+  __shared__ uint32_t pwin[256 * kPropsSlotWords];
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = i < a.m;
+  PropsFields pf;
+  bool pf_ok = false;
   const uint64_t off = live ? a.msg_off[i] : 0;
   const bool in_region = live && off <= a.region_len;
   const uint64_t rem = in_region ? a.region_len - off : 0;
@@ -236,10 +266,36 @@ __global__ __launch_bounds__(256) void msg_parse_kernel(MsgArgs a, TransformArgs
       end = 0;
       break;
     }
+    if (rel[1] != -1) {  // properties: staged, then parsed (the transform's ASCII scan too: DESC)
+      const uint8_t* q = p + rel[1];
+      const uint64_t avail = rem - (uint64_t)rel[1];
+      const uint32_t w = (uint32_t)(avail < kPropsWin ? avail : kPropsWin) & ~15u;
+      uint32_t* slot = pwin + threadIdx.x * kPropsSlotWords;
+      uint32_t v[kPropsWin / 4];
+#pragma unroll
+      for (uint32_t j = 0; j < kPropsWin / 16; ++j)
+        if (16 * j + 16 <= w) __builtin_memcpy(&v[4 * j], q + 16 * j, 16);  // one round trip
+#pragma unroll
+      for (uint32_t j = 0; j < kPropsWin / 4; ++j)
+        if (4 * j + 4 <= w) slot[j] = v[j];
+      const uint64_t span = rend[1] - (uint64_t)rel[1];
+      uint32_t ps = AMBRYCRC_MSG_BAD_RECORD;
+      if (span >= 10) {
+        const uint32_t ver = w >= 2 ? (uint32_t)reinterpret_cast<const uint8_t*>(slot)[0] << 8 |
+                                          reinterpret_cast<const uint8_t*>(slot)[1]
+                                    : be16(q);
+        ps = ver != 1 ? AMBRYCRC_MSG_BAD_VERSION
+                      : props_parse_b<DESC>(WinBytes{reinterpret_cast<const uint8_t*>(slot) + 2, q + 2,
+                                                     w >= 2 ? w - 2 : 0u},
+                                            span - 10, &pf);
+      }
+      pf_ok = ps == 0;
+      status |= ps;
+    }
     for (int k = 0; k < kMsgSlots; ++k) {
       if (rel[k] == -1) continue;
       const uint64_t e = rend[k];
-      status |= record_check(k, p + rel[k], e - (uint64_t)rel[k]);
+      if (k != 1) status |= record_check(k, p + rel[k], e - (uint64_t)rel[k]);
       jo[k] = off + (uint64_t)rel[k];
       jl[k] = e - (uint64_t)rel[k] - 8;
       // Records the group phase takes whole have their stored CRC read there, from the line
@@ -259,7 +315,7 @@ __global__ __launch_bounds__(256) void msg_parse_kernel(MsgArgs a, TransformArgs
   }
   a.status[i] = status;
   if (a.msg_end) a.msg_end[i] = end ? off + end : 0;
-  if constexpr (DESC) transform_describe(t, i, status);
+  if constexpr (DESC) transform_describe(t, i, status, pf_ok ? &pf : nullptr);
 }
 
 __global__ __launch_bounds__(256) void msg_reduce_kernel(MsgArgs a) {
@@ -357,7 +413,8 @@ __global__ __launch_bounds__(256) void props_fix_kernel(TransformArgs a) {
   props_apply_fix(a.out + d.out_off + (uint64_t)L.bp_rel + 2, x);
 }
 
-__device__ __forceinline__ void transform_describe(const TransformArgs& a, uint64_t i, uint32_t st0) {
+__device__ __forceinline__ void transform_describe(const TransformArgs& a, uint64_t i, uint32_t st0,
+                                                   const PropsFields* pre) {
   uint32_t st = st0;
   ambrycrc_put_desc d;
   __builtin_memset(&d, 0, sizeof(d));  // header_version 0: nothing to write
@@ -399,7 +456,8 @@ __device__ __forceinline__ void transform_describe(const TransformArgs& a, uint6
       ok = ok && props_len >= 0 && (int64_t)um + 6 + um_len + 8 == blob;
       // deserializeBlobProperties -> serializeBlobProperties at VERSION_5 (record_fields.h)
       PropsFields pf;
-      ok = ok && props_parse<true>(p + bp + 2, (uint64_t)props_len, &pf) == 0;
+      if (pre) pf = *pre;  // the fused parse kernel parsed them already (from its LDS window)
+      else ok = ok && props_parse<true>(p + bp + 2, (uint64_t)props_len, &pf) == 0;
       const bool encodable = !ok || pf.ascii;
       const PropsFix fx = ok ? props_fix_of(pf, (uint32_t)props_len) : PropsFix{};
       const uint32_t bv = be16(p + blob);  // Blob_Format_V1 / V2 / V3 (:1668-1833)

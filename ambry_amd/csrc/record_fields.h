@@ -52,19 +52,28 @@ __host__ __device__ inline bool bytes_ascii(const uint8_t* p, uint64_t n) {
   return (acc & 0x8080808080808080ull) == 0;
 }
 
+// Byte source of a parse: plain memory (host, or device global memory).
+struct MemBytes {
+  const uint8_t* p;
+  __host__ __device__ uint32_t u8(uint64_t i) const { return p[i]; }
+  __host__ __device__ uint32_t be16(uint64_t i) const { return ld_be16(p + i); }
+  __host__ __device__ uint32_t be32(uint64_t i) const { return ld_be32(p + i); }
+  __host__ __device__ bool ascii(uint64_t i, uint64_t n) const { return bytes_ascii(p + i, n); }
+};
+
 // BlobPropertiesSerDe.getBlobPropertiesFromStream over the n bytes at s (the record's payload:
 // its span minus the 2-B record version and the 8-B CRC). 0, or AMBRYCRC_MSG_BAD_RECORD when a
 // read throws (unknown SerDe version, a negative string size, a field past the span --
 // BlobProperties_Format_V1.deserializeBlobPropertiesRecord maps each to DataCorrupt,
 // MessageFormatRecord.java:1192-1195) or the fields end before the span does (the reference would
 // take other bytes for the CRC). ASCII: also scan the string bytes (the transform's question).
-template <bool ASCII>
-__host__ __device__ inline uint32_t props_parse(const uint8_t* s, uint64_t n, PropsFields* f) {
+template <bool ASCII, class B>
+__host__ __device__ inline uint32_t props_parse_b(const B& s, uint64_t n, PropsFields* f) {
   if (n < kSerdeFixed) return AMBRYCRC_MSG_BAD_RECORD;
-  const int32_t v = (int16_t)ld_be16(s);
+  const int32_t v = (int16_t)s.be16(0);
   if (v < 1 || v > 5) return AMBRYCRC_MSG_BAD_RECORD;  // "stream has unknown blob property version"
   f->version = (uint32_t)v;
-  f->priv_raw = s[kSerdePrivate];
+  f->priv_raw = (uint8_t)s.u8(kSerdePrivate);
   f->enc_raw = 0;
   f->enc_pos = 0;
   bool ascii = true;
@@ -78,15 +87,15 @@ __host__ __device__ inline uint32_t props_parse(const uint8_t* s, uint64_t n, Pr
       if (v > 2) {
         if (pos + 1 > n) return AMBRYCRC_MSG_BAD_RECORD;
         f->enc_pos = (uint32_t)pos;
-        f->enc_raw = s[pos];
+        f->enc_raw = (uint8_t)s.u8(pos);
         pos += 1;
       }
     }
     if (pos + 4 > n) return AMBRYCRC_MSG_BAD_RECORD;
-    const int32_t len = (int32_t)ld_be32(s + pos);
+    const int32_t len = (int32_t)s.be32(pos);
     pos += 4;
     if (len < 0 || (uint64_t)len > n - pos) return AMBRYCRC_MSG_BAD_RECORD;
-    if (ASCII) ascii = ascii && bytes_ascii(s + pos, (uint64_t)len);
+    if (ASCII) ascii = ascii && s.ascii(pos, (uint64_t)len);
     pos += (uint64_t)len;
   }
   if (nstr == 3) {  // V1..V3: the shorts / byte follow the last string
@@ -94,13 +103,18 @@ __host__ __device__ inline uint32_t props_parse(const uint8_t* s, uint64_t n, Pr
     if (v > 2) {
       if (pos + 1 > n) return AMBRYCRC_MSG_BAD_RECORD;
       f->enc_pos = (uint32_t)pos;
-      f->enc_raw = s[pos];
+      f->enc_raw = (uint8_t)s.u8(pos);
       pos += 1;
     }
     if (pos > n) return AMBRYCRC_MSG_BAD_RECORD;
   }
   f->ascii = ascii;
   return pos == n ? 0u : AMBRYCRC_MSG_BAD_RECORD;
+}
+
+template <bool ASCII>
+__host__ __device__ inline uint32_t props_parse(const uint8_t* s, uint64_t n, PropsFields* f) {
+  return props_parse_b<ASCII>(MemBytes{s}, n, f);
 }
 
 // The BlobProperties record check of verify: record version 1 (else UnknownFormatVersion,

@@ -720,6 +720,30 @@ def test_default_workspace_concurrent_threads(gpu, oracle):
         assert np.array_equal(got, oracle.batch(mem, off, ln, threads=8))
 
 
+def test_many_short_lived_streams_default_workspace(gpu, oracle):
+    """Default workspaces (d_ws NULL) are kept per stream up to a cap (kMaxStreamWs = 16), the least
+    recently used retired behind its last call's event: 40 short-lived streams, each running a batch
+    (some while earlier streams' work is still queued), every result right."""
+    torch = _torch()
+    rng = np.random.default_rng(31)
+    mem = stream_bytes(31, 0, 8 << 20)
+    base = dev_bytes(mem)
+    jobs = []
+    for k in range(40):
+        n = int(rng.integers(1, 3000))
+        ln = rng.integers(0, 40000, size=n)
+        off = rng.integers(0, (8 << 20) - 40000, size=n)
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            out = gpu.crc32_batch(base, dev_u64(off), dev_u64(ln), stream=s)
+        jobs.append((off, ln, out, s))
+        if k % 5 == 4:  # drop some streams early (their buffers may be evicted while others queue)
+            jobs[-3][3].synchronize()
+    torch.cuda.synchronize()
+    for off, ln, out, _ in jobs:
+        assert np.array_equal(host_u32(out), oracle.batch(mem, off, ln))
+
+
 def test_diagnostic_variants_not_selectable(gpu):
     """Variants 100-102 (timing builds that return wrong CRCs) are not in the product library."""
     from ambry_amd._lib import AmbryCrcError

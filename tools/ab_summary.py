@@ -1,6 +1,7 @@
 """Summarize tools/ab_cases.sh: per case and library build, the average duration of the batch's
-CRC kernels (crc32_sweep_kernel, plus crc32_group_kernel where it runs) over the interleaved
-rounds, and each build's ratio to the first."""
+CRC kernels (crc32_sweep_kernel, plus crc32_group_kernel where it runs; AB_MATCH=comma-separated
+name substrings for other kernels) over the interleaved rounds, and each build's ratio to the
+first."""
 import csv
 import glob
 import json
@@ -13,8 +14,8 @@ res = {}
 for f in sorted(glob.glob(os.path.join(src, "*", "*", "r*", "kt_kernel_stats.csv"))):
     tag, case, rnd = f.split(os.sep)[-4:-1]
     # the batch's CRC kernels: the sweep, plus the group kernel of variant 31 (one call each per batch)
-    us = sum(float(r["AverageNs"]) / 1e3 for r in csv.DictReader(open(f))
-             if "sweep_kernel" in r["Name"] or "group_kernel" in r["Name"])
+    match = os.environ.get("AB_MATCH", "sweep_kernel,group_kernel").split(",")
+    us = sum(float(r["AverageNs"]) / 1e3 for r in csv.DictReader(open(f)) if any(m in r["Name"] for m in match))
     res.setdefault(case, {}).setdefault(tag, []).append(us)
 out = {}
 for case, by in res.items():
