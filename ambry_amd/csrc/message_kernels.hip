@@ -142,7 +142,7 @@ __device__ __forceinline__ void transform_describe(const TransformArgs& a, uint6
 // the properties parse walks int-length strings, one dependent read per field, which from LDS
 // costs an LDS round trip instead of a memory one.
 #ifndef AMBRY_PROPS_WIN
-#define AMBRY_PROPS_WIN 128
+#define AMBRY_PROPS_WIN 96
 #endif
 constexpr uint32_t kPropsWin = AMBRY_PROPS_WIN;        // bytes staged per thread (a multiple of 16)
 constexpr uint32_t kPropsSlotWords = kPropsWin / 4 + 1;  // +1 word: consecutive slots start on consecutive banks
