@@ -637,8 +637,13 @@ __device__ __forceinline__ uint32_t group_crc_g(const uint8_t* __restrict__ base
   const uint32_t k0 = BPL * (G - 1 - gl);  // this lane's bytes sit at distance k0..k0+BPL-1 from the end
   // the trailing bytes are loaded with the blocks, not after the chain (one round trip)
   uint32_t tb[BPL];
+#if AMBRY_PROBE_TAIL0  // timing probe: no trailing-byte loads (wrong CRCs)
+#pragma unroll
+  for (uint32_t i = 0; i < BPL; ++i) tb[i] = k0 + i < t ? (uint32_t)(ce & 0xFF) : 0u;
+#else
 #pragma unroll
   for (uint32_t i = 0; i < BPL; ++i) tb[i] = k0 + i < t ? base[ce - 1 - (k0 + i)] : 0u;
+#endif
   if constexpr (COPY) {
 #pragma unroll
     for (uint32_t i = 0; i < BPL; ++i)
@@ -975,6 +980,11 @@ __device__ __forceinline__ void group_class(const SweepArgs& a, uint64_t lo, uin
 #pragma unroll 1
   for (uint64_t i = i0; i < i1; i += S) {
     const bool act = i + gi < i1;
+#if AMBRY_PROBE_DESC0  // timing probe (batch100 layout only): no descriptor loads
+    const uint32_t ci = act ? (uint32_t)(i + gi) : 0u;
+    const uint64_t len = act ? 100u : 0u, off = act ? 112ull * ci : 0u;
+    const uint32_t cin = 0;
+#else
     const uint32_t ci = act ? a.small_idx[i + gi] : 0u;
     uint64_t len = 0, off = 0;
     uint32_t cin = 0;
@@ -983,6 +993,7 @@ __device__ __forceinline__ void group_class(const SweepArgs& a, uint64_t lo, uin
       off = a.off[ci];
       cin = a.crc_in ? a.crc_in[ci] : 0u;
     }
+#endif
     const uint64_t cb = aligned_end(off, off + len);
     constexpr uint32_t BLK = 16 * G;  // bytes per chain step
     const uint32_t nb = (uint32_t)((cb - off + BLK - 1) / BLK);
