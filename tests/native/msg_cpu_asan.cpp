@@ -44,11 +44,12 @@ int main(int argc, char** argv) {
     std::vector<unsigned char> msg(all.begin() + lo, all.begin() + hi);
     run(msg, &runs);
     for (size_t cut = 0; cut < msg.size(); cut += 1 + cut / 8) run(std::vector<unsigned char>(msg.begin(), msg.begin() + cut), &runs);
-    for (int t = 0; t < 200; ++t) {  // flips in the first 64 bytes and around every 4-byte field
+    for (int t = 0; t < 300; ++t) {  // flips in the header and record heads: the first 64 bytes, then the first 320
       std::vector<unsigned char> bad(msg);
+      const size_t span = t < 200 ? 64 : 320;  // (the properties record's int-length strings sit past byte 64)
       for (int k = 0; k < 3; ++k) {
         rng = rng * 6364136223846793005ull + 1442695040888963407ull;
-        const size_t at = (size_t)(rng >> 33) % (bad.size() < 64 ? bad.size() : 64);
+        const size_t at = (size_t)(rng >> 33) % (bad.size() < span ? bad.size() : span);
         bad[at] ^= (unsigned char)(1u << ((rng >> 20) & 7));
       }
       run(bad, &runs);

@@ -252,9 +252,19 @@ def test_message_cpu_under_asan(ambry, tmp_path):
     from test_message_format import build_region
 
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    from test_gpu_transform import build_region as transform_region
+    from test_message_format import MF, record_level_cases
+
     region, _, _ = build_region(n=30, seed=8, corrupt_frac=0.0, big_every=10**9)
     rf = tmp_path / "region.bin"
     rf.write_bytes(region)
+    # properties at SerDe V1..V5 (non-canonical flags, non-ASCII strings) and the record-level cases:
+    # the properties / update parsers walk data-dependent offsets
+    r2, offs2 = transform_region(MF, 40, seed=5, corrupt=False)
+    rf2 = tmp_path / "region2.bin"  # the messages back to back (the harness chains them from offset 0)
+    rf2.write_bytes(b"".join(r2[o:MF.verify_message(r2, o)[1]] for o in offs2))
+    rf3 = tmp_path / "region3.bin"
+    rf3.write_bytes(b"".join(m for m, _ in record_level_cases()))
     exe = tmp_path / "msg_cpu_asan"
     csrc = os.path.join(ROOT, "ambry_amd", "csrc")
     host_o = tmp_path / "host_crc.o"
@@ -269,9 +279,10 @@ def test_message_cpu_under_asan(ambry, tmp_path):
                     os.path.join(csrc, "ambrycrc_msg_cpu.cpp"), os.path.join(csrc, "crc32_kernels.hip"), os.path.join(csrc, "group_kernels.hip"),
                     os.path.join(csrc, "message_kernels.hip"), os.path.join(csrc, "put_kernels.hip"), "-ldl",
                     "-o", str(exe)], check=True, timeout=900)
-    r = subprocess.run([str(exe), str(rf)], capture_output=True, text=True, timeout=600)
-    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
-    assert "runs=" in r.stdout
+    for f in (rf, rf2, rf3):
+        r = subprocess.run([str(exe), str(f)], capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+        assert "runs=" in r.stdout
 
 
 def test_update_iov_gather_list(ambry):
