@@ -35,6 +35,10 @@
 #ifndef AMBRY_GRP_PRIO
 #define AMBRY_GRP_PRIO 0
 #endif
+// A/B knob: class 0's trailing bytes from one 8-B window load per lane instead of byte loads.
+#ifndef AMBRY_C0_TAIL_WINDOW
+#define AMBRY_C0_TAIL_WINDOW 0
+#endif
 
 namespace ambrycrc {
 
@@ -637,13 +641,24 @@ __device__ __forceinline__ uint32_t group_crc_g(const uint8_t* __restrict__ base
   const uint32_t k0 = BPL * (G - 1 - gl);  // this lane's bytes sit at distance k0..k0+BPL-1 from the end
   // the trailing bytes are loaded with the blocks, not after the chain (one round trip)
   uint32_t tb[BPL];
-#if AMBRY_PROBE_TAIL0  // timing probe: no trailing-byte loads (wrong CRCs)
+#if AMBRY_C0_TAIL_WINDOW
+  if constexpr (BPL == 8) {
+    // The lane's trailing bytes are the 8 bytes ending at ce - k0 (the byte at distance k0 + i from
+    // the chunk end is byte 7 - i of that window): one unaligned 8-B load when the window lies inside
+    // the chunk, byte loads for the rest (chunks shorter than 16 B).
+    const int64_t wend = (int64_t)ce - (int64_t)k0;
+    uint64_t w = 0;
+    const bool win = k0 < t && wend - 8 >= (int64_t)cs;
+    if (win) __builtin_memcpy(&w, base + wend - 8, 8);
 #pragma unroll
-  for (uint32_t i = 0; i < BPL; ++i) tb[i] = k0 + i < t ? (uint32_t)(ce & 0xFF) : 0u;
-#else
-#pragma unroll
-  for (uint32_t i = 0; i < BPL; ++i) tb[i] = k0 + i < t ? base[ce - 1 - (k0 + i)] : 0u;
+    for (uint32_t i = 0; i < BPL; ++i)
+      tb[i] = k0 + i >= t ? 0u : win ? (uint32_t)(w >> (8 * (7 - i))) & 0xFFu : base[ce - 1 - (k0 + i)];
+  } else
 #endif
+  {
+#pragma unroll
+    for (uint32_t i = 0; i < BPL; ++i) tb[i] = k0 + i < t ? base[ce - 1 - (k0 + i)] : 0u;
+  }
   if constexpr (COPY) {
 #pragma unroll
     for (uint32_t i = 0; i < BPL; ++i)
@@ -806,13 +821,8 @@ __device__ __forceinline__ uint64_t t4_aux(const SweepArgs& a, const uint8_t* __
                                            uint32_t lane, uint32_t (&tb)[16 / G]) {
   constexpr uint32_t BPL = 16u / G;
   const uint32_t k0 = BPL * (G - 1 - (lane & (G - 1)));
-#if AMBRY_PROBE_TAIL  // timing probe (chunks without trailing bytes only)
-#pragma unroll
-  for (uint32_t i = 0; i < BPL; ++i) tb[i] = 0;
-#else
 #pragma unroll
   for (uint32_t i = 0; i < BPL; ++i) tb[i] = *(k0 + i < r.t ? a.base + (r.ce - 1 - (k0 + i)) : dummy);
-#endif
   uint64_t stored = 0;
   if (a.exp_fill) {
     const bool leader = (lane & (G - 1)) == 0 && r.act;
@@ -871,25 +881,17 @@ __device__ __forceinline__ void group_class_t4s(const SweepArgs& a, uint64_t lo,
   const uint64_t i1 = i0 + per < hi ? i0 + per : hi;
   const uint32_t gi = lane / G;
   const uint8_t* dummy = reinterpret_cast<const uint8_t*>(a.img);
-#if AMBRY_PROBE_DESC  // timing probe (batch4k only): no descriptor loads
-  auto idx_at = [&](uint64_t i) -> uint32_t { return (uint32_t)(i + gi < i1 ? i + gi : i0); };
-#define PLEN(c) ((uint64_t)4096)
-#define POFF(c) ((uint64_t)(c) * 4096)
-#else
   auto idx_at = [&](uint64_t i) -> uint32_t { return a.small_idx[i + gi < i1 ? i + gi : i0]; };
-#define PLEN(c) a.len[c]
-#define POFF(c) a.off[c]
-#endif
   const uint32_t ci0 = idx_at(i0);
   uint32_t ci_n = idx_at(i0 + S);
-  T4Round r = t4_round<G>(ci0, PLEN(ci0), POFF(ci0), a.crc_in ? a.crc_in[ci0] : 0u, i0 + gi < i1, lane);
+  T4Round r = t4_round<G>(ci0, a.len[ci0], a.off[ci0], a.crc_in ? a.crc_in[ci0] : 0u, i0 + gi < i1, lane);
   if constexpr (COPY) {
     const uint64_t co = a.copy_off[ci0];
     r.dsh = co == kCopySkip ? 0 : (uint64_t)(uintptr_t)a.copy_dst + co - r.cs;
   }
   uint32_t tb[BPL];
   uint64_t stored = t4_aux<G>(a, dummy, r, lane, tb);
-  uint64_t len_n = PLEN(ci_n), off_n = POFF(ci_n);
+  uint64_t len_n = a.len[ci_n], off_n = a.off[ci_n];
   uint32_t cin_n = a.crc_in ? a.crc_in[ci_n] : 0u;
   uint64_t dst_n = COPY ? a.copy_off[ci_n] : 0;
   uint32_t ci_nn = idx_at(i0 + 2 * S);
@@ -909,8 +911,8 @@ __device__ __forceinline__ void group_class_t4s(const SweepArgs& a, uint64_t lo,
       if constexpr (COPY) rn.dsh = dst_n == kCopySkip ? 0 : (uint64_t)(uintptr_t)a.copy_dst + dst_n - rn.cs;
       stored_n = t4_aux<G>(a, dummy, rn, lane, tbn);
       ci_n = ci_nn;
-      len_n = PLEN(ci_n);
-      off_n = POFF(ci_n);
+      len_n = a.len[ci_n];
+      off_n = a.off[ci_n];
       cin_n = a.crc_in ? a.crc_in[ci_n] : 0u;
       if constexpr (COPY) dst_n = a.copy_off[ci_n];
       ci_nn = idx_at(i + 3 * S);
@@ -980,11 +982,6 @@ __device__ __forceinline__ void group_class(const SweepArgs& a, uint64_t lo, uin
 #pragma unroll 1
   for (uint64_t i = i0; i < i1; i += S) {
     const bool act = i + gi < i1;
-#if AMBRY_PROBE_DESC0  // timing probe (batch100 layout only): no descriptor loads
-    const uint32_t ci = act ? (uint32_t)(i + gi) : 0u;
-    const uint64_t len = act ? 100u : 0u, off = act ? 112ull * ci : 0u;
-    const uint32_t cin = 0;
-#else
     const uint32_t ci = act ? a.small_idx[i + gi] : 0u;
     uint64_t len = 0, off = 0;
     uint32_t cin = 0;
@@ -993,7 +990,6 @@ __device__ __forceinline__ void group_class(const SweepArgs& a, uint64_t lo, uin
       off = a.off[ci];
       cin = a.crc_in ? a.crc_in[ci] : 0u;
     }
-#endif
     const uint64_t cb = aligned_end(off, off + len);
     constexpr uint32_t BLK = 16 * G;  // bytes per chain step
     const uint32_t nb = (uint32_t)((cb - off + BLK - 1) / BLK);
@@ -1304,8 +1300,11 @@ __device__ __forceinline__ bool is_small(uint64_t len, uint64_t small_max) { ret
 // Size class of a small chunk (<= 256 B, 1 KiB, 4 KiB, more): the compacted list is
 // ordered by class, so a group-phase round (64/G consecutive entries) holds chunks of
 // similar length and its chain -- the longest chunk's block count -- wastes little.
+#ifndef AMBRY_C1_MAX  // A/B knob: the largest class-1 (8-lane group) chunk
+#define AMBRY_C1_MAX 1024
+#endif
 __device__ __forceinline__ uint32_t small_class(uint64_t len) {
-  return len <= 256 ? 0u : len <= 1024 ? 1u : len <= 4096 ? 2u : 3u;
+  return len <= 256 ? 0u : len <= AMBRY_C1_MAX ? 1u : len <= 4096 ? 2u : 3u;
 }
 // Per-chunk class indicator packed as 16-bit fields (a plan block has <= kPlanPerBlock <= 65535 chunks).
 __device__ __forceinline__ uint64_t class_onehot(uint64_t len, uint64_t small_max) {
