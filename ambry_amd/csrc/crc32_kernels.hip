@@ -35,10 +35,6 @@
 #ifndef AMBRY_GRP_PRIO
 #define AMBRY_GRP_PRIO 0
 #endif
-// A/B knob: class 0's trailing bytes from one 8-B window load per lane instead of byte loads.
-#ifndef AMBRY_C0_TAIL_WINDOW
-#define AMBRY_C0_TAIL_WINDOW 0
-#endif
 
 namespace ambrycrc {
 
@@ -641,24 +637,8 @@ __device__ __forceinline__ uint32_t group_crc_g(const uint8_t* __restrict__ base
   const uint32_t k0 = BPL * (G - 1 - gl);  // this lane's bytes sit at distance k0..k0+BPL-1 from the end
   // the trailing bytes are loaded with the blocks, not after the chain (one round trip)
   uint32_t tb[BPL];
-#if AMBRY_C0_TAIL_WINDOW
-  if constexpr (BPL == 8) {
-    // The lane's trailing bytes are the 8 bytes ending at ce - k0 (the byte at distance k0 + i from
-    // the chunk end is byte 7 - i of that window): one unaligned 8-B load when the window lies inside
-    // the chunk, byte loads for the rest (chunks shorter than 16 B).
-    const int64_t wend = (int64_t)ce - (int64_t)k0;
-    uint64_t w = 0;
-    const bool win = k0 < t && wend - 8 >= (int64_t)cs;
-    if (win) __builtin_memcpy(&w, base + wend - 8, 8);
 #pragma unroll
-    for (uint32_t i = 0; i < BPL; ++i)
-      tb[i] = k0 + i >= t ? 0u : win ? (uint32_t)(w >> (8 * (7 - i))) & 0xFFu : base[ce - 1 - (k0 + i)];
-  } else
-#endif
-  {
-#pragma unroll
-    for (uint32_t i = 0; i < BPL; ++i) tb[i] = k0 + i < t ? base[ce - 1 - (k0 + i)] : 0u;
-  }
+  for (uint32_t i = 0; i < BPL; ++i) tb[i] = k0 + i < t ? base[ce - 1 - (k0 + i)] : 0u;
   if constexpr (COPY) {
 #pragma unroll
     for (uint32_t i = 0; i < BPL; ++i)
