@@ -8,7 +8,9 @@ untimed; the profiler's per-dispatch counters are the measurement.
   batch4k    4 KiB chunks, aligned, 0.5 GiB                                     -- group class 2
   batch4109  4109-B chunks at 16-B offsets (the blob records of 4 KiB PUTs)     -- group class 3
   batch2000  2000-B chunks, packed (8-B offsets); batch3000: 3000 B at 16-B offsets -- class 2
+  batch16k   16 KiB chunks, aligned                                               -- class 3
   msg4k      ambrycrc_verify_messages_dev over 262,144 x PUT(4 KiB blob), 1.29 GiB
+  msg3k      the same with 3000 B blobs (blob records in class 2)
   put4k      ambrycrc_serialize_puts_dev, copy mode, 262,144 x PUT(4 KiB blob); put4k_inplace in place
   xform4k    ambrycrc_transform_messages_dev over 262,144 stored PUT(4 KiB blob) messages
   single100  one 100 B chunk per ambrycrc_batch_dev call
@@ -28,7 +30,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 SIZES = {"batch100": (100, 112), "batch1k": (1024, 1024), "batch4k": (4096, 4096), "batch4109": (4109, 4112),
-         "batch2000": (2000, 2000), "batch3000": (3000, 3008)}
+         "batch2000": (2000, 2000), "batch3000": (3000, 3008), "batch16k": (16384, 16384)}
 
 
 def main():
@@ -78,10 +80,10 @@ def main():
         for _ in range(args.reps):
             D.crc32_batch(buf, off, ln, out=out, workspace=ws)
         info.update(chunks=1, chunk_bytes=size, alg_bytes_per_launch=size + 4)
-    elif args.case == "msg4k":
+    elif args.case in ("msg4k", "msg3k"):
         from bench_messages import gpu_region, load_mf
 
-        res = gpu_region(load_mf(), 262144, 4 << 10, args.reps)
+        res = gpu_region(load_mf(), 262144, 4 << 10 if args.case == "msg4k" else 3000, args.reps)
         info.update(res)
         # CRC'd bytes per message: header 32 + props + usermeta 1006 + blob record 4109 (+ stored CRCs read)
         info["alg_bytes_per_launch"] = res["region_bytes"]
