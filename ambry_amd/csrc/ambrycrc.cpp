@@ -53,7 +53,7 @@ uint32_t host_xpow8(uint64_t n) {
 
 // ------------------------------------------------------------ LDS image
 std::vector<uint32_t> build_table_image() {
-  const uint32_t words = kLdsBytes / 4 + 64;
+  const uint32_t words = kImgBytes / 4;
   std::vector<uint32_t> img(words, 0u);
   uint32_t t[4][256];
   slice_tables(t, 4);
@@ -74,6 +74,17 @@ std::vector<uint32_t> build_table_image() {
   for (uint32_t k = 0; k < kPowTables; ++k) put_nib(kPowOff + kNibSetBytes * k, host_xpow8(1ull << k));
   const HostTables& h = host_tables();
   for (int k = 0; k < 64; ++k) img[kLdsBytes / 4 + k] = h.xpow2[k];
+  // x^-1 in the reflected order: u * x = v  <=>  u = v << 1 (bit 31 of v clear), or
+  // ((v ^ P) << 1) | 1 (set), since u * x = (u >> 1) ^ (P if bit 0 of u).
+  uint32_t inv = kOne;
+  for (int i = 0; i < 8; ++i) inv = (inv & 0x80000000u) ? (((inv ^ kPoly) << 1) | 1u) : (inv << 1);  // x^-8
+  for (uint32_t k = 0; k < kInvPowSets; ++k) {
+    uint32_t nt[8][16];
+    nibble_tables(inv, nt);
+    for (int n = 0; n < 8; ++n)
+      for (int x = 0; x < 16; ++x) img[(kImgInvOff + kNibSetBytes * k + 64u * n + 4u * x) / 4] = nt[n][x];
+    inv = gf2_mul(inv, inv);
+  }
   return img;
 }
 
@@ -559,6 +570,7 @@ int ambrycrc_init(int device) {
     const long x = strtol(v, &end, 10);
     if (end != v && *end == '\0' && x >= 0 && x < 1000 && variant_supported((int)x)) c->variant = (int)x;
   }
+  if (const char* v = getenv("AMBRYCRC_REGION")) c->region_mode = strcmp(v, "0") != 0;
   std::vector<uint32_t> img = build_table_image();
   if (hipMalloc(reinterpret_cast<void**>(&c->d_img), img.size() * 4) != hipSuccess) {
     delete c;
@@ -804,6 +816,19 @@ int ambrycrc_set_variant(int device, int variant) {
   return AMBRYCRC_OK;
 }
 
+int ambrycrc_set_region_mode(int device, int enable) {
+  DevCtx* c = ctx_for(device);
+  if (!c) return AMBRYCRC_ENOINIT;
+  if (enable != 0 && enable != 1) return AMBRYCRC_EINVAL;
+  c->region_mode = enable != 0;
+  return AMBRYCRC_OK;
+}
+
+int ambrycrc_get_region_mode(int device) {
+  DevCtx* c = ctx_for(device);
+  return c ? (c->region_mode ? 1 : 0) : AMBRYCRC_ENOINIT;
+}
+
 int ambrycrc_get_variant(int device) {
   DevCtx* c = ctx_for(device);
   return c ? c->variant : AMBRYCRC_ENOINIT;
@@ -891,9 +916,10 @@ int ambrycrc_debug_readbw_dev(const uint8_t* d_base, uint64_t nbytes, uint32_t* 
 }
 
 size_t ambrycrc_messages_workspace_bytes(size_t m) {
-  const size_t j = (size_t)kMsgSlots * m;
-  const size_t jobs = (j * 2 * sizeof(uint64_t) + j * 2 * sizeof(uint32_t) + j + 255) & ~size_t(255);
-  return jobs + ws_need(j);
+  // job arrays, then the batch workspace of job mode or the run sums of region mode (a region of
+  // up to kRegionMaxPerMessage bytes per message: region / 16 bytes + two super-blocks' slack)
+  const size_t region = m * (kRegionMaxPerMessage / 16) + 2048;
+  return msg_jobs_bytes(m) + std::max(ws_need((size_t)kMsgSlots * m), region);
 }
 
 }  // extern "C"
@@ -903,11 +929,43 @@ namespace detail {
 
 // The device message pipeline (parse -> plan + sweep -> reduce) on `stream`; d_ws holds
 // at least ambrycrc_messages_workspace_bytes(m).
+size_t msg_jobs_bytes(size_t m) {
+  const size_t j = (size_t)kMsgSlots * m;
+  return (j * 2 * sizeof(uint64_t) + j * 2 * sizeof(uint32_t) + j + 255) & ~size_t(255);
+}
+
 int enqueue_messages(DevCtx* c, const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off, size_t m,
-                     uint32_t* d_status, uint64_t* d_msg_end, void* d_ws, hipStream_t stream) {
+                     uint32_t* d_status, uint64_t* d_msg_end, void* d_ws, size_t ws_bytes, hipStream_t stream) {
+  const bool region = c->region_mode && region_len > 0 && region_len <= kRegionMaxPerMessage * (uint64_t)m &&
+                      msg_jobs_bytes(m) + region_ws_bytes(d_region, region_len) <= ws_bytes;
   MsgStage st;
-  const int rc = enqueue_messages_parse(c, d_region, region_len, d_msg_off, m, d_status, d_msg_end, d_ws, stream, &st);
-  return rc ? rc : enqueue_messages_check(c, st, stream);
+  if (!region) {
+    const int rc = enqueue_messages_parse(c, d_region, region_len, d_msg_off, m, d_status, d_msg_end, d_ws, stream, &st);
+    return rc ? rc : enqueue_messages_check(c, st, stream);
+  }
+  // Region mode: pass 1 sweeps the region into 64-B run sums (kept where job mode keeps its batch
+  // workspace), pass 2 parses every message and assembles its record CRCs from them.
+  st.a.region = d_region;
+  st.a.region_len = region_len;
+  st.a.msg_off = d_msg_off;
+  st.a.m = m;
+  st.a.img = c->d_img;
+  st.a.status = d_status;
+  st.a.msg_end = d_msg_end;
+  st.a.inline_max = 0;
+  st.batch_ws = static_cast<uint8_t*>(d_ws) + msg_jobs_bytes(m);
+  RegionArgs r;
+  const uintptr_t rp = reinterpret_cast<uintptr_t>(d_region);
+  r.base = d_region - (rp & 63u);
+  r.reg0 = rp & 63u;
+  r.reg_end = r.reg0 + region_len;
+  r.lo16 = r.reg0 & ~uint64_t(15);
+  r.hi16 = (r.reg_end - 1) & ~uint64_t(15);
+  r.nsb = region_nsb(d_region, region_len);
+  r.rk = static_cast<uint32_t*>(st.batch_ws);
+  r.img = c->d_img;
+  if (launch_region_runs(r, c->grid, stream) != hipSuccess) return AMBRYCRC_EHIP;
+  return hip_err(launch_region_msg(st.a, r, stream));
 }
 
 int enqueue_messages_parse(DevCtx* c, const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off,
@@ -932,7 +990,7 @@ int enqueue_messages_parse(DevCtx* c, const uint8_t* d_region, uint64_t region_l
   // takes whole; the parse kernel reads the rest.
   const bool inline_exp = variant_groups(c->variant);
   a.inline_max = inline_exp ? batch_small_max(c, j) : 0;
-  st->batch_ws = w + ((j * 2 * sizeof(uint64_t) + j * 2 * sizeof(uint32_t) + j + 255) & ~size_t(255));
+  st->batch_ws = w + msg_jobs_bytes(m);
   st->crc = crc;
   st->j = j;
   return hip_err(desc ? launch_msg_parse_desc(a, *desc, stream) : launch_msg_parse(a, stream));
@@ -1004,9 +1062,11 @@ int ambrycrc_verify_messages_dev(const uint8_t* d_region, uint64_t region_len, c
   DevCtx* c = ctx_current();
   if (!c) return AMBRYCRC_ENOINIT;
   WsLease lease;
-  const int rc = lease.acquire(c, stream, &d_ws, ws_bytes, ambrycrc_messages_workspace_bytes(m));
+  const size_t need = ambrycrc_messages_workspace_bytes(m);
+  const int rc = lease.acquire(c, stream, &d_ws, ws_bytes, need);
   if (rc) return rc;
-  return enqueue_messages(c, d_region, region_len, d_msg_off, m, d_status, d_msg_end, d_ws, stream);
+  return enqueue_messages(c, d_region, region_len, d_msg_off, m, d_status, d_msg_end, d_ws,
+                          ws_bytes ? ws_bytes : need, stream);
 }
 
 int ambrycrc_verify_messages_host(const uint8_t* region, uint64_t region_len, const uint64_t* msg_off, size_t m,
@@ -1104,7 +1164,7 @@ int ambrycrc_verify_messages_host(const uint8_t* region, uint64_t region_len, co
                  hipMemcpy(d_o, &zero, 8, hipMemcpyHostToDevice) != hipSuccess) {
         rc = AMBRYCRC_EHIP;
       } else {
-        rc = enqueue_messages(c, d_buf, ext[first], d_o, 1, d_s, d_e, d_w, nullptr);
+        rc = enqueue_messages(c, d_buf, ext[first], d_o, 1, d_s, d_e, d_w, ambrycrc_messages_workspace_bytes(1), nullptr);
         if (!rc && (hipMemcpy(&st, d_s, 4, hipMemcpyDeviceToHost) != hipSuccess ||
                     hipMemcpy(&en, d_e, 8, hipMemcpyDeviceToHost) != hipSuccess))
           rc = AMBRYCRC_EHIP;
@@ -1154,7 +1214,9 @@ int ambrycrc_verify_messages_host(const uint8_t* region, uint64_t region_len, co
     const size_t nm = sp.msgs.size();
     if (!rc && hipMemcpyAsync(ms.d_off, ms.h_off, nm * sizeof(uint64_t), hipMemcpyHostToDevice, s.stream) != hipSuccess)
       rc = AMBRYCRC_EHIP;
-    if (!rc) rc = enqueue_messages(c, s.d_data, span, ms.d_off, nm, ms.d_status, ms.d_end, ms.d_ws, s.stream);
+    if (!rc)
+      rc = enqueue_messages(c, s.d_data, span, ms.d_off, nm, ms.d_status, ms.d_end, ms.d_ws,
+                            ambrycrc_messages_workspace_bytes(kSlabMsgs), s.stream);
     if (!rc && (hipMemcpyAsync(ms.h_status, ms.d_status, nm * sizeof(uint32_t), hipMemcpyDeviceToHost, s.stream) !=
                     hipSuccess ||
                 hipMemcpyAsync(ms.h_end, ms.d_end, nm * sizeof(uint64_t), hipMemcpyDeviceToHost, s.stream) !=

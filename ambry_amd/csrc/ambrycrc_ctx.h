@@ -63,6 +63,9 @@ struct DevCtx {
 #define AMBRY_DEFAULT_VARIANT kVariantDefault
 #endif
   int variant = AMBRY_DEFAULT_VARIANT;  // (A/B builds: -DAMBRY_DEFAULT_VARIANT=...)
+  // Message verify of regions of at most kRegionMaxPerMessage bytes per message: region mode
+  // (region_runs_kernel + region_jobs_kernel) instead of jobs through the batch engine.
+  bool region_mode = true;
   // Sweep rounds of at most this many bytes (SweepArgs::window); 0 = one round.
   uint64_t window = 32ull << 30;
   uint32_t* d_img = nullptr;
@@ -114,10 +117,14 @@ int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uin
                   uint32_t* out, size_t n, void* ws, hipStream_t s, uint32_t* exp_fill = nullptr,
                   uint8_t* copy_dst = nullptr, const uint64_t* copy_off = nullptr);
 
-// The device message-verify pipeline (parse -> plan + sweep -> reduce) on `stream`; d_ws holds at
-// least ambrycrc_messages_workspace_bytes(m). d_msg_end may be null.
+// The device message-verify pipeline on `stream`: parse -> plan + sweep -> reduce (job mode), or
+// parse, region runs, region jobs -> reduce (region mode: c->region_mode, a region of at most
+// kRegionMaxPerMessage bytes per message, and ws_bytes room for its run sums). d_ws holds
+// ws_bytes >= ambrycrc_messages_workspace_bytes(m) bytes. d_msg_end may be null.
 int enqueue_messages(DevCtx* c, const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off, size_t m,
-                     uint32_t* d_status, uint64_t* d_msg_end, void* d_ws, hipStream_t stream);
+                     uint32_t* d_status, uint64_t* d_msg_end, void* d_ws, size_t ws_bytes, hipStream_t stream);
+// Bytes of the job arrays at the start of a message-verify workspace (the rest: batch / run sums).
+size_t msg_jobs_bytes(size_t m);
 // The same in two halves: the parse kernel (jobs and their stored CRCs in st->a), then the CRC
 // batch and the reduce -- with copy_dst / copy_off, the batch is the copy-through kernel
 // (SweepArgs::copy_dst), which the transform uses to copy the records while verifying them.

@@ -105,6 +105,38 @@ constexpr bool variant_supported(int v) {
 constexpr bool variant_groups(int v) { return v == kVariantDefault || v == kVariantSplit; }
 constexpr int kDiagNoFold = 100;  // diagnostic timing build, selectable via ambrycrc_set_variant only
 
+// Region mode of the message verify: the log region is swept once as contiguous
+// memory, each 64-B run's raw CRC (zero register, no xor-out) stored (crc32_kernels.hip
+// region_runs_kernel), then one thread per message parses it and assembles its record CRCs from
+// the runs they cover (message_kernels.hip region_msg_kernel, region_crc.h). Runs are [base + 64k, base + 64k + 64) with
+// base = the region's start rounded down to 64 B; only 16-B pieces holding region bytes are read.
+struct RegionArgs {
+  const uint8_t* base;   // region start rounded down to 64 B
+  uint64_t reg0;         // region start - base (0..63)
+  uint64_t reg_end;      // region end - base
+  uint64_t lo16, hi16;   // offsets from base of the first and last 16-B pieces holding region bytes
+  uint64_t nsb;          // 4 KiB super-blocks (64 runs each) from base over the region
+  uint32_t* rk;          // [kRunPad + nsb * 64 + 256]: run k's raw CRC at rk[kRunPad + k]; then a
+                         // 1 KiB spill line for the stores of lanes with no sums to write
+  const uint32_t* img;   // the table image (kImgBytes)
+};
+// Words ahead of run 0: a run group read before run 0 stays inside rk, and each super-block's 64
+// sums (one wave store) fill exactly two 128-B lines (a misaligned window left partial lines,
+// which cost pass 1 ~80 us per 1.4 GB region).
+constexpr uint64_t kRunPad = 32;
+constexpr uint64_t kSuperBlock = 4096;
+// Region bytes per message up to which the message verify takes region mode (64-B run sums in
+// the workspace: region / 16 bytes) instead of CRC jobs through the batch engine.
+constexpr uint64_t kRegionMaxPerMessage = 8192;
+inline uint64_t region_nsb(const uint8_t* region, uint64_t len) {
+  const uint64_t b = reinterpret_cast<uintptr_t>(region) & ~uint64_t(63);
+  return (reinterpret_cast<uintptr_t>(region) + len - b + kSuperBlock - 1) / kSuperBlock;
+}
+inline size_t region_ws_bytes(const uint8_t* region, uint64_t len) {
+  return (size_t)((kRunPad + region_nsb(region, len) * 64 + 256) * 4 + 255) & ~size_t(255);
+}
+hipError_t launch_region_runs(const RegionArgs& a, int grid, hipStream_t s);
+
 // Message verify (message_kernels.hip): kMsgSlots CRC jobs per message, slot order
 // encryption key, blob properties, update, user metadata, blob.
 constexpr int kMsgSlots = 5;
@@ -249,6 +281,8 @@ hipError_t launch_trailer_parse(const TrailerArgs& a, hipStream_t s);
 hipError_t launch_trailer_verify(const TrailerArgs& a, hipStream_t s);
 
 hipError_t launch_msg_parse(const MsgArgs& a, hipStream_t s);
+// Region mode, pass 2: parse, record CRCs from the run sums, status (a.job_* / expected / crc unused).
+hipError_t launch_region_msg(const MsgArgs& a, const RegionArgs& g, hipStream_t s);
 hipError_t launch_msg_reduce(const MsgArgs& a, hipStream_t s);
 
 hipError_t launch_plan(const PlanArgs& a, hipStream_t s);

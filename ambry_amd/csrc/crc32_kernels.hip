@@ -60,8 +60,16 @@ __device__ __forceinline__ void fill_lds(const uint32_t* __restrict__ img) {
   __syncthreads();
 }
 
+// Region mode's pass 1 (region_runs_kernel) stages only the slice tables, plus a 1 KiB buffer per
+// wave for its run sums: its own LDS array, so that kernel is not sized by the full image.
+constexpr uint32_t kRunsBufBytes = 1024;
+__shared__ __attribute__((aligned(16))) uint32_t g_lds_runs[(kSliceBytes + 16 * kRunsBufBytes) / 4];
+
+// W = 0: the full image (g_lds); W = 1: the slice tables of region_runs_kernel (g_lds_runs).
+template <int W = 0>
 __device__ __forceinline__ uint32_t lds_rd(uint32_t byte_addr) {
-  return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(g_lds) + byte_addr);
+  const char* base = W == 0 ? reinterpret_cast<const char*>(g_lds) : reinterpret_cast<const char*>(g_lds_runs);
+  return *reinterpret_cast<const uint32_t*>(base + byte_addr);
 }
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
@@ -106,13 +114,14 @@ __device__ __forceinline__ LaneConst make_lane_const(uint32_t lane) {
 
 // One slice-by-4 step on x = state ^ word: T3[x.b0]^T2[x.b1]^T1[x.b2]^T0[x.b3] ^ xin.
 // perm(L, x, sel): result byte0 = L.b0 (lane column), byte1 = x.b_k, byte2 = L.b2 (region), byte3 = 0.
+template <int W = 0>
 __device__ __forceinline__ uint32_t slice4(uint32_t x, const LaneConst& k, uint32_t xin) {
   const uint32_t a0 = __builtin_amdgcn_perm(k.L3, x, 0x0C060004u);
   const uint32_t a1 = __builtin_amdgcn_perm(k.L2, x, 0x0C060104u);
   const uint32_t a2 = __builtin_amdgcn_perm(k.L1, x, 0x0C060204u);
   const uint32_t a3 = __builtin_amdgcn_perm(k.L0, x, 0x0C060304u);
-  const uint32_t t = xor3(lds_rd(a0), lds_rd(a1), lds_rd(a2));
-  return xor3(t, lds_rd(a3), xin);
+  const uint32_t t = xor3(lds_rd<W>(a0), lds_rd<W>(a1), lds_rd<W>(a2));
+  return xor3(t, lds_rd<W>(a3), xin);
 }
 
 // Raw CRC (zero register, no xor-out) of one 16-B piece, xor xin.
@@ -313,15 +322,15 @@ __device__ __forceinline__ uint32_t body_crc(const uint8_t* __restrict__ base, u
 
 // Raw CRC of a lane's run of R consecutive 16-B pieces (R slice-by-4 chains of 4 steps, back
 // to back), xor xin into the last step.
-template <int R>
+template <int R, int W = 0>
 __device__ __forceinline__ uint32_t run_crc(const u32x4 (&w)[R], const LaneConst& k, uint32_t xin) {
   uint32_t x = w[0].x;
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    x = slice4(x, k, w[r].y);
-    x = slice4(x, k, w[r].z);
-    x = slice4(x, k, w[r].w);
-    x = slice4(x, k, r + 1 < R ? w[r + 1].x : xin);
+    x = slice4<W>(x, k, w[r].y);
+    x = slice4<W>(x, k, w[r].z);
+    x = slice4<W>(x, k, w[r].w);
+    x = slice4<W>(x, k, r + 1 < R ? w[r + 1].x : xin);
   }
   return x;
 }
@@ -1519,6 +1528,160 @@ hipError_t launch_sweep_copy(const SweepArgs& a, int grid, int variant, hipStrea
   } else {
     hipLaunchKernelGGL((crc32_sweep_kernel<true, true, 0, true>), dim3(grid), dim3(1024), 0, s, a);
   }
+  return hipGetLastError();
+}
+
+// ---- region mode, pass 1 (RegionArgs): the raw CRC of every 64-B run of a log region ----
+// The wave body of C3 without its fold and tree: each wave streams a contiguous share of 4 KiB
+// super-blocks (four coalesced 1 KiB loads per lane, nontemporal, s_setprio 3 while issuing
+// them, the next super-block in flight), the quad transpose leaves lane 4m + j the run
+// [64m, 64m + 64) of block j, one 16-step slice-by-4 chain from a zero register gives its raw
+// CRC, stored at run index 16j + m of the super-block. Loads are unconditional: a piece outside
+// the region reads the nearest piece that holds region bytes, zeroed after (the run sums of
+// runs that straddle the region's ends are never used; region_jobs_kernel recomputes those
+// runs from the bytes). Runs have no loop-carried state, so consecutive super-blocks' chains
+// are independent.
+__device__ __forceinline__ void region_sb_load(const RegionArgs& a, uint64_t s, uint32_t lane, u32x4 (&x)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint64_t p = s * kSuperBlock + (uint64_t)kBlockBytes * i + 16u * lane;
+    const uint64_t q = p < a.lo16 ? a.lo16 : (p > a.hi16 ? a.hi16 : p);
+    x[i] = ld16<true>(reinterpret_cast<const u32x4*>(a.base + q));
+  }
+}
+
+__device__ __forceinline__ void region_sb_zero(const RegionArgs& a, uint64_t s, uint32_t lane, u32x4 (&x)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint64_t p = s * kSuperBlock + (uint64_t)kBlockBytes * i + 16u * lane;
+    if (p < a.lo16 || p > a.hi16) x[i] = u32x4{0u, 0u, 0u, 0u};
+  }
+}
+
+// A/B knobs: AMBRY_RUNS_PROBE 1 = no run sums into LDS, 4 = every store of a wave to one 1 KiB
+// line set, 5 = no global stores (timing only, wrong sums); AMBRY_RUNS_STORE_NT 0 = plain stores.
+#ifndef AMBRY_RUNS_STORE_NT
+#define AMBRY_RUNS_STORE_NT 1
+#endif
+#ifndef AMBRY_RUNS_IL
+#define AMBRY_RUNS_IL 0
+#endif
+#ifndef AMBRY_RUNS_CU_MAJOR
+#define AMBRY_RUNS_CU_MAJOR 1
+#endif
+#ifndef AMBRY_RUNS_PROBE
+#define AMBRY_RUNS_PROBE 0
+#endif
+__global__ __launch_bounds__(1024) void region_runs_kernel(RegionArgs a) {
+  const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  // Shares CU-major (the waves of a workgroup take adjacent shares) once every wave has at least a
+  // few super-blocks: a CU then reads from a few translation pages and stores its run sums into
+  // one, where wave-major shares (the sweep kernel's, which spread a small batch over every CU)
+  // put 16 read and 16 store streams pages apart on each CU -- address translation, not HBM,
+  // then cost pass 1 a quarter of its time. Smaller regions stay wave-major.
+  const bool cu_major = AMBRY_RUNS_CU_MAJOR && a.nsb >= 4 * nwaves;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(cu_major ? blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)
+                                                                : (threadIdx.x >> 6) * gridDim.x + blockIdx.x);
+  const uint64_t s0 = a.nsb * wave / nwaves, s1 = a.nsb * (wave + 1) / nwaves;
+  {  // LDS-DMA of the slice tables (image bytes [0, 128 KiB)), as fill_lds
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (uint32_t c = wv; c < kSliceBytes / 1024; c += nw)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(reinterpret_cast<const uint8_t*>(a.img) + c * 1024 + lane * 16),
+          (__attribute__((address_space(3))) void*)(reinterpret_cast<uint8_t*>(g_lds_runs) + c * 1024), 16, 0, 0);
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+  }
+  const uint32_t lane = threadIdx.x & 63u;
+  const LaneConst k = make_lane_const(lane);
+#if AMBRY_RUNS_IL
+  // Interleaved: wave w hashes super-blocks w, w + nwaves, ... (all waves inside one window of the
+  // region, and their stores inside one window of rk); a 4-B store per lane per super-block.
+  {
+    uint32_t* out = a.rk + kRunPad + 16u * (lane & 3u) + (lane >> 2);
+    const uint64_t last = a.nsb - 1;
+    auto nx = [&](uint64_t s) { return s < a.nsb ? s : last; };
+    u32x4 c0[4], c1[4], c2[4], c3[4];
+    region_sb_load(a, nx(wave), lane, c0);
+    region_sb_load(a, nx(wave + nwaves), lane, c1);
+    region_sb_load(a, nx(wave + 2 * nwaves), lane, c2);
+    region_sb_load(a, nx(wave + 3 * nwaves), lane, c3);
+    auto h = [&](uint64_t s, u32x4 (&cur)[4]) {
+      region_sb_zero(a, s, lane, cur);
+      quad_transpose_asm(cur);
+      const uint32_t r = run_crc<4, 1>(cur, k, 0u);
+      __builtin_nontemporal_store(r, out + (s < a.nsb ? s : a.nsb) * 64);  // past the end: the spill line
+    };
+    if (wave >= a.nsb) return;
+    for (uint64_t s = wave; s < a.nsb; s += 4 * nwaves) {
+      h(s, c0);
+      region_sb_load(a, nx(s + 4 * nwaves), lane, c0);
+      h(s + nwaves, c1);
+      region_sb_load(a, nx(s + 5 * nwaves), lane, c1);
+      h(s + 2 * nwaves, c2);
+      region_sb_load(a, nx(s + 6 * nwaves), lane, c2);
+      h(s + 3 * nwaves, c3);
+      region_sb_load(a, nx(s + 7 * nwaves), lane, c3);
+    }
+    return;
+  }
+#endif
+  if (s0 >= s1) return;
+  // Four super-block buffers: while one is hashed the next three are in flight. Each buffer is
+  // hashed in place and only then reloaded (no register copies of loads still in flight), and every
+  // load and store is issued on every path (indices past the share re-read its last super-block;
+  // lanes with nothing to store write the workspace's spill line), so each wait is for the oldest
+  // buffer only. The four super-blocks' sums gather in the wave's LDS buffer (word 64u + run
+  // index) and go out as one 16-B store per lane: 1 KiB contiguous per wave, 8 whole 128-B lines.
+  uint32_t* buf = g_lds_runs + kSliceBytes / 4 + (threadIdx.x >> 6) * (kRunsBufBytes / 4);
+  const uint32_t slot = 16u * (lane & 3u) + (lane >> 2);
+  const uint64_t slast = s1 - 1;
+  auto hash = [&](uint64_t s, uint32_t u, u32x4 (&cur)[4]) {
+    region_sb_zero(a, s, lane, cur);
+    quad_transpose_asm(cur);
+    const uint32_t r = run_crc<4, 1>(cur, k, 0u);
+    if (AMBRY_RUNS_PROBE == 0 || r == 0x9E3779B9u) buf[64u * u + slot] = r;
+  };
+  u32x4 b0[4], b1[4], b2[4], b3[4];
+  region_sb_load(a, s0, lane, b0);
+  region_sb_load(a, s0 + 1 < s1 ? s0 + 1 : slast, lane, b1);
+  region_sb_load(a, s0 + 2 < s1 ? s0 + 2 : slast, lane, b2);
+  region_sb_load(a, s0 + 3 < s1 ? s0 + 3 : slast, lane, b3);
+  u32x4* spill = reinterpret_cast<u32x4*>(a.rk + kRunPad + a.nsb * 64) + lane;
+  for (uint64_t s = s0; s < s1; s += 4) {
+    hash(s, 0, b0);
+    __builtin_amdgcn_s_setprio(3);
+    region_sb_load(a, s + 4 < s1 ? s + 4 : slast, lane, b0);
+    __builtin_amdgcn_s_setprio(0);
+    if (s + 1 < s1) hash(s + 1, 1, b1);
+    __builtin_amdgcn_s_setprio(3);
+    region_sb_load(a, s + 5 < s1 ? s + 5 : slast, lane, b1);
+    __builtin_amdgcn_s_setprio(0);
+    if (s + 2 < s1) hash(s + 2, 2, b2);
+    __builtin_amdgcn_s_setprio(3);
+    region_sb_load(a, s + 6 < s1 ? s + 6 : slast, lane, b2);
+    __builtin_amdgcn_s_setprio(0);
+    if (s + 3 < s1) hash(s + 3, 3, b3);
+    __builtin_amdgcn_s_setprio(3);
+    region_sb_load(a, s + 7 < s1 ? s + 7 : slast, lane, b3);
+    __builtin_amdgcn_s_setprio(0);
+    const u32x4 v = *reinterpret_cast<const u32x4*>(buf + 4u * lane);
+    u32x4* dst = 4u * lane < 64u * (s1 - s) ? reinterpret_cast<u32x4*>(a.rk + kRunPad + s * 64) + lane : spill;
+    if constexpr (AMBRY_RUNS_PROBE == 4) dst = reinterpret_cast<u32x4*>(a.rk + kRunPad + s0 * 64) + lane;
+    if constexpr (AMBRY_RUNS_PROBE == 6) dst = reinterpret_cast<u32x4*>(a.rk + kRunPad) + lane;
+    if constexpr (AMBRY_RUNS_PROBE == 5) {
+      if (v.x == 0x9E3779B9u) *dst = v;
+    } else if constexpr (AMBRY_RUNS_STORE_NT) {
+      __builtin_nontemporal_store(v, dst);
+    } else {
+      *dst = v;
+    }
+  }
+}
+
+hipError_t launch_region_runs(const RegionArgs& a, int grid, hipStream_t s) {
+  if (a.nsb == 0) return hipSuccess;
+  hipLaunchKernelGGL(region_runs_kernel, dim3(grid), dim3(1024), 0, s, a);
   return hipGetLastError();
 }
 

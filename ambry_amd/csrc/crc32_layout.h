@@ -30,6 +30,13 @@ constexpr uint32_t kLdsBytes = kNibBase + kPowOff + kPowTables * kNibSetBytes;
 static_assert(kLdsBytes <= 160u * 1024u, "LDS image must fit one CU (160 KiB)");
 static_assert(kPowOff + kPowTables * kNibSetBytes < 65536u, "nibble offsets must fit ds_read offset");
 
+// The global image (not staged by the sweep): kLdsBytes of LDS image, 64 words x^(8*2^k), then
+// the nibble sets of x^(-8*2^k), k = 0..kInvPowSets-1 (region mode's final un-shift,
+// region_kernels.hip).
+constexpr uint32_t kImgInvOff = kLdsBytes + 256u;
+constexpr uint32_t kInvPowSets = 6;
+constexpr uint32_t kImgBytes = kImgInvOff + kInvPowSets * kNibSetBytes;
+
 constexpr uint32_t kBlockBytes = 1024;  // one wave-wide 16 B/lane load
 constexpr uint32_t kWaveLanes = 64;
 

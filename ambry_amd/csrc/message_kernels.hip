@@ -23,6 +23,7 @@
 #include "crc_img.h"
 #include "put_layout.h"
 #include "record_fields.h"
+#include "region_crc.h"
 
 namespace ambrycrc {
 
@@ -164,57 +165,48 @@ struct WinBytes {
   }
 };
 
-// DESC: the transform's speculative pass -- describe each message right after parsing it, from
-// the header and record heads this thread just loaded (transform_describe's reads hit the cache).
-template <bool DESC>
-__global__ __launch_bounds__(256) void msg_parse_kernel(MsgArgs a, TransformArgs t) {
-  __shared__ uint32_t tbl[1024];
-  __shared__ uint32_t pwin[256 * kPropsSlotWords];
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool live = i < a.m;
-  PropsFields pf;
-  bool pf_ok = false;
-  const uint64_t off = live ? a.msg_off[i] : 0;
-  const bool in_region = live && off <= a.region_len;
-  const uint64_t rem = in_region ? a.region_len - off : 0;
-  const uint8_t* p = a.region + (in_region ? off : 0);
-  const HeaderWords hw = load_header(p, rem);  // in flight across the table staging
-  stage_slice_tables(tbl, a.img);
-  __syncthreads();
-  if (!live) return;
-  // Jobs are slot-major (job k*m + i = slot k of message i), so each slot's store below is
-  // one coalesced wave store; every slot is written exactly once.
+// One message's header, record checks and CRC jobs (job k = [jo[k], jo[k] + jl[k]) from the
+// region start, its stored CRC ex[k]; records of 1..inline_max bytes leave ex[k] to the group
+// phase). slot: this thread's LDS window for the properties. DESC: the transform's ASCII scan.
+struct MsgParse {
   uint64_t jo[kMsgSlots] = {0, 0, 0, 0, 0}, jl[kMsgSlots] = {0, 0, 0, 0, 0};
   uint32_t ex[kMsgSlots] = {0, 0, 0, 0, 0};
   uint32_t status = 0;
   uint64_t end = 0;
+};
+
+template <bool DESC>
+__device__ __forceinline__ void parse_message(uint64_t off, bool in_region, uint64_t rem, const uint8_t* p,
+                                              const HeaderWords& hw, const uint32_t* __restrict__ tbl,
+                                              uint32_t* __restrict__ slot, uint64_t inline_max, MsgParse& r,
+                                              PropsFields& pf, bool& pf_ok) {
   do {
     if (!in_region || rem < 2) {
-      status = AMBRYCRC_MSG_BAD_LAYOUT;
+      r.status = AMBRYCRC_MSG_BAD_LAYOUT;
       break;
     }
     const int v = (int16_t)__builtin_bswap16((uint16_t)hw.w[0]);
     const uint32_t h = v == 1 ? 34u : v == 2 ? 38u : v == 3 ? 40u : 0u;
     if (h == 0) {
-      status = AMBRYCRC_MSG_BAD_VERSION;
+      r.status = AMBRYCRC_MSG_BAD_VERSION;
       break;
     }
     if (rem < h) {
-      status = AMBRYCRC_MSG_BAD_LAYOUT;
+      r.status = AMBRYCRC_MSG_BAD_LAYOUT;
       break;
     }
     // stored header CRC: bytes [h-8, h)
     const uint32_t st_hi = v == 3 ? be32_w0(hw, 8) : v == 2 ? be32_w2(hw, 7) : be32_w2(hw, 6);
     const uint32_t st_lo = v == 3 ? be32_w0(hw, 9) : v == 2 ? be32_w2(hw, 8) : be32_w2(hw, 7);
     if (st_hi != 0 || header_crc(hw, h - 8, tbl) != st_lo) {  // verifyHeader: nothing else is read
-      status = AMBRYCRC_MSG_HEADER_CRC;
+      r.status = AMBRYCRC_MSG_HEADER_CRC;
       break;
     }
     int64_t total;
     int32_t rel[kMsgSlots];
     if (v == 3) {
       if ((int16_t)__builtin_bswap16((uint16_t)(hw.w[0] >> 16)) < 0) {  // lifeVersion >= 0
-        status = AMBRYCRC_MSG_BAD_LAYOUT;
+        r.status = AMBRYCRC_MSG_BAD_LAYOUT;
         break;
       }
       total = (int64_t)(((uint64_t)be32_w0(hw, 1) << 32) | be32_w0(hw, 2));
@@ -235,7 +227,7 @@ __global__ __launch_bounds__(256) void msg_parse_kernel(MsgArgs a, TransformArgs
     const bool is_put = rel[1] != -1 && rel[2] == -1 && rel[3] != -1 && rel[4] != -1;
     const bool is_upd = rel[2] != -1 && rel[0] == -1 && rel[1] == -1 && rel[3] == -1 && rel[4] == -1;
     if (total <= 0 || !(is_put || is_upd)) {
-      status = AMBRYCRC_MSG_BAD_LAYOUT;
+      r.status = AMBRYCRC_MSG_BAD_LAYOUT;
       break;
     }
     int64_t prev = -1, first = -1;
@@ -247,13 +239,13 @@ __global__ __launch_bounds__(256) void msg_parse_kernel(MsgArgs a, TransformArgs
       prev = rel[k];
     }
     if (!ok || (uint64_t)total > rem || (uint64_t)first > rem - (uint64_t)total) {
-      status = AMBRYCRC_MSG_BAD_LAYOUT;
+      r.status = AMBRYCRC_MSG_BAD_LAYOUT;
       break;
     }
-    end = (uint64_t)first + (uint64_t)total;
+    r.end = (uint64_t)first + (uint64_t)total;
     uint64_t rend[kMsgSlots];  // end of record k (its stored CRC's last byte + 1)
     for (int k = 0; k < kMsgSlots; ++k) {
-      rend[k] = end;
+      rend[k] = r.end;
       for (int j = k + 1; j < kMsgSlots; ++j)
         if (rel[j] != -1) {
           rend[k] = (uint64_t)rel[j];
@@ -262,15 +254,14 @@ __global__ __launch_bounds__(256) void msg_parse_kernel(MsgArgs a, TransformArgs
       if (rel[k] != -1 && rend[k] < (uint64_t)rel[k] + 8) ok = false;
     }
     if (!ok) {
-      status = AMBRYCRC_MSG_BAD_LAYOUT;
-      end = 0;
+      r.status = AMBRYCRC_MSG_BAD_LAYOUT;
+      r.end = 0;
       break;
     }
     if (rel[1] != -1) {  // properties: staged, then parsed (the transform's ASCII scan too: DESC)
       const uint8_t* q = p + rel[1];
       const uint64_t avail = rem - (uint64_t)rel[1];
       const uint32_t w = (uint32_t)(avail < kPropsWin ? avail : kPropsWin) & ~15u;
-      uint32_t* slot = pwin + threadIdx.x * kPropsSlotWords;
       uint32_t v[kPropsWin / 4];
 #pragma unroll
       for (uint32_t j = 0; j < kPropsWin / 16; ++j)
@@ -290,32 +281,117 @@ __global__ __launch_bounds__(256) void msg_parse_kernel(MsgArgs a, TransformArgs
                                             span - 10, &pf);
       }
       pf_ok = ps == 0;
-      status |= ps;
+      r.status |= ps;
     }
     for (int k = 0; k < kMsgSlots; ++k) {
       if (rel[k] == -1) continue;
       const uint64_t e = rend[k];
-      if (k != 1) status |= record_check(k, p + rel[k], e - (uint64_t)rel[k]);
-      jo[k] = off + (uint64_t)rel[k];
-      jl[k] = e - (uint64_t)rel[k] - 8;
+      if (k != 1) r.status |= record_check(k, p + rel[k], e - (uint64_t)rel[k]);
+      r.jo[k] = off + (uint64_t)rel[k];
+      r.jl[k] = e - (uint64_t)rel[k] - 8;
       // Records the group phase takes whole have their stored CRC read there, from the line
       // it is already streaming (SweepArgs::exp_fill); only the others cost a fetch here.
-      if (jl[k] == 0 || jl[k] > a.inline_max) {
+      if (r.jl[k] == 0 || r.jl[k] > inline_max) {
         const uint64_t stored = be64(p + e - 8);
-        if (stored >> 32) status |= kRecordBit[k];  // a CRC32 never has upper bits: mismatch regardless
-        ex[k] = (uint32_t)stored;
+        if (stored >> 32) r.status |= kRecordBit[k];  // a CRC32 never has upper bits: mismatch regardless
+        r.ex[k] = (uint32_t)stored;
       }
     }
   } while (false);
+}
+
+// DESC: the transform's speculative pass -- describe each message right after parsing it, from
+// the header and record heads this thread just loaded (transform_describe's reads hit the cache).
+template <bool DESC>
+__global__ __launch_bounds__(256) void msg_parse_kernel(MsgArgs a, TransformArgs t) {
+  __shared__ uint32_t tbl[1024];
+  __shared__ uint32_t pwin[256 * kPropsSlotWords];
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = i < a.m;
+  PropsFields pf;
+  bool pf_ok = false;
+  const uint64_t off = live ? a.msg_off[i] : 0;
+  const bool in_region = live && off <= a.region_len;
+  const uint64_t rem = in_region ? a.region_len - off : 0;
+  const uint8_t* p = a.region + (in_region ? off : 0);
+  const HeaderWords hw = load_header(p, rem);  // in flight across the table staging
+  stage_slice_tables(tbl, a.img);
+  __syncthreads();
+  if (!live) return;
+  MsgParse r;
+  parse_message<DESC>(off, in_region, rem, p, hw, tbl, pwin + threadIdx.x * kPropsSlotWords, a.inline_max, r, pf,
+                      pf_ok);
+  // Jobs are slot-major (job k*m + i = slot k of message i), so each slot's store below is
+  // one coalesced wave store; every slot is written exactly once.
 #pragma unroll
   for (int k = 0; k < kMsgSlots; ++k) {
-    a.job_off[(uint64_t)k * a.m + i] = jo[k];
-    a.job_len[(uint64_t)k * a.m + i] = jl[k];
-    a.expected[(uint64_t)k * a.m + i] = ex[k];
+    a.job_off[(uint64_t)k * a.m + i] = r.jo[k];
+    a.job_len[(uint64_t)k * a.m + i] = r.jl[k];
+    a.expected[(uint64_t)k * a.m + i] = r.ex[k];
+  }
+  a.status[i] = r.status;
+  if (a.msg_end) a.msg_end[i] = r.end ? off + r.end : 0;
+  if constexpr (DESC) transform_describe(t, i, r.status, pf_ok ? &pf : nullptr);
+}
+
+// Region mode, pass 2: one thread per message parses it as msg_parse_kernel does
+// (every stored CRC read here), assembles each record's CRC from the run sums of pass 1
+// (region_crc.h) and writes the message's status: parse, CRC jobs, plan, sweep and reduce in one
+// kernel, with no job arrays.
+#ifndef AMBRY_REGION_WPE
+#define AMBRY_REGION_WPE 4
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AMBRY_REGION_WPE))) void region_msg_kernel(
+    MsgArgs a, RegionArgs g) {
+  __shared__ uint32_t tbl[1024];
+  __shared__ uint32_t pwin[256 * kPropsSlotWords];
+  __shared__ uint32_t nib[region::kSets * region::kNibWords];
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = i < a.m;
+  PropsFields pf;
+  bool pf_ok = false;
+  const uint64_t off = live ? a.msg_off[i] : 0;
+  const bool in_region = live && off <= a.region_len;
+  const uint64_t rem = in_region ? a.region_len - off : 0;
+  const uint8_t* p = a.region + (in_region ? off : 0);
+  const HeaderWords hw = load_header(p, rem);
+  stage_slice_tables(tbl, a.img);
+  region::stage_nib(nib, a.img);
+  __syncthreads();
+  if (!live) return;
+  uint32_t* slot = pwin + threadIdx.x * kPropsSlotWords;
+  uint32_t status;
+  uint64_t end;
+  {
+    MsgParse r;
+    parse_message<false>(off, in_region, rem, p, hw, tbl, slot, 0, r, pf, pf_ok);
+    // The jobs go to this thread's LDS slot (the properties window is done with), so the five
+    // descriptors do not stay live in VGPRs across the record CRCs: 4 words per slot, job start
+    // relative to the message (records < 4 GiB: an int32 size field, blobs <= Integer.MAX_VALUE).
+#pragma unroll
+    for (int k = 0; k < kMsgSlots; ++k) {
+      slot[4 * k] = (uint32_t)(r.jo[k] - off);
+      slot[4 * k + 1] = (uint32_t)((r.jo[k] - off) >> 32);
+      slot[4 * k + 2] = (uint32_t)r.jl[k];
+      slot[4 * k + 3] = r.ex[k];
+    }
+    status = r.status;
+    end = r.end;
+  }
+  static_assert(4 * kMsgSlots <= kPropsSlotWords, "job slots fit the properties window");
+  const uint32_t* rk = g.rk + kRunPad;
+  for (int k = 0; k < kMsgSlots; ++k) {
+    const uint64_t jo = off + ((uint64_t)slot[4 * k + 1] << 32 | slot[4 * k]);
+    const uint32_t jl = slot[4 * k + 2], ex = slot[4 * k + 3];
+#if AMBRY_REGION_PROBE == 1
+    const uint32_t c = ex;
+#else
+    const uint32_t c = jl ? region::record_crc(tbl, nib, g.base, rk, g.reg0 + jo, jl) : 0u;
+#endif
+    if (c != ex) status |= AMBRYCRC_MSG_ENCKEY_CRC << k;
   }
   a.status[i] = status;
   if (a.msg_end) a.msg_end[i] = end ? off + end : 0;
-  if constexpr (DESC) transform_describe(t, i, status, pf_ok ? &pf : nullptr);
 }
 
 __global__ __launch_bounds__(256) void msg_reduce_kernel(MsgArgs a) {
@@ -684,6 +760,12 @@ hipError_t launch_msg_parse_desc(const MsgArgs& a, const TransformArgs& t, hipSt
   if (a.m == 0) return hipSuccess;
   if (t.m != a.m || t.region != a.region || t.msg_off != a.msg_off) return hipErrorInvalidValue;
   hipLaunchKernelGGL(msg_parse_kernel<true>, dim3((uint32_t)((a.m + 255) / 256)), dim3(256), 0, s, a, t);
+  return hipGetLastError();
+}
+
+hipError_t launch_region_msg(const MsgArgs& a, const RegionArgs& g, hipStream_t s) {
+  if (a.m == 0) return hipSuccess;
+  hipLaunchKernelGGL(region_msg_kernel, dim3((uint32_t)((a.m + 255) / 256)), dim3(256), 0, s, a, g);
   return hipGetLastError();
 }
 

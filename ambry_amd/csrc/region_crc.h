@@ -1,0 +1,184 @@
+// region_crc.h -- region mode of the message verify, pass 2: a record's CRC assembled from the
+// 64-B run sums of pass 1 (region_runs_kernel, crc32_kernels.hip), for the fused per-message
+// kernel region_msg_kernel (message_kernels.hip).
+//
+// Why: a region of small PUT messages read as CRC jobs puts every record through
+// the batch engine's group phase, where each record pays a round of descriptors, chain and tree
+// (4 KiB-blob messages: 4.5 TB/s). Read as contiguous memory the region streams at the C3 wave
+// body's rate; what is left per record is arithmetic on run sums, and re-reading the at most
+// two runs its ends cut.
+//
+// A record = [pa, pb) (offsets from RegionArgs::base), zlib CRC-32 out:
+//   runs     A0 = pa rounded down, B1 = pb rounded up to 64 B: n = (B1 - A0) / 64 runs, run r at
+//            A0 + 64r. Every value below is a raw CRC register "at the end of its run".
+//   head     run 0 from the bytes: bytes outside [pa, pb) zeroed (leading zeros leave a zero
+//            register unchanged; trailing ones advance it to the run end), the initial register
+//            ~0 XORed into the first four record bytes (when the run holds t < 4 of them, the
+//            rest of the register, ~0 >> 8t, is added at the run end).
+//   tail     run n-1 from the bytes (bytes from pb on zeroed) when pb is not 64-aligned, else
+//            its run sum.
+//   interior run sums rk[k], k = A0/64 + 1 .. B1/64 - 2.
+//   combine  V = xor_r v_r * x^(8*64*(n-1-r)): four interleaved Horner streams (fold x^(8*256)),
+//            run groups of four read as one 16-B load aligned to the record's last run (elements
+//            before run 0 count as zero), streams merged by x^(8*64), x^(8*128).
+//   un-shift the register at pb is V * x^(-8(B1-pb)) (nibble sets of x^(-8*2^k), crc32_layout.h);
+//            the CRC is its complement.
+// Model: tests/kernel_model.py RegionModel (checked against zlib on the CPU).
+#pragma once
+#include <hip/hip_runtime.h>
+
+// A/B probe builds (tools/ab_build.sh AB_FLAGS=-DAMBRY_REGION_PROBE=n; timing only, wrong CRCs):
+// 1 = records not CRC'd (parse alone), 2 = no run-sum loads, 3 = no head / tail loads.
+#ifndef AMBRY_REGION_PROBE
+#define AMBRY_REGION_PROBE 0
+#endif
+#include <stdint.h>
+
+#include "crc32_kernels.h"
+#include "crc32_layout.h"
+
+namespace ambrycrc {
+namespace region {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// LDS (besides T0..T3, one copy: t[256j + b], crc_img.h stage_slice_tables): 11 nibble sets,
+// POW[4..8] (x^(8*16) .. x^(8*256)) then x^(-8*2^k), k = 0..5.
+constexpr uint32_t kNibWords = kNibSetBytes / 4;  // 128
+constexpr uint32_t kSets = 5 + kInvPowSets;
+constexpr uint32_t kP16 = 0, kP32 = 1, kP64 = 2, kP128 = 3, kP256 = 4, kInv0 = 5;
+
+__device__ __forceinline__ uint32_t nmul(const uint32_t* __restrict__ nib, uint32_t v, uint32_t set) {
+  const uint32_t* s = nib + set * kNibWords;
+  uint32_t x = 0;
+#pragma unroll
+  for (int n = 0; n < 8; ++n) x ^= s[16 * n + __builtin_amdgcn_ubfe(v, 4 * n, 4)];
+  return x;
+}
+
+__device__ __forceinline__ uint32_t step4(const uint32_t* __restrict__ t, uint32_t x) {
+  return t[768 + (x & 0xffu)] ^ t[512 + ((x >> 8) & 0xffu)] ^ t[256 + ((x >> 16) & 0xffu)] ^ t[x >> 24];
+}
+
+// Bytes of a little-endian word w at run byte offsets [4w, 4w + 4) with offset >= lo / < hi.
+__device__ __forceinline__ uint32_t keep_ge(int d) {  // bytes at index >= d (d = lo - 4w)
+  return d <= 0 ? 0xFFFFFFFFu : (d >= 4 ? 0u : (0xFFFFFFFFu << (8 * d)));
+}
+__device__ __forceinline__ uint32_t keep_lt(int d) {  // bytes at index < d (d = hi - 4w)
+  return d >= 4 ? 0xFFFFFFFFu : (d <= 0 ? 0u : (0xFFFFFFFFu >> (32 - 8 * d)));
+}
+
+// The 16-B pieces of the 64-B run at base + r0 that hold bytes of [lo, hi) (others zero).
+__device__ __forceinline__ void load_run(const uint8_t* __restrict__ base, uint64_t r0, int lo, int hi, u32x4 (&w)[4]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    w[q] = u32x4{0u, 0u, 0u, 0u};
+#if AMBRY_REGION_PROBE != 3  // probe 3 (timing only, wrong CRCs): no head / tail loads
+    if (16 * q + 16 > lo && 16 * q < hi) w[q] = *reinterpret_cast<const u32x4*>(base + r0 + 16 * q);
+#endif
+  }
+}
+
+// Raw CRC register at the end of that run over its bytes [lo, hi) (others zero), with 0xFF XORed
+// into bytes [lo, lo + ninit): four independent 4-step chains, one per piece, merged by x^(8*16)
+// and x^(8*32) (depth 4 + 2 instead of 16 dependent steps).
+__device__ __forceinline__ uint32_t hash_run(const uint32_t* __restrict__ t, const uint32_t* __restrict__ nib,
+                                             const u32x4 (&w)[4], int lo, int hi, int ninit) {
+  uint32_t p[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t s = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const int o = 16 * q + 4 * d;
+      uint32_t v = w[q][d] & keep_ge(lo - o) & keep_lt(hi - o);
+      v ^= keep_ge(lo - o) & keep_lt(lo + ninit - o);
+      s = step4(t, s ^ v);
+    }
+    p[q] = s;
+  }
+  return nmul(nib, nmul(nib, p[0], kP16) ^ p[1], kP32) ^ nmul(nib, p[2], kP16) ^ p[3];
+}
+
+// Stage the nibble sets into nib[kSets * kNibWords] (the caller syncs).
+__device__ __forceinline__ void stage_nib(uint32_t* __restrict__ nib, const uint32_t* __restrict__ img) {
+  for (uint32_t i = threadIdx.x; i < kSets * kNibWords; i += blockDim.x) {
+    const uint32_t set = i / kNibWords, w = i % kNibWords;
+    const uint32_t byte = set < 5 ? kNibBase + kPowOff + kNibSetBytes * (4 + set) : kImgInvOff + kNibSetBytes * (set - 5);
+    nib[i] = img[byte / 4 + w];
+  }
+}
+
+// Four run groups (16 run sums) from group g on, as 16-B loads; groups past ng are not read.
+__device__ __forceinline__ void load_groups(const uint32_t* __restrict__ rk, int64_t e0, int64_t g, int64_t ng,
+                                            u32x4 (&r)[4]) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+#if AMBRY_REGION_PROBE == 2  // probe 2 (timing only, wrong CRCs): no run-sum loads
+    r[u] = u32x4{(uint32_t)g, 0u, 0u, (uint32_t)u};
+#else
+    if (g + u < ng) __builtin_memcpy(&r[u], rk + e0 + 4 * (g + u), 16);
+#endif
+  }
+}
+
+// zlib CRC-32 of the len bytes at offset pa from base; rk = RegionArgs::rk + kRunPad. Every load
+// is issued before the first is used (head and tail runs, the first 16 run sums), and each
+// Horner step group prefetches the next 16 sums.
+__device__ __forceinline__ uint32_t record_crc(const uint32_t* __restrict__ t, const uint32_t* __restrict__ nib,
+                                               const uint8_t* __restrict__ base, const uint32_t* __restrict__ rk,
+                                               uint64_t pa, uint64_t len) {
+  if (len == 0) return 0;
+  const uint64_t pb = pa + len;
+  if (len < 4) {
+    uint32_t c = 0xFFFFFFFFu;
+    for (uint64_t i = pa; i < pb; ++i) c = t[(c ^ base[i]) & 0xffu] ^ (c >> 8);
+    return ~c;
+  }
+  const uint64_t A0 = pa & ~uint64_t(63), B1 = (pb + 63) & ~uint64_t(63);
+  const int64_t n = (int64_t)((B1 - A0) >> 6), k0 = (int64_t)(A0 >> 6);
+  const int lo = (int)(pa - A0), hi = pb - A0 < 64 ? (int)(pb - A0) : 64;
+  const int tin = hi - lo;
+  const bool tail_bytes = n >= 2 && (pb & 63u) != 0;
+  const int thi = (int)(pb - (B1 - 64));
+  const int64_t ng = (n + 3) >> 2, e0 = k0 + n - 4 * ng, elast = k0 + n - 1;
+  u32x4 hw[4], tw[4], nxt[4];
+  load_run(base, A0, lo, hi, hw);
+  load_run(base, B1 - 64, 0, tail_bytes ? thi : 0, tw);
+  load_groups(rk, e0, 0, ng, nxt);
+  uint32_t H = hash_run(t, nib, hw, lo, hi, tin < 4 ? tin : 4);
+  if (tin < 4) H ^= 0xFFFFFFFFu >> (8 * tin);
+  const uint32_t T = tail_bytes ? hash_run(t, nib, tw, 0, thi, 0) : 0u;
+  // Horner over runs k0 .. k0+n-1 in groups of four ending at the last run.
+  uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;  // s3: the stream updated last
+  for (int64_t g = 0; g < ng; g += 4) {
+    u32x4 r[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) r[u] = nxt[u];
+    if (g + 4 < ng) load_groups(rk, e0, g + 4, ng, nxt);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (g + u < ng) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int64_t e = e0 + 4 * (g + u) + q;
+          const uint32_t v = e < k0 ? 0u : e == k0 ? H : (e == elast && tail_bytes) ? T : r[u][q];
+          const uint32_t nv = nmul(nib, s0, kP256) ^ v;
+          s0 = s1;
+          s1 = s2;
+          s2 = s3;
+          s3 = nv;
+        }
+      }
+    }
+  }
+  uint32_t V = s3 ^ nmul(nib, s2, kP64) ^ nmul(nib, s1, kP128) ^ nmul(nib, nmul(nib, s0, kP64), kP128);
+  const uint32_t d = (uint32_t)(B1 - pb);
+#pragma unroll
+  for (uint32_t k = 0; k < kInvPowSets; ++k)
+    if (d & (1u << k)) V = nmul(nib, V, kInv0 + k);
+  return ~V;
+}
+
+}  // namespace region
+}  // namespace ambrycrc

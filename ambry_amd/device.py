@@ -159,6 +159,16 @@ def get_variant(device: int = 0) -> int:
     return check(lib().ambrycrc_get_variant(device), "ambrycrc_get_variant")
 
 
+def set_region_mode(device: int, enable: bool) -> None:
+    """Message verify in region mode (one sweep of the region, record CRCs from 64-B run sums)
+    or as CRC jobs through the batch engine; ambrycrc_set_region_mode."""
+    check(lib().ambrycrc_set_region_mode(device, 1 if enable else 0), "ambrycrc_set_region_mode")
+
+
+def get_region_mode(device: int = 0) -> bool:
+    return bool(check(lib().ambrycrc_get_region_mode(device), "ambrycrc_get_region_mode"))
+
+
 def set_grid(device: int, workgroups: int) -> None:
     check(lib().ambrycrc_set_grid(device, workgroups), "ambrycrc_set_grid")
 

@@ -453,6 +453,14 @@ int ambrycrc_range_checksums_host(const uint8_t* file, uint64_t file_len, const 
  * the current one. */
 int ambrycrc_set_variant(int device, int variant);
 int ambrycrc_get_variant(int device);
+/* Message verify (ambrycrc_verify_messages_dev / _host) of a region of at most 8 KiB per
+ * message: region mode (1, the default; AMBRYCRC_REGION=0 in the environment at init turns it
+ * off) sweeps the region once as contiguous memory, keeping the raw CRC of every 64-B run, and
+ * assembles each record's CRC from the runs it covers, re-reading only the two runs its ends
+ * cut; 0 = every record as a CRC job through the batch engine (plan, group phase, sweep). Same
+ * status bits either way. */
+int ambrycrc_set_region_mode(int device, int enable);
+int ambrycrc_get_region_mode(int device);
 /* Grid size of the persistent sweep kernel (workgroups; 0 = one per CU). */
 int ambrycrc_set_grid(int device, int workgroups);
 
@@ -495,7 +503,8 @@ int ambrycrc_fill_random_dev(uint8_t* d_dst, uint64_t nbytes, uint64_t seed, uin
 int ambrycrc_debug_readbw_dev(const uint8_t* d_base, uint64_t nbytes, uint32_t* d_out, int variant,
                               hipStream_t stream);
 
-/* Copy of the LDS table image (kLdsBytes + 256 B) into host memory `out` (for
+/* Copy of the table image (the LDS image kLdsBytes, 64 words x^(8*2^k), then the nibble sets
+ * of x^(-8*2^k), k = 0..5: kImgBytes in all) into host memory `out` (for
  * tests that model the kernel on the CPU). Returns the byte size, or <0. */
 long ambrycrc_debug_table_image(uint32_t* out, size_t max_words);
 

@@ -22,6 +22,9 @@ K_TREE_OFF = K_FOLD_OFF + K_NIB_SET
 K_POW_OFF = K_TREE_OFF + 6 * K_NIB_SET
 K_POW_TABLES = 36
 K_LDS_BYTES = K_NIB_BASE + K_POW_OFF + K_POW_TABLES * K_NIB_SET
+K_IMG_INV_OFF = K_LDS_BYTES + 256  # nibble sets of x^(-8*2^k), k = 0..5 (crc32_layout.h)
+K_INV_SETS = 6
+K_IMG_BYTES = K_IMG_INV_OFF + K_INV_SETS * K_NIB_SET
 BLOCK = 1024
 LANES = np.arange(64, dtype=np.uint32)
 
@@ -29,7 +32,7 @@ LANES = np.arange(64, dtype=np.uint32)
 def table_image():
     from ambry_amd._lib import lib
 
-    words = K_LDS_BYTES // 4 + 64
+    words = K_IMG_BYTES // 4
     buf = (ctypes.c_uint32 * words)()
     nbytes = lib().ambrycrc_debug_table_image(buf, words)
     assert nbytes == words * 4, nbytes
@@ -39,7 +42,7 @@ def table_image():
 class KernelModel:
     def __init__(self, img=None):
         self.img = table_image() if img is None else img
-        self.xpow2 = self.img[K_LDS_BYTES // 4:]
+        self.xpow2 = self.img[K_LDS_BYTES // 4:K_LDS_BYTES // 4 + 64]
         col = (LANES & 31) << 2
         self.L = [((j >> 1) << 16) | ((j & 1) << 7) | col for j in range(4)]
 
@@ -330,6 +333,99 @@ class KernelModel:
                 out[c] ^= r
                 c += 1
         return [x & 0xFFFFFFFF for x in out]
+
+
+class RegionModel:
+    """Region mode of the message verify (crc32_kernels.hip region_runs_kernel, region_kernels.hip
+    region_jobs_kernel), scalar: run sums of the 64-B runs from base = region start rounded down
+    to 64 B, then each job's CRC from its head / tail runs' bytes, the run sums between, four
+    Horner streams and the x^(-8d) un-shift, with the image's one-copy slice tables and nibble
+    sets exactly as the kernel addresses them."""
+
+    def __init__(self, img):
+        self.img = img
+        self.T = [[int(img[(((j >> 1) << 16) | (b << 8) | ((j & 1) << 7)) >> 2]) for b in range(256)]
+                  for j in range(4)]
+
+    def _nib(self, v, byte_off):
+        r = 0
+        for n in range(8):
+            r ^= int(self.img[(byte_off + 64 * n + 4 * ((v >> (4 * n)) & 15)) >> 2])
+        return r
+
+    def pow_(self, v, k):  # v * x^(8*2^k)
+        return self._nib(v, K_NIB_BASE + K_POW_OFF + K_NIB_SET * k)
+
+    def inv(self, v, k):  # v * x^(-8*2^k)
+        return self._nib(v, K_IMG_INV_OFF + K_NIB_SET * k)
+
+    def step4(self, x):
+        T = self.T
+        return T[3][x & 0xFF] ^ T[2][(x >> 8) & 0xFF] ^ T[1][(x >> 16) & 0xFF] ^ T[0][x >> 24]
+
+    def runs(self, mem: bytes, reg0: int):
+        """Pass 1: rk[k] = raw CRC of bytes [64k, 64k + 64) of base (zeros outside the region)."""
+        nruns = (reg0 + len(mem) + 63) // 64
+        buf = bytes(reg0) + mem + bytes(nruns * 64 - reg0 - len(mem))
+        out = []
+        for k in range(nruns):
+            s = 0
+            for w in range(16):
+                s = self.step4(s ^ int.from_bytes(buf[64 * k + 4 * w:64 * k + 4 * w + 4], "little"))
+            out.append(s)
+        return out
+
+    def run_bytes(self, buf, r0, lo, hi, ninit):
+        """hash_run: four 4-step piece chains merged by x^(8*16), x^(8*32)."""
+        p = []
+        for q in range(4):
+            s = 0
+            for w in range(4 * q, 4 * q + 4):
+                v = 0
+                for b in range(4):
+                    o = 4 * w + b
+                    x = buf[r0 + o] if lo <= o < hi else 0
+                    if lo <= o < lo + ninit:
+                        x ^= 0xFF
+                    v |= x << (8 * b)
+                s = self.step4(s ^ v)
+            p.append(s)
+        return self.pow_(self.pow_(p[0], 4) ^ p[1], 5) ^ self.pow_(p[2], 4) ^ p[3]
+
+    def job_crc(self, mem: bytes, reg0: int, rk, off: int, ln: int) -> int:
+        if ln == 0:
+            return 0
+        nruns = len(rk)
+        buf = bytes(reg0) + mem + bytes(nruns * 64 - reg0 - len(mem))
+        pa = reg0 + off
+        pb = pa + ln
+        if ln < 4:
+            c = 0xFFFFFFFF
+            for i in range(pa, pb):
+                c = self.T[0][(c ^ buf[i]) & 0xFF] ^ (c >> 8)
+            return c ^ 0xFFFFFFFF
+        A0, B1 = pa & ~63, (pb + 63) & ~63
+        n, k0 = (B1 - A0) >> 6, A0 >> 6
+        lo, hi = pa - A0, min(pb - A0, 64)
+        tin = hi - lo
+        H = self.run_bytes(buf, A0, lo, hi, min(tin, 4))
+        if tin < 4:
+            H ^= 0xFFFFFFFF >> (8 * tin)
+        tail = n >= 2 and pb & 63 != 0
+        T = self.run_bytes(buf, B1 - 64, 0, pb - (B1 - 64), 0) if tail else 0
+        ng = (n + 3) >> 2
+        e0, elast = k0 + n - 4 * ng, k0 + n - 1
+        s = [0, 0, 0, 0]  # s[3]: updated last
+        for e in range(e0, e0 + 4 * ng):
+            v = 0 if e < k0 else H if e == k0 else T if (e == elast and tail) else rk[e]
+            nv = self.pow_(s[0], 8) ^ v
+            s = [s[1], s[2], s[3], nv]
+        V = s[3] ^ self.pow_(s[2], 6) ^ self.pow_(s[1], 7) ^ self.pow_(self.pow_(s[0], 6), 7)
+        d = B1 - pb
+        for k in range(K_INV_SETS):
+            if d >> k & 1:
+                V = self.inv(V, k)
+        return V ^ 0xFFFFFFFF
 
 
 def snap_cut(cs: int, ln: int, r: int) -> int:

@@ -94,9 +94,9 @@ def test_table_image_layout(ambry):
     """The LDS image's slice region holds T0..T3 at the v_perm-addressed, lane-replicated slots."""
     import ctypes
 
-    from kernel_model import K_LDS_BYTES
+    from kernel_model import K_IMG_BYTES
 
-    words = K_LDS_BYTES // 4 + 64
+    words = K_IMG_BYTES // 4
     buf = (ctypes.c_uint32 * words)()
     assert ambry.lib().ambrycrc_debug_table_image(buf, words) == words * 4
     img = np.frombuffer(buf, dtype=np.uint32)

@@ -14,14 +14,60 @@ from test_message_format import MF, build_region
 pytestmark = pytest.mark.gpu
 
 
-def run(gpu, region: bytes, offs):
+@pytest.fixture(autouse=True, params=["region", "jobs"])
+def msg_mode(request, gpu):
+    """Every test runs in both message-verify modes: region mode (one sweep of the region, record
+    CRCs from 64-B run sums; engaged for regions of <= 8 KiB per message) and CRC jobs through the
+    batch engine."""
+    gpu.set_region_mode(0, request.param == "region")
+    yield request.param
+    gpu.set_region_mode(0, True)
+
+
+def run(gpu, region: bytes, offs, shift: int = 0):
+    """Verify on the GPU; shift > 0 places the region `shift` bytes into its allocation."""
     import torch
 
-    r = torch.from_numpy(np.frombuffer(region, dtype=np.uint8).copy()).cuda()
+    buf = np.zeros(len(region) + shift, dtype=np.uint8)
+    buf[shift:] = np.frombuffer(region, dtype=np.uint8)
+    r = torch.from_numpy(buf).cuda()[shift:]
     o = torch.tensor(np.asarray(offs, dtype=np.int64), device="cuda")
     status, end = gpu.verify_messages(r, o)
     torch.cuda.synchronize()
     return status.cpu().numpy().view(np.uint32).tolist(), end.cpu().numpy().tolist()
+
+
+@pytest.mark.parametrize("shift", [0, 1, 13, 48, 63])
+def test_small_messages_unaligned_region(gpu, msg_mode, shift):
+    """Small PUT / update messages (region mode engages: < 8 KiB per message) with 8 % corrupted,
+    the region starting at every kind of offset from a 64-B boundary, so record ends fall on every
+    residue of the run grid; status and ends bit-exact vs the oracle."""
+    region, offs, expect = build_region(n=700, seed=40 + shift, corrupt_frac=0.08, big_every=10**9)
+    assert len(region) <= 8192 * len(offs)
+    st, end = run(gpu, region, offs, shift)
+    assert st == [s for s, _ in expect]
+    assert end == [e for _, e in expect]
+    assert sum(1 for s in st if s) >= 40
+
+
+def test_region_mode_sparse_and_overlapping_offsets(gpu, msg_mode):
+    """Messages listed out of order, one listed twice, gaps of junk between them, offsets past the
+    region end: region mode sweeps every byte and still reads each record's own runs."""
+    region, offs, _ = build_region(n=300, seed=77, corrupt_frac=0.05, big_every=10**9)
+    junk = bytes(range(256)) * 3
+    spaced, offs2 = bytearray(), []
+    for i, o in enumerate(offs):
+        e = offs[i + 1] if i + 1 < len(offs) else len(region)
+        if i % 7 == 3:
+            spaced += junk[: (i * 37) % 700]
+        offs2.append(len(spaced))
+        spaced += region[o:e]
+    spaced = bytes(spaced)
+    order = list(reversed(offs2)) + [offs2[5], len(spaced) + 3, len(spaced) - 1]
+    expect = [MF.verify_message(spaced, o) if o + 2 <= len(spaced) else (MF.BAD_LAYOUT, 0) for o in order]
+    st, end = run(gpu, spaced, order, shift=9)
+    assert st == [s for s, _ in expect]
+    assert end == [e for _, e in expect]
 
 
 @pytest.mark.parametrize("seed", [1, 2, 3])

@@ -94,3 +94,26 @@ def test_model_sweep_rounds(model, oracle, nwaves, window):
     exp = list(oracle.batch(mem, off, ln))
     assert model.batch(mem, off, ln, nwaves=nwaves, window=window, run=-4) == exp
     assert model.batch(mem, off, ln, nwaves=nwaves, window=window, min_share=16384) == exp
+
+
+def test_region_model_matches_zlib(ambry):
+    """Region mode's algebra (64-B run sums, head / tail runs from the bytes with the initial
+    register folded in, four Horner streams, x^(-8d) un-shift) against zlib, on jobs that start and
+    end at every residue mod 64 (and 1-3 B jobs), in regions whose start is not 64-aligned."""
+    import random
+    import zlib
+
+    from kernel_model import RegionModel, table_image
+
+    rm = RegionModel(table_image())
+    rng = random.Random(7)
+    for reg0 in (0, 5, 63):
+        mem = stream_bytes(900 + reg0, 0, 1500).tobytes()
+        rk = rm.runs(mem, reg0)
+        jobs = [(0, len(mem)), (0, 1), (1, 2), (2, 3), (len(mem) - 3, 3), (len(mem) - 4, 4)]
+        jobs += [(a, ln) for a in (0, 1, 58, 59, 60, 61, 62, 63, 64) for ln in (4, 5, 6, 7, 63, 64, 65, 127, 128, 129, 700)]
+        jobs += [(rng.randrange(0, 1000), rng.randrange(0, 500)) for _ in range(60)]
+        for a, ln in jobs:
+            if a + ln > len(mem):
+                continue
+            assert rm.job_crc(mem, reg0, rk, a, ln) == zlib.crc32(mem[a:a + ln]), (reg0, a, ln)
