@@ -126,8 +126,10 @@ struct RegionArgs {
 constexpr uint64_t kRunPad = 32;
 constexpr uint64_t kSuperBlock = 4096;
 // Region bytes per message up to which the message verify takes region mode (64-B run sums in
-// the workspace: region / 16 bytes) instead of CRC jobs through the batch engine.
-constexpr uint64_t kRegionMaxPerMessage = 8192;
+// the workspace: region / 16 bytes) instead of CRC jobs through the batch engine. Measured
+// crossover (profiles/r03z4_messages.jsonl, one box, ~1.3 GB regions): 2.2 KiB per message region
+// 1.20x, 3.2 KiB 1.06x, 4.2 KiB 0.99x, 5.3 KiB 0.96x.
+constexpr uint64_t kRegionMaxPerMessage = 4096;
 inline uint64_t region_nsb(const uint8_t* region, uint64_t len) {
   const uint64_t b = reinterpret_cast<uintptr_t>(region) & ~uint64_t(63);
   return (reinterpret_cast<uintptr_t>(region) + len - b + kSuperBlock - 1) / kSuperBlock;

@@ -1558,30 +1558,19 @@ __device__ __forceinline__ void region_sb_zero(const RegionArgs& a, uint64_t s, 
   }
 }
 
-// A/B knobs: AMBRY_RUNS_PROBE 1 = no run sums into LDS, 4 = every store of a wave to one 1 KiB
-// line set, 5 = no global stores (timing only, wrong sums); AMBRY_RUNS_STORE_NT 0 = plain stores.
+// A/B knobs: AMBRY_RUNS_PROBE 1 = no run sums into LDS, 5 = no global stores,
+// 6 = every wave's stores to one 1 KiB line set (timing only, wrong sums); AMBRY_RUNS_STORE_NT 0 =
+// plain stores.
 #ifndef AMBRY_RUNS_STORE_NT
-#define AMBRY_RUNS_STORE_NT 1
-#endif
-#ifndef AMBRY_RUNS_IL
-#define AMBRY_RUNS_IL 0
-#endif
-#ifndef AMBRY_RUNS_CU_MAJOR
-#define AMBRY_RUNS_CU_MAJOR 1
+#define AMBRY_RUNS_STORE_NT 0
 #endif
 #ifndef AMBRY_RUNS_PROBE
 #define AMBRY_RUNS_PROBE 0
 #endif
 __global__ __launch_bounds__(1024) void region_runs_kernel(RegionArgs a) {
   const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-  // Shares CU-major (the waves of a workgroup take adjacent shares) once every wave has at least a
-  // few super-blocks: a CU then reads from a few translation pages and stores its run sums into
-  // one, where wave-major shares (the sweep kernel's, which spread a small batch over every CU)
-  // put 16 read and 16 store streams pages apart on each CU -- address translation, not HBM,
-  // then cost pass 1 a quarter of its time. Smaller regions stay wave-major.
-  const bool cu_major = AMBRY_RUNS_CU_MAJOR && a.nsb >= 4 * nwaves;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(cu_major ? blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)
-                                                                : (threadIdx.x >> 6) * gridDim.x + blockIdx.x);
+  // Shares wave-major over workgroups, as the sweep kernel's (CU-major shares measured the same).
+  const uint32_t wave = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * gridDim.x + blockIdx.x);
   const uint64_t s0 = a.nsb * wave / nwaves, s1 = a.nsb * (wave + 1) / nwaves;
   {  // LDS-DMA of the slice tables (image bytes [0, 128 KiB)), as fill_lds
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -1594,38 +1583,6 @@ __global__ __launch_bounds__(1024) void region_runs_kernel(RegionArgs a) {
   }
   const uint32_t lane = threadIdx.x & 63u;
   const LaneConst k = make_lane_const(lane);
-#if AMBRY_RUNS_IL
-  // Interleaved: wave w hashes super-blocks w, w + nwaves, ... (all waves inside one window of the
-  // region, and their stores inside one window of rk); a 4-B store per lane per super-block.
-  {
-    uint32_t* out = a.rk + kRunPad + 16u * (lane & 3u) + (lane >> 2);
-    const uint64_t last = a.nsb - 1;
-    auto nx = [&](uint64_t s) { return s < a.nsb ? s : last; };
-    u32x4 c0[4], c1[4], c2[4], c3[4];
-    region_sb_load(a, nx(wave), lane, c0);
-    region_sb_load(a, nx(wave + nwaves), lane, c1);
-    region_sb_load(a, nx(wave + 2 * nwaves), lane, c2);
-    region_sb_load(a, nx(wave + 3 * nwaves), lane, c3);
-    auto h = [&](uint64_t s, u32x4 (&cur)[4]) {
-      region_sb_zero(a, s, lane, cur);
-      quad_transpose_asm(cur);
-      const uint32_t r = run_crc<4, 1>(cur, k, 0u);
-      __builtin_nontemporal_store(r, out + (s < a.nsb ? s : a.nsb) * 64);  // past the end: the spill line
-    };
-    if (wave >= a.nsb) return;
-    for (uint64_t s = wave; s < a.nsb; s += 4 * nwaves) {
-      h(s, c0);
-      region_sb_load(a, nx(s + 4 * nwaves), lane, c0);
-      h(s + nwaves, c1);
-      region_sb_load(a, nx(s + 5 * nwaves), lane, c1);
-      h(s + 2 * nwaves, c2);
-      region_sb_load(a, nx(s + 6 * nwaves), lane, c2);
-      h(s + 3 * nwaves, c3);
-      region_sb_load(a, nx(s + 7 * nwaves), lane, c3);
-    }
-    return;
-  }
-#endif
   if (s0 >= s1) return;
   // Four super-block buffers: while one is hashed the next three are in flight. Each buffer is
   // hashed in place and only then reloaded (no register copies of loads still in flight), and every
@@ -1667,7 +1624,6 @@ __global__ __launch_bounds__(1024) void region_runs_kernel(RegionArgs a) {
     __builtin_amdgcn_s_setprio(0);
     const u32x4 v = *reinterpret_cast<const u32x4*>(buf + 4u * lane);
     u32x4* dst = 4u * lane < 64u * (s1 - s) ? reinterpret_cast<u32x4*>(a.rk + kRunPad + s * 64) + lane : spill;
-    if constexpr (AMBRY_RUNS_PROBE == 4) dst = reinterpret_cast<u32x4*>(a.rk + kRunPad + s0 * 64) + lane;
     if constexpr (AMBRY_RUNS_PROBE == 6) dst = reinterpret_cast<u32x4*>(a.rk + kRunPad) + lane;
     if constexpr (AMBRY_RUNS_PROBE == 5) {
       if (v.x == 0x9E3779B9u) *dst = v;

@@ -123,7 +123,7 @@ def gpu_region(mf, m, blob_bytes, reps, variant=None, host=False, mode="region")
     times.sort()
     med = times[len(times) // 2]
     res = {"config": f"verify {m} x PUT({blob_bytes} B blob)", "variant": variant,
-           "mode": mode if m * L <= 8192 * m else "jobs (region > 8 KiB per message)", "messages": m, "region_bytes": m * L,
+           "mode": mode if L <= 4096 else "jobs (region > 4 KiB per message)", "messages": m, "region_bytes": m * L,
            "ms_median": round(med, 4), "GiBps": round(m * L / (med / 1e3) / 2**30, 1),
            "messages_per_s": round(m / (med / 1e3)), "parity": "clean=0, 1% injected flips flagged exactly"}
     if host and m * L <= (5 << 30):
@@ -163,7 +163,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--no-gpu", action="store_true")
     ap.add_argument("--variants", default="29")
-    ap.add_argument("--cases", default="64k,4m,4k", help="subset of 64k,4m,4k,1k,100")
+    ap.add_argument("--cases", default="64k,4m,4k", help="subset of 64k,4m,4k,3k,2k,1k,100")
     ap.add_argument("--modes", default="region", help="message-verify modes: region,jobs")
     ap.add_argument("--host", action="store_true", help="also time the host-region path (regions <= 5 GiB)")
     args = ap.parse_args()
@@ -171,8 +171,8 @@ def main():
     print(json.dumps(c1_cpu(mf)), flush=True)
     if args.no_gpu:
         return
-    cases = {"64k": (65536, 64 << 10), "4m": (4096, 4 << 20), "4k": (262144, 4 << 10), "1k": (524288, 1 << 10),
-             "100": (1048576, 100)}
+    cases = {"64k": (65536, 64 << 10), "4m": (4096, 4 << 20), "4k": (262144, 4 << 10), "3k": (327680, 3 << 10),
+             "2k": (393216, 2 << 10), "1k": (524288, 1 << 10), "100": (1048576, 100)}
     for m, s in (cases[c] for c in args.cases.split(",")):
         for v in [int(x) for x in args.variants.split(",")]:
             for mode in args.modes.split(","):
