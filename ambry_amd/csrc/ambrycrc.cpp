@@ -571,6 +571,11 @@ int ambrycrc_init(int device) {
     if (end != v && *end == '\0' && x >= 0 && x < 1000 && variant_supported((int)x)) c->variant = (int)x;
   }
   if (const char* v = getenv("AMBRYCRC_REGION")) c->region_mode = strcmp(v, "0") != 0;
+  if (const char* v = getenv("AMBRYCRC_REGION_MAX_PER_MESSAGE")) {  // A/B: the region-mode cut-off
+    char* end = nullptr;
+    const unsigned long long x = strtoull(v, &end, 10);
+    if (end != v && *end == '\0' && x > 0 && x <= (1ull << 30)) c->region_max = x;
+  }
   std::vector<uint32_t> img = build_table_image();
   if (hipMalloc(reinterpret_cast<void**>(&c->d_img), img.size() * 4) != hipSuccess) {
     delete c;
@@ -936,7 +941,7 @@ size_t msg_jobs_bytes(size_t m) {
 
 int enqueue_messages(DevCtx* c, const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off, size_t m,
                      uint32_t* d_status, uint64_t* d_msg_end, void* d_ws, size_t ws_bytes, hipStream_t stream) {
-  const bool region = c->region_mode && region_len > 0 && region_len <= kRegionMaxPerMessage * (uint64_t)m &&
+  const bool region = c->region_mode && region_len > 0 && region_len <= c->region_max * (uint64_t)m &&
                       msg_jobs_bytes(m) + region_ws_bytes(d_region, region_len) <= ws_bytes;
   MsgStage st;
   if (!region) {
@@ -1062,7 +1067,11 @@ int ambrycrc_verify_messages_dev(const uint8_t* d_region, uint64_t region_len, c
   DevCtx* c = ctx_current();
   if (!c) return AMBRYCRC_ENOINIT;
   WsLease lease;
-  const size_t need = ambrycrc_messages_workspace_bytes(m);
+  size_t need = ambrycrc_messages_workspace_bytes(m);
+  // The library's own workspace also covers region mode past the default per-message size
+  // (AMBRYCRC_REGION_MAX_PER_MESSAGE, for A/B runs); a caller's is used as sized.
+  if (!d_ws && c->region_mode && region_len <= c->region_max * (uint64_t)m)
+    need = std::max(need, msg_jobs_bytes(m) + region_ws_bytes(d_region, region_len));
   const int rc = lease.acquire(c, stream, &d_ws, ws_bytes, need);
   if (rc) return rc;
   return enqueue_messages(c, d_region, region_len, d_msg_off, m, d_status, d_msg_end, d_ws,

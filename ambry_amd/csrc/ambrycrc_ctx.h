@@ -66,6 +66,7 @@ struct DevCtx {
   // Message verify of regions of at most kRegionMaxPerMessage bytes per message: region mode
   // (region_runs_kernel + region_jobs_kernel) instead of jobs through the batch engine.
   bool region_mode = true;
+  uint64_t region_max = kRegionMaxPerMessage;  // region bytes per message up to which it applies
   // Sweep rounds of at most this many bytes (SweepArgs::window); 0 = one round.
   uint64_t window = 32ull << 30;
   uint32_t* d_img = nullptr;

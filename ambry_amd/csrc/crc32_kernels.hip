@@ -1564,6 +1564,9 @@ __device__ __forceinline__ void region_sb_zero(const RegionArgs& a, uint64_t s, 
 #ifndef AMBRY_RUNS_STORE_NT
 #define AMBRY_RUNS_STORE_NT 0
 #endif
+#ifndef AMBRY_RUNS_GIL
+#define AMBRY_RUNS_GIL 1
+#endif
 #ifndef AMBRY_RUNS_PROBE
 #define AMBRY_RUNS_PROBE 0
 #endif
@@ -1571,7 +1574,6 @@ __global__ __launch_bounds__(1024) void region_runs_kernel(RegionArgs a) {
   const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
   // Shares wave-major over workgroups, as the sweep kernel's (CU-major shares measured the same).
   const uint32_t wave = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * gridDim.x + blockIdx.x);
-  const uint64_t s0 = a.nsb * wave / nwaves, s1 = a.nsb * (wave + 1) / nwaves;
   {  // LDS-DMA of the slice tables (image bytes [0, 128 KiB)), as fill_lds
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
     for (uint32_t c = wv; c < kSliceBytes / 1024; c += nw)
@@ -1583,16 +1585,25 @@ __global__ __launch_bounds__(1024) void region_runs_kernel(RegionArgs a) {
   }
   const uint32_t lane = threadIdx.x & 63u;
   const LaneConst k = make_lane_const(lane);
-  if (s0 >= s1) return;
+  // Groups of four super-blocks: contiguous shares (wave w: [s0, s1) in steps of 4), or with
+  // AMBRY_RUNS_GIL interleaved over the waves (wave w: groups w, w + nwaves, ...), which keeps all
+  // waves' concurrent reads inside a 64 MiB window and their stores inside 4 MiB.
+#if AMBRY_RUNS_GIL
+  const uint64_t first = 4 * (uint64_t)wave, step = 4 * nwaves, end = a.nsb;
+#else
+  const uint64_t first = a.nsb * wave / nwaves, step = 4, end = a.nsb * (wave + 1) / nwaves;
+#endif
+  if (first >= end) return;
   // Four super-block buffers: while one is hashed the next three are in flight. Each buffer is
   // hashed in place and only then reloaded (no register copies of loads still in flight), and every
-  // load and store is issued on every path (indices past the share re-read its last super-block;
+  // load and store is issued on every path (indices past the end re-read the last super-block;
   // lanes with nothing to store write the workspace's spill line), so each wait is for the oldest
-  // buffer only. The four super-blocks' sums gather in the wave's LDS buffer (word 64u + run
+  // buffer only. A group's four super-blocks' sums gather in the wave's LDS buffer (word 64u + run
   // index) and go out as one 16-B store per lane: 1 KiB contiguous per wave, 8 whole 128-B lines.
   uint32_t* buf = g_lds_runs + kSliceBytes / 4 + (threadIdx.x >> 6) * (kRunsBufBytes / 4);
   const uint32_t slot = 16u * (lane & 3u) + (lane >> 2);
-  const uint64_t slast = s1 - 1;
+  const uint64_t slast = end - 1;
+  auto at = [&](uint64_t s) { return s < end ? s : slast; };
   auto hash = [&](uint64_t s, uint32_t u, u32x4 (&cur)[4]) {
     region_sb_zero(a, s, lane, cur);
     quad_transpose_asm(cur);
@@ -1600,30 +1611,31 @@ __global__ __launch_bounds__(1024) void region_runs_kernel(RegionArgs a) {
     if (AMBRY_RUNS_PROBE == 0 || r == 0x9E3779B9u) buf[64u * u + slot] = r;
   };
   u32x4 b0[4], b1[4], b2[4], b3[4];
-  region_sb_load(a, s0, lane, b0);
-  region_sb_load(a, s0 + 1 < s1 ? s0 + 1 : slast, lane, b1);
-  region_sb_load(a, s0 + 2 < s1 ? s0 + 2 : slast, lane, b2);
-  region_sb_load(a, s0 + 3 < s1 ? s0 + 3 : slast, lane, b3);
+  region_sb_load(a, first, lane, b0);
+  region_sb_load(a, at(first + 1), lane, b1);
+  region_sb_load(a, at(first + 2), lane, b2);
+  region_sb_load(a, at(first + 3), lane, b3);
   u32x4* spill = reinterpret_cast<u32x4*>(a.rk + kRunPad + a.nsb * 64) + lane;
-  for (uint64_t s = s0; s < s1; s += 4) {
-    hash(s, 0, b0);
+  for (uint64_t g = first; g < end; g += step) {
+    const uint64_t nx = g + step;
+    hash(g, 0, b0);
     __builtin_amdgcn_s_setprio(3);
-    region_sb_load(a, s + 4 < s1 ? s + 4 : slast, lane, b0);
+    region_sb_load(a, at(nx), lane, b0);
     __builtin_amdgcn_s_setprio(0);
-    if (s + 1 < s1) hash(s + 1, 1, b1);
+    if (g + 1 < end) hash(g + 1, 1, b1);
     __builtin_amdgcn_s_setprio(3);
-    region_sb_load(a, s + 5 < s1 ? s + 5 : slast, lane, b1);
+    region_sb_load(a, at(nx + 1), lane, b1);
     __builtin_amdgcn_s_setprio(0);
-    if (s + 2 < s1) hash(s + 2, 2, b2);
+    if (g + 2 < end) hash(g + 2, 2, b2);
     __builtin_amdgcn_s_setprio(3);
-    region_sb_load(a, s + 6 < s1 ? s + 6 : slast, lane, b2);
+    region_sb_load(a, at(nx + 2), lane, b2);
     __builtin_amdgcn_s_setprio(0);
-    if (s + 3 < s1) hash(s + 3, 3, b3);
+    if (g + 3 < end) hash(g + 3, 3, b3);
     __builtin_amdgcn_s_setprio(3);
-    region_sb_load(a, s + 7 < s1 ? s + 7 : slast, lane, b3);
+    region_sb_load(a, at(nx + 3), lane, b3);
     __builtin_amdgcn_s_setprio(0);
     const u32x4 v = *reinterpret_cast<const u32x4*>(buf + 4u * lane);
-    u32x4* dst = 4u * lane < 64u * (s1 - s) ? reinterpret_cast<u32x4*>(a.rk + kRunPad + s * 64) + lane : spill;
+    u32x4* dst = 4u * lane < 64u * (end - g) ? reinterpret_cast<u32x4*>(a.rk + kRunPad + g * 64) + lane : spill;
     if constexpr (AMBRY_RUNS_PROBE == 6) dst = reinterpret_cast<u32x4*>(a.rk + kRunPad) + lane;
     if constexpr (AMBRY_RUNS_PROBE == 5) {
       if (v.x == 0x9E3779B9u) *dst = v;
