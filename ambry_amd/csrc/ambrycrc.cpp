@@ -970,7 +970,7 @@ int enqueue_messages(DevCtx* c, const uint8_t* d_region, uint64_t region_len, co
   r.rk = static_cast<uint32_t*>(st.batch_ws);
   r.img = c->d_img;
   if (launch_region_runs(r, c->grid, stream) != hipSuccess) return AMBRYCRC_EHIP;
-  return hip_err(launch_region_msg(st.a, r, stream));
+  return hip_err(launch_region_msg(st.a, r, c->num_cu, stream));
 }
 
 int enqueue_messages_parse(DevCtx* c, const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off,

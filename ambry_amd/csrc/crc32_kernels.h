@@ -126,10 +126,10 @@ struct RegionArgs {
 constexpr uint64_t kRunPad = 32;
 constexpr uint64_t kSuperBlock = 4096;
 // Region bytes per message up to which the message verify takes region mode (64-B run sums in
-// the workspace: region / 16 bytes) instead of CRC jobs through the batch engine. Measured
-// crossover (profiles/r03z4_messages.jsonl, one box, ~1.3 GB regions): 2.2 KiB per message region
-// 1.20x, 3.2 KiB 1.06x, 4.2 KiB 0.99x, 5.3 KiB 0.96x.
-constexpr uint64_t kRegionMaxPerMessage = 4096;
+// the workspace: region / 16 bytes) instead of CRC jobs through the batch engine. Region / job
+// mode per call (profiles/r03za_messages.jsonl, one box, ~1.3 GB regions): 1.3 KiB per message
+// 1.21x, 2.2 KiB 1.35x, 3.2 KiB 1.17x, 4.2 KiB 1.07x, 5.3 KiB 1.02x; 64 KiB blobs stream in job mode.
+constexpr uint64_t kRegionMaxPerMessage = 6144;
 inline uint64_t region_nsb(const uint8_t* region, uint64_t len) {
   const uint64_t b = reinterpret_cast<uintptr_t>(region) & ~uint64_t(63);
   return (reinterpret_cast<uintptr_t>(region) + len - b + kSuperBlock - 1) / kSuperBlock;
@@ -284,7 +284,7 @@ hipError_t launch_trailer_verify(const TrailerArgs& a, hipStream_t s);
 
 hipError_t launch_msg_parse(const MsgArgs& a, hipStream_t s);
 // Region mode, pass 2: parse, record CRCs from the run sums, status (a.job_* / expected / crc unused).
-hipError_t launch_region_msg(const MsgArgs& a, const RegionArgs& g, hipStream_t s);
+hipError_t launch_region_msg(const MsgArgs& a, const RegionArgs& g, int num_cu, hipStream_t s);
 hipError_t launch_msg_reduce(const MsgArgs& a, hipStream_t s);
 
 hipError_t launch_plan(const PlanArgs& a, hipStream_t s);

@@ -338,60 +338,69 @@ __global__ __launch_bounds__(256) void msg_parse_kernel(MsgArgs a, TransformArgs
 // (every stored CRC read here), assembles each record's CRC from the run sums of pass 1
 // (region_crc.h) and writes the message's status: parse, CRC jobs, plan, sweep and reduce in one
 // kernel, with no job arrays.
+// Grid: AMBRY_REGION_BPC 256-thread blocks per CU (8 waves), each thread looping over messages,
+// registers allowed for 2 waves per SIMD (AMBRY_REGION_WPE). Fewer messages in flight keep each
+// thread's header / record-head lines in L2 until its own end-run reads (A/B, 4 KiB-blob messages:
+// one thread per message at 16 waves per CU 120.1 us; 2 blocks per CU 104.9, with WPE 2 102.7; 3
+// blocks 109.5; 1 block 135.4). 0 = one thread per message.
 #ifndef AMBRY_REGION_WPE
-#define AMBRY_REGION_WPE 4
+#define AMBRY_REGION_WPE 2
+#endif
+#ifndef AMBRY_REGION_BPC
+#define AMBRY_REGION_BPC 2
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AMBRY_REGION_WPE))) void region_msg_kernel(
     MsgArgs a, RegionArgs g) {
   __shared__ uint32_t tbl[1024];
   __shared__ uint32_t pwin[256 * kPropsSlotWords];
   __shared__ uint32_t nib[region::kSets * region::kNibWords];
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool live = i < a.m;
-  PropsFields pf;
-  bool pf_ok = false;
-  const uint64_t off = live ? a.msg_off[i] : 0;
-  const bool in_region = live && off <= a.region_len;
-  const uint64_t rem = in_region ? a.region_len - off : 0;
-  const uint8_t* p = a.region + (in_region ? off : 0);
-  const HeaderWords hw = load_header(p, rem);
   stage_slice_tables(tbl, a.img);
   region::stage_nib(nib, a.img);
   __syncthreads();
-  if (!live) return;
   uint32_t* slot = pwin + threadIdx.x * kPropsSlotWords;
-  uint32_t status;
-  uint64_t end;
-  {
-    MsgParse r;
-    parse_message<false>(off, in_region, rem, p, hw, tbl, slot, 0, r, pf, pf_ok);
-    // The jobs go to this thread's LDS slot (the properties window is done with), so the five
-    // descriptors do not stay live in VGPRs across the record CRCs: 4 words per slot, job start
-    // relative to the message (records < 4 GiB: an int32 size field, blobs <= Integer.MAX_VALUE).
-#pragma unroll
-    for (int k = 0; k < kMsgSlots; ++k) {
-      slot[4 * k] = (uint32_t)(r.jo[k] - off);
-      slot[4 * k + 1] = (uint32_t)((r.jo[k] - off) >> 32);
-      slot[4 * k + 2] = (uint32_t)r.jl[k];
-      slot[4 * k + 3] = r.ex[k];
-    }
-    status = r.status;
-    end = r.end;
-  }
-  static_assert(4 * kMsgSlots <= kPropsSlotWords, "job slots fit the properties window");
   const uint32_t* rk = g.rk + kRunPad;
-  for (int k = 0; k < kMsgSlots; ++k) {
-    const uint64_t jo = off + ((uint64_t)slot[4 * k + 1] << 32 | slot[4 * k]);
-    const uint32_t jl = slot[4 * k + 2], ex = slot[4 * k + 3];
+  // Grid-stride over the messages (a grid of one thread per message unless capped; no barrier
+  // below, so threads leave the loop independently).
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.m; i += (uint64_t)gridDim.x * blockDim.x) {
+    PropsFields pf;
+    bool pf_ok = false;
+    const uint64_t off = a.msg_off[i];
+    const bool in_region = off <= a.region_len;
+    const uint64_t rem = in_region ? a.region_len - off : 0;
+    const uint8_t* p = a.region + (in_region ? off : 0);
+    const HeaderWords hw = load_header(p, rem);
+    uint32_t status;
+    uint64_t end;
+    {
+      MsgParse r;
+      parse_message<false>(off, in_region, rem, p, hw, tbl, slot, 0, r, pf, pf_ok);
+      // The jobs go to this thread's LDS slot (the properties window is done with), so the five
+      // descriptors do not stay live in VGPRs across the record CRCs: 4 words per slot, job start
+      // relative to the message (records < 4 GiB: an int32 size field, blobs <= Integer.MAX_VALUE).
+#pragma unroll
+      for (int k = 0; k < kMsgSlots; ++k) {
+        slot[4 * k] = (uint32_t)(r.jo[k] - off);
+        slot[4 * k + 1] = (uint32_t)((r.jo[k] - off) >> 32);
+        slot[4 * k + 2] = (uint32_t)r.jl[k];
+        slot[4 * k + 3] = r.ex[k];
+      }
+      status = r.status;
+      end = r.end;
+    }
+    static_assert(4 * kMsgSlots <= kPropsSlotWords, "job slots fit the properties window");
+    for (int k = 0; k < kMsgSlots; ++k) {
+      const uint64_t jo = off + ((uint64_t)slot[4 * k + 1] << 32 | slot[4 * k]);
+      const uint32_t jl = slot[4 * k + 2], ex = slot[4 * k + 3];
 #if AMBRY_REGION_PROBE == 1
-    const uint32_t c = ex;
+      const uint32_t c = ex;
 #else
-    const uint32_t c = jl ? region::record_crc(tbl, nib, g.base, rk, g.reg0 + jo, jl) : 0u;
+      const uint32_t c = jl ? region::record_crc(tbl, nib, g.base, rk, g.reg0 + jo, jl) : 0u;
 #endif
-    if (c != ex) status |= AMBRYCRC_MSG_ENCKEY_CRC << k;
+      if (c != ex) status |= AMBRYCRC_MSG_ENCKEY_CRC << k;
+    }
+    a.status[i] = status;
+    if (a.msg_end) a.msg_end[i] = end ? off + end : 0;
   }
-  a.status[i] = status;
-  if (a.msg_end) a.msg_end[i] = end ? off + end : 0;
 }
 
 __global__ __launch_bounds__(256) void msg_reduce_kernel(MsgArgs a) {
@@ -763,9 +772,11 @@ hipError_t launch_msg_parse_desc(const MsgArgs& a, const TransformArgs& t, hipSt
   return hipGetLastError();
 }
 
-hipError_t launch_region_msg(const MsgArgs& a, const RegionArgs& g, hipStream_t s) {
+hipError_t launch_region_msg(const MsgArgs& a, const RegionArgs& g, int num_cu, hipStream_t s) {
   if (a.m == 0) return hipSuccess;
-  hipLaunchKernelGGL(region_msg_kernel, dim3((uint32_t)((a.m + 255) / 256)), dim3(256), 0, s, a, g);
+  uint64_t blocks = (a.m + 255) / 256;
+  if (AMBRY_REGION_BPC > 0 && blocks > (uint64_t)num_cu * AMBRY_REGION_BPC) blocks = (uint64_t)num_cu * AMBRY_REGION_BPC;
+  hipLaunchKernelGGL(region_msg_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, a, g);
   return hipGetLastError();
 }
 

@@ -453,7 +453,7 @@ int ambrycrc_range_checksums_host(const uint8_t* file, uint64_t file_len, const 
  * the current one. */
 int ambrycrc_set_variant(int device, int variant);
 int ambrycrc_get_variant(int device);
-/* Message verify (ambrycrc_verify_messages_dev / _host) of a region of at most 4 KiB per
+/* Message verify (ambrycrc_verify_messages_dev / _host) of a region of at most 6 KiB per
  * message: region mode (1, the default; AMBRYCRC_REGION=0 in the environment at init turns it
  * off) sweeps the region once as contiguous memory, keeping the raw CRC of every 64-B run, and
  * assembles each record's CRC from the runs it covers, re-reading only the two runs its ends

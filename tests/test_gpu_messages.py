@@ -17,7 +17,7 @@ pytestmark = pytest.mark.gpu
 @pytest.fixture(autouse=True, params=["region", "jobs"])
 def msg_mode(request, gpu):
     """Every test runs in both message-verify modes: region mode (one sweep of the region, record
-    CRCs from 64-B run sums; engaged for regions of <= 4 KiB per message) and CRC jobs through the
+    CRCs from 64-B run sums; engaged for regions of <= 6 KiB per message) and CRC jobs through the
     batch engine."""
     gpu.set_region_mode(0, request.param == "region")
     yield request.param
@@ -39,11 +39,11 @@ def run(gpu, region: bytes, offs, shift: int = 0):
 
 @pytest.mark.parametrize("shift", [0, 1, 13, 48, 63])
 def test_small_messages_unaligned_region(gpu, msg_mode, shift):
-    """Small PUT / update messages (region mode engages: < 4 KiB per message) with 8 % corrupted,
+    """Small PUT / update messages (region mode engages: < 6 KiB per message) with 8 % corrupted,
     the region starting at every kind of offset from a 64-B boundary, so record ends fall on every
     residue of the run grid; status and ends bit-exact vs the oracle."""
     region, offs, expect = build_region(n=700, seed=40 + shift, corrupt_frac=0.08, big_every=10**9)
-    assert len(region) <= 4096 * len(offs)
+    assert len(region) <= 6144 * len(offs)
     st, end = run(gpu, region, offs, shift)
     assert st == [s for s, _ in expect]
     assert end == [e for _, e in expect]

@@ -123,7 +123,8 @@ def gpu_region(mf, m, blob_bytes, reps, variant=None, host=False, mode="region")
     times.sort()
     med = times[len(times) // 2]
     res = {"config": f"verify {m} x PUT({blob_bytes} B blob)", "variant": variant,
-           "mode": mode if L <= 4096 else "jobs (region > 4 KiB per message)", "messages": m, "region_bytes": m * L,
+           "mode": mode if L <= int(os.environ.get("AMBRYCRC_REGION_MAX_PER_MESSAGE", "6144")) else
+                   "jobs (region > cut-off per message)", "messages": m, "region_bytes": m * L,
            "ms_median": round(med, 4), "GiBps": round(m * L / (med / 1e3) / 2**30, 1),
            "messages_per_s": round(m / (med / 1e3)), "parity": "clean=0, 1% injected flips flagged exactly"}
     if host and m * L <= (5 << 30):
