@@ -64,7 +64,7 @@ struct DevCtx {
 #endif
   int variant = AMBRY_DEFAULT_VARIANT;  // (A/B builds: -DAMBRY_DEFAULT_VARIANT=...)
   // Message verify of regions of at most kRegionMaxPerMessage bytes per message: region mode
-  // (region_runs_kernel + region_jobs_kernel) instead of jobs through the batch engine.
+  // (region_runs_kernel + region_msg_kernel) instead of jobs through the batch engine.
   bool region_mode = true;
   uint64_t region_max = kRegionMaxPerMessage;  // region bytes per message up to which it applies
   // Sweep rounds of at most this many bytes (SweepArgs::window); 0 = one round.

@@ -1538,7 +1538,7 @@ hipError_t launch_sweep_copy(const SweepArgs& a, int grid, int variant, hipStrea
 // [64m, 64m + 64) of block j, one 16-step slice-by-4 chain from a zero register gives its raw
 // CRC, stored at run index 16j + m of the super-block. Loads are unconditional: a piece outside
 // the region reads the nearest piece that holds region bytes, zeroed after (the run sums of
-// runs that straddle the region's ends are never used; region_jobs_kernel recomputes those
+// runs that straddle the region's ends are never used; region_msg_kernel (region_crc.h) recomputes those
 // runs from the bytes). Runs have no loop-carried state, so consecutive super-blocks' chains
 // are independent.
 __device__ __forceinline__ void region_sb_load(const RegionArgs& a, uint64_t s, uint32_t lane, u32x4 (&x)[4]) {

@@ -32,7 +32,7 @@ static_assert(kPowOff + kPowTables * kNibSetBytes < 65536u, "nibble offsets must
 
 // The global image (not staged by the sweep): kLdsBytes of LDS image, 64 words x^(8*2^k), then
 // the nibble sets of x^(-8*2^k), k = 0..kInvPowSets-1 (region mode's final un-shift,
-// region_kernels.hip).
+// region_crc.h).
 constexpr uint32_t kImgInvOff = kLdsBytes + 256u;
 constexpr uint32_t kInvPowSets = 6;
 constexpr uint32_t kImgBytes = kImgInvOff + kInvPowSets * kNibSetBytes;

@@ -336,8 +336,8 @@ class KernelModel:
 
 
 class RegionModel:
-    """Region mode of the message verify (crc32_kernels.hip region_runs_kernel, region_kernels.hip
-    region_jobs_kernel), scalar: run sums of the 64-B runs from base = region start rounded down
+    """Region mode of the message verify (crc32_kernels.hip region_runs_kernel, region_crc.h
+    record_crc), scalar: run sums of the 64-B runs from base = region start rounded down
     to 64 B, then each job's CRC from its head / tail runs' bytes, the run sums between, four
     Horner streams and the x^(-8d) un-shift, with the image's one-copy slice tables and nibble
     sets exactly as the kernel addresses them."""
