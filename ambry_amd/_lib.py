@@ -22,6 +22,7 @@ AMBRYCRC_ENOMEM = -3
 AMBRYCRC_ENOINIT = -4
 AMBRYCRC_ENODEV = -5
 AMBRYCRC_ECOMM = -6
+AMBRYCRC_EPROBE = -7
 UNIQUE_ID_BYTES = 128
 
 
@@ -78,6 +79,7 @@ _SIGNATURES = [
     ("ambrycrc_serialize_puts_dev", ctypes.c_int,
      [_u8p, ctypes.c_size_t, _u8p, _u8p, _u8p, _u8p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
     ("ambrycrc_transform_workspace_bytes", ctypes.c_size_t, [ctypes.c_size_t]),
+    ("ambrycrc_transform_out_bound", ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_size_t]),
     ("ambrycrc_transform_messages_dev", ctypes.c_int,
      [_u8p, ctypes.c_uint64, _u8p, ctypes.c_size_t, _u8p, ctypes.c_int, _u8p, ctypes.c_uint64, _u8p, _u8p, _u8p,
       ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),

@@ -14,6 +14,7 @@
 #include <condition_variable>
 #include <functional>
 #include <mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -376,8 +377,8 @@ int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uin
     }
     if (hipEventRecord(ev.a, s) != hipSuccess) return AMBRYCRC_EHIP;
   }
-  e = copy_dst ? launch_sweep_copy(t, c->grid, c->variant == kVariantSplit ? kVariantSplit : kVariantDefault, s)
-               : launch_sweep(t, c->grid, c->variant, s);
+  e = copy_dst ? launch_sweep_copy(t, c->grid, c->num_cu, c->variant == kVariantSplit ? kVariantSplit : kVariantDefault, s)
+               : launch_sweep(t, c->grid, c->num_cu, c->variant, s);
   if (e != hipSuccess) return AMBRYCRC_EHIP;
   if (c->timing) {
     if (hipEventRecord(ev.b, s) != hipSuccess) return AMBRYCRC_EHIP;
@@ -474,11 +475,25 @@ const char* ambrycrc_strerror(int code) {
     case AMBRYCRC_ENOINIT: return "ambrycrc_init() not called for the current device";
     case AMBRYCRC_ENODEV: return "no usable gfx950 device";
     case AMBRYCRC_ECOMM: return "RCCL unavailable or a collective call failed";
+    case AMBRYCRC_EPROBE: return "A/B probe build (wrong CRCs) refused: set AMBRYCRC_ALLOW_PROBE=1 to time it";
     default: return "unknown error";
   }
 }
 
-const char* ambrycrc_version(void) { return "ambrycrc 0.1.0 gfx950"; }
+const char* ambrycrc_version(void) {
+  // "ambrycrc <semver> gfx950", then " ab-probe-build" and " AMBRY_X=v" for every compile-time
+  // knob that differs from its product default (build_knobs.h): the product build has neither.
+  static const std::string v = [] {
+    std::string s = "ambrycrc 0.4.0 gfx950";
+    if (AMBRY_IS_PROBE_BUILD) s += " ab-probe-build";
+#define AMBRY_KNOB_REPORT(name, def) \
+  if ((long)(name) != (long)(def)) s += " " #name "=" + std::to_string((long)(name));
+    AMBRY_KNOB_LIST(AMBRY_KNOB_REPORT)
+#undef AMBRY_KNOB_REPORT
+    return s;
+  }();
+  return v.c_str();
+}
 
 uint32_t ambrycrc_update(uint32_t crc, const void* p, size_t n) {
   if (!p || n == 0) return crc;
@@ -546,6 +561,10 @@ uint32_t ambrycrc_zeros(uint32_t crc, uint64_t n) {
 
 int ambrycrc_init(int device) {
   if (device < 0 || device >= kMaxDevices) return AMBRYCRC_EINVAL;
+  if (AMBRY_IS_PROBE_BUILD) {  // a timing build: its CRCs are wrong by construction
+    const char* allow = getenv("AMBRYCRC_ALLOW_PROBE");
+    if (!allow || strcmp(allow, "1") != 0) return AMBRYCRC_EPROBE;
+  }
   std::lock_guard<std::mutex> g(g_mu);
   if (g_ctx[device]) return AMBRYCRC_OK;
   int count = 0;

@@ -59,9 +59,6 @@ struct DevCtx {
   // the loads; plus, for batches of >= kGroupMinChunks chunks, whole chunks <= 16 KiB in the
   // fused group phase, each size class spread over all waves with a class-sized group
   // (G = 2 / 8 / 16 lanes). Measured against the round-1 alternatives in DESIGN.md §4-5.
-#ifndef AMBRY_DEFAULT_VARIANT
-#define AMBRY_DEFAULT_VARIANT kVariantDefault
-#endif
   int variant = AMBRY_DEFAULT_VARIANT;  // (A/B builds: -DAMBRY_DEFAULT_VARIANT=...)
   // Message verify of regions of at most kRegionMaxPerMessage bytes per message: region mode
   // (region_runs_kernel + region_msg_kernel) instead of jobs through the batch engine.

@@ -184,6 +184,13 @@ size_t ambrycrc_transform_workspace_bytes(size_t m) {
          std::max(ambrycrc_messages_workspace_bytes(m), ambrycrc_serialize_puts_workspace_bytes(m));
 }
 
+uint64_t ambrycrc_transform_out_bound(uint64_t region_len, size_t m) {
+  static_assert(AMBRYCRC_TRANSFORM_GROWTH_MAX == (40 - 34) + kPropsAppendixMax + (13 - 10), "growth bound");
+  const uint64_t g = (uint64_t)AMBRYCRC_TRANSFORM_GROWTH_MAX;
+  if ((uint64_t)m > (UINT64_MAX - region_len) / g) return UINT64_MAX;
+  return region_len + (uint64_t)m * g;
+}
+
 int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off, size_t m,
                                     const int16_t* d_life_version, int header_version, uint8_t* d_out,
                                     uint64_t out_cap, uint64_t* d_out_off, uint64_t* d_out_len, uint32_t* d_status,

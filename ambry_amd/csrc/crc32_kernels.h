@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "../../include/ambrycrc.h"
+#include "build_knobs.h"
 
 namespace ambrycrc {
 
@@ -29,9 +30,6 @@ struct PlanArgs {
   const uint32_t* gate;    // run only when *gate != 0 (null: always): the transform's fallback pass
 };
 
-#ifndef AMBRY_PLAN_PER_BLOCK
-#define AMBRY_PLAN_PER_BLOCK 2048
-#endif
 // chunks per planning workgroup (a multiple of 256, <= 65535 so per-block class counts fit 16 bits)
 constexpr uint32_t kPlanPerBlock = AMBRY_PLAN_PER_BLOCK;
 static_assert(kPlanPerBlock % 256 == 0 && kPlanPerBlock <= 65535, "plan block size");
@@ -87,11 +85,12 @@ constexpr uint64_t kGroupSmallMax = 16384;
 //      v_cndmask_b32_dpp, one x^(8*4096) fold per 64 B), s_setprio 3 around the loads, plus
 //      the class-sized group phase (G = 4 / 8 / 16 lanes for <= 256 B / 1 KiB / 16 KiB) with
 //      the stored CRC read inline for message verify (SweepArgs::exp_fill).
-// 100..102: timing diagnostics that produce wrong CRCs, compiled only with
-// -DAMBRYCRC_DIAGNOSTICS (never in the product library).
-//   32 (kVariantSplit): the group phase as a kernel of its own (group_kernels.hip: 72.5 KiB LDS
-//      image, <= 64 VGPRs, two 1024-thread workgroups = 32 waves per CU), then variant 29's
-//      sweep kernel without its fused group phase.
+// A/B builds only (tools/ab_build.sh, -DAMBRY_AB_PROBE_BUILD; never in the product library):
+//   100..102: timing diagnostics that produce wrong CRCs (-DAMBRYCRC_DIAGNOSTICS).
+//   32 (kVariantSplit): the group phase as a kernel of its own (tools/probes/group_kernels.hip,
+//      -DAMBRY_AB_SPLIT_GROUP: 72.5 KiB LDS image, <= 64 VGPRs, two 1024-thread workgroups = 32
+//      waves per CU), then variant 29's sweep kernel without its fused group phase. It lost to 29
+//      at every size and occupancy (0.45-0.90x).
 constexpr int kVariantPieces = 0;
 constexpr int kVariantDefault = 29;
 constexpr int kVariantSplit = 32;
@@ -99,7 +98,10 @@ constexpr bool variant_supported(int v) {
 #ifdef AMBRYCRC_DIAGNOSTICS
   if (v >= 100 && v <= 102) return true;
 #endif
-  return v == kVariantPieces || v == kVariantDefault || v == kVariantSplit;
+#ifdef AMBRY_AB_SPLIT_GROUP
+  if (v == kVariantSplit) return true;
+#endif
+  return v == kVariantPieces || v == kVariantDefault;
 }
 // variants 29 and 32 read group-phase records' stored CRCs inline
 constexpr bool variant_groups(int v) { return v == kVariantDefault || v == kVariantSplit; }
@@ -288,10 +290,14 @@ hipError_t launch_region_msg(const MsgArgs& a, const RegionArgs& g, int num_cu, 
 hipError_t launch_msg_reduce(const MsgArgs& a, hipStream_t s);
 
 hipError_t launch_plan(const PlanArgs& a, hipStream_t s);
-hipError_t launch_sweep(const SweepArgs& a, int grid, int variant, hipStream_t s);
-hipError_t launch_sweep_copy(const SweepArgs& a, int grid, int variant, hipStream_t s);
-// The separate group kernel (group_kernels.hip) on num_cu CUs (it sizes its own grid).
+// grid: workgroups of the persistent sweep; num_cu: the device's CUs (the A/B split group kernel
+// sizes its own grid from it)
+hipError_t launch_sweep(const SweepArgs& a, int grid, int num_cu, int variant, hipStream_t s);
+hipError_t launch_sweep_copy(const SweepArgs& a, int grid, int num_cu, int variant, hipStream_t s);
+#ifdef AMBRY_AB_SPLIT_GROUP
+// The separate group kernel (tools/probes/group_kernels.hip) on num_cu CUs (it sizes its own grid).
 hipError_t launch_group(const SweepArgs& a, int num_cu, hipStream_t s);
+#endif
 hipError_t launch_verify(const uint32_t* crc, const uint32_t* expected, uint8_t* mismatch, uint32_t* count,
                          uint32_t n, hipStream_t s);
 hipError_t launch_readbw(const uint8_t* base, uint64_t nbytes, uint32_t* out, int grid, int variant,

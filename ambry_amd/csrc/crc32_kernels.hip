@@ -32,9 +32,6 @@
 #include "crc32_kernels.h"
 
 // A/B knob: s_setprio 3 around the streamed group path's loads, as the wave-mode body has it.
-#ifndef AMBRY_GRP_PRIO
-#define AMBRY_GRP_PRIO 0
-#endif
 
 namespace ambrycrc {
 
@@ -599,9 +596,6 @@ __device__ __forceinline__ uint64_t group_per(uint64_t ns, uint64_t nwaves) {
 // move through the class's list together. Default: class 2 (1-4 KiB) interleaved -- 4 KiB
 // records 1.10x, 3000 B 1.03x, 2000 B 1.02x, 4 KiB PUT serialization 1.03x; interleaving classes
 // 0 (100 B 0.96x) or 3 (4 KiB-blob message verify 0.94x) loses.
-#ifndef AMBRY_GRP_IL
-#define AMBRY_GRP_IL 4
-#endif
 struct GroupRange {
   uint64_t i0, i1, stride;
 };
@@ -1030,12 +1024,6 @@ __device__ __forceinline__ void group_class(const SweepArgs& a, uint64_t lo, uin
 // Class 0's group width and ring depth (A/B knobs for tools/ab_build.sh AB_FLAGS): 2-lane groups,
 // 8 blocks in flight, 32 chunks per round -- measured 1.57x faster than 4-lane groups on 100 B
 // records. Class 1 at G = 4 or 2 measured slower (1.1x, 1.75x).
-#ifndef AMBRY_C0_G
-#define AMBRY_C0_G 2
-#endif
-#ifndef AMBRY_C0_NB
-#define AMBRY_C0_NB 8
-#endif
 
 // class bounds from the plan: small_total = {total, start of class 1, 2, 3}
 __device__ __forceinline__ bool group_cls_has_work(const SweepArgs& a, uint32_t first_wave, uint64_t nwaves) {
@@ -1309,9 +1297,6 @@ __device__ __forceinline__ bool is_small(uint64_t len, uint64_t small_max) { ret
 // Size class of a small chunk (<= 256 B, 1 KiB, 4 KiB, more): the compacted list is
 // ordered by class, so a group-phase round (64/G consecutive entries) holds chunks of
 // similar length and its chain -- the longest chunk's block count -- wastes little.
-#ifndef AMBRY_C1_MAX  // A/B knob: the largest class-1 (8-lane group) chunk
-#define AMBRY_C1_MAX 1024
-#endif
 __device__ __forceinline__ uint32_t small_class(uint64_t len) {
   return len <= 256 ? 0u : len <= AMBRY_C1_MAX ? 1u : len <= 4096 ? 2u : 3u;
 }
@@ -1521,13 +1506,20 @@ hipError_t launch_plan(const PlanArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_sweep_copy(const SweepArgs& a, int grid, int variant, hipStream_t s) {
+hipError_t launch_sweep_copy(const SweepArgs& a, int grid, int num_cu, int variant, hipStream_t s) {
+#ifdef AMBRY_AB_SPLIT_GROUP
   if (variant == kVariantSplit) {
-    if (a.small_max && launch_group(a, grid, s) != hipSuccess) return hipGetLastError();
+    if (a.small_max) {
+      const hipError_t e = launch_group(a, num_cu, s);
+      if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL((crc32_sweep_kernel<true, false, 0, true>), dim3(grid), dim3(1024), 0, s, a);
-  } else {
-    hipLaunchKernelGGL((crc32_sweep_kernel<true, true, 0, true>), dim3(grid), dim3(1024), 0, s, a);
+    return hipGetLastError();
   }
+#endif
+  (void)variant;
+  (void)num_cu;
+  hipLaunchKernelGGL((crc32_sweep_kernel<true, true, 0, true>), dim3(grid), dim3(1024), 0, s, a);
   return hipGetLastError();
 }
 
@@ -1561,15 +1553,6 @@ __device__ __forceinline__ void region_sb_zero(const RegionArgs& a, uint64_t s, 
 // A/B knobs: AMBRY_RUNS_PROBE 1 = no run sums into LDS, 5 = no global stores,
 // 6 = every wave's stores to one 1 KiB line set (timing only, wrong sums); AMBRY_RUNS_STORE_NT 0 =
 // plain stores.
-#ifndef AMBRY_RUNS_STORE_NT
-#define AMBRY_RUNS_STORE_NT 0
-#endif
-#ifndef AMBRY_RUNS_GIL
-#define AMBRY_RUNS_GIL 1
-#endif
-#ifndef AMBRY_RUNS_PROBE
-#define AMBRY_RUNS_PROBE 0
-#endif
 __global__ __launch_bounds__(1024) void region_runs_kernel(RegionArgs a) {
   const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
   // Shares wave-major over workgroups, as the sweep kernel's (CU-major shares measured the same).
@@ -1653,17 +1636,23 @@ hipError_t launch_region_runs(const RegionArgs& a, int grid, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_sweep(const SweepArgs& a, int grid, int variant, hipStream_t s) {
+hipError_t launch_sweep(const SweepArgs& a, int grid, int num_cu, int variant, hipStream_t s) {
+  (void)num_cu;
   switch (variant) {
     // 0: 16-B pieces, every chunk in the sweep (no group phase): the fallback shape
     case kVariantPieces: hipLaunchKernelGGL((crc32_sweep_kernel<false, false>), dim3(grid), dim3(1024), 0, s, a); break;
     // 29 (default): 64-B lane runs + the class-sized group phase for whole chunks <= 16 KiB
     case kVariantDefault: hipLaunchKernelGGL((crc32_sweep_kernel<true, true>), dim3(grid), dim3(1024), 0, s, a); break;
     // 32: the group kernel (two workgroups per CU), then the sweep without its group phase
+#ifdef AMBRY_AB_SPLIT_GROUP
     case kVariantSplit:
-      if (a.small_max && launch_group(a, grid, s) != hipSuccess) return hipGetLastError();
+      if (a.small_max) {
+        const hipError_t e = launch_group(a, num_cu, s);
+        if (e != hipSuccess) return e;
+      }
       hipLaunchKernelGGL((crc32_sweep_kernel<true, false>), dim3(grid), dim3(1024), 0, s, a);
       break;
+#endif
 #ifdef AMBRYCRC_DIAGNOSTICS
     // timing-only diagnostics (wrong CRCs; debug builds only): 100 FOLD lookups removed, 101 no
     // per-segment atomic, 102 no wave tree

@@ -142,9 +142,6 @@ __device__ __forceinline__ void transform_describe(const TransformArgs& a, uint6
 // The first bytes of a record staged in this thread's LDS slot, the rest read from global memory:
 // the properties parse walks int-length strings, one dependent read per field, which from LDS
 // costs an LDS round trip instead of a memory one.
-#ifndef AMBRY_PROPS_WIN
-#define AMBRY_PROPS_WIN 96
-#endif
 constexpr uint32_t kPropsWin = AMBRY_PROPS_WIN;        // bytes staged per thread (a multiple of 16)
 constexpr uint32_t kPropsSlotWords = kPropsWin / 4 + 1;  // +1 word: consecutive slots start on consecutive banks
 struct WinBytes {
@@ -306,9 +303,6 @@ __device__ __forceinline__ void parse_message(uint64_t off, bool in_region, uint
 // thread per message); fewer messages in flight keep a thread's lines in L2 between its dependent
 // reads (as region_msg_kernel's grid cap). A/B, the transform's fused parse over 262,144 4 KiB-blob
 // messages: one thread per message 99.1 us, 2 blocks per CU 95.8, 4 blocks 99.0.
-#ifndef AMBRY_PARSE_BPC
-#define AMBRY_PARSE_BPC 2
-#endif
 template <bool DESC>
 __global__ __launch_bounds__(256) void msg_parse_kernel(MsgArgs a, TransformArgs t) {
   __shared__ uint32_t tbl[1024];
@@ -359,12 +353,6 @@ static uint32_t parse_blocks(uint64_t m) {
 // thread's header / record-head lines in L2 until its own end-run reads (A/B, 4 KiB-blob messages:
 // one thread per message at 16 waves per CU 120.1 us; 2 blocks per CU 104.9, with WPE 2 102.7; 3
 // blocks 109.5; 1 block 135.4). 0 = one thread per message.
-#ifndef AMBRY_REGION_WPE
-#define AMBRY_REGION_WPE 2
-#endif
-#ifndef AMBRY_REGION_BPC
-#define AMBRY_REGION_BPC 2
-#endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AMBRY_REGION_WPE))) void region_msg_kernel(
     MsgArgs a, RegionArgs g) {
   __shared__ uint32_t tbl[1024];

@@ -29,9 +29,6 @@
 
 // A/B probe builds (tools/ab_build.sh AB_FLAGS=-DAMBRY_REGION_PROBE=n; timing only, wrong CRCs):
 // 1 = records not CRC'd (parse alone), 2 = no run-sum loads, 3 = no head / tail loads.
-#ifndef AMBRY_REGION_PROBE
-#define AMBRY_REGION_PROBE 0
-#endif
 #include <stdint.h>
 
 #include "crc32_kernels.h"

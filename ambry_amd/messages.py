@@ -135,7 +135,8 @@ def verify_message_cpu(region, off: int):
 def transform_message_cpu(region, off: int, header_version: int = 3, life=None, out_cap=None):
     """ambrycrc_transform_message_cpu: (status bits, the re-serialized message or None)."""
     buf = np.frombuffer(region, dtype=np.uint8) if not isinstance(region, np.ndarray) else region
-    cap = out_cap if out_cap is not None else buf.size + 64  # a transform grows a message by <= 9 B
+    # default: the ABI's bound (the stored bytes after off + TRANSFORM_GROWTH_MAX), never NO_ROOM
+    cap = out_cap if out_cap is not None else out_bound(buf.size - min(off, buf.size), 1)
     out = np.zeros(max(cap, 1), dtype=np.uint8)
     st, n = ctypes.c_uint32(0), ctypes.c_uint64(0)
     check(lib().ambrycrc_transform_message_cpu(buf.ctypes.data_as(ctypes.c_void_p), buf.size, off,
@@ -149,13 +150,25 @@ def transform_message_cpu(region, off: int, header_version: int = 3, life=None, 
 MSG_NOT_PUT = 1 << 10
 MSG_BAD_RECORD = 1 << 11
 MSG_NO_ROOM = 1 << 12
+MSG_NOT_ENCODABLE = 1 << 13
+
+# A transformed message is at most this many bytes longer than the stored one: header V1 -> V3 (+6),
+# BlobProperties SerDe V1 -> V5 (+17), Blob_Format_V1 -> V3 head (+3) (AMBRYCRC_TRANSFORM_GROWTH_MAX).
+TRANSFORM_GROWTH_MAX = 26
+
+
+def out_bound(region_len: int, m: int) -> int:
+    """ambrycrc_transform_out_bound: an output capacity that never yields MSG_NO_ROOM for m
+    messages that share no bytes of a region_len-byte region."""
+    return int(lib().ambrycrc_transform_out_bound(region_len, m))
 
 
 def transform_dev(region, msg_off, header_version: int = 3, life_version=None, out=None, stream=None):
     """ambrycrc_transform_messages_dev -- ValidatingTransformer.transform for a batch of stored
     messages in HBM: every clean PUT re-serialized at `header_version` (and life version
     life_version[i], an int16 CUDA tensor, or the stored one), packed in order into `out` (a uint8
-    CUDA tensor; default: region bytes + 6 per message, enough for any header change).
+    CUDA tensor; default: out_bound(region bytes, m), enough for every message of a region whose
+    messages do not overlap -- TRANSFORM_GROWTH_MAX = 26 B of growth per message).
     Returns (out, out_off int64[m], out_len int64[m], status int32[m])."""
     import torch
 
@@ -171,7 +184,7 @@ def transform_dev(region, msg_off, header_version: int = 3, life_version=None, o
                                      or not life_version.is_cuda or not life_version.is_contiguous()):
         raise TypeError("life_version must be a contiguous int16 CUDA tensor of m elements")
     if out is None:
-        out = torch.empty(region.numel() + 6 * m, dtype=torch.uint8, device=region.device)
+        out = torch.empty(out_bound(region.numel(), m), dtype=torch.uint8, device=region.device)
     elif out.dtype != torch.uint8 or not out.is_cuda or not out.is_contiguous() or out.device != region.device:
         raise TypeError("out must be a contiguous uint8 CUDA tensor on the region's device")
     out_off = torch.empty(m, dtype=torch.int64, device=region.device)

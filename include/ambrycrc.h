@@ -46,6 +46,8 @@ extern "C" {
 #define AMBRYCRC_ENOINIT (-4)  /* ambrycrc_init() not called for the current device */
 #define AMBRYCRC_ENODEV (-5)   /* no usable gfx950 device */
 #define AMBRYCRC_ECOMM (-6)    /* RCCL unavailable, or a collective / communicator call failed */
+#define AMBRYCRC_EPROBE (-7)   /* ambrycrc_init: this library is an A/B timing build (wrong CRCs) and
+                                  AMBRYCRC_ALLOW_PROBE=1 is not set */
 
 /* ---------------------------------------------------------------- lifecycle */
 
@@ -60,7 +62,9 @@ int ambrycrc_shutdown(void);
 /* Static, human-readable description of an error code. */
 const char* ambrycrc_strerror(int code);
 
-/* Library version string ("ambrycrc <semver> gfx950"). */
+/* Library version string: "ambrycrc <semver> gfx950", followed by " ab-probe-build" and
+ * " AMBRY_<KNOB>=<value>" for every compile-time A/B knob that differs from the product default
+ * (ambry_amd/csrc/build_knobs.h). The product build reports neither. */
 const char* ambrycrc_version(void);
 
 /* ------------------------------------------------- host streaming primitives */
@@ -262,6 +266,22 @@ int ambrycrc_serialize_puts_dev(const ambrycrc_put_desc* d_desc, size_t m, const
  * region. Asynchronous on `stream`; d_ws >= ambrycrc_transform_workspace_bytes(m) or NULL. The
  * store-key comparison with the index entry stays with the caller (it owns the StoreKey type). */
 size_t ambrycrc_transform_workspace_bytes(size_t m);
+
+/* Output size contract of the transform. A transformed message is at most
+ * AMBRYCRC_TRANSFORM_GROWTH_MAX bytes longer than the stored message it comes from:
+ *   header V1 (34 B) -> V3 (40 B)                                   +6
+ *   BlobProperties SerDe V1 -> VERSION_5 (account, container, encrypted, three null strings) +17
+ *   Blob_Format_V1 head (10 B) -> Blob_Format_V3 head (13 B)          +3
+ * (every other record keeps its size; a V1 output header drops the encryption-key record). The
+ * reference sizes its buffer from the same fields: PutMessageFormatInputStream.java:88-90,122 and
+ * BlobPropertiesSerDe.java:43-54, MessageInfo size at ValidatingTransformer.java:91.
+ * ambrycrc_transform_out_bound(region_len, m) = region_len + m * AMBRYCRC_TRANSFORM_GROWTH_MAX
+ * (saturating): an out_cap that never yields AMBRYCRC_MSG_NO_ROOM when no two messages share region
+ * bytes (a log region, a GetResponse) -- the cap for ambrycrc_transform_messages_dev/_host and, with
+ * m = 1 and the stored message's length, for ambrycrc_transform_message_cpu. */
+#define AMBRYCRC_TRANSFORM_GROWTH_MAX 26
+uint64_t ambrycrc_transform_out_bound(uint64_t region_len, size_t m);
+
 int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off, size_t m,
                                     const int16_t* d_life_version, int header_version, uint8_t* d_out,
                                     uint64_t out_cap, uint64_t* d_out_off, uint64_t* d_out_len, uint32_t* d_status,

@@ -28,8 +28,58 @@ def test_exports_every_declared_symbol(ambry):
 def test_version_and_errors(ambry):
     lib = ambry.lib()
     assert lib.ambrycrc_version().decode().startswith("ambrycrc")
-    for code in (0, -1, -2, -3, -4, -5, -6):
+    for code in (0, -1, -2, -3, -4, -5, -6, -7):
         assert lib.ambrycrc_strerror(code)
+
+
+def test_product_build_has_no_knob_overrides(ambry):
+    """The in-tree library is the product build: no A/B knob differs from build_knobs.h's defaults,
+    it is not a probe build, and the split group kernel (variant 32) is not linked into it."""
+    import subprocess
+
+    v = ambry.lib().ambrycrc_version().decode()
+    assert v == "ambrycrc 0.4.0 gfx950", v
+    syms = subprocess.run(["nm", "-D", "--defined-only", ambry.LIB_PATH], capture_output=True, text=True).stdout
+    assert "launch_group" not in syms and "crc32_group_kernel" not in syms
+
+
+@pytest.mark.parametrize("flag", ["-DAMBRY_REGION_PROBE=1", "-DAMBRY_RUNS_PROBE=5", "-DAMBRYCRC_DIAGNOSTICS",
+                                  "-DAMBRY_AB_SPLIT_GROUP"])
+def test_probe_knobs_need_probe_build(flag):
+    """A wrong-CRC probe knob does not compile without -DAMBRY_AB_PROBE_BUILD (tools/ab_build.sh)."""
+    import subprocess
+
+    hdr = os.path.join(ROOT, "ambry_amd", "csrc", "build_knobs.h")
+    bad = subprocess.run(["cpp", flag, hdr], capture_output=True, text=True)
+    assert bad.returncode != 0 and "AMBRY_AB_PROBE_BUILD" in bad.stderr
+    ok = subprocess.run(["cpp", flag, "-DAMBRY_AB_PROBE_BUILD", hdr], capture_output=True, text=True)
+    assert ok.returncode == 0, ok.stderr
+
+
+def test_probe_build_refused_and_reported(tmp_path):
+    """A probe build names itself in ambrycrc_version() and its overridden knobs, and ambrycrc_init
+    refuses it (AMBRYCRC_EPROBE, before any device call) unless AMBRYCRC_ALLOW_PROBE=1."""
+    import glob
+    import subprocess
+    import sys
+
+    d = os.path.join(ROOT, "ambry_amd")
+    objs = [o for o in glob.glob(os.path.join(d, "build", "obj", "*.o")) if not o.endswith("ambrycrc.cpp.o")]
+    if len(objs) < 6 or not os.path.exists(os.path.join(d, "host_crc.o")):
+        pytest.skip("in-tree objects not built (make -C ambry_amd)")
+    so = str(tmp_path / "libprobe.so")
+    cc = ["/opt/rocm/bin/hipcc", "-O1", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-DAMBRY_AB_PROBE_BUILD",
+          "-DAMBRY_REGION_PROBE=2", "-c", "-o", str(tmp_path / "a.o"), os.path.join(d, "csrc", "ambrycrc.cpp")]
+    subprocess.run(cc, check=True, capture_output=True, timeout=600)
+    subprocess.run(["/opt/rocm/bin/hipcc", "-shared", "--offload-arch=gfx950", "-o", so, str(tmp_path / "a.o"),
+                    os.path.join(d, "host_crc.o")] + objs + ["-ldl"], check=True, capture_output=True, timeout=600)
+    code = ("import ctypes; l = ctypes.CDLL(%r); l.ambrycrc_version.restype = ctypes.c_char_p; "
+            "print(l.ambrycrc_version().decode()); print(l.ambrycrc_init(0))" % so)
+    env = {k: v for k, v in os.environ.items() if k != "AMBRYCRC_ALLOW_PROBE"}
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=120)
+    version, rc = r.stdout.split("\n")[:2]
+    assert "ab-probe-build" in version and "AMBRY_REGION_PROBE=2" in version
+    assert int(rc) == -7
 
 
 def test_host_update_golden(ambry, vectors):
@@ -235,7 +285,7 @@ def test_chain_messages_host_under_asan(tmp_path):
                     "-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
                     "-Xarch_host", "-fno-sanitize-recover=all", str(host_o),
                     os.path.join(ROOT, "tests", "native", "chain_asan.cpp"), os.path.join(csrc, "ambrycrc.cpp"),
-                    os.path.join(csrc, "ambrycrc_multi.cpp"), os.path.join(csrc, "crc32_kernels.hip"), os.path.join(csrc, "group_kernels.hip"),
+                    os.path.join(csrc, "ambrycrc_multi.cpp"), os.path.join(csrc, "crc32_kernels.hip"),
                     os.path.join(csrc, "message_kernels.hip"), "-ldl", "-o", str(exe)], check=True, timeout=900)
     r = subprocess.run([str(exe), str(rf)], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
@@ -276,7 +326,7 @@ def test_message_cpu_under_asan(ambry, tmp_path):
                     "-Xarch_host", "-fno-sanitize-recover=all", str(host_o),
                     os.path.join(ROOT, "tests", "native", "msg_cpu_asan.cpp"), os.path.join(csrc, "ambrycrc.cpp"),
                     os.path.join(csrc, "ambrycrc_multi.cpp"), os.path.join(csrc, "ambrycrc_put.cpp"),
-                    os.path.join(csrc, "ambrycrc_msg_cpu.cpp"), os.path.join(csrc, "crc32_kernels.hip"), os.path.join(csrc, "group_kernels.hip"),
+                    os.path.join(csrc, "ambrycrc_msg_cpu.cpp"), os.path.join(csrc, "crc32_kernels.hip"),
                     os.path.join(csrc, "message_kernels.hip"), os.path.join(csrc, "put_kernels.hip"), "-ldl",
                     "-o", str(exe)], check=True, timeout=900)
     for f in (rf, rf2, rf3):

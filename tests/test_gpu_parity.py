@@ -110,7 +110,7 @@ def test_ragged_batch_grid_sizes(gpu, oracle, grid):
     assert np.array_equal(got, oracle.batch(mem, off, ln, threads=8))
 
 
-VARIANTS = (0, 29, 32)  # built into the library: the 16-B-piece fallback, the default, the split group kernel
+VARIANTS = (0, 29)  # built into the library: the 16-B-piece fallback and the default (32: A/B builds only)
 
 
 @pytest.mark.parametrize("variant", VARIANTS)
@@ -745,17 +745,18 @@ def test_many_short_lived_streams_default_workspace(gpu, oracle):
 
 
 def test_diagnostic_variants_not_selectable(gpu):
-    """Variants 100-102 (timing builds that return wrong CRCs) are not in the product library."""
+    """Variants 100-102 (timing builds that return wrong CRCs) and 32 (the split group kernel, which
+    lost everywhere) are not in the product library."""
     from ambry_amd._lib import AmbryCrcError
 
     before = gpu.get_variant(0)
-    for v in (1, 22, 28, 30, 31, 33, 100, 101, 102, -1):
+    for v in (1, 22, 28, 30, 31, 32, 33, 100, 101, 102, -1):
         with pytest.raises(AmbryCrcError):
             gpu.set_variant(0, v)
     assert gpu.get_variant(0) == before
 
 
-@pytest.mark.parametrize("value,expect", [("0", 0), ("29", 29), ("32", 32), ("101", 29), ("abc", 29), ("29x", 29),
+@pytest.mark.parametrize("value,expect", [("0", 0), ("29", 29), ("32", 29), ("101", 29), ("abc", 29), ("29x", 29),
                                           ("-5", 29)])
 def test_variant_environment_validated(value, expect):
     """AMBRYCRC_VARIANT selects only a built-in shape; anything else is ignored."""

@@ -74,6 +74,52 @@ def build_region(mf, n, seed, corrupt=True):
     return bytes(region), offs
 
 
+def dense_old_region(mf, n, seed):
+    """A dense, gap-free region of clean messages as old servers stored them -- header V1 (some
+    V2), BlobProperties at SerDe V1 (some V2 / V3), Blob_Format_V1 -- so a transform to header V3
+    grows nearly every message by the full 26 B (+6 header, +17 props, +3 blob head): an old
+    replica being re-replicated (PutMessageFormatInputStream.java:88-90,122)."""
+    rng = np.random.default_rng(seed)
+    msgs = []
+    for i in range(n):
+        blen = int(rng.choice([0, 1, 100, 4096]))
+        content = stream_bytes(seed + i, 0, blen).tobytes()
+        um = stream_bytes(seed + i, 1 << 20, int(rng.choice([0, 5, 300]))).tobytes()
+        sv = int(rng.choice([1, 2, 3], p=[0.7, 0.15, 0.15]))
+        props = mf.blob_properties_bytes(blen, service_id="s%d" % (i % 7), owner_id="o%d" % (i % 3),
+                                         private=bool(i % 2), serde_version=sv)
+        hv = 1 if rng.random() < 0.8 else 2
+        msgs.append(_blob_v1_message(mf, mf.store_key("old-%d" % i), props, um, content, hv))
+    offs = np.cumsum([0] + [len(x) for x in msgs[:-1]]).tolist()
+    return b"".join(msgs), offs
+
+
+def test_transform_dense_old_region_default_out(gpu, mf):
+    """The default `out` (ambrycrc_transform_out_bound) holds every message of a dense region of
+    old messages grown by up to 26 B each: no MSG_NO_ROOM, every status 0, byte-exact output."""
+    import torch
+
+    from ambry_amd.messages import TRANSFORM_GROWTH_MAX, out_bound, transform_dev
+
+    region, offs = dense_old_region(mf, 700, seed=5)
+    assert out_bound(len(region), len(offs)) == len(region) + TRANSFORM_GROWTH_MAX * len(offs)
+    dev = torch.frombuffer(bytearray(region), dtype=torch.uint8).cuda()
+    out, out_off, out_len, status = transform_dev(dev, torch.tensor(offs, dtype=torch.int64, device="cuda"))
+    torch.cuda.synchronize()
+    st, oo, ol = status.cpu().numpy().view(np.uint32), out_off.cpu().numpy(), out_len.cpu().numpy()
+    out_h = out.cpu().numpy().tobytes()
+    assert st.tolist() == [0] * len(offs)
+    pos, grown = 0, 0
+    for i, o in enumerate(offs):
+        exp_st, exp = mf.transform_message(region, o, version=3)
+        assert exp_st == 0
+        assert oo[i] == pos and ol[i] == len(exp), i
+        assert out_h[pos:pos + len(exp)] == exp, i
+        pos += len(exp)
+        grown += len(exp) - ((offs[i + 1] if i + 1 < len(offs) else len(region)) - o)
+    assert grown > 20 * len(offs)  # the region really grows by ~26 B per message
+
+
 @pytest.mark.parametrize("version", [3, 2, 1])
 def test_transform_matches_oracle(gpu, mf, version):
     import torch

@@ -84,3 +84,25 @@ def test_verdict_probes_props(ambry):
                           um, content)
     assert out == want and MF.transform_message(msg, 0) == (0, want)
     assert verify_message_cpu(out, 0) == (0, len(out))
+
+
+def test_transform_dense_old_region_bound(ambry):
+    """Each old message (header V1/V2, SerDe V1-V3 properties, Blob_Format_V1) fits the ABI's
+    bound for its own length (ambrycrc_transform_out_bound(len, 1)); the bound is tight for the
+    worst case (V1 header + V1 props + blob V1 -> V3: exactly +26 B)."""
+    from test_gpu_transform import dense_old_region
+
+    from ambry_amd.messages import TRANSFORM_GROWTH_MAX, out_bound, transform_message_cpu
+
+    region, offs = dense_old_region(MF, 200, seed=5)
+    ends = offs[1:] + [len(region)]
+    worst = 0
+    for o, e in zip(offs, ends):
+        exp_st, exp = MF.transform_message(region, o, version=3)
+        assert exp_st == 0
+        msg = region[o:e]
+        assert transform_message_cpu(msg, 0, out_cap=out_bound(len(msg), 1)) == (0, exp)
+        assert transform_message_cpu(region, o) == (0, exp)  # the default cap
+        worst = max(worst, len(exp) - len(msg))
+    assert worst == TRANSFORM_GROWTH_MAX
+    assert out_bound(2**64 - 10, 1) == 2**64 - 1  # saturates

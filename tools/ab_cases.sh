@@ -3,6 +3,7 @@
 # rocprofv3 kernel trace, once per library build in $LIBS (paths to libambrycrc.so builds, loaded
 # through AMBRYCRC_LIBRARY), interleaved A B A B ... $ROUNDS times so box-to-box and drift
 # variance cancels. Then `python tools/ab_summary.py`.
+export AMBRYCRC_ALLOW_PROBE=1  # the A/B libraries are probe builds (tools/ab_build.sh)
 set -euo pipefail
 export TMPDIR=/tmp
 CASES=${CASES:-"batch100 batch1k batch4k batch4109 msg4k"}

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-mapping A/B (AMBRY_GRP_IL class bitmask): GPU parity of the builds in $BUILDS, then the
 # interleaved kernel-time A/B (tools/ab_cases.sh) of base and them.
+export AMBRYCRC_ALLOW_PROBE=1  # the A/B libraries are probe builds (tools/ab_build.sh)
 set -euo pipefail
 BUILDS=${BUILDS:-"il12 il4 il8 il15"}
 for b in $BUILDS; do

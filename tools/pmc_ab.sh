@@ -2,6 +2,7 @@
 # SQ counters of library builds side by side (A/B of kernel shapes): for each lib in $LIBS and
 # case in $CASES (tools/probes/pmc_case.py), two rocprofv3 --pmc passes of <= 8 SQ counters each
 # (no trace domain with --pmc), every pass its own run. Then `python tools/pmc_ab_summary.py`.
+export AMBRYCRC_ALLOW_PROBE=1  # the A/B libraries are probe builds (tools/ab_build.sh)
 set -euo pipefail
 export TMPDIR=/tmp
 CASES=${CASES:-"batch4k"}

@@ -2,6 +2,7 @@
 # Vector-memory front-end counters (TA / TD / TCP / TCC) of library builds side by side, for the
 # small-record cases: is a CU's L1 path (addresses and cache lines per wave load) what bounds a
 # group-phase round? One rocprofv3 --pmc pass per block limit (TA 2, TD 2, TCP 4, TCC 4).
+export AMBRYCRC_ALLOW_PROBE=1  # the A/B libraries are probe builds (tools/ab_build.sh)
 set -euo pipefail
 export TMPDIR=/tmp
 CASES=${CASES:-"batch100 batch4k"}

@@ -21,6 +21,9 @@
 //              lane states merge by a log2(G)-level nibble tree, the < 16 trailing bytes go
 //              16/G per lane, xor-out; the group leader stores out[chunk] (and exp_fill / the
 //              copy-through bytes as the fused phase does).
+#ifndef AMBRY_AB_SPLIT_GROUP
+#error "A/B only: tools/ab_build.sh builds it with -DAMBRY_AB_SPLIT_GROUP -DAMBRY_AB_PROBE_BUILD"
+#endif
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
