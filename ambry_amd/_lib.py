@@ -83,6 +83,10 @@ _SIGNATURES = [
     ("ambrycrc_transform_messages_dev", ctypes.c_int,
      [_u8p, ctypes.c_uint64, _u8p, ctypes.c_size_t, _u8p, ctypes.c_int, _u8p, ctypes.c_uint64, _u8p, _u8p, _u8p,
       ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    ("ambrycrc_transform_messages_host", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int,
+      ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+      ctypes.POINTER(ctypes.c_uint32), ctypes.c_int, ctypes.c_int]),
     ("ambrycrc_trailed_workspace_bytes", ctypes.c_size_t, [ctypes.c_size_t]),
     ("ambrycrc_verify_trailed_dev", ctypes.c_int,
      [_u8p, _u8p, _u8p, _u8p, _u8p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),

@@ -446,6 +446,16 @@ void free_ctx(DevCtx* c) {
     if (ms.d_end) (void)hipFree(ms.d_end);
     if (ms.d_ws) (void)hipFree(ms.d_ws);
   }
+  for (auto& x : c->xform_slab) {
+    if (x.h_life) (void)hipHostFree(x.h_life);
+    if (x.h_out) (void)hipHostFree(x.h_out);
+    if (x.h_olen) (void)hipHostFree(x.h_olen);
+    if (x.d_life) (void)hipFree(x.d_life);
+    if (x.d_out) (void)hipFree(x.d_out);
+    if (x.d_olen) (void)hipFree(x.d_olen);
+    if (x.d_ooff) (void)hipFree(x.d_ooff);
+    if (x.d_ws) (void)hipFree(x.d_ws);
+  }
   for (auto& s : c->slab) {  // whatever setup_slabs got to, even if it failed part way
     if (s.h_data) (void)hipHostFree(s.h_data);
     if (s.h_meta) (void)hipHostFree(s.h_meta);
@@ -1041,6 +1051,43 @@ uint32_t rd_be32(const uint8_t* p) {
 }
 uint64_t rd_be64(const uint8_t* p) { return ((uint64_t)rd_be32(p) << 32) | rd_be32(p + 4); }
 
+// member by member, skipping what an earlier (failed) attempt already allocated
+template <class T>
+bool host_alloc(T** p, size_t bytes) {
+  return *p || hipHostMalloc(reinterpret_cast<void**>(p), bytes, hipHostMallocDefault) == hipSuccess;
+}
+template <class T>
+bool dev_alloc(T** p, size_t bytes) {
+  return *p || hipMalloc(reinterpret_cast<void**>(p), bytes) == hipSuccess;
+}
+
+// The message-verify members of the host slabs (caller holds c->mu, c's device current).
+int setup_msg_slabs(DevCtx* c) {
+  if (c->msg_slabs_ready) return AMBRYCRC_OK;
+  for (MsgSlab& ms : c->msg_slab)
+    if (!host_alloc(&ms.h_off, kSlabMsgs * sizeof(uint64_t)) || !host_alloc(&ms.h_status, kSlabMsgs * sizeof(uint32_t)) ||
+        !host_alloc(&ms.h_end, kSlabMsgs * sizeof(uint64_t)) || !dev_alloc(&ms.d_off, kSlabMsgs * sizeof(uint64_t)) ||
+        !dev_alloc(&ms.d_status, kSlabMsgs * sizeof(uint32_t)) || !dev_alloc(&ms.d_end, kSlabMsgs * sizeof(uint64_t)) ||
+        !(ms.d_ws || hipMalloc(&ms.d_ws, ambrycrc_messages_workspace_bytes(kSlabMsgs)) == hipSuccess))
+      return AMBRYCRC_ENOMEM;
+  c->msg_slabs_ready = true;
+  return AMBRYCRC_OK;
+}
+
+// The transform members (ambrycrc_transform_messages_host), on top of setup_msg_slabs.
+int setup_xform_slabs(DevCtx* c) {
+  if (c->xform_slabs_ready) return AMBRYCRC_OK;
+  for (XformSlab& x : c->xform_slab)
+    if (!host_alloc(&x.h_life, kSlabMsgs * sizeof(int16_t)) || !dev_alloc(&x.d_life, kSlabMsgs * sizeof(int16_t)) ||
+        !host_alloc(&x.h_out, kXformOutBytes) || !dev_alloc(&x.d_out, kXformOutBytes) ||
+        !host_alloc(&x.h_olen, kSlabMsgs * sizeof(uint64_t)) || !dev_alloc(&x.d_olen, kSlabMsgs * sizeof(uint64_t)) ||
+        !dev_alloc(&x.d_ooff, kSlabMsgs * sizeof(uint64_t)) ||
+        !(x.d_ws || hipMalloc(&x.d_ws, ambrycrc_transform_workspace_bytes(kSlabMsgs)) == hipSuccess))
+      return AMBRYCRC_ENOMEM;
+  c->xform_slabs_ready = true;
+  return AMBRYCRC_OK;
+}
+
 // Bytes from a message's start that the device pipeline may read: the 40-B header window,
 // and, when the header's sizes fit the region, the whole message [0, first record + total).
 // Every early exit of msg_parse_kernel reads the header alone, so a staging copy of this
@@ -1108,26 +1155,10 @@ int ambrycrc_verify_messages_host(const uint8_t* region, uint64_t region_len, co
   (void)hipGetDevice(&prev);
   if (hipSetDevice(device) != hipSuccess) return AMBRYCRC_EHIP;
   int rc = setup_slabs(c);
-  if (rc) return rc;
-  if (!c->msg_slabs_ready) {
-    for (int w = 0; w < kSlabs; ++w) {
-      MsgSlab& ms = c->msg_slab[w];
-      // member by member, skipping what an earlier (failed) attempt already allocated
-      auto hhost = [](auto** p, size_t bytes) {
-        return *p || hipHostMalloc(reinterpret_cast<void**>(p), bytes, hipHostMallocDefault) == hipSuccess;
-      };
-      auto hdev = [](auto** p, size_t bytes) {
-        return *p || hipMalloc(reinterpret_cast<void**>(p), bytes) == hipSuccess;
-      };
-      if (!hhost(&ms.h_off, kSlabMsgs * sizeof(uint64_t)) || !hhost(&ms.h_status, kSlabMsgs * sizeof(uint32_t)) ||
-          !hhost(&ms.h_end, kSlabMsgs * sizeof(uint64_t)) || !hdev(&ms.d_off, kSlabMsgs * sizeof(uint64_t)) ||
-          !hdev(&ms.d_status, kSlabMsgs * sizeof(uint32_t)) || !hdev(&ms.d_end, kSlabMsgs * sizeof(uint64_t)) ||
-          !(ms.d_ws || hipMalloc(&ms.d_ws, ambrycrc_messages_workspace_bytes(kSlabMsgs)) == hipSuccess)) {
-        (void)hipSetDevice(prev);
-        return AMBRYCRC_ENOMEM;
-      }
-    }
-    c->msg_slabs_ready = true;
+  if (!rc) rc = setup_msg_slabs(c);
+  if (rc) {
+    (void)hipSetDevice(prev);
+    return rc;
   }
 
   // Messages in offset order; each slab stages one contiguous span [lo, hi) of the region
@@ -1261,6 +1292,200 @@ int ambrycrc_verify_messages_host(const uint8_t* region, uint64_t region_len, co
   for (int d = 0; d < kSlabs; ++d) {
     const int r = drain((k + d) % kSlabs);
     if (!rc2) rc2 = r;
+  }
+  (void)hipSetDevice(prev);
+  return rc ? rc : rc2;
+}
+
+int ambrycrc_transform_messages_host(const uint8_t* region, uint64_t region_len, const uint64_t* msg_off, size_t m,
+                                     const int16_t* life_version, int header_version, uint8_t* out, uint64_t out_cap,
+                                     uint64_t* out_off, uint64_t* out_len, uint32_t* status, int device, int pinned) {
+  if (m == 0) return AMBRYCRC_OK;
+  if (!msg_off || !out_len || !status || (!region && region_len) || (!out && out_cap) || header_version < 1 ||
+      header_version > 3)
+    return AMBRYCRC_EINVAL;
+  DevCtx* c = ctx_for(device);
+  if (!c) return AMBRYCRC_ENOINIT;
+  std::lock_guard<std::mutex> g(c->mu);
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  if (hipSetDevice(device) != hipSuccess) return AMBRYCRC_EHIP;
+  int rc = setup_slabs(c);
+  if (!rc) rc = setup_msg_slabs(c);
+  if (!rc) rc = setup_xform_slabs(c);
+  if (rc) {
+    (void)hipSetDevice(prev);
+    return rc;
+  }
+  // Extents as the verify's (message_extent: a transform reads nothing outside them either).
+  std::vector<uint64_t> ext(m);
+  {
+    CopyPool& pool = CopyPool::get();
+    const int parts = (int)std::min<size_t>((size_t)pool.threads(), std::max<size_t>(1, m / 4096));
+    pool.run(parts, [&](int p) {
+      for (size_t i = m * (size_t)p / (size_t)parts; i < m * (size_t)(p + 1) / (size_t)parts; ++i)
+        ext[i] = msg_off[i] > region_len ? 0 : message_extent(region + msg_off[i], region_len - msg_off[i]);
+    });
+  }
+  // Packing follows ambrycrc_transform_messages_dev over the whole batch: message i's bytes go at
+  // the sum of the transformed lengths of the messages before it, or it gets AMBRYCRC_MSG_NO_ROOM
+  // when they would pass out_cap (that sum still grows by its length, as the device's exclusive
+  // scan of the lengths does). Slabs hold runs of consecutive messages in index order, each run's
+  // span [lo, hi) staged once; the slab's transform packs its messages from 0 in the same order.
+  uint64_t vpos = 0;  // the device scan's running start
+  auto place = [&](size_t i, uint32_t st, uint64_t len, const uint8_t* bytes, std::vector<CopyJob>* jobs) {
+    if (st == 0 && len) {
+      if (vpos + len <= out_cap) {
+        if (out_off) out_off[i] = vpos;
+        out_len[i] = len;
+        status[i] = 0;
+        if (jobs) jobs->push_back({out + vpos, bytes, len});
+        else memcpy(out + vpos, bytes, len);
+      } else {
+        if (out_off) out_off[i] = ~0ull;
+        out_len[i] = 0;
+        status[i] = AMBRYCRC_MSG_NO_ROOM;
+      }
+      vpos += len;
+      return;
+    }
+    if (out_off) out_off[i] = ~0ull;
+    out_len[i] = 0;
+    status[i] = st;
+  };
+  struct Run {
+    size_t i0 = 0, n = 0;
+  };
+  Run inflight[kSlabs];
+  std::vector<CopyJob> jobs;
+  auto drain = [&](int which) -> int {
+    Run& r = inflight[which];
+    if (!r.n) return AMBRYCRC_OK;
+    if (hipEventSynchronize(c->slab[which].done) != hipSuccess) return AMBRYCRC_EHIP;
+    const MsgSlab& ms = c->msg_slab[which];
+    const XformSlab& x = c->xform_slab[which];
+    jobs.clear();
+    uint64_t at = 0, bytes = 0;  // the slab's packed output
+    for (size_t q = 0; q < r.n; ++q) {
+      const uint64_t len = ms.h_status[q] == 0 ? x.h_olen[q] : 0;
+      const size_t before = jobs.size();
+      place(r.i0 + q, ms.h_status[q], len, x.h_out + at, &jobs);
+      if (jobs.size() > before) bytes += len;
+      at += len;
+    }
+    parallel_copy(jobs, bytes);
+    r.n = 0;
+    return AMBRYCRC_OK;
+  };
+  // One message too large for a slab: its own device buffers, synchronously.
+  auto oversize = [&](size_t i) -> int {
+    const uint64_t lo = std::min(msg_off[i], region_len), n = ext[i];
+    const uint64_t cap = ambrycrc_transform_out_bound(n, 1);
+    uint8_t *d_buf = nullptr, *d_out = nullptr;
+    uint64_t *d_o = nullptr, *d_oo = nullptr, *d_ol = nullptr;
+    uint32_t* d_s = nullptr;
+    int16_t* d_l = nullptr;
+    void* d_w = nullptr;
+    std::vector<uint8_t> h;
+    const uint64_t zero = 0;
+    uint32_t st = 0;
+    uint64_t len = 0;
+    int e = AMBRYCRC_OK;
+    if (hipMalloc(reinterpret_cast<void**>(&d_buf), n) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&d_out), cap) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&d_o), 8) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&d_oo), 8) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&d_ol), 8) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&d_s), 4) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&d_l), 2) != hipSuccess ||
+        hipMalloc(&d_w, ambrycrc_transform_workspace_bytes(1)) != hipSuccess) {
+      e = AMBRYCRC_ENOMEM;
+    } else if (hipMemcpy(d_buf, region + lo, n, hipMemcpyHostToDevice) != hipSuccess ||
+               hipMemcpy(d_o, &zero, 8, hipMemcpyHostToDevice) != hipSuccess ||
+               (life_version && hipMemcpy(d_l, life_version + i, 2, hipMemcpyHostToDevice) != hipSuccess)) {
+      e = AMBRYCRC_EHIP;
+    } else {
+      e = ambrycrc_transform_messages_dev(d_buf, n, d_o, 1, life_version ? d_l : nullptr, header_version, d_out, cap,
+                                          d_oo, d_ol, d_s, d_w, ambrycrc_transform_workspace_bytes(1), nullptr);
+      if (!e && (hipMemcpy(&st, d_s, 4, hipMemcpyDeviceToHost) != hipSuccess ||
+                 hipMemcpy(&len, d_ol, 8, hipMemcpyDeviceToHost) != hipSuccess))
+        e = AMBRYCRC_EHIP;
+      if (!e && st == 0) {
+        h.resize(len);
+        if (len && hipMemcpy(h.data(), d_out, len, hipMemcpyDeviceToHost) != hipSuccess) e = AMBRYCRC_EHIP;
+      }
+    }
+    for (void* p : {(void*)d_buf, (void*)d_out, (void*)d_o, (void*)d_oo, (void*)d_ol, (void*)d_s, (void*)d_l, d_w})
+      if (p) (void)hipFree(p);
+    if (!e) place(i, st, st == 0 ? len : 0, h.data(), nullptr);
+    return e;
+  };
+  size_t i = 0;
+  int k = 0;
+  while (i < m && !rc) {
+    if (ext[i] > kSlabBytes) {
+      for (int d = 0; d < kSlabs && !rc; ++d) rc = drain((k + d) % kSlabs);  // keep the output in order
+      if (!rc) rc = oversize(i);
+      ++i;
+      continue;
+    }
+    const int w = k % kSlabs;
+    rc = drain(w);
+    if (rc) break;
+    HostSlab& s = c->slab[w];
+    MsgSlab& ms = c->msg_slab[w];
+    XformSlab& x = c->xform_slab[w];
+    Run& r = inflight[w];
+    r.i0 = i;
+    uint64_t lo = std::min(msg_off[i], region_len), hi = lo + ext[i];
+    size_t n = 0;
+    while (i + n < m && n < kSlabMsgs && ext[i + n] <= kSlabBytes) {
+      const uint64_t o = std::min(msg_off[i + n], region_len), e = o + ext[i + n];
+      const uint64_t nlo = std::min(lo, o), nhi = std::max(hi, e);
+      if (nhi - nlo > kSlabBytes) break;
+      lo = nlo;
+      hi = nhi;
+      ++n;
+    }
+    const uint64_t span = hi - lo;
+    for (size_t q = 0; q < n; ++q) {
+      ms.h_off[q] = msg_off[i + q] > region_len ? span + 1 : msg_off[i + q] - lo;
+      if (life_version) x.h_life[q] = life_version[i + q];
+    }
+    if (span) {
+      if (pinned) {
+        if (hipMemcpyAsync(s.d_data, region + lo, span, hipMemcpyHostToDevice, s.stream) != hipSuccess) rc = AMBRYCRC_EHIP;
+      } else {
+        jobs.clear();
+        jobs.push_back({s.h_data, region + lo, span});
+        parallel_copy(jobs, span);  // overlaps the DMA and kernels of the slabs already issued
+        if (hipMemcpyAsync(s.d_data, s.h_data, span, hipMemcpyHostToDevice, s.stream) != hipSuccess) rc = AMBRYCRC_EHIP;
+      }
+    }
+    const uint64_t cap = ambrycrc_transform_out_bound(span, n);
+    if (!rc && (hipMemcpyAsync(ms.d_off, ms.h_off, n * sizeof(uint64_t), hipMemcpyHostToDevice, s.stream) != hipSuccess ||
+                (life_version &&
+                 hipMemcpyAsync(x.d_life, x.h_life, n * sizeof(int16_t), hipMemcpyHostToDevice, s.stream) != hipSuccess)))
+      rc = AMBRYCRC_EHIP;
+    if (!rc)
+      rc = ambrycrc_transform_messages_dev(s.d_data, span, ms.d_off, n, life_version ? x.d_life : nullptr, header_version,
+                                           x.d_out, cap, x.d_ooff, x.d_olen, ms.d_status, x.d_ws,
+                                           ambrycrc_transform_workspace_bytes(kSlabMsgs), s.stream);
+    if (!rc && (hipMemcpyAsync(ms.h_status, ms.d_status, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s.stream) !=
+                    hipSuccess ||
+                hipMemcpyAsync(x.h_olen, x.d_olen, n * sizeof(uint64_t), hipMemcpyDeviceToHost, s.stream) != hipSuccess ||
+                hipMemcpyAsync(x.h_out, x.d_out, cap, hipMemcpyDeviceToHost, s.stream) != hipSuccess ||
+                hipEventRecord(s.done, s.stream) != hipSuccess))
+      rc = AMBRYCRC_EHIP;
+    if (rc) break;
+    r.n = n;
+    i += n;
+    ++k;
+  }
+  int rc2 = AMBRYCRC_OK;
+  for (int d = 0; d < kSlabs; ++d) {  // oldest first: the output is packed in message order
+    const int rr = drain((k + d) % kSlabs);
+    if (!rc2) rc2 = rr;
   }
   (void)hipSetDevice(prev);
   return rc ? rc : rc2;

@@ -50,6 +50,20 @@ struct MsgSlab {  // message verify staging per HostSlab, allocated on first use
   void* d_ws = nullptr;
 };
 
+// Transform staging per HostSlab (ambrycrc_transform_messages_host), allocated on first use: the
+// slab's re-serialized messages (at most ambrycrc_transform_out_bound of its span and count).
+constexpr size_t kXformOutBytes = kSlabBytes + (size_t)AMBRYCRC_TRANSFORM_GROWTH_MAX * kSlabMsgs;
+struct XformSlab {
+  int16_t* h_life = nullptr;  // pinned [kSlabMsgs]
+  int16_t* d_life = nullptr;
+  uint8_t* h_out = nullptr;   // pinned [kXformOutBytes]
+  uint8_t* d_out = nullptr;
+  uint64_t* h_olen = nullptr;  // pinned [kSlabMsgs]
+  uint64_t* d_olen = nullptr;
+  uint64_t* d_ooff = nullptr;
+  void* d_ws = nullptr;       // ambrycrc_transform_workspace_bytes(kSlabMsgs)
+};
+
 struct DevCtx {
   int device = -1;
   int num_cu = 0;
@@ -93,6 +107,8 @@ struct DevCtx {
   HostSlab slab[kSlabs];
   bool msg_slabs_ready = false;
   MsgSlab msg_slab[kSlabs];
+  bool xform_slabs_ready = false;
+  XformSlab xform_slab[kSlabs];
   std::mutex mu;     // guards the slabs (held across a whole host-path call)
   std::mutex ev_mu;  // guards the timing events (taken inside enqueue_batch, which host-path calls reach with mu held)
 };

@@ -196,3 +196,34 @@ def transform_dev(region, msg_off, header_version: int = 3, life_version=None, o
                                                 ptr(status), None, 0, ctypes.c_void_p(_stream_handle(stream))),
           "ambrycrc_transform_messages_dev")
     return out, out_off, out_len, status
+
+
+def transform_host(region, msg_off, header_version: int = 3, life_version=None, out_cap=None, device: int = 0,
+                   pinned: bool = False):
+    """ambrycrc_transform_messages_host: the batched transform of a region in host memory (bytes,
+    bytearray, uint8 numpy array or uint8 CPU tensor; pinned=True for a pin_memory() tensor), staged
+    through the pinned slabs. Returns (out bytes packed in message order, out_off int64[m] (-1: not
+    transformed), out_len int64[m], status uint32[m])."""
+    if hasattr(region, "data_ptr"):
+        base, n = region.data_ptr(), region.numel()
+        keep = region
+    else:
+        keep = np.frombuffer(region, dtype=np.uint8) if not isinstance(region, np.ndarray) else region
+        base, n = keep.ctypes.data, keep.size
+    offs = np.ascontiguousarray(np.asarray(msg_off, dtype=np.uint64))
+    m = offs.size
+    cap = out_bound(n, m) if out_cap is None else int(out_cap)
+    out = np.zeros(max(cap, 1), dtype=np.uint8)
+    life = None if life_version is None else np.ascontiguousarray(np.asarray(life_version, dtype=np.int16))
+    oo = np.zeros(m, dtype=np.uint64)
+    ol = np.zeros(m, dtype=np.uint64)
+    st = np.zeros(m, dtype=np.uint32)
+    u64p = ctypes.POINTER(ctypes.c_uint64)
+    check(lib().ambrycrc_transform_messages_host(
+        ctypes.c_void_p(base), n, offs.ctypes.data_as(u64p), m, None if life is None else life.ctypes.data,
+        header_version, out.ctypes.data, cap, oo.ctypes.data_as(u64p), ol.ctypes.data_as(u64p),
+        st.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), device, 1 if pinned else 0),
+        "ambrycrc_transform_messages_host")
+    del keep
+    used = int((oo[st == 0] + ol[st == 0]).max()) if (st == 0).any() else 0
+    return out[:used].tobytes(), oo.view(np.int64), ol.view(np.int64), st

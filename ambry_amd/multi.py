@@ -56,28 +56,32 @@ def gather_compact(padded: np.ndarray, counts: Sequence[int]) -> np.ndarray:
     return out
 
 
-def gather_crcs(local, lo: int, hi: int, n: int, shards, dist, group=None):
-    """All-gather each rank's CRCs (int32 CPU tensor of hi-lo) into the full int32[n] on every rank:
-    the padded segment layout of ambrycrc_gather_layout, one all_gather_into_tensor, then the C
-    compaction."""
+def gather_crcs(local, lo: int, hi: int, n: int, shards, dist, group=None, device=None):
+    """All-gather each rank's CRCs (int32 tensor of hi-lo) into the full int32[n] on every rank: the
+    padded segment layout of ambrycrc_gather_layout, one all_gather_into_tensor on `device` (None:
+    the CPU, for gloo; a CUDA device for an NCCL/RCCL group, which rejects CPU tensors), then the C
+    compaction on the host. The result lives on `device` (CPU when None)."""
     import torch
 
     counts = [h - l for l, h in shards]
     world = len(shards)
     width, _, _ = gather_layout(counts)
     seg = max(width, 1)
-    padded = torch.zeros(seg, dtype=torch.int32)
+    padded = torch.zeros(seg, dtype=torch.int32, device=device)
     if hi > lo:
-        padded[: hi - lo] = local
-    gathered = torch.empty(world * seg, dtype=torch.int32)
+        padded[: hi - lo] = local.to(padded.device)
+    gathered = torch.empty(world * seg, dtype=torch.int32, device=device)
     dist.all_gather_into_tensor(gathered, padded, group=group)
-    out = gather_compact(gathered.numpy().view(np.uint32), counts)
+    out = gather_compact(gathered.cpu().numpy().view(np.uint32), counts)
     assert out.size == n
-    return torch.from_numpy(out.view(np.int32).copy())
+    res = torch.from_numpy(out.view(np.int32).copy())
+    return res if device is None else res.to(device)
 
 
-def distributed_batch(lengths: Sequence[int], compute: Callable[[int, int], "object"], dist, group=None):
-    """Shard chunks by bytes, run `compute(lo, hi)` (-> int32 tensor of hi-lo CRCs) on this rank, all-gather.
+def distributed_batch(lengths: Sequence[int], compute: Callable[[int, int], "object"], dist, group=None,
+                      device=None):
+    """Shard chunks by bytes, run `compute(lo, hi)` (-> int32 tensor of hi-lo CRCs) on this rank, all-gather
+    (on `device`: None for a gloo group, the rank's CUDA device for NCCL/RCCL -- gather_crcs).
 
     Returns (all CRCs as int32[n] tensor, (lo, hi) of this rank).
     """
@@ -86,7 +90,7 @@ def distributed_batch(lengths: Sequence[int], compute: Callable[[int, int], "obj
     shards = shard_by_bytes(lengths, world)
     lo, hi = shards[rank]
     local = compute(lo, hi)
-    return gather_crcs(local, lo, hi, len(lengths), shards, dist, group=group), (lo, hi)
+    return gather_crcs(local, lo, hi, len(lengths), shards, dist, group=group, device=device), (lo, hi)
 
 
 def split_blob(total: int, world: int) -> list[tuple[int, int]]:

@@ -316,6 +316,20 @@ int ambrycrc_verify_trailed_host(const void* const* ptrs, const uint64_t* lens, 
 int ambrycrc_verify_messages_host(const uint8_t* region, uint64_t region_len, const uint64_t* msg_off, size_t m,
                                   uint32_t* status, uint64_t* msg_end, int device, int pinned);
 
+/* ambrycrc_transform_messages_dev for a region in HOST memory (replication's batch: the messages of
+ * one GetResponse, MessageSievingInputStream.java:130,278-288 over ReplicaThread.java:1810-1815).
+ * Messages are staged in index order through the context's pinned slabs (runs of consecutive
+ * messages whose span fits 64 MiB; a message larger than a slab gets its own buffers) and each
+ * slab's re-serialized messages come back through pinned memory. Outputs equal those of one
+ * ambrycrc_transform_messages_dev call over the whole region: out[0 .. out_cap) packed in message
+ * order, out_off[i] (nullable; UINT64_MAX when not transformed), out_len[i], status[i] (host arrays);
+ * life_version (nullable) host int16[m]. out_cap = ambrycrc_transform_out_bound(region_len, m)
+ * never yields AMBRYCRC_MSG_NO_ROOM for messages that share no bytes. pinned != 0: region is
+ * hipHostMalloc'd / registered. Synchronous. */
+int ambrycrc_transform_messages_host(const uint8_t* region, uint64_t region_len, const uint64_t* msg_off, size_t m,
+                                     const int16_t* life_version, int header_version, uint8_t* out, uint64_t out_cap,
+                                     uint64_t* out_off, uint64_t* out_len, uint32_t* status, int device, int pinned);
+
 /* Host-side message chain for a log region in host memory (the sequential hop of
  * BlobStoreRecovery.recover, BlobStoreRecovery.java:43-110): starting at `start`,
  * read each header (V1/V2/V3, header CRC checked) and follow its size to the next

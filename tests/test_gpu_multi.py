@@ -174,3 +174,35 @@ def test_c5_shard_256gib_through_multi_entry(gpu, oracle):
     assert acc == int(whole.cpu().numpy().view(np.uint32)[0])
     del buf
     torch.cuda.empty_cache()
+
+
+def test_distributed_batch_on_rccl_group(gpu, oracle):
+    """ambry_amd.multi.distributed_batch on an NCCL (= RCCL) process group of world size 1 with
+    device="cuda": the padded all-gather runs on device tensors (RCCL rejects CPU ones), the
+    compaction in C, and the CRCs equal the oracle's (the device argument)."""
+    import os
+    import socket
+
+    import torch
+    import torch.distributed as dist
+
+    from ambry_amd import device as D
+    from ambry_amd.multi import distributed_batch
+
+    mem, off, ln = _batch(61, 300, 100000)
+    base, d_off, d_len = _dev(torch, mem, off, ln)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        def compute(lo, hi):
+            return D.crc32_batch(base, d_off[lo:hi].contiguous(), d_len[lo:hi].contiguous())
+
+        crcs, (lo, hi) = distributed_batch(ln.tolist(), compute, dist, device="cuda")
+        torch.cuda.synchronize()
+        assert crcs.is_cuda and (lo, hi) == (0, len(ln))
+        assert np.array_equal(crcs.cpu().numpy().view(np.uint32), oracle.batch(mem, off, ln))
+    finally:
+        dist.destroy_process_group()

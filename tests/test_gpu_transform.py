@@ -234,3 +234,88 @@ def test_transform_speculative_pass(gpu, mf, version):
             assert oo[i] == pos and ol[i] == len(exp), i
             assert out[pos:pos + len(exp)] == exp, i
             pos += len(exp)
+
+
+@pytest.mark.parametrize("version", [3, 1])
+def test_transform_host_matches_dev_and_oracle(gpu, mf, version):
+    """ambrycrc_transform_messages_host (the region in host memory, staged through the pinned slabs)
+    gives the device call's outputs over the whole region -- packed in message order, byte-exact
+    against the oracle -- on the mixed region (failures, updates, gaps) and on a dense old one."""
+    import torch
+
+    from ambry_amd.messages import transform_dev, transform_host
+
+    for region, offs in (build_region(mf, 500, seed=140 + version), dense_old_region(mf, 300, seed=9)):
+        life = np.random.default_rng(3).integers(0, 9, size=len(offs)).astype(np.int16)
+        out, oo, ol, st = transform_host(region, offs, header_version=version, life_version=life)
+        dev = torch.frombuffer(bytearray(region), dtype=torch.uint8).cuda()
+        dout, doo, dol, dst = transform_dev(dev, torch.tensor(offs, dtype=torch.int64, device="cuda"),
+                                            header_version=version, life_version=torch.from_numpy(life).cuda())
+        torch.cuda.synchronize()
+        assert np.array_equal(st, dst.cpu().numpy().view(np.uint32))
+        assert np.array_equal(oo, doo.cpu().numpy()) and np.array_equal(ol, dol.cpu().numpy())
+        assert out == dout.cpu().numpy().tobytes()[:len(out)]
+        pos = 0
+        for i, o in enumerate(offs):
+            exp_st, exp = mf.transform_message(region, o, life=int(life[i]), version=version)
+            assert int(st[i]) == exp_st, i
+            if exp is not None:
+                assert oo[i] == pos and out[pos:pos + len(exp)] == exp, i
+                pos += len(exp)
+
+
+def test_transform_host_slabs_order_room_and_pinned(gpu, mf):
+    """Many slabs (a 150 MiB region of 64 KiB-blob messages: three 64 MiB slabs), pinned and pageable
+    sources, unsorted offsets (packing follows the message order, not the offsets), and a capacity
+    that cuts the batch: the prefix that fits is placed, the rest get MSG_NO_ROOM (as the device
+    call's exclusive scan of the lengths decides)."""
+    import torch
+
+    from ambry_amd.messages import MSG_NO_ROOM, transform_host
+
+    msgs = [mf.put_message(mf.store_key("s%d" % i), mf.blob_properties_bytes(65536, serde_version=1 + i % 5),
+                           b"m" * (i % 50), stream_bytes(i, 0, 65536).tobytes(), version=1 + i % 3)
+            for i in range(16)]
+    tmpl = b"".join(msgs)
+    reps = 150
+    region = tmpl * reps
+    offs = np.cumsum([0] + [len(x) for x in msgs[:-1]]).tolist()
+    all_offs = [r * len(tmpl) + o for r in range(reps) for o in offs]
+    want = [mf.transform_message(region, o)[1] for o in all_offs[:16]]
+    out, oo, ol, st = transform_host(region, all_offs)
+    assert st.tolist() == [0] * len(all_offs)
+    assert out == b"".join(want) * reps
+    pinned = torch.frombuffer(bytearray(region), dtype=torch.uint8).pin_memory()
+    out_p, oo_p, _, st_p = transform_host(pinned, all_offs, pinned=True)
+    assert out_p == out and np.array_equal(oo_p, oo) and np.array_equal(st_p, st)
+    # unsorted: message order decides the packing
+    perm = np.random.default_rng(1).permutation(64)
+    sub = [all_offs[j] for j in perm]
+    out_u, oo_u, ol_u, st_u = transform_host(region, sub)
+    pos = 0
+    for k, j in enumerate(perm):
+        exp = want[j % 16]
+        assert oo_u[k] == pos and out_u[pos:pos + len(exp)] == exp
+        pos += len(exp)
+    # a cap that holds the first 20 of them
+    cap = int(oo_u[20])
+    _, oo_c, ol_c, st_c = transform_host(region, sub, out_cap=cap)
+    assert st_c[:20].tolist() == [0] * 20 and all(s == MSG_NO_ROOM for s in st_c[20:])
+    assert (oo_c[20:] == -1).all() and (ol_c[20:] == 0).all()
+
+
+def test_transform_host_oversize_message(gpu, mf):
+    """A message larger than a 64 MiB staging slab (a 70 MiB blob, Blob_Format_V1 under a V1 header)
+    gets its own device buffers; the messages around it keep their order and bytes."""
+    from ambry_amd.messages import transform_host
+
+    big = _blob_v1_message(mf, mf.store_key("big"), mf.blob_properties_bytes(70 << 20, serde_version=1), b"meta",
+                           stream_bytes(5, 0, 70 << 20).tobytes(), 1)
+    small = mf.put_message(mf.store_key("s"), mf.blob_properties_bytes(10), b"", b"0123456789")
+    region = small + big + small
+    offs = [0, len(small), len(small) + len(big)]
+    out, oo, ol, st = transform_host(region, offs)
+    assert st.tolist() == [0, 0, 0]
+    want = [mf.transform_message(region, o)[1] for o in offs]
+    assert out == b"".join(want)
+    assert len(want[1]) == len(big) + 26

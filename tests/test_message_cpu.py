@@ -106,3 +106,24 @@ def test_transform_dense_old_region_bound(ambry):
         worst = max(worst, len(exp) - len(msg))
     assert worst == TRANSFORM_GROWTH_MAX
     assert out_bound(2**64 - 10, 1) == 2**64 - 1  # saturates
+
+
+def test_transform_host_argument_errors(ambry):
+    """ambrycrc_transform_messages_host rejects bad arguments before touching a device, and reports
+    ENOINIT for a device with no context (no GPU in the build container)."""
+    import ctypes
+
+    from ambry_amd._lib import lib
+
+    region = (ctypes.c_uint8 * 64)()
+    offs = (ctypes.c_uint64 * 1)(0)
+    st = (ctypes.c_uint32 * 1)()
+    ol = (ctypes.c_uint64 * 1)()
+    out = (ctypes.c_uint8 * 128)()
+    f = lib().ambrycrc_transform_messages_host
+    assert f(region, 64, offs, 0, None, 3, out, 128, None, ol, st, 0, 0) == 0  # m == 0: nothing to do
+    assert f(region, 64, offs, 1, None, 4, out, 128, None, ol, st, 0, 0) == -1  # header version
+    assert f(region, 64, None, 1, None, 3, out, 128, None, ol, st, 0, 0) == -1
+    assert f(region, 64, offs, 1, None, 3, out, 128, None, None, st, 0, 0) == -1
+    assert f(region, 64, offs, 1, None, 3, None, 128, None, ol, st, 0, 0) == -1  # out NULL with a capacity
+    assert f(region, 64, offs, 1, None, 3, out, 128, None, ol, st, 63, 0) == -4  # no context
