@@ -26,6 +26,8 @@
  *   int  nativeVerifyMessage(ByteBuffer region, long offset, long[] end)
  *   int  nativeTransformMessage(ByteBuffer region, long offset, int lifeVersion, int headerVersion,
  *                               ByteBuffer out, long[] outLen)
+ *   void nativeTransformMessages(ByteBuffer region, long[] offsets, short[] lifeVersions, int headerVersion,
+ *                                ByteBuffer out, long[] outOffsets, long[] outLens, int[] status, int device)
  * CRC values travel as Java ints holding the uint32 bit pattern.
  */
 #include <jni.h>
@@ -285,4 +287,57 @@ JNIEXPORT jint JNICALL JNI_FN(nativeTransformMessage)(JNIEnv* env, jclass cls, j
   const jlong jn = (jlong)n;
   (*env)->SetLongArrayRegion(env, out_len, 0, 1, &jn);
   return (jint)st;
+}
+
+/* ValidatingTransformer.transform over a batch (MessageSievingInputStream.java:130,278-288 over one
+ * GetResponse, ReplicaThread.java:1810-1815) -> ambrycrc_transform_messages_host: the messages at
+ * `offsets` in the direct buffer `region`, re-serialized at headerVersion with lifeVersions[i]
+ * (null: the stored ones), packed in message order into the direct buffer `out` from 0 (its
+ * capacity is the output cap: NativeCrc32.transformOutBound sizes it). outOffsets[i] (nullable;
+ * -1 when not transformed), outLens[i] and status[i] get the per-message results. */
+JNIEXPORT void JNICALL JNI_FN(nativeTransformMessages)(JNIEnv* env, jclass cls, jobject region, jlongArray offsets,
+                                                       jshortArray life_versions, jint header_version, jobject out,
+                                                       jlongArray out_offsets, jlongArray out_lens, jintArray status,
+                                                       jint device) {
+  (void)cls;
+  if (!region || !offsets || !out || !out_lens || !status) {
+    raise(env, AJC_ENULL);
+    return;
+  }
+  const jsize m = (*env)->GetArrayLength(env, offsets);
+  if (raise(env, ajc_transform_lengths(m, life_versions ? (*env)->GetArrayLength(env, life_versions) : -1,
+                                       out_offsets ? (*env)->GetArrayLength(env, out_offsets) : -1,
+                                       (*env)->GetArrayLength(env, out_lens), (*env)->GetArrayLength(env, status))))
+    return;
+  int64_t cap, ocap;
+  const uint8_t* base = direct(env, region, &cap);
+  uint8_t* dst = (uint8_t*)direct(env, out, &ocap);
+  if (!base || !dst) {
+    raise(env, AJC_ENOTDIRECT);
+    return;
+  }
+  if (m == 0) return;
+  uint64_t* offs = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)m);
+  int16_t* life = life_versions ? (int16_t*)malloc(sizeof(int16_t) * (size_t)m) : NULL;
+  uint64_t* oo = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)m);
+  uint64_t* ol = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)m);
+  uint32_t* st = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)m);
+  int rc = AMBRYCRC_ENOMEM;
+  if (offs && oo && ol && st && (!life_versions || life)) {
+    (*env)->GetLongArrayRegion(env, offsets, 0, m, (jlong*)offs);
+    if (life_versions) (*env)->GetShortArrayRegion(env, life_versions, 0, m, (jshort*)life);
+    rc = ambrycrc_transform_messages_host(base, (uint64_t)cap, offs, (size_t)m, life, header_version, dst,
+                                          (uint64_t)ocap, oo, ol, st, device, 0);
+    if (rc == AMBRYCRC_OK) {
+      if (out_offsets) (*env)->SetLongArrayRegion(env, out_offsets, 0, m, (const jlong*)oo);
+      (*env)->SetLongArrayRegion(env, out_lens, 0, m, (const jlong*)ol);
+      (*env)->SetIntArrayRegion(env, status, 0, m, (const jint*)st);
+    }
+  }
+  free(offs);
+  free(life);
+  free(oo);
+  free(ol);
+  free(st);
+  raise(env, rc);
 }

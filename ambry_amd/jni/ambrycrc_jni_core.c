@@ -80,3 +80,10 @@ int ajc_verify_lengths(int64_t m, int64_t status_len, int64_t ends_len) {
   if (status_len < m || (ends_len >= 0 && ends_len < m)) return AJC_ESHORT;
   return AJC_OK;
 }
+
+int ajc_transform_lengths(int64_t m, int64_t life_len, int64_t out_off_len, int64_t out_len_len, int64_t status_len) {
+  if (m < 0 || out_len_len < 0 || status_len < 0) return AJC_ENULL;
+  if (status_len < m || out_len_len < m || (out_off_len >= 0 && out_off_len < m) || (life_len >= 0 && life_len < m))
+    return AJC_ESHORT;
+  return AJC_OK;
+}

@@ -57,6 +57,10 @@ int ajc_batch_lengths(int64_t n, int64_t pos_len, int64_t len_len, int64_t crc_i
 /* nativeVerifyMessages: m offsets; status holds >= m entries; ends (-1: null) too. */
 int ajc_verify_lengths(int64_t m, int64_t status_len, int64_t ends_len);
 
+/* nativeTransformMessages: m offsets; status, outLens, outOffsets (-1: null) and lifeVersions (-1: null)
+ * hold >= m entries each. */
+int ajc_transform_lengths(int64_t m, int64_t life_len, int64_t out_off_len, int64_t out_len_len, int64_t status_len);
+
 #ifdef __cplusplus
 }
 #endif

@@ -136,11 +136,38 @@ public final class NativeCrc32 implements Checksum {
    * ValidatingTransformer.transform for one stored message on the CPU (ambrycrc_transform_message_cpu):
    * verify, refuse update records, re-serialize at `headerVersion` (1..3) with `lifeVersion` (< 0:
    * the stored one) into `out` from position 0. Returns the status bits (0: transformed; MSG_NOT_PUT,
-   * MSG_BAD_RECORD, MSG_NO_ROOM or verify bits otherwise); outLen[0] = bytes written.
+   * MSG_BAD_RECORD, MSG_NOT_ENCODABLE, MSG_NO_ROOM or verify bits otherwise); outLen[0] = bytes
+   * written. An `out` of transformOutBound(storedSize, 1) bytes never yields MSG_NO_ROOM.
    */
   public static int transformMessage(ByteBuffer region, long offset, int lifeVersion, int headerVersion,
       ByteBuffer out, long[] outLen) {
     return nativeTransformMessage(region, offset, lifeVersion, headerVersion, out, outLen);
+  }
+
+  /**
+   * ValidatingTransformer.transform for a batch of stored messages on GPU `device`
+   * (ambrycrc_transform_messages_host): the messages at `offsets` in the direct buffer `region` (one
+   * GetResponse's bytes, MessageSievingInputStream.java:130,278-288), re-serialized at `headerVersion`
+   * with lifeVersions[i] (null: the stored ones) and packed in message order into the direct buffer
+   * `out` from 0 -- its capacity is the output cap; transformOutBound(regionBytes, offsets.length)
+   * never yields MSG_NO_ROOM. outOffsets[i] (may be null; -1 when not transformed), outLens[i] and
+   * status[i] get each message's result.
+   */
+  public static void transformMessages(ByteBuffer region, long[] offsets, short[] lifeVersions, int headerVersion,
+      ByteBuffer out, long[] outOffsets, long[] outLens, int[] status, int device) {
+    nativeTransformMessages(region, offsets, lifeVersions, headerVersion, out, outOffsets, outLens, status, device);
+  }
+
+  /**
+   * Largest growth of one message under the transform (AMBRYCRC_TRANSFORM_GROWTH_MAX): header V1 to V3
+   * (+6), BlobProperties SerDe V1 to VERSION_5 (+17), Blob_Format_V1 to V3 head (+3); the reference
+   * sizes its output from the same fields (PutMessageFormatInputStream.java:88-90,122).
+   */
+  public static final int TRANSFORM_GROWTH_MAX = 26;
+
+  /** Output capacity for m messages that share no bytes of a regionBytes-long region (ambrycrc_transform_out_bound). */
+  public static long transformOutBound(long regionBytes, int m) {
+    return regionBytes + (long) m * TRANSFORM_GROWTH_MAX;
   }
 
   /** AMBRYCRC_MSG_* status bits of verifyMessages (include/ambrycrc.h). */
@@ -155,6 +182,8 @@ public final class NativeCrc32 implements Checksum {
   public static final int MSG_NOT_PUT = 1 << 10;
   public static final int MSG_BAD_RECORD = 1 << 11;
   public static final int MSG_NO_ROOM = 1 << 12;
+  /** A BlobProperties string is not ASCII: the reference's V5 re-serialization overflows its buffer. */
+  public static final int MSG_NOT_ENCODABLE = 1 << 13;
 
   private static native void nativeInit(int device);
 
@@ -178,4 +207,7 @@ public final class NativeCrc32 implements Checksum {
 
   private static native int nativeTransformMessage(ByteBuffer region, long offset, int lifeVersion,
       int headerVersion, ByteBuffer out, long[] outLen);
+
+  private static native void nativeTransformMessages(ByteBuffer region, long[] offsets, short[] lifeVersions,
+      int headerVersion, ByteBuffer out, long[] outOffsets, long[] outLens, int[] status, int device);
 }

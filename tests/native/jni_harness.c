@@ -13,7 +13,7 @@
 #include <stdlib.h>
 #include <string.h>
 
-enum Kind { K_CLASS, K_BYTES, K_INTS, K_LONGS, K_OBJS, K_BUFFER };
+enum Kind { K_CLASS, K_BYTES, K_INTS, K_LONGS, K_SHORTS, K_OBJS, K_BUFFER };
 
 struct _jobject {
   enum Kind kind;
@@ -95,6 +95,11 @@ static void set_long_region(JNIEnv* env, jlongArray a, jsize s, jsize n, const j
   region_check(a, s, n);
   memcpy((jlong*)a->data + s, buf, sizeof(jlong) * (size_t)n);
 }
+static void get_short_region(JNIEnv* env, jshortArray a, jsize s, jsize n, jshort* buf) {
+  (void)env;
+  region_check(a, s, n);
+  memcpy(buf, (jshort*)a->data + s, sizeof(jshort) * (size_t)n);
+}
 static void* get_critical(JNIEnv* env, jarray a, jboolean* copy) {
   (void)env;
   if (copy) *copy = JNI_FALSE;
@@ -118,8 +123,8 @@ static jlong direct_capacity(JNIEnv* env, jobject b) {
 static const struct JNINativeInterface_ g_fns = {
     find_class,         throw_new,       exception_check, delete_local_ref, get_method_id,
     call_int_method,    get_array_length, get_object_array_element, get_int_region, set_int_region,
-    get_long_region,    set_long_region, get_critical,    release_critical, direct_address,
-    direct_capacity,
+    get_long_region,    set_long_region, get_short_region, get_critical,   release_critical,
+    direct_address,     direct_capacity,
 };
 static JNIEnv g_env = &g_fns;
 
@@ -151,6 +156,38 @@ static struct _jobject arr(enum Kind k, void* data, jsize len) {
 
 JNIEXPORT jint JNICALL FN(nativeVerifyMessage)(JNIEnv*, jclass, jobject, jlong, jlongArray);
 JNIEXPORT jint JNICALL FN(nativeTransformMessage)(JNIEnv*, jclass, jobject, jlong, jint, jint, jobject, jlongArray);
+JNIEXPORT void JNICALL FN(nativeTransformMessages)(JNIEnv*, jclass, jobject, jlongArray, jshortArray, jint, jobject,
+                                                   jlongArray, jlongArray, jintArray, jint);
+
+/* argv[1] == "gpumsg", argv[2] = one PUT message (header V3, properties at SerDe V5): the batched
+ * transform over a region holding it twice, on the GPU. */
+static int gpumsg_cases(const char* path) {
+  FILE* f = fopen(path, "rb");
+  if (!f) return 2;
+  static uint8_t region[2 << 20], out[2 << 20];
+  const size_t n = fread(region, 1, 1 << 20, f);
+  fclose(f);
+  memcpy(region + n, region, n);
+  FN(nativeInit)(&g_env, NULL, 0);
+  report("gpumsg_init", 0);
+  struct _jobject reg = arr(K_BUFFER, region, (jsize)(2 * n)), dst = arr(K_BUFFER, out, (jsize)(2 * n + 52));
+  jlong offs[2] = {0, (jlong)n}, oo[2] = {-5, -5}, ol[2] = {-5, -5};
+  jshort life[2] = {0, 0};
+  jint st[2] = {-5, -5};
+  struct _jobject joffs = arr(K_LONGS, offs, 2), joo = arr(K_LONGS, oo, 2), jol = arr(K_LONGS, ol, 2);
+  struct _jobject jlife = arr(K_SHORTS, life, 2), jst = arr(K_INTS, st, 2);
+  FN(nativeTransformMessages)(&g_env, NULL, &reg, &joffs, &jlife, 3, &dst, &joo, &jol, &jst, 0);
+  report("gpumsg_xform_st", st[0] | st[1]);
+  report("gpumsg_xform_off1", (jint)oo[1]);
+  report("gpumsg_xform_len", (jint)(ol[0] + ol[1]));
+  report("gpumsg_xform_same", (jint)(memcmp(out, region, 2 * n) == 0));
+  /* no room for the second message: cap = one message */
+  struct _jobject one = arr(K_BUFFER, out, (jsize)n);
+  FN(nativeTransformMessages)(&g_env, NULL, &reg, &joffs, NULL, 3, &one, NULL, &jol, &jst, 0);
+  report("gpumsg_xform_room0", st[0]);
+  report("gpumsg_xform_room1", st[1]);
+  return 0;
+}
 
 /* argv[1] == "msg", argv[2] = a file holding one PUT message: the per-message CPU entries. */
 static int msg_cases(const char* path) {
@@ -212,6 +249,7 @@ static int gpu_cases(void) {
 int main(int argc, char** argv) {
   if (argc > 1 && strcmp(argv[1], "gpu") == 0) return gpu_cases();
   if (argc > 2 && strcmp(argv[1], "msg") == 0) return msg_cases(argv[2]);
+  if (argc > 2 && strcmp(argv[1], "gpumsg") == 0) return gpumsg_cases(argv[2]);
   static uint8_t digits[] = "123456789";
   struct _jobject b9 = arr(K_BYTES, digits, 9);
   report("array_full", FN(nativeUpdateArray)(&g_env, NULL, 0, &b9, 0, 9));
@@ -267,6 +305,24 @@ int main(int argc, char** argv) {
   report("verify_heap", 0);
   FN(nativeVerifyMessages)(&g_env, NULL, NULL, &joffs, &jst, NULL, 0);
   report("verify_null", 0);
+
+  /* batched transform: argument errors first, then (no context for device 0 here) the device error */
+  jlong xo[2] = {0, 4}, xol[2] = {0, 0}, xol1[1] = {0};
+  int16_t xlife1[1] = {0};
+  jint xst[2] = {0, 0};
+  static uint8_t xout[64];
+  struct _jobject jxo = arr(K_LONGS, xo, 2), jxol = arr(K_LONGS, xol, 2), jxol1 = arr(K_LONGS, xol1, 1);
+  struct _jobject jxlife1 = arr(K_SHORTS, xlife1, 1), jxst = arr(K_INTS, xst, 2), xdst = arr(K_BUFFER, xout, 64);
+  FN(nativeTransformMessages)(&g_env, NULL, &direct_buf, &jxo, NULL, 3, &xdst, NULL, &jxol1, &jxst, 0);
+  report("xform_short_lens", 0);
+  FN(nativeTransformMessages)(&g_env, NULL, &direct_buf, &jxo, &jxlife1, 3, &xdst, NULL, &jxol, &jxst, 0);
+  report("xform_short_life", 0);
+  FN(nativeTransformMessages)(&g_env, NULL, &direct_buf, &jxo, NULL, 3, NULL, NULL, &jxol, &jxst, 0);
+  report("xform_null_out", 0);
+  FN(nativeTransformMessages)(&g_env, NULL, &heap_buf, &jxo, NULL, 3, &xdst, NULL, &jxol, &jxst, 0);
+  report("xform_heap", 0);
+  FN(nativeTransformMessages)(&g_env, NULL, &direct_buf, &jxo, NULL, 3, &xdst, NULL, &jxol, &jxst, 0);
+  report("xform_no_context", 0);
 
   FN(nativeInit)(&g_env, NULL, 0); /* no GPU in the build container: the init error is thrown */
   report("init_no_gpu", 0);

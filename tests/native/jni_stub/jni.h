@@ -21,6 +21,7 @@
 typedef int32_t jint;
 typedef int64_t jlong;
 typedef int8_t jbyte;
+typedef int16_t jshort;
 typedef uint8_t jboolean;
 typedef jint jsize;
 
@@ -31,6 +32,7 @@ typedef jobject jarray;
 typedef jarray jbyteArray;
 typedef jarray jintArray;
 typedef jarray jlongArray;
+typedef jarray jshortArray;
 typedef jarray jobjectArray;
 typedef jobject jthrowable;
 struct _jmethodID;
@@ -52,6 +54,7 @@ struct JNINativeInterface_ {
   void (*SetIntArrayRegion)(JNIEnv* env, jintArray array, jsize start, jsize len, const jint* buf);
   void (*GetLongArrayRegion)(JNIEnv* env, jlongArray array, jsize start, jsize len, jlong* buf);
   void (*SetLongArrayRegion)(JNIEnv* env, jlongArray array, jsize start, jsize len, const jlong* buf);
+  void (*GetShortArrayRegion)(JNIEnv* env, jshortArray array, jsize start, jsize len, jshort* buf);
   void* (*GetPrimitiveArrayCritical)(JNIEnv* env, jarray array, jboolean* isCopy);
   void (*ReleasePrimitiveArrayCritical)(JNIEnv* env, jarray array, void* carray, jint mode);
   void* (*GetDirectBufferAddress)(JNIEnv* env, jobject buf);

@@ -151,7 +151,9 @@ def test_jni_shim_against_fake_jvm(core, tmp_path):
         "combine_negative": (0, IAE), "direct_all": (crc(b"123456789"), "-"), "direct_all_bounds": (0, IOOBE),
         "direct_all_heap": (0, IAE), "batch_short_out": (0, IAE), "batch_null": (0, NPE),
         "batch_bounds": (0, IOOBE), "verify_short_status": (0, IAE), "verify_heap": (0, IAE),
-        "verify_null": (0, NPE),
+        "verify_null": (0, NPE), "xform_short_lens": (0, IAE), "xform_short_life": (0, IAE),
+        "xform_null_out": (0, NPE), "xform_heap": (0, IAE),
+        "xform_no_context": (0, "java/lang/IllegalStateException"),
     }
     for name, want in expect.items():
         assert got[name] == want, name
@@ -196,3 +198,21 @@ def test_jni_shim_message_entries(core, tmp_path):
     assert got["msg_transform_small"] == (1 << 12, "-") and got["msg_transform_small_len"] == (0, "-")
     assert got["msg_transform_badver"][1] in (IAE, ISE)
     assert got["msg_verify_corrupt"] == (1 << 5, "-") and got["msg_transform_corrupt"] == (1 << 5, "-")
+
+
+@pytest.mark.gpu
+def test_jni_shim_batched_transform(core, tmp_path):
+    """nativeTransformMessages (ambrycrc_transform_messages_host) in the fake JVM on the GPU: the C1
+    message twice in a direct buffer, transformed at header V3 with life versions 0 -- the output
+    reproduces the region, the second message packed right after the first -- then an output
+    buffer of one message's capacity: the first transforms, the second gets MSG_NO_ROOM."""
+    from c1_message import c1_message_bytes
+
+    msg = c1_message_bytes()
+    path = tmp_path / "msg.bin"
+    path.write_bytes(msg)
+    got = _run_harness(tmp_path, "gpumsg", str(path))
+    assert got["gpumsg_init"] == (0, "-")
+    assert got["gpumsg_xform_st"] == (0, "-") and got["gpumsg_xform_off1"] == (len(msg), "-")
+    assert got["gpumsg_xform_len"] == (2 * len(msg), "-") and got["gpumsg_xform_same"] == (1, "-")
+    assert got["gpumsg_xform_room0"] == (0, "-") and got["gpumsg_xform_room1"] == (1 << 12, "-")
