@@ -599,7 +599,7 @@ int ambrycrc_init(int device) {
     const long x = strtol(v, &end, 10);
     if (end != v && *end == '\0' && x >= 0 && x < 1000 && variant_supported((int)x)) c->variant = (int)x;
   }
-  if (const char* v = getenv("AMBRYCRC_REGION")) c->region_mode = strcmp(v, "0") != 0;
+  if (const char* v = getenv("AMBRYCRC_REGION")) c->region_mode = strcmp(v, "0") == 0 ? 0 : strcmp(v, "2") == 0 ? 2 : 1;
   if (const char* v = getenv("AMBRYCRC_REGION_MAX_PER_MESSAGE")) {  // A/B: the region-mode cut-off
     char* end = nullptr;
     const unsigned long long x = strtoull(v, &end, 10);
@@ -853,14 +853,19 @@ int ambrycrc_set_variant(int device, int variant) {
 int ambrycrc_set_region_mode(int device, int enable) {
   DevCtx* c = ctx_for(device);
   if (!c) return AMBRYCRC_ENOINIT;
-  if (enable != 0 && enable != 1) return AMBRYCRC_EINVAL;
-  c->region_mode = enable != 0;
+  if (enable < 0 || enable > 2) return AMBRYCRC_EINVAL;
+  c->region_mode = enable;
   return AMBRYCRC_OK;
 }
 
 int ambrycrc_get_region_mode(int device) {
   DevCtx* c = ctx_for(device);
-  return c ? (c->region_mode ? 1 : 0) : AMBRYCRC_ENOINIT;
+  return c ? c->region_mode : AMBRYCRC_ENOINIT;
+}
+
+int ambrycrc_last_message_mode(int device) {
+  DevCtx* c = ctx_for(device);
+  return c ? c->last_msg_mode.load() : AMBRYCRC_ENOINIT;
 }
 
 int ambrycrc_get_variant(int device) {
@@ -952,7 +957,7 @@ int ambrycrc_debug_readbw_dev(const uint8_t* d_base, uint64_t nbytes, uint32_t* 
 size_t ambrycrc_messages_workspace_bytes(size_t m) {
   // job arrays, then the batch workspace of job mode or the run sums of region mode (a region of
   // up to kRegionMaxPerMessage bytes per message: region / 16 bytes + two super-blocks' slack)
-  const size_t region = m * (kRegionMaxPerMessage / 16) + 2048;
+  const size_t region = m * (kRegionMaxPerMessage / 16) + 2048 + 512 + 4 * m;
   return msg_jobs_bytes(m) + std::max(ws_need((size_t)kMsgSlots * m), region);
 }
 
@@ -971,8 +976,9 @@ size_t msg_jobs_bytes(size_t m) {
 int enqueue_messages(DevCtx* c, const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off, size_t m,
                      uint32_t* d_status, uint64_t* d_msg_end, void* d_ws, size_t ws_bytes, hipStream_t stream) {
   const bool region = c->region_mode && region_len > 0 && region_len <= c->region_max * (uint64_t)m &&
-                      msg_jobs_bytes(m) + region_ws_bytes(d_region, region_len) <= ws_bytes;
+                      msg_jobs_bytes(m) + region_ws_bytes(d_region, region_len, m) <= ws_bytes;
   MsgStage st;
+  c->last_msg_mode.store(region ? c->region_mode : 0);
   if (!region) {
     const int rc = enqueue_messages_parse(c, d_region, region_len, d_msg_off, m, d_status, d_msg_end, d_ws, stream, &st);
     return rc ? rc : enqueue_messages_check(c, st, stream);
@@ -998,8 +1004,18 @@ int enqueue_messages(DevCtx* c, const uint8_t* d_region, uint64_t region_len, co
   r.nsb = region_nsb(d_region, region_len);
   r.rk = static_cast<uint32_t*>(st.batch_ws);
   r.img = c->d_img;
-  if (launch_region_runs(r, c->grid, stream) != hipSuccess) return AMBRYCRC_EHIP;
-  return hip_err(launch_region_msg(st.a, r, c->num_cu, stream));
+  if (c->region_mode == 2) {  // the two-pass form (A/B): runs kernel, then one thread per message
+    if (launch_region_runs(r, c->grid, stream) != hipSuccess) return AMBRYCRC_EHIP;
+    return hip_err(launch_region_msg(st.a, r, c->num_cu, stream));
+  }
+  FusedArgs f;
+  f.a = st.a;
+  f.g = r;
+  f.ngroups = (r.nsb + 3) / 4;
+  f.ctl = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(st.batch_ws) + region_rk_bytes(d_region, region_len));
+  f.defer = f.ctl + 64;
+  if (hipMemsetAsync(f.ctl, 0, 8, stream) != hipSuccess) return AMBRYCRC_EHIP;
+  return hip_err(launch_region_fused(f, c->num_cu, stream));
 }
 
 int enqueue_messages_parse(DevCtx* c, const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off,
@@ -1137,7 +1153,7 @@ int ambrycrc_verify_messages_dev(const uint8_t* d_region, uint64_t region_len, c
   // The library's own workspace also covers region mode past the default per-message size
   // (AMBRYCRC_REGION_MAX_PER_MESSAGE, for A/B runs); a caller's is used as sized.
   if (!d_ws && c->region_mode && region_len <= c->region_max * (uint64_t)m)
-    need = std::max(need, msg_jobs_bytes(m) + region_ws_bytes(d_region, region_len));
+    need = std::max(need, msg_jobs_bytes(m) + region_ws_bytes(d_region, region_len, m));
   const int rc = lease.acquire(c, stream, &d_ws, ws_bytes, need);
   if (rc) return rc;
   return enqueue_messages(c, d_region, region_len, d_msg_off, m, d_status, d_msg_end, d_ws,

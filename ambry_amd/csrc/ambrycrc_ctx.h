@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -76,7 +77,11 @@ struct DevCtx {
   int variant = AMBRY_DEFAULT_VARIANT;  // (A/B builds: -DAMBRY_DEFAULT_VARIANT=...)
   // Message verify of regions of at most kRegionMaxPerMessage bytes per message: region mode
   // (region_runs_kernel + region_msg_kernel) instead of jobs through the batch engine.
-  bool region_mode = true;
+  // 1: one pass (region_fused_kernel + region_tail_kernel), 2: two passes (region_runs_kernel +
+  // region_msg_kernel, kept for A/B), 0: off.
+  int region_mode = 1;
+  // The form the last message verify on this device took (ambrycrc_last_message_mode).
+  std::atomic<int> last_msg_mode{-1};
   uint64_t region_max = kRegionMaxPerMessage;  // region bytes per message up to which it applies
   // Sweep rounds of at most this many bytes (SweepArgs::window); 0 = one round.
   uint64_t window = 32ull << 30;

@@ -136,8 +136,13 @@ inline uint64_t region_nsb(const uint8_t* region, uint64_t len) {
   const uint64_t b = reinterpret_cast<uintptr_t>(region) & ~uint64_t(63);
   return (reinterpret_cast<uintptr_t>(region) + len - b + kSuperBlock - 1) / kSuperBlock;
 }
-inline size_t region_ws_bytes(const uint8_t* region, uint64_t len) {
+// Run sums (rk), then the one-pass kernels' control words and deferred list (FusedArgs ctl, defer)
+// for m messages.
+inline size_t region_rk_bytes(const uint8_t* region, uint64_t len) {
   return (size_t)((kRunPad + region_nsb(region, len) * 64 + 256) * 4 + 255) & ~size_t(255);
+}
+inline size_t region_ws_bytes(const uint8_t* region, uint64_t len, uint64_t m) {
+  return region_rk_bytes(region, len) + ((256 + 4 * m + 255) & ~size_t(255));
 }
 hipError_t launch_region_runs(const RegionArgs& a, int grid, hipStream_t s);
 
@@ -288,6 +293,26 @@ hipError_t launch_msg_parse(const MsgArgs& a, hipStream_t s);
 // Region mode, pass 2: parse, record CRCs from the run sums, status (a.job_* / expected / crc unused).
 hipError_t launch_region_msg(const MsgArgs& a, const RegionArgs& g, int num_cu, hipStream_t s);
 hipError_t launch_msg_reduce(const MsgArgs& a, hipStream_t s);
+
+// Region mode in one pass: region_fused_kernel, one workgroup per CU over a
+// contiguous share of 16 KiB groups (4 super-blocks). Its streaming waves hash the share into run
+// sums (as region_runs_kernel); its processor waves take the messages whose headers lie in the
+// share, 64 at a time, as soon as the share's run sums cover them, while the bytes are still in
+// the caches. Messages that run past the share (or start before it) are deferred to
+// region_tail_kernel, which also redoes every message when the offsets turn out unsorted (each CU
+// finds its messages by binary search). ctl[0]: unsorted flag, ctl[1]: deferred count (zeroed
+// before the launch); defer[m]: deferred message indices.
+struct FusedArgs {
+  MsgArgs a;
+  RegionArgs g;
+  uint64_t ngroups;  // 16 KiB groups over the region: ceil(nsb / 4)
+  uint32_t* ctl;
+  uint32_t* defer;
+};
+constexpr uint64_t kGroupBytes = 4 * kSuperBlock;
+constexpr int kFusedProc = AMBRY_FUSED_PROC;        // processor waves per workgroup
+constexpr int kFusedStreamers = 16 - kFusedProc;    // streaming waves
+hipError_t launch_region_fused(const FusedArgs& f, int num_cu, hipStream_t s);
 
 hipError_t launch_plan(const PlanArgs& a, hipStream_t s);
 // grid: workgroups of the persistent sweep; num_cu: the device's CUs (the A/B split group kernel

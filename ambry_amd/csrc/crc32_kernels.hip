@@ -30,6 +30,8 @@
 #include "crc32_gf2.h"
 #include "crc32_layout.h"
 #include "crc32_kernels.h"
+#include "crc_img.h"
+#include "region_proc.h"
 
 // A/B knob: s_setprio 3 around the streamed group path's loads, as the wave-mode body has it.
 
@@ -1633,6 +1635,213 @@ __global__ __launch_bounds__(1024) void region_runs_kernel(RegionArgs a) {
 hipError_t launch_region_runs(const RegionArgs& a, int grid, hipStream_t s) {
   if (a.nsb == 0) return hipSuccess;
   hipLaunchKernelGGL(region_runs_kernel, dim3(grid), dim3(1024), 0, s, a);
+  return hipGetLastError();
+}
+
+// ---- region mode in one pass: region_fused_kernel (FusedArgs, crc32_kernels.h) ----
+// Workgroup b (one per CU) owns groups [G0, G1) of 16 KiB (4 super-blocks). Streaming wave v <
+// kFusedStreamers takes groups G0 + v, G0 + v + S, ... (S = kFusedStreamers): the CU's frontier
+// advances S groups at a time, each wave's 4 super-blocks hashed as region_runs_kernel does them,
+// the next 4 in flight, the 256 run sums stored as one 1 KiB wave store. At the top of each group
+// the wave waits for all its memory operations (the previous group's store included) and publishes
+// how many of its groups are complete in LDS (done[v]).
+// Processor wave p takes 64-message batches p, p + kFusedProc, ... of the CU's messages -- those
+// whose offsets lie in the share, found by a 64-way search of the sorted offsets -- waiting on the
+// frontier (the longest complete prefix of the share's groups) first until the batch's headers are
+// streamed, then until its messages' ends are; then region::process_message. A message that
+// starts before the share or ends past it goes to the deferred list for region_tail_kernel.
+// Offsets out of order anywhere set ctl[0], and the tail kernel then redoes every message.
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t w = __shfl_xor(v, o);
+    v = w > v ? w : v;
+  }
+  return v;
+}
+
+// Base-relative position of message i's start (past the region: its end).
+__device__ __forceinline__ uint64_t msg_pos(const FusedArgs& f, uint64_t i) {
+  const uint64_t o = f.a.msg_off[i];
+  return f.g.reg0 + (o < f.a.region_len ? o : f.a.region_len);
+}
+
+// Smallest i in [0, m] with msg_pos(i) >= key (sorted offsets), by 64-way probes; every lane
+// gets it. Unsorted offsets give some index in [0, m] (the tail kernel redoes them all).
+__device__ uint64_t lower_bound_wave(const FusedArgs& f, uint64_t key, uint32_t lane) {
+  uint64_t lo = 0, hi = f.a.m;  // answer in [lo, hi]
+  while (hi - lo > 64) {
+    const uint64_t n = hi - lo;
+    const uint64_t q = lo + n * (lane + 1) / 65;  // lo <= q < hi, increasing with lane
+    const uint64_t ball = __ballot(msg_pos(f, q) >= key);
+    if (ball == 0) {
+      lo = lo + n * 64 / 65 + 1;
+    } else {
+      const uint32_t L = (uint32_t)__builtin_ctzll(ball);
+      const uint64_t qL = lo + n * (L + 1) / 65;
+      const uint64_t qP = L ? lo + n * L / 65 : lo;
+      hi = qL;
+      lo = L ? qP + 1 : lo;
+    }
+  }
+  const uint64_t i = lo + lane;
+  const uint64_t ball = __ballot(i < hi && msg_pos(f, i) < key);
+  return lo + (uint64_t)__popcll(ball);
+}
+
+__global__ __launch_bounds__(1024) void region_fused_kernel(FusedArgs f) {
+  __shared__ uint32_t tbl[1024];
+  __shared__ uint32_t nib[region::kSets * region::kNibWords];
+  __shared__ uint32_t done[16];
+  {  // LDS-DMA of the slice tables (the streamers'), then the processors' compact tables and nibble sets
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (uint32_t c = wv; c < kSliceBytes / 1024; c += nw)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(reinterpret_cast<const uint8_t*>(f.g.img) + c * 1024 +
+                                                          lane * 16),
+          (__attribute__((address_space(3))) void*)(reinterpret_cast<uint8_t*>(g_lds_runs) + c * 1024), 16, 0, 0);
+    {
+      const uint32_t i = threadIdx.x, j = i >> 8, b = i & 255u;
+      tbl[i] = f.g.img[(((j >> 1) << 16) | (b << 8) | ((j & 1) << 7)) >> 2];
+    }
+    region::stage_nib(nib, f.g.img);
+    if (threadIdx.x < 16) done[threadIdx.x] = 0;
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+  }
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t v = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t G0 = f.ngroups * blockIdx.x / gridDim.x, G1 = f.ngroups * (blockIdx.x + 1) / gridDim.x;
+  const RegionArgs& a = f.g;
+  if (v < (uint32_t)kFusedStreamers) {
+    // ---- streaming wave
+    const LaneConst k = make_lane_const(lane);
+    uint32_t* buf = g_lds_runs + kSliceBytes / 4 + v * (kRunsBufBytes / 4);
+    const uint32_t slot = 16u * (lane & 3u) + (lane >> 2);
+    const uint64_t mine = G1 - G0 > v ? (G1 - G0 - v + kFusedStreamers - 1) / kFusedStreamers : 0;
+    auto hash = [&](uint64_t sb, uint32_t u, u32x4 (&cur)[4]) {
+      region_sb_zero(a, sb, lane, cur);
+      quad_transpose_asm(cur);
+      buf[64u * u + slot] = run_crc<4, 1>(cur, k, 0u);
+    };
+    if (mine) {
+      u32x4 b0[4], b1[4], b2[4], b3[4];
+      uint64_t g = G0 + v;
+      region_sb_load(a, 4 * g, lane, b0);
+      region_sb_load(a, 4 * g + 1, lane, b1);
+      region_sb_load(a, 4 * g + 2, lane, b2);
+      region_sb_load(a, 4 * g + 3, lane, b3);
+      for (uint64_t j = 0; j < mine; ++j, g += kFusedStreamers) {
+        if (j) {  // the previous group's store has completed: publish it
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __hip_atomic_store(&done[v], (uint32_t)j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        const uint64_t nx = j + 1 < mine ? g + kFusedStreamers : g;  // the last group re-reads itself
+        hash(4 * g, 0, b0);
+        __builtin_amdgcn_s_setprio(3);
+        region_sb_load(a, 4 * nx, lane, b0);
+        __builtin_amdgcn_s_setprio(0);
+        hash(4 * g + 1, 1, b1);
+        __builtin_amdgcn_s_setprio(3);
+        region_sb_load(a, 4 * nx + 1, lane, b1);
+        __builtin_amdgcn_s_setprio(0);
+        hash(4 * g + 2, 2, b2);
+        __builtin_amdgcn_s_setprio(3);
+        region_sb_load(a, 4 * nx + 2, lane, b2);
+        __builtin_amdgcn_s_setprio(0);
+        hash(4 * g + 3, 3, b3);
+        __builtin_amdgcn_s_setprio(3);
+        region_sb_load(a, 4 * nx + 3, lane, b3);
+        __builtin_amdgcn_s_setprio(0);
+        const u32x4 sums = *reinterpret_cast<const u32x4*>(buf + 4u * lane);
+        *(reinterpret_cast<u32x4*>(a.rk + kRunPad + g * 256) + lane) = sums;
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __hip_atomic_store(&done[v], (uint32_t)mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return;
+  }
+  // ---- processor wave
+  const uint32_t p = v - (uint32_t)kFusedStreamers;
+  const uint64_t s_lo = G0 * kGroupBytes, s_hi = G1 * kGroupBytes;  // the share, base-relative
+  {  // this wave's slice of the global sortedness check
+    const uint64_t waves = (uint64_t)gridDim.x * kFusedProc, w = (uint64_t)blockIdx.x * kFusedProc + p;
+    const uint64_t c0 = f.a.m * w / waves, c1 = f.a.m * (w + 1) / waves;
+    bool bad = false;
+    for (uint64_t i = c0 + lane; i < c1; i += 64)
+      if (i + 1 < f.a.m && f.a.msg_off[i] > f.a.msg_off[i + 1]) bad = true;
+    if (__ballot(bad) && lane == 0) atomicOr(f.ctl, 1u);
+  }
+  const uint64_t M0 = blockIdx.x == 0 ? 0 : lower_bound_wave(f, s_lo, lane);
+  const uint64_t M1 = blockIdx.x + 1 == gridDim.x ? f.a.m : lower_bound_wave(f, s_hi, lane);
+  // frontier: base-relative end of the longest complete prefix of the share's groups
+  auto frontier = [&]() -> uint64_t {
+    uint64_t q = ~0ull;
+    if (lane < (uint32_t)kFusedStreamers)
+      q = lane + (uint64_t)kFusedStreamers *
+                     __hip_atomic_load(&done[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const uint64_t w = __shfl_xor(q, o);
+      q = w < q ? w : q;
+    }
+    return G0 * kGroupBytes + (q < G1 - G0 ? q : G1 - G0) * kGroupBytes;
+  };
+  auto wait_for = [&](uint64_t target) {
+    if (target > s_hi) target = s_hi;
+    while (frontier() < target) __builtin_amdgcn_s_sleep(8);
+    asm volatile("" ::: "memory");  // no run-sum load above the poll
+  };
+  for (uint64_t b = M0 + 64 * (uint64_t)p; b < M1; b += 64 * (uint64_t)kFusedProc) {
+    const uint64_t i = b + lane;
+    bool have = i < M1;
+    const uint64_t pos = have ? msg_pos(f, i) : 0;
+    wait_for(wave_max_u64(have ? pos + 128 : 0));  // the batch's headers streamed past
+    uint64_t end = 0;
+    if (have) {
+      const uint64_t off = f.a.msg_off[i];
+      const bool in_region = off <= f.a.region_len;
+      const uint64_t rem = in_region ? f.a.region_len - off : 0;
+      end = header_end(load_header(f.a.region + (in_region ? off : 0), rem), rem);
+      if (end && (pos < s_lo || pos + end > s_hi)) {  // runs past the share: the tail kernel's
+        const uint32_t at = atomicAdd(f.ctl + 1, 1u);
+        if (at < f.a.m) f.defer[at] = (uint32_t)i;  // (unsorted offsets may defer more: ctl[0] covers them)
+        have = false;
+      }
+    }
+    wait_for(wave_max_u64(have && end ? pos + end : 0));
+    region::process_message(f.a, f.g, tbl, nib, have, i, lane);
+  }
+}
+
+// The deferred messages (or, with ctl[0] set, every message) once all run sums exist: one lane
+// per message, 64 per wave, grid-stride over the list.
+__global__ __launch_bounds__(256) void region_tail_kernel(FusedArgs f) {
+  const bool all = *f.ctl != 0;
+  const uint64_t n = all ? f.a.m : f.ctl[1];
+  if (n == 0) return;
+  __shared__ uint32_t tbl[1024];
+  __shared__ uint32_t nib[region::kSets * region::kNibWords];
+  stage_slice_tables(tbl, f.g.img);
+  region::stage_nib(nib, f.g.img);
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  for (uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); 64 * w < n; w += waves) {
+    const uint64_t j = 64 * w + lane;
+    const bool have = j < n;
+    const uint64_t i = have ? (all ? j : f.defer[j]) : 0;
+    region::process_message(f.a, f.g, tbl, nib, have, i, lane);
+  }
+}
+
+hipError_t launch_region_fused(const FusedArgs& f, int num_cu, hipStream_t s) {
+  if (f.a.m == 0) return hipSuccess;
+  if (f.ngroups) hipLaunchKernelGGL(region_fused_kernel, dim3((uint32_t)num_cu), dim3(1024), 0, s, f);
+  else if (hipMemsetAsync(f.ctl, 0xFF, 4, s) != hipSuccess) return hipGetLastError();  // empty region: all to the tail
+  uint64_t blocks = (f.a.m + 255) / 256;
+  if (blocks > (uint64_t)num_cu * 2) blocks = (uint64_t)num_cu * 2;
+  hipLaunchKernelGGL(region_tail_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, f);
   return hipGetLastError();
 }
 

@@ -1,0 +1,182 @@
+// region_proc.h -- the message processors of region mode: one lane per message,
+// a wave per 64 messages. A lane parses its message (msg_parse.h, properties read from memory) and
+// assembles each record's CRC from the 64-B run sums (region_crc.h); a record longer than
+// kLongRuns runs is taken by the whole wave (record_crc_wave), so one 4 MiB blob in a region of
+// small messages costs the wave ~20 us instead of one lane ~1 ms.
+//
+// Used by region_fused_kernel (crc32_kernels.hip), whose processor waves run beside its streaming
+// waves and take the messages of their CU's share as the share's run sums complete, and by
+// region_tail_kernel, which takes the messages the fused kernel deferred (or all of them when the
+// offsets were not sorted) once every run sum exists.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "crc32_gf2.h"
+#include "crc_img.h"
+#include "msg_parse.h"
+#include "region_crc.h"
+
+namespace ambrycrc {
+namespace region {
+
+// Records of more runs than this go to the whole wave.
+constexpr int64_t kLongRuns = 512;
+
+// Lane (l - 2^LVL)'s v, for lanes with bit LVL set (others: 0): DPP row shifts, then row broadcasts.
+template <int LVL>
+__device__ __forceinline__ uint32_t left_partner(uint32_t v) {
+  if constexpr (LVL < 4) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x110 + (1 << LVL), 0xf, 0xf, false);
+  else if constexpr (LVL == 4) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);
+  else return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);
+}
+
+template <int LVL>
+__device__ __forceinline__ uint32_t wave_fold(uint32_t s, uint32_t c, uint32_t lane) {
+  const uint32_t sh = gf2_mul(left_partner<LVL>(s), c);
+  return (lane & (1u << LVL)) ? (s ^ sh) : s;
+}
+
+// zlib CRC-32 of the len bytes at offset pa from base, by the whole wave (every lane passes the
+// same pa, len; every lane gets the CRC). The runs of the record are cut into 64 equal lane slices
+// of 4*gs runs aligned to the record's last run (runs before the record count as zero, as in
+// record_crc); each lane folds its slice with record_crc's four Horner streams, then a DPP tree
+// merges the lanes with the shifts x^(8*256*gs*2^k) (gf2_mul by wave-uniform constants from the
+// image's x^(8*2^k) words), and the register at B1 is un-shifted to pb.
+__device__ __noinline__ uint32_t record_crc_wave(const uint32_t* __restrict__ t, const uint32_t* __restrict__ nib,
+                                                 const uint8_t* __restrict__ base, const uint32_t* __restrict__ rk,
+                                                 const uint32_t* __restrict__ img, uint64_t pa, uint64_t len,
+                                                 uint32_t lane) {
+  const uint64_t pb = pa + len;
+  const uint64_t A0 = pa & ~uint64_t(63), B1 = (pb + 63) & ~uint64_t(63);
+  const int64_t n = (int64_t)((B1 - A0) >> 6), k0 = (int64_t)(A0 >> 6);
+  const int lo = (int)(pa - A0), hi = pb - A0 < 64 ? (int)(pb - A0) : 64;
+  const int tin = hi - lo;
+  const bool tail_bytes = n >= 2 && (pb & 63u) != 0;
+  const int thi = (int)(pb - (B1 - 64));
+  const int64_t ng = (n + 3) >> 2;            // 4-run groups
+  const int64_t gs = (ng + 63) >> 6;          // groups per lane
+  const int64_t e0 = k0 + n - 256 * gs;       // virtual first run (<= k0)
+  const int64_t elast = k0 + n - 1;
+  u32x4 hw[4], tw[4];
+  load_run(base, A0, lo, hi, hw);
+  load_run(base, B1 - 64, 0, tail_bytes ? thi : 0, tw);
+  uint32_t H = hash_run(t, nib, hw, lo, hi, tin < 4 ? tin : 4);
+  if (tin < 4) H ^= 0xFFFFFFFFu >> (8 * tin);
+  const uint32_t T = tail_bytes ? hash_run(t, nib, tw, 0, thi, 0) : 0u;
+  // this lane's groups [g0, g0 + gs) counted from e0; groups wholly before k0 are zero
+  const int64_t g0 = (int64_t)lane * gs;
+  uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+  for (int64_t g = g0; g < g0 + gs; ++g) {
+    const int64_t eg = e0 + 4 * g;
+    u32x4 r = u32x4{0u, 0u, 0u, 0u};
+    if (eg + 3 >= k0) __builtin_memcpy(&r, rk + eg, 16);  // eg >= k0 - 3 >= -3: inside rk's pad
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t e = eg + q;
+      const uint32_t v = e < k0 ? 0u : e == k0 ? H : (e == elast && tail_bytes) ? T : r[q];
+      const uint32_t nv = nmul(nib, s0, kP256) ^ v;
+      s0 = s1;
+      s1 = s2;
+      s2 = s3;
+      s3 = nv;
+    }
+  }
+  uint32_t V = s3 ^ nmul(nib, s2, kP64) ^ nmul(nib, s1, kP128) ^ nmul(nib, nmul(nib, s0, kP64), kP128);
+  // lane slices are 256*gs bytes: level k shifts the left half by x^(8*256*gs*2^k)
+  uint32_t c = mul_xpow8_img(img, 0x80000000u, (uint64_t)256 * (uint64_t)gs);
+  V = wave_fold<0>(V, c, lane);
+  c = gf2_mul(c, c);
+  V = wave_fold<1>(V, c, lane);
+  c = gf2_mul(c, c);
+  V = wave_fold<2>(V, c, lane);
+  c = gf2_mul(c, c);
+  V = wave_fold<3>(V, c, lane);
+  c = gf2_mul(c, c);
+  V = wave_fold<4>(V, c, lane);
+  c = gf2_mul(c, c);
+  V = wave_fold<5>(V, c, lane);
+  V = __builtin_amdgcn_readlane(V, 63);
+  const uint32_t d = (uint32_t)(B1 - pb);
+#pragma unroll
+  for (uint32_t k = 0; k < kInvPowSets; ++k)
+    if (d & (1u << k)) V = nmul(nib, V, kInv0 + k);
+  return ~V;
+}
+
+// The message processor of one lane (message i when `have`), all run sums of its records
+// available: status and message end written. Long records are collected and done by the wave
+// after the per-lane ones, so every lane of the wave must call this (have = false for none).
+// t: compact slice-by-4 tables (stage_slice_tables), nib: stage_nib's sets; g.rk's run sums.
+__device__ __forceinline__ void process_message(const MsgArgs& a, const RegionArgs& g,
+                                                const uint32_t* __restrict__ t, const uint32_t* __restrict__ nib,
+                                                bool have, uint64_t i, uint32_t lane) {
+  const uint32_t* rk = g.rk + kRunPad;
+  uint32_t status = 0;
+  uint64_t end = 0, off = 0;
+  uint64_t jo[kMsgSlots] = {0, 0, 0, 0, 0}, jl[kMsgSlots] = {0, 0, 0, 0, 0};
+  uint32_t ex[kMsgSlots] = {0, 0, 0, 0, 0};
+  uint32_t longs = 0;  // record slots left to the wave
+  if (have) {
+    off = a.msg_off[i];
+    const bool in_region = off <= a.region_len;
+    const uint64_t rem = in_region ? a.region_len - off : 0;
+    const uint8_t* p = a.region + (in_region ? off : 0);
+    const HeaderWords hw = load_header(p, rem);
+    MsgParse r;
+    PropsFields pf;
+    bool pf_ok = false;
+    parse_message<false, false>(off, in_region, rem, p, hw, t, nullptr, 0, r, pf, pf_ok);
+    status = r.status;
+    end = r.end;
+#pragma unroll
+    for (int k = 0; k < kMsgSlots; ++k) {
+      jo[k] = r.jo[k];
+      jl[k] = r.jl[k];
+      ex[k] = r.ex[k];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kMsgSlots; ++k) {
+    if (!have || jl[k] == 0) continue;
+    const uint64_t pa = g.reg0 + jo[k];
+    const int64_t runs = (int64_t)((((pa + jl[k] + 63) & ~uint64_t(63)) - (pa & ~uint64_t(63))) >> 6);
+    if (runs > kLongRuns) {
+      longs |= 1u << k;
+      continue;
+    }
+    if (record_crc(t, nib, g.base, rk, pa, jl[k]) != ex[k]) status |= record_bit(k);
+  }
+  // the wave takes the long records one by one
+  for (;;) {
+    const uint64_t ball = __ballot(longs != 0);
+    if (ball == 0) break;
+    const uint32_t owner = (uint32_t)__builtin_ctzll(ball);
+    const uint32_t kk = (uint32_t)__builtin_ctz(__shfl(longs, (int)owner));
+    uint64_t rjo = 0, rjl = 0;
+#pragma unroll
+    for (int k = 0; k < kMsgSlots; ++k)
+      if ((uint32_t)k == kk) {
+        rjo = jo[k];
+        rjl = jl[k];
+      }
+    rjo = __shfl(rjo, (int)owner);
+    rjl = __shfl(rjl, (int)owner);
+    const uint32_t c = record_crc_wave(t, nib, g.base, rk, g.img, g.reg0 + rjo, rjl, lane);
+    if (lane == owner) {
+      uint32_t e = 0;
+#pragma unroll
+      for (int k = 0; k < kMsgSlots; ++k)
+        if ((uint32_t)k == kk) e = ex[k];
+      if (c != e) status |= record_bit((int)kk);
+      longs &= ~(1u << kk);
+    }
+  }
+  if (have) {
+    a.status[i] = status;
+    if (a.msg_end) a.msg_end[i] = end ? off + end : 0;
+  }
+}
+
+}  // namespace region
+}  // namespace ambrycrc

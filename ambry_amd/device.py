@@ -159,14 +159,21 @@ def get_variant(device: int = 0) -> int:
     return check(lib().ambrycrc_get_variant(device), "ambrycrc_get_variant")
 
 
-def set_region_mode(device: int, enable: bool) -> None:
-    """Message verify in region mode (one sweep of the region, record CRCs from 64-B run sums)
-    or as CRC jobs through the batch engine; ambrycrc_set_region_mode."""
-    check(lib().ambrycrc_set_region_mode(device, 1 if enable else 0), "ambrycrc_set_region_mode")
+def set_region_mode(device: int, mode) -> None:
+    """Message verify form (ambrycrc_set_region_mode): 1 / True = region mode in one pass (the
+    default), 2 = region mode in two passes (A/B), 0 / False = CRC jobs through the batch engine."""
+    m = int(mode) if not isinstance(mode, bool) else (1 if mode else 0)
+    check(lib().ambrycrc_set_region_mode(device, m), "ambrycrc_set_region_mode")
 
 
-def get_region_mode(device: int = 0) -> bool:
-    return bool(check(lib().ambrycrc_get_region_mode(device), "ambrycrc_get_region_mode"))
+def get_region_mode(device: int = 0) -> int:
+    return check(lib().ambrycrc_get_region_mode(device), "ambrycrc_get_region_mode")
+
+
+def last_message_mode(device: int = 0) -> int:
+    """The form the device's last message verify took: 0 jobs, 1 region one-pass, 2 region two-pass
+    (-1: none yet); ambrycrc_last_message_mode."""
+    return lib().ambrycrc_last_message_mode(device)
 
 
 def set_grid(device: int, workgroups: int) -> None:

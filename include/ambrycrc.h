@@ -488,13 +488,18 @@ int ambrycrc_range_checksums_host(const uint8_t* file, uint64_t file_len, const 
 int ambrycrc_set_variant(int device, int variant);
 int ambrycrc_get_variant(int device);
 /* Message verify (ambrycrc_verify_messages_dev / _host) of a region of at most 6 KiB per
- * message: region mode (1, the default; AMBRYCRC_REGION=0 in the environment at init turns it
- * off) sweeps the region once as contiguous memory, keeping the raw CRC of every 64-B run, and
- * assembles each record's CRC from the runs it covers, re-reading only the two runs its ends
- * cut; 0 = every record as a CRC job through the batch engine (plan, group phase, sweep). Same
- * status bits either way. */
+ * message: region mode sweeps the region once as contiguous memory, keeping the raw CRC of every
+ * 64-B run, and assembles each record's CRC from the runs it covers, re-reading only the two runs
+ * its ends cut. 1 (the default): one pass -- each CU's processor waves take the messages of its
+ * share of the region while its streaming waves are still sweeping it, so the message bytes are
+ * parsed from the caches; 2: two passes (the sweep, then one thread per message; A/B);
+ * 0: every record as a CRC job through the batch engine (plan, group phase, sweep).
+ * AMBRYCRC_REGION=0 / 2 in the environment at init selects 0 / 2. Same status bits every way.
+ * ambrycrc_last_message_mode: the form the device's last message verify took (0 / 1 / 2; -1
+ * before the first), for profiles that must say which kernels they timed. */
 int ambrycrc_set_region_mode(int device, int enable);
 int ambrycrc_get_region_mode(int device);
+int ambrycrc_last_message_mode(int device);
 /* Grid size of the persistent sweep kernel (workgroups; 0 = one per CU). */
 int ambrycrc_set_grid(int device, int workgroups);
 

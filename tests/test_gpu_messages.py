@@ -14,14 +14,18 @@ from test_message_format import MF, build_region
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["region", "jobs"])
+MODES = {"region": 1, "region2": 2, "jobs": 0}
+
+
+@pytest.fixture(autouse=True, params=list(MODES))
 def msg_mode(request, gpu):
-    """Every test runs in both message-verify modes: region mode (one sweep of the region, record
-    CRCs from 64-B run sums; engaged for regions of <= 6 KiB per message) and CRC jobs through the
-    batch engine."""
-    gpu.set_region_mode(0, request.param == "region")
+    """Every test runs in every message-verify form: region mode in one pass (the default: the
+    region swept once into 64-B run sums while each CU's processor waves take its messages),
+    region mode in two passes, and CRC jobs through the batch engine. Region mode engages for
+    regions of <= 6 KiB per message."""
+    gpu.set_region_mode(0, MODES[request.param])
     yield request.param
-    gpu.set_region_mode(0, True)
+    gpu.set_region_mode(0, 1)
 
 
 def run(gpu, region: bytes, offs, shift: int = 0):
@@ -304,3 +308,64 @@ def test_record_level_checks(gpu):
     st, end = run(gpu, bytes(region), offs)
     assert st == [want for _, want in cases]
     assert end == [o + len(m) for o, (m, _) in zip(offs, cases)]
+
+
+def _expect_mode(gpu, msg_mode, region_len, m):
+    if region_len <= 6144 * m:
+        assert gpu.last_message_mode(0) == MODES[msg_mode]
+    else:
+        assert gpu.last_message_mode(0) == 0
+
+
+def test_many_shares_boundary_messages(gpu, msg_mode):
+    """30,000 small messages (~90 MB): every CU share boundary cuts a message, which the one-pass
+    kernel defers to the tail kernel; status and ends bit-exact, and the call took the form asked."""
+    region, offs, expect = build_region(n=30000, seed=5, corrupt_frac=0.02, big_every=10**9)
+    st, end = run(gpu, region, offs, shift=7)
+    _expect_mode(gpu, msg_mode, len(region), len(offs))
+    assert st == [s for s, _ in expect]
+    assert end == [e for _, e in expect]
+
+
+def test_long_records_inside_region_mode(gpu, msg_mode):
+    """A region of small messages around long records: one 4 MiB blob (crossing many
+    CU shares: deferred, then taken by a whole wave in the tail kernel) and 48 KiB blobs (768 runs:
+    taken by the whole wave, inside a share in the one-pass kernel or deferred when they cross one),
+    corrupted and clean; region mode still engages (<= 6 KiB per message on average)."""
+    rng = np.random.default_rng(8)
+    msgs = []
+    for i in range(20000):
+        if i == 1500:
+            size = 4 << 20
+        elif i % 400 == 17:
+            size = 48 << 10
+        else:
+            size = int(rng.integers(0, 1500))
+        from datagen import stream_bytes
+
+        content = stream_bytes(i, 0, size).tobytes()
+        msgs.append(MF.put_message(MF.store_key("L%d" % i), MF.blob_properties_bytes(size), b"m" * (i % 30), content,
+                                   version=3))
+    offs = np.cumsum([0] + [len(x) for x in msgs[:-1]]).tolist()
+    region = bytearray(b"".join(msgs))
+    for i in (1500, 17, 417):  # flip a byte deep inside each long blob
+        region[offs[i] + len(msgs[i]) - 5000] ^= 0x10
+    region = bytes(region)
+    expect = [MF.verify_message(region, o) for o in offs]
+    assert len(region) <= 6144 * len(offs)
+    st, end = run(gpu, region, offs)
+    _expect_mode(gpu, msg_mode, len(region), len(offs))
+    assert st == [s for s, _ in expect]
+    assert end == [e for _, e in expect]
+    assert st[1500] == MF.BLOB_CRC and st[17] == MF.BLOB_CRC and st[817] == 0
+
+
+def test_unsorted_offsets_take_the_tail(gpu, msg_mode):
+    """Offsets in random order over a region large enough for every CU: the one-pass kernel finds
+    its messages by binary search of sorted offsets, sees they are not, and the tail kernel redoes
+    every message; results identical to the sorted call's, reordered."""
+    region, offs, expect = build_region(n=6000, seed=12, corrupt_frac=0.05, big_every=10**9)
+    perm = np.random.default_rng(2).permutation(len(offs))
+    st, end = run(gpu, region, [offs[j] for j in perm])
+    assert st == [expect[j][0] for j in perm]
+    assert end == [expect[j][1] for j in perm]

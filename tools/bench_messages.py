@@ -73,7 +73,7 @@ def gpu_region(mf, m, blob_bytes, reps, variant=None, host=False, mode="region")
     D.init(0)
     if variant is not None:
         D.set_variant(0, variant)
-    D.set_region_mode(0, mode == "region")
+    D.set_region_mode(0, {"region": 1, "region2": 2, "jobs": 0}[mode])
     tmpl = mf.put_message(mf.store_key("blob-00000000"), mf.blob_properties_bytes(blob_bytes), b"u" * 1000,
                           bytes(blob_bytes), version=3)
     L = len(tmpl)
@@ -126,7 +126,8 @@ def gpu_region(mf, m, blob_bytes, reps, variant=None, host=False, mode="region")
            "mode": mode if L <= int(os.environ.get("AMBRYCRC_REGION_MAX_PER_MESSAGE", "6144")) else
                    "jobs (region > cut-off per message)", "messages": m, "region_bytes": m * L,
            "ms_median": round(med, 4), "GiBps": round(m * L / (med / 1e3) / 2**30, 1),
-           "messages_per_s": round(m / (med / 1e3)), "parity": "clean=0, 1% injected flips flagged exactly"}
+           "messages_per_s": round(m / (med / 1e3)), "parity": "clean=0, 1% injected flips flagged exactly",
+           "mode_taken": {0: "jobs", 1: "region one-pass", 2: "region two-pass"}.get(D.last_message_mode(0))}
     if host and m * L <= (5 << 30):
         res["host"] = host_region_rate(D, region, base, m, L)
     return res
@@ -165,7 +166,7 @@ def main():
     ap.add_argument("--no-gpu", action="store_true")
     ap.add_argument("--variants", default="29")
     ap.add_argument("--cases", default="64k,4m,4k", help="subset of 64k,4m,4k,3k,2k,1k,100")
-    ap.add_argument("--modes", default="region", help="message-verify modes: region,jobs")
+    ap.add_argument("--modes", default="region", help="message-verify modes: region (one pass), region2, jobs")
     ap.add_argument("--host", action="store_true", help="also time the host-region path (regions <= 5 GiB)")
     args = ap.parse_args()
     mf = load_mf()
