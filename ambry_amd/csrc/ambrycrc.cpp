@@ -331,10 +331,10 @@ uint64_t batch_small_max(const DevCtx* c, size_t n) {
 // before it initialises out, and the CRC kernels read the copy.
 int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len, const uint32_t* crc_in,
                   uint32_t* out, size_t n, void* ws, hipStream_t s, uint32_t* exp_fill, uint8_t* copy_dst,
-                  const uint64_t* copy_off) {
+                  const uint64_t* copy_off, const uint32_t* gate) {
   if (n == 0) return AMBRYCRC_OK;
   PlanArgs p;
-  p.gate = nullptr;
+  p.gate = gate;
   p.off = off;
   p.len = len;
   p.crc_in = crc_in;
@@ -366,6 +366,8 @@ int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uin
   t.window = c->window;
   t.copy_dst = copy_dst;
   t.copy_off = copy_off;
+  t.gate = gate;
+  if (gate && !copy_dst) return AMBRYCRC_EINVAL;  // only the copy-through sweep checks the gate
   EventPair ev{nullptr, nullptr};
   if (c->timing) {
     std::lock_guard<std::mutex> g(c->ev_mu);
@@ -1020,10 +1022,11 @@ int enqueue_messages(DevCtx* c, const uint8_t* d_region, uint64_t region_len, co
 
 int enqueue_messages_parse(DevCtx* c, const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off,
                            size_t m, uint32_t* d_status, uint64_t* d_msg_end, void* d_ws, hipStream_t stream,
-                           MsgStage* st, const TransformArgs* desc) {
+                           MsgStage* st, const TransformArgs* desc, const uint32_t* gate) {
   const size_t j = (size_t)kMsgSlots * m;
   uint8_t* w = static_cast<uint8_t*>(d_ws);
   MsgArgs& a = st->a;
+  a.gate = gate;
   a.region = d_region;
   a.region_len = region_len;
   a.msg_off = d_msg_off;
@@ -1052,7 +1055,7 @@ int enqueue_messages_check(DevCtx* c, const MsgStage& st, hipStream_t stream, ui
   // copy-through runs the group-phase kernel whatever c's variant, so the stored CRCs of the records
   // it takes are read there exactly when the parse kernel left them to it (inline_max)
   const int rc = enqueue_batch(c, a.region, a.job_off, a.job_len, nullptr, st.crc, st.j, st.batch_ws, stream,
-                               a.inline_max ? a.expected : nullptr, copy_dst, copy_off);
+                               a.inline_max ? a.expected : nullptr, copy_dst, copy_off, copy_dst ? a.gate : nullptr);
   if (rc) return rc;
   return hip_err(launch_msg_reduce(a, stream));
 }

@@ -134,7 +134,7 @@ uint64_t batch_small_max(const DevCtx* c, size_t n);
 // copy_off: see SweepArgs (copy_dst set: the copy-through kernel, whatever c's variant).
 int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len, const uint32_t* crc_in,
                   uint32_t* out, size_t n, void* ws, hipStream_t s, uint32_t* exp_fill = nullptr,
-                  uint8_t* copy_dst = nullptr, const uint64_t* copy_off = nullptr);
+                  uint8_t* copy_dst = nullptr, const uint64_t* copy_off = nullptr, const uint32_t* gate = nullptr);
 
 // The device message-verify pipeline on `stream`: parse -> plan + sweep -> reduce (job mode), or
 // parse, region runs, region jobs -> reduce (region mode: c->region_mode, a region of at most
@@ -155,7 +155,7 @@ struct MsgStage {
 };
 int enqueue_messages_parse(DevCtx* c, const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off,
                            size_t m, uint32_t* d_status, uint64_t* d_msg_end, void* d_ws, hipStream_t stream,
-                           MsgStage* st, const TransformArgs* desc = nullptr);
+                           MsgStage* st, const TransformArgs* desc = nullptr, const uint32_t* gate = nullptr);
 int enqueue_messages_check(DevCtx* c, const MsgStage& st, hipStream_t stream, uint8_t* copy_dst = nullptr,
                            const uint64_t* copy_off = nullptr);
 // The PUT serialization pipeline (layout -> copy -> plan + CRC -> seal); d_ws holds at least

@@ -184,6 +184,14 @@ size_t ambrycrc_transform_workspace_bytes(size_t m) {
          std::max(ambrycrc_messages_workspace_bytes(m), ambrycrc_serialize_puts_workspace_bytes(m));
 }
 
+namespace {
+// The one-pass fast path keeps its run sums, control words and deferred list where the general
+// path's verify / serializer workspace goes (it runs first, on the same stream).
+size_t transform_fast_bytes(const uint8_t* d_region, uint64_t region_len, size_t m) {
+  return region_ws_bytes(d_region, region_len, m);
+}
+}  // namespace
+
 uint64_t ambrycrc_transform_out_bound(uint64_t region_len, size_t m) {
   static_assert(AMBRYCRC_TRANSFORM_GROWTH_MAX == (40 - 34) + kPropsAppendixMax + (13 - 10), "growth bound");
   const uint64_t g = (uint64_t)AMBRYCRC_TRANSFORM_GROWTH_MAX;
@@ -201,9 +209,16 @@ int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len
     return AMBRYCRC_EINVAL;
   DevCtx* c = ctx_current();
   if (!c) return AMBRYCRC_ENOINIT;
+  // Fast path (FusedArgs::out): header V3 out, region mode on, a region to sweep, and workspace room
+  // for the run sums (the library's own workspace is sized for them; a caller's as given).
+  const size_t base_need = ambrycrc_transform_workspace_bytes(m);
+  const size_t fast_need = transform_own_bytes(m) + ws_need(m) + transform_fast_bytes(d_region, region_len, m);
+  const bool want_fast = header_version == 3 && c->region_mode == 1 && region_len > 0;
+  const size_t need = want_fast && !d_ws ? std::max(base_need, fast_need) : base_need;
   WsLease lease;
-  int rc = lease.acquire(c, stream, &d_ws, ws_bytes, ambrycrc_transform_workspace_bytes(m));
+  int rc = lease.acquire(c, stream, &d_ws, ws_bytes, need);
   if (rc) return rc;
+  const bool fast = want_fast && (ws_bytes ? ws_bytes : need) >= fast_need;
   // workspace: desc[m] | scan scratch (uint32 per message) | in_crc[4m] | xstatus[m] | fail |
   //            copy_off[5m] | pfix[m] | plan workspace for the m lengths | the verify pipeline's, then the
   //            serializer's (one after the other on the stream)
@@ -225,6 +240,7 @@ int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len
   t.in_crc = scan_out + m;
   uint32_t* xstatus = t.in_crc + 4 * m;
   uint32_t* fail = xstatus + m;
+  uint32_t* xfail = fail + 1;  // set: the fast path did not take the batch (transform_head_bytes' slack)
   uint64_t* copy_off = reinterpret_cast<uint64_t*>(w + transform_head_bytes(m));
   t.pfix = reinterpret_cast<PropsFix*>(copy_off + (size_t)kPutSlots * m);
   t.img = c->d_img;
@@ -254,12 +270,53 @@ int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len
   // before the CRCs are known; the verify's CRC batch is the copy-through kernel. A message that
   // then fails verification sets `fail`, and the fallback pass below rebuilds the output exactly as
   // the three-pass form did (verify bits first, then the transform's own, then the placement).
-  if (hipMemsetAsync(fail, 0, sizeof(uint32_t), stream) != hipSuccess) return AMBRYCRC_EHIP;
+  if (hipMemsetAsync(fail, 0, 2 * sizeof(uint32_t), stream) != hipSuccess) return AMBRYCRC_EHIP;  // fail, xfail
+  const uint32_t* general = nullptr;  // the general path's gate (null: it always runs)
+  if (fast) {
+    // One pass (region_fused_kernel's copy form, then region_tail_kernel): verify every message
+    // while copying the region into the output; when every message qualifies the headers are
+    // patched and the general path below is skipped by its gate (*xfail == 0).
+    FusedArgs f;
+    f.a.region = d_region;
+    f.a.region_len = region_len;
+    f.a.msg_off = d_msg_off;
+    f.a.m = m;
+    f.a.img = c->d_img;
+    f.a.status = d_status;
+    f.a.msg_end = nullptr;
+    f.a.inline_max = 0;
+    const uintptr_t rp = reinterpret_cast<uintptr_t>(d_region);
+    f.g.base = d_region - (rp & 63u);
+    f.g.reg0 = rp & 63u;
+    f.g.reg_end = f.g.reg0 + region_len;
+    f.g.lo16 = f.g.reg0 & ~uint64_t(15);
+    f.g.hi16 = (f.g.reg_end - 1) & ~uint64_t(15);
+    f.g.nsb = region_nsb(d_region, region_len);
+    f.g.rk = reinterpret_cast<uint32_t*>(shared);
+    f.g.img = c->d_img;
+    f.ngroups = (f.g.nsb + 3) / 4;
+    f.ctl = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(shared) + region_rk_bytes(d_region, region_len));
+    f.defer = f.ctl + 64;
+    f.out = d_out;
+    f.out_cap = out_cap;
+    f.out_off = d_out_off;
+    f.out_len = d_out_len;
+    f.life = d_life_version;
+    f.xstatus = xstatus;
+    f.xfail = xfail;
+    if (hipMemsetAsync(f.ctl, 0, 8, stream) != hipSuccess) return AMBRYCRC_EHIP;
+    if (launch_region_fused(f, c->num_cu, stream) != hipSuccess) return AMBRYCRC_EHIP;
+    general = xfail;
+  }
+  p.gate = general;
+  t.gate = general;
+  t.gate_when = 1;
   MsgStage ms;
   t.xstatus = xstatus;
   t.copy_off = copy_off;
   // the parse kernel describes each message as it parses it (transform_desc_kernel fused)
-  rc = enqueue_messages_parse(c, d_region, region_len, d_msg_off, m, d_status, nullptr, shared, stream, &ms, &t);
+  rc = enqueue_messages_parse(c, d_region, region_len, d_msg_off, m, d_status, nullptr, shared, stream, &ms, &t,
+                              general);
   if (rc) return rc;
   t.job_off = ms.a.job_off;
   if (launch_plan(p, stream) != hipSuccess) return AMBRYCRC_EHIP;
@@ -268,7 +325,7 @@ int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len
   rc = enqueue_messages_check(c, ms, stream, d_out, copy_off);
   if (rc) return rc;
   if (launch_transform_finish(t, stream) != hipSuccess) return AMBRYCRC_EHIP;
-  rc = enqueue_serialize(c, t.desc, m, d_region, d_region, d_out, nullptr, shared, stream, t.in_crc, true);
+  rc = enqueue_serialize(c, t.desc, m, d_region, d_region, d_out, nullptr, shared, stream, t.in_crc, true, general);
   if (rc) return rc;
   if (launch_props_fix(t, stream) != hipSuccess) return AMBRYCRC_EHIP;  // after the copy-through
   t.gate = fail;

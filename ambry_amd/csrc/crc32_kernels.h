@@ -68,6 +68,9 @@ struct SweepArgs {
   // field is read once for both its copy and its CRC. Null for every other launch.
   uint8_t* copy_dst;
   const uint64_t* copy_off;  // kCopySkip: chunk c is read (CRC'd) but not copied
+  // Run only when *gate != 0 (null: always): the transform's general path behind its one-pass
+  // fast path (ambrycrc_put.cpp).
+  const uint32_t* gate = nullptr;
 };
 constexpr uint64_t kCopySkip = ~0ull;
 
@@ -164,6 +167,7 @@ struct MsgArgs {
   uint64_t* msg_end;        // [m] or null
   uint64_t inline_max;      // records of 1..inline_max bytes: stored CRC read by the sweep's
                             // group phase (SweepArgs::exp_fill), not by the parse kernel
+  const uint32_t* gate = nullptr;  // parse / reduce kernels run only when *gate != 0 (null: always)
 };
 
 // CRC-trailered records (index segment files, log segment headers, user metadata, ...):
@@ -308,11 +312,24 @@ struct FusedArgs {
   uint64_t ngroups;  // 16 KiB groups over the region: ceil(nsb / 4)
   uint32_t* ctl;
   uint32_t* defer;
+  // Transform fast path (launch_region_fused with copy): when every message is a clean PUT stored
+  // at header V3 with canonical V5 properties and a Blob_Format_V3 record, back to back from
+  // msg_off[0], the output is the region from msg_off[0] on with each header's life version and
+  // CRC rewritten. The streamers copy every byte they stream to out + (position - msg_off[0]);
+  // the processors patch the headers and write out_off / out_len / xstatus (0), or set *xfail when
+  // a message does not qualify -- the transform's general path then runs (gated on *xfail).
+  uint8_t* out = nullptr;
+  uint64_t out_cap = 0;
+  uint64_t* out_off = nullptr;  // nullable
+  uint64_t* out_len = nullptr;
+  const int16_t* life = nullptr;  // nullable: the stored life versions
+  uint32_t* xstatus = nullptr;
+  uint32_t* xfail = nullptr;
 };
 constexpr uint64_t kGroupBytes = 4 * kSuperBlock;
 constexpr int kFusedProc = AMBRY_FUSED_PROC;        // processor waves per workgroup
 constexpr int kFusedStreamers = 16 - kFusedProc;    // streaming waves
-hipError_t launch_region_fused(const FusedArgs& f, int num_cu, hipStream_t s);
+hipError_t launch_region_fused(const FusedArgs& f, int num_cu, hipStream_t s);  // f.out set: the copy form
 
 hipError_t launch_plan(const PlanArgs& a, hipStream_t s);
 // grid: workgroups of the persistent sweep; num_cu: the device's CUs (the A/B split group kernel

@@ -1088,6 +1088,7 @@ __device__ __forceinline__ uint64_t snap_cut(uint64_t cs, uint64_t len, uint64_t
 template <bool T4, bool GROUP, int DIAG = 0, bool COPY = false>
 __global__ __launch_bounds__(1024) void crc32_sweep_kernel(SweepArgs a) {
   static_assert(!COPY || (T4 && DIAG == 0), "copy-through is built for the 64-B-run sweep only");
+  if (COPY && a.gate && *a.gate == 0) return;  // the transform's gated general path (uniform)
   // Shares are wave-major over workgroups (share i -> wave i / gridDim.x of workgroup
   // i % gridDim.x), so when a batch has fewer shares than waves they spread over every
   // CU. A share is at least kMinShare bytes: a lone large chunk is cut into ~total/16 KiB
@@ -1689,6 +1690,7 @@ __device__ uint64_t lower_bound_wave(const FusedArgs& f, uint64_t key, uint32_t 
   return lo + (uint64_t)__popcll(ball);
 }
 
+template <bool COPY>
 __global__ __launch_bounds__(1024) void region_fused_kernel(FusedArgs f) {
   __shared__ uint32_t tbl[1024];
   __shared__ uint32_t nib[region::kSets * region::kNibWords];
@@ -1719,7 +1721,27 @@ __global__ __launch_bounds__(1024) void region_fused_kernel(FusedArgs f) {
     uint32_t* buf = g_lds_runs + kSliceBytes / 4 + v * (kRunsBufBytes / 4);
     const uint32_t slot = 16u * (lane & 3u) + (lane >> 2);
     const uint64_t mine = G1 - G0 > v ? (G1 - G0 - v + kFusedStreamers - 1) / kFusedStreamers : 0;
+    // COPY: out[0] is region byte msg_off[0] (base-relative `shift`); every piece holding region
+    // bytes is stored at its place, cut to [shift, shift + out_cap)
+    const uint64_t shift = COPY ? a.reg0 + f.a.msg_off[0] : 0;
+    auto copy = [&](uint64_t sb, const u32x4 (&cur)[4]) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint64_t p = sb * kSuperBlock + (uint64_t)kBlockBytes * q + 16u * lane;
+        if (p < a.lo16 || p > a.hi16 || p + 16 <= shift) continue;  // no region byte at or after out[0]
+        const uint64_t d0 = p >= shift ? p - shift : 0;               // its first output byte
+        if (d0 >= f.out_cap) continue;
+        if (p >= shift && d0 + 16 <= f.out_cap) {
+          st16u(f.out + (p - shift), cur[q]);
+        } else {
+#pragma unroll
+          for (int b = 0; b < 16; ++b)
+            if (p + b >= shift && p + b - shift < f.out_cap) st8g(f.out + (p + b - shift), cur[q][b >> 2] >> (8 * (b & 3)));
+        }
+      }
+    };
     auto hash = [&](uint64_t sb, uint32_t u, u32x4 (&cur)[4]) {
+      if constexpr (COPY) copy(sb, cur);
       region_sb_zero(a, sb, lane, cur);
       quad_transpose_asm(cur);
       buf[64u * u + slot] = run_crc<4, 1>(cur, k, 0u);
@@ -1810,16 +1832,24 @@ __global__ __launch_bounds__(1024) void region_fused_kernel(FusedArgs f) {
       }
     }
     wait_for(wave_max_u64(have && end ? pos + end : 0));
-    region::process_message(f.a, f.g, tbl, nib, have, i, lane);
+    uint32_t st;
+    uint64_t mend;
+    region::process_message(f.a, f.g, tbl, nib, have, i, lane, st, mend);
+    if constexpr (COPY) region::transform_fast(f, tbl, have, i, st, mend);
   }
 }
 
 // The deferred messages (or, with ctl[0] set, every message) once all run sums exist: one lane
 // per message, 64 per wave, grid-stride over the list.
+template <bool COPY>
 __global__ __launch_bounds__(256) void region_tail_kernel(FusedArgs f) {
   const bool all = *f.ctl != 0;
   const uint64_t n = all ? f.a.m : f.ctl[1];
   if (n == 0) return;
+  if (COPY && all) {  // offsets out of order: not the fast path's layout
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(f.xfail, 1u);
+    return;
+  }
   __shared__ uint32_t tbl[1024];
   __shared__ uint32_t nib[region::kSets * region::kNibWords];
   stage_slice_tables(tbl, f.g.img);
@@ -1831,17 +1861,26 @@ __global__ __launch_bounds__(256) void region_tail_kernel(FusedArgs f) {
     const uint64_t j = 64 * w + lane;
     const bool have = j < n;
     const uint64_t i = have ? (all ? j : f.defer[j]) : 0;
-    region::process_message(f.a, f.g, tbl, nib, have, i, lane);
+    uint32_t st;
+    uint64_t mend;
+    region::process_message(f.a, f.g, tbl, nib, have, i, lane, st, mend);
+    if constexpr (COPY) region::transform_fast(f, tbl, have, i, st, mend);
   }
 }
 
 hipError_t launch_region_fused(const FusedArgs& f, int num_cu, hipStream_t s) {
   if (f.a.m == 0) return hipSuccess;
-  if (f.ngroups) hipLaunchKernelGGL(region_fused_kernel, dim3((uint32_t)num_cu), dim3(1024), 0, s, f);
-  else if (hipMemsetAsync(f.ctl, 0xFF, 4, s) != hipSuccess) return hipGetLastError();  // empty region: all to the tail
+  const bool copy = f.out != nullptr;
+  if (f.ngroups) {
+    if (copy) hipLaunchKernelGGL(region_fused_kernel<true>, dim3((uint32_t)num_cu), dim3(1024), 0, s, f);
+    else hipLaunchKernelGGL(region_fused_kernel<false>, dim3((uint32_t)num_cu), dim3(1024), 0, s, f);
+  } else if (hipMemsetAsync(f.ctl, 0xFF, 4, s) != hipSuccess) {  // empty region: all to the tail
+    return hipGetLastError();
+  }
   uint64_t blocks = (f.a.m + 255) / 256;
   if (blocks > (uint64_t)num_cu * 2) blocks = (uint64_t)num_cu * 2;
-  hipLaunchKernelGGL(region_tail_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, f);
+  if (copy) hipLaunchKernelGGL(region_tail_kernel<true>, dim3((uint32_t)blocks), dim3(256), 0, s, f);
+  else hipLaunchKernelGGL(region_tail_kernel<false>, dim3((uint32_t)blocks), dim3(256), 0, s, f);
   return hipGetLastError();
 }
 

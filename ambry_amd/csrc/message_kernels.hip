@@ -40,6 +40,7 @@ __device__ __forceinline__ void transform_describe(const TransformArgs& a, uint6
 // messages: one thread per message 99.1 us, 2 blocks per CU 95.8, 4 blocks 99.0.
 template <bool DESC>
 __global__ __launch_bounds__(256) void msg_parse_kernel(MsgArgs a, TransformArgs t) {
+  if (a.gate && *a.gate == 0) return;  // uniform
   __shared__ uint32_t tbl[1024];
   __shared__ uint32_t pwin[256 * kPropsSlotWords];
   stage_slice_tables(tbl, a.img);
@@ -144,7 +145,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AMBRY_REGIO
 
 __global__ __launch_bounds__(256) void msg_reduce_kernel(MsgArgs a) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.m) return;
+  if (i >= a.m || (a.gate && *a.gate == 0)) return;
   uint32_t s = a.status[i];
 #pragma unroll
   for (int k = 0; k < kMsgSlots; ++k) {
@@ -392,7 +393,7 @@ __global__ __launch_bounds__(256) void transform_place_kernel(TransformArgs a, c
 // the V3 head put_layout_kernel writes afterwards); the rest is read but not copied.
 __global__ __launch_bounds__(256) void transform_jobs_kernel(TransformArgs a) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.m) return;
+  if (i >= a.m || gated_off(a.gate, a.gate_when)) return;
   const ambrycrc_put_desc d = a.desc[i];
   uint64_t co[kMsgSlots] = {kCopySkip, kCopySkip, kCopySkip, kCopySkip, kCopySkip};
   PutLayout L;
@@ -412,7 +413,7 @@ __global__ __launch_bounds__(256) void transform_jobs_kernel(TransformArgs a) {
 // no verify job covers.
 __global__ __launch_bounds__(256) void transform_finish_kernel(TransformArgs a) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.m) return;
+  if (i >= a.m || gated_off(a.gate, a.gate_when)) return;
   const ambrycrc_put_desc d = a.desc[i];
   if (d.header_version == 0) return;
   if (a.status[i] != 0) {

@@ -110,7 +110,8 @@ __device__ __noinline__ uint32_t record_crc_wave(const uint32_t* __restrict__ t,
 // t: compact slice-by-4 tables (stage_slice_tables), nib: stage_nib's sets; g.rk's run sums.
 __device__ __forceinline__ void process_message(const MsgArgs& a, const RegionArgs& g,
                                                 const uint32_t* __restrict__ t, const uint32_t* __restrict__ nib,
-                                                bool have, uint64_t i, uint32_t lane) {
+                                                bool have, uint64_t i, uint32_t lane, uint32_t& st_ret,
+                                                uint64_t& end_ret) {
   const uint32_t* rk = g.rk + kRunPad;
   uint32_t status = 0;
   uint64_t end = 0, off = 0;
@@ -176,6 +177,60 @@ __device__ __forceinline__ void process_message(const MsgArgs& a, const RegionAr
     a.status[i] = status;
     if (a.msg_end) a.msg_end[i] = end ? off + end : 0;
   }
+  st_ret = status;
+  end_ret = end;
+}
+
+// The transform's fast path for message i (FusedArgs::out; verify status st, end `end`): a clean
+// PUT at header V3 with canonical V5 properties and a Blob_Format_V3 record, followed directly by
+// message i + 1, transforms to its own bytes with the life version rewritten
+// (ValidatingTransformer.java:86-95: PutMessageFormatInputStream over the deserialized fields gives
+// back the same records, their CRCs unchanged) -- the streamers copied those bytes to
+// out + (offset - msg_off[0]); this writes the header (life version, CRC) and the outputs.
+// Anything else sets *xfail: the general path then redoes the whole batch.
+__device__ __forceinline__ void transform_fast(const FusedArgs& f, const uint32_t* __restrict__ t, bool have,
+                                               uint64_t i, uint32_t st, uint64_t end) {
+  if (!have) return;
+  const MsgArgs& a = f.a;
+  const uint64_t off = a.msg_off[i], off0 = a.msg_off[0];
+  bool ok = st == 0 && end != 0 && off >= off0 && off - off0 + end <= f.out_cap &&
+            (i + 1 == a.m || a.msg_off[i + 1] == off + end);
+  const uint8_t* p = a.region + off;
+  HeaderWords hw;
+  if (ok) {  // verified: the header and every record lie inside the region
+    hw = load_header(p, 40);
+    ok = be16(p) == 3;
+  }
+  if (ok) {
+    int32_t rel[kMsgSlots];
+#pragma unroll
+    for (int k = 0; k < kMsgSlots; ++k) rel[k] = (int32_t)be32_w0(hw, 3 + k);
+    ok = rel[2] == -1 && rel[1] != -1 && rel[3] != -1 && rel[4] != -1 && be16(p + rel[4]) == 3;
+    if (ok) {  // properties already canonical VERSION_5 bytes, every string ASCII (record_fields.h)
+      const uint32_t stored = (uint32_t)(rel[3] - rel[1] - 10);
+      PropsFields pf;
+      ok = props_parse<true>(p + rel[1] + 2, stored, &pf) == 0 && pf.ascii && props_fix_of(pf, stored).version == 0;
+    }
+  }
+  if (ok && f.life && f.life[i] < 0) ok = false;  // not a life version a V3 header holds
+  if (!ok) {
+    atomicOr(f.xfail, 1u);
+    return;
+  }
+  if (f.life) {  // the index's life version (MessageInfo.getLifeVersion), header CRC recomputed
+    const uint32_t lv = (uint16_t)f.life[i];
+    hw.w[0] = (hw.w[0] & 0xFFFFu) | (((lv >> 8) | ((lv & 0xFFu) << 8)) << 16);
+    const uint32_t c = header_crc(hw, 32, t);
+    hw.w[8] = 0;
+    hw.w[9] = __builtin_bswap32(c);
+  }
+  uint8_t* o = f.out + (off - off0);
+  __builtin_memcpy(o, &hw.w[0], 16);
+  __builtin_memcpy(o + 16, &hw.w[4], 16);
+  __builtin_memcpy(o + 32, &hw.w[8], 8);
+  if (f.out_off) f.out_off[i] = off - off0;
+  f.out_len[i] = end;
+  f.xstatus[i] = 0;
 }
 
 }  // namespace region

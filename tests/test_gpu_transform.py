@@ -319,3 +319,98 @@ def test_transform_host_oversize_message(gpu, mf):
     want = [mf.transform_message(region, o)[1] for o in offs]
     assert out == b"".join(want)
     assert len(want[1]) == len(big) + 26
+
+
+def dense_v3_region(mf, n, seed, lead=0, trail=0):
+    """Clean PUTs as a current server stores them -- header V3, BlobProperties at VERSION_5, a
+    Blob_Format_V3 record, some with an encryption key -- back to back after `lead` junk bytes and
+    before `trail` more: replication's common case, which the transform's one-pass fast path takes
+    (the output is the messages' own bytes with each header's life version rewritten)."""
+    rng = np.random.default_rng(seed)
+    msgs = []
+    for i in range(n):
+        blen = int(rng.choice([0, 1, 100, 1000, 4096, 4109]))
+        content = stream_bytes(seed + i, 0, blen).tobytes()
+        um = stream_bytes(seed + i, 1 << 20, int(rng.choice([0, 7, 300]))).tobytes()
+        props = mf.blob_properties_bytes(blen, service_id="s%d" % (i % 7), private=bool(i % 2),
+                                         encrypted=bool(i % 3 == 0), filename="f%d" % i if i % 4 else None)
+        enc = stream_bytes(seed, 9, 32).tobytes() if i % 5 == 0 else None
+        msgs.append(mf.put_message(mf.store_key("v3-%d" % i), props, um, content, version=3, enc_key=enc,
+                                   life=int(rng.integers(0, 3)), compressed=bool(i % 6 == 0),
+                                   blob_type=int(i % 7 == 0)))
+    junk = stream_bytes(seed, 1 << 30, lead + trail).tobytes()
+    region = junk[:lead] + b"".join(msgs) + junk[lead:]
+    offs = (lead + np.cumsum([0] + [len(x) for x in msgs[:-1]])).tolist()
+    return region, offs
+
+
+@pytest.mark.parametrize("n,lead,use_life", [(2000, 0, True), (1500, 13, False), (30000, 0, True)])
+def test_transform_fast_path_dense_v3(gpu, mf, n, lead, use_life):
+    """The one-pass fast path (region_fused_kernel's copy form): a dense clean V3 region -- at the
+    region start or after junk, with and without index life versions, and (30,000 messages) with
+    messages cut by CU share boundaries, which the tail kernel finishes -- transforms byte-exact
+    against the oracle, packed from 0, every status 0."""
+    import torch
+
+    from ambry_amd.messages import transform_dev
+
+    region, offs = dense_v3_region(mf, n, seed=n + lead, lead=lead, trail=29)
+    life = np.random.default_rng(4).integers(0, 9, size=n).astype(np.int16)
+    dev = torch.frombuffer(bytearray(region), dtype=torch.uint8).cuda()
+    out, oo, ol, st = transform_dev(dev, torch.tensor(offs, dtype=torch.int64, device="cuda"), header_version=3,
+                                    life_version=torch.from_numpy(life).cuda() if use_life else None)
+    torch.cuda.synchronize()
+    st, oo, ol = st.cpu().numpy().view(np.uint32), oo.cpu().numpy(), ol.cpu().numpy()
+    out_h = out.cpu().numpy().tobytes()
+    assert st.tolist() == [0] * n
+    pos = 0
+    for i in range(0, n, 1 if n <= 2000 else 7):
+        o = offs[i]
+        exp_st, exp = mf.transform_message(region, o, life=int(life[i]) if use_life else None, version=3)
+        assert exp_st == 0
+        assert oo[i] == o - offs[0] and ol[i] == len(exp), i
+        assert out_h[oo[i]:oo[i] + len(exp)] == exp, i
+    assert oo[-1] + ol[-1] == len(region) - lead - 29
+
+
+@pytest.mark.parametrize("spoil", ["corrupt", "v1_props", "gap", "update", "order"])
+def test_transform_fast_path_falls_back(gpu, mf, spoil):
+    """One message the fast path cannot take -- a flipped byte, properties stored at SerDe V1 (a
+    re-encode), a gap between two messages, an update record, two offsets swapped -- sends the
+    batch through the general path; the result is the oracle's for every message."""
+    import torch
+
+    from ambry_amd.messages import transform_dev
+
+    region, offs = dense_v3_region(mf, 800, seed=3)
+    region = bytearray(region)
+    k = 400
+    if spoil == "corrupt":
+        region[offs[k] + 70] ^= 0x08
+    elif spoil in ("v1_props", "gap", "update"):
+        if spoil == "v1_props":
+            new = mf.put_message(mf.store_key("x"), mf.blob_properties_bytes(10, serde_version=1), b"", b"0123456789")
+        elif spoil == "update":
+            new = mf.update_message(mf.store_key("x"), version=3)
+        else:
+            new = bytes(region[offs[k]:offs[k + 1]]) + b"\0\0\0"
+        region = region[:offs[k]] + new + region[offs[k + 1]:]
+        d = len(new) - (offs[k + 1] - offs[k])
+        offs = offs[:k + 1] + [o + d for o in offs[k + 1:]]
+    elif spoil == "order":
+        offs[k], offs[k + 1] = offs[k + 1], offs[k]
+    region = bytes(region)
+    dev = torch.frombuffer(bytearray(region), dtype=torch.uint8).cuda()
+    out, oo, ol, st = transform_dev(dev, torch.tensor(offs, dtype=torch.int64, device="cuda"))
+    torch.cuda.synchronize()
+    st, oo, ol = st.cpu().numpy().view(np.uint32), oo.cpu().numpy(), ol.cpu().numpy()
+    out_h = out.cpu().numpy().tobytes()
+    pos = 0
+    for i, o in enumerate(offs):
+        exp_st, exp = mf.transform_message(region, o, version=3)
+        assert int(st[i]) == exp_st, i
+        if exp is None:
+            assert ol[i] == 0 and oo[i] == -1
+            continue
+        assert oo[i] == pos and out_h[pos:pos + len(exp)] == exp, i
+        pos += len(exp)
