@@ -538,7 +538,9 @@ int ambrycrc_fill_random_dev(uint8_t* d_dst, uint64_t nbytes, uint64_t seed, uin
  * [0, nbytes/2 - 4096) and storing each piece at the same offset from d_base + nbytes/2;
  * 40 + k = the same with the destination 11 B further (unaligned stores); 48 = contiguous
  * per-wave shares; 49 / 50 = grid-stride copy over 32 blocks of 256 threads per CU, plain /
- * nontemporal stores (the plain copy roof). */
+ * nontemporal stores (the plain copy roof).
+ * FETCH_SIZE calibration (60 / 61 / 62): every 128-B line of the largest power-of-two number of
+ * lines in nbytes read once, in scattered order, by one 16-B / 4-B / unaligned 8-B load. */
 int ambrycrc_debug_readbw_dev(const uint8_t* d_base, uint64_t nbytes, uint32_t* d_out, int variant,
                               hipStream_t stream);
 

@@ -117,3 +117,20 @@ def test_region_model_matches_zlib(ambry):
             if a + ln > len(mem):
                 continue
             assert rm.job_crc(mem, reg0, rk, a, ln) == zlib.crc32(mem[a:a + ln]), (reg0, a, ln)
+
+
+def test_region_wave_model_matches_zlib(ambry):
+    """The whole-wave form of a long record's CRC (region_proc.h record_crc_wave: 64 lane slices of
+    4*gs runs aligned to the record's last run, lane partials merged by a DPP tree of gf2 shifts by
+    x^(8*256*gs*2^k)) against zlib, on records from 1 to ~3 groups per lane, starting and ending at
+    odd offsets, in a region whose start is not 64-aligned."""
+    import zlib
+
+    from kernel_model import RegionModel, table_image
+
+    rm = RegionModel(table_image())
+    reg0 = 37
+    mem = stream_bytes(4242, 0, 60000).tobytes()
+    rk = rm.runs(mem, reg0)
+    for a, ln in ((0, 33000), (5, 16411), (63, 40000), (1000, 17000), (3, 59990), (129, 257 * 64)):
+        assert rm.job_crc_wave(mem, reg0, rk, a, ln) == zlib.crc32(mem[a:a + ln]), (a, ln)

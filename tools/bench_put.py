@@ -122,14 +122,14 @@ def run(m, blob_bytes, reps, in_place, um_len=1000):
 
 def run_transform(m, blob_bytes, reps):
     """ValidatingTransformer (ambrycrc_transform_messages_dev) over a region of m stored V3 PUTs (made by
-    the serializer), re-serialized at V3. Clean messages take the speculative pass: the verify reads
-    each message once and its copy-through writes the output once, the CRCs coming from the
-    verified input trailers: 2 passes over the bytes."""
+    the serializer), re-serialized at V3. A dense clean V3 region takes the one-pass fast path: the
+    region kernel reads each message once, verifying it, and writes it once into the output; the
+    CRCs are the verified input trailers."""
     import numpy as np
     import torch
 
     from ambry_amd import device as D
-    from ambry_amd.messages import PUT_DESC_DTYPE, PutMessage, layout, serialize_dev, transform_dev
+    from ambry_amd.messages import PUT_DESC_DTYPE, PutMessage, layout, out_bound, serialize_dev, transform_dev
 
     key_len, props_len, um_len = 24, 94, 1000
     L, fo = layout(PutMessage(key=bytes(key_len), props=bytes(props_len), usermeta=bytes(um_len),
@@ -147,7 +147,7 @@ def run_transform(m, blob_bytes, reps):
     region.view(m, L)[:, p0:p0 + props_len] = _props_tensor(torch)
     serialize_dev(torch.from_numpy(descs.view(np.uint8).copy()).cuda(), region)  # in place: random fields
     offs = torch.from_numpy((idx * L).astype(np.int64)).cuda()
-    out = torch.empty(m * L + 6 * m, dtype=torch.uint8, device="cuda")
+    out = torch.empty(out_bound(m * L, m), dtype=torch.uint8, device="cuda")
     _, oo, ol, st = transform_dev(region, offs, out=out)
     torch.cuda.synchronize()
     assert int(st.abs().sum().item()) == 0 and bool(torch.equal(out[: m * L], region))  # V3 -> V3: identical

@@ -9,10 +9,14 @@ untimed; the profiler's per-dispatch counters are the measurement.
   batch4109  4109-B chunks at 16-B offsets (the blob records of 4 KiB PUTs)     -- group class 3
   batch2000  2000-B chunks, packed (8-B offsets); batch3000: 3000 B at 16-B offsets -- class 2
   batch16k   16 KiB chunks, aligned                                               -- class 3
-  msg4k      ambrycrc_verify_messages_dev over 262,144 x PUT(4 KiB blob), 1.29 GiB
-  msg3k      the same with 3000 B blobs (blob records in class 2)
+  msg4k      ambrycrc_verify_messages_dev over 262,144 x PUT(4 KiB blob), 1.29 GiB (region mode, one pass)
+  msg1k      the same over 524,288 x PUT(1 KiB blob); msg3k with 3000 B blobs
+  msg4k_2pass / msg4k_jobs   msg4k in region mode's two-pass form / in job mode
+  scatter16 / scatter4 / scatter8   FETCH_SIZE calibration: every 128-B line of 1 GiB read once in
+             scattered order by one 16-B / 4-B / unaligned 8-B load (ambrycrc_debug_readbw_dev 60-62)
   put4k      ambrycrc_serialize_puts_dev, copy mode, 262,144 x PUT(4 KiB blob); put4k_inplace in place
-  xform4k    ambrycrc_transform_messages_dev over 262,144 stored PUT(4 KiB blob) messages
+  xform4k    ambrycrc_transform_messages_dev over 262,144 stored PUT(4 KiB blob) messages (fast path)
+  xform64k   the same over 65,536 PUT(64 KiB blob) messages
   single100  one 100 B chunk per ambrycrc_batch_dev call
   single4m   one 4 MiB chunk per ambrycrc_batch_dev call
 """
@@ -80,10 +84,12 @@ def main():
         for _ in range(args.reps):
             D.crc32_batch(buf, off, ln, out=out, workspace=ws)
         info.update(chunks=1, chunk_bytes=size, alg_bytes_per_launch=size + 4)
-    elif args.case in ("msg4k", "msg3k"):
+    elif args.case in ("msg4k", "msg3k", "msg1k", "msg4k_2pass", "msg4k_jobs"):
         from bench_messages import gpu_region, load_mf
 
-        res = gpu_region(load_mf(), 262144, 4 << 10 if args.case == "msg4k" else 3000, args.reps)
+        m, blob = {"msg3k": (262144, 3000), "msg1k": (524288, 1024)}.get(args.case, (262144, 4096))
+        mode = "region2" if args.case.endswith("_2pass") else "jobs" if args.case.endswith("_jobs") else "region"
+        res = gpu_region(load_mf(), m, blob, args.reps, mode=mode)
         info.update(res)
         # CRC'd bytes per message: header 32 + props + usermeta 1006 + blob record 4109 (+ stored CRCs read)
         info["alg_bytes_per_launch"] = res["region_bytes"]
@@ -95,14 +101,28 @@ def main():
         res = run(262144, 4096, args.reps, args.case == "put4k_inplace")
         info.update(res)
         info["alg_bytes_per_launch"] = res["hbm_bytes_min"]  # fields + blobs read, messages written (copy)
-    elif args.case == "xform4k":
-        # ambrycrc_transform_messages_dev over 262,144 stored 4 KiB-blob PUTs (the speculative pass: the
-        # verify's copy-through reads each record once and writes it into the output)
+    elif args.case in ("xform4k", "xform64k"):
+        # ambrycrc_transform_messages_dev over stored 4 KiB / 64 KiB-blob PUTs (the one-pass fast path
+        # reads each message once and writes it once into the output)
         from bench_put import run_transform
 
-        res = run_transform(262144, 4096, args.reps)
+        res = run_transform(262144, 4096, args.reps) if args.case == "xform4k" else run_transform(65536, 65536,
+                                                                                                  args.reps)
         info.update(res)
         info["alg_bytes_per_launch"] = 2 * res["message_bytes"]
+    elif args.case in ("scatter16", "scatter4", "scatter8"):
+        from ambry_amd._lib import check, lib
+
+        nbytes = 1 << 30
+        buf = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+        D.fill_random(buf, 3, 0)
+        scratch = torch.zeros(1024, dtype=torch.int32, device="cuda")
+        v = {"scatter16": 60, "scatter4": 61, "scatter8": 62}[args.case]
+        for _ in range(args.reps + 1):
+            check(lib().ambrycrc_debug_readbw_dev(buf.data_ptr(), nbytes, scratch.data_ptr(), v,
+                                                  torch.cuda.current_stream().cuda_stream), "readbw")
+        info.update(lines=nbytes // 128, line_bytes=128, alg_bytes_per_launch=nbytes,
+                    what="every 128-B line read once by one %s load" % args.case[7:] + "-B")
     else:
         raise SystemExit(f"unknown case {args.case}")
     torch.cuda.synchronize()

@@ -4,7 +4,13 @@ per case and kernel, the kernel-trace duration and per-dispatch PMC averages, pl
 figures: HBM bytes (2*FETCH_SIZE + WRITE_SIZE, KiB; MI355X_MICROARCH.md §HBM) against the
 algorithmic bytes, achieved GB/s, VALU and LDS instructions per KiB of chunk data, the share
 of wave-cycles parked (SQ_WAIT_ANY), stalled on LDS issue (SQ_WAIT_INST_LDS) and issuing
-(SQ_ACTIVE_INST_ANY), and the effective clock (GRBM_GUI_ACTIVE / 8 / duration)."""
+(SQ_ACTIVE_INST_ANY), and the effective clock (GRBM_GUI_ACTIVE / 8 / duration).
+
+Per case also the whole call ("call": every kernel of one call, median durations summed, bytes
+summed) -- the message verify's and the transform's figures are per call -- and the mode the call
+took as the library reported it (ambrycrc_last_message_mode, "mode_taken"). The scatter16 / scatter4
+/ scatter8 cases calibrate FETCH_SIZE for scattered small reads: measured FETCH bytes per read line
+("fetch_per_line") against the 128 B each line holds."""
 from __future__ import annotations
 
 import argparse
@@ -16,7 +22,10 @@ import os
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNELS = ("crc32_sweep_kernel", "crc32_plan_scan_kernel", "crc32_plan_count_kernel", "msg_parse_kernel",
-           "msg_reduce_kernel")
+           "msg_reduce_kernel", "region_runs_kernel", "region_msg_kernel", "region_fused_kernel",
+           "region_tail_kernel", "transform_place_kernel", "transform_jobs_kernel", "transform_finish_kernel",
+           "transform_merge_kernel", "transform_desc_kernel", "props_fix_kernel", "put_layout_kernel",
+           "put_seal_kernel", "gather_copy_kernel", "readbw_scatter_kernel")
 
 
 def kname(full):
@@ -121,14 +130,30 @@ def main():
             if "GRBM_GUI_ACTIVE" in c:
                 row["grbm_gui_active"] = c["GRBM_GUI_ACTIVE"]
             kern[k] = row
-        res["cases"][case] = {"info": info, "kernels": kern}
+        # the whole call: kernels launched once per call (reps + the checked first call), medians summed
+        reps = max((tv["calls"] for tv in t.values()), default=0)
+        call = {"kernels": sorted(k for k, tv in t.items() if tv["calls"] >= max(1, reps // 2)),
+                "ns": sum(tv["median_ns"] for k, tv in t.items() if tv["calls"] >= max(1, reps // 2))}
+        hb = [kern[k].get("hbm_bytes") for k in call["kernels"]]
+        if hb and all(x is not None for x in hb):
+            call["hbm_bytes"] = sum(hb)
+        if alg and call["ns"]:
+            call["alg_bytes"] = alg
+            call["achieved_GBps"] = round(alg / call["ns"], 1)
+            call["frac_of_8TBps"] = round(alg / call["ns"] / 8000, 4)
+            if "hbm_bytes" in call:
+                call["traffic_over_alg"] = round(call["hbm_bytes"] / alg, 4)
+        if case.startswith("scatter") and "readbw_scatter_kernel" in counters:
+            c = counters["readbw_scatter_kernel"]
+            if "FETCH_SIZE" in c and info.get("lines"):
+                call["fetch_per_line"] = round(c["FETCH_SIZE"] * 1024 / info["lines"], 2)
+                call["fetch_over_bytes"] = round(c["FETCH_SIZE"] * 1024 / (info["lines"] * 128), 4)
+        res["cases"][case] = {"info": info, "mode_taken": info.get("mode_taken"), "kernels": kern, "call": call}
     out = os.path.join(ROOT, "profiles", f"{args.tag}_small_cases.json")
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
     for case, v in res["cases"].items():
-        sw = v["kernels"].get("crc32_sweep_kernel", {})
-        print(case, {k: sw.get(k) for k in ("achieved_GBps", "traffic_over_alg", "valu_per_kib", "lds_per_kib",
-                                            "wait_any_frac", "wait_inst_lds_frac", "active_inst_frac")}, sw.get("trace", {}).get("median_ns"))
+        print(case, v.get("mode_taken"), v["call"])
 
 
 if __name__ == "__main__":
