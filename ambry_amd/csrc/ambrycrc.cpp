@@ -602,6 +602,11 @@ int ambrycrc_init(int device) {
     if (end != v && *end == '\0' && x >= 0 && x < 1000 && variant_supported((int)x)) c->variant = (int)x;
   }
   if (const char* v = getenv("AMBRYCRC_REGION")) c->region_mode = strcmp(v, "0") == 0 ? 0 : strcmp(v, "2") == 0 ? 2 : 1;
+  if (const char* v = getenv("AMBRYCRC_FUSED_PROC")) {  // A/B: processor waves of the one-pass kernels
+    char* end = nullptr;
+    const long x = strtol(v, &end, 10);
+    if (end != v && *end == '\0' && x >= 0 && x <= kFusedProcMax) c->fused_proc = (int)x;
+  }
   if (const char* v = getenv("AMBRYCRC_REGION_MAX_PER_MESSAGE")) {  // A/B: the region-mode cut-off
     char* end = nullptr;
     const unsigned long long x = strtoull(v, &end, 10);
@@ -975,6 +980,15 @@ size_t msg_jobs_bytes(size_t m) {
   return (j * 2 * sizeof(uint64_t) + j * 2 * sizeof(uint32_t) + j + 255) & ~size_t(255);
 }
 
+// A processor wave finishes a 64-message batch in ~20-40 us (a chain of dependent reads under the
+// streamers' load), so the processors a CU needs grow with its messages; the rest of its 16 waves
+// stream. One processor per 512 messages per CU, 2 to kFusedProcMax.
+uint32_t fused_proc_waves(const DevCtx* c, size_t m) {
+  if (c->fused_proc > 0) return (uint32_t)std::min(c->fused_proc, kFusedProcMax);
+  const size_t per_cu = m / (size_t)std::max(1, c->num_cu);
+  return (uint32_t)std::max<size_t>(2, std::min<size_t>(kFusedProcMax, (per_cu + 511) / 512));
+}
+
 int enqueue_messages(DevCtx* c, const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off, size_t m,
                      uint32_t* d_status, uint64_t* d_msg_end, void* d_ws, size_t ws_bytes, hipStream_t stream) {
   const bool region = c->region_mode && region_len > 0 && region_len <= c->region_max * (uint64_t)m &&
@@ -1016,6 +1030,7 @@ int enqueue_messages(DevCtx* c, const uint8_t* d_region, uint64_t region_len, co
   f.ngroups = (r.nsb + 3) / 4;
   f.ctl = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(st.batch_ws) + region_rk_bytes(d_region, region_len));
   f.defer = f.ctl + 64;
+  f.nproc = fused_proc_waves(c, m);
   if (hipMemsetAsync(f.ctl, 0, 8, stream) != hipSuccess) return AMBRYCRC_EHIP;
   return hip_err(launch_region_fused(f, c->num_cu, stream));
 }

@@ -82,6 +82,8 @@ struct DevCtx {
   int region_mode = 1;
   // The form the last message verify on this device took (ambrycrc_last_message_mode).
   std::atomic<int> last_msg_mode{-1};
+  // Processor waves of the one-pass kernels (0: per call, fused_proc_waves); AMBRYCRC_FUSED_PROC.
+  int fused_proc = AMBRY_FUSED_PROC;
   uint64_t region_max = kRegionMaxPerMessage;  // region bytes per message up to which it applies
   // Sweep rounds of at most this many bytes (SweepArgs::window); 0 = one round.
   uint64_t window = 32ull << 30;
@@ -142,6 +144,8 @@ int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uin
 // ws_bytes >= ambrycrc_messages_workspace_bytes(m) bytes. d_msg_end may be null.
 int enqueue_messages(DevCtx* c, const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off, size_t m,
                      uint32_t* d_status, uint64_t* d_msg_end, void* d_ws, size_t ws_bytes, hipStream_t stream);
+// Processor waves per workgroup of the one-pass region kernels for m messages (FusedArgs::nproc).
+uint32_t fused_proc_waves(const DevCtx* c, size_t m);
 // Bytes of the job arrays at the start of a message-verify workspace (the rest: batch / run sums).
 size_t msg_jobs_bytes(size_t m);
 // The same in two halves: the parse kernel (jobs and their stored CRCs in st->a), then the CRC

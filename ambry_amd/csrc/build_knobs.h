@@ -21,8 +21,8 @@
 #ifndef AMBRY_REGION_BPC  // region pass 2: blocks per CU (0: one thread per message)
 #define AMBRY_REGION_BPC 2
 #endif
-#ifndef AMBRY_FUSED_PROC  // one-pass region verify: processor waves per 16-wave workgroup
-#define AMBRY_FUSED_PROC 2
+#ifndef AMBRY_FUSED_PROC  // one-pass region verify: processor waves per 16-wave workgroup (0: per call)
+#define AMBRY_FUSED_PROC 0
 #endif
 
 // ---- batch CRC kernels (crc32_kernels.hip, crc32_kernels.h, ambrycrc_ctx.h)
@@ -70,7 +70,7 @@
 // X(name, default) for every knob above: ambrycrc_version() reports those that differ.
 #define AMBRY_KNOB_LIST(X)                                                                                  \
   X(AMBRY_PROPS_WIN, 96) X(AMBRY_PARSE_BPC, 2) X(AMBRY_REGION_WPE, 2) X(AMBRY_REGION_BPC, 2)                  \
-  X(AMBRY_FUSED_PROC, 2)                                                                                      \
+  X(AMBRY_FUSED_PROC, 0)                                                                                      \
   X(AMBRY_GRP_PRIO, 0) X(AMBRY_GRP_IL, 4) X(AMBRY_C0_G, 2) X(AMBRY_C0_NB, 8) X(AMBRY_C1_MAX, 1024)           \
   X(AMBRY_RUNS_STORE_NT, 0) X(AMBRY_RUNS_GIL, 1) X(AMBRY_PLAN_PER_BLOCK, 2048) X(AMBRY_DEFAULT_VARIANT, 29) \
   X(AMBRY_REGION_PROBE, 0) X(AMBRY_RUNS_PROBE, 0)

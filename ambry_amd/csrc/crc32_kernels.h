@@ -312,6 +312,7 @@ struct FusedArgs {
   uint64_t ngroups;  // 16 KiB groups over the region: ceil(nsb / 4)
   uint32_t* ctl;
   uint32_t* defer;
+  uint32_t nproc;    // processor waves per workgroup (1..kFusedProcMax); waves 16 - nproc .. 15
   // Transform fast path (launch_region_fused with copy): when every message is a clean PUT stored
   // at header V3 with canonical V5 properties and a Blob_Format_V3 record, back to back from
   // msg_off[0], the output is the region from msg_off[0] on with each header's life version and
@@ -327,8 +328,9 @@ struct FusedArgs {
   uint32_t* xfail = nullptr;
 };
 constexpr uint64_t kGroupBytes = 4 * kSuperBlock;
-constexpr int kFusedProc = AMBRY_FUSED_PROC;        // processor waves per workgroup
-constexpr int kFusedStreamers = 16 - kFusedProc;    // streaming waves
+// Processor waves per 16-wave workgroup (the rest stream): chosen per call from the messages per
+// CU (fused_proc_waves, ambrycrc.cpp); AMBRY_FUSED_PROC > 0 or AMBRYCRC_FUSED_PROC fixes it (A/B).
+constexpr int kFusedProcMax = 12;
 hipError_t launch_region_fused(const FusedArgs& f, int num_cu, hipStream_t s);  // f.out set: the copy form
 
 hipError_t launch_plan(const PlanArgs& a, hipStream_t s);

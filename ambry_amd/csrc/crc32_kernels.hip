@@ -1641,12 +1641,12 @@ hipError_t launch_region_runs(const RegionArgs& a, int grid, hipStream_t s) {
 
 // ---- region mode in one pass: region_fused_kernel (FusedArgs, crc32_kernels.h) ----
 // Workgroup b (one per CU) owns groups [G0, G1) of 16 KiB (4 super-blocks). Streaming wave v <
-// kFusedStreamers takes groups G0 + v, G0 + v + S, ... (S = kFusedStreamers): the CU's frontier
+// S = 16 - f.nproc takes groups G0 + v, G0 + v + S, ...: the CU's frontier
 // advances S groups at a time, each wave's 4 super-blocks hashed as region_runs_kernel does them,
 // the next 4 in flight, the 256 run sums stored as one 1 KiB wave store. At the top of each group
 // the wave waits for all its memory operations (the previous group's store included) and publishes
 // how many of its groups are complete in LDS (done[v]).
-// Processor wave p takes 64-message batches p, p + kFusedProc, ... of the CU's messages -- those
+// Processor wave p takes 64-message batches p, p + f.nproc, ... of the CU's messages -- those
 // whose offsets lie in the share, found by a 64-way search of the sorted offsets -- waiting on the
 // frontier (the longest complete prefix of the share's groups) first until the batch's headers are
 // streamed, then until its messages' ends are; then region::process_message. A message that
@@ -1715,12 +1715,13 @@ __global__ __launch_bounds__(1024) void region_fused_kernel(FusedArgs f) {
   const uint32_t v = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t G0 = f.ngroups * blockIdx.x / gridDim.x, G1 = f.ngroups * (blockIdx.x + 1) / gridDim.x;
   const RegionArgs& a = f.g;
-  if (v < (uint32_t)kFusedStreamers) {
+  const uint32_t nstream = 16u - f.nproc;
+  if (v < nstream) {
     // ---- streaming wave
     const LaneConst k = make_lane_const(lane);
     uint32_t* buf = g_lds_runs + kSliceBytes / 4 + v * (kRunsBufBytes / 4);
     const uint32_t slot = 16u * (lane & 3u) + (lane >> 2);
-    const uint64_t mine = G1 - G0 > v ? (G1 - G0 - v + kFusedStreamers - 1) / kFusedStreamers : 0;
+    const uint64_t mine = G1 - G0 > v ? (G1 - G0 - v + nstream - 1) / nstream : 0;
     // COPY: out[0] is region byte msg_off[0] (base-relative `shift`); every piece holding region
     // bytes is stored at its place, cut to [shift, shift + out_cap)
     const uint64_t shift = COPY ? a.reg0 + f.a.msg_off[0] : 0;
@@ -1753,12 +1754,12 @@ __global__ __launch_bounds__(1024) void region_fused_kernel(FusedArgs f) {
       region_sb_load(a, 4 * g + 1, lane, b1);
       region_sb_load(a, 4 * g + 2, lane, b2);
       region_sb_load(a, 4 * g + 3, lane, b3);
-      for (uint64_t j = 0; j < mine; ++j, g += kFusedStreamers) {
+      for (uint64_t j = 0; j < mine; ++j, g += nstream) {
         if (j) {  // the previous group's store has completed: publish it
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           __hip_atomic_store(&done[v], (uint32_t)j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
-        const uint64_t nx = j + 1 < mine ? g + kFusedStreamers : g;  // the last group re-reads itself
+        const uint64_t nx = j + 1 < mine ? g + nstream : g;  // the last group re-reads itself
         hash(4 * g, 0, b0);
         __builtin_amdgcn_s_setprio(3);
         region_sb_load(a, 4 * nx, lane, b0);
@@ -1784,10 +1785,10 @@ __global__ __launch_bounds__(1024) void region_fused_kernel(FusedArgs f) {
     return;
   }
   // ---- processor wave
-  const uint32_t p = v - (uint32_t)kFusedStreamers;
+  const uint32_t p = v - nstream;
   const uint64_t s_lo = G0 * kGroupBytes, s_hi = G1 * kGroupBytes;  // the share, base-relative
   {  // this wave's slice of the global sortedness check
-    const uint64_t waves = (uint64_t)gridDim.x * kFusedProc, w = (uint64_t)blockIdx.x * kFusedProc + p;
+    const uint64_t waves = (uint64_t)gridDim.x * f.nproc, w = (uint64_t)blockIdx.x * f.nproc + p;
     const uint64_t c0 = f.a.m * w / waves, c1 = f.a.m * (w + 1) / waves;
     bool bad = false;
     for (uint64_t i = c0 + lane; i < c1; i += 64)
@@ -1799,8 +1800,8 @@ __global__ __launch_bounds__(1024) void region_fused_kernel(FusedArgs f) {
   // frontier: base-relative end of the longest complete prefix of the share's groups
   auto frontier = [&]() -> uint64_t {
     uint64_t q = ~0ull;
-    if (lane < (uint32_t)kFusedStreamers)
-      q = lane + (uint64_t)kFusedStreamers *
+    if (lane < nstream)
+      q = lane + (uint64_t)nstream *
                      __hip_atomic_load(&done[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -1814,28 +1815,24 @@ __global__ __launch_bounds__(1024) void region_fused_kernel(FusedArgs f) {
     while (frontier() < target) __builtin_amdgcn_s_sleep(8);
     asm volatile("" ::: "memory");  // no run-sum load above the poll
   };
-  for (uint64_t b = M0 + 64 * (uint64_t)p; b < M1; b += 64 * (uint64_t)kFusedProc) {
+  for (uint64_t b = M0 + 64 * (uint64_t)p; b < M1; b += 64 * (uint64_t)f.nproc) {
     const uint64_t i = b + lane;
-    bool have = i < M1;
-    const uint64_t pos = have ? msg_pos(f, i) : 0;
-    wait_for(wave_max_u64(have ? pos + 128 : 0));  // the batch's headers streamed past
-    uint64_t end = 0;
-    if (have) {
-      const uint64_t off = f.a.msg_off[i];
-      const bool in_region = off <= f.a.region_len;
-      const uint64_t rem = in_region ? f.a.region_len - off : 0;
-      end = header_end(load_header(f.a.region + (in_region ? off : 0), rem), rem);
-      if (end && (pos < s_lo || pos + end > s_hi)) {  // runs past the share: the tail kernel's
-        const uint32_t at = atomicAdd(f.ctl + 1, 1u);
-        if (at < f.a.m) f.defer[at] = (uint32_t)i;  // (unsorted offsets may defer more: ctl[0] covers them)
-        have = false;
-      }
-    }
-    wait_for(wave_max_u64(have && end ? pos + end : 0));
+    const bool have = i < M1;
+    // First wait: until the next batch's first message (for back-to-back messages the end of this
+    // batch's last one); the processor waits again only for a message that runs further.
+    wait_for(b + 64 < f.a.m ? msg_pos(f, b + 64) : s_hi);
     uint32_t st;
     uint64_t mend;
-    region::process_message(f.a, f.g, tbl, nib, have, i, lane, st, mend);
-    if constexpr (COPY) region::transform_fast(f, tbl, have, i, st, mend);
+    region::process_message(f.a, f.g, tbl, nib, have, i, lane, st, mend, [&](uint64_t pos, uint64_t end) -> bool {
+      // the lane's message ends at pos + end (base-relative): past the share or before it -> the tail's
+      if (pos < s_lo || pos + end > s_hi) {
+        const uint32_t at = atomicAdd(f.ctl + 1, 1u);
+        if (at < f.a.m) f.defer[at] = (uint32_t)i;  // (unsorted offsets may defer more: ctl[0] covers them)
+        return false;
+      }
+      return true;
+    }, [&](uint64_t need) { wait_for(need); });
+    if constexpr (COPY) region::transform_fast(f, tbl, st != ~0u, i, st, mend);
   }
 }
 
@@ -1863,7 +1860,8 @@ __global__ __launch_bounds__(256) void region_tail_kernel(FusedArgs f) {
     const uint64_t i = have ? (all ? j : f.defer[j]) : 0;
     uint32_t st;
     uint64_t mend;
-    region::process_message(f.a, f.g, tbl, nib, have, i, lane, st, mend);
+    region::process_message(f.a, f.g, tbl, nib, have, i, lane, st, mend,
+                            [](uint64_t, uint64_t) -> bool { return true; }, [](uint64_t) {});
     if constexpr (COPY) region::transform_fast(f, tbl, have, i, st, mend);
   }
 }

@@ -23,6 +23,15 @@ namespace region {
 // Records of more runs than this go to the whole wave.
 constexpr int64_t kLongRuns = 512;
 
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t w = __shfl_xor(v, o);
+    v = w > v ? w : v;
+  }
+  return v;
+}
+
 // Lane (l - 2^LVL)'s v, for lanes with bit LVL set (others: 0): DPP row shifts, then row broadcasts.
 template <int LVL>
 __device__ __forceinline__ uint32_t left_partner(uint32_t v) {
@@ -108,10 +117,14 @@ __device__ __noinline__ uint32_t record_crc_wave(const uint32_t* __restrict__ t,
 // available: status and message end written. Long records are collected and done by the wave
 // after the per-lane ones, so every lane of the wave must call this (have = false for none).
 // t: compact slice-by-4 tables (stage_slice_tables), nib: stage_nib's sets; g.rk's run sums.
+// keep(pos, end): called for a parsed message whose records need CRCs (pos: its base-relative
+// start, end: its length); false = the lane drops it (deferred: no status written, st_ret ~0).
+// wait(need): the whole wave waits until every run up to base-relative `need` exists.
+template <class Keep, class Wait>
 __device__ __forceinline__ void process_message(const MsgArgs& a, const RegionArgs& g,
                                                 const uint32_t* __restrict__ t, const uint32_t* __restrict__ nib,
                                                 bool have, uint64_t i, uint32_t lane, uint32_t& st_ret,
-                                                uint64_t& end_ret) {
+                                                uint64_t& end_ret, Keep keep, Wait wait) {
   const uint32_t* rk = g.rk + kRunPad;
   uint32_t status = 0;
   uint64_t end = 0, off = 0;
@@ -137,6 +150,15 @@ __device__ __forceinline__ void process_message(const MsgArgs& a, const RegionAr
       ex[k] = r.ex[k];
     }
   }
+  // records to CRC: the message must end inside what the caller streams, else it is deferred
+  bool crcs = false;
+#pragma unroll
+  for (int k = 0; k < kMsgSlots; ++k) crcs |= have && jl[k] != 0;
+  if (crcs && !keep(g.reg0 + off, end)) {
+    have = false;
+    crcs = false;
+  }
+  wait(wave_max_u64(crcs ? g.reg0 + off + end : 0));
 #pragma unroll
   for (int k = 0; k < kMsgSlots; ++k) {
     if (!have || jl[k] == 0) continue;
@@ -177,7 +199,7 @@ __device__ __forceinline__ void process_message(const MsgArgs& a, const RegionAr
     a.status[i] = status;
     if (a.msg_end) a.msg_end[i] = end ? off + end : 0;
   }
-  st_ret = status;
+  st_ret = have ? status : ~0u;
   end_ret = end;
 }
 
@@ -190,7 +212,7 @@ __device__ __forceinline__ void process_message(const MsgArgs& a, const RegionAr
 // Anything else sets *xfail: the general path then redoes the whole batch.
 __device__ __forceinline__ void transform_fast(const FusedArgs& f, const uint32_t* __restrict__ t, bool have,
                                                uint64_t i, uint32_t st, uint64_t end) {
-  if (!have) return;
+  if (!have || st == ~0u) return;  // no message, or deferred to the tail kernel
   const MsgArgs& a = f.a;
   const uint64_t off = a.msg_off[i], off0 = a.msg_off[0];
   bool ok = st == 0 && end != 0 && off >= off0 && off - off0 + end <= f.out_cap &&
