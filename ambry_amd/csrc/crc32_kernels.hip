@@ -1734,10 +1734,13 @@ __global__ __launch_bounds__(1024) void region_fused_kernel(FusedArgs f) {
         if (d0 >= f.out_cap) continue;
         if (p >= shift && d0 + 16 <= f.out_cap) {
           st16u(f.out + (p - shift), cur[q]);
-        } else {
-#pragma unroll
-          for (int b = 0; b < 16; ++b)
-            if (p + b >= shift && p + b - shift < f.out_cap) st8g(f.out + (p + b - shift), cur[q][b >> 2] >> (8 * (b & 3)));
+        } else {  // the piece holding out[0] or out[out_cap - 1]: byte by byte (rare)
+          const u32x4 v = cur[q];
+#pragma unroll 1
+          for (uint32_t b = 0; b < 16; ++b) {
+            const uint32_t w = b < 4 ? v.x : b < 8 ? v.y : b < 12 ? v.z : v.w;
+            if (p + b >= shift && p + b - shift < f.out_cap) st8g(f.out + (p + b - shift), w >> (8 * (b & 3)));
+          }
         }
       }
     };

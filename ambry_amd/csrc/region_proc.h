@@ -170,7 +170,27 @@ __device__ __forceinline__ void process_message(const MsgArgs& a, const RegionAr
     }
     if (record_crc(t, nib, g.base, rk, pa, jl[k]) != ex[k]) status |= record_bit(k);
   }
-  // the wave takes the long records one by one
+  // The long records: the wave takes them one by one, unless enough lanes have one that the lanes
+  // doing their own in parallel finish first (a lane's chain is runs/4 nibble multiplies deep; the
+  // wave's per record ~runs/256 plus ~64 for the tree's gf2 shifts).
+  {
+    int64_t lane_runs = 0;
+#pragma unroll
+    for (int k = 0; k < kMsgSlots; ++k)
+      if (longs & (1u << k))
+        lane_runs += (int64_t)((((g.reg0 + jo[k] + jl[k] + 63) & ~uint64_t(63)) - ((g.reg0 + jo[k]) & ~uint64_t(63))) >> 6);
+    const int64_t per_lane = (int64_t)wave_max_u64((uint64_t)lane_runs) / 4;
+    int64_t wave = 0;
+    for (int o = 32; o > 0; o >>= 1) lane_runs += __shfl_xor(lane_runs, o);  // sum over lanes
+    wave = lane_runs / 256 + 64 * (int64_t)__popcll(__ballot(longs != 0));
+    if (per_lane <= wave) {
+#pragma unroll
+      for (int k = 0; k < kMsgSlots; ++k)
+        if (longs & (1u << k))
+          if (record_crc(t, nib, g.base, rk, g.reg0 + jo[k], jl[k]) != ex[k]) status |= record_bit(k);
+      longs = 0;
+    }
+  }
   for (;;) {
     const uint64_t ball = __ballot(longs != 0);
     if (ball == 0) break;
