@@ -11,7 +11,7 @@ for c in $CASES; do
   d=gpurun_out/kt/$TAG/$c
   mkdir -p $d
   timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $d/raw -o kt -- python3 tools/probes/pmc_case.py $c --reps $REPS > $d/kt.log 2>&1
-  find $d/raw -mindepth 2 -name '*.csv' -exec cp {} $d/ \;
+  find $d/raw -name '*.csv' -exec cp {} $d/ \;
   rm -rf $d/raw
   echo "case $c done"
 done
