@@ -1744,11 +1744,13 @@ __global__ __launch_bounds__(1024) void region_fused_kernel(FusedArgs f) {
         }
       }
     };
-    auto hash = [&](uint64_t sb, uint32_t u, u32x4 (&cur)[4]) {
+    auto hash = [&](uint64_t sb, uint32_t u, u32x4 (&cur)[4]) -> uint32_t {
       if constexpr (COPY) copy(sb, cur);
       region_sb_zero(a, sb, lane, cur);
       quad_transpose_asm(cur);
-      buf[64u * u + slot] = run_crc<4, 1>(cur, k, 0u);
+      const uint32_t r = run_crc<4, 1>(cur, k, 0u);
+      buf[64u * u + slot] = r;
+      return r;
     };
     if (mine) {
       u32x4 b0[4], b1[4], b2[4], b3[4];
@@ -1758,12 +1760,19 @@ __global__ __launch_bounds__(1024) void region_fused_kernel(FusedArgs f) {
       region_sb_load(a, 4 * g + 2, lane, b2);
       region_sb_load(a, 4 * g + 3, lane, b3);
       for (uint64_t j = 0; j < mine; ++j, g += nstream) {
-        if (j) {  // the previous group's store has completed: publish it
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          __hip_atomic_store(&done[v], (uint32_t)j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
         const uint64_t nx = j + 1 < mine ? g + nstream : g;  // the last group re-reads itself
-        hash(4 * g, 0, b0);
+        const uint32_t r0 = hash(4 * g, 0, b0);
+        if (j >= 2) {
+          // Group j's first loads have landed (r0 used them), and vector memory operations retire in
+          // issue order, so the sum store of group j - 2 (issued before them) is in L2: groups
+          // 0 .. j - 2 of this wave are complete. z = 0, computed from r0, so the LDS store below
+          // cannot move above that wait; no s_waitcnt vmcnt(0), which would also drain the loads
+          // in flight.
+          uint32_t z;
+          asm volatile("v_mov_b32 %0, 0" : "=v"(z) : "v"(r0));
+          __hip_atomic_store(&done[v], (uint32_t)j - 1u + __builtin_amdgcn_readfirstlane(z), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
         __builtin_amdgcn_s_setprio(3);
         region_sb_load(a, 4 * nx, lane, b0);
         __builtin_amdgcn_s_setprio(0);
@@ -1857,7 +1866,20 @@ __global__ __launch_bounds__(256) void region_tail_kernel(FusedArgs f) {
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-  for (uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); 64 * w < n; w += waves) {
+  const uint64_t w0 = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (n <= waves) {
+    // Few messages (the share boundaries' deferrals): a wave per message, every record by the
+    // whole wave -- a lane alone would walk a 64 KiB record's run sums one dependent load at a time.
+    for (uint64_t w = w0; w < n; w += waves) {
+      const uint64_t i = all ? w : f.defer[w];
+      uint32_t st;
+      uint64_t mend;
+      region::process_message_wave(f.a, f.g, tbl, nib, i, lane, st, mend);
+      if constexpr (COPY) region::transform_fast(f, tbl, lane == 0, i, st, mend);
+    }
+    return;
+  }
+  for (uint64_t w = w0; 64 * w < n; w += waves) {
     const uint64_t j = 64 * w + lane;
     const bool have = j < n;
     const uint64_t i = have ? (all ? j : f.defer[j]) : 0;
@@ -1879,7 +1901,7 @@ hipError_t launch_region_fused(const FusedArgs& f, int num_cu, hipStream_t s) {
     return hipGetLastError();
   }
   uint64_t blocks = (f.a.m + 255) / 256;
-  if (blocks > (uint64_t)num_cu * 2) blocks = (uint64_t)num_cu * 2;
+  if (blocks > (uint64_t)num_cu * 4) blocks = (uint64_t)num_cu * 4;
   if (copy) hipLaunchKernelGGL(region_tail_kernel<true>, dim3((uint32_t)blocks), dim3(256), 0, s, f);
   else hipLaunchKernelGGL(region_tail_kernel<false>, dim3((uint32_t)blocks), dim3(256), 0, s, f);
   return hipGetLastError();

@@ -56,6 +56,7 @@ __device__ __noinline__ uint32_t record_crc_wave(const uint32_t* __restrict__ t,
                                                  const uint8_t* __restrict__ base, const uint32_t* __restrict__ rk,
                                                  const uint32_t* __restrict__ img, uint64_t pa, uint64_t len,
                                                  uint32_t lane) {
+  if (len < 4) return record_crc(t, nib, base, rk, pa, len);  // bytes, no runs (every lane the same)
   const uint64_t pb = pa + len;
   const uint64_t A0 = pa & ~uint64_t(63), B1 = (pb + 63) & ~uint64_t(63);
   const int64_t n = (int64_t)((B1 - A0) >> 6), k0 = (int64_t)(A0 >> 6);
@@ -221,6 +222,35 @@ __device__ __forceinline__ void process_message(const MsgArgs& a, const RegionAr
   }
   st_ret = have ? status : ~0u;
   end_ret = end;
+}
+
+// process_message for ONE message by the whole wave (every lane passes the same i): the parse is
+// repeated in every lane (the same loads, broadcast), each record's CRC is record_crc_wave.
+__device__ __forceinline__ void process_message_wave(const MsgArgs& a, const RegionArgs& g,
+                                                     const uint32_t* __restrict__ t, const uint32_t* __restrict__ nib,
+                                                     uint64_t i, uint32_t lane, uint32_t& st_ret, uint64_t& end_ret) {
+  const uint32_t* rk = g.rk + kRunPad;
+  const uint64_t off = a.msg_off[i];
+  const bool in_region = off <= a.region_len;
+  const uint64_t rem = in_region ? a.region_len - off : 0;
+  const uint8_t* p = a.region + (in_region ? off : 0);
+  const HeaderWords hw = load_header(p, rem);
+  MsgParse r;
+  PropsFields pf;
+  bool pf_ok = false;
+  parse_message<false, false>(off, in_region, rem, p, hw, t, nullptr, 0, r, pf, pf_ok);
+  uint32_t status = r.status;
+#pragma unroll 1
+  for (int k = 0; k < kMsgSlots; ++k) {
+    if (r.jl[k] == 0) continue;
+    if (record_crc_wave(t, nib, g.base, rk, g.img, g.reg0 + r.jo[k], r.jl[k], lane) != r.ex[k]) status |= record_bit(k);
+  }
+  if (lane == 0) {
+    a.status[i] = status;
+    if (a.msg_end) a.msg_end[i] = r.end ? off + r.end : 0;
+  }
+  st_ret = status;
+  end_ret = r.end;
 }
 
 // The transform's fast path for message i (FusedArgs::out; verify status st, end `end`): a clean
