@@ -1761,6 +1761,9 @@ __global__ __launch_bounds__(1024) void region_fused_kernel(FusedArgs f) {
       region_sb_load(a, 4 * g + 3, lane, b3);
       for (uint64_t j = 0; j < mine; ++j, g += nstream) {
         const uint64_t nx = j + 1 < mine ? g + nstream : g;  // the last group re-reads itself
+        // COPY: a message that cannot take the fast path anywhere ends the pass (the general path
+        // redoes the batch); every 8th group, one L2 read
+        if (COPY && (j & 7) == 7 && __hip_atomic_load(f.xfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
         const uint32_t r0 = hash(4 * g, 0, b0);
         if (j >= 2) {
           // Group j's first loads have landed (r0 used them), and vector memory operations retire in
@@ -1828,6 +1831,7 @@ __global__ __launch_bounds__(1024) void region_fused_kernel(FusedArgs f) {
     asm volatile("" ::: "memory");  // no run-sum load above the poll
   };
   for (uint64_t b = M0 + 64 * (uint64_t)p; b < M1; b += 64 * (uint64_t)f.nproc) {
+    if (COPY && __hip_atomic_load(f.xfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;  // as the streamers
     const uint64_t i = b + lane;
     const bool have = i < M1;
     // First wait: until the next batch's first message (for back-to-back messages the end of this

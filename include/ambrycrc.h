@@ -263,8 +263,14 @@ int ambrycrc_serialize_puts_dev(const ambrycrc_put_desc* d_desc, size_t m, const
  * transformed), d_out_len (0 when not transformed), d_out_off (nullable; the message's offset in
  * d_out). Bytes of d_out outside the returned spans are unspecified (a clean batch is copied while
  * it is verified; a batch with a failing message is then rebuilt). d_out must not overlap the
- * region. Asynchronous on `stream`; d_ws >= ambrycrc_transform_workspace_bytes(m) or NULL. The
- * store-key comparison with the index entry stays with the caller (it owns the StoreKey type). */
+ * region. Enqueued on `stream`; d_ws >= ambrycrc_transform_workspace_bytes(m) or NULL. The
+ * store-key comparison with the index entry stays with the caller (it owns the StoreKey type).
+ * Fast path (header_version 3, region mode 1, workspace room for the region's run sums -- the
+ * default workspace has it): one pass verifies the messages while copying the region into d_out
+ * and rewrites the headers' life versions; it takes the batch when every message is a clean PUT
+ * stored at header V3 with VERSION_5 properties and a Blob_Format_V3 record, back to back from
+ * d_msg_off[0]. The call then synchronizes with `stream` once to learn whether it did, and returns
+ * (done) or enqueues the general path (not done), which gives the same outputs. */
 size_t ambrycrc_transform_workspace_bytes(size_t m);
 
 /* Output size contract of the transform. A transformed message is at most
