@@ -1669,7 +1669,7 @@ __device__ __forceinline__ uint64_t msg_pos(const FusedArgs& f, uint64_t i) {
 
 // Smallest i in [0, m] with msg_pos(i) >= key (sorted offsets), by 64-way probes; every lane
 // gets it. Unsorted offsets give some index in [0, m] (the tail kernel redoes them all).
-__device__ uint64_t lower_bound_wave(const FusedArgs& f, uint64_t key, uint32_t lane) {
+__device__ __forceinline__ uint64_t lower_bound_wave(const FusedArgs& f, uint64_t key, uint32_t lane) {
   uint64_t lo = 0, hi = f.a.m;  // answer in [lo, hi]
   while (hi - lo > 64) {
     const uint64_t n = hi - lo;
@@ -1714,7 +1714,7 @@ __global__ __launch_bounds__(1024) void region_fused_kernel(FusedArgs f) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t v = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t G0 = f.ngroups * blockIdx.x / gridDim.x, G1 = f.ngroups * (blockIdx.x + 1) / gridDim.x;
-  const RegionArgs& a = f.g;
+  const RegionArgs a = f.g;
   const uint32_t nstream = 16u - f.nproc;
   if (v < nstream) {
     // ---- streaming wave
