@@ -52,10 +52,22 @@ __device__ __forceinline__ uint32_t wave_fold(uint32_t s, uint32_t c, uint32_t l
 // record_crc); each lane folds its slice with record_crc's four Horner streams, then a DPP tree
 // merges the lanes with the shifts x^(8*256*gs*2^k) (gf2_mul by wave-uniform constants from the
 // image's x^(8*2^k) words), and the register at B1 is un-shifted to pb.
-__device__ __noinline__ uint32_t record_crc_wave(const uint32_t* __restrict__ t, const uint32_t* __restrict__ nib,
-                                                 const uint8_t* __restrict__ base, const uint32_t* __restrict__ rk,
-                                                 const uint32_t* __restrict__ img, uint64_t pa, uint64_t len,
+typedef const __attribute__((address_space(3))) uint32_t lds_u32;
+typedef const __attribute__((address_space(1))) uint32_t glb_u32;
+typedef const __attribute__((address_space(1))) uint8_t glb_u8;
+
+// Not inlined (it would add to its callers' register pressure), so its pointer arguments arrive as
+// generic pointers: they are cast back to their address spaces (t, nib: LDS; base, rk, img: global)
+// so the accesses below are ds_read / global_load, not flat (a flat access waits on both counters).
+__device__ __noinline__ uint32_t record_crc_wave(const uint32_t* __restrict__ t_g, const uint32_t* __restrict__ nib_g,
+                                                 const uint8_t* __restrict__ base_g, const uint32_t* __restrict__ rk_g,
+                                                 const uint32_t* __restrict__ img_g, uint64_t pa, uint64_t len,
                                                  uint32_t lane) {
+  const uint32_t* __restrict__ t = (const uint32_t*)(lds_u32*)t_g;
+  const uint32_t* __restrict__ nib = (const uint32_t*)(lds_u32*)nib_g;
+  const uint8_t* __restrict__ base = (const uint8_t*)(glb_u8*)base_g;
+  const uint32_t* __restrict__ rk = (const uint32_t*)(glb_u32*)rk_g;
+  const uint32_t* __restrict__ img = (const uint32_t*)(glb_u32*)img_g;
   if (len < 4) return record_crc(t, nib, base, rk, pa, len);  // bytes, no runs (every lane the same)
   const uint64_t pb = pa + len;
   const uint64_t A0 = pa & ~uint64_t(63), B1 = (pb + 63) & ~uint64_t(63);
