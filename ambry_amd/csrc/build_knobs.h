@@ -61,8 +61,11 @@
 #ifndef AMBRY_RUNS_PROBE  // 1 = no run sums into LDS, 5 = no global stores, 6 = stores to one line set
 #define AMBRY_RUNS_PROBE 0
 #endif
+#ifndef AMBRY_FUSED_PROBE  // one-pass kernel: 1 = processors do nothing (the streaming alone)
+#define AMBRY_FUSED_PROBE 0
+#endif
 
-#if (AMBRY_REGION_PROBE != 0 || AMBRY_RUNS_PROBE != 0 || defined(AMBRYCRC_DIAGNOSTICS) || \
+#if (AMBRY_REGION_PROBE != 0 || AMBRY_RUNS_PROBE != 0 || AMBRY_FUSED_PROBE != 0 || defined(AMBRYCRC_DIAGNOSTICS) || \
      defined(AMBRY_AB_SPLIT_GROUP)) && !defined(AMBRY_AB_PROBE_BUILD)
 #error "probe / diagnostic knobs build a library that returns wrong CRCs or runs unshipped kernels: define AMBRY_AB_PROBE_BUILD (tools/ab_build.sh does)"
 #endif
@@ -73,7 +76,7 @@
   X(AMBRY_FUSED_PROC, 0)                                                                                      \
   X(AMBRY_GRP_PRIO, 0) X(AMBRY_GRP_IL, 4) X(AMBRY_C0_G, 2) X(AMBRY_C0_NB, 8) X(AMBRY_C1_MAX, 1024)           \
   X(AMBRY_RUNS_STORE_NT, 0) X(AMBRY_RUNS_GIL, 1) X(AMBRY_PLAN_PER_BLOCK, 2048) X(AMBRY_DEFAULT_VARIANT, 29) \
-  X(AMBRY_REGION_PROBE, 0) X(AMBRY_RUNS_PROBE, 0)
+  X(AMBRY_REGION_PROBE, 0) X(AMBRY_RUNS_PROBE, 0) X(AMBRY_FUSED_PROBE, 0)
 
 #if defined(AMBRY_AB_PROBE_BUILD)
 #define AMBRY_IS_PROBE_BUILD 1

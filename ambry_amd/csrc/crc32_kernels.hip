@@ -1800,6 +1800,7 @@ __global__ __launch_bounds__(1024) void region_fused_kernel(FusedArgs f) {
     return;
   }
   // ---- processor wave
+  if (AMBRY_FUSED_PROBE == 1) return;  // A/B probe: the streaming alone (wrong statuses)
   const uint32_t p = v - nstream;
   const uint64_t s_lo = G0 * kGroupBytes, s_hi = G1 * kGroupBytes;  // the share, base-relative
   {  // this wave's slice of the global sortedness check
