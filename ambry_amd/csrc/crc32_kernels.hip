@@ -1840,7 +1840,8 @@ __global__ __launch_bounds__(1024) void region_fused_kernel(FusedArgs f) {
     wait_for(b + 64 < f.a.m ? msg_pos(f, b + 64) : s_hi);
     uint32_t st;
     uint64_t mend;
-    region::process_message(f.a, f.g, tbl, nib, have, i, lane, st, mend, [&](uint64_t pos, uint64_t end) -> bool {
+    const region::TabR tr{reinterpret_cast<const uint8_t*>(g_lds_runs), (lane & 31u) << 2};
+    region::process_message(f.a, f.g, tbl, tr, nib, have, i, lane, st, mend, [&](uint64_t pos, uint64_t end) -> bool {
       // the lane's message ends at pos + end (base-relative): past the share or before it -> the tail's
       if (pos < s_lo || pos + end > s_hi) {
         const uint32_t at = atomicAdd(f.ctl + 1, 1u);
@@ -1890,7 +1891,7 @@ __global__ __launch_bounds__(256) void region_tail_kernel(FusedArgs f) {
     const uint64_t i = have ? (all ? j : f.defer[j]) : 0;
     uint32_t st;
     uint64_t mend;
-    region::process_message(f.a, f.g, tbl, nib, have, i, lane, st, mend,
+    region::process_message(f.a, f.g, tbl, region::TabC{tbl}, nib, have, i, lane, st, mend,
                             [](uint64_t, uint64_t) -> bool { return true; }, [](uint64_t) {});
     if constexpr (COPY) region::transform_fast(f, tbl, have, i, st, mend);
   }

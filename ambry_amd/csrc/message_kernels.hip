@@ -134,7 +134,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AMBRY_REGIO
 #if AMBRY_REGION_PROBE == 1
       const uint32_t c = ex;
 #else
-      const uint32_t c = jl ? region::record_crc(tbl, nib, g.base, rk, g.reg0 + jo, jl) : 0u;
+      const uint32_t c = jl ? region::record_crc(region::TabC{tbl}, nib, g.base, rk, g.reg0 + jo, jl) : 0u;
 #endif
       if (c != ex) status |= AMBRYCRC_MSG_ENCKEY_CRC << k;
     }

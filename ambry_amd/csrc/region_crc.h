@@ -57,6 +57,27 @@ __device__ __forceinline__ uint32_t step4(const uint32_t* __restrict__ t, uint32
   return t[768 + (x & 0xffu)] ^ t[512 + ((x >> 8) & 0xffu)] ^ t[256 + ((x >> 16) & 0xffu)] ^ t[x >> 24];
 }
 
+// Slice-by-4 table access for hash_run / record_crc. TabC: the compact one-copy tables t[256j + b]
+// (stage_slice_tables; lanes looking up different bytes conflict on LDS banks). TabR: the
+// lane-column replicated slice tables of the streaming kernels (crc32_layout.h: T_j[b] at
+// (j>>1)<<16 | b<<8 | (j&1)<<7 | (lane&31)<<2), conflict-free -- the one-pass kernel's processors
+// use them so their lookups do not take LDS cycles from the streamers beside them.
+struct TabC {
+  const uint32_t* __restrict__ t;
+  __device__ __forceinline__ uint32_t step4(uint32_t x) const { return region::step4(t, x); }
+  __device__ __forceinline__ uint32_t t0(uint32_t b) const { return t[b]; }
+};
+struct TabR {
+  const uint8_t* __restrict__ lds;  // the slice tables' base
+  uint32_t col;                     // (lane & 31) << 2
+  __device__ __forceinline__ uint32_t ld(uint32_t a) const { return *reinterpret_cast<const uint32_t*>(lds + a); }
+  __device__ __forceinline__ uint32_t step4(uint32_t x) const {
+    return ld((1u << 16) | (1u << 7) | ((x & 0xffu) << 8) | col) ^ ld((1u << 16) | (((x >> 8) & 0xffu) << 8) | col) ^
+           ld((1u << 7) | (((x >> 16) & 0xffu) << 8) | col) ^ ld(((x >> 24) << 8) | col);
+  }
+  __device__ __forceinline__ uint32_t t0(uint32_t b) const { return ld((b << 8) | col); }
+};
+
 // Bytes of a little-endian word w at run byte offsets [4w, 4w + 4) with offset >= lo / < hi.
 __device__ __forceinline__ uint32_t keep_ge(int d) {  // bytes at index >= d (d = lo - 4w)
   return d <= 0 ? 0xFFFFFFFFu : (d >= 4 ? 0u : (0xFFFFFFFFu << (8 * d)));
@@ -79,8 +100,9 @@ __device__ __forceinline__ void load_run(const uint8_t* __restrict__ base, uint6
 // Raw CRC register at the end of that run over its bytes [lo, hi) (others zero), with 0xFF XORed
 // into bytes [lo, lo + ninit): four independent 4-step chains, one per piece, merged by x^(8*16)
 // and x^(8*32) (depth 4 + 2 instead of 16 dependent steps).
-__device__ __forceinline__ uint32_t hash_run(const uint32_t* __restrict__ t, const uint32_t* __restrict__ nib,
-                                             const u32x4 (&w)[4], int lo, int hi, int ninit) {
+template <class Tab>
+__device__ __forceinline__ uint32_t hash_run(const Tab& t, const uint32_t* __restrict__ nib, const u32x4 (&w)[4],
+                                             int lo, int hi, int ninit) {
   uint32_t p[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -90,7 +112,7 @@ __device__ __forceinline__ uint32_t hash_run(const uint32_t* __restrict__ t, con
       const int o = 16 * q + 4 * d;
       uint32_t v = w[q][d] & keep_ge(lo - o) & keep_lt(hi - o);
       v ^= keep_ge(lo - o) & keep_lt(lo + ninit - o);
-      s = step4(t, s ^ v);
+      s = t.step4(s ^ v);
     }
     p[q] = s;
   }
@@ -122,14 +144,15 @@ __device__ __forceinline__ void load_groups(const uint32_t* __restrict__ rk, int
 // zlib CRC-32 of the len bytes at offset pa from base; rk = RegionArgs::rk + kRunPad. Every load
 // is issued before the first is used (head and tail runs, the first 16 run sums), and each
 // Horner step group prefetches the next 16 sums.
-__device__ __forceinline__ uint32_t record_crc(const uint32_t* __restrict__ t, const uint32_t* __restrict__ nib,
+template <class Tab>
+__device__ __forceinline__ uint32_t record_crc(const Tab& t, const uint32_t* __restrict__ nib,
                                                const uint8_t* __restrict__ base, const uint32_t* __restrict__ rk,
                                                uint64_t pa, uint64_t len) {
   if (len == 0) return 0;
   const uint64_t pb = pa + len;
   if (len < 4) {
     uint32_t c = 0xFFFFFFFFu;
-    for (uint64_t i = pa; i < pb; ++i) c = t[(c ^ base[i]) & 0xffu] ^ (c >> 8);
+    for (uint64_t i = pa; i < pb; ++i) c = t.t0((c ^ base[i]) & 0xffu) ^ (c >> 8);
     return ~c;
   }
   const uint64_t A0 = pa & ~uint64_t(63), B1 = (pb + 63) & ~uint64_t(63);
@@ -175,6 +198,12 @@ __device__ __forceinline__ uint32_t record_crc(const uint32_t* __restrict__ t, c
   for (uint32_t k = 0; k < kInvPowSets; ++k)
     if (d & (1u << k)) V = nmul(nib, V, kInv0 + k);
   return ~V;
+}
+
+__device__ __forceinline__ uint32_t record_crc(const uint32_t* __restrict__ t, const uint32_t* __restrict__ nib,
+                                               const uint8_t* __restrict__ base, const uint32_t* __restrict__ rk,
+                                               uint64_t pa, uint64_t len) {
+  return record_crc(TabC{t}, nib, base, rk, pa, len);
 }
 
 }  // namespace region

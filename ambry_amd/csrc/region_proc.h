@@ -68,7 +68,8 @@ __device__ __noinline__ uint32_t record_crc_wave(const uint32_t* __restrict__ t_
   const uint8_t* __restrict__ base = (const uint8_t*)(glb_u8*)base_g;
   const uint32_t* __restrict__ rk = (const uint32_t*)(glb_u32*)rk_g;
   const uint32_t* __restrict__ img = (const uint32_t*)(glb_u32*)img_g;
-  if (len < 4) return record_crc(t, nib, base, rk, pa, len);  // bytes, no runs (every lane the same)
+  const TabC tc{t};
+  if (len < 4) return record_crc(tc, nib, base, rk, pa, len);  // bytes, no runs (every lane the same)
   const uint64_t pb = pa + len;
   const uint64_t A0 = pa & ~uint64_t(63), B1 = (pb + 63) & ~uint64_t(63);
   const int64_t n = (int64_t)((B1 - A0) >> 6), k0 = (int64_t)(A0 >> 6);
@@ -83,9 +84,9 @@ __device__ __noinline__ uint32_t record_crc_wave(const uint32_t* __restrict__ t_
   u32x4 hw[4], tw[4];
   load_run(base, A0, lo, hi, hw);
   load_run(base, B1 - 64, 0, tail_bytes ? thi : 0, tw);
-  uint32_t H = hash_run(t, nib, hw, lo, hi, tin < 4 ? tin : 4);
+  uint32_t H = hash_run(tc, nib, hw, lo, hi, tin < 4 ? tin : 4);
   if (tin < 4) H ^= 0xFFFFFFFFu >> (8 * tin);
-  const uint32_t T = tail_bytes ? hash_run(t, nib, tw, 0, thi, 0) : 0u;
+  const uint32_t T = tail_bytes ? hash_run(tc, nib, tw, 0, thi, 0) : 0u;
   // this lane's groups [g0, g0 + gs) counted from e0; groups wholly before k0 are zero
   const int64_t g0 = (int64_t)lane * gs;
   uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
@@ -133,11 +134,13 @@ __device__ __noinline__ uint32_t record_crc_wave(const uint32_t* __restrict__ t_
 // keep(pos, end): called for a parsed message whose records need CRCs (pos: its base-relative
 // start, end: its length); false = the lane drops it (deferred: no status written, st_ret ~0).
 // wait(need): the whole wave waits until every run up to base-relative `need` exists.
-template <class Keep, class Wait>
+// tr: the table access of the per-lane record CRCs (TabR in the one-pass kernel, TabC elsewhere).
+template <class Tab, class Keep, class Wait>
 __device__ __forceinline__ void process_message(const MsgArgs& a, const RegionArgs& g,
-                                                const uint32_t* __restrict__ t, const uint32_t* __restrict__ nib,
-                                                bool have, uint64_t i, uint32_t lane, uint32_t& st_ret,
-                                                uint64_t& end_ret, Keep keep, Wait wait) {
+                                                const uint32_t* __restrict__ t, const Tab& tr,
+                                                const uint32_t* __restrict__ nib, bool have, uint64_t i,
+                                                uint32_t lane, uint32_t& st_ret, uint64_t& end_ret, Keep keep,
+                                                Wait wait) {
   const uint32_t* rk = g.rk + kRunPad;
   uint32_t status = 0;
   uint64_t end = 0, off = 0;
@@ -181,7 +184,7 @@ __device__ __forceinline__ void process_message(const MsgArgs& a, const RegionAr
       longs |= 1u << k;
       continue;
     }
-    if (record_crc(t, nib, g.base, rk, pa, jl[k]) != ex[k]) status |= record_bit(k);
+    if (record_crc(tr, nib, g.base, rk, pa, jl[k]) != ex[k]) status |= record_bit(k);
   }
   // The long records: the wave takes them one by one, unless enough lanes have one that the lanes
   // doing their own in parallel finish first (a lane's chain is runs/4 nibble multiplies deep; the
@@ -200,7 +203,7 @@ __device__ __forceinline__ void process_message(const MsgArgs& a, const RegionAr
 #pragma unroll
       for (int k = 0; k < kMsgSlots; ++k)
         if (longs & (1u << k))
-          if (record_crc(t, nib, g.base, rk, g.reg0 + jo[k], jl[k]) != ex[k]) status |= record_bit(k);
+          if (record_crc(tr, nib, g.base, rk, g.reg0 + jo[k], jl[k]) != ex[k]) status |= record_bit(k);
       longs = 0;
     }
   }
