@@ -982,11 +982,13 @@ size_t msg_jobs_bytes(size_t m) {
 
 // A processor wave finishes a 64-message batch in ~20-40 us (a chain of dependent reads under the
 // streamers' load), so the processors a CU needs grow with its messages; the rest of its 16 waves
-// stream. One processor per 512 messages per CU, 2 to kFusedProcMax.
+// stream. One processor per 128 messages per CU, 2 to 10 (r04f sweep: 4 KiB blobs, 1,024 messages
+// per CU, best at 8; 1 KiB blobs, 2,048, at 8-10; 100-B blobs, 4,096, at 10; 8 streamers alone
+// stream a 1.38 GB region in 285 us).
 uint32_t fused_proc_waves(const DevCtx* c, size_t m) {
   if (c->fused_proc > 0) return (uint32_t)std::min(c->fused_proc, kFusedProcMax);
   const size_t per_cu = m / (size_t)std::max(1, c->num_cu);
-  return (uint32_t)std::max<size_t>(2, std::min<size_t>(kFusedProcMax, (per_cu + 511) / 512));
+  return (uint32_t)std::max<size_t>(2, std::min<size_t>(10, (per_cu + 127) / 128));
 }
 
 int enqueue_messages(DevCtx* c, const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off, size_t m,

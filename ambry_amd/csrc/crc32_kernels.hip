@@ -1733,7 +1733,7 @@ __global__ __launch_bounds__(1024) void region_fused_kernel(FusedArgs f) {
         const uint64_t d0 = p >= shift ? p - shift : 0;               // its first output byte
         if (d0 >= f.out_cap) continue;
         if (p >= shift && d0 + 16 <= f.out_cap) {
-          st16u(f.out + (p - shift), cur[q]);
+          st16u_nt(f.out + (p - shift), cur[q]);  // streamed once: nontemporal
         } else {  // the piece holding out[0] or out[out_cap - 1]: byte by byte (rare)
           const u32x4 v = cur[q];
 #pragma unroll 1
