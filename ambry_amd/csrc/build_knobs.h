@@ -61,7 +61,7 @@
 #ifndef AMBRY_RUNS_PROBE  // 1 = no run sums into LDS, 5 = no global stores, 6 = stores to one line set
 #define AMBRY_RUNS_PROBE 0
 #endif
-#ifndef AMBRY_FUSED_PROBE  // one-pass kernel: 1 = processors do nothing (the streaming alone)
+#ifndef AMBRY_FUSED_PROBE  // one-pass kernel: 1 = processors do nothing (the streaming alone), 2 = timestamps
 #define AMBRY_FUSED_PROBE 0
 #endif
 

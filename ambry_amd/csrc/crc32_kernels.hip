@@ -1690,8 +1690,17 @@ __device__ __forceinline__ uint64_t lower_bound_wave(const FusedArgs& f, uint64_
   return lo + (uint64_t)__popcll(ball);
 }
 
+#if AMBRY_FUSED_PROBE == 2
+// A/B probe: per workgroup, s_memrealtime (100 MHz) at entry, when its last streamer finished and
+// when its last processor finished (ambrycrc_debug_fused_times).
+__device__ unsigned long long g_fused_t[3 * 2048];
+#endif
+
 template <bool COPY>
 __global__ __launch_bounds__(1024) void region_fused_kernel(FusedArgs f) {
+#if AMBRY_FUSED_PROBE == 2
+  if (threadIdx.x == 0) g_fused_t[3 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+#endif
   __shared__ uint32_t tbl[1024];
   __shared__ uint32_t nib[region::kSets * region::kNibWords];
   __shared__ uint32_t done[16];
@@ -1797,6 +1806,9 @@ __global__ __launch_bounds__(1024) void region_fused_kernel(FusedArgs f) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __hip_atomic_store(&done[v], (uint32_t)mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#if AMBRY_FUSED_PROBE == 2
+    if (lane == 0) atomicMax(&g_fused_t[3 * blockIdx.x + 1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#endif
     return;
   }
   // ---- processor wave
@@ -1852,6 +1864,9 @@ __global__ __launch_bounds__(1024) void region_fused_kernel(FusedArgs f) {
     }, [&](uint64_t need) { wait_for(need); });
     if constexpr (COPY) region::transform_fast(f, tbl, st != ~0u, i, st, mend);
   }
+#if AMBRY_FUSED_PROBE == 2
+  if (lane == 0) atomicMax(&g_fused_t[3 * blockIdx.x + 2], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#endif
 }
 
 // The deferred messages (or, with ctl[0] set, every message) once all run sums exist: one lane
@@ -1897,7 +1912,15 @@ __global__ __launch_bounds__(256) void region_tail_kernel(FusedArgs f) {
   }
 }
 
+#if AMBRY_FUSED_PROBE == 2
+extern "C" int ambrycrc_debug_fused_times(unsigned long long* out, int n) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fused_t), sizeof(unsigned long long) * 3 * n) != hipSuccess) return -2;
+  return 0;
+}
+#endif
+
 hipError_t launch_region_fused(const FusedArgs& f, int num_cu, hipStream_t s) {
+
   if (f.a.m == 0) return hipSuccess;
   const bool copy = f.out != nullptr;
   if (f.ngroups) {
