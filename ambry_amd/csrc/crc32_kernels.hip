@@ -1847,9 +1847,10 @@ __global__ __launch_bounds__(1024) void region_fused_kernel(FusedArgs f) {
     if (COPY && __hip_atomic_load(f.xfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;  // as the streamers
     const uint64_t i = b + lane;
     const bool have = i < M1;
-    // First wait: until the next batch's first message (for back-to-back messages the end of this
-    // batch's last one); the processor waits again only for a message that runs further.
-    wait_for(b + 64 < f.a.m ? msg_pos(f, b + 64) : s_hi);
+    // The batch is parsed at once (headers, properties, record heads, stored CRCs: region bytes,
+    // there whether streamed or not), then the processor waits until the frontier passes its
+    // messages' ends and assembles their record CRCs: after the last group of a share, only that
+    // last step is left.
     uint32_t st;
     uint64_t mend;
     const region::TabR tr{reinterpret_cast<const uint8_t*>(g_lds_runs), (lane & 31u) << 2};
