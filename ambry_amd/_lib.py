@@ -139,6 +139,7 @@ _SIGNATURES = [
     ("ambrycrc_set_region_mode", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     ("ambrycrc_get_region_mode", ctypes.c_int, [ctypes.c_int]),
     ("ambrycrc_last_message_mode", ctypes.c_int, [ctypes.c_int]),
+    ("ambrycrc_last_transform_path", ctypes.c_int, [ctypes.c_int]),
     ("ambrycrc_set_grid", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     ("ambrycrc_set_window", ctypes.c_int, [ctypes.c_int, ctypes.c_uint64]),
     ("ambrycrc_timing_enable", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),

@@ -601,7 +601,12 @@ int ambrycrc_init(int device) {
     const long x = strtol(v, &end, 10);
     if (end != v && *end == '\0' && x >= 0 && x < 1000 && variant_supported((int)x)) c->variant = (int)x;
   }
-  if (const char* v = getenv("AMBRYCRC_REGION")) c->region_mode = strcmp(v, "0") == 0 ? 0 : strcmp(v, "2") == 0 ? 2 : 1;
+  if (const char* v = getenv("AMBRYCRC_REGION")) c->region_mode = strcmp(v, "0") == 0 ? 0 : strcmp(v, "1") == 0 ? 1 : 2;
+  if (const char* v = getenv("AMBRYCRC_XFORM_FAST_MAX")) {  // A/B: the transform fast path's cut-off
+    char* end = nullptr;
+    const unsigned long long x = strtoull(v, &end, 10);
+    if (end != v && *end == '\0' && x <= (1ull << 30)) c->xform_fast_max = x;
+  }
   if (const char* v = getenv("AMBRYCRC_FUSED_PROC")) {  // A/B: processor waves of the one-pass kernels
     char* end = nullptr;
     const long x = strtol(v, &end, 10);
@@ -873,6 +878,11 @@ int ambrycrc_get_region_mode(int device) {
 int ambrycrc_last_message_mode(int device) {
   DevCtx* c = ctx_for(device);
   return c ? c->last_msg_mode.load() : AMBRYCRC_ENOINIT;
+}
+
+int ambrycrc_last_transform_path(int device) {
+  DevCtx* c = ctx_for(device);
+  return c ? c->last_xform_path.load() : AMBRYCRC_ENOINIT;
 }
 
 int ambrycrc_get_variant(int device) {

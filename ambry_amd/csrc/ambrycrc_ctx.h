@@ -77,11 +77,16 @@ struct DevCtx {
   int variant = AMBRY_DEFAULT_VARIANT;  // (A/B builds: -DAMBRY_DEFAULT_VARIANT=...)
   // Message verify of regions of at most kRegionMaxPerMessage bytes per message: region mode
   // (region_runs_kernel + region_msg_kernel) instead of jobs through the batch engine.
-  // 1: one pass (region_fused_kernel + region_tail_kernel), 2: two passes (region_runs_kernel +
-  // region_msg_kernel, kept for A/B), 0: off.
-  int region_mode = 1;
+  // 2 (default): two passes (region_runs_kernel, then region_msg_kernel: one thread per message),
+  // 1: one pass (region_fused_kernel + region_tail_kernel; measured 1.5-14 % slower, DESIGN.md
+  // §10.1), 0: off. The transform's fast path is the one-pass kernel's copy form whenever region
+  // mode is on and the region holds at most xform_fast_max bytes per message.
+  int region_mode = 2;
+  uint64_t xform_fast_max = kXformFastMaxPerMessage;
   // The form the last message verify on this device took (ambrycrc_last_message_mode).
   std::atomic<int> last_msg_mode{-1};
+  // The path the last transform took (ambrycrc_last_transform_path): 1 fast, 0 general.
+  std::atomic<int> last_xform_path{-1};
   // Processor waves of the one-pass kernels (0: per call, fused_proc_waves); AMBRYCRC_FUSED_PROC.
   int fused_proc = AMBRY_FUSED_PROC;
   uint64_t region_max = kRegionMaxPerMessage;  // region bytes per message up to which it applies

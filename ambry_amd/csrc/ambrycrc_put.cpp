@@ -213,7 +213,8 @@ int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len
   // for the run sums (the library's own workspace is sized for them; a caller's as given).
   const size_t base_need = ambrycrc_transform_workspace_bytes(m);
   const size_t fast_need = transform_own_bytes(m) + ws_need(m) + transform_fast_bytes(d_region, region_len, m);
-  const bool want_fast = header_version == 3 && c->region_mode == 1 && region_len > 0;
+  const bool want_fast = header_version == 3 && c->region_mode != 0 && region_len > 0 &&
+                         region_len <= c->xform_fast_max * (uint64_t)m;
   const size_t need = want_fast && !d_ws ? std::max(base_need, fast_need) : base_need;
   WsLease lease;
   int rc = lease.acquire(c, stream, &d_ws, ws_bytes, need);
@@ -313,9 +314,13 @@ int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len
     if (hipMemcpyAsync(&h_xfail, xfail, sizeof h_xfail, hipMemcpyDeviceToHost, stream) != hipSuccess ||
         hipStreamSynchronize(stream) != hipSuccess)
       return AMBRYCRC_EHIP;
-    if (h_xfail == 0) return AMBRYCRC_OK;
+    if (h_xfail == 0) {
+      c->last_xform_path.store(1);
+      return AMBRYCRC_OK;
+    }
     if (hipMemsetAsync(fail, 0, sizeof(uint32_t), stream) != hipSuccess) return AMBRYCRC_EHIP;
   }
+  c->last_xform_path.store(0);
   p.gate = general;
   t.gate = general;
   t.gate_when = 1;

@@ -61,7 +61,8 @@
 #ifndef AMBRY_RUNS_PROBE  // 1 = no run sums into LDS, 5 = no global stores, 6 = stores to one line set
 #define AMBRY_RUNS_PROBE 0
 #endif
-#ifndef AMBRY_FUSED_PROBE  // one-pass kernel: 1 = processors do nothing (the streaming alone), 2 = timestamps
+#ifndef AMBRY_FUSED_PROBE  // one-pass kernel: 1 = processors do nothing (the streaming alone), 2 = timestamps,
+                           // 3-5 = the streaming alone without sum stores / stores CU-interleaved / groups interleaved
 #define AMBRY_FUSED_PROBE 0
 #endif
 

@@ -135,6 +135,12 @@ constexpr uint64_t kSuperBlock = 4096;
 // mode per call (profiles/r03za_messages.jsonl, one box, ~1.3 GB regions): 1.3 KiB per message
 // 1.21x, 2.2 KiB 1.35x, 3.2 KiB 1.17x, 4.2 KiB 1.07x, 5.3 KiB 1.02x; 64 KiB blobs stream in job mode.
 constexpr uint64_t kRegionMaxPerMessage = 6144;
+// Region bytes per message up to which the transform (header V3 out) tries the one-pass fast path
+// first. Fast / general path on one box (profiles/r04o_put_*.jsonl): 5.3 KiB per message 0.757 /
+// 1.163 ms (262,144 4 KiB PUTs), 17.4 KiB 0.672 / 0.645, 67 KiB 3.85 / 1.96 -- past a few KiB the
+// processors' record CRCs no longer hide under the stream.
+// AMBRYCRC_XFORM_FAST_MAX overrides it (A/B; 0 = never).
+constexpr uint64_t kXformFastMaxPerMessage = 8192;
 inline uint64_t region_nsb(const uint8_t* region, uint64_t len) {
   const uint64_t b = reinterpret_cast<uintptr_t>(region) & ~uint64_t(63);
   return (reinterpret_cast<uintptr_t>(region) + len - b + kSuperBlock - 1) / kSuperBlock;

@@ -1702,7 +1702,7 @@ __global__ __launch_bounds__(1024) void region_fused_kernel(FusedArgs f) {
   if (threadIdx.x == 0) g_fused_t[3 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
 #endif
   __shared__ uint32_t tbl[1024];
-  __shared__ uint32_t nib[region::kSets * region::kNibWords];
+  __shared__ uint32_t nib[region::kNibTotal];
   __shared__ uint32_t done[16];
   {  // LDS-DMA of the slice tables (the streamers'), then the processors' compact tables and nibble sets
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -1761,15 +1761,25 @@ __global__ __launch_bounds__(1024) void region_fused_kernel(FusedArgs f) {
       buf[64u * u + slot] = r;
       return r;
     };
-    if (mine) {
+    // A/B probe 5 (timing only, wrong sums): streamer v of workgroup b takes the region's groups
+    // (j*S + v)*grid + b -- every CU's reads and stores inside one window, as region_runs_kernel's
+    uint64_t gfirst = G0 + v, gstep = nstream;
+    uint64_t mine_n = mine;
+    if constexpr (AMBRY_FUSED_PROBE == 5) {
+      const uint64_t L = f.ngroups > blockIdx.x ? (f.ngroups - blockIdx.x + gridDim.x - 1) / gridDim.x : 0;
+      gfirst = (uint64_t)v * gridDim.x + blockIdx.x;
+      gstep = (uint64_t)nstream * gridDim.x;
+      mine_n = L > v ? (L - v + nstream - 1) / nstream : 0;
+    }
+    if (mine_n) {
       u32x4 b0[4], b1[4], b2[4], b3[4];
-      uint64_t g = G0 + v;
+      uint64_t g = gfirst;
       region_sb_load(a, 4 * g, lane, b0);
       region_sb_load(a, 4 * g + 1, lane, b1);
       region_sb_load(a, 4 * g + 2, lane, b2);
       region_sb_load(a, 4 * g + 3, lane, b3);
-      for (uint64_t j = 0; j < mine; ++j, g += nstream) {
-        const uint64_t nx = j + 1 < mine ? g + nstream : g;  // the last group re-reads itself
+      for (uint64_t j = 0; j < mine_n; ++j, g += gstep) {
+        const uint64_t nx = j + 1 < mine_n ? g + gstep : g;  // the last group re-reads itself
         // COPY: a message that cannot take the fast path anywhere ends the pass (the general path
         // redoes the batch); every 8th group, one L2 read
         if (COPY && (j & 7) == 7 && __hip_atomic_load(f.xfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
@@ -1801,7 +1811,14 @@ __global__ __launch_bounds__(1024) void region_fused_kernel(FusedArgs f) {
         region_sb_load(a, 4 * nx + 3, lane, b3);
         __builtin_amdgcn_s_setprio(0);
         const u32x4 sums = *reinterpret_cast<const u32x4*>(buf + 4u * lane);
-        *(reinterpret_cast<u32x4*>(a.rk + kRunPad + g * 256) + lane) = sums;
+        if constexpr (AMBRY_FUSED_PROBE == 3) {  // A/B probe 3: no sum stores (timing only)
+          if (sums.x == 0x9E3779B9u) *(reinterpret_cast<u32x4*>(a.rk + kRunPad + g * 256) + lane) = sums;
+        } else if constexpr (AMBRY_FUSED_PROBE == 4) {  // A/B probe 4: sums stored CU-interleaved (timing only)
+          const uint64_t gi = (g - G0) * gridDim.x + blockIdx.x;
+          *(reinterpret_cast<u32x4*>(a.rk + kRunPad + (gi < f.ngroups ? gi : g) * 256) + lane) = sums;
+        } else {
+          *(reinterpret_cast<u32x4*>(a.rk + kRunPad + g * 256) + lane) = sums;
+        }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -1812,7 +1829,7 @@ __global__ __launch_bounds__(1024) void region_fused_kernel(FusedArgs f) {
     return;
   }
   // ---- processor wave
-  if (AMBRY_FUSED_PROBE == 1) return;  // A/B probe: the streaming alone (wrong statuses)
+  if (AMBRY_FUSED_PROBE == 1 || AMBRY_FUSED_PROBE >= 3) return;  // A/B probes: the streaming alone (wrong statuses)
   const uint32_t p = v - nstream;
   const uint64_t s_lo = G0 * kGroupBytes, s_hi = G1 * kGroupBytes;  // the share, base-relative
   {  // this wave's slice of the global sortedness check
@@ -1881,13 +1898,14 @@ __global__ __launch_bounds__(256) void region_tail_kernel(FusedArgs f) {
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(f.xfail, 1u);
     return;
   }
+  const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  if (n <= waves && (uint64_t)blockIdx.x * (blockDim.x >> 6) >= n) return;  // no message for this block
   __shared__ uint32_t tbl[1024];
-  __shared__ uint32_t nib[region::kSets * region::kNibWords];
+  __shared__ uint32_t nib[region::kNibTotal];
   stage_slice_tables(tbl, f.g.img);
   region::stage_nib(nib, f.g.img);
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
   const uint64_t w0 = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (n <= waves) {
     // Few messages (the share boundaries' deferrals): a wave per message, every record by the
@@ -1930,7 +1948,10 @@ hipError_t launch_region_fused(const FusedArgs& f, int num_cu, hipStream_t s) {
   } else if (hipMemsetAsync(f.ctl, 0xFF, 4, s) != hipSuccess) {  // empty region: all to the tail
     return hipGetLastError();
   }
-  uint64_t blocks = (f.a.m + 255) / 256;
+  // A wave per deferred message whenever there are at most 4 per CU (~1 per share boundary, each
+  // maybe a 4 MiB message whose records a lane alone would walk for milliseconds): blocks without a
+  // message return before staging their tables.
+  uint64_t blocks = (f.a.m + 3) / 4;
   if (blocks > (uint64_t)num_cu * 4) blocks = (uint64_t)num_cu * 4;
   if (copy) hipLaunchKernelGGL(region_tail_kernel<true>, dim3((uint32_t)blocks), dim3(256), 0, s, f);
   else hipLaunchKernelGGL(region_tail_kernel<false>, dim3((uint32_t)blocks), dim3(256), 0, s, f);

@@ -93,7 +93,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AMBRY_REGIO
     MsgArgs a, RegionArgs g) {
   __shared__ uint32_t tbl[1024];
   __shared__ uint32_t pwin[256 * kPropsSlotWords];
-  __shared__ uint32_t nib[region::kSets * region::kNibWords];
+  __shared__ uint32_t nib[region::kNibTotal];
   stage_slice_tables(tbl, a.img);
   region::stage_nib(nib, a.img);
   __syncthreads();

@@ -44,6 +44,10 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 constexpr uint32_t kNibWords = kNibSetBytes / 4;  // 128
 constexpr uint32_t kSets = 5 + kInvPowSets;
 constexpr uint32_t kP16 = 0, kP32 = 1, kP64 = 2, kP128 = 3, kP256 = 4, kInv0 = 5;
+// After the sets: x^(8*2^k), k = 0..63 (the image's power words), for the wave-wide record CRC's
+// shift constants without a dependent global load each.
+constexpr uint32_t kXpOff = kSets * kNibWords;
+constexpr uint32_t kNibTotal = kXpOff + 64;
 
 __device__ __forceinline__ uint32_t nmul(const uint32_t* __restrict__ nib, uint32_t v, uint32_t set) {
   const uint32_t* s = nib + set * kNibWords;
@@ -121,6 +125,7 @@ __device__ __forceinline__ uint32_t hash_run(const Tab& t, const uint32_t* __res
 
 // Stage the nibble sets into nib[kSets * kNibWords] (the caller syncs).
 __device__ __forceinline__ void stage_nib(uint32_t* __restrict__ nib, const uint32_t* __restrict__ img) {
+  if (threadIdx.x < 64) nib[kXpOff + threadIdx.x] = img[kLdsBytes / 4 + threadIdx.x];
   for (uint32_t i = threadIdx.x; i < kSets * kNibWords; i += blockDim.x) {
     const uint32_t set = i / kNibWords, w = i % kNibWords;
     const uint32_t byte = set < 5 ? kNibBase + kPowOff + kNibSetBytes * (4 + set) : kImgInvOff + kNibSetBytes * (set - 5);

@@ -67,7 +67,7 @@ __device__ __noinline__ uint32_t record_crc_wave(const uint32_t* __restrict__ t_
   const uint32_t* __restrict__ nib = (const uint32_t*)(lds_u32*)nib_g;
   const uint8_t* __restrict__ base = (const uint8_t*)(glb_u8*)base_g;
   const uint32_t* __restrict__ rk = (const uint32_t*)(glb_u32*)rk_g;
-  const uint32_t* __restrict__ img = (const uint32_t*)(glb_u32*)img_g;
+  (void)img_g;
   const TabC tc{t};
   if (len < 4) return record_crc(tc, nib, base, rk, pa, len);  // bytes, no runs (every lane the same)
   const uint64_t pb = pa + len;
@@ -88,26 +88,45 @@ __device__ __noinline__ uint32_t record_crc_wave(const uint32_t* __restrict__ t_
   if (tin < 4) H ^= 0xFFFFFFFFu >> (8 * tin);
   const uint32_t T = tail_bytes ? hash_run(tc, nib, tw, 0, thi, 0) : 0u;
   // this lane's groups [g0, g0 + gs) counted from e0; groups wholly before k0 are zero
-  const int64_t g0 = (int64_t)lane * gs;
+  // (four groups per step, the next four in flight: a loop of one load per group waited a memory
+  // latency per group -- ~380 us for a 4 MiB record)
+  const int64_t g0 = (int64_t)lane * gs, g1 = g0 + gs;
   uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-  for (int64_t g = g0; g < g0 + gs; ++g) {
+  auto load1 = [&](int64_t g, u32x4& r) {
     const int64_t eg = e0 + 4 * g;
-    u32x4 r = u32x4{0u, 0u, 0u, 0u};
-    if (eg + 3 >= k0) __builtin_memcpy(&r, rk + eg, 16);  // eg >= k0 - 3 >= -3: inside rk's pad
+    r = u32x4{0u, 0u, 0u, 0u};
+    if (g < g1 && eg + 3 >= k0) __builtin_memcpy(&r, rk + eg, 16);  // eg >= k0 - 3: inside rk's pad
+  };
+  u32x4 buf[4];  // group gb + u in buf[u]; each reloaded (for gb + 4 + u) right after its use
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int64_t e = eg + q;
-      const uint32_t v = e < k0 ? 0u : e == k0 ? H : (e == elast && tail_bytes) ? T : r[q];
-      const uint32_t nv = nmul(nib, s0, kP256) ^ v;
-      s0 = s1;
-      s1 = s2;
-      s2 = s3;
-      s3 = nv;
+  for (int u = 0; u < 4; ++u) load1(g0 + u, buf[u]);
+  for (int64_t gb = g0; gb < g1; gb += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (gb + u < g1) {
+        const int64_t eg = e0 + 4 * (gb + u);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int64_t e = eg + q;
+          const uint32_t v = e < k0 ? 0u : e == k0 ? H : (e == elast && tail_bytes) ? T : buf[u][q];
+          const uint32_t nv = nmul(nib, s0, kP256) ^ v;
+          s0 = s1;
+          s1 = s2;
+          s2 = s3;
+          s3 = nv;
+        }
+      }
+      load1(gb + 4 + u, buf[u]);
     }
   }
   uint32_t V = s3 ^ nmul(nib, s2, kP64) ^ nmul(nib, s1, kP128) ^ nmul(nib, nmul(nib, s0, kP64), kP128);
   // lane slices are 256*gs bytes: level k shifts the left half by x^(8*256*gs*2^k)
-  uint32_t c = mul_xpow8_img(img, 0x80000000u, (uint64_t)256 * (uint64_t)gs);
+  uint32_t c = 0x80000000u;  // x^(8*256*gs) from the LDS copy of the power words
+  {
+    uint64_t n = (uint64_t)256 * (uint64_t)gs;
+    for (uint32_t k = 0; n; ++k, n >>= 1)
+      if (n & 1u) c = gf2_mul(c, nib[kXpOff + k]);
+  }
   V = wave_fold<0>(V, c, lane);
   c = gf2_mul(c, c);
   V = wave_fold<1>(V, c, lane);
@@ -174,39 +193,30 @@ __device__ __forceinline__ void process_message(const MsgArgs& a, const RegionAr
     have = false;
     crcs = false;
   }
-  wait(wave_max_u64(crcs ? g.reg0 + off + end : 0));
-#pragma unroll
-  for (int k = 0; k < kMsgSlots; ++k) {
-    if (!have || jl[k] == 0) continue;
-    const uint64_t pa = g.reg0 + jo[k];
-    const int64_t runs = (int64_t)((((pa + jl[k] + 63) & ~uint64_t(63)) - (pa & ~uint64_t(63))) >> 6);
-    if (runs > kLongRuns) {
-      longs |= 1u << k;
-      continue;
-    }
-    if (record_crc(tr, nib, g.base, rk, pa, jl[k]) != ex[k]) status |= record_bit(k);
-  }
-  // The long records: the wave takes them one by one, unless enough lanes have one that the lanes
+  // Long records are the wave's, one by one, each once the frontier passes its own end (a CU's
+  // 4 MiB blobs are verified as the stream passes them, not all after it); then the lanes' own
+  // records, once it passes the last of them. Unless enough lanes have a long record that the lanes
   // doing their own in parallel finish first (a lane's chain is runs/4 nibble multiplies deep; the
   // wave's per record ~runs/256 plus ~64 for the tree's gf2 shifts).
-  {
-    int64_t lane_runs = 0;
+  auto runs_of = [&](int k) -> int64_t {
+    const uint64_t pa = g.reg0 + jo[k];
+    return (int64_t)((((pa + jl[k] + 63) & ~uint64_t(63)) - (pa & ~uint64_t(63))) >> 6);
+  };
+  int64_t lane_runs = 0;
 #pragma unroll
-    for (int k = 0; k < kMsgSlots; ++k)
-      if (longs & (1u << k))
-        lane_runs += (int64_t)((((g.reg0 + jo[k] + jl[k] + 63) & ~uint64_t(63)) - ((g.reg0 + jo[k]) & ~uint64_t(63))) >> 6);
-    const int64_t per_lane = (int64_t)wave_max_u64((uint64_t)lane_runs) / 4;
-    int64_t wave = 0;
-    for (int o = 32; o > 0; o >>= 1) lane_runs += __shfl_xor(lane_runs, o);  // sum over lanes
-    wave = lane_runs / 256 + 64 * (int64_t)__popcll(__ballot(longs != 0));
-    if (per_lane <= wave) {
-#pragma unroll
-      for (int k = 0; k < kMsgSlots; ++k)
-        if (longs & (1u << k))
-          if (record_crc(tr, nib, g.base, rk, g.reg0 + jo[k], jl[k]) != ex[k]) status |= record_bit(k);
-      longs = 0;
+  for (int k = 0; k < kMsgSlots; ++k)
+    if (have && jl[k] != 0 && runs_of(k) > kLongRuns) {
+      longs |= 1u << k;
+      lane_runs += runs_of(k);
     }
+  {
+    const int64_t per_lane = (int64_t)wave_max_u64((uint64_t)lane_runs) / 4;
+    int64_t tot = lane_runs;
+    for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);  // sum over lanes
+    const int64_t wave = tot / 256 + 64 * (int64_t)__popcll(__ballot(longs != 0));
+    if (per_lane <= wave) longs = 0;  // every record by its lane
   }
+  const uint32_t own_long = longs;
   for (;;) {
     const uint64_t ball = __ballot(longs != 0);
     if (ball == 0) break;
@@ -221,6 +231,7 @@ __device__ __forceinline__ void process_message(const MsgArgs& a, const RegionAr
       }
     rjo = __shfl(rjo, (int)owner);
     rjl = __shfl(rjl, (int)owner);
+    wait(g.reg0 + rjo + rjl);
     const uint32_t c = record_crc_wave(t, nib, g.base, rk, g.img, g.reg0 + rjo, rjl, lane);
     if (lane == owner) {
       uint32_t e = 0;
@@ -230,6 +241,16 @@ __device__ __forceinline__ void process_message(const MsgArgs& a, const RegionAr
       if (c != e) status |= record_bit((int)kk);
       longs &= ~(1u << kk);
     }
+  }
+  uint64_t need = 0;  // base-relative end of the lane's last own record
+#pragma unroll
+  for (int k = 0; k < kMsgSlots; ++k)
+    if (have && jl[k] != 0 && !(own_long & (1u << k)) && g.reg0 + jo[k] + jl[k] > need) need = g.reg0 + jo[k] + jl[k];
+  wait(wave_max_u64(need));
+#pragma unroll
+  for (int k = 0; k < kMsgSlots; ++k) {
+    if (!have || jl[k] == 0 || (own_long & (1u << k))) continue;
+    if (record_crc(tr, nib, g.base, rk, g.reg0 + jo[k], jl[k]) != ex[k]) status |= record_bit(k);
   }
   if (have) {
     a.status[i] = status;

@@ -160,8 +160,9 @@ def get_variant(device: int = 0) -> int:
 
 
 def set_region_mode(device: int, mode) -> None:
-    """Message verify form (ambrycrc_set_region_mode): 1 / True = region mode in one pass (the
-    default), 2 = region mode in two passes (A/B), 0 / False = CRC jobs through the batch engine."""
+    """Message verify form (ambrycrc_set_region_mode): 2 = region mode in two passes (the
+    default), 1 / True = region mode in one pass, 0 / False = CRC jobs through the batch engine.
+    The transform's one-pass fast path runs whenever region mode is on (1 or 2)."""
     m = int(mode) if not isinstance(mode, bool) else (1 if mode else 0)
     check(lib().ambrycrc_set_region_mode(device, m), "ambrycrc_set_region_mode")
 
@@ -174,6 +175,12 @@ def last_message_mode(device: int = 0) -> int:
     """The form the device's last message verify took: 0 jobs, 1 region one-pass, 2 region two-pass
     (-1: none yet); ambrycrc_last_message_mode."""
     return lib().ambrycrc_last_message_mode(device)
+
+
+def last_transform_path(device: int = 0) -> int:
+    """The path the device's last transform took: 1 the one-pass fast path, 0 the general path
+    (-1: none yet); ambrycrc_last_transform_path."""
+    return lib().ambrycrc_last_transform_path(device)
 
 
 def set_grid(device: int, workgroups: int) -> None:

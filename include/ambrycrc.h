@@ -265,8 +265,9 @@ int ambrycrc_serialize_puts_dev(const ambrycrc_put_desc* d_desc, size_t m, const
  * it is verified; a batch with a failing message is then rebuilt). d_out must not overlap the
  * region. Enqueued on `stream`; d_ws >= ambrycrc_transform_workspace_bytes(m) or NULL. The
  * store-key comparison with the index entry stays with the caller (it owns the StoreKey type).
- * Fast path (header_version 3, region mode 1, workspace room for the region's run sums -- the
- * default workspace has it): one pass verifies the messages while copying the region into d_out
+ * Fast path (header_version 3, region mode on, at most 8 KiB of region per message
+ * (AMBRYCRC_XFORM_FAST_MAX at init overrides; 0 = never), workspace room for the region's run sums
+ * -- the default workspace has it): one pass verifies the messages while copying the region into d_out
  * and rewrites the headers' life versions; it takes the batch when every message is a clean PUT
  * stored at header V3 with VERSION_5 properties and a Blob_Format_V3 record, back to back from
  * d_msg_off[0]. The call then synchronizes with `stream` once to learn whether it did, and returns
@@ -496,16 +497,22 @@ int ambrycrc_get_variant(int device);
 /* Message verify (ambrycrc_verify_messages_dev / _host) of a region of at most 6 KiB per
  * message: region mode sweeps the region once as contiguous memory, keeping the raw CRC of every
  * 64-B run, and assembles each record's CRC from the runs it covers, re-reading only the two runs
- * its ends cut. 1 (the default): one pass -- each CU's processor waves take the messages of its
- * share of the region while its streaming waves are still sweeping it, so the message bytes are
- * parsed from the caches; 2: two passes (the sweep, then one thread per message; A/B);
- * 0: every record as a CRC job through the batch engine (plan, group phase, sweep).
- * AMBRYCRC_REGION=0 / 2 in the environment at init selects 0 / 2. Same status bits every way.
+ * its ends cut. 2 (the default): two passes -- the sweep, then one thread per message;
+ * 1: one pass -- each CU's processor waves take the messages of its share of the region while its
+ * streaming waves are still sweeping it (measured 1.5-14 % slower than 2 for verify: the
+ * processors' dependent loads wait behind the saturated stream; it is the transform's fast path,
+ * which runs when the mode is 1 or 2); 0: every record as a CRC job through the batch engine
+ * (plan, group phase, sweep). AMBRYCRC_REGION=0 / 1 in the environment at init selects 0 / 1.
+ * Same status bits every way.
  * ambrycrc_last_message_mode: the form the device's last message verify took (0 / 1 / 2; -1
  * before the first), for profiles that must say which kernels they timed. */
 int ambrycrc_set_region_mode(int device, int enable);
 int ambrycrc_get_region_mode(int device);
 int ambrycrc_last_message_mode(int device);
+/* The path the device's last ambrycrc_transform_messages_dev call (or _host slab) took: 1 = the one-pass
+ * fast path alone (header V3, every message a clean dense V3 PUT with canonical properties), 0 = the
+ * general path (after the fast pass gave up, or without it), -1 = none yet. */
+int ambrycrc_last_transform_path(int device);
 /* Grid size of the persistent sweep kernel (workgroups; 0 = one per CU). */
 int ambrycrc_set_grid(int device, int workgroups);
 

@@ -19,13 +19,13 @@ MODES = {"region": 1, "region2": 2, "jobs": 0}
 
 @pytest.fixture(autouse=True, params=list(MODES))
 def msg_mode(request, gpu):
-    """Every test runs in every message-verify form: region mode in one pass (the default: the
-    region swept once into 64-B run sums while each CU's processor waves take its messages),
-    region mode in two passes, and CRC jobs through the batch engine. Region mode engages for
+    """Every test runs in every message-verify form: region mode in one pass (the region swept
+    once into 64-B run sums while each CU's processor waves take its messages), region mode in two
+    passes (the default), and CRC jobs through the batch engine. Region mode engages for
     regions of <= 6 KiB per message."""
     gpu.set_region_mode(0, MODES[request.param])
     yield request.param
-    gpu.set_region_mode(0, 1)
+    gpu.set_region_mode(0, 2)
 
 
 def run(gpu, region: bytes, offs, shift: int = 0):

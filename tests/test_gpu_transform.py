@@ -363,7 +363,7 @@ def test_transform_fast_path_dense_v3(gpu, mf, n, lead, use_life):
     st, oo, ol = st.cpu().numpy().view(np.uint32), oo.cpu().numpy(), ol.cpu().numpy()
     out_h = out.cpu().numpy().tobytes()
     assert st.tolist() == [0] * n
-    pos = 0
+    assert gpu.last_transform_path(0) == 1  # the fast path took the batch alone
     for i in range(0, n, 1 if n <= 2000 else 7):
         o = offs[i]
         exp_st, exp = mf.transform_message(region, o, life=int(life[i]) if use_life else None, version=3)
@@ -403,6 +403,7 @@ def test_transform_fast_path_falls_back(gpu, mf, spoil):
     dev = torch.frombuffer(bytearray(region), dtype=torch.uint8).cuda()
     out, oo, ol, st = transform_dev(dev, torch.tensor(offs, dtype=torch.int64, device="cuda"))
     torch.cuda.synchronize()
+    assert gpu.last_transform_path(0) == 0  # the general path redid the batch
     st, oo, ol = st.cpu().numpy().view(np.uint32), oo.cpu().numpy(), ol.cpu().numpy()
     out_h = out.cpu().numpy().tobytes()
     pos = 0
@@ -414,3 +415,40 @@ def test_transform_fast_path_falls_back(gpu, mf, spoil):
             continue
         assert oo[i] == pos and out_h[pos:pos + len(exp)] == exp, i
         pos += len(exp)
+
+
+def test_transform_fast_path_long_messages(gpu, mf):
+    """Long messages between small ones on the fast path (~2.5 KiB per message on average): two of
+    3 MiB span many CU shares and go to the tail kernel, which takes each with a whole wave (a lane
+    alone would walk its ~50,000 run sums one step at a time); 48 KiB blobs inside a share are the
+    processors' long records (more than 512 runs), each verified once the stream has passed it."""
+    import torch
+
+    from ambry_amd.messages import transform_dev
+
+    rng = np.random.default_rng(77)
+    msgs = []
+    for i in range(8000):
+        if i in (1500, 6100):
+            blen = (3 << 20) + 77 * i
+        elif i % 250 == 7:
+            blen = (48 << 10) + i
+        else:
+            blen = int(rng.integers(0, 3000))
+        content = stream_bytes(500 + i, 0, blen).tobytes()
+        msgs.append(mf.put_message(mf.store_key("long-%d" % i), mf.blob_properties_bytes(blen), b"um" * (i % 9),
+                                   content, version=3))
+    region = b"".join(msgs)
+    assert len(region) <= 8192 * len(msgs)  # the fast path's cut-off
+    offs = np.cumsum([0] + [len(x) for x in msgs[:-1]]).tolist()
+    dev = torch.frombuffer(bytearray(region), dtype=torch.uint8).cuda()
+    out, oo, ol, st = transform_dev(dev, torch.tensor(offs, dtype=torch.int64, device="cuda"), header_version=3)
+    torch.cuda.synchronize()
+    assert st.cpu().numpy().view(np.uint32).tolist() == [0] * len(msgs)
+    assert gpu.last_transform_path(0) == 1
+    oo, ol = oo.cpu().numpy(), ol.cpu().numpy()
+    out_h = out.cpu().numpy().tobytes()
+    for i in list(range(0, len(msgs), 13)) + [1500, 6100] + [i for i in range(len(msgs)) if i % 250 == 7]:
+        o = offs[i]
+        exp_st, exp = mf.transform_message(region, o, version=3)
+        assert exp_st == 0 and oo[i] == o and ol[i] == len(exp) and out_h[o:o + len(exp)] == exp, i

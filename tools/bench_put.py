@@ -169,7 +169,8 @@ def run_transform(m, blob_bytes, reps):
     return {"case": f"transform {m} x PUT({blob_bytes} B blob) V3 -> V3", "messages": m, "message_bytes": nbytes,
             "ms_median": round(ms, 4), "GiBps_messages": round(nbytes / (ms / 1e3) / 2**30, 1),
             "messages_per_s": round(m / (ms / 1e3)), "GBps_hbm_min": round(2 * nbytes / (ms / 1e3) / 1e9, 1),
-            "parity": "every message verifies and the V3 -> V3 output equals the input region byte for byte"}
+            "parity": "every message verifies and the V3 -> V3 output equals the input region byte for byte",
+            "path_taken": {1: "one-pass fast path", 0: "general path"}.get(D.last_transform_path(0))}
 
 
 def main():
@@ -186,7 +187,7 @@ def main():
 
     torch.cuda.set_device(0)
     D.init(0)
-    cases = {"64k": (65536, 64 << 10), "4k": (262144, 4 << 10), "4m": (4096, 4 << 20)}
+    cases = {"64k": (65536, 64 << 10), "16k": (65536, 16 << 10), "4k": (262144, 4 << 10), "4m": (4096, 4 << 20)}
     for c in [x for x in args.cases.split(",") if x]:
         m, s = cases[c]
         for in_place in (False, True):

@@ -2,7 +2,8 @@
 """A/B probe (a library built with -DAMBRY_FUSED_PROBE=2, loaded through AMBRYCRC_LIBRARY): per
 workgroup of the one-pass region kernel, when its streamers and its processors finished, relative
 to its start (s_memrealtime, 100 MHz), for the message-verify case given (tools/bench_messages.py's
-gpu_region). Prints the distribution over workgroups."""
+gpu_region), or the transform case given as x4k / x64k / x4m (tools/bench_put.py's run_transform: the
+copy form). Prints the distribution over workgroups."""
 import ctypes
 import json
 import os
@@ -20,8 +21,20 @@ def main():
     from ambry_amd._lib import lib
     from bench_messages import gpu_region, load_mf
 
-    m, blob = {"4k": (262144, 4096), "1k": (524288, 1024), "100": (1048576, 100)}[sys.argv[1] if len(sys.argv) > 1 else "4k"]
-    res = gpu_region(load_mf(), m, blob, 5)
+    case = sys.argv[1] if len(sys.argv) > 1 else "4k"
+    if case.startswith("x"):
+        import torch
+        from ambry_amd import device as D
+        from bench_put import run_transform
+
+        torch.cuda.set_device(0)
+        D.init(0)
+        m, blob = {"x4k": (262144, 4096), "x64k": (65536, 65536), "x4m": (4096, 4 << 20)}[case]
+        res = run_transform(m, blob, 5)
+        res["config"] = res["case"]
+    else:
+        m, blob = {"4k": (262144, 4096), "1k": (524288, 1024), "100": (1048576, 100)}[case]
+        res = gpu_region(load_mf(), m, blob, 5)
     n = 256
     buf = (ctypes.c_ulonglong * (3 * 2048))()
     fn = lib().ambrycrc_debug_fused_times
