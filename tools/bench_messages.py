@@ -166,7 +166,7 @@ def main():
     ap.add_argument("--no-gpu", action="store_true")
     ap.add_argument("--variants", default="29")
     ap.add_argument("--cases", default="64k,4m,4k", help="subset of 64k,4m,4k,3k,2k,1k,100")
-    ap.add_argument("--modes", default="region", help="message-verify modes: region (one pass), region2, jobs")
+    ap.add_argument("--modes", default="region2", help="message-verify modes: region2 (two passes, the default), region (one pass), jobs")
     ap.add_argument("--host", action="store_true", help="also time the host-region path (regions <= 5 GiB)")
     args = ap.parse_args()
     mf = load_mf()

@@ -5,7 +5,7 @@
 # no trace domain combined with --pmc. Then `python tools/summarize_cases.py --tag <tag>`.
 set -euo pipefail
 export TMPDIR=/tmp
-CASES=${CASES:-"scatter16 scatter4 scatter8 msg4k msg1k msg4k_2pass xform4k xform64k batch100 batch4k"}
+CASES=${CASES:-"scatter16 scatter4 scatter8 msg4k msg1k msg4k_1pass xform4k xform64k batch100 batch4k put4k"}
 REPS=${REPS:-5}
 mkdir -p gpurun_out/pmc_cases
 # keep only the SQ counters this rocprofv3 lists for the device

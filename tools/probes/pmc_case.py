@@ -9,9 +9,10 @@ untimed; the profiler's per-dispatch counters are the measurement.
   batch4109  4109-B chunks at 16-B offsets (the blob records of 4 KiB PUTs)     -- group class 3
   batch2000  2000-B chunks, packed (8-B offsets); batch3000: 3000 B at 16-B offsets -- class 2
   batch16k   16 KiB chunks, aligned                                               -- class 3
-  msg4k      ambrycrc_verify_messages_dev over 262,144 x PUT(4 KiB blob), 1.29 GiB (region mode, one pass)
+  msg4k      ambrycrc_verify_messages_dev over 262,144 x PUT(4 KiB blob), 1.29 GiB (the default: region
+             mode, two passes)
   msg1k      the same over 524,288 x PUT(1 KiB blob); msg3k with 3000 B blobs
-  msg4k_2pass / msg4k_jobs   msg4k in region mode's two-pass form / in job mode
+  msg4k_1pass / msg4k_jobs   msg4k in region mode's one-pass form / in job mode (msg4k_2pass = msg4k)
   scatter16 / scatter4 / scatter8   FETCH_SIZE calibration: every 128-B line of 1 GiB read once in
              scattered order by one 16-B / 4-B / unaligned 8-B load (ambrycrc_debug_readbw_dev 60-62)
   put4k      ambrycrc_serialize_puts_dev, copy mode, 262,144 x PUT(4 KiB blob); put4k_inplace in place
@@ -84,11 +85,11 @@ def main():
         for _ in range(args.reps):
             D.crc32_batch(buf, off, ln, out=out, workspace=ws)
         info.update(chunks=1, chunk_bytes=size, alg_bytes_per_launch=size + 4)
-    elif args.case in ("msg4k", "msg3k", "msg1k", "msg4k_2pass", "msg4k_jobs"):
+    elif args.case in ("msg4k", "msg3k", "msg1k", "msg4k_2pass", "msg4k_1pass", "msg4k_jobs"):
         from bench_messages import gpu_region, load_mf
 
         m, blob = {"msg3k": (262144, 3000), "msg1k": (524288, 1024)}.get(args.case, (262144, 4096))
-        mode = "region2" if args.case.endswith("_2pass") else "jobs" if args.case.endswith("_jobs") else "region"
+        mode = "region" if args.case.endswith("_1pass") else "jobs" if args.case.endswith("_jobs") else "region2"
         res = gpu_region(load_mf(), m, blob, args.reps, mode=mode)
         info.update(res)
         # CRC'd bytes per message: header 32 + props + usermeta 1006 + blob record 4109 (+ stored CRCs read)
