@@ -602,6 +602,11 @@ int ambrycrc_init(int device) {
     if (end != v && *end == '\0' && x >= 0 && x < 1000 && variant_supported((int)x)) c->variant = (int)x;
   }
   if (const char* v = getenv("AMBRYCRC_REGION")) c->region_mode = strcmp(v, "0") == 0 ? 0 : strcmp(v, "1") == 0 ? 1 : 2;
+  if (const char* v = getenv("AMBRYCRC_ASM_MAX")) {  // A/B: whole-message assembly cut-off
+    char* end = nullptr;
+    const unsigned long x = strtoul(v, &end, 10);
+    if (end != v && *end == '\0' && x <= kAsmMaxBytes) c->asm_max = (uint32_t)x;
+  }
   if (const char* v = getenv("AMBRYCRC_XFORM_FAST_MAX")) {  // A/B: the transform fast path's cut-off
     char* end = nullptr;
     const unsigned long long x = strtoull(v, &end, 10);
@@ -868,6 +873,15 @@ int ambrycrc_set_region_mode(int device, int enable) {
   if (enable < 0 || enable > 2) return AMBRYCRC_EINVAL;
   c->region_mode = enable;
   return AMBRYCRC_OK;
+}
+
+int ambrycrc_set_put_assembly(int device, int max_bytes) {
+  DevCtx* c = ctx_for(device);
+  if (!c) return AMBRYCRC_ENOINIT;
+  if (max_bytes < 0 || (uint32_t)max_bytes > kAsmMaxBytes) return AMBRYCRC_EINVAL;
+  const int prev = (int)c->asm_max;
+  c->asm_max = (uint32_t)max_bytes;
+  return prev;
 }
 
 int ambrycrc_get_region_mode(int device) {

@@ -83,6 +83,10 @@ struct DevCtx {
   // mode is on and the region holds at most xform_fast_max bytes per message.
   int region_mode = 2;
   uint64_t xform_fast_max = kXformFastMaxPerMessage;
+  // Serialize copy mode: messages of at most this many bytes are assembled whole
+  // (put_assemble_kernel); ambrycrc_set_put_assembly / AMBRYCRC_ASM_MAX (0 = never, at most
+  // kAsmMaxBytes). Off by default until it beats the job path.
+  uint32_t asm_max = 0;
   // The form the last message verify on this device took (ambrycrc_last_message_mode).
   std::atomic<int> last_msg_mode{-1};
   // The path the last transform took (ambrycrc_last_transform_path): 1 fast, 0 general.

@@ -76,13 +76,22 @@ int enqueue_serialize(DevCtx* c, const ::ambrycrc_put_desc* d_desc, size_t m, co
   }
   a.pfix = pfix;
   void* batch_ws = w + put_jobs_bytes(m);
+  if (a.copy_through && d_fields && d_blobs && c->asm_max && !gate) {
+    // whole-message assembly for messages of at most asm_max bytes; the job path below runs (on
+    // the device) only if a longer one set *big, and skips the assembled ones
+    a.asm_max = c->asm_max;
+    a.big = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(batch_ws) + ws_need(j));
+    if (hipMemsetAsync(a.big, 0, sizeof(uint32_t), stream) != hipSuccess) return AMBRYCRC_EHIP;
+    if (launch_put_assemble(a, c->num_cu, stream) != hipSuccess) return AMBRYCRC_EHIP;
+    a.gate = a.big;
+  }
   if (launch_put_layout(a, stream) != hipSuccess) return AMBRYCRC_EHIP;
   if (layout_only) return AMBRYCRC_OK;
   if (a.copy_through) {
     // one pass over the fields: the copy-through sweep reads each from its source, writes it into
     // the message and CRCs it (job k*m+i = slot k of message i, as the CRC jobs)
     const int rc = enqueue_batch(c, reinterpret_cast<const uint8_t*>((uintptr_t)a.src_base), a.cp_src, a.cp_len,
-                                 a.crc_in, crc, j, batch_ws, stream, nullptr, d_out, a.cp_dst);
+                                 a.crc_in, crc, j, batch_ws, stream, nullptr, d_out, a.cp_dst, a.gate);
     if (rc) return rc;
     return hip_err(launch_put_seal(a, stream));
   }
@@ -163,7 +172,7 @@ int ambrycrc_serialize_put_host(const ambrycrc_put_desc* d, const uint8_t* field
 }
 
 size_t ambrycrc_serialize_puts_workspace_bytes(size_t m) {
-  return put_jobs_bytes(m) + ws_need((size_t)kPutSlots * m);
+  return put_jobs_bytes(m) + ws_need((size_t)kPutSlots * m) + 256;  // + the assembly's `big` word
 }
 
 int ambrycrc_serialize_puts_dev(const ambrycrc_put_desc* d_desc, size_t m, const uint8_t* d_fields,

@@ -228,7 +228,16 @@ struct PutArgs {
   // is the record CRC; the layout kernel writes the header trailer itself. A slot with no source
   // buffer (fields or blobs null) re-reads its bytes in place (src = dst).
   bool copy_through;
+  // Whole-message assembly (put_assemble_kernel, copy mode with both field buffers): messages of
+  // at most asm_max bytes are written by it, and put_layout_kernel gives them no jobs; a longer one
+  // sets *big, which gates the job path (layout, plan + sweep, seal). 0: no assembly.
+  uint32_t asm_max = 0;
+  uint32_t* big = nullptr;
 };
+
+// Messages of at most this many bytes are assembled whole by put_assemble_kernel (a wave per
+// message through a 7 KiB LDS image per wave: 4 waves and 37.5 KiB of LDS per block, 4 blocks per CU).
+constexpr uint32_t kAsmMaxBytes = 6144;
 
 // Each copy job costs its bytes plus kCopyJobCost: a wave pays about one memory round trip
 // (~2 us, ~1.6 KB of its share of HBM bandwidth) per job whatever its size, so balancing bytes
@@ -294,6 +303,7 @@ hipError_t launch_props_fix(const TransformArgs& a, hipStream_t s);
 
 hipError_t launch_put_layout(const PutArgs& a, hipStream_t s);
 hipError_t launch_put_seal(const PutArgs& a, hipStream_t s);
+hipError_t launch_put_assemble(const PutArgs& a, int num_cu, hipStream_t s);
 hipError_t launch_gather_copy(const CopyArgs& a, int grid, hipStream_t s);
 
 hipError_t launch_trailer_parse(const TrailerArgs& a, hipStream_t s);

@@ -1908,14 +1908,18 @@ __global__ __launch_bounds__(256) void region_tail_kernel(FusedArgs f) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t w0 = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (n <= waves) {
-    // Few messages (the share boundaries' deferrals): a wave per message, every record by the
-    // whole wave -- a lane alone would walk a 64 KiB record's run sums one dependent load at a time.
+    // Few messages (the share boundaries' deferrals): a wave per message, in lane 0. Its short
+    // records are lane 0's; a long one (more than 512 runs) goes to the whole wave -- a lane alone
+    // would walk a 4 MiB record's run sums one dependent load at a time (r04: 12 ms for 4 MiB PUTs).
+    // (Every record by the wave cost 60 us per 262,144 4 KiB PUTs: a wave-wide tree per record.)
     for (uint64_t w = w0; w < n; w += waves) {
+      const bool have = lane == 0;
       const uint64_t i = all ? w : f.defer[w];
       uint32_t st;
       uint64_t mend;
-      region::process_message_wave(f.a, f.g, tbl, nib, i, lane, st, mend);
-      if constexpr (COPY) region::transform_fast(f, tbl, lane == 0, i, st, mend);
+      region::process_message(f.a, f.g, tbl, region::TabC{tbl}, nib, have, i, lane, st, mend,
+                              [](uint64_t, uint64_t) -> bool { return true; }, [](uint64_t) {});
+      if constexpr (COPY) region::transform_fast(f, tbl, have, i, st, mend);
     }
     return;
   }

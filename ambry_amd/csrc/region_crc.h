@@ -82,6 +82,14 @@ struct TabR {
   __device__ __forceinline__ uint32_t t0(uint32_t b) const { return ld((b << 8) | col); }
 };
 
+// Lane (l - 2^LVL)'s v, for lanes with bit LVL set (others: 0): DPP row shifts, then row broadcasts.
+template <int LVL>
+__device__ __forceinline__ uint32_t left_partner(uint32_t v) {
+  if constexpr (LVL < 4) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x110 + (1 << LVL), 0xf, 0xf, false);
+  else if constexpr (LVL == 4) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);
+  else return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);
+}
+
 // Bytes of a little-endian word w at run byte offsets [4w, 4w + 4) with offset >= lo / < hi.
 __device__ __forceinline__ uint32_t keep_ge(int d) {  // bytes at index >= d (d = lo - 4w)
   return d <= 0 ? 0xFFFFFFFFu : (d >= 4 ? 0u : (0xFFFFFFFFu << (8 * d)));

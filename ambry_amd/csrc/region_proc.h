@@ -32,14 +32,6 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
   return v;
 }
 
-// Lane (l - 2^LVL)'s v, for lanes with bit LVL set (others: 0): DPP row shifts, then row broadcasts.
-template <int LVL>
-__device__ __forceinline__ uint32_t left_partner(uint32_t v) {
-  if constexpr (LVL < 4) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x110 + (1 << LVL), 0xf, 0xf, false);
-  else if constexpr (LVL == 4) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);
-  else return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);
-}
-
 template <int LVL>
 __device__ __forceinline__ uint32_t wave_fold(uint32_t s, uint32_t c, uint32_t lane) {
   const uint32_t sh = gf2_mul(left_partner<LVL>(s), c);
@@ -260,34 +252,6 @@ __device__ __forceinline__ void process_message(const MsgArgs& a, const RegionAr
   end_ret = end;
 }
 
-// process_message for ONE message by the whole wave (every lane passes the same i): the parse is
-// repeated in every lane (the same loads, broadcast), each record's CRC is record_crc_wave.
-__device__ __forceinline__ void process_message_wave(const MsgArgs& a, const RegionArgs& g,
-                                                     const uint32_t* __restrict__ t, const uint32_t* __restrict__ nib,
-                                                     uint64_t i, uint32_t lane, uint32_t& st_ret, uint64_t& end_ret) {
-  const uint32_t* rk = g.rk + kRunPad;
-  const uint64_t off = a.msg_off[i];
-  const bool in_region = off <= a.region_len;
-  const uint64_t rem = in_region ? a.region_len - off : 0;
-  const uint8_t* p = a.region + (in_region ? off : 0);
-  const HeaderWords hw = load_header(p, rem);
-  MsgParse r;
-  PropsFields pf;
-  bool pf_ok = false;
-  parse_message<false, false>(off, in_region, rem, p, hw, t, nullptr, 0, r, pf, pf_ok);
-  uint32_t status = r.status;
-#pragma unroll 1
-  for (int k = 0; k < kMsgSlots; ++k) {
-    if (r.jl[k] == 0) continue;
-    if (record_crc_wave(t, nib, g.base, rk, g.img, g.reg0 + r.jo[k], r.jl[k], lane) != r.ex[k]) status |= record_bit(k);
-  }
-  if (lane == 0) {
-    a.status[i] = status;
-    if (a.msg_end) a.msg_end[i] = r.end ? off + r.end : 0;
-  }
-  st_ret = status;
-  end_ret = r.end;
-}
 
 // The transform's fast path for message i (FusedArgs::out; verify status st, end `end`): a clean
 // PUT at header V3 with canonical V5 properties and a Blob_Format_V3 record, followed directly by

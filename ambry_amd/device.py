@@ -167,6 +167,12 @@ def set_region_mode(device: int, mode) -> None:
     check(lib().ambrycrc_set_region_mode(device, m), "ambrycrc_set_region_mode")
 
 
+def set_put_assembly(device: int, max_bytes: int) -> int:
+    """Serialize copy mode: messages of at most max_bytes (<= 6144; 0 = none) assembled whole by
+    put_assemble_kernel (ambrycrc_set_put_assembly). Returns the previous value."""
+    return check(lib().ambrycrc_set_put_assembly(device, int(max_bytes)), "ambrycrc_set_put_assembly")
+
+
 def get_region_mode(device: int = 0) -> int:
     return check(lib().ambrycrc_get_region_mode(device), "ambrycrc_get_region_mode")
 

@@ -508,6 +508,11 @@ int ambrycrc_get_variant(int device);
  * before the first), for profiles that must say which kernels they timed. */
 int ambrycrc_set_region_mode(int device, int enable);
 int ambrycrc_get_region_mode(int device);
+/* Serialize copy mode (ambrycrc_serialize_puts_dev with both field buffers): messages of at most
+ * max_bytes (<= 6144; 0 = none) are assembled whole by one kernel -- a wave per message builds it
+ * in LDS, hashes its records and stores it as whole 16-B pieces -- instead of the layout + copy-
+ * through sweep + seal kernels. Same bytes either way. Returns the previous value. */
+int ambrycrc_set_put_assembly(int device, int max_bytes);
 int ambrycrc_last_message_mode(int device);
 /* The path the device's last ambrycrc_transform_messages_dev call (or _host slab) took: 1 = the one-pass
  * fast path alone (header V3, every message a clean dense V3 PUT with canonical properties), 0 = the

@@ -392,6 +392,41 @@ class RegionModel:
             p.append(s)
         return self.pow_(self.pow_(p[0], 4) ^ p[1], 5) ^ self.pow_(p[2], 4) ^ p[3]
 
+    def assembly_crc(self, msg: bytes, a0: int, s: int, e: int) -> int:
+        """put_assemble_kernel's record CRC (put_kernels.hip): the message on the output's 16-B grid
+        (piece p = bytes [16p - a0, 16p - a0 + 16)), each lane's pieces l, l + 64, ... up to q (the
+        piece of byte e - 1) hashed from zero with bytes outside [s, e) zeroed and the first four
+        XORed with 0xFF, folded by x^(8*1024); lanes rotated so that lane q mod 64 is last, merged by
+        the 6-level x^(8*16*2^k) tree, un-shifted by d = 16(q + 1) - a0 - e bytes."""
+        fold = lambda v: self._nib(v, K_NIB_BASE + K_FOLD_OFF)  # noqa: E731
+        tree = lambda v, k: self._nib(v, K_NIB_BASE + K_TREE_OFF + K_NIB_SET * k)  # noqa: E731
+        q = (e - 1 + a0) // 16
+        d = 16 * (q + 1) - a0 - e
+        ni = min(4, e - s)
+        acc = [0] * 64
+        for p in range(q + 1):
+            c = 0
+            for w in range(4):
+                v = 0
+                for b in range(4):
+                    pos = 16 * p - a0 + 4 * w + b
+                    x = msg[pos] if s <= pos < e else 0
+                    if s <= pos < s + ni:
+                        x ^= 0xFF
+                    v |= x << (8 * b)
+                c = self.step4(c ^ v)
+            acc[p % 64] = fold(acc[p % 64]) ^ c
+        t = [acc[(v + q + 1) % 64] for v in range(64)]  # virtual lane v
+        for k in range(6):
+            t = [t[v] ^ tree(t[v - (1 << k)], k) if v & (1 << k) else t[v] for v in range(64)]
+        V = t[63]
+        for k in range(4):
+            if d & (1 << k):
+                V = self.inv(V, k)
+        if e - s < 4:
+            V ^= 0xFFFFFFFF >> (8 * (e - s))
+        return V ^ 0xFFFFFFFF
+
     def job_crc(self, mem: bytes, reg0: int, rk, off: int, ln: int) -> int:
         if ln == 0:
             return 0

@@ -11,6 +11,16 @@ from test_put_serialize import expected, random_messages
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, params=["assembly", "jobs"])
+def put_form(request, gpu):
+    """Every test in both serialize copy-mode forms: whole-message assembly for messages of at most
+    6 KiB (put_assemble_kernel; longer ones take the jobs) and the job path alone (layout,
+    copy-through sweep, seal)."""
+    prev = gpu.set_put_assembly(0, 6144 if request.param == "assembly" else 0)
+    yield request.param
+    gpu.set_put_assembly(0, prev)
+
+
 @pytest.fixture(scope="module")
 def mf():
     import importlib.util

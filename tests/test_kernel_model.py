@@ -134,3 +134,25 @@ def test_region_wave_model_matches_zlib(ambry):
     rk = rm.runs(mem, reg0)
     for a, ln in ((0, 33000), (5, 16411), (63, 40000), (1000, 17000), (3, 59990), (129, 257 * 64)):
         assert rm.job_crc_wave(mem, reg0, rk, a, ln) == zlib.crc32(mem[a:a + ln]), (a, ln)
+
+
+def test_assembly_model_matches_zlib(ambry):
+    """The serializer's whole-message assembly (put_kernels.hip put_assemble_kernel): a record's
+    CRC from the message's pieces on the output's 16-B grid -- per-lane piece hashes folded over the
+    wave's 1 KiB chunks, the lanes rotated so the record's last piece comes last, the x^(8*16*2^k)
+    tree, the x^(-8d) un-shift -- against zlib, for records of 2 B to ~6 KiB at every message
+    alignment mod 16."""
+    import random
+    import zlib
+
+    from kernel_model import RegionModel, table_image
+
+    rm = RegionModel(table_image())
+    rng = random.Random(11)
+    msg = stream_bytes(777, 0, 6200).tobytes()
+    cases = [(0, 2), (0, 3), (5, 9), (17, 4), (40, 6 + 1000), (1063, 13 + 4096), (3, 6144)]
+    cases += [(rng.randrange(0, 6000), rng.choice([2, 3, 4, 5, 15, 16, 17, 63, 64, 65, 1024, 1040])) for _ in range(20)]
+    for a0 in (0, 1, 7, 15):
+        for s, ln in cases:
+            e = min(s + ln, len(msg))
+            assert rm.assembly_crc(msg, a0, s, e) == zlib.crc32(msg[s:e]), (a0, s, ln)
