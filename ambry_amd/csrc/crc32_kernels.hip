@@ -1902,24 +1902,25 @@ __global__ __launch_bounds__(256) void region_tail_kernel(FusedArgs f) {
   if (n <= waves && (uint64_t)blockIdx.x * (blockDim.x >> 6) >= n) return;  // no message for this block
   __shared__ uint32_t tbl[1024];
   __shared__ uint32_t nib[region::kNibTotal];
+  __shared__ uint32_t dn[region::kDirSets * region::kNibWords];
   stage_slice_tables(tbl, f.g.img);
   region::stage_nib(nib, f.g.img);
+  region::stage_direct_nib(dn, f.g.img);
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t w0 = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (n <= waves) {
-    // Few messages (the share boundaries' deferrals): a wave per message, in lane 0. Its short
-    // records are lane 0's; a long one (more than 512 runs) goes to the whole wave -- a lane alone
-    // would walk a 4 MiB record's run sums one dependent load at a time (r04: 12 ms for 4 MiB PUTs).
-    // (Every record by the wave cost 60 us per 262,144 4 KiB PUTs: a wave-wide tree per record.)
+    // Few messages (the share boundaries' deferrals): a wave per message, each short record hashed
+    // by the wave straight from the region (record_crc_direct), a long one (more than 512 runs)
+    // from the run sums (record_crc_wave). Lane 0 alone walking the run sums took 69 us per
+    // 262,144-message transform; a run-sum tree per record with gf2 multiplies, 60 us; a lane per
+    // 4 MiB message, 12 ms for 4,096 of them.
     for (uint64_t w = w0; w < n; w += waves) {
-      const bool have = lane == 0;
       const uint64_t i = all ? w : f.defer[w];
       uint32_t st;
       uint64_t mend;
-      region::process_message(f.a, f.g, tbl, region::TabC{tbl}, nib, have, i, lane, st, mend,
-                              [](uint64_t, uint64_t) -> bool { return true; }, [](uint64_t) {});
-      if constexpr (COPY) region::transform_fast(f, tbl, have, i, st, mend);
+      region::process_message_direct(f.a, f.g, tbl, nib, dn, i, lane, st, mend);
+      if constexpr (COPY) region::transform_fast(f, tbl, lane == 0, i, st, mend);
     }
     return;
   }

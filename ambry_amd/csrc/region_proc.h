@@ -138,6 +138,163 @@ __device__ __noinline__ uint32_t record_crc_wave(const uint32_t* __restrict__ t_
   return ~V;
 }
 
+// ---- the whole wave on one short record straight from the region's bytes (no run sums)
+// Used by region_tail_kernel's wave-per-message path: a deferred message's records are hashed by
+// the wave from memory in one or two round trips, where one lane walking the run sums needs ~20
+// dependent loads per message (69 us of tail per 262,144-message transform).
+// LDS sets: x^(8*64*2^k) for k = 0..5 (the tree), x^(8*4096) (the fold): the image's POW[6..12].
+constexpr uint32_t kDirSets = 7;
+constexpr uint32_t kDirFold = 6;
+__device__ __forceinline__ void stage_direct_nib(uint32_t* __restrict__ dn, const uint32_t* __restrict__ img) {
+  for (uint32_t i = threadIdx.x; i < kDirSets * kNibWords; i += blockDim.x) {
+    const uint32_t set = i / kNibWords, w = i % kNibWords;
+    dn[i] = img[(kNibBase + kPowOff + kNibSetBytes * (6 + set)) / 4 + w];
+  }
+}
+
+// Bytes [sh, sh + 16) of w0 || w1, sh wave-uniform.
+__device__ __forceinline__ u32x4 funnel_bytes(const u32x4& w0, const u32x4& w1, uint32_t sh) {
+  const uint32_t r = sh & 3u;
+  switch (sh >> 2) {
+    case 0:
+      return u32x4{__builtin_amdgcn_alignbyte(w0.y, w0.x, r), __builtin_amdgcn_alignbyte(w0.z, w0.y, r),
+                   __builtin_amdgcn_alignbyte(w0.w, w0.z, r), __builtin_amdgcn_alignbyte(w1.x, w0.w, r)};
+    case 1:
+      return u32x4{__builtin_amdgcn_alignbyte(w0.z, w0.y, r), __builtin_amdgcn_alignbyte(w0.w, w0.z, r),
+                   __builtin_amdgcn_alignbyte(w1.x, w0.w, r), __builtin_amdgcn_alignbyte(w1.y, w1.x, r)};
+    case 2:
+      return u32x4{__builtin_amdgcn_alignbyte(w0.w, w0.z, r), __builtin_amdgcn_alignbyte(w1.x, w0.w, r),
+                   __builtin_amdgcn_alignbyte(w1.y, w1.x, r), __builtin_amdgcn_alignbyte(w1.z, w1.y, r)};
+    default:
+      return u32x4{__builtin_amdgcn_alignbyte(w1.x, w0.w, r), __builtin_amdgcn_alignbyte(w1.y, w1.x, r),
+                   __builtin_amdgcn_alignbyte(w1.z, w1.y, r), __builtin_amdgcn_alignbyte(w1.w, w1.z, r)};
+  }
+}
+
+// zlib CRC-32 of the len bytes at base-relative pa, by the whole wave (every lane the same pa, len)
+// from the region's bytes: 64-B runs aligned to the record's end; in round v lane l takes run
+// R - 64(V - v) + l (runs before the record: zero), hashed from zero (bytes before pa zeroed, the
+// first four XORed with 0xFF), folded over rounds by x^(8*4096), merged by the x^(8*64*2^k) tree:
+// lane 63 ends at pb, so no un-shift. Loads are 16-B aligned blocks inside the region's first and
+// last blocks (lo16 / hi16), funnel-shifted by pb mod 16.
+__device__ __forceinline__ uint32_t record_crc_direct(const TabC& tc, const uint32_t* __restrict__ nib,
+                                                      const uint32_t* __restrict__ dn, const RegionArgs& g,
+                                                      uint64_t pa, uint64_t len, uint32_t lane) {
+  if (len < 4) return record_crc(tc, nib, g.base, g.rk + kRunPad, pa, len);  // bytes (every lane)
+  const int64_t pb = (int64_t)(pa + len);
+  const int64_t R = (int64_t)((len + 63) >> 6), V = (R + 63) >> 6;
+  const uint32_t sh = (uint32_t)(pb & 15);
+  const int64_t lo16 = (int64_t)g.lo16, hi16 = (int64_t)g.hi16;
+  const int ni = 4;
+  uint32_t acc = 0;
+  for (int64_t v = 0; v < V; ++v) {
+    const int64_t j = R - 64 * (V - v) + (int64_t)lane;  // run index from the record's first
+    uint32_t c = 0;
+    if (j >= 0) {
+      const int64_t o = pb - 64 * (R - j);  // the run's start (may precede pa)
+      u32x4 blk[5];
+#pragma unroll
+      for (int b = 0; b < 5; ++b) {
+        int64_t bo = o - (int64_t)sh + 16 * b;
+        bo = bo < lo16 ? lo16 : (bo > hi16 ? hi16 : bo);
+        blk[b] = *reinterpret_cast<const u32x4*>(g.base + bo);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        u32x4 w = funnel_bytes(blk[q], blk[q + 1], sh);
+        const int lo = (int)((int64_t)pa - (o + 16 * q));  // record bytes start at piece offset lo
+        if (lo > 0) {
+          w.x &= keep_ge(lo);
+          w.y &= keep_ge(lo - 4);
+          w.z &= keep_ge(lo - 8);
+          w.w &= keep_ge(lo - 12);
+        }
+        if (lo > -4 && lo < 16) {  // zlib's initial register over the record's first four bytes
+          w.x ^= keep_ge(lo) & keep_lt(lo + ni);
+          w.y ^= keep_ge(lo - 4) & keep_lt(lo + ni - 4);
+          w.z ^= keep_ge(lo - 8) & keep_lt(lo + ni - 8);
+          w.w ^= keep_ge(lo - 12) & keep_lt(lo + ni - 12);
+        }
+        c = tc.step4(c ^ w.x);
+        c = tc.step4(c ^ w.y);
+        c = tc.step4(c ^ w.z);
+        c = tc.step4(c ^ w.w);
+      }
+    }
+    acc = nmul(dn, acc, kDirFold) ^ c;
+  }
+  {
+    const uint32_t pt = left_partner<0>(acc);
+    if (lane & 1u) acc ^= nmul(dn, pt, 0);
+  }
+  {
+    const uint32_t pt = left_partner<1>(acc);
+    if (lane & 2u) acc ^= nmul(dn, pt, 1);
+  }
+  {
+    const uint32_t pt = left_partner<2>(acc);
+    if (lane & 4u) acc ^= nmul(dn, pt, 2);
+  }
+  {
+    const uint32_t pt = left_partner<3>(acc);
+    if (lane & 8u) acc ^= nmul(dn, pt, 3);
+  }
+  {
+    const uint32_t pt = left_partner<4>(acc);
+    if (lane & 16u) acc ^= nmul(dn, pt, 4);
+  }
+  {
+    const uint32_t pt = left_partner<5>(acc);
+    if (lane & 32u) acc ^= nmul(dn, pt, 5);
+  }
+  return ~__builtin_amdgcn_readlane(acc, 63);
+}
+
+// ONE message by the whole wave (every lane the same i; the parse repeated in every lane, the same
+// loads broadcast): short records by record_crc_direct, long ones (more than kLongRuns runs) by
+// record_crc_wave from the run sums.
+__device__ __forceinline__ void process_message_direct(const MsgArgs& a, const RegionArgs& g,
+                                                       const uint32_t* __restrict__ t, const uint32_t* __restrict__ nib,
+                                                       const uint32_t* __restrict__ dn, uint64_t i, uint32_t lane,
+                                                       uint32_t& st_ret, uint64_t& end_ret) {
+  const uint32_t* rk = g.rk + kRunPad;
+  const uint64_t off = a.msg_off[i];
+  const bool in_region = off <= a.region_len;
+  const uint64_t rem = in_region ? a.region_len - off : 0;
+  const uint8_t* p = a.region + (in_region ? off : 0);
+  const HeaderWords hw = load_header(p, rem);
+  MsgParse r;
+  PropsFields pf;
+  bool pf_ok = false;
+  parse_message<false, false>(off, in_region, rem, p, hw, t, nullptr, 0, r, pf, pf_ok);
+  uint32_t status = r.status;
+  const TabC tc{t};
+#pragma unroll 1
+  for (int k = 0; k < kMsgSlots; ++k) {
+    uint64_t jo = 0, jl = 0;
+    uint32_t ex = 0;
+#pragma unroll
+    for (int q = 0; q < kMsgSlots; ++q)
+      if (q == k) {
+        jo = r.jo[q];
+        jl = r.jl[q];
+        ex = r.ex[q];
+      }
+    if (jl == 0) continue;
+    const uint64_t pa = g.reg0 + jo;
+    const int64_t runs = (int64_t)((((pa + jl + 63) & ~uint64_t(63)) - (pa & ~uint64_t(63))) >> 6);
+    const uint32_t c = runs > kLongRuns ? record_crc_wave(t, nib, g.base, rk, g.img, pa, jl, lane)
+                                        : record_crc_direct(tc, nib, dn, g, pa, jl, lane);
+    if (c != ex) status |= record_bit(k);
+  }
+  if (lane == 0) {
+    a.status[i] = status;
+    if (a.msg_end) a.msg_end[i] = r.end ? off + r.end : 0;
+  }
+  st_ret = status;
+  end_ret = r.end;
+}
+
 // The message processor of one lane (message i when `have`), all run sums of its records
 // available: status and message end written. Long records are collected and done by the wave
 // after the per-lane ones, so every lane of the wave must call this (have = false for none).

@@ -392,6 +392,36 @@ class RegionModel:
             p.append(s)
         return self.pow_(self.pow_(p[0], 4) ^ p[1], 5) ^ self.pow_(p[2], 4) ^ p[3]
 
+    def direct_crc(self, mem: bytes, reg0: int, off: int, ln: int) -> int:
+        """region_proc.h record_crc_direct: the wave on one record straight from the bytes -- 64-B
+        runs aligned to the record's end, run R - 64(V - v) + l in lane l of round v (bytes before
+        the record zeroed, its first four XORed with 0xFF), folded by x^(8*4096), merged by the
+        x^(8*64*2^k) tree (POW[6..11]); lane 63 ends at the record's end."""
+        buf = bytes(reg0) + mem
+        pa, pb = reg0 + off, reg0 + off + ln
+        R = (ln + 63) // 64
+        V = (R + 63) // 64
+        acc = [0] * 64
+        for v in range(V):
+            for l in range(64):
+                j = R - 64 * (V - v) + l
+                c = 0
+                if j >= 0:
+                    o = pb - 64 * (R - j)
+                    for w in range(16):
+                        x = 0
+                        for b in range(4):
+                            pos = o + 4 * w + b
+                            y = buf[pos] if pa <= pos < pb else 0
+                            if pa <= pos < pa + 4:
+                                y ^= 0xFF
+                            x |= y << (8 * b)
+                        c = self.step4(c ^ x)
+                acc[l] = self.pow_(acc[l], 12) ^ c
+        for k in range(6):
+            acc = [acc[l] ^ self.pow_(acc[l - (1 << k)], 6 + k) if l & (1 << k) else acc[l] for l in range(64)]
+        return acc[63] ^ 0xFFFFFFFF
+
     def assembly_crc(self, msg: bytes, a0: int, s: int, e: int) -> int:
         """put_assemble_kernel's record CRC (put_kernels.hip): the message on the output's 16-B grid
         (piece p = bytes [16p - a0, 16p - a0 + 16)), each lane's pieces l, l + 64, ... up to q (the

@@ -156,3 +156,18 @@ def test_assembly_model_matches_zlib(ambry):
         for s, ln in cases:
             e = min(s + ln, len(msg))
             assert rm.assembly_crc(msg, a0, s, e) == zlib.crc32(msg[s:e]), (a0, s, ln)
+
+
+def test_direct_record_model_matches_zlib(ambry):
+    """The tail kernel's wave-wide record CRC straight from the region's bytes (region_proc.h
+    record_crc_direct: end-aligned 64-B runs, a fold by x^(8*4096) over rounds, the x^(8*64*2^k)
+    tree) against zlib, for records of 4 B to ~9 KiB (one and three rounds) at odd offsets."""
+    import zlib
+
+    from kernel_model import RegionModel, table_image
+
+    rm = RegionModel(table_image())
+    mem = stream_bytes(4343, 0, 12000).tobytes()
+    for reg0 in (0, 13):
+        for a, ln in ((0, 4), (1, 5), (63, 64), (7, 65), (100, 1006), (33, 4109), (5, 4096), (9, 9000)):
+            assert rm.direct_crc(mem, reg0, a, ln) == zlib.crc32(mem[a:a + ln]), (reg0, a, ln)
