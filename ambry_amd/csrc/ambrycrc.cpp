@@ -423,6 +423,7 @@ void free_ctx(DevCtx* c) {
   (void)hipSetDevice(c->device);
   (void)hipDeviceSynchronize();
   if (c->d_img) (void)hipFree(c->d_img);
+  if (c->h_words) (void)hipHostFree(c->h_words);
   for (auto& w : c->ws_list) {
     if (w.ptr) (void)hipFree(w.ptr);
     if (w.last) (void)hipEventDestroy(w.last);
@@ -630,6 +631,12 @@ int ambrycrc_init(int device) {
   if (hipMemcpy(c->d_img, img.data(), img.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
     free_ctx(c);
     return AMBRYCRC_EHIP;
+  }
+  if (hipHostMalloc(reinterpret_cast<void**>(&c->h_words), DevCtx::kHostWords * sizeof(uint32_t),
+                    hipHostMallocDefault) != hipSuccess) {
+    c->h_words = nullptr;
+    free_ctx(c);
+    return AMBRYCRC_ENOMEM;
   }
   g_ctx[device] = c;
   (void)hipSetDevice(prev);

@@ -91,6 +91,11 @@ struct DevCtx {
   std::atomic<int> last_msg_mode{-1};
   // The path the last transform took (ambrycrc_last_transform_path): 1 fast, 0 general.
   std::atomic<int> last_xform_path{-1};
+  // Pinned words for one-word device-to-host reads (the transform fast path's verdict): call k
+  // takes word k mod kHostWords, so concurrent calls do not share one.
+  static constexpr uint32_t kHostWords = 256;
+  uint32_t* h_words = nullptr;
+  std::atomic<uint32_t> h_word_next{0};
   // Processor waves of the one-pass kernels (0: per call, fused_proc_waves); AMBRYCRC_FUSED_PROC.
   int fused_proc = AMBRY_FUSED_PROC;
   uint64_t region_max = kRegionMaxPerMessage;  // region bytes per message up to which it applies

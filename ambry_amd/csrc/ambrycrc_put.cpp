@@ -250,7 +250,6 @@ int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len
   t.in_crc = scan_out + m;
   uint32_t* xstatus = t.in_crc + 4 * m;
   uint32_t* fail = xstatus + m;
-  uint32_t* xfail = fail + 1;  // set: the fast path did not take the batch (transform_head_bytes' slack)
   uint64_t* copy_off = reinterpret_cast<uint64_t*>(w + transform_head_bytes(m));
   t.pfix = reinterpret_cast<PropsFix*>(copy_off + (size_t)kPutSlots * m);
   t.img = c->d_img;
@@ -280,12 +279,11 @@ int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len
   // before the CRCs are known; the verify's CRC batch is the copy-through kernel. A message that
   // then fails verification sets `fail`, and the fallback pass below rebuilds the output exactly as
   // the three-pass form did (verify bits first, then the transform's own, then the placement).
-  if (hipMemsetAsync(fail, 0, 2 * sizeof(uint32_t), stream) != hipSuccess) return AMBRYCRC_EHIP;  // fail, xfail
   const uint32_t* general = nullptr;  // the general path's gate (null: it always runs)
   if (fast) {
     // One pass (region_fused_kernel's copy form, then region_tail_kernel): verify every message
     // while copying the region into the output; when every message qualifies the headers are
-    // patched and the general path below is skipped by its gate (*xfail == 0).
+    // patched, xfail stays 0, and the call returns without the general path below.
     FusedArgs f;
     f.a.region = d_region;
     f.a.region_len = region_len;
@@ -314,21 +312,23 @@ int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len
     f.out_len = d_out_len;
     f.life = d_life_version;
     f.xstatus = xstatus;
-    f.xfail = xfail;
-    if (hipMemsetAsync(f.ctl, 0, 8, stream) != hipSuccess) return AMBRYCRC_EHIP;
+    f.xfail = f.ctl + 2;  // ctl[0] unsorted, ctl[1] deferred count, ctl[2] xfail: one memset
+    if (hipMemsetAsync(f.ctl, 0, 12, stream) != hipSuccess) return AMBRYCRC_EHIP;
     if (launch_region_fused(f, c->num_cu, stream) != hipSuccess) return AMBRYCRC_EHIP;
     // One synchronization with the stream decides: the batch is done, or the general path runs
     // (~20 launches, ~95 us of empty dispatches if they were launched behind a device gate instead).
-    uint32_t h_xfail = 1;
-    if (hipMemcpyAsync(&h_xfail, xfail, sizeof h_xfail, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+    // The verdict comes back through a pinned word (a pageable one costs a staged copy).
+    uint32_t* h_xfail = c->h_words + (c->h_word_next.fetch_add(1) % DevCtx::kHostWords);
+    *h_xfail = 1;
+    if (hipMemcpyAsync(h_xfail, f.xfail, sizeof(uint32_t), hipMemcpyDeviceToHost, stream) != hipSuccess ||
         hipStreamSynchronize(stream) != hipSuccess)
       return AMBRYCRC_EHIP;
-    if (h_xfail == 0) {
+    if (*h_xfail == 0) {
       c->last_xform_path.store(1);
       return AMBRYCRC_OK;
     }
-    if (hipMemsetAsync(fail, 0, sizeof(uint32_t), stream) != hipSuccess) return AMBRYCRC_EHIP;
   }
+  if (hipMemsetAsync(fail, 0, sizeof(uint32_t), stream) != hipSuccess) return AMBRYCRC_EHIP;
   c->last_xform_path.store(0);
   p.gate = general;
   t.gate = general;
