@@ -344,6 +344,10 @@ struct FusedArgs {
   uint32_t* xfail = nullptr;
 };
 constexpr uint64_t kGroupBytes = 4 * kSuperBlock;
+// A message that starts in a CU's share and ends at most this far past it is finished by that
+// share's processors, its records past the share hashed straight from the bytes
+// (region::record_crc_direct); one reaching further goes to region_tail_kernel.
+constexpr uint64_t kDirectSpan = 65536;
 // Processor waves per 16-wave workgroup (the rest stream): chosen per call from the messages per
 // CU (fused_proc_waves, ambrycrc.cpp); AMBRY_FUSED_PROC > 0 or AMBRYCRC_FUSED_PROC fixes it (A/B).
 constexpr int kFusedProcMax = 12;

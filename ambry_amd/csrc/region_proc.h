@@ -303,12 +303,17 @@ __device__ __forceinline__ void process_message_direct(const MsgArgs& a, const R
 // start, end: its length); false = the lane drops it (deferred: no status written, st_ret ~0).
 // wait(need): the whole wave waits until every run up to base-relative `need` exists.
 // tr: the table access of the per-lane record CRCs (TabR in the one-pass kernel, TabC elsewhere).
+// direct_from (base-relative; ~0: none): a record ending past it has no run sums yet (it runs into
+// the next CU's share) and is hashed by the wave straight from the region's bytes
+// (record_crc_direct with dn's sets), without waiting -- so the message that straddles a share's
+// end is finished by its own share's processor instead of the tail kernel.
 template <class Tab, class Keep, class Wait>
 __device__ __forceinline__ void process_message(const MsgArgs& a, const RegionArgs& g,
                                                 const uint32_t* __restrict__ t, const Tab& tr,
                                                 const uint32_t* __restrict__ nib, bool have, uint64_t i,
                                                 uint32_t lane, uint32_t& st_ret, uint64_t& end_ret, Keep keep,
-                                                Wait wait) {
+                                                Wait wait, const uint32_t* __restrict__ dn = nullptr,
+                                                uint64_t direct_from = ~0ull) {
   const uint32_t* rk = g.rk + kRunPad;
   uint32_t status = 0;
   uint64_t end = 0, off = 0;
@@ -352,12 +357,17 @@ __device__ __forceinline__ void process_message(const MsgArgs& a, const RegionAr
     return (int64_t)((((pa + jl[k] + 63) & ~uint64_t(63)) - (pa & ~uint64_t(63))) >> 6);
   };
   int64_t lane_runs = 0;
+  uint32_t direct = 0;  // record slots hashed straight from the bytes by the wave
 #pragma unroll
-  for (int k = 0; k < kMsgSlots; ++k)
-    if (have && jl[k] != 0 && runs_of(k) > kLongRuns) {
+  for (int k = 0; k < kMsgSlots; ++k) {
+    if (!have || jl[k] == 0) continue;
+    if (g.reg0 + jo[k] + jl[k] > direct_from) {
+      direct |= 1u << k;
+    } else if (runs_of(k) > kLongRuns) {
       longs |= 1u << k;
       lane_runs += runs_of(k);
     }
+  }
   {
     const int64_t per_lane = (int64_t)wave_max_u64((uint64_t)lane_runs) / 4;
     int64_t tot = lane_runs;
@@ -365,6 +375,7 @@ __device__ __forceinline__ void process_message(const MsgArgs& a, const RegionAr
     const int64_t wave = tot / 256 + 64 * (int64_t)__popcll(__ballot(longs != 0));
     if (per_lane <= wave) longs = 0;  // every record by its lane
   }
+  longs |= direct;
   const uint32_t own_long = longs;
   for (;;) {
     const uint64_t ball = __ballot(longs != 0);
@@ -380,8 +391,13 @@ __device__ __forceinline__ void process_message(const MsgArgs& a, const RegionAr
       }
     rjo = __shfl(rjo, (int)owner);
     rjl = __shfl(rjl, (int)owner);
-    wait(g.reg0 + rjo + rjl);
-    const uint32_t c = record_crc_wave(t, nib, g.base, rk, g.img, g.reg0 + rjo, rjl, lane);
+    uint32_t c;
+    if (__shfl(direct, (int)owner) & (1u << kk)) {  // (wave-uniform) past the share: from the bytes
+      c = record_crc_direct(TabC{t}, nib, dn, g, g.reg0 + rjo, rjl, lane);
+    } else {
+      wait(g.reg0 + rjo + rjl);
+      c = record_crc_wave(t, nib, g.base, rk, g.img, g.reg0 + rjo, rjl, lane);
+    }
     if (lane == owner) {
       uint32_t e = 0;
 #pragma unroll

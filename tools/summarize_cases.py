@@ -76,8 +76,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--src", default=os.path.join(ROOT, "gpurun_out", "pmc_cases"))
     ap.add_argument("--tag", required=True)
+    ap.add_argument("--supersedes", default="", help="an earlier summary this one replaces, and why")
     args = ap.parse_args()
     res = {"what": __doc__.split("\n\n")[0], "cases": {}}
+    if args.supersedes:
+        res["supersedes"] = args.supersedes
     for cdir in sorted(glob.glob(os.path.join(args.src, "*", ""))):
         case = os.path.basename(os.path.dirname(cdir))
         info = {}
@@ -149,6 +152,20 @@ def main():
                 call["fetch_per_line"] = round(c["FETCH_SIZE"] * 1024 / info["lines"], 2)
                 call["fetch_over_bytes"] = round(c["FETCH_SIZE"] * 1024 / (info["lines"] * 128), 4)
         res["cases"][case] = {"info": info, "mode_taken": info.get("mode_taken"), "kernels": kern, "call": call}
+    # FETCH_SIZE calibration for scattered reads (MI355X_MICROARCH.md: the x2 correction is for
+    # wide streams): the scatter cases read a known number of 128-B lines; bytes per counted KiB
+    # = 128 / fetch_per_line. Applied to the per-message kernels, whose reads are scattered lines.
+    cal = [v["call"]["fetch_per_line"] for c, v in res["cases"].items()
+           if c.startswith("scatter") and "fetch_per_line" in v["call"]]
+    if cal:
+        f = 128.0 / (sum(cal) / len(cal))
+        res["scatter_fetch_factor"] = round(f, 3)
+        for v in res["cases"].values():
+            for k in ("region_msg_kernel", "region_tail_kernel", "msg_parse_kernel"):
+                row = v["kernels"].get(k)
+                if row and "FETCH_SIZE" in row["counters"]:
+                    row["hbm_bytes_scatter_calibrated"] = (f * row["counters"]["FETCH_SIZE"] +
+                                                           row["counters"].get("WRITE_SIZE", 0.0)) * 1024
     out = os.path.join(ROOT, "profiles", f"{args.tag}_small_cases.json")
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
