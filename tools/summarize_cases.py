@@ -133,13 +133,17 @@ def main():
             if "GRBM_GUI_ACTIVE" in c:
                 row["grbm_gui_active"] = c["GRBM_GUI_ACTIVE"]
             kern[k] = row
-        # the whole call: kernels launched once per call (reps + the checked first call), medians summed
-        reps = max((tv["calls"] for tv in t.values()), default=0)
-        call = {"kernels": sorted(k for k, tv in t.items() if tv["calls"] >= max(1, reps // 2)),
-                "ns": sum(tv["median_ns"] for k, tv in t.items() if tv["calls"] >= max(1, reps // 2))}
-        hb = [kern[k].get("hbm_bytes") for k in call["kernels"]]
-        if hb and all(x is not None for x in hb):
-            call["hbm_bytes"] = sum(hb)
+        # the whole call: the calls are those of the kernel with the most total time; a kernel
+        # launched at least half as often belongs to every call, `per_call` times (a transform runs
+        # the plan kernels twice per call), medians summed
+        heavy = max(t.values(), key=lambda tv: tv["median_ns"] * tv["calls"], default=None)
+        reps = heavy["calls"] if heavy else 0
+        per_call = {k: max(1, round(tv["calls"] / reps)) for k, tv in t.items() if reps and tv["calls"] >= max(1, reps // 2)}
+        call = {"kernels": sorted(per_call), "launches_per_call": per_call,
+                "ns": sum(t[k]["median_ns"] * n for k, n in per_call.items())}
+        hb = [(kern[k].get("hbm_bytes"), n) for k, n in per_call.items()]
+        if hb and all(x is not None for x, _ in hb):
+            call["hbm_bytes"] = sum(x * n for x, n in hb)
         if alg and call["ns"]:
             call["alg_bytes"] = alg
             call["achieved_GBps"] = round(alg / call["ns"], 1)
