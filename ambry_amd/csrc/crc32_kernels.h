@@ -136,11 +136,11 @@ constexpr uint64_t kSuperBlock = 4096;
 // 1.21x, 2.2 KiB 1.35x, 3.2 KiB 1.17x, 4.2 KiB 1.07x, 5.3 KiB 1.02x; 64 KiB blobs stream in job mode.
 constexpr uint64_t kRegionMaxPerMessage = 6144;
 // Region bytes per message up to which the transform (header V3 out) tries the one-pass fast path
-// first. Fast / general path on one box (profiles/r04o_put_*.jsonl): 5.3 KiB per message 0.757 /
-// 1.163 ms (262,144 4 KiB PUTs), 17.4 KiB 0.672 / 0.645, 67 KiB 3.85 / 1.96 -- past a few KiB the
-// processors' record CRCs no longer hide under the stream.
-// AMBRYCRC_XFORM_FAST_MAX overrides it (A/B; 0 = never).
-constexpr uint64_t kXformFastMaxPerMessage = 8192;
+// first. Fast / general path, ms per ~1.2 GB batch, interleaved on one box (profiles/
+// r04x_put_xform_fastmax*.jsonl): 9.2 KiB per message 0.631-0.634 / 0.899-0.903, 17.4 KiB
+// 0.616-0.619 / 0.624, 33.8 KiB 0.593-0.597 / 0.595; 5.3 KiB 0.693-0.697 / 1.163; 67 KiB (before
+// the tail work) 2.07 / 1.96. AMBRYCRC_XFORM_FAST_MAX overrides it (A/B; 0 = never).
+constexpr uint64_t kXformFastMaxPerMessage = 24576;
 inline uint64_t region_nsb(const uint8_t* region, uint64_t len) {
   const uint64_t b = reinterpret_cast<uintptr_t>(region) & ~uint64_t(63);
   return (reinterpret_cast<uintptr_t>(region) + len - b + kSuperBlock - 1) / kSuperBlock;

@@ -439,7 +439,7 @@ def test_transform_fast_path_long_messages(gpu, mf):
         msgs.append(mf.put_message(mf.store_key("long-%d" % i), mf.blob_properties_bytes(blen), b"um" * (i % 9),
                                    content, version=3))
     region = b"".join(msgs)
-    assert len(region) <= 8192 * len(msgs)  # the fast path's cut-off
+    assert len(region) <= 24576 * len(msgs)  # the fast path's cut-off
     offs = np.cumsum([0] + [len(x) for x in msgs[:-1]]).tolist()
     dev = torch.frombuffer(bytearray(region), dtype=torch.uint8).cuda()
     out, oo, ol, st = transform_dev(dev, torch.tensor(offs, dtype=torch.int64, device="cuda"), header_version=3)

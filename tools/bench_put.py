@@ -187,7 +187,8 @@ def main():
 
     torch.cuda.set_device(0)
     D.init(0)
-    cases = {"64k": (65536, 64 << 10), "16k": (65536, 16 << 10), "4k": (262144, 4 << 10), "4m": (4096, 4 << 20)}
+    cases = {"64k": (65536, 64 << 10), "32k": (32768, 32 << 10), "16k": (65536, 16 << 10), "8k": (131072, 8 << 10),
+             "4k": (262144, 4 << 10), "4m": (4096, 4 << 20)}
     for c in [x for x in args.cases.split(",") if x]:
         m, s = cases[c]
         for in_place in (False, True):
