@@ -1917,7 +1917,7 @@ __global__ __launch_bounds__(256) void region_tail_kernel(FusedArgs f) {
   if (n <= waves) {
     // Few messages (the share boundaries' deferrals): a wave per message, each short record hashed
     // by the wave straight from the region (record_crc_direct), a long one (more than 512 runs)
-    // from the run sums (record_crc_wave). Lane 0 alone walking the run sums took 69 us per
+    // from the run sums (record_crc_runs_wave). Lane 0 alone walking the run sums took 69 us per
     // 262,144-message transform; a run-sum tree per record with gf2 multiplies, 60 us; a lane per
     // 4 MiB message, 12 ms for 4,096 of them.
     for (uint64_t w = w0; w < n; w += waves) {
@@ -1936,7 +1936,7 @@ __global__ __launch_bounds__(256) void region_tail_kernel(FusedArgs f) {
     uint32_t st;
     uint64_t mend;
     region::process_message(f.a, f.g, tbl, region::TabC{tbl}, nib, have, i, lane, st, mend,
-                            [](uint64_t, uint64_t) -> bool { return true; }, [](uint64_t) {});
+                            [](uint64_t, uint64_t) -> bool { return true; }, [](uint64_t) {}, dn);
     if constexpr (COPY) region::transform_fast(f, tbl, have, i, st, mend);
   }
 }

@@ -94,9 +94,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AMBRY_REGIO
   __shared__ uint32_t tbl[1024];
   __shared__ uint32_t pwin[256 * kPropsSlotWords];
   __shared__ uint32_t nib[region::kNibTotal];
+  __shared__ uint32_t dn[region::kDirSets * region::kNibWords];
+  // Long records (more than region::kLongRuns runs: a 4 MiB blob among small messages) are queued
+  // per wave and taken by the whole wave after its messages (record_crc_runs_wave): one thread
+  // walking 65,536 run sums would hold the kernel for milliseconds.
+  constexpr uint32_t kLongQ = 32;
+  __shared__ uint64_t lq_jo[4][kLongQ], lq_i[4][kLongQ];
+  __shared__ uint32_t lq_jl[4][kLongQ], lq_ex[4][kLongQ], lq_bit[4][kLongQ], lq_n[4];
   stage_slice_tables(tbl, a.img);
   region::stage_nib(nib, a.img);
+  region::stage_direct_nib(dn, a.img);
+  if (threadIdx.x < 4) lq_n[threadIdx.x] = 0;
   __syncthreads();
+  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   uint32_t* slot = pwin + threadIdx.x * kPropsSlotWords;
   const uint32_t* rk = g.rk + kRunPad;
   // Grid-stride over the messages (a grid of one thread per message unless capped; no barrier
@@ -131,15 +141,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AMBRY_REGIO
     for (int k = 0; k < kMsgSlots; ++k) {
       const uint64_t jo = off + ((uint64_t)slot[4 * k + 1] << 32 | slot[4 * k]);
       const uint32_t jl = slot[4 * k + 2], ex = slot[4 * k + 3];
+      const uint64_t pa = g.reg0 + jo;
+      if (jl && (int64_t)((((pa + jl + 63) & ~uint64_t(63)) - (pa & ~uint64_t(63))) >> 6) > region::kLongRuns) {
+        const uint32_t at = atomicAdd(&lq_n[wv], 1u);
+        if (at < kLongQ) {  // the wave's, after the loop (its bit ORed into the status then)
+          lq_jo[wv][at] = pa;
+          lq_i[wv][at] = i;
+          lq_jl[wv][at] = jl;
+          lq_ex[wv][at] = ex;
+          lq_bit[wv][at] = AMBRYCRC_MSG_ENCKEY_CRC << k;
+          continue;
+        }
+      }
 #if AMBRY_REGION_PROBE == 1
       const uint32_t c = ex;
 #else
-      const uint32_t c = jl ? region::record_crc(region::TabC{tbl}, nib, g.base, rk, g.reg0 + jo, jl) : 0u;
+      const uint32_t c = jl ? region::record_crc(region::TabC{tbl}, nib, g.base, rk, pa, jl) : 0u;
 #endif
       if (c != ex) status |= AMBRYCRC_MSG_ENCKEY_CRC << k;
     }
     a.status[i] = status;
     if (a.msg_end) a.msg_end[i] = end ? off + end : 0;
+  }
+  // the wave's long records (the loop above ended in every lane: the wave is whole again)
+  const uint32_t nq = min(__builtin_amdgcn_readfirstlane(lq_n[wv]), kLongQ);
+  for (uint32_t q = 0; q < nq; ++q) {
+    const uint64_t pa = lq_jo[wv][q];
+    const uint32_t c = region::record_crc_runs_wave(region::TabC{tbl}, nib, dn, g.base, rk, pa, lq_jl[wv][q], lane);
+    if (lane == 0 && c != lq_ex[wv][q]) atomicOr(&a.status[lq_i[wv][q]], lq_bit[wv][q]);
   }
 }
 

@@ -213,6 +213,94 @@ __device__ __forceinline__ uint32_t record_crc(const Tab& t, const uint32_t* __r
   return ~V;
 }
 
+// LDS sets: x^(8*64*2^k) for k = 0..5 (the tree), x^(8*4096) (the fold): the image's POW[6..12].
+constexpr uint32_t kDirSets = 7;
+// Records of more runs than this go to the whole wave (record_crc_runs_wave).
+constexpr int64_t kLongRuns = 512;
+constexpr uint32_t kDirFold = 6;
+__device__ __forceinline__ void stage_direct_nib(uint32_t* __restrict__ dn, const uint32_t* __restrict__ img) {
+  for (uint32_t i = threadIdx.x; i < kDirSets * kNibWords; i += blockDim.x) {
+    const uint32_t set = i / kNibWords, w = i % kNibWords;
+    dn[i] = img[(kNibBase + kPowOff + kNibSetBytes * (6 + set)) / 4 + w];
+  }
+}
+
+// zlib CRC-32 of a long record by the whole wave from the run sums (every lane the same pa, len;
+// len >= 4): the record's runs [A0, B1) as record_crc takes them (head and tail runs from the
+// bytes, the interior from rk), run n - 64(V - v) + l in lane l of round v (runs before the record:
+// zero; eight rounds' sums loaded at once), folded over rounds by x^(8*4096), merged by the
+// x^(8*64*2^k) tree from dn's LDS sets (lane 63 ends at B1), un-shifted to the record's end.
+// Nibble multiplies only: round 3's form (per-lane slices of variable length) needed gf2_mul
+// shifts -- 32-round loops -- for its tree. A 64 KiB record: 16 rounds, one memory round trip.
+template <class Tab>
+__device__ __forceinline__ uint32_t record_crc_runs_wave(const Tab& t, const uint32_t* __restrict__ nib,
+                                                         const uint32_t* __restrict__ dn,
+                                                         const uint8_t* __restrict__ base,
+                                                         const uint32_t* __restrict__ rk, uint64_t pa, uint64_t len,
+                                                         uint32_t lane) {
+  const uint64_t pb = pa + len;
+  const uint64_t A0 = pa & ~uint64_t(63), B1 = (pb + 63) & ~uint64_t(63);
+  const int64_t n = (int64_t)((B1 - A0) >> 6), k0 = (int64_t)(A0 >> 6);
+  const int lo = (int)(pa - A0), hi = pb - A0 < 64 ? (int)(pb - A0) : 64;
+  const int tin = hi - lo;
+  const bool tail_bytes = n >= 2 && (pb & 63u) != 0;
+  const int thi = (int)(pb - (B1 - 64));
+  u32x4 hw[4], tw[4];
+  load_run(base, A0, lo, hi, hw);
+  load_run(base, B1 - 64, 0, tail_bytes ? thi : 0, tw);
+  uint32_t H = hash_run(t, nib, hw, lo, hi, tin < 4 ? tin : 4);
+  if (tin < 4) H ^= 0xFFFFFFFFu >> (8 * tin);
+  const uint32_t T = tail_bytes ? hash_run(t, nib, tw, 0, thi, 0) : 0u;
+  const int64_t V = (n + 63) >> 6;
+  uint32_t acc = 0;
+  for (int64_t v0 = 0; v0 < V; v0 += 8) {
+    uint32_t sum[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int64_t r = n - 64 * (V - (v0 + u)) + (int64_t)lane;
+      sum[u] = 0;
+      if (v0 + u < V && r >= 1 && r <= n - 1 && !(r == n - 1 && tail_bytes)) sum[u] = rk[k0 + r];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (v0 + u >= V) break;
+      const int64_t r = n - 64 * (V - (v0 + u)) + (int64_t)lane;
+      const uint32_t val = r < 0 ? 0u : r == 0 ? H : (r == n - 1 && tail_bytes) ? T : sum[u];
+      acc = nmul(dn, acc, kDirFold) ^ val;
+    }
+  }
+  {
+    const uint32_t pt = left_partner<0>(acc);
+    if (lane & 1u) acc ^= nmul(dn, pt, 0);
+  }
+  {
+    const uint32_t pt = left_partner<1>(acc);
+    if (lane & 2u) acc ^= nmul(dn, pt, 1);
+  }
+  {
+    const uint32_t pt = left_partner<2>(acc);
+    if (lane & 4u) acc ^= nmul(dn, pt, 2);
+  }
+  {
+    const uint32_t pt = left_partner<3>(acc);
+    if (lane & 8u) acc ^= nmul(dn, pt, 3);
+  }
+  {
+    const uint32_t pt = left_partner<4>(acc);
+    if (lane & 16u) acc ^= nmul(dn, pt, 4);
+  }
+  {
+    const uint32_t pt = left_partner<5>(acc);
+    if (lane & 32u) acc ^= nmul(dn, pt, 5);
+  }
+  uint32_t Vv = __builtin_amdgcn_readlane(acc, 63);
+  const uint32_t d = (uint32_t)(B1 - pb);
+#pragma unroll
+  for (uint32_t k = 0; k < kInvPowSets; ++k)
+    if (d & (1u << k)) Vv = nmul(nib, Vv, kInv0 + k);
+  return ~Vv;
+}
+
 __device__ __forceinline__ uint32_t record_crc(const uint32_t* __restrict__ t, const uint32_t* __restrict__ nib,
                                                const uint8_t* __restrict__ base, const uint32_t* __restrict__ rk,
                                                uint64_t pa, uint64_t len) {

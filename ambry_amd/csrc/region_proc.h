@@ -1,8 +1,9 @@
 // region_proc.h -- the message processors of region mode: one lane per message,
 // a wave per 64 messages. A lane parses its message (msg_parse.h, properties read from memory) and
 // assembles each record's CRC from the 64-B run sums (region_crc.h); a record longer than
-// kLongRuns runs is taken by the whole wave (record_crc_wave), so one 4 MiB blob in a region of
-// small messages costs the wave ~20 us instead of one lane ~1 ms.
+// kLongRuns runs is taken by the whole wave (record_crc_runs_wave, region_crc.h), so one 4 MiB blob
+// in a region of small messages costs the wave ~1,000 folds instead of one lane ~65,000 dependent
+// Horner steps.
 //
 // Used by region_fused_kernel (crc32_kernels.hip), whose processor waves run beside its streaming
 // waves and take the messages of their CU's share as the share's run sums complete, and by
@@ -20,8 +21,6 @@
 namespace ambrycrc {
 namespace region {
 
-// Records of more runs than this go to the whole wave.
-constexpr int64_t kLongRuns = 512;
 
 __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
 #pragma unroll
@@ -38,119 +37,11 @@ __device__ __forceinline__ uint32_t wave_fold(uint32_t s, uint32_t c, uint32_t l
   return (lane & (1u << LVL)) ? (s ^ sh) : s;
 }
 
-// zlib CRC-32 of the len bytes at offset pa from base, by the whole wave (every lane passes the
-// same pa, len; every lane gets the CRC). The runs of the record are cut into 64 equal lane slices
-// of 4*gs runs aligned to the record's last run (runs before the record count as zero, as in
-// record_crc); each lane folds its slice with record_crc's four Horner streams, then a DPP tree
-// merges the lanes with the shifts x^(8*256*gs*2^k) (gf2_mul by wave-uniform constants from the
-// image's x^(8*2^k) words), and the register at B1 is un-shifted to pb.
-typedef const __attribute__((address_space(3))) uint32_t lds_u32;
-typedef const __attribute__((address_space(1))) uint32_t glb_u32;
-typedef const __attribute__((address_space(1))) uint8_t glb_u8;
-
-// Not inlined (it would add to its callers' register pressure), so its pointer arguments arrive as
-// generic pointers: they are cast back to their address spaces (t, nib: LDS; base, rk, img: global)
-// so the accesses below are ds_read / global_load, not flat (a flat access waits on both counters).
-__device__ __noinline__ uint32_t record_crc_wave(const uint32_t* __restrict__ t_g, const uint32_t* __restrict__ nib_g,
-                                                 const uint8_t* __restrict__ base_g, const uint32_t* __restrict__ rk_g,
-                                                 const uint32_t* __restrict__ img_g, uint64_t pa, uint64_t len,
-                                                 uint32_t lane) {
-  const uint32_t* __restrict__ t = (const uint32_t*)(lds_u32*)t_g;
-  const uint32_t* __restrict__ nib = (const uint32_t*)(lds_u32*)nib_g;
-  const uint8_t* __restrict__ base = (const uint8_t*)(glb_u8*)base_g;
-  const uint32_t* __restrict__ rk = (const uint32_t*)(glb_u32*)rk_g;
-  (void)img_g;
-  const TabC tc{t};
-  if (len < 4) return record_crc(tc, nib, base, rk, pa, len);  // bytes, no runs (every lane the same)
-  const uint64_t pb = pa + len;
-  const uint64_t A0 = pa & ~uint64_t(63), B1 = (pb + 63) & ~uint64_t(63);
-  const int64_t n = (int64_t)((B1 - A0) >> 6), k0 = (int64_t)(A0 >> 6);
-  const int lo = (int)(pa - A0), hi = pb - A0 < 64 ? (int)(pb - A0) : 64;
-  const int tin = hi - lo;
-  const bool tail_bytes = n >= 2 && (pb & 63u) != 0;
-  const int thi = (int)(pb - (B1 - 64));
-  const int64_t ng = (n + 3) >> 2;            // 4-run groups
-  const int64_t gs = (ng + 63) >> 6;          // groups per lane
-  const int64_t e0 = k0 + n - 256 * gs;       // virtual first run (<= k0)
-  const int64_t elast = k0 + n - 1;
-  u32x4 hw[4], tw[4];
-  load_run(base, A0, lo, hi, hw);
-  load_run(base, B1 - 64, 0, tail_bytes ? thi : 0, tw);
-  uint32_t H = hash_run(tc, nib, hw, lo, hi, tin < 4 ? tin : 4);
-  if (tin < 4) H ^= 0xFFFFFFFFu >> (8 * tin);
-  const uint32_t T = tail_bytes ? hash_run(tc, nib, tw, 0, thi, 0) : 0u;
-  // this lane's groups [g0, g0 + gs) counted from e0; groups wholly before k0 are zero
-  // (four groups per step, the next four in flight: a loop of one load per group waited a memory
-  // latency per group -- ~380 us for a 4 MiB record)
-  const int64_t g0 = (int64_t)lane * gs, g1 = g0 + gs;
-  uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-  auto load1 = [&](int64_t g, u32x4& r) {
-    const int64_t eg = e0 + 4 * g;
-    r = u32x4{0u, 0u, 0u, 0u};
-    if (g < g1 && eg + 3 >= k0) __builtin_memcpy(&r, rk + eg, 16);  // eg >= k0 - 3: inside rk's pad
-  };
-  u32x4 buf[4];  // group gb + u in buf[u]; each reloaded (for gb + 4 + u) right after its use
-#pragma unroll
-  for (int u = 0; u < 4; ++u) load1(g0 + u, buf[u]);
-  for (int64_t gb = g0; gb < g1; gb += 4) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (gb + u < g1) {
-        const int64_t eg = e0 + 4 * (gb + u);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int64_t e = eg + q;
-          const uint32_t v = e < k0 ? 0u : e == k0 ? H : (e == elast && tail_bytes) ? T : buf[u][q];
-          const uint32_t nv = nmul(nib, s0, kP256) ^ v;
-          s0 = s1;
-          s1 = s2;
-          s2 = s3;
-          s3 = nv;
-        }
-      }
-      load1(gb + 4 + u, buf[u]);
-    }
-  }
-  uint32_t V = s3 ^ nmul(nib, s2, kP64) ^ nmul(nib, s1, kP128) ^ nmul(nib, nmul(nib, s0, kP64), kP128);
-  // lane slices are 256*gs bytes: level k shifts the left half by x^(8*256*gs*2^k)
-  uint32_t c = 0x80000000u;  // x^(8*256*gs) from the LDS copy of the power words
-  {
-    uint64_t n = (uint64_t)256 * (uint64_t)gs;
-    for (uint32_t k = 0; n; ++k, n >>= 1)
-      if (n & 1u) c = gf2_mul(c, nib[kXpOff + k]);
-  }
-  V = wave_fold<0>(V, c, lane);
-  c = gf2_mul(c, c);
-  V = wave_fold<1>(V, c, lane);
-  c = gf2_mul(c, c);
-  V = wave_fold<2>(V, c, lane);
-  c = gf2_mul(c, c);
-  V = wave_fold<3>(V, c, lane);
-  c = gf2_mul(c, c);
-  V = wave_fold<4>(V, c, lane);
-  c = gf2_mul(c, c);
-  V = wave_fold<5>(V, c, lane);
-  V = __builtin_amdgcn_readlane(V, 63);
-  const uint32_t d = (uint32_t)(B1 - pb);
-#pragma unroll
-  for (uint32_t k = 0; k < kInvPowSets; ++k)
-    if (d & (1u << k)) V = nmul(nib, V, kInv0 + k);
-  return ~V;
-}
-
 // ---- the whole wave on one short record straight from the region's bytes (no run sums)
 // Used by region_tail_kernel's wave-per-message path: a deferred message's records are hashed by
 // the wave from memory in one or two round trips, where one lane walking the run sums needs ~20
-// dependent loads per message (69 us of tail per 262,144-message transform).
-// LDS sets: x^(8*64*2^k) for k = 0..5 (the tree), x^(8*4096) (the fold): the image's POW[6..12].
-constexpr uint32_t kDirSets = 7;
-constexpr uint32_t kDirFold = 6;
-__device__ __forceinline__ void stage_direct_nib(uint32_t* __restrict__ dn, const uint32_t* __restrict__ img) {
-  for (uint32_t i = threadIdx.x; i < kDirSets * kNibWords; i += blockDim.x) {
-    const uint32_t set = i / kNibWords, w = i % kNibWords;
-    dn[i] = img[(kNibBase + kPowOff + kNibSetBytes * (6 + set)) / 4 + w];
-  }
-}
+// dependent loads per message (69 us of tail per 262,144-message transform). The LDS sets (dn):
+// stage_direct_nib (region_crc.h).
 
 // Bytes [sh, sh + 16) of w0 || w1, sh wave-uniform.
 __device__ __forceinline__ u32x4 funnel_bytes(const u32x4& w0, const u32x4& w1, uint32_t sh) {
@@ -252,7 +143,7 @@ __device__ __forceinline__ uint32_t record_crc_direct(const TabC& tc, const uint
 
 // ONE message by the whole wave (every lane the same i; the parse repeated in every lane, the same
 // loads broadcast): short records by record_crc_direct, long ones (more than kLongRuns runs) by
-// record_crc_wave from the run sums.
+// record_crc_runs_wave from the run sums.
 __device__ __forceinline__ void process_message_direct(const MsgArgs& a, const RegionArgs& g,
                                                        const uint32_t* __restrict__ t, const uint32_t* __restrict__ nib,
                                                        const uint32_t* __restrict__ dn, uint64_t i, uint32_t lane,
@@ -283,7 +174,7 @@ __device__ __forceinline__ void process_message_direct(const MsgArgs& a, const R
     if (jl == 0) continue;
     const uint64_t pa = g.reg0 + jo;
     const int64_t runs = (int64_t)((((pa + jl + 63) & ~uint64_t(63)) - (pa & ~uint64_t(63))) >> 6);
-    const uint32_t c = runs > kLongRuns ? record_crc_wave(t, nib, g.base, rk, g.img, pa, jl, lane)
+    const uint32_t c = runs > kLongRuns ? record_crc_runs_wave(tc, nib, dn, g.base, rk, pa, jl, lane)
                                         : record_crc_direct(tc, nib, dn, g, pa, jl, lane);
     if (c != ex) status |= record_bit(k);
   }
@@ -312,7 +203,7 @@ __device__ __forceinline__ void process_message(const MsgArgs& a, const RegionAr
                                                 const uint32_t* __restrict__ t, const Tab& tr,
                                                 const uint32_t* __restrict__ nib, bool have, uint64_t i,
                                                 uint32_t lane, uint32_t& st_ret, uint64_t& end_ret, Keep keep,
-                                                Wait wait, const uint32_t* __restrict__ dn = nullptr,
+                                                Wait wait, const uint32_t* __restrict__ dn,
                                                 uint64_t direct_from = ~0ull) {
   const uint32_t* rk = g.rk + kRunPad;
   uint32_t status = 0;
@@ -396,7 +287,7 @@ __device__ __forceinline__ void process_message(const MsgArgs& a, const RegionAr
       c = record_crc_direct(TabC{t}, nib, dn, g, g.reg0 + rjo, rjl, lane);
     } else {
       wait(g.reg0 + rjo + rjl);
-      c = record_crc_wave(t, nib, g.base, rk, g.img, g.reg0 + rjo, rjl, lane);
+      c = record_crc_runs_wave(TabC{t}, nib, dn, g.base, rk, g.reg0 + rjo, rjl, lane);
     }
     if (lane == owner) {
       uint32_t e = 0;

@@ -494,54 +494,38 @@ class RegionModel:
 
 
     def job_crc_wave(self, mem: bytes, reg0: int, rk, off: int, ln: int) -> int:
-        """record_crc_wave (region_proc.h): the record's runs cut into 64 lane slices of 4*gs runs
-        aligned to its last run, each folded with the four Horner streams, the lanes merged by a
-        tree of shifts x^(8*256*gs*2^k) (gf2_mul by the image's x^(8*2^k) words), then the un-shift."""
+        """region_crc.h record_crc_runs_wave: a long record by the whole wave from the run sums --
+        the record's runs [A0, B1) (head and tail runs from the bytes, as job_crc), run
+        n - 64(V - v) + l in lane l of round v, folded over rounds by x^(8*4096) (POW[12]), merged by
+        the x^(8*64*2^k) tree (POW[6 + k]), lane 63 ending at B1, then the x^(-8d) un-shift."""
         nruns = len(rk)
         buf = bytes(reg0) + mem + bytes(nruns * 64 - reg0 - len(mem))
         pa = reg0 + off
         pb = pa + ln
         A0, B1 = pa & ~63, (pb + 63) & ~63
-        n, k0 = (B1 - A0) >> 6, A0 >> 6
+        n, k0 = (B1 - A0) // 64, A0 // 64
         lo, hi = pa - A0, min(pb - A0, 64)
         tin = hi - lo
+        tail_bytes = n >= 2 and (pb & 63) != 0
         H = self.run_bytes(buf, A0, lo, hi, min(tin, 4))
         if tin < 4:
             H ^= 0xFFFFFFFF >> (8 * tin)
-        tail = n >= 2 and pb & 63 != 0
-        T = self.run_bytes(buf, B1 - 64, 0, pb - (B1 - 64), 0) if tail else 0
-        ng = (n + 3) >> 2
-        gs = (ng + 63) >> 6
-        e0, elast = k0 + n - 256 * gs, k0 + n - 1
-        lanes = []
-        for lane in range(64):
-            s = [0, 0, 0, 0]
-            for g in range(lane * gs, lane * gs + gs):
-                for q in range(4):
-                    e = e0 + 4 * g + q
-                    v = 0 if e < k0 else H if e == k0 else T if (e == elast and tail) else rk[e]
-                    s = [s[1], s[2], s[3], self.pow_(s[0], 8) ^ v]
-            lanes.append(s[3] ^ self.pow_(s[2], 6) ^ self.pow_(s[1], 7) ^ self.pow_(self.pow_(s[0], 6), 7))
-        xp = [int(x) for x in self.img[K_LDS_BYTES // 4:K_LDS_BYTES // 4 + 64]]
-        c = 0x80000000
-        nb = 256 * gs
-        for k in range(64):
-            if nb >> k & 1:
-                c = gf2_mul(c, xp[k])
-        for lvl in range(6):  # lane l with bit lvl set takes lane l - 2^lvl, shifted
-            new = list(lanes)
-            for lane in range(64):
-                if lane >> lvl & 1:
-                    new[lane] = lanes[lane] ^ gf2_mul(lanes[lane - (1 << lvl)], c)
-            lanes = new
-            c = gf2_mul(c, c)
-        V = lanes[63]
+        T = self.run_bytes(buf, B1 - 64, 0, pb - (B1 - 64), 0) if tail_bytes else 0
+        V = (n + 63) // 64
+        acc = [0] * 64
+        for v in range(V):
+            for l in range(64):
+                r = n - 64 * (V - v) + l
+                val = 0 if r < 0 else H if r == 0 else T if (r == n - 1 and tail_bytes) else rk[k0 + r]
+                acc[l] = self.pow_(acc[l], 12) ^ val
+        for k in range(6):
+            acc = [acc[l] ^ self.pow_(acc[l - (1 << k)], 6 + k) if l & (1 << k) else acc[l] for l in range(64)]
+        x = acc[63]
         d = B1 - pb
-        for k in range(K_INV_SETS):
-            if d >> k & 1:
-                V = self.inv(V, k)
-        return V ^ 0xFFFFFFFF
-
+        for k in range(6):
+            if d & (1 << k):
+                x = self.inv(x, k)
+        return x ^ 0xFFFFFFFF
 
 def snap_cut(cs: int, ln: int, r: int) -> int:
     a = (cs + r + 15) & ~15

@@ -120,10 +120,10 @@ def test_region_model_matches_zlib(ambry):
 
 
 def test_region_wave_model_matches_zlib(ambry):
-    """The whole-wave form of a long record's CRC (region_proc.h record_crc_wave: 64 lane slices of
-    4*gs runs aligned to the record's last run, lane partials merged by a DPP tree of gf2 shifts by
-    x^(8*256*gs*2^k)) against zlib, on records from 1 to ~3 groups per lane, starting and ending at
-    odd offsets, in a region whose start is not 64-aligned."""
+    """The whole-wave form of a long record's CRC (region_crc.h record_crc_runs_wave: rounds of 64
+    run sums aligned to the record's last run, folded by x^(8*4096), merged by the x^(8*64*2^k) DPP
+    tree, un-shifted to the record's end) against zlib, on records of one to ~15 rounds starting
+    and ending at odd offsets, in a region whose start is not 64-aligned."""
     import zlib
 
     from kernel_model import RegionModel, table_image
