@@ -214,7 +214,7 @@ __device__ __forceinline__ uint32_t record_crc(const Tab& t, const uint32_t* __r
 }
 
 // LDS sets: x^(8*64*2^k) for k = 0..5 (the tree), x^(8*4096) (the fold): the image's POW[6..12].
-constexpr uint32_t kDirSets = 7;
+constexpr uint32_t kDirSets = 9;  // + x^(8*8192), x^(8*16384): record_crc_runs_wave's four streams
 // Records of more runs than this go to the whole wave (record_crc_runs_wave).
 constexpr int64_t kLongRuns = 512;
 constexpr uint32_t kDirFold = 6;
@@ -251,24 +251,35 @@ __device__ __forceinline__ uint32_t record_crc_runs_wave(const Tab& t, const uin
   uint32_t H = hash_run(t, nib, hw, lo, hi, tin < 4 ? tin : 4);
   if (tin < 4) H ^= 0xFFFFFFFFu >> (8 * tin);
   const uint32_t T = tail_bytes ? hash_run(t, nib, tw, 0, thi, 0) : 0u;
-  const int64_t V = (n + 63) >> 6;
-  uint32_t acc = 0;
-  for (int64_t v0 = 0; v0 < V; v0 += 8) {
-    uint32_t sum[8];
+  // V rounds padded at the front to a multiple of four; round v feeds stream v mod 4, each stream
+  // folded by x^(8*16384): four independent chains a quarter as deep (a 4 MiB record: 256 steps,
+  // not 1,024), sixteen rounds' sums in flight
+  const int64_t V = (((n + 63) >> 6) + 3) & ~int64_t(3);
+  uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+  for (int64_t v0 = 0; v0 < V; v0 += 16) {
+    uint32_t sum[16];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < 16; ++u) {
       const int64_t r = n - 64 * (V - (v0 + u)) + (int64_t)lane;
       sum[u] = 0;
       if (v0 + u < V && r >= 1 && r <= n - 1 && !(r == n - 1 && tail_bytes)) sum[u] = rk[k0 + r];
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < 16; u += 4) {
       if (v0 + u >= V) break;
-      const int64_t r = n - 64 * (V - (v0 + u)) + (int64_t)lane;
-      const uint32_t val = r < 0 ? 0u : r == 0 ? H : (r == n - 1 && tail_bytes) ? T : sum[u];
-      acc = nmul(dn, acc, kDirFold) ^ val;
+      uint32_t val[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t r = n - 64 * (V - (v0 + u + q)) + (int64_t)lane;
+        val[q] = r < 0 ? 0u : r == 0 ? H : (r == n - 1 && tail_bytes) ? T : sum[u + q];
+      }
+      s0 = nmul(dn, s0, kDirFold + 2) ^ val[0];
+      s1 = nmul(dn, s1, kDirFold + 2) ^ val[1];
+      s2 = nmul(dn, s2, kDirFold + 2) ^ val[2];
+      s3 = nmul(dn, s3, kDirFold + 2) ^ val[3];
     }
   }
+  uint32_t acc = nmul(dn, nmul(dn, nmul(dn, s0, kDirFold) ^ s1, kDirFold) ^ s2, kDirFold) ^ s3;
   {
     const uint32_t pt = left_partner<0>(acc);
     if (lane & 1u) acc ^= nmul(dn, pt, 0);

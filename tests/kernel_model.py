@@ -511,13 +511,14 @@ class RegionModel:
         if tin < 4:
             H ^= 0xFFFFFFFF >> (8 * tin)
         T = self.run_bytes(buf, B1 - 64, 0, pb - (B1 - 64), 0) if tail_bytes else 0
-        V = (n + 63) // 64
-        acc = [0] * 64
+        V = ((n + 63) // 64 + 3) & ~3  # padded at the front; round v feeds stream v mod 4
+        st = [[0] * 4 for _ in range(64)]
         for v in range(V):
             for l in range(64):
                 r = n - 64 * (V - v) + l
                 val = 0 if r < 0 else H if r == 0 else T if (r == n - 1 and tail_bytes) else rk[k0 + r]
-                acc[l] = self.pow_(acc[l], 12) ^ val
+                st[l][v % 4] = self.pow_(st[l][v % 4], 14) ^ val
+        acc = [self.pow_(self.pow_(self.pow_(s[0], 12) ^ s[1], 12) ^ s[2], 12) ^ s[3] for s in st]
         for k in range(6):
             acc = [acc[l] ^ self.pow_(acc[l - (1 << k)], 6 + k) if l & (1 << k) else acc[l] for l in range(64)]
         x = acc[63]
