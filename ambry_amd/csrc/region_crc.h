@@ -253,24 +253,17 @@ __device__ __forceinline__ uint32_t record_crc_runs_wave(const Tab& t, const uin
   const uint32_t T = tail_bytes ? hash_run(t, nib, tw, 0, thi, 0) : 0u;
   // V rounds padded at the front to a multiple of four; round v feeds stream v mod 4, each stream
   // folded by x^(8*16384): four independent chains a quarter as deep (a 4 MiB record: 256 steps,
-  // not 1,024), the next sixteen rounds' sums in flight while these are folded
+  // not 1,024), sixteen rounds' sums in flight
   const int64_t V = (((n + 63) >> 6) + 3) & ~int64_t(3);
   uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-  auto load16 = [&](int64_t v0, uint32_t (&sum)[16]) {
+  for (int64_t v0 = 0; v0 < V; v0 += 16) {
+    uint32_t sum[16];
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
       const int64_t r = n - 64 * (V - (v0 + u)) + (int64_t)lane;
       sum[u] = 0;
       if (v0 + u < V && r >= 1 && r <= n - 1 && !(r == n - 1 && tail_bytes)) sum[u] = rk[k0 + r];
     }
-  };
-  uint32_t nxt[16];
-  load16(0, nxt);
-  for (int64_t v0 = 0; v0 < V; v0 += 16) {
-    uint32_t sum[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) sum[u] = nxt[u];
-    if (v0 + 16 < V) load16(v0 + 16, nxt);  // the next sixteen rounds in flight meanwhile
 #pragma unroll
     for (int u = 0; u < 16; u += 4) {
       if (v0 + u >= V) break;
