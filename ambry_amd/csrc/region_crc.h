@@ -214,7 +214,11 @@ __device__ __forceinline__ uint32_t record_crc(const Tab& t, const uint32_t* __r
 }
 
 // LDS sets: x^(8*64*2^k) for k = 0..5 (the tree), x^(8*4096) (the fold): the image's POW[6..12].
-constexpr uint32_t kDirSets = 9;  // + x^(8*8192), x^(8*16384): record_crc_runs_wave's four streams
+// x^(8*2^(6+s)) for s = 0..10 (the image's POW[6..16]): record_crc_direct's tree (s = 0..5,
+// 64-B runs) and fold (s = 6); record_crc_runs_wave's in-lane fold of 64-B runs (s = 0), tree of
+// 256-B lane slices (s = 2..7), round combine (s = 8) and stream fold (s = 10).
+constexpr uint32_t kDirSets = 11;
+constexpr uint32_t kDirRun = 0, kDirRunTree = 2, kDirRound = 8, kDirStream = 10;
 // Records of more runs than this go to the whole wave (record_crc_runs_wave).
 constexpr int64_t kLongRuns = 512;
 constexpr uint32_t kDirFold = 6;
@@ -227,11 +231,12 @@ __device__ __forceinline__ void stage_direct_nib(uint32_t* __restrict__ dn, cons
 
 // zlib CRC-32 of a long record by the whole wave from the run sums (every lane the same pa, len;
 // len >= 4): the record's runs [A0, B1) as record_crc takes them (head and tail runs from the
-// bytes, the interior from rk), run n - 64(V - v) + l in lane l of round v (runs before the record:
-// zero; eight rounds' sums loaded at once), folded over rounds by x^(8*4096), merged by the
-// x^(8*64*2^k) tree from dn's LDS sets (lane 63 ends at B1), un-shifted to the record's end.
+// bytes, the interior from rk), in rounds of 256 aligned to the record's last run -- lane l takes
+// runs 4l .. 4l + 3 of a round (one 16-B load of sums, folded by x^(8*64)) -- four streams of rounds
+// folded by x^(8*65536), combined by x^(8*16384), the lanes merged by the tree over 256-B slices
+// (x^(8*256*2^k)) from dn's LDS sets (lane 63 ends at B1), then un-shifted to the record's end.
 // Nibble multiplies only: round 3's form (per-lane slices of variable length) needed gf2_mul
-// shifts -- 32-round loops -- for its tree. A 64 KiB record: 16 rounds, one memory round trip.
+// shifts -- 32-round loops -- for its tree.
 template <class Tab>
 __device__ __forceinline__ uint32_t record_crc_runs_wave(const Tab& t, const uint32_t* __restrict__ nib,
                                                          const uint32_t* __restrict__ dn,
@@ -251,58 +256,66 @@ __device__ __forceinline__ uint32_t record_crc_runs_wave(const Tab& t, const uin
   uint32_t H = hash_run(t, nib, hw, lo, hi, tin < 4 ? tin : 4);
   if (tin < 4) H ^= 0xFFFFFFFFu >> (8 * tin);
   const uint32_t T = tail_bytes ? hash_run(t, nib, tw, 0, thi, 0) : 0u;
-  // V rounds padded at the front to a multiple of four; round v feeds stream v mod 4, each stream
-  // folded by x^(8*16384): four independent chains a quarter as deep (a 4 MiB record: 256 steps,
-  // not 1,024), sixteen rounds' sums in flight
-  const int64_t V = (((n + 63) >> 6) + 3) & ~int64_t(3);
+  // Rounds of 256 runs, lane l taking runs 4l .. 4l + 3 of each (one 16-B load of sums, folded in
+  // the lane by x^(8*64)), V rounds padded at the front to a multiple of four; round v feeds stream
+  // v mod 4, each folded by x^(8*65536): four independent chains, eight rounds' sums in flight.
+  // (A run a lane a round took one 4-B load each: ~64 round trips per 4 MiB record.)
+  const int64_t V = (((n + 255) >> 8) + 3) & ~int64_t(3);
   uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-  for (int64_t v0 = 0; v0 < V; v0 += 16) {
-    uint32_t sum[16];
+  for (int64_t v0 = 0; v0 < V; v0 += 8) {
+    u32x4 sum[8];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int64_t r = n - 64 * (V - (v0 + u)) + (int64_t)lane;
-      sum[u] = 0;
-      if (v0 + u < V && r >= 1 && r <= n - 1 && !(r == n - 1 && tail_bytes)) sum[u] = rk[k0 + r];
+    for (int u = 0; u < 8; ++u) {
+      const int64_t r0 = n - 256 * (V - (v0 + u)) + 4 * (int64_t)lane;
+      sum[u] = u32x4{0u, 0u, 0u, 0u};
+      if (v0 + u < V && r0 + 3 >= 1) __builtin_memcpy(&sum[u], rk + k0 + r0, 16);  // r0 >= -3: inside rk's pad
     }
 #pragma unroll
-    for (int u = 0; u < 16; u += 4) {
+    for (int u = 0; u < 8; u += 4) {
       if (v0 + u >= V) break;
-      uint32_t val[4];
+      uint32_t w[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int64_t r = n - 64 * (V - (v0 + u + q)) + (int64_t)lane;
-        val[q] = r < 0 ? 0u : r == 0 ? H : (r == n - 1 && tail_bytes) ? T : sum[u + q];
+        const int64_t r0 = n - 256 * (V - (v0 + u + q)) + 4 * (int64_t)lane;
+        uint32_t x = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int64_t r = r0 + j;
+          const uint32_t val = r < 0 ? 0u : r == 0 ? H : (r == n - 1 && tail_bytes) ? T : sum[u + q][j];
+          x = j ? nmul(dn, x, kDirRun) ^ val : val;
+        }
+        w[q] = x;
       }
-      s0 = nmul(dn, s0, kDirFold + 2) ^ val[0];
-      s1 = nmul(dn, s1, kDirFold + 2) ^ val[1];
-      s2 = nmul(dn, s2, kDirFold + 2) ^ val[2];
-      s3 = nmul(dn, s3, kDirFold + 2) ^ val[3];
+      s0 = nmul(dn, s0, kDirStream) ^ w[0];
+      s1 = nmul(dn, s1, kDirStream) ^ w[1];
+      s2 = nmul(dn, s2, kDirStream) ^ w[2];
+      s3 = nmul(dn, s3, kDirStream) ^ w[3];
     }
   }
-  uint32_t acc = nmul(dn, nmul(dn, nmul(dn, s0, kDirFold) ^ s1, kDirFold) ^ s2, kDirFold) ^ s3;
+  uint32_t acc = nmul(dn, nmul(dn, nmul(dn, s0, kDirRound) ^ s1, kDirRound) ^ s2, kDirRound) ^ s3;
   {
     const uint32_t pt = left_partner<0>(acc);
-    if (lane & 1u) acc ^= nmul(dn, pt, 0);
+    if (lane & 1u) acc ^= nmul(dn, pt, kDirRunTree + 0);
   }
   {
     const uint32_t pt = left_partner<1>(acc);
-    if (lane & 2u) acc ^= nmul(dn, pt, 1);
+    if (lane & 2u) acc ^= nmul(dn, pt, kDirRunTree + 1);
   }
   {
     const uint32_t pt = left_partner<2>(acc);
-    if (lane & 4u) acc ^= nmul(dn, pt, 2);
+    if (lane & 4u) acc ^= nmul(dn, pt, kDirRunTree + 2);
   }
   {
     const uint32_t pt = left_partner<3>(acc);
-    if (lane & 8u) acc ^= nmul(dn, pt, 3);
+    if (lane & 8u) acc ^= nmul(dn, pt, kDirRunTree + 3);
   }
   {
     const uint32_t pt = left_partner<4>(acc);
-    if (lane & 16u) acc ^= nmul(dn, pt, 4);
+    if (lane & 16u) acc ^= nmul(dn, pt, kDirRunTree + 4);
   }
   {
     const uint32_t pt = left_partner<5>(acc);
-    if (lane & 32u) acc ^= nmul(dn, pt, 5);
+    if (lane & 32u) acc ^= nmul(dn, pt, kDirRunTree + 5);
   }
   uint32_t Vv = __builtin_amdgcn_readlane(acc, 63);
   const uint32_t d = (uint32_t)(B1 - pb);

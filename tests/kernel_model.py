@@ -497,7 +497,7 @@ class RegionModel:
         """region_crc.h record_crc_runs_wave: a long record by the whole wave from the run sums --
         the record's runs [A0, B1) (head and tail runs from the bytes, as job_crc), run
         n - 64(V - v) + l in lane l of round v, folded over rounds by x^(8*4096) (POW[12]), merged by
-        the x^(8*64*2^k) tree (POW[6 + k]), lane 63 ending at B1, then the x^(-8d) un-shift."""
+        the tree over 256-B lane slices (POW[8 + k]), lane 63 ending at B1, then the x^(-8d) un-shift."""
         nruns = len(rk)
         buf = bytes(reg0) + mem + bytes(nruns * 64 - reg0 - len(mem))
         pa = reg0 + off
@@ -511,16 +511,19 @@ class RegionModel:
         if tin < 4:
             H ^= 0xFFFFFFFF >> (8 * tin)
         T = self.run_bytes(buf, B1 - 64, 0, pb - (B1 - 64), 0) if tail_bytes else 0
-        V = ((n + 63) // 64 + 3) & ~3  # padded at the front; round v feeds stream v mod 4
+        V = ((n + 255) // 256 + 3) & ~3  # 256-run rounds padded at the front; round v -> stream v mod 4
         st = [[0] * 4 for _ in range(64)]
         for v in range(V):
             for l in range(64):
-                r = n - 64 * (V - v) + l
-                val = 0 if r < 0 else H if r == 0 else T if (r == n - 1 and tail_bytes) else rk[k0 + r]
-                st[l][v % 4] = self.pow_(st[l][v % 4], 14) ^ val
-        acc = [self.pow_(self.pow_(self.pow_(s[0], 12) ^ s[1], 12) ^ s[2], 12) ^ s[3] for s in st]
+                x = 0
+                for j in range(4):  # lane l: runs 4l .. 4l + 3 of the round, folded by x^(8*64)
+                    r = n - 256 * (V - v) + 4 * l + j
+                    val = 0 if r < 0 else H if r == 0 else T if (r == n - 1 and tail_bytes) else rk[k0 + r]
+                    x = self.pow_(x, 6) ^ val if j else val
+                st[l][v % 4] = self.pow_(st[l][v % 4], 16) ^ x
+        acc = [self.pow_(self.pow_(self.pow_(s[0], 14) ^ s[1], 14) ^ s[2], 14) ^ s[3] for s in st]
         for k in range(6):
-            acc = [acc[l] ^ self.pow_(acc[l - (1 << k)], 6 + k) if l & (1 << k) else acc[l] for l in range(64)]
+            acc = [acc[l] ^ self.pow_(acc[l - (1 << k)], 8 + k) if l & (1 << k) else acc[l] for l in range(64)]
         x = acc[63]
         d = B1 - pb
         for k in range(6):
