@@ -12,8 +12,8 @@ timeout -k 10 300 python tools/bench_messages.py --cases ${MSG_CASES:-4k,1k,100,
 grep -o '"config": "[^"]*"\|"mode_taken": "[^"]*"\|"ms_median": [0-9.]*\|"GiBps": [0-9.]*' gpurun_out/${TAG}_messages.jsonl | paste - - - - | grep -v C1
 timeout -k 10 400 python tools/bench_put.py --cases ${PUT_CASES:-4k,64k} --transform ${XFORM_CASES:-64k,4k,4m} --copy-only > gpurun_out/${TAG}_put.jsonl 2>&1 || { echo PUT_BENCH_FAILED; tail -5 gpurun_out/${TAG}_put.jsonl; exit 1; }
 grep -o '"case": "[^"]*"\|"ms_median": [0-9.]*' gpurun_out/${TAG}_put.jsonl | paste - -
-if [ -n "${KT_CASES:-msg4k msg1k xform4k}" ]; then
-  TAG=${TAG}_kt CASES="${KT_CASES:-msg4k msg1k xform4k}" timeout -k 10 400 bash tools/kt_cases.sh > /dev/null 2>&1 || { echo KT_FAILED; exit 1; }
+if [ -n "${KT_CASES-msg4k msg1k xform4k}" ]; then
+  TAG=${TAG}_kt CASES="${KT_CASES-msg4k msg1k xform4k}" timeout -k 10 400 bash tools/kt_cases.sh > /dev/null 2>&1 || { echo KT_FAILED; exit 1; }
   python tools/kt_summary.py gpurun_out/kt/${TAG}_kt | grep -v "rocprim\|at::native\|rocclr\|fill_splitmix"
 fi
 timeout -k 10 300 python bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || { echo BENCH_FAILED; tail -5 gpurun_out/${TAG}_bench.err; exit 1; }
