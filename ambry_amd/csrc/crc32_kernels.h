@@ -348,6 +348,9 @@ constexpr uint64_t kGroupBytes = 4 * kSuperBlock;
 // share's processors, its records past the share hashed straight from the bytes
 // (region::record_crc_direct); one reaching further goes to region_tail_kernel.
 constexpr uint64_t kDirectSpan = 65536;
+// Bytes at a message's start that the transform's fast path may rewrite in `out` (the header's life
+// version and CRC; header V3 is 40 B).
+constexpr uint64_t kHeaderPatchMax = 64;
 // Processor waves per 16-wave workgroup (the rest stream): chosen per call from the messages per
 // CU (fused_proc_waves, ambrycrc.cpp); AMBRY_FUSED_PROC > 0 or AMBRYCRC_FUSED_PROC fixes it (A/B).
 constexpr int kFusedProcMax = 12;

@@ -1877,15 +1877,24 @@ __global__ __launch_bounds__(1024) void region_fused_kernel(FusedArgs f) {
       // the lane's message ends at pos + end (base-relative): before the share, or past it (the
       // copy form: more than kDirectSpan past it; its records past the share are hashed from the
       // bytes) -> the tail's. (Measured: the copy form 0.713 -> 0.695 ms per 262,144 4 KiB PUTs;
-      // the verify form 0.385 -> 0.399 ms, so it keeps deferring them.)
-      if (pos < s_lo || pos + end > s_hi + (COPY ? kDirectSpan : 0)) {
+      // the verify form 0.385 -> 0.399 ms, so it keeps deferring them.) The copy form also defers
+      // one whose header reaches past the share: transform_fast rewrites the header in `out`, and
+      // bytes past the share are the next CU's streamers' to copy, at their own pace -- the copy
+      // could land after the patch.
+      if (pos < s_lo || pos + end > s_hi + (COPY ? kDirectSpan : 0) ||
+          (COPY && pos + end > s_hi && pos + kHeaderPatchMax > s_hi)) {
         const uint32_t at = atomicAdd(f.ctl + 1, 1u);
         if (at < f.a.m) f.defer[at] = (uint32_t)i;  // (unsorted offsets may defer more: ctl[0] covers them)
         return false;
       }
       return true;
     }, [&](uint64_t need) { wait_for(need); }, dn, COPY ? s_hi : ~0ull);
-    if constexpr (COPY) region::transform_fast(f, tbl, st != ~0u, i, st, mend);
+    if constexpr (COPY) {
+      // the header's pieces must be copied before the patch lands on them: a message whose records
+      // all lie past the share (hashed from the bytes, no wait) may not have waited for them yet
+      wait_for(region::wave_max_u64(st != ~0u ? msg_pos(f, i) + kHeaderPatchMax : 0));
+      region::transform_fast(f, tbl, st != ~0u, i, st, mend);
+    }
   }
 #if AMBRY_FUSED_PROBE == 2
   if (lane == 0) atomicMax(&g_fused_t[3 * blockIdx.x + 2], (unsigned long long)__builtin_amdgcn_s_memrealtime());
