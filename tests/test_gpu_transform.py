@@ -452,3 +452,57 @@ def test_transform_fast_path_long_messages(gpu, mf):
         o = offs[i]
         exp_st, exp = mf.transform_message(region, o, version=3)
         assert exp_st == 0 and oo[i] == o and ol[i] == len(exp) and out_h[o:o + len(exp)] == exp, i
+
+
+def test_transform_fast_path_share_boundaries(gpu, mf):
+    """Messages placed against the one-pass kernel's CU share boundaries (a region of 48 KiB per
+    CU: three 16 KiB groups per share): at each boundary B a message starts d bytes before it, for d
+    from 1 to 3000 -- headers that cross into the next CU's share (d < 64: deferred to the tail
+    kernel), and straddlers whose records lie past the share (finished by their own processor from
+    the bytes, the header patched only once its copy landed). Every message byte-exact against the
+    oracle, life versions rewritten, the fast path alone."""
+    import torch
+
+    from ambry_amd.messages import transform_dev
+
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    share = 3 * 16384
+    total = ncu * share
+    base_msg = lambda i, blen: mf.put_message(mf.store_key("sb-%d" % i), mf.blob_properties_bytes(blen),  # noqa: E731
+                                              b"m" * (i % 5), stream_bytes(900 + i, 0, blen).tobytes(), version=3)
+    ds = [1, 10, 39, 40, 41, 63, 64, 65, 100, 400, 3000]
+    rng = np.random.default_rng(17)
+    msgs, pos, i = [], 0, 0
+    for b in range(1, ncu + 1):
+        target = min(b * share - ds[b % len(ds)], total)
+        while pos < target:
+            rem = target - pos
+            ovh = len(base_msg(i, 0))  # (the key's length varies with i)
+            if ovh <= rem <= ovh + 6000:  # one message lands exactly on the target
+                blen = rem - ovh
+            else:
+                blen = int(rng.integers(200, 3000))
+                if rem - (ovh + blen) < ovh + 16:  # leave room for a landing message
+                    blen = max(0, rem - 2 * ovh - 1000)
+            m = base_msg(i, blen)
+            msgs.append(m)
+            pos += len(m)
+            i += 1
+    region = b"".join(msgs)
+    offs = np.cumsum([0] + [len(x) for x in msgs[:-1]]).tolist()
+    starts = set(offs)
+    hit = [b * share - ds[b % len(ds)] in starts for b in range(1, ncu)]
+    assert sum(hit) >= ncu // 2  # most boundaries got their placed message
+    life = np.random.default_rng(5).integers(0, 9, size=len(msgs)).astype(np.int16)
+    dev = torch.frombuffer(bytearray(region), dtype=torch.uint8).cuda()
+    assert dev.data_ptr() % 64 == 0  # the shares are then exactly 48 KiB of the region
+    out, oo, ol, st = transform_dev(dev, torch.tensor(offs, dtype=torch.int64, device="cuda"), header_version=3,
+                                    life_version=torch.from_numpy(life).cuda())
+    torch.cuda.synchronize()
+    assert st.cpu().numpy().view(np.uint32).tolist() == [0] * len(msgs)
+    assert gpu.last_transform_path(0) == 1
+    oo, ol = oo.cpu().numpy(), ol.cpu().numpy()
+    out_h = out.cpu().numpy().tobytes()
+    for k, o in enumerate(offs):
+        exp_st, exp = mf.transform_message(region, o, life=int(life[k]), version=3)
+        assert exp_st == 0 and oo[k] == o and out_h[o:o + len(exp)] == exp, k
