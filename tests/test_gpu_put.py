@@ -153,3 +153,26 @@ def test_serialize_large_blobs_copy_through(gpu, mf):
                                usermeta=stream_bytes(i, 3 << 20, 1000 + i).tobytes(),
                                blob=stream_bytes(i, 0, blen).tobytes(), header_version=3, life_version=i % 3))
     _run(gpu, mf, msgs, 1, 7, 5)
+
+
+def test_serialize_assembly_cutoff(gpu, mf, put_form):
+    """Messages of 6,100 to 6,200 bytes, byte by byte across the assembly cut-off (6,144 B: at or under
+    it the whole-message kernel writes it, over it the job path), under header versions 1-3, with and
+    without an encryption key, at unaligned output offsets: every byte as the oracle lays it out."""
+    from ambry_amd.messages import PutMessage, layout
+    from datagen import stream_bytes
+
+    msgs = []
+    for i, want in enumerate(range(6100, 6201)):
+        v = 1 + i % 3
+        enc = b"k" * (i % 17) if v >= 2 and i % 2 else None
+        base = PutMessage(key=mf.store_key("cut-%d" % i), props=mf.blob_properties_bytes(10), usermeta=b"u" * (i % 7),
+                          blob=b"", enckey=enc, header_version=v, life_version=i % 4 if v == 3 else 0)
+        L0, _ = layout(base)
+        blen = want - L0
+        props = mf.blob_properties_bytes(blen)
+        m = PutMessage(key=base.key, props=props, usermeta=base.usermeta, blob=stream_bytes(i, 3, blen).tobytes(),
+                       enckey=enc, header_version=v, life_version=base.life_version)
+        assert layout(m)[0] == want
+        msgs.append(m)
+    _run(gpu, mf, msgs, 1, 3, 5)
