@@ -18,6 +18,9 @@
 #ifndef AMBRY_REGION_WPE  // region pass 2: waves per SIMD the register budget allows
 #define AMBRY_REGION_WPE 2
 #endif
+#ifndef AMBRY_REGION_BPC_SMALL  // the same for regions of <= 1.5 KiB per message
+#define AMBRY_REGION_BPC_SMALL 3
+#endif
 #ifndef AMBRY_REGION_BPC  // region pass 2: blocks per CU (0: one thread per message)
 #define AMBRY_REGION_BPC 2
 #endif
@@ -74,6 +77,7 @@
 // X(name, default) for every knob above: ambrycrc_version() reports those that differ.
 #define AMBRY_KNOB_LIST(X)                                                                                  \
   X(AMBRY_PROPS_WIN, 96) X(AMBRY_PARSE_BPC, 2) X(AMBRY_REGION_WPE, 2) X(AMBRY_REGION_BPC, 2)                  \
+  X(AMBRY_REGION_BPC_SMALL, 3)                                                                              \
   X(AMBRY_FUSED_PROC, 0)                                                                                      \
   X(AMBRY_GRP_PRIO, 0) X(AMBRY_GRP_IL, 4) X(AMBRY_C0_G, 2) X(AMBRY_C0_NB, 8) X(AMBRY_C1_MAX, 1024)           \
   X(AMBRY_RUNS_STORE_NT, 0) X(AMBRY_RUNS_GIL, 1) X(AMBRY_PLAN_PER_BLOCK, 2048) X(AMBRY_DEFAULT_VARIANT, 29) \

@@ -540,10 +540,17 @@ hipError_t launch_msg_parse_desc(const MsgArgs& a, const TransformArgs& t, hipSt
   return hipGetLastError();
 }
 
+// Blocks per CU by message size (one box, ms per call, two interleaved runs; the
+// kernel's 145 VGPRs allow 3 waves per SIMD): 2 blocks per CU 0.376 / 0.375 / 0.535 for 4 KiB /
+// 1 KiB / 100-B blobs (5.3 / 2.2 / 1.3 KiB per message); 3: 0.383 / 0.391 / 0.522 -- more messages
+// in flight pay only when each is small. Regions of at most kRegionSmallPerMessage bytes per
+// message take AMBRY_REGION_BPC_SMALL blocks per CU.
+constexpr uint64_t kRegionSmallPerMessage = 1536;
 hipError_t launch_region_msg(const MsgArgs& a, const RegionArgs& g, int num_cu, hipStream_t s) {
   if (a.m == 0) return hipSuccess;
+  const uint64_t bpc = a.region_len <= kRegionSmallPerMessage * a.m ? AMBRY_REGION_BPC_SMALL : AMBRY_REGION_BPC;
   uint64_t blocks = (a.m + 255) / 256;
-  if (AMBRY_REGION_BPC > 0 && blocks > (uint64_t)num_cu * AMBRY_REGION_BPC) blocks = (uint64_t)num_cu * AMBRY_REGION_BPC;
+  if (bpc > 0 && blocks > (uint64_t)num_cu * bpc) blocks = (uint64_t)num_cu * bpc;
   hipLaunchKernelGGL(region_msg_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, a, g);
   return hipGetLastError();
 }
