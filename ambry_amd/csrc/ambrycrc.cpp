@@ -1012,14 +1012,22 @@ size_t msg_jobs_bytes(size_t m) {
 }
 
 // A processor wave finishes a 64-message batch in ~20-40 us (a chain of dependent reads under the
-// streamers' load), so the processors a CU needs grow with its messages; the rest of its 16 waves
-// stream. One processor per 128 messages per CU, 2 to 10 (r04f sweep: 4 KiB blobs, 1,024 messages
-// per CU, best at 8; 1 KiB blobs, 2,048, at 8-10; 100-B blobs, 4,096, at 10; 8 streamers alone
-// stream a 1.38 GB region in 285 us).
-uint32_t fused_proc_waves(const DevCtx* c, size_t m) {
-  if (c->fused_proc > 0) return (uint32_t)std::min(c->fused_proc, kFusedProcMax);
+// streamers' load), so the processors a CU needs grow with its messages; the rest of its waves
+// stream, and too few streamers starve them (a cliff: 3 of 12 at 1 KiB blobs, 0.367 -> 0.438 ms).
+// Measured per messages per CU (r04am-ao, one box, ms per call): verify form (12 waves) 4 KiB blobs
+// (1,024 per CU) best at 5 (0.377; 8: 0.410), 1 KiB (2,048) at 8 (0.367), 100 B (4,096) at 9
+// (0.532; 8: 0.575); copy form (8 waves), 4 KiB PUTs at 4 (0.663; 3: 0.69, 5: 0.78). Below 512 per
+// CU (not swept) one processor per 128 messages, at least 2.
+uint32_t fused_proc_waves(const DevCtx* c, size_t m, bool copy) {
+  const int waves = copy ? kFusedWavesCopy : kFusedWavesVerify;
+  const int most = std::min(kFusedProcMax, waves - 2);  // at least two streamers
+  if (c->fused_proc > 0) return (uint32_t)std::min(c->fused_proc, most);
   const size_t per_cu = m / (size_t)std::max(1, c->num_cu);
-  return (uint32_t)std::max<size_t>(2, std::min<size_t>(10, (per_cu + 127) / 128));
+  int p;
+  if (per_cu <= 512) p = (int)std::max<size_t>(2, (per_cu + 127) / 128);
+  else if (copy) p = 4;
+  else p = per_cu <= 1536 ? 5 : per_cu <= 3072 ? 8 : 9;
+  return (uint32_t)std::min(p, most);
 }
 
 int enqueue_messages(DevCtx* c, const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off, size_t m,
@@ -1063,7 +1071,7 @@ int enqueue_messages(DevCtx* c, const uint8_t* d_region, uint64_t region_len, co
   f.ngroups = (r.nsb + 3) / 4;
   f.ctl = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(st.batch_ws) + region_rk_bytes(d_region, region_len));
   f.defer = f.ctl + 64;
-  f.nproc = fused_proc_waves(c, m);
+  f.nproc = fused_proc_waves(c, m, false);
   if (hipMemsetAsync(f.ctl, 0, 8, stream) != hipSuccess) return AMBRYCRC_EHIP;
   return hip_err(launch_region_fused(f, c->num_cu, stream));
 }

@@ -159,7 +159,7 @@ int enqueue_batch(DevCtx* c, const uint8_t* base, const uint64_t* off, const uin
 int enqueue_messages(DevCtx* c, const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off, size_t m,
                      uint32_t* d_status, uint64_t* d_msg_end, void* d_ws, size_t ws_bytes, hipStream_t stream);
 // Processor waves per workgroup of the one-pass region kernels for m messages (FusedArgs::nproc).
-uint32_t fused_proc_waves(const DevCtx* c, size_t m);
+uint32_t fused_proc_waves(const DevCtx* c, size_t m, bool copy);
 // Bytes of the job arrays at the start of a message-verify workspace (the rest: batch / run sums).
 size_t msg_jobs_bytes(size_t m);
 // The same in two halves: the parse kernel (jobs and their stored CRCs in st->a), then the CRC

@@ -305,7 +305,7 @@ int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len
     f.ngroups = (f.g.nsb + 3) / 4;
     f.ctl = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(shared) + region_rk_bytes(d_region, region_len));
     f.defer = f.ctl + 64;
-    f.nproc = fused_proc_waves(c, m);
+    f.nproc = fused_proc_waves(c, m, true);
     f.out = d_out;
     f.out_cap = out_cap;
     f.out_off = d_out_off;

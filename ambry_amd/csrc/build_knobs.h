@@ -24,8 +24,14 @@
 #ifndef AMBRY_REGION_BPC  // region pass 2: blocks per CU (0: one thread per message)
 #define AMBRY_REGION_BPC 2
 #endif
-#ifndef AMBRY_FUSED_PROC  // one-pass region verify: processor waves per 16-wave workgroup (0: per call)
+#ifndef AMBRY_FUSED_PROC  // one-pass region verify: processor waves per workgroup (0: per call)
 #define AMBRY_FUSED_PROC 0
+#endif
+#ifndef AMBRY_FUSED_WAVES_VERIFY  // one-pass region kernel, verify form: waves per workgroup (one per CU)
+#define AMBRY_FUSED_WAVES_VERIFY 12
+#endif
+#ifndef AMBRY_FUSED_WAVES_COPY  // the same, the transform's copy form
+#define AMBRY_FUSED_WAVES_COPY 8
 #endif
 
 // ---- batch CRC kernels (crc32_kernels.hip, crc32_kernels.h, ambrycrc_ctx.h)
@@ -79,6 +85,8 @@
   X(AMBRY_PROPS_WIN, 96) X(AMBRY_PARSE_BPC, 2) X(AMBRY_REGION_WPE, 2) X(AMBRY_REGION_BPC, 2)                  \
   X(AMBRY_REGION_BPC_SMALL, 3)                                                                              \
   X(AMBRY_FUSED_PROC, 0)                                                                                      \
+  X(AMBRY_FUSED_WAVES_VERIFY, 12)                                                                               \
+  X(AMBRY_FUSED_WAVES_COPY, 8)                                                                                      \
   X(AMBRY_GRP_PRIO, 0) X(AMBRY_GRP_IL, 4) X(AMBRY_C0_G, 2) X(AMBRY_C0_NB, 8) X(AMBRY_C1_MAX, 1024)           \
   X(AMBRY_RUNS_STORE_NT, 0) X(AMBRY_RUNS_GIL, 1) X(AMBRY_PLAN_PER_BLOCK, 2048) X(AMBRY_DEFAULT_VARIANT, 29) \
   X(AMBRY_REGION_PROBE, 0) X(AMBRY_RUNS_PROBE, 0) X(AMBRY_FUSED_PROBE, 0)

@@ -328,7 +328,7 @@ struct FusedArgs {
   uint64_t ngroups;  // 16 KiB groups over the region: ceil(nsb / 4)
   uint32_t* ctl;
   uint32_t* defer;
-  uint32_t nproc;    // processor waves per workgroup (1..kFusedProcMax); waves 16 - nproc .. 15
+  uint32_t nproc;    // processor waves per workgroup (1..kFusedProcMax); the workgroup's last nproc waves
   // Transform fast path (launch_region_fused with copy): when every message is a clean PUT stored
   // at header V3 with canonical V5 properties and a Blob_Format_V3 record, back to back from
   // msg_off[0], the output is the region from msg_off[0] on with each header's life version and
@@ -351,8 +351,17 @@ constexpr uint64_t kDirectSpan = 65536;
 // Bytes at a message's start that the transform's fast path may rewrite in `out` (the header's life
 // version and CRC; header V3 is 40 B).
 constexpr uint64_t kHeaderPatchMax = 64;
-// Processor waves per 16-wave workgroup (the rest stream): chosen per call from the messages per
-// CU (fused_proc_waves, ambrycrc.cpp); AMBRY_FUSED_PROC > 0 or AMBRYCRC_FUSED_PROC fixes it (A/B).
+// Waves per workgroup of the one-pass kernel (one workgroup per CU, its LDS): fewer waves than 16
+// give each more than 128 VGPRs -- at 16 the processors' parse and record code spilled ~400
+// VGPRs to scratch (r04an/ao A/B, ms per call: the copy form at 8 waves 0.663 vs 0.767 at 16 for
+// 262,144 4 KiB PUTs; verify at 12 waves 0.377 / 0.367 / 0.532 vs 0.422 / 0.484 / 0.81 for 4 KiB
+// / 1 KiB / 100-B blobs).
+constexpr int kFusedWavesVerify = AMBRY_FUSED_WAVES_VERIFY, kFusedWavesCopy = AMBRY_FUSED_WAVES_COPY;
+static_assert(kFusedWavesVerify >= 4 && kFusedWavesVerify <= 16 && kFusedWavesCopy >= 4 && kFusedWavesCopy <= 16,
+              "one-pass workgroups: 4 to 16 waves (16 run-sum buffers in LDS)");
+// Processor waves per workgroup (the rest stream): chosen per call from the messages per CU
+// (fused_proc_waves, ambrycrc.cpp); AMBRY_FUSED_PROC > 0 or AMBRYCRC_FUSED_PROC fixes it (A/B),
+// at most the workgroup's waves less two.
 constexpr int kFusedProcMax = 12;
 hipError_t launch_region_fused(const FusedArgs& f, int num_cu, hipStream_t s);  // f.out set: the copy form
 

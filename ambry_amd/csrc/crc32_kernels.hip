@@ -1696,8 +1696,8 @@ __device__ __forceinline__ uint64_t lower_bound_wave(const FusedArgs& f, uint64_
 __device__ unsigned long long g_fused_t[3 * 2048];
 #endif
 
-template <bool COPY>
-__global__ __launch_bounds__(1024) void region_fused_kernel(FusedArgs f) {
+template <bool COPY, int W>
+__global__ __launch_bounds__(64 * W) void region_fused_kernel(FusedArgs f) {
 #if AMBRY_FUSED_PROBE == 2
   if (threadIdx.x == 0) g_fused_t[3 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1712,8 +1712,8 @@ __global__ __launch_bounds__(1024) void region_fused_kernel(FusedArgs f) {
           (const __attribute__((address_space(1))) void*)(reinterpret_cast<const uint8_t*>(f.g.img) + c * 1024 +
                                                           lane * 16),
           (__attribute__((address_space(3))) void*)(reinterpret_cast<uint8_t*>(g_lds_runs) + c * 1024), 16, 0, 0);
-    {
-      const uint32_t i = threadIdx.x, j = i >> 8, b = i & 255u;
+    for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) {
+      const uint32_t j = i >> 8, b = i & 255u;
       tbl[i] = f.g.img[(((j >> 1) << 16) | (b << 8) | ((j & 1) << 7)) >> 2];
     }
     region::stage_nib(nib, f.g.img);
@@ -1726,7 +1726,7 @@ __global__ __launch_bounds__(1024) void region_fused_kernel(FusedArgs f) {
   const uint32_t v = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t G0 = f.ngroups * blockIdx.x / gridDim.x, G1 = f.ngroups * (blockIdx.x + 1) / gridDim.x;
   const RegionArgs a = f.g;
-  const uint32_t nstream = 16u - f.nproc;
+  const uint32_t nstream = W - f.nproc;
   if (v < nstream) {
     // ---- streaming wave
     const LaneConst k = make_lane_const(lane);
@@ -1962,8 +1962,11 @@ hipError_t launch_region_fused(const FusedArgs& f, int num_cu, hipStream_t s) {
   if (f.a.m == 0) return hipSuccess;
   const bool copy = f.out != nullptr;
   if (f.ngroups) {
-    if (copy) hipLaunchKernelGGL(region_fused_kernel<true>, dim3((uint32_t)num_cu), dim3(1024), 0, s, f);
-    else hipLaunchKernelGGL(region_fused_kernel<false>, dim3((uint32_t)num_cu), dim3(1024), 0, s, f);
+    if (copy)
+      hipLaunchKernelGGL((region_fused_kernel<true, kFusedWavesCopy>), dim3((uint32_t)num_cu), dim3(64 * kFusedWavesCopy), 0, s, f);
+    else
+      hipLaunchKernelGGL((region_fused_kernel<false, kFusedWavesVerify>), dim3((uint32_t)num_cu), dim3(64 * kFusedWavesVerify),
+                         0, s, f);
   } else if (hipMemsetAsync(f.ctl, 0xFF, 4, s) != hipSuccess) {  // empty region: all to the tail
     return hipGetLastError();
   }
