@@ -1014,9 +1014,10 @@ size_t msg_jobs_bytes(size_t m) {
 // A processor wave finishes a 64-message batch in ~20-40 us (a chain of dependent reads under the
 // streamers' load), so the processors a CU needs grow with its messages; the rest of its waves
 // stream, and too few streamers starve them (a cliff: 3 of 12 at 1 KiB blobs, 0.367 -> 0.438 ms).
-// Measured per messages per CU (r04am-ao, one box, ms per call): verify form (12 waves) 4 KiB blobs
-// (1,024 per CU) best at 5 (0.377; 8: 0.410), 1 KiB (2,048) at 8 (0.367), 100 B (4,096) at 9
-// (0.532; 8: 0.575); copy form (8 waves), 4 KiB PUTs at 4 (0.663; 3: 0.69, 5: 0.78). Below 512 per
+// Measured per messages per CU (r04am-ao, r04au; ms per call): verify form (12 waves) 4 KiB blobs
+// (1,024 per CU) best at 5 (0.377; 8: 0.410), 3 KiB (1,280) at 6 (0.408; 5: 0.418), 2 KiB (1,536)
+// at 6 (0.374; 5: 0.397, 8: 0.387), 1 KiB (2,048) at 8 (0.367), 100 B (4,096) at 9 (0.532; 8:
+// 0.575); copy form (8 waves), 4 KiB PUTs at 4 (0.663; 3: 0.69, 5: 0.78). Below 512 per
 // CU (not swept) one processor per 128 messages, at least 2.
 uint32_t fused_proc_waves(const DevCtx* c, size_t m, bool copy) {
   const int waves = copy ? kFusedWavesCopy : kFusedWavesVerify;
@@ -1026,7 +1027,7 @@ uint32_t fused_proc_waves(const DevCtx* c, size_t m, bool copy) {
   int p;
   if (per_cu <= 512) p = (int)std::max<size_t>(2, (per_cu + 127) / 128);
   else if (copy) p = 4;
-  else p = per_cu <= 1536 ? 5 : per_cu <= 3072 ? 8 : 9;
+  else p = per_cu <= 1024 ? 5 : per_cu <= 1536 ? 6 : per_cu <= 3072 ? 8 : 9;
   return (uint32_t)std::min(p, most);
 }
 
