@@ -139,8 +139,10 @@ constexpr uint64_t kRegionMaxPerMessage = 6144;
 // first. Fast / general path, ms per ~1.2 GB batch, interleaved on one box (profiles/
 // r04x_put_xform_fastmax*.jsonl): 9.2 KiB per message 0.631-0.634 / 0.899-0.903, 17.4 KiB
 // 0.616-0.619 / 0.624, 33.8 KiB 0.593-0.597 / 0.595; 5.3 KiB 0.693-0.697 / 1.163; 67 KiB (before
-// the tail work) 2.07 / 1.96. AMBRYCRC_XFORM_FAST_MAX overrides it (A/B; 0 = never).
-constexpr uint64_t kXformFastMaxPerMessage = 24576;
+// the tail work) 2.07 / 1.96. With the copy form's 8-wave workgroups (r04ax,
+// r04aq): 9.2 KiB 0.581 / 0.893, 17.4 KiB 0.563 / 0.629, 33.8 KiB 0.567 / 0.601-0.604, 67 KiB
+// 2.00 / 1.975 -- hence 40 KiB. AMBRYCRC_XFORM_FAST_MAX overrides it (A/B; 0 = never).
+constexpr uint64_t kXformFastMaxPerMessage = 40960;
 inline uint64_t region_nsb(const uint8_t* region, uint64_t len) {
   const uint64_t b = reinterpret_cast<uintptr_t>(region) & ~uint64_t(63);
   return (reinterpret_cast<uintptr_t>(region) + len - b + kSuperBlock - 1) / kSuperBlock;

@@ -265,7 +265,7 @@ int ambrycrc_serialize_puts_dev(const ambrycrc_put_desc* d_desc, size_t m, const
  * it is verified; a batch with a failing message is then rebuilt). d_out must not overlap the
  * region. Enqueued on `stream`; d_ws >= ambrycrc_transform_workspace_bytes(m) or NULL. The
  * store-key comparison with the index entry stays with the caller (it owns the StoreKey type).
- * Fast path (header_version 3, region mode on, at most 24 KiB of region per message
+ * Fast path (header_version 3, region mode on, at most 40 KiB of region per message
  * (AMBRYCRC_XFORM_FAST_MAX at init overrides; 0 = never), workspace room for the region's run sums
  * -- the default workspace has it): one pass verifies the messages while copying the region into d_out
  * and rewrites the headers' life versions; it takes the batch when every message is a clean PUT

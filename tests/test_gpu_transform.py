@@ -454,6 +454,36 @@ def test_transform_fast_path_long_messages(gpu, mf):
         assert exp_st == 0 and oo[i] == o and ol[i] == len(exp) and out_h[o:o + len(exp)] == exp, i
 
 
+def test_transform_fast_path_32k_blobs(gpu, mf):
+    """PUTs of ~32 KiB blobs (~33 KiB of region per message, under the 40 KiB cut-off) on the fast
+    path: every blob is a long record (more than 512 runs) for a processor's wave, and a CU share of
+    the region (~8 messages) ends inside a message each time -- its records past the share are
+    hashed from the bytes (within kDirectSpan)."""
+    import torch
+
+    from ambry_amd.messages import transform_dev
+
+    msgs = []
+    for i in range(2000):
+        blen = (32 << 10) - 500 + 7 * (i % 97)
+        msgs.append(mf.put_message(mf.store_key("b32-%d" % i), mf.blob_properties_bytes(blen), b"u" * (i % 5),
+                                   stream_bytes(900 + i, 0, blen).tobytes(), version=3))
+    region = b"".join(msgs)
+    assert 24576 * len(msgs) < len(region) <= 40960 * len(msgs)
+    offs = np.cumsum([0] + [len(x) for x in msgs[:-1]]).tolist()
+    dev = torch.frombuffer(bytearray(region), dtype=torch.uint8).cuda()
+    out, oo, ol, st = transform_dev(dev, torch.tensor(offs, dtype=torch.int64, device="cuda"), header_version=3)
+    torch.cuda.synchronize()
+    assert st.cpu().numpy().view(np.uint32).tolist() == [0] * len(msgs)
+    assert gpu.last_transform_path(0) == 1
+    oo, ol = oo.cpu().numpy(), ol.cpu().numpy()
+    out_h = out.cpu().numpy().tobytes()
+    for i in list(range(0, len(msgs), 7)) + [len(msgs) - 1]:
+        o = offs[i]
+        exp_st, exp = mf.transform_message(region, o, version=3)
+        assert exp_st == 0 and oo[i] == o and ol[i] == len(exp) and out_h[o:o + len(exp)] == exp, i
+
+
 def test_transform_fast_path_share_boundaries(gpu, mf):
     """Messages placed against the one-pass kernel's CU share boundaries (a region of 48 KiB per
     CU: three 16 KiB groups per share): at each boundary B a message starts d bytes before it, for d
