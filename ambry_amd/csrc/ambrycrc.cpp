@@ -1017,16 +1017,17 @@ size_t msg_jobs_bytes(size_t m) {
 // Measured per messages per CU (r04am-ao, r04au; ms per call): verify form (12 waves) 4 KiB blobs
 // (1,024 per CU) best at 5 (0.377; 8: 0.410), 3 KiB (1,280) at 6 (0.408; 5: 0.418), 2 KiB (1,536)
 // at 6 (0.374; 5: 0.397, 8: 0.387), 1 KiB (2,048) at 8 (0.367), 100 B (4,096) at 9 (0.532; 8:
-// 0.575); copy form (8 waves), 4 KiB PUTs at 4 (0.663; 3: 0.69, 5: 0.78). Below 512 per
-// CU (not swept) one processor per 128 messages, at least 2.
+// 0.575); copy form (8 waves) at 4 from 128 to 1,024 per CU (4 KiB PUTs 0.663; 3: 0.69, 5: 0.78;
+// 16 KiB PUTs 0.549, 2: 0.562; 32 KiB 0.563, 2: 0.570; r04ba). Verify below 512 per CU (not swept):
+// one processor per 128 messages, at least 2.
 uint32_t fused_proc_waves(const DevCtx* c, size_t m, bool copy) {
   const int waves = copy ? kFusedWavesCopy : kFusedWavesVerify;
   const int most = std::min(kFusedProcMax, waves - 2);  // at least two streamers
   if (c->fused_proc > 0) return (uint32_t)std::min(c->fused_proc, most);
   const size_t per_cu = m / (size_t)std::max(1, c->num_cu);
   int p;
-  if (per_cu <= 512) p = (int)std::max<size_t>(2, (per_cu + 127) / 128);
-  else if (copy) p = 4;
+  if (copy) p = 4;
+  else if (per_cu <= 512) p = (int)std::max<size_t>(2, (per_cu + 127) / 128);
   else p = per_cu <= 1024 ? 5 : per_cu <= 1536 ? 6 : per_cu <= 3072 ? 8 : 9;
   return (uint32_t)std::min(p, most);
 }
