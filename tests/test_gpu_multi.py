@@ -180,9 +180,6 @@ def test_distributed_batch_on_rccl_group(gpu, oracle):
     """ambry_amd.multi.distributed_batch on an NCCL (= RCCL) process group of world size 1 with
     device="cuda": the padded all-gather runs on device tensors (RCCL rejects CPU ones), the
     compaction in C, and the CRCs equal the oracle's (the device argument)."""
-    import os
-    import socket
-
     import torch
     import torch.distributed as dist
 
@@ -191,11 +188,9 @@ def test_distributed_batch_on_rccl_group(gpu, oracle):
 
     mem, off, ln = _batch(61, 300, 100000)
     base, d_off, d_len = _dev(torch, mem, off, ln)
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    # an in-process store: world size 1 needs no rendezvous port (a probed free port can be taken
+    # by another process on a shared box before the group binds it)
+    dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=torch.device("cuda", 0))
     try:
         def compute(lo, hi):
             return D.crc32_batch(base, d_off[lo:hi].contiguous(), d_len[lo:hi].contiguous())
