@@ -138,9 +138,9 @@ _SIGNATURES = [
     ("ambrycrc_get_variant", ctypes.c_int, [ctypes.c_int]),
     ("ambrycrc_set_region_mode", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     ("ambrycrc_get_region_mode", ctypes.c_int, [ctypes.c_int]),
-    ("ambrycrc_set_put_assembly", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     ("ambrycrc_last_message_mode", ctypes.c_int, [ctypes.c_int]),
     ("ambrycrc_last_transform_path", ctypes.c_int, [ctypes.c_int]),
+    ("ambrycrc_set_transform_verdict", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     ("ambrycrc_set_grid", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     ("ambrycrc_set_window", ctypes.c_int, [ctypes.c_int, ctypes.c_uint64]),
     ("ambrycrc_timing_enable", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),

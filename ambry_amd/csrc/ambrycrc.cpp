@@ -603,11 +603,13 @@ int ambrycrc_init(int device) {
     if (end != v && *end == '\0' && x >= 0 && x < 1000 && variant_supported((int)x)) c->variant = (int)x;
   }
   if (const char* v = getenv("AMBRYCRC_REGION")) c->region_mode = strcmp(v, "0") == 0 ? 0 : strcmp(v, "1") == 0 ? 1 : 2;
+#ifdef AMBRY_AB_PUT_ASSEMBLE
   if (const char* v = getenv("AMBRYCRC_ASM_MAX")) {  // A/B: whole-message assembly cut-off
     char* end = nullptr;
     const unsigned long x = strtoul(v, &end, 10);
     if (end != v && *end == '\0' && x <= kAsmMaxBytes) c->asm_max = (uint32_t)x;
   }
+#endif
   if (const char* v = getenv("AMBRYCRC_XFORM_FAST_MAX")) {  // A/B: the transform fast path's cut-off
     char* end = nullptr;
     const unsigned long long x = strtoull(v, &end, 10);
@@ -623,12 +625,17 @@ int ambrycrc_init(int device) {
     const unsigned long long x = strtoull(v, &end, 10);
     if (end != v && *end == '\0' && x > 0 && x <= (1ull << 30)) c->region_max = x;
   }
+  if (const char* v = getenv("AMBRYCRC_XFORM_HOST_VERDICT")) c->xform_host_verdict = strcmp(v, "1") == 0;
   std::vector<uint32_t> img = build_table_image();
-  if (hipMalloc(reinterpret_cast<void**>(&c->d_img), img.size() * 4) != hipSuccess) {
+  // the table image, then one 256-B line of device words (d_path)
+  const size_t img_bytes = (img.size() * 4 + 255) & ~size_t(255);
+  if (hipMalloc(reinterpret_cast<void**>(&c->d_img), img_bytes + 256) != hipSuccess) {
     delete c;
     return AMBRYCRC_ENOMEM;
   }
-  if (hipMemcpy(c->d_img, img.data(), img.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+  c->d_path = c->d_img + img_bytes / 4;
+  if (hipMemcpy(c->d_img, img.data(), img.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(c->d_path, 0xFF, 256) != hipSuccess) {
     free_ctx(c);
     return AMBRYCRC_EHIP;
   }
@@ -882,14 +889,6 @@ int ambrycrc_set_region_mode(int device, int enable) {
   return AMBRYCRC_OK;
 }
 
-int ambrycrc_set_put_assembly(int device, int max_bytes) {
-  DevCtx* c = ctx_for(device);
-  if (!c) return AMBRYCRC_ENOINIT;
-  if (max_bytes < 0 || (uint32_t)max_bytes > kAsmMaxBytes) return AMBRYCRC_EINVAL;
-  const int prev = (int)c->asm_max;
-  c->asm_max = (uint32_t)max_bytes;
-  return prev;
-}
 
 int ambrycrc_get_region_mode(int device) {
   DevCtx* c = ctx_for(device);
@@ -903,7 +902,29 @@ int ambrycrc_last_message_mode(int device) {
 
 int ambrycrc_last_transform_path(int device) {
   DevCtx* c = ctx_for(device);
-  return c ? c->last_xform_path.load() : AMBRYCRC_ENOINIT;
+  if (!c) return AMBRYCRC_ENOINIT;
+  const int p = c->last_xform_path.load();
+  if (p != 2) return p;
+  // decided on the device: region_patch_kernel's word, once the device has finished the call
+  uint32_t w = ~0u;
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  if (hipSetDevice(c->device) != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpy(&w, c->d_path, sizeof w, hipMemcpyDeviceToHost) != hipSuccess) {
+    (void)hipSetDevice(prev);
+    return AMBRYCRC_EHIP;
+  }
+  (void)hipSetDevice(prev);
+  return w <= 1 ? (int)w : -1;
+}
+
+int ambrycrc_set_transform_verdict(int device, int host) {
+  DevCtx* c = ctx_for(device);
+  if (!c) return AMBRYCRC_ENOINIT;
+  if (host != 0 && host != 1) return AMBRYCRC_EINVAL;
+  const int prev = c->xform_host_verdict;
+  c->xform_host_verdict = host;
+  return prev;
 }
 
 int ambrycrc_get_variant(int device) {
@@ -1516,12 +1537,19 @@ int ambrycrc_transform_messages_host(const uint8_t* region, uint64_t region_len,
     r.i0 = i;
     uint64_t lo = std::min(msg_off[i], region_len), hi = lo + ext[i];
     size_t n = 0;
+    // A run ends where its span would pass a slab, or where the summed extents of its messages
+    // (each output at most its extent + the growth bound) would pass the slab's output buffer:
+    // messages that share bytes (duplicate offsets) never meet a cap one call over the whole region
+    // would not have.
+    uint64_t outs = 0;
     while (i + n < m && n < kSlabMsgs && ext[i + n] <= kSlabBytes) {
       const uint64_t o = std::min(msg_off[i + n], region_len), e = o + ext[i + n];
       const uint64_t nlo = std::min(lo, o), nhi = std::max(hi, e);
-      if (nhi - nlo > kSlabBytes) break;
+      const uint64_t nouts = outs + ext[i + n] + AMBRYCRC_TRANSFORM_GROWTH_MAX;
+      if (nhi - nlo > kSlabBytes || (n && nouts > kXformOutBytes)) break;
       lo = nlo;
       hi = nhi;
+      outs = nouts;
       ++n;
     }
     const uint64_t span = hi - lo;
@@ -1539,7 +1567,7 @@ int ambrycrc_transform_messages_host(const uint8_t* region, uint64_t region_len,
         if (hipMemcpyAsync(s.d_data, s.h_data, span, hipMemcpyHostToDevice, s.stream) != hipSuccess) rc = AMBRYCRC_EHIP;
       }
     }
-    const uint64_t cap = ambrycrc_transform_out_bound(span, n);
+    const uint64_t cap = std::min<uint64_t>(kXformOutBytes, std::max(outs, ambrycrc_transform_out_bound(span, n)));
     if (!rc && (hipMemcpyAsync(ms.d_off, ms.h_off, n * sizeof(uint64_t), hipMemcpyHostToDevice, s.stream) != hipSuccess ||
                 (life_version &&
                  hipMemcpyAsync(x.d_life, x.h_life, n * sizeof(int16_t), hipMemcpyHostToDevice, s.stream) != hipSuccess)))

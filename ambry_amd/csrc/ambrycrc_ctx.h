@@ -83,19 +83,36 @@ struct DevCtx {
   // mode is on and the region holds at most xform_fast_max bytes per message.
   int region_mode = 2;
   uint64_t xform_fast_max = kXformFastMaxPerMessage;
-  // Serialize copy mode: messages of at most this many bytes are assembled whole
-  // (put_assemble_kernel); ambrycrc_set_put_assembly / AMBRYCRC_ASM_MAX (0 = never, at most
-  // kAsmMaxBytes). Off by default until it beats the job path.
+#ifdef AMBRY_AB_PUT_ASSEMBLE
+  // A/B builds only (tools/probes/put_assemble.hip): serialize copy mode assembles messages of at
+  // most this many bytes whole; AMBRYCRC_ASM_MAX (0 = never, at most kAsmMaxBytes). DESIGN.md §10.4.
   uint32_t asm_max = 0;
+#endif
   // The form the last message verify on this device took (ambrycrc_last_message_mode).
   std::atomic<int> last_msg_mode{-1};
-  // The path the last transform took (ambrycrc_last_transform_path): 1 fast, 0 general.
+  // The path the last transform took (ambrycrc_last_transform_path): 1 fast, 0 general, 2 decided
+  // on the device (region_patch_kernel wrote 1 or 0 to d_path).
   std::atomic<int> last_xform_path{-1};
-  // Pinned words for one-word device-to-host reads (the transform fast path's verdict): call k
-  // takes word k mod kHostWords, so concurrent calls do not share one.
+  uint32_t* d_path = nullptr;  // (inside the d_img allocation)
+  // The transform fast path's verdict read by the host (ambrycrc_set_transform_verdict): off by
+  // default -- the general path is then enqueued behind a device gate, and the call never blocks.
+  int xform_host_verdict = 0;
+  // Pinned words for one-word device-to-host reads (the host verdict): a call holds slot k (busy[k])
+  // from its copy until it has read the word, so no two calls in flight share one; with every slot
+  // held the call takes the device-gated form instead.
   static constexpr uint32_t kHostWords = 256;
   uint32_t* h_words = nullptr;
-  std::atomic<uint32_t> h_word_next{0};
+  std::atomic<bool> h_word_busy[kHostWords] = {};
+  int take_host_word() {
+    for (uint32_t k = 0; k < kHostWords; ++k) {
+      bool f = false;
+      if (!h_word_busy[k].load(std::memory_order_relaxed) &&
+          h_word_busy[k].compare_exchange_strong(f, true, std::memory_order_acquire))
+        return (int)k;
+    }
+    return -1;
+  }
+  void release_host_word(int k) { h_word_busy[k].store(false, std::memory_order_release); }
   // Processor waves of the one-pass kernels (0: per call, fused_proc_waves); AMBRYCRC_FUSED_PROC.
   int fused_proc = AMBRY_FUSED_PROC;
   uint64_t region_max = kRegionMaxPerMessage;  // region bytes per message up to which it applies

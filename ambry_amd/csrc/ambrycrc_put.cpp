@@ -76,6 +76,7 @@ int enqueue_serialize(DevCtx* c, const ::ambrycrc_put_desc* d_desc, size_t m, co
   }
   a.pfix = pfix;
   void* batch_ws = w + put_jobs_bytes(m);
+#ifdef AMBRY_AB_PUT_ASSEMBLE
   if (a.copy_through && d_fields && d_blobs && c->asm_max && !gate) {
     // whole-message assembly for messages of at most asm_max bytes; the job path below runs (on
     // the device) only if a longer one set *big, and skips the assembled ones
@@ -85,6 +86,7 @@ int enqueue_serialize(DevCtx* c, const ::ambrycrc_put_desc* d_desc, size_t m, co
     if (launch_put_assemble(a, c->num_cu, stream) != hipSuccess) return AMBRYCRC_EHIP;
     a.gate = a.big;
   }
+#endif
   if (launch_put_layout(a, stream) != hipSuccess) return AMBRYCRC_EHIP;
   if (layout_only) return AMBRYCRC_OK;
   if (a.copy_through) {
@@ -172,7 +174,7 @@ int ambrycrc_serialize_put_host(const ambrycrc_put_desc* d, const uint8_t* field
 }
 
 size_t ambrycrc_serialize_puts_workspace_bytes(size_t m) {
-  return put_jobs_bytes(m) + ws_need((size_t)kPutSlots * m) + 256;  // + the assembly's `big` word
+  return put_jobs_bytes(m) + ws_need((size_t)kPutSlots * m) + 256;  // + the A/B assembly's `big` word
 }
 
 int ambrycrc_serialize_puts_dev(const ambrycrc_put_desc* d_desc, size_t m, const uint8_t* d_fields,
@@ -312,24 +314,47 @@ int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len
     f.out_len = d_out_len;
     f.life = d_life_version;
     f.xstatus = xstatus;
-    f.xfail = f.ctl + 2;  // ctl[0] unsorted, ctl[1] deferred count, ctl[2] xfail: one memset
-    if (hipMemsetAsync(f.ctl, 0, 12, stream) != hipSuccess) return AMBRYCRC_EHIP;
-    if (launch_region_fused(f, c->num_cu, stream) != hipSuccess) return AMBRYCRC_EHIP;
-    // One synchronization with the stream decides: the batch is done, or the general path runs
-    // (~20 launches, ~95 us of empty dispatches if they were launched behind a device gate instead).
-    // The verdict comes back through a pinned word (a pageable one costs a staged copy).
-    uint32_t* h_xfail = c->h_words + (c->h_word_next.fetch_add(1) % DevCtx::kHostWords);
-    *h_xfail = 1;
-    if (hipMemcpyAsync(h_xfail, f.xfail, sizeof(uint32_t), hipMemcpyDeviceToHost, stream) != hipSuccess ||
-        hipStreamSynchronize(stream) != hipSuccess)
+    // xfail beside `fail`, outside the shared workspace: the general path's kernels reuse `shared`
+    // (ctl included) and read their device gate, *xfail, at every launch
+    f.xfail = fail + 1;
+    f.patch = copy_off;  // (the general path's, unused until then)
+    if (hipMemsetAsync(f.ctl, 0, 8, stream) != hipSuccess || hipMemsetAsync(fail, 0, 8, stream) != hipSuccess)
       return AMBRYCRC_EHIP;
-    if (*h_xfail == 0) {
-      c->last_xform_path.store(1);
-      return AMBRYCRC_OK;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &cap) != hipSuccess) return AMBRYCRC_EHIP;
+    const int slot = c->xform_host_verdict && cap == hipStreamCaptureStatusNone ? c->take_host_word() : -1;
+    f.path_out = slot < 0 ? c->d_path : nullptr;
+    if (launch_region_fused(f, c->num_cu, stream) != hipSuccess) {
+      if (slot >= 0) c->release_host_word(slot);
+      return AMBRYCRC_EHIP;
     }
+    if (slot >= 0) {
+      // Host verdict (ambrycrc_set_transform_verdict): one synchronization with the stream decides
+      // -- the batch is done, or the general path is enqueued -- instead of the ~20 gated launches
+      // of the general path's empty dispatches. Blocks the calling thread.
+      uint32_t* h_xfail = c->h_words + slot;
+      *h_xfail = 1;
+      const bool ok = hipMemcpyAsync(h_xfail, f.xfail, sizeof(uint32_t), hipMemcpyDeviceToHost, stream) == hipSuccess &&
+                      hipStreamSynchronize(stream) == hipSuccess;
+      const uint32_t v = *h_xfail;
+      c->release_host_word(slot);
+      if (!ok) return AMBRYCRC_EHIP;
+      if (v == 0) {
+        c->last_xform_path.store(1);
+        return AMBRYCRC_OK;
+      }
+      c->last_xform_path.store(0);
+    } else {
+      // Device verdict (the default, and always under stream capture): the general path below is
+      // enqueued behind *xfail -- every one of its kernels returns at once when the fast path took
+      // the batch -- so the call only enqueues work, as every *_dev entry does.
+      general = f.xfail;
+      c->last_xform_path.store(2);
+    }
+  } else {
+    c->last_xform_path.store(0);
   }
   if (hipMemsetAsync(fail, 0, sizeof(uint32_t), stream) != hipSuccess) return AMBRYCRC_EHIP;
-  c->last_xform_path.store(0);
   p.gate = general;
   t.gate = general;
   t.gate_when = 1;

@@ -230,15 +230,15 @@ struct PutArgs {
   // is the record CRC; the layout kernel writes the header trailer itself. A slot with no source
   // buffer (fields or blobs null) re-reads its bytes in place (src = dst).
   bool copy_through;
-  // Whole-message assembly (put_assemble_kernel, copy mode with both field buffers): messages of
+  // A/B builds only -- whole-message assembly (tools/probes/put_assemble.hip, copy mode with both field buffers): messages of
   // at most asm_max bytes are written by it, and put_layout_kernel gives them no jobs; a longer one
   // sets *big, which gates the job path (layout, plan + sweep, seal). 0: no assembly.
   uint32_t asm_max = 0;
   uint32_t* big = nullptr;
 };
 
-// Messages of at most this many bytes are assembled whole by put_assemble_kernel (a wave per
-// message through a 7 KiB LDS image per wave: 4 waves and 37.5 KiB of LDS per block, 4 blocks per CU).
+// A/B builds: messages of at most this many bytes are assembled whole by put_assemble_kernel (a wave
+// per message through a 7 KiB LDS image per wave: 4 waves and 37.5 KiB of LDS per block, 4 blocks per CU).
 constexpr uint32_t kAsmMaxBytes = 6144;
 
 // Each copy job costs its bytes plus kCopyJobCost: a wave pays about one memory round trip
@@ -305,7 +305,9 @@ hipError_t launch_props_fix(const TransformArgs& a, hipStream_t s);
 
 hipError_t launch_put_layout(const PutArgs& a, hipStream_t s);
 hipError_t launch_put_seal(const PutArgs& a, hipStream_t s);
-hipError_t launch_put_assemble(const PutArgs& a, int num_cu, hipStream_t s);
+#ifdef AMBRY_AB_PUT_ASSEMBLE
+hipError_t launch_put_assemble(const PutArgs& a, int num_cu, hipStream_t s);  // tools/probes/put_assemble.hip
+#endif
 hipError_t launch_gather_copy(const CopyArgs& a, int grid, hipStream_t s);
 
 hipError_t launch_trailer_parse(const TrailerArgs& a, hipStream_t s);
@@ -335,8 +337,11 @@ struct FusedArgs {
   // at header V3 with canonical V5 properties and a Blob_Format_V3 record, back to back from
   // msg_off[0], the output is the region from msg_off[0] on with each header's life version and
   // CRC rewritten. The streamers copy every byte they stream to out + (position - msg_off[0]);
-  // the processors patch the headers and write out_off / out_len / xstatus (0), or set *xfail when
-  // a message does not qualify -- the transform's general path then runs (gated on *xfail).
+  // the processors (and the tail kernel, for the deferred messages) write out_off / out_len /
+  // xstatus (0) and each header's new life version and CRC into patch[i], or set *xfail when a
+  // message does not qualify -- the transform's general path then runs. region_patch_kernel, the
+  // last launch, writes the patches into `out` when *xfail is clear: every byte of `out` is then
+  // written by one kernel after the one that wrote it before, in stream order.
   uint8_t* out = nullptr;
   uint64_t out_cap = 0;
   uint64_t* out_off = nullptr;  // nullable
@@ -344,15 +349,14 @@ struct FusedArgs {
   const int16_t* life = nullptr;  // nullable: the stored life versions
   uint32_t* xstatus = nullptr;
   uint32_t* xfail = nullptr;
+  uint64_t* patch = nullptr;     // [m] life version | header CRC << 32 (with life only)
+  uint32_t* path_out = nullptr;  // nullable: region_patch_kernel writes 1 (fast path took the batch) or 0
 };
 constexpr uint64_t kGroupBytes = 4 * kSuperBlock;
 // A message that starts in a CU's share and ends at most this far past it is finished by that
 // share's processors, its records past the share hashed straight from the bytes
 // (region::record_crc_direct); one reaching further goes to region_tail_kernel.
 constexpr uint64_t kDirectSpan = 65536;
-// Bytes at a message's start that the transform's fast path may rewrite in `out` (the header's life
-// version and CRC; header V3 is 40 B).
-constexpr uint64_t kHeaderPatchMax = 64;
 // Waves per workgroup of the one-pass kernel (one workgroup per CU, its LDS): fewer waves than 16
 // give each more than 128 VGPRs -- at 16 the processors' parse and record code spilled ~400
 // VGPRs to scratch (r04an/ao A/B, ms per call: the copy form at 8 waves 0.663 vs 0.767 at 16 for

@@ -1877,24 +1877,15 @@ __global__ __launch_bounds__(64 * W) void region_fused_kernel(FusedArgs f) {
       // the lane's message ends at pos + end (base-relative): before the share, or past it (the
       // copy form: more than kDirectSpan past it; its records past the share are hashed from the
       // bytes) -> the tail's. (Measured: the copy form 0.713 -> 0.695 ms per 262,144 4 KiB PUTs;
-      // the verify form 0.385 -> 0.399 ms, so it keeps deferring them.) The copy form also defers
-      // one whose header reaches past the share: transform_fast rewrites the header in `out`, and
-      // bytes past the share are the next CU's streamers' to copy, at their own pace -- the copy
-      // could land after the patch.
-      if (pos < s_lo || pos + end > s_hi + (COPY ? kDirectSpan : 0) ||
-          (COPY && pos + end > s_hi && pos + kHeaderPatchMax > s_hi)) {
+      // the verify form 0.385 -> 0.399 ms, so it keeps deferring them.)
+      if (pos < s_lo || pos + end > s_hi + (COPY ? kDirectSpan : 0)) {
         const uint32_t at = atomicAdd(f.ctl + 1, 1u);
         if (at < f.a.m) f.defer[at] = (uint32_t)i;  // (unsorted offsets may defer more: ctl[0] covers them)
         return false;
       }
       return true;
     }, [&](uint64_t need) { wait_for(need); }, dn, COPY ? s_hi : ~0ull);
-    if constexpr (COPY) {
-      // the header's pieces must be copied before the patch lands on them: a message whose records
-      // all lie past the share (hashed from the bytes, no wait) may not have waited for them yet
-      wait_for(region::wave_max_u64(st != ~0u ? msg_pos(f, i) + kHeaderPatchMax : 0));
-      region::transform_fast(f, tbl, st != ~0u, i, st, mend);
-    }
+    if constexpr (COPY) region::transform_fast(f, tbl, st != ~0u, i, st, mend);  // `out` untouched
   }
 #if AMBRY_FUSED_PROBE == 2
   if (lane == 0) atomicMax(&g_fused_t[3 * blockIdx.x + 2], (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -1950,6 +1941,29 @@ __global__ __launch_bounds__(256) void region_tail_kernel(FusedArgs f) {
   }
 }
 
+// The transform fast path's last step: with *xfail clear (every message qualified, in the fused
+// and the tail kernel), each message's life version (bytes 2-3) and header CRC (bytes 36-39; 32-35
+// are the stored CRC's zero high word) go into `out` -- after both kernels that wrote `out`'s
+// bytes have completed, so no store of theirs can land after these. One lane per message. Also
+// the device-side verdict for ambrycrc_last_transform_path (path_out).
+__global__ __launch_bounds__(256) void region_patch_kernel(FusedArgs f) {
+  const bool fail = __hip_atomic_load(f.xfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  if (f.path_out && blockIdx.x == 0 && threadIdx.x == 0) *f.path_out = fail ? 0u : 1u;
+  if (fail || !f.life) return;
+  const uint64_t off0 = f.a.msg_off[0];
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < f.a.m; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t pt = f.patch[i];
+    uint8_t* o = f.out + (f.a.msg_off[i] - off0);
+    const uint32_t lv = (uint32_t)pt, c = (uint32_t)(pt >> 32);
+    o[2] = (uint8_t)(lv >> 8);
+    o[3] = (uint8_t)lv;
+    o[36] = (uint8_t)(c >> 24);
+    o[37] = (uint8_t)(c >> 16);
+    o[38] = (uint8_t)(c >> 8);
+    o[39] = (uint8_t)c;
+  }
+}
+
 #if AMBRY_FUSED_PROBE == 2
 extern "C" int ambrycrc_debug_fused_times(unsigned long long* out, int n) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fused_t), sizeof(unsigned long long) * 3 * n) != hipSuccess) return -2;
@@ -1977,6 +1991,11 @@ hipError_t launch_region_fused(const FusedArgs& f, int num_cu, hipStream_t s) {
   if (blocks > (uint64_t)num_cu * 4) blocks = (uint64_t)num_cu * 4;
   if (copy) hipLaunchKernelGGL(region_tail_kernel<true>, dim3((uint32_t)blocks), dim3(256), 0, s, f);
   else hipLaunchKernelGGL(region_tail_kernel<false>, dim3((uint32_t)blocks), dim3(256), 0, s, f);
+  if (copy && (f.life || f.path_out)) {
+    uint64_t pb = f.life ? (f.a.m + 255) / 256 : 1;
+    if (pb > (uint64_t)num_cu * 8) pb = (uint64_t)num_cu * 8;
+    hipLaunchKernelGGL(region_patch_kernel, dim3((uint32_t)pb), dim3(256), 0, s, f);
+  }
   return hipGetLastError();
 }
 

@@ -321,8 +321,9 @@ __device__ __forceinline__ void process_message(const MsgArgs& a, const RegionAr
 // PUT at header V3 with canonical V5 properties and a Blob_Format_V3 record, followed directly by
 // message i + 1, transforms to its own bytes with the life version rewritten
 // (ValidatingTransformer.java:86-95: PutMessageFormatInputStream over the deserialized fields gives
-// back the same records, their CRCs unchanged) -- the streamers copied those bytes to
-// out + (offset - msg_off[0]); this writes the header (life version, CRC) and the outputs.
+// back the same records, their CRCs unchanged) -- the streamers copy those bytes to
+// out + (offset - msg_off[0]); this records the header's new life version and CRC in patch[i]
+// (applied by region_patch_kernel once the copy is complete) and writes the outputs.
 // Anything else sets *xfail: the general path then redoes the whole batch.
 __device__ __forceinline__ void transform_fast(const FusedArgs& f, const uint32_t* __restrict__ t, bool have,
                                                uint64_t i, uint32_t st, uint64_t end) {
@@ -356,14 +357,10 @@ __device__ __forceinline__ void transform_fast(const FusedArgs& f, const uint32_
   if (f.life) {  // the index's life version (MessageInfo.getLifeVersion), header CRC recomputed
     const uint32_t lv = (uint16_t)f.life[i];
     hw.w[0] = (hw.w[0] & 0xFFFFu) | (((lv >> 8) | ((lv & 0xFFu) << 8)) << 16);
-    const uint32_t c = header_crc(hw, 32, t);
-    hw.w[8] = 0;
-    hw.w[9] = __builtin_bswap32(c);
+    // region_patch_kernel writes it into `out` after the copy has completed (kernel order, no
+    // store-ordering argument between this wave and the waves copying the header's bytes)
+    f.patch[i] = (uint64_t)lv | ((uint64_t)header_crc(hw, 32, t) << 32);
   }
-  uint8_t* o = f.out + (off - off0);
-  __builtin_memcpy(o, &hw.w[0], 16);
-  __builtin_memcpy(o + 16, &hw.w[4], 16);
-  __builtin_memcpy(o + 32, &hw.w[8], 8);
   if (f.out_off) f.out_off[i] = off - off0;
   f.out_len[i] = end;
   f.xstatus[i] = 0;

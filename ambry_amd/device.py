@@ -167,12 +167,6 @@ def set_region_mode(device: int, mode) -> None:
     check(lib().ambrycrc_set_region_mode(device, m), "ambrycrc_set_region_mode")
 
 
-def set_put_assembly(device: int, max_bytes: int) -> int:
-    """Serialize copy mode: messages of at most max_bytes (<= 6144; 0 = none) assembled whole by
-    put_assemble_kernel (ambrycrc_set_put_assembly). Returns the previous value."""
-    return check(lib().ambrycrc_set_put_assembly(device, int(max_bytes)), "ambrycrc_set_put_assembly")
-
-
 def get_region_mode(device: int = 0) -> int:
     return check(lib().ambrycrc_get_region_mode(device), "ambrycrc_get_region_mode")
 
@@ -187,6 +181,13 @@ def last_transform_path(device: int = 0) -> int:
     """The path the device's last transform took: 1 the one-pass fast path, 0 the general path
     (-1: none yet); ambrycrc_last_transform_path."""
     return lib().ambrycrc_last_transform_path(device)
+
+
+def set_transform_verdict(device: int, host: bool) -> int:
+    """How the transform learns whether its fast path took the batch (ambrycrc_set_transform_verdict):
+    False = on the device, the call stays asynchronous (the default); True = read back by the
+    calling thread (one stream synchronization, no gated dispatches). Returns the previous value."""
+    return check(lib().ambrycrc_set_transform_verdict(device, 1 if host else 0), "ambrycrc_set_transform_verdict")
 
 
 def set_grid(device: int, workgroups: int) -> None:

@@ -24,6 +24,7 @@
  *   void nativeBatchDirect(ByteBuffer[] bufs, int[] pos, int[] len, int[] crcIn, int[] out, int device)
  *   void nativeVerifyMessages(ByteBuffer region, long[] offsets, int[] status, long[] ends, int device)
  *   int  nativeVerifyMessage(ByteBuffer region, long offset, long[] end)
+ *   int  nativeChainMessages(ByteBuffer region, long start, long[] offsets)
  *   int  nativeTransformMessage(ByteBuffer region, long offset, int lifeVersion, int headerVersion,
  *                               ByteBuffer out, long[] outLen)
  *   void nativeTransformMessages(ByteBuffer region, long[] offsets, short[] lifeVersions, int headerVersion,
@@ -264,6 +265,27 @@ JNIEXPORT jint JNICALL JNI_FN(nativeVerifyMessage)(JNIEnv* env, jclass cls, jobj
     (*env)->SetLongArrayRegion(env, end, 0, 1, &je);
   }
   return (jint)st;
+}
+
+/* BlobStoreRecovery's hop from header to header (BlobStoreRecovery.java:43-110) over a log span in
+ * a direct buffer -> ambrycrc_chain_messages_host: up to offsets.length message starts from `start`.
+ * Returns how many. */
+JNIEXPORT jint JNICALL JNI_FN(nativeChainMessages)(JNIEnv* env, jclass cls, jobject region, jlong start,
+                                                   jlongArray offsets) {
+  (void)cls;
+  if (!region || !offsets) return raise(env, AJC_ENULL), 0;
+  if (start < 0) return raise(env, AJC_EBOUNDS), 0;
+  int64_t cap;
+  const uint8_t* base = direct(env, region, &cap);
+  if (!base) return raise(env, AJC_ENOTDIRECT), 0;
+  const jsize max = (*env)->GetArrayLength(env, offsets);
+  if (max == 0 || start >= cap) return 0;
+  uint64_t* offs = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)max);
+  if (!offs) return raise(env, AMBRYCRC_ENOMEM), 0;
+  const size_t n = ambrycrc_chain_messages_host(base, (uint64_t)cap, (uint64_t)start, offs, (size_t)max);
+  if (n) (*env)->SetLongArrayRegion(env, offsets, 0, (jsize)n, (const jlong*)offs);
+  free(offs);
+  return (jint)n;
 }
 
 /* ValidatingTransformer.transform for one message (ambrycrc_transform_message_cpu) into the direct

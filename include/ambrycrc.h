@@ -270,8 +270,14 @@ int ambrycrc_serialize_puts_dev(const ambrycrc_put_desc* d_desc, size_t m, const
  * -- the default workspace has it): one pass verifies the messages while copying the region into d_out
  * and rewrites the headers' life versions; it takes the batch when every message is a clean PUT
  * stored at header V3 with VERSION_5 properties and a Blob_Format_V3 record, back to back from
- * d_msg_off[0]. The call then synchronizes with `stream` once to learn whether it did, and returns
- * (done) or enqueues the general path (not done), which gives the same outputs. */
+ * d_msg_off[0]; otherwise the general path redoes the batch, with the same outputs.
+ * Asynchronous, as every *_dev entry: the fast path's verdict stays on the device and the general
+ * path is enqueued behind it (each of its kernels returns at once when the fast path took the
+ * batch), so the call never blocks and may be captured into a HIP graph (the workspace must then
+ * be the caller's, or the stream's default one grown by an earlier uncaptured call). With
+ * ambrycrc_set_transform_verdict(device, 1) an uncaptured call instead reads the verdict back --
+ * one synchronization of `stream`, blocking the calling thread -- and enqueues the general path
+ * only when it is needed (no empty dispatches); a capturing stream always gets the device form. */
 size_t ambrycrc_transform_workspace_bytes(size_t m);
 
 /* Output size contract of the transform. A transformed message is at most
@@ -508,16 +514,17 @@ int ambrycrc_get_variant(int device);
  * before the first), for profiles that must say which kernels they timed. */
 int ambrycrc_set_region_mode(int device, int enable);
 int ambrycrc_get_region_mode(int device);
-/* Serialize copy mode (ambrycrc_serialize_puts_dev with both field buffers): messages of at most
- * max_bytes (<= 6144; 0 = none) are assembled whole by one kernel -- a wave per message builds it
- * in LDS, hashes its records and stores it as whole 16-B pieces -- instead of the layout + copy-
- * through sweep + seal kernels. Same bytes either way. Returns the previous value. */
-int ambrycrc_set_put_assembly(int device, int max_bytes);
 int ambrycrc_last_message_mode(int device);
 /* The path the device's last ambrycrc_transform_messages_dev call (or _host slab) took: 1 = the one-pass
  * fast path alone (header V3, every message a clean dense V3 PUT with canonical properties), 0 = the
- * general path (after the fast pass gave up, or without it), -1 = none yet. */
+ * general path (after the fast pass gave up, or without it), -1 = none yet. When that call left
+ * the verdict on the device (the default), this waits for the device to go idle and reads it. */
 int ambrycrc_last_transform_path(int device);
+/* How ambrycrc_transform_messages_dev learns whether its fast path took the batch: 0 (the default;
+ * AMBRYCRC_XFORM_HOST_VERDICT=1 at init sets 1) = on the device, the general path enqueued behind a
+ * device gate -- asynchronous; 1 = read back by the calling thread (one stream synchronization per
+ * call, 256 calls in flight at most; more take the device form). Returns the previous value. */
+int ambrycrc_set_transform_verdict(int device, int host);
 /* Grid size of the persistent sweep kernel (workgroups; 0 = one per CU). */
 int ambrycrc_set_grid(int device, int workgroups);
 

@@ -58,6 +58,9 @@ public class NativeValidatingTransformer implements Transformer {
   public TransformationOutput transform(Message message) {
     MessageInfo msgInfo = message.getMessageInfo();
     try {
+      if (NativeCrc32.transformOutBound(msgInfo.getSize(), 1) > Integer.MAX_VALUE) {
+        throw new IOException("message of " + msgInfo.getSize() + " bytes: past a direct buffer's reach");
+      }
       int size = (int) msgInfo.getSize();
       ByteBuffer in = ByteBuffer.allocateDirect(size);
       in.put(Utils.readBytesFromStream(message.getStream(), size));
@@ -94,6 +97,7 @@ public class NativeValidatingTransformer implements Transformer {
     if (at > region.capacity()) {
       throw new IOException("GetResponse region holds " + region.capacity() + " bytes, message infos " + at);
     }
+    // every offset below is < at <= capacity (an int); the output bound is checked before its allocation
     if (device < 0) {
       for (int i : live) {
         ByteBuffer msg = region.duplicate();
@@ -112,7 +116,11 @@ public class NativeValidatingTransformer implements Transformer {
       life[k] = info.getLifeVersion();
       bytes += info.getSize();
     }
-    ByteBuffer out = ByteBuffer.allocateDirect((int) NativeCrc32.transformOutBound(bytes, m));
+    long bound = NativeCrc32.transformOutBound(bytes, m);
+    if (bound > Integer.MAX_VALUE) {
+      throw new IOException("transform output bound " + bound + " B: past a direct buffer's reach; split the batch");
+    }
+    ByteBuffer out = ByteBuffer.allocateDirect((int) bound);
     long[] outOffsets = new long[m];
     long[] outLens = new long[m];
     int[] status = new int[m];

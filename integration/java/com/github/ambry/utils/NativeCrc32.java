@@ -123,6 +123,17 @@ public final class NativeCrc32 implements Checksum {
   }
 
   /**
+   * BlobStoreRecovery's hop from message to message (BlobStoreRecovery.java:43-110) over a log span in a
+   * direct buffer (ambrycrc_chain_messages_host): from `start`, each header is read (version, header CRC,
+   * sizes) and its message length followed; offsets[0 .. returned) get the message starts. The chain stops
+   * at the first header that does not parse, at a message that runs past the buffer, or when `offsets` is
+   * full. CPU only.
+   */
+  public static int chainMessages(ByteBuffer region, long start, long[] offsets) {
+    return nativeChainMessages(region, start, offsets);
+  }
+
+  /**
    * One message on the CPU (ambrycrc_verify_message_cpu): deserializeBlobAll's checks (header, record
    * versions and sizes, every CRC) for the message at `offset` in a direct buffer. Returns the
    * AMBRYCRC_MSG_* bits (0: intact); end[0] (if end is non-null) = the message's end offset, 0 when
@@ -204,6 +215,8 @@ public final class NativeCrc32 implements Checksum {
       int device);
 
   private static native int nativeVerifyMessage(ByteBuffer region, long offset, long[] end);
+
+  private static native int nativeChainMessages(ByteBuffer region, long start, long[] offsets);
 
   private static native int nativeTransformMessage(ByteBuffer region, long offset, int lifeVersion,
       int headerVersion, ByteBuffer out, long[] outLen);

@@ -13,6 +13,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "../../include/ambrycrc.h"
+
 enum Kind { K_CLASS, K_BYTES, K_INTS, K_LONGS, K_SHORTS, K_OBJS, K_BUFFER };
 
 struct _jobject {
@@ -220,6 +222,145 @@ static int msg_cases(const char* path) {
   return 0;
 }
 
+JNIEXPORT jint JNICALL FN(nativeChainMessages)(JNIEnv*, jclass, jobject, jlong, jlongArray);
+
+static uint8_t* slurp(const char* path, size_t* n) {
+  FILE* f = fopen(path, "rb");
+  if (!f) return NULL;
+  fseek(f, 0, SEEK_END);
+  const long len = ftell(f);
+  fseek(f, 0, SEEK_SET);
+  uint8_t* b = (uint8_t*)malloc(len > 0 ? (size_t)len : 1);
+  *n = b ? fread(b, 1, (size_t)len, f) : 0;
+  fclose(f);
+  return b;
+}
+
+/* argv[1] == "sieve", argv[2] = one GetResponse's bytes, argv[3] = its message infos, one line each:
+ * "<size> <flag> <lifeVersion>" (flag 0 live, 1 deleted, 2 expired). The call sequence of
+ * MessageSievingInputStream with ambry-messageformat-batch-sieve.patch: every message in one direct
+ * buffer, NativeValidatingTransformer.transformAll -> NativeCrc32.transformMessages over the live
+ * ones at their response offsets (header V3), then applyOutput per message. Prints per message
+ * sieve_<i>: 0 skipped (deleted / expired), 1 sieved (then sieve_<i>_len and sieve_<i>_crc of its
+ * output bytes), 2 invalid (MessageFormatException: skipped, counted), 3 fatal (the exception that
+ * fails the stream: an update record, a property string the V5 re-encoding cannot hold). */
+static int sieve_cases(const char* rpath, const char* mpath) {
+  size_t rn = 0;
+  uint8_t* region = slurp(rpath, &rn);
+  FILE* f = fopen(mpath, "r");
+  if (!region || !f) return 2;
+  static jlong offs[4096], oo[4096], ol[4096];
+  static int flag[4096];
+  static jshort life[4096];
+  static jint st[4096];
+  int n = 0, m = 0;
+  long long sz;
+  int fl, lv;
+  jlong at = 0, live_bytes = 0;
+  while (n < 4096 && fscanf(f, "%lld %d %d", &sz, &fl, &lv) == 3) {
+    flag[n] = fl;
+    if (fl == 0) {  /* transformAll: live messages at their offsets in the response */
+      offs[m] = at;
+      life[m] = (jshort)lv;
+      live_bytes += sz;
+      ++m;
+    }
+    at += sz;
+    ++n;
+  }
+  fclose(f);
+  if ((size_t)at > rn) return 3;
+  const jlong cap = live_bytes + 26 * (jlong)m; /* NativeCrc32.transformOutBound(bytes, m) */
+  uint8_t* out = (uint8_t*)malloc((size_t)cap + 1);
+  FN(nativeInit)(&g_env, NULL, 0);
+  report("sieve_init", 0);
+  struct _jobject reg = arr(K_BUFFER, region, (jsize)rn), dst = arr(K_BUFFER, out, (jsize)cap);
+  struct _jobject joffs = arr(K_LONGS, offs, m), jlife = arr(K_SHORTS, life, m), joo = arr(K_LONGS, oo, m);
+  struct _jobject jol = arr(K_LONGS, ol, m), jst = arr(K_INTS, st, m);
+  FN(nativeTransformMessages)(&g_env, NULL, &reg, &joffs, &jlife, 3, &dst, &joo, &jol, &jst, 0);
+  report("sieve_transform", 0);
+  int k = 0;
+  char name[64];
+  for (int i = 0; i < n; ++i) {
+    snprintf(name, sizeof name, "sieve_%d", i);
+    if (flag[i] != 0) {
+      report(name, 0);
+      continue;
+    }
+    const uint32_t s = (uint32_t)st[k];
+    const jlong off = offs[k];
+    ++k;
+    if (s == 0) {
+      report(name, 1);
+      snprintf(name, sizeof name, "sieve_%d_len", i);
+      report(name, (jint)ol[k - 1]);
+      snprintf(name, sizeof name, "sieve_%d_crc", i);
+      report(name, (jint)ambrycrc_update(0, out + oo[k - 1], (size_t)ol[k - 1]));
+      continue;
+    }
+    /* NativeValidatingTransformer.exceptionFor's classes, in its order of checks */
+    const int v = (int16_t)((region[off] << 8) | region[off + 1]);
+    int cls = 2;
+    if (v >= 1 && v <= 3 && !(s & AMBRYCRC_MSG_HEADER_CRC) && !(s & AMBRYCRC_MSG_BAD_LAYOUT)) {
+      const uint8_t* u = region + off + (v == 1 ? 14 : v == 2 ? 18 : 20);
+      const int32_t upd = (int32_t)(((uint32_t)u[0] << 24) | ((uint32_t)u[1] << 16) | ((uint32_t)u[2] << 8) | u[3]);
+      const uint32_t recs = AMBRYCRC_MSG_ENCKEY_CRC | AMBRYCRC_MSG_PROPS_CRC | AMBRYCRC_MSG_USERMETA_CRC |
+                            AMBRYCRC_MSG_BLOB_CRC | AMBRYCRC_MSG_BAD_VERSION | AMBRYCRC_MSG_BAD_RECORD;
+      if ((s & AMBRYCRC_MSG_NOT_PUT) || upd != -1) cls = 3;
+      else if (s & recs) cls = 2;
+      else cls = 3; /* NOT_ENCODABLE (BufferOverflowException) or an unknown bit */
+    }
+    report(name, cls);
+  }
+  free(out);
+  free(region);
+  return 0;
+}
+
+/* argv[1] == "recover", argv[2] = a log span: the call sequence of NativeBlobStoreRecovery.recover
+ * (BlobStoreRecovery.recover with ambry-messageformat-batch-recovery.patch): chainMessages from the
+ * span's start in batches of argv[3] offsets, verifyMessages on each batch, the first failing message
+ * (or the first header the chain cannot follow) stopping the scan. Prints recover_count (messages
+ * recovered), recover_stop (the startOffset the result reports) and recover_failed (1: a
+ * LogFileFormatError). */
+static int recover_cases(const char* rpath, int batch) {
+  size_t rn = 0;
+  uint8_t* region = slurp(rpath, &rn);
+  if (!region || batch < 1 || batch > 65536) return 2;
+  FN(nativeInit)(&g_env, NULL, 0);
+  report("recover_init", 0);
+  static jlong offs[65536], ends[65536];
+  static jint st[65536];
+  struct _jobject reg = arr(K_BUFFER, region, (jsize)rn);
+  jlong pos = 0;
+  int count = 0, failed = 0;
+  while (pos < (jlong)rn && !failed) {
+    struct _jobject joffs = arr(K_LONGS, offs, batch);
+    const jint n = FN(nativeChainMessages)(&g_env, NULL, &reg, pos, &joffs);
+    if (g_pending) return 4;
+    if (n == 0) {
+      failed = 1;
+      break;
+    }
+    struct _jobject jo = arr(K_LONGS, offs, n), js = arr(K_INTS, st, n), je = arr(K_LONGS, ends, n);
+    FN(nativeVerifyMessages)(&g_env, NULL, &reg, &jo, &js, &je, 0);
+    if (g_pending) return 5;
+    for (int k = 0; k < n; ++k) {
+      if (st[k] != 0) {
+        failed = 1;
+        break;
+      }
+      ++count;
+      pos = ends[k];
+    }
+  }
+  report("recover_count", count);
+  report("recover_stop", (jint)pos);
+  report("recover_failed", failed);
+  free(region);
+  return 0;
+}
+
 /* With a GPU (argv[1] == "gpu"): the device entries on valid arguments. */
 static int gpu_cases(void) {
   FN(nativeInit)(&g_env, NULL, 0);
@@ -250,6 +391,8 @@ int main(int argc, char** argv) {
   if (argc > 1 && strcmp(argv[1], "gpu") == 0) return gpu_cases();
   if (argc > 2 && strcmp(argv[1], "msg") == 0) return msg_cases(argv[2]);
   if (argc > 2 && strcmp(argv[1], "gpumsg") == 0) return gpumsg_cases(argv[2]);
+  if (argc > 3 && strcmp(argv[1], "sieve") == 0) return sieve_cases(argv[2], argv[3]);
+  if (argc > 3 && strcmp(argv[1], "recover") == 0) return recover_cases(argv[2], atoi(argv[3]));
   static uint8_t digits[] = "123456789";
   struct _jobject b9 = arr(K_BYTES, digits, 9);
   report("array_full", FN(nativeUpdateArray)(&g_env, NULL, 0, &b9, 0, 9));
@@ -323,6 +466,14 @@ int main(int argc, char** argv) {
   report("xform_heap", 0);
   FN(nativeTransformMessages)(&g_env, NULL, &direct_buf, &jxo, NULL, 3, &xdst, NULL, &jxol, &jxst, 0);
   report("xform_no_context", 0);
+
+  /* chain: argument errors (the message hop itself: test_jni_recovery_chain_cpu) */
+  jlong co[2] = {0, 0};
+  struct _jobject jco = arr(K_LONGS, co, 2);
+  report("chain_null", FN(nativeChainMessages)(&g_env, NULL, NULL, 0, &jco));
+  report("chain_heap", FN(nativeChainMessages)(&g_env, NULL, &heap_buf, 0, &jco));
+  report("chain_negative", FN(nativeChainMessages)(&g_env, NULL, &direct_buf, -1, &jco));
+  report("chain_none", FN(nativeChainMessages)(&g_env, NULL, &direct_buf, 0, &jco)); /* "123456789": no header */
 
   FN(nativeInit)(&g_env, NULL, 0); /* no GPU in the build container: the init error is thrown */
   report("init_no_gpu", 0);

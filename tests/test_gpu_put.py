@@ -11,16 +11,6 @@ from test_put_serialize import expected, random_messages
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["assembly", "jobs"])
-def put_form(request, gpu):
-    """Every test in both serialize copy-mode forms: whole-message assembly for messages of at most
-    6 KiB (put_assemble_kernel; longer ones take the jobs) and the job path alone (layout,
-    copy-through sweep, seal)."""
-    prev = gpu.set_put_assembly(0, 6144 if request.param == "assembly" else 0)
-    yield request.param
-    gpu.set_put_assembly(0, prev)
-
-
 @pytest.fixture(scope="module")
 def mf():
     import importlib.util
@@ -155,10 +145,11 @@ def test_serialize_large_blobs_copy_through(gpu, mf):
     _run(gpu, mf, msgs, 1, 7, 5)
 
 
-def test_serialize_assembly_cutoff(gpu, mf, put_form):
-    """Messages of 6,100 to 6,200 bytes, byte by byte across the assembly cut-off (6,144 B: at or under
-    it the whole-message kernel writes it, over it the job path), under header versions 1-3, with and
-    without an encryption key, at unaligned output offsets: every byte as the oracle lays it out."""
+def test_serialize_6k_messages(gpu, mf):
+    """Messages of 6,100 to 6,200 bytes, byte by byte (round 4's whole-message assembly cut-off, 6,144
+    B; that kernel is now an A/B probe, tools/probes/put_assemble.hip), under header versions 1-3,
+    with and without an encryption key, at unaligned output offsets: every byte as the oracle lays
+    it out."""
     from ambry_amd.messages import PutMessage, layout
     from datagen import stream_bytes
 

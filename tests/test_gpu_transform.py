@@ -5,6 +5,7 @@ every CRC recomputed. Byte-exact against oracle/message_format.py's transform_me
 restates ValidatingTransformer.java:46-104; outputs packed in message order; every output
 verifies clean."""
 import struct
+import zlib
 
 import numpy as np
 import pytest
@@ -344,6 +345,35 @@ def dense_v3_region(mf, n, seed, lead=0, trail=0):
     return region, offs
 
 
+def fast_expected(region, offs, end, life=None):
+    """What the fast path must produce for clean V3 PUTs back to back over region[offs[0]:end]: those
+    bytes with each header's life version (bytes 2-3, big-endian) set from `life` and its CRC (the
+    8-B big-endian trailer at 32, over bytes 0-31) recomputed (ValidatingTransformer.java:86-95 on a
+    V3 PUT rewrites nothing else). Returns (bytes, out_off, out_len) for every message."""
+    out = bytearray(region[offs[0]:end])
+    oo = np.asarray(offs, dtype=np.int64) - offs[0]
+    ol = np.diff(np.append(oo, end - offs[0]))
+    if life is not None:
+        for i, o in enumerate(oo.tolist()):
+            out[o + 2:o + 4] = struct.pack(">h", int(life[i]))
+            out[o + 32:o + 40] = struct.pack(">Q", zlib.crc32(bytes(out[o:o + 32])))
+    return bytes(out), oo, ol
+
+
+def assert_fast_output(out_h, oo, ol, region, offs, end, life=None):
+    """Every byte and every (out_off, out_len) of a fast-path result against fast_expected."""
+    exp, eoo, eol = fast_expected(region, offs, end, life)
+    assert np.array_equal(oo, eoo) and np.array_equal(ol, eol)
+    assert len(out_h) >= len(exp)
+    if out_h[:len(exp)] != exp:
+        a = np.frombuffer(out_h[:len(exp)], dtype=np.uint8)
+        b = np.frombuffer(exp, dtype=np.uint8)
+        bad = np.nonzero(a != b)[0]
+        k = int(np.searchsorted(eoo, bad[0], side="right") - 1)
+        raise AssertionError("%d bytes differ; first at output byte %d (message %d, byte %d): %#x vs %#x"
+                             % (len(bad), bad[0], k, bad[0] - eoo[k], a[bad[0]], b[bad[0]]))
+
+
 @pytest.mark.parametrize("n,lead,use_life", [(2000, 0, True), (1500, 13, False), (30000, 0, True)])
 def test_transform_fast_path_dense_v3(gpu, mf, n, lead, use_life):
     """The one-pass fast path (region_fused_kernel's copy form): a dense clean V3 region -- at the
@@ -364,13 +394,14 @@ def test_transform_fast_path_dense_v3(gpu, mf, n, lead, use_life):
     out_h = out.cpu().numpy().tobytes()
     assert st.tolist() == [0] * n
     assert gpu.last_transform_path(0) == 1  # the fast path took the batch alone
-    for i in range(0, n, 1 if n <= 2000 else 7):
+    # every byte, then the oracle on a sample (which pins fast_expected itself)
+    assert_fast_output(out_h, oo, ol, region, offs, len(region) - 29, life if use_life else None)
+    for i in range(0, n, 1 if n <= 2000 else 29):
         o = offs[i]
         exp_st, exp = mf.transform_message(region, o, life=int(life[i]) if use_life else None, version=3)
         assert exp_st == 0
         assert oo[i] == o - offs[0] and ol[i] == len(exp), i
         assert out_h[oo[i]:oo[i] + len(exp)] == exp, i
-    assert oo[-1] + ol[-1] == len(region) - lead - 29
 
 
 @pytest.mark.parametrize("spoil", ["corrupt", "v1_props", "gap", "update", "order"])
@@ -448,7 +479,8 @@ def test_transform_fast_path_long_messages(gpu, mf):
     assert gpu.last_transform_path(0) == 1
     oo, ol = oo.cpu().numpy(), ol.cpu().numpy()
     out_h = out.cpu().numpy().tobytes()
-    for i in list(range(0, len(msgs), 13)) + [1500, 6100] + [i for i in range(len(msgs)) if i % 250 == 7]:
+    assert_fast_output(out_h, oo, ol, region, offs, len(region))
+    for i in list(range(0, len(msgs), 97)) + [1500, 6100] + [i for i in range(len(msgs)) if i % 1000 == 7]:
         o = offs[i]
         exp_st, exp = mf.transform_message(region, o, version=3)
         assert exp_st == 0 and oo[i] == o and ol[i] == len(exp) and out_h[o:o + len(exp)] == exp, i
@@ -478,7 +510,8 @@ def test_transform_fast_path_32k_blobs(gpu, mf):
     assert gpu.last_transform_path(0) == 1
     oo, ol = oo.cpu().numpy(), ol.cpu().numpy()
     out_h = out.cpu().numpy().tobytes()
-    for i in list(range(0, len(msgs), 7)) + [len(msgs) - 1]:
+    assert_fast_output(out_h, oo, ol, region, offs, len(region))
+    for i in list(range(0, len(msgs), 97)) + [len(msgs) - 1]:
         o = offs[i]
         exp_st, exp = mf.transform_message(region, o, version=3)
         assert exp_st == 0 and oo[i] == o and ol[i] == len(exp) and out_h[o:o + len(exp)] == exp, i
@@ -487,10 +520,10 @@ def test_transform_fast_path_32k_blobs(gpu, mf):
 def test_transform_fast_path_share_boundaries(gpu, mf):
     """Messages placed against the one-pass kernel's CU share boundaries (a region of 48 KiB per
     CU: three 16 KiB groups per share): at each boundary B a message starts d bytes before it, for d
-    from 1 to 3000 -- headers that cross into the next CU's share (d < 64: deferred to the tail
-    kernel), and straddlers whose records lie past the share (finished by their own processor from
-    the bytes, the header patched only once its copy landed). Every message byte-exact against the
-    oracle, life versions rewritten, the fast path alone."""
+    from 1 to 3000 -- headers that cross into the next CU's share, and straddlers whose records
+    lie past the share, finished by their own processor from the bytes; every header is patched by
+    region_patch_kernel after the copy. Every output byte against fast_expected and every message
+    against the oracle, life versions rewritten, the fast path alone."""
     import torch
 
     from ambry_amd.messages import transform_dev
@@ -533,6 +566,133 @@ def test_transform_fast_path_share_boundaries(gpu, mf):
     assert gpu.last_transform_path(0) == 1
     oo, ol = oo.cpu().numpy(), ol.cpu().numpy()
     out_h = out.cpu().numpy().tobytes()
+    assert_fast_output(out_h, oo, ol, region, offs, len(region), life)
     for k, o in enumerate(offs):
         exp_st, exp = mf.transform_message(region, o, life=int(life[k]), version=3)
         assert exp_st == 0 and oo[k] == o and out_h[o:o + len(exp)] == exp, k
+
+
+def test_transform_graph_capture_and_replay(gpu, mf):
+    """ambrycrc_transform_messages_dev only enqueues work (the fast path's verdict stays on the
+    device, the general path behind its gate), so it can be captured into a HIP graph. Captured once
+    over a clean V3 region (the fast path) and replayed: with new life versions (new header bytes),
+    then after one message is corrupted in place (the general path, behind its device gate). Every
+    replay gives every byte, offset and status the oracle gives."""
+    import torch
+
+    from ambry_amd.messages import transform_dev
+
+    n = 600
+    region, offs = dense_v3_region(mf, n, seed=41)
+    life = np.random.default_rng(6).integers(0, 9, size=n).astype(np.int16)
+    dev = torch.frombuffer(bytearray(region), dtype=torch.uint8).cuda()
+    off_t = torch.tensor(offs, dtype=torch.int64, device="cuda")
+    life_t = torch.from_numpy(life).cuda()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        transform_dev(dev, off_t, life_version=life_t)  # sizes the stream's default workspace
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            out, oo, ol, st = transform_dev(dev, off_t, life_version=life_t)
+    torch.cuda.synchronize()
+
+    def replay():
+        g.replay()
+        torch.cuda.synchronize()
+        return (out.cpu().numpy().tobytes(), oo.cpu().numpy(), ol.cpu().numpy(), st.cpu().numpy().view(np.uint32))
+
+    out_h, oo_h, ol_h, st_h = replay()
+    assert st_h.tolist() == [0] * n and gpu.last_transform_path(0) == 1
+    assert_fast_output(out_h, oo_h, ol_h, region, offs, len(region), life)
+    life2 = (life + 3).astype(np.int16)
+    life_t.copy_(torch.from_numpy(life2).cuda())
+    out_h, oo_h, ol_h, st_h = replay()
+    assert st_h.tolist() == [0] * n and gpu.last_transform_path(0) == 1
+    assert_fast_output(out_h, oo_h, ol_h, region, offs, len(region), life2)
+    bad = bytearray(region)
+    bad[offs[300] + 70] ^= 0x10
+    dev.copy_(torch.frombuffer(bytes(bad), dtype=torch.uint8).cuda())
+    out_h, oo_h, ol_h, st_h = replay()
+    assert gpu.last_transform_path(0) == 0
+    pos = 0
+    for i, o in enumerate(offs):
+        exp_st, exp = mf.transform_message(bytes(bad), o, life=int(life2[i]), version=3)
+        assert int(st_h[i]) == exp_st, i
+        if exp is None:
+            assert ol_h[i] == 0 and oo_h[i] == -1
+            continue
+        assert oo_h[i] == pos and out_h[pos:pos + len(exp)] == exp, i
+        pos += len(exp)
+    assert st_h[300] != 0 and pos > 0
+
+
+@pytest.mark.parametrize("clean", [True, False])
+def test_transform_host_verdict(gpu, mf, clean):
+    """ambrycrc_set_transform_verdict(device, 1): the call reads the fast path's verdict back (one
+    stream synchronization) and enqueues the general path only when it must. Same outputs either
+    way: a clean dense V3 batch (the fast path alone) and one with a corrupt message (the general
+    path), against the oracle."""
+    import torch
+
+    from ambry_amd.messages import transform_dev
+
+    region, offs = dense_v3_region(mf, 700, seed=43)
+    if not clean:
+        region = bytearray(region)
+        region[offs[350] + 60] ^= 0x01
+        region = bytes(region)
+    life = np.random.default_rng(8).integers(0, 9, size=len(offs)).astype(np.int16)
+    prev = gpu.set_transform_verdict(0, True)
+    try:
+        dev = torch.frombuffer(bytearray(region), dtype=torch.uint8).cuda()
+        out, oo, ol, st = transform_dev(dev, torch.tensor(offs, dtype=torch.int64, device="cuda"),
+                                        life_version=torch.from_numpy(life).cuda())
+        torch.cuda.synchronize()
+        assert gpu.last_transform_path(0) == (1 if clean else 0)
+    finally:
+        gpu.set_transform_verdict(0, bool(prev))
+    out_h, oo, ol, st = out.cpu().numpy().tobytes(), oo.cpu().numpy(), ol.cpu().numpy(), st.cpu().numpy().view(np.uint32)
+    if clean:
+        assert st.tolist() == [0] * len(offs)
+        assert_fast_output(out_h, oo, ol, region, offs, len(region), life)
+        return
+    pos = 0
+    for i, o in enumerate(offs):
+        exp_st, exp = mf.transform_message(region, o, life=int(life[i]), version=3)
+        assert int(st[i]) == exp_st, i
+        if exp is None:
+            continue
+        assert oo[i] == pos and out_h[pos:pos + len(exp)] == exp, i
+        pos += len(exp)
+
+
+def test_transform_host_shared_bytes_matches_dev(gpu, mf):
+    """Messages that share region bytes (every offset listed twice) through the host entry's staging
+    slabs: their outputs sum past one slab's output buffer while their span fits one slab, so a run
+    ends by output size -- the result equals one _dev call over the whole region, with the same cap
+    (the slab's own cap could report NO_ROOM the whole-region call would not)."""
+    import torch
+
+    from ambry_amd.messages import transform_dev, transform_host
+
+    msgs = [mf.put_message(mf.store_key("dup-%d" % i), mf.blob_properties_bytes(9 << 20), b"u" * i,
+                           stream_bytes(70 + i, 0, 9 << 20).tobytes(), version=3) for i in range(5)]
+    region = b"".join(msgs)
+    base = np.cumsum([0] + [len(x) for x in msgs[:-1]]).tolist()
+    offs = [o for o in base for _ in range(2)]
+    cap = 2 * len(region) + 26 * len(offs)
+    out_h, oo_h, ol_h, st_h = transform_host(region, offs, out_cap=cap)
+    dev = torch.frombuffer(bytearray(region), dtype=torch.uint8).cuda()
+    out_d, oo_d, ol_d, st_d = transform_dev(dev, torch.tensor(offs, dtype=torch.int64, device="cuda"),
+                                            out=torch.empty(cap, dtype=torch.uint8, device="cuda"))
+    torch.cuda.synchronize()
+    assert st_h.tolist() == [0] * len(offs) == st_d.cpu().numpy().view(np.uint32).tolist()
+    assert np.array_equal(ol_h.astype(np.int64), ol_d.cpu().numpy())
+    assert np.array_equal(oo_h.astype(np.int64), oo_d.cpu().numpy())
+    total = int(oo_h[-1] + ol_h[-1])
+    assert out_h[:total] == out_d.cpu().numpy().tobytes()[:total]
+    for i in (0, 1, 9):
+        exp_st, exp = mf.transform_message(region, offs[i], version=3)
+        assert exp_st == 0 and out_h[oo_h[i]:oo_h[i] + ol_h[i]] == exp

@@ -154,6 +154,7 @@ def test_jni_shim_against_fake_jvm(core, tmp_path):
         "verify_null": (0, NPE), "xform_short_lens": (0, IAE), "xform_short_life": (0, IAE),
         "xform_null_out": (0, NPE), "xform_heap": (0, IAE),
         "xform_no_context": (0, "java/lang/IllegalStateException"),
+        "chain_null": (0, NPE), "chain_heap": (0, IAE), "chain_negative": (0, IOOBE), "chain_none": (0, "-"),
     }
     for name, want in expect.items():
         assert got[name] == want, name
@@ -216,3 +217,125 @@ def test_jni_shim_batched_transform(core, tmp_path):
     assert got["gpumsg_xform_st"] == (0, "-") and got["gpumsg_xform_off1"] == (len(msg), "-")
     assert got["gpumsg_xform_len"] == (2 * len(msg), "-") and got["gpumsg_xform_same"] == (1, "-")
     assert got["gpumsg_xform_room0"] == (0, "-") and got["gpumsg_xform_room1"] == (1 << 12, "-")
+
+
+def _sieve_response(mf):
+    """One GetResponse as ReplicaThread hands it to MessageSievingInputStream: clean PUTs (header V1/V2/V3,
+    some with an encryption key), one with a corrupt blob byte, one update record, and messages the
+    index marks deleted or expired (read and skipped). Returns (bytes, [(size, flag, life)])."""
+    import numpy as np
+
+    from datagen import stream_bytes
+
+    rng = np.random.default_rng(55)
+    msgs, infos = [], []
+    for i in range(40):
+        blen = int(rng.choice([0, 5, 300, 4096, 9000]))
+        v = 1 + i % 3
+        enc = stream_bytes(i, 7, 32).tobytes() if v >= 2 and i % 4 == 1 else None
+        if i == 17:
+            m = mf.update_message(mf.store_key("upd"), version=3)
+        else:
+            m = mf.put_message(mf.store_key("sv-%d" % i), mf.blob_properties_bytes(blen), b"m" * (i % 5),
+                               stream_bytes(300 + i, 0, blen).tobytes(), version=v, enc_key=enc, life=i % 3)
+        if i == 23:
+            m = bytearray(m)
+            m[-12] ^= 0x40  # inside the blob content / record tail
+            m = bytes(m)
+        msgs.append(m)
+        infos.append((len(m), 1 if i % 11 == 5 else 2 if i % 13 == 7 else 0, int(rng.integers(0, 5))))
+    return b"".join(msgs), infos
+
+
+@pytest.mark.gpu
+def test_jni_sieve_call_sequence(core, tmp_path):
+    """The replication sieve with ambry-messageformat-batch-sieve.patch, as its Java code calls the shim,
+    run in the fake JVM: one direct buffer holding the whole response, NativeCrc32.transformMessages
+    over the live messages at their response offsets (deleted / expired ones skipped, leaving gaps),
+    then each result classified as applyOutput does. Every sieved message's bytes are the oracle's
+    ValidatingTransformer output (length and CRC), the corrupt one is skipped as invalid, and the
+    update record is the exception that fails the stream -- the reference's outcomes, message by
+    message."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("message_format", os.path.join(ROOT, "oracle", "message_format.py"))
+    mf = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mf)
+    region, infos = _sieve_response(mf)
+    (tmp_path / "resp.bin").write_bytes(region)
+    (tmp_path / "infos.txt").write_text("".join("%d %d %d\n" % x for x in infos))
+    got = _run_harness(tmp_path, "sieve", str(tmp_path / "resp.bin"), str(tmp_path / "infos.txt"))
+    assert got["sieve_init"] == (0, "-") and got["sieve_transform"] == (0, "-")
+    at, seen = 0, set()
+    for i, (size, flag, life) in enumerate(infos):
+        cls = got["sieve_%d" % i]
+        if flag:
+            assert cls == (0, "-"), i
+        else:
+            st, exp = mf.transform_message(region, at, life=life, version=3)
+            if st == 0:
+                assert cls == (1, "-"), i
+                assert got["sieve_%d_len" % i] == (len(exp), "-"), i
+                assert got["sieve_%d_crc" % i] == (zlib.crc32(exp), "-"), i
+            else:
+                want = 3 if i == 17 else 2  # the update record fails the stream; corruption skips one message
+                assert cls == (want, "-"), (i, st)
+            seen.add(cls[0])
+        at += size
+    assert seen == {1, 2, 3}
+
+
+def _log_span(mf, corrupt_at=None, truncate=False):
+    from datagen import stream_bytes
+
+    msgs = []
+    for i in range(30):
+        if i % 6 == 4:
+            m = mf.update_message(mf.store_key("lg-%d" % i), version=1 + i % 3, life=i % 2)
+        else:
+            blen = [0, 1, 700, 5000, 70000][i % 5]
+            m = mf.put_message(mf.store_key("lg-%d" % i), mf.blob_properties_bytes(blen), b"u" * (i % 7),
+                               stream_bytes(800 + i, 0, blen).tobytes(), version=1 + i % 3)
+        msgs.append(m)
+    if corrupt_at is not None:
+        m = bytearray(msgs[corrupt_at])
+        m[len(m) // 2] ^= 0x02
+        msgs[corrupt_at] = bytes(m)
+    span = b"".join(msgs)
+    if truncate:
+        span = span[:-100]
+    return span, [len(m) for m in msgs]
+
+
+def _oracle_recover(mf, span):
+    """BlobStoreRecovery.recover's outcome (BlobStoreRecovery.java:43-110) by the oracle: messages from the
+    span's start while each verifies, stopping at the first that does not (LogFileFormatError)."""
+    pos, count = 0, 0
+    while pos < len(span):
+        st, end = mf.verify_message(span, pos)
+        if st or not end:
+            return count, pos, 1
+        count, pos = count + 1, end
+    return count, pos, 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["clean", "corrupt", "truncated"])
+def test_jni_recovery_call_sequence(core, tmp_path, case):
+    """Store recovery with ambry-messageformat-batch-recovery.patch, as NativeBlobStoreRecovery calls the
+    shim, in the fake JVM: nativeChainMessages in batches of 7 offsets, nativeVerifyMessages per batch on
+    the GPU, the first failure stopping the scan. Recovered count, reported startOffset and the
+    LogFileFormatError equal the oracle's reading of the reference loop -- a clean span to its end, a
+    corrupt blob byte in message 13, and a span whose last message is cut short."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("message_format", os.path.join(ROOT, "oracle", "message_format.py"))
+    mf = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mf)
+    span, _ = _log_span(mf, corrupt_at=13 if case == "corrupt" else None, truncate=case == "truncated")
+    (tmp_path / "span.bin").write_bytes(span)
+    got = _run_harness(tmp_path, "recover", str(tmp_path / "span.bin"), "7")
+    count, stop, failed = _oracle_recover(mf, span)
+    assert got["recover_init"] == (0, "-")
+    assert (got["recover_count"][0], got["recover_stop"][0], got["recover_failed"][0]) == (count, stop, failed)
+    assert failed == (case != "clean") and count == {"clean": 30, "corrupt": 13, "truncated": 29}[case]

@@ -120,7 +120,7 @@ def run(m, blob_bytes, reps, in_place, um_len=1000):
             "parity": "3 sampled messages byte-exact vs ambrycrc_serialize_put_host; all verify clean on the GPU"}
 
 
-def run_transform(m, blob_bytes, reps):
+def run_transform(m, blob_bytes, reps, verdict="device"):
     """ValidatingTransformer (ambrycrc_transform_messages_dev) over a region of m stored V3 PUTs (made by
     the serializer), re-serialized at V3. A dense clean V3 region takes the one-pass fast path: the
     region kernel reads each message once, verifying it, and writes it once into the output; the
@@ -131,6 +131,7 @@ def run_transform(m, blob_bytes, reps):
     from ambry_amd import device as D
     from ambry_amd.messages import PUT_DESC_DTYPE, PutMessage, layout, out_bound, serialize_dev, transform_dev
 
+    prev = D.set_transform_verdict(0, verdict == "host")
     key_len, props_len, um_len = 24, 94, 1000
     L, fo = layout(PutMessage(key=bytes(key_len), props=bytes(props_len), usermeta=bytes(um_len),
                               blob=bytes(blob_bytes)))
@@ -166,11 +167,14 @@ def run_transform(m, blob_bytes, reps):
     times.sort()
     ms = times[len(times) // 2]
     nbytes = m * L
-    return {"case": f"transform {m} x PUT({blob_bytes} B blob) V3 -> V3", "messages": m, "message_bytes": nbytes,
+    path = D.last_transform_path(0)
+    D.set_transform_verdict(0, bool(prev))
+    return {"case": f"transform {m} x PUT({blob_bytes} B blob) V3 -> V3", "verdict": verdict,
+            "messages": m, "message_bytes": nbytes,
             "ms_median": round(ms, 4), "GiBps_messages": round(nbytes / (ms / 1e3) / 2**30, 1),
             "messages_per_s": round(m / (ms / 1e3)), "GBps_hbm_min": round(2 * nbytes / (ms / 1e3) / 1e9, 1),
             "parity": "every message verifies and the V3 -> V3 output equals the input region byte for byte",
-            "path_taken": {1: "one-pass fast path", 0: "general path"}.get(D.last_transform_path(0))}
+            "path_taken": {1: "one-pass fast path", 0: "general path"}.get(path)}
 
 
 def main():
@@ -180,6 +184,8 @@ def main():
     ap.add_argument("--um-len", type=int, default=1000, help="user metadata bytes per PUT (1005: blob stores aligned)")
     ap.add_argument("--copy-only", action="store_true", help="skip the in-place mode")
     ap.add_argument("--transform", default="64k,4k,4m", help="ValidatingTransformer cases ('' for none)")
+    ap.add_argument("--verdict", default="device,host",
+                    help="how the transform learns its fast path's verdict: device (async, the default), host")
     args = ap.parse_args()
     import torch
 
@@ -200,8 +206,9 @@ def main():
             torch.cuda.empty_cache()
     for c in [x for x in args.transform.split(",") if x]:
         m, s = cases[c]
-        print(json.dumps(run_transform(m, s, args.reps)), flush=True)
-        torch.cuda.empty_cache()
+        for v in [x for x in args.verdict.split(",") if x]:
+            print(json.dumps(run_transform(m, s, args.reps, v)), flush=True)
+            torch.cuda.empty_cache()
 
 
 if __name__ == "__main__":
