@@ -10,6 +10,7 @@
 #include <sched.h>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <condition_variable>
 #include <functional>
@@ -398,6 +399,45 @@ bool same_or_disjoint(const uint32_t* a, const uint32_t* b, size_t n) {
   return x + 4 * n <= y || y + 4 * n <= x;
 }
 
+int host_cpu_threads() {
+  for (const char* name : {"AMBRYCRC_CPU_THREADS", "OMP_NUM_THREADS"})
+    if (const char* v = getenv(name)) {
+      const int t = atoi(v);
+      if (t > 0) return std::min(t, 256);
+    }
+  cpu_set_t set;
+  return sched_getaffinity(0, sizeof(set), &set) == 0 ? std::max(1, CPU_COUNT(&set)) : 1;
+}
+
+double host_cpu_gibps() {
+  static const double per_thread = [] {
+    std::vector<uint8_t> buf(4u << 20);
+    for (size_t i = 0; i < buf.size(); ++i) buf[i] = (uint8_t)(i * 131u + 7u);
+    double best = 1e30;
+    volatile uint32_t sink = 0;
+    for (int r = 0; r < 3; ++r) {
+      const auto t0 = std::chrono::steady_clock::now();
+      sink = sink ^ ambrycrc_update(0, buf.data(), buf.size());
+      best = std::min(best, std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+    }
+    return (double)buf.size() / best / (double)(1ull << 30);
+  }();
+  return per_thread * host_cpu_threads() * 0.85;
+}
+
+bool host_take_cpu(DevCtx* c, int device, int pinned) {
+  if (device < 0) return true;
+  if (!c || c->host_policy == 1) return false;
+  if (c->host_policy == 2) return true;
+  return !pinned && host_cpu_gibps() > c->gpu_host_gibps.load();
+}
+
+void host_note_gpu(DevCtx* c, uint64_t bytes, double seconds) {
+  if (!c || bytes < (64ull << 20) || seconds <= 0) return;
+  const double r = (double)bytes / seconds / (double)(1ull << 30);
+  c->gpu_host_gibps.store(0.5 * c->gpu_host_gibps.load() + 0.5 * r);
+}
+
 int setup_slabs(DevCtx* c) {
   if (c->slabs_ready) return AMBRYCRC_OK;
   // member by member, skipping what an earlier (failed) attempt already allocated
@@ -696,12 +736,9 @@ int ambrycrc_verify_dev(const uint8_t* d_base, const uint64_t* d_off, const uint
   return hip_err(launch_verify(d_out, d_expected, d_mismatch, d_mismatch_count, (uint32_t)n, stream));
 }
 
-int ambrycrc_batch_host(const void* const* ptrs, const uint64_t* lens, const uint32_t* crc_in, uint32_t* out, size_t n,
-                        int device, int pinned) {
-  if (n == 0) return AMBRYCRC_OK;
-  if (!ptrs || !lens || !out) return AMBRYCRC_EINVAL;
-  DevCtx* c = ctx_for(device);
-  if (!c) return AMBRYCRC_ENOINIT;
+// ambrycrc_batch_host's GPU leg (the dispatcher below picks it or the CPU leg).
+static int batch_host_gpu(DevCtx* c, const void* const* ptrs, const uint64_t* lens, const uint32_t* crc_in,
+                          uint32_t* out, size_t n, int device, int pinned) {
   std::lock_guard<std::mutex> g(c->mu);
   int prev = 0;
   (void)hipGetDevice(&prev);
@@ -822,6 +859,16 @@ int ambrycrc_batch_multi(const void* const* ptrs, const uint64_t* lens, const ui
     dev[g] = devices ? devices[g] : g;
     if (!ctx_for(dev[g])) return AMBRYCRC_ENOINIT;
   }
+  // host-resident dispatch once for the whole batch: the CPU leg when the CPU threads beat every
+  // listed GPU's host path together (auto, pageable), else each range on its GPU
+  {
+    DevCtx* c0 = ctx_for(dev[0]);
+    double gpus = 0;
+    for (int g = 0; g < ndev; ++g) gpus += ctx_for(dev[g])->gpu_host_gibps.load();
+    const bool cpu = c0->host_policy == 2 || (c0->host_policy == 0 && !pinned && host_cpu_gibps() > gpus);
+    c0->last_host_path.store(cpu ? 0 : 1);
+    if (cpu) return ambrycrc_batch_cpu(ptrs, lens, crc_in, out, n, host_cpu_threads());
+  }
   std::vector<size_t> cut(ndev + 1, n);
   const int src = ambrycrc_shard_by_bytes(lens, n, ndev, cut.data());
   if (src) return src;
@@ -832,7 +879,8 @@ int ambrycrc_batch_multi(const void* const* ptrs, const uint64_t* lens, const ui
     const size_t a = cut[r], b = cut[r + 1];
     if (a >= b) continue;
     th.emplace_back([&, r, a, b] {
-      rc[r] = ambrycrc_batch_host(ptrs + a, lens + a, crc_in ? crc_in + a : nullptr, out + a, b - a, dev[r], pinned);
+      rc[r] = batch_host_gpu(ctx_for(dev[r]), ptrs + a, lens + a, crc_in ? crc_in + a : nullptr, out + a, b - a, dev[r],
+                             pinned);
     });
   }
   for (auto& t : th) t.join();
@@ -1084,9 +1132,18 @@ int enqueue_messages(DevCtx* c, const uint8_t* d_region, uint64_t region_len, co
   r.nsb = region_nsb(d_region, region_len);
   r.rk = static_cast<uint32_t*>(st.batch_ws);
   r.img = c->d_img;
-  if (c->region_mode == 2) {  // the two-pass form (A/B): runs kernel, then one thread per message
-    if (launch_region_runs(r, c->grid, stream) != hipSuccess) return AMBRYCRC_EHIP;
-    return hip_err(launch_region_msg(st.a, r, c->num_cu, stream));
+  if (c->region_mode == 2) {  // the two-pass form: runs kernel, then one thread per message
+    // long records (more than region::kLongRuns runs) listed in the job arrays' space, which
+    // region mode does not use: the whole grid takes them after pass 2
+    uint8_t* lw = static_cast<uint8_t*>(d_ws);
+    r.lng.ctr = reinterpret_cast<unsigned long long*>(lw);
+    r.lng.claim = reinterpret_cast<uint32_t*>(lw + 8);
+    r.lng.rec = reinterpret_cast<LongRec*>(lw + 64);
+    r.lng.cap = (uint32_t)std::min<size_t>(4096, (msg_jobs_bytes(m) - 64) / sizeof(LongRec));
+    if (launch_region_runs(r, c->grid, stream) != hipSuccess ||
+        launch_region_msg(st.a, r, c->num_cu, stream) != hipSuccess)
+      return AMBRYCRC_EHIP;
+    return hip_err(launch_region_long(st.a, r, c->num_cu, stream));
   }
   FusedArgs f;
   f.a = st.a;
@@ -1221,6 +1278,12 @@ uint64_t message_extent(const uint8_t* p, uint64_t rem) {
 
 }  // namespace
 
+namespace ambrycrc {
+namespace detail {
+uint64_t message_extent_of(const uint8_t* p, uint64_t rem) { return message_extent(p, rem); }
+}  // namespace detail
+}  // namespace ambrycrc
+
 extern "C" {
 
 int ambrycrc_verify_messages_dev(const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off, size_t m,
@@ -1242,12 +1305,9 @@ int ambrycrc_verify_messages_dev(const uint8_t* d_region, uint64_t region_len, c
                           ws_bytes ? ws_bytes : need, stream);
 }
 
-int ambrycrc_verify_messages_host(const uint8_t* region, uint64_t region_len, const uint64_t* msg_off, size_t m,
-                                  uint32_t* status, uint64_t* msg_end, int device, int pinned) {
-  if (m == 0) return AMBRYCRC_OK;
-  if (!msg_off || !status || (!region && region_len)) return AMBRYCRC_EINVAL;
-  DevCtx* c = ctx_for(device);
-  if (!c) return AMBRYCRC_ENOINIT;
+// ambrycrc_verify_messages_host's GPU leg.
+static int verify_messages_host_gpu(DevCtx* c, const uint8_t* region, uint64_t region_len, const uint64_t* msg_off,
+                                    size_t m, uint32_t* status, uint64_t* msg_end, int device, int pinned) {
   std::lock_guard<std::mutex> g(c->mu);
   int prev = 0;
   (void)hipGetDevice(&prev);
@@ -1395,15 +1455,11 @@ int ambrycrc_verify_messages_host(const uint8_t* region, uint64_t region_len, co
   return rc ? rc : rc2;
 }
 
-int ambrycrc_transform_messages_host(const uint8_t* region, uint64_t region_len, const uint64_t* msg_off, size_t m,
-                                     const int16_t* life_version, int header_version, uint8_t* out, uint64_t out_cap,
-                                     uint64_t* out_off, uint64_t* out_len, uint32_t* status, int device, int pinned) {
-  if (m == 0) return AMBRYCRC_OK;
-  if (!msg_off || !out_len || !status || (!region && region_len) || (!out && out_cap) || header_version < 1 ||
-      header_version > 3)
-    return AMBRYCRC_EINVAL;
-  DevCtx* c = ctx_for(device);
-  if (!c) return AMBRYCRC_ENOINIT;
+// ambrycrc_transform_messages_host's GPU leg.
+static int transform_messages_host_gpu(DevCtx* c, const uint8_t* region, uint64_t region_len, const uint64_t* msg_off,
+                                       size_t m, const int16_t* life_version, int header_version, uint8_t* out,
+                                       uint64_t out_cap, uint64_t* out_off, uint64_t* out_len, uint32_t* status,
+                                       int device, int pinned) {
   std::lock_guard<std::mutex> g(c->mu);
   int prev = 0;
   (void)hipGetDevice(&prev);
@@ -1594,6 +1650,93 @@ int ambrycrc_transform_messages_host(const uint8_t* region, uint64_t region_len,
   }
   (void)hipSetDevice(prev);
   return rc ? rc : rc2;
+}
+
+// ---- host-resident dispatch: the CPU leg or the GPU leg per call
+namespace {
+double seconds_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+// The context of a host call (device < 0: none, the CPU leg) and its status.
+int host_ctx(int device, DevCtx** c) {
+  *c = device >= 0 ? ctx_for(device) : nullptr;
+  return device >= 0 && !*c ? AMBRYCRC_ENOINIT : AMBRYCRC_OK;
+}
+}  // namespace
+
+int ambrycrc_batch_host(const void* const* ptrs, const uint64_t* lens, const uint32_t* crc_in, uint32_t* out, size_t n,
+                        int device, int pinned) {
+  if (n == 0) return AMBRYCRC_OK;
+  if (!ptrs || !lens || !out) return AMBRYCRC_EINVAL;
+  DevCtx* c;
+  if (const int rc = host_ctx(device, &c)) return rc;
+  if (host_take_cpu(c, device, pinned)) {
+    if (c) c->last_host_path.store(0);
+    return ambrycrc_batch_cpu(ptrs, lens, crc_in, out, n, host_cpu_threads());
+  }
+  c->last_host_path.store(1);
+  uint64_t bytes = 0;
+  for (size_t i = 0; i < n; ++i) bytes += lens[i];
+  const auto t0 = std::chrono::steady_clock::now();
+  const int rc = batch_host_gpu(c, ptrs, lens, crc_in, out, n, device, pinned);
+  if (rc == AMBRYCRC_OK && !pinned) host_note_gpu(c, bytes, seconds_since(t0));
+  return rc;
+}
+
+int ambrycrc_verify_messages_host(const uint8_t* region, uint64_t region_len, const uint64_t* msg_off, size_t m,
+                                  uint32_t* status, uint64_t* msg_end, int device, int pinned) {
+  if (m == 0) return AMBRYCRC_OK;
+  if (!msg_off || !status || (!region && region_len)) return AMBRYCRC_EINVAL;
+  DevCtx* c;
+  if (const int rc = host_ctx(device, &c)) return rc;
+  if (host_take_cpu(c, device, pinned)) {
+    if (c) c->last_host_path.store(0);
+    return verify_messages_cpu(region, region_len, msg_off, m, status, msg_end, host_cpu_threads());
+  }
+  c->last_host_path.store(1);
+  return verify_messages_host_gpu(c, region, region_len, msg_off, m, status, msg_end, device, pinned);
+}
+
+int ambrycrc_transform_messages_host(const uint8_t* region, uint64_t region_len, const uint64_t* msg_off, size_t m,
+                                     const int16_t* life_version, int header_version, uint8_t* out, uint64_t out_cap,
+                                     uint64_t* out_off, uint64_t* out_len, uint32_t* status, int device, int pinned) {
+  if (m == 0) return AMBRYCRC_OK;
+  if (!msg_off || !out_len || !status || (!region && region_len) || (!out && out_cap) || header_version < 1 ||
+      header_version > 3)
+    return AMBRYCRC_EINVAL;
+  DevCtx* c;
+  if (const int rc = host_ctx(device, &c)) return rc;
+  if (host_take_cpu(c, device, pinned)) {
+    if (c) c->last_host_path.store(0);
+    return transform_messages_cpu(region, region_len, msg_off, m, life_version, header_version, out, out_cap, out_off,
+                                  out_len, status, host_cpu_threads());
+  }
+  c->last_host_path.store(1);
+  return transform_messages_host_gpu(c, region, region_len, msg_off, m, life_version, header_version, out, out_cap,
+                                     out_off, out_len, status, device, pinned);
+}
+
+int ambrycrc_set_host_policy(int device, int policy) {
+  DevCtx* c = ctx_for(device);
+  if (!c) return AMBRYCRC_ENOINIT;
+  if (policy < 0 || policy > 2) return AMBRYCRC_EINVAL;
+  const int prev = c->host_policy;
+  c->host_policy = policy;
+  return prev;
+}
+
+int ambrycrc_host_rates(int device, double* cpu_gibps, double* gpu_gibps, int* cpu_threads) {
+  DevCtx* c = ctx_for(device);
+  if (!c) return AMBRYCRC_ENOINIT;
+  if (cpu_gibps) *cpu_gibps = host_cpu_gibps();
+  if (gpu_gibps) *gpu_gibps = c->gpu_host_gibps.load();
+  if (cpu_threads) *cpu_threads = host_cpu_threads();
+  return host_take_cpu(c, device, 0) ? 0 : 1;
+}
+
+int ambrycrc_last_host_path(int device) {
+  DevCtx* c = ctx_for(device);
+  return c ? c->last_host_path.load() : AMBRYCRC_ENOINIT;
 }
 
 size_t ambrycrc_trailed_workspace_bytes(size_t n) {

@@ -113,6 +113,13 @@ struct DevCtx {
     return -1;
   }
   void release_host_word(int k) { h_word_busy[k].store(false, std::memory_order_release); }
+  // Host-resident dispatch (ambrycrc_set_host_policy): 0 auto, 1 the GPU, 2 the CPU. Auto sends
+  // pageable host bytes to the CPU leg when the CPU threads' CRC rate beats gpu_host_gibps, the
+  // GPU host path's rate (PCIe-bound: 51 GiB/s measured, BENCH_r04 host_path; refreshed by every
+  // GPU host call of >= 64 MiB). last_host_path: 0 CPU, 1 GPU, -1 none yet.
+  int host_policy = 0;
+  std::atomic<double> gpu_host_gibps{51.0};
+  std::atomic<int> last_host_path{-1};
   // Processor waves of the one-pass kernels (0: per call, fused_proc_waves); AMBRYCRC_FUSED_PROC.
   int fused_proc = AMBRY_FUSED_PROC;
   uint64_t region_max = kRegionMaxPerMessage;  // region bytes per message up to which it applies
@@ -152,6 +159,16 @@ struct DevCtx {
 };
 
 int hip_err(hipError_t e);
+// Host-resident dispatch: the CPU threads the CPU leg uses (AMBRYCRC_CPU_THREADS, else
+// OMP_NUM_THREADS, else the CPUs this process may run on) and their combined CRC rate in GiB/s
+// (measured once per process on a 4 MiB buffer, x threads x 0.85).
+int host_cpu_threads();
+double host_cpu_gibps();
+// True when a host call over `bytes` of host memory should take the CPU leg (device < 0, the
+// CPU policy, or auto with pageable bytes the CPU threads hash faster than the GPU host path).
+bool host_take_cpu(DevCtx* c, int device, int pinned);
+// After a GPU host call over `bytes` that took `seconds`: refresh c->gpu_host_gibps.
+void host_note_gpu(DevCtx* c, uint64_t bytes, double seconds);
 DevCtx* ctx_for(int device);
 DevCtx* ctx_current();
 // Bytes of batch workspace for n chunks (ambrycrc_workspace_bytes).
@@ -203,6 +220,18 @@ int enqueue_serialize(DevCtx* c, const ::ambrycrc_put_desc* d_desc, size_t m, co
                       const uint8_t* d_blobs, uint8_t* d_out, uint64_t* d_msg_len, void* d_ws, hipStream_t stream,
                       const uint32_t* d_in_crc = nullptr, bool layout_only = false, const uint32_t* gate = nullptr,
                       const PropsFix* pfix = nullptr);
+
+// Bytes from a message's start that its verify may read (the header window, or the whole message
+// when the header's sizes fit `rem`).
+uint64_t message_extent_of(const uint8_t* p, uint64_t rem);
+// The host entries' CPU leg (ambrycrc_msg_cpu.cpp): the batch on `threads` CPU threads, each
+// message through ambrycrc_verify_message_cpu / ambrycrc_transform_message_cpu; outputs as the
+// device batch's.
+int verify_messages_cpu(const uint8_t* region, uint64_t region_len, const uint64_t* msg_off, size_t m,
+                        uint32_t* status, uint64_t* msg_end, int threads);
+int transform_messages_cpu(const uint8_t* region, uint64_t region_len, const uint64_t* msg_off, size_t m,
+                           const int16_t* life_version, int header_version, uint8_t* out, uint64_t out_cap,
+                           uint64_t* out_off, uint64_t* out_len, uint32_t* status, int threads);
 
 // Holds c->ws_mu for the lifetime of a *_dev call that uses the default workspace (d_ws ==
 // NULL); a call with its own workspace takes no lock.

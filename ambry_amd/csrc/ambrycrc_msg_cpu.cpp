@@ -211,3 +211,103 @@ int ambrycrc_transform_message_cpu(const uint8_t* region, uint64_t region_len, u
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- CPU batch forms
+// The host entries' CPU leg (ambrycrc_set_host_policy; DESIGN.md §5 "host-resident dispatch"):
+// ambrycrc_verify_messages_host / _transform_messages_host over messages in host memory, split
+// across `threads` CPU threads by region bytes, each message through the single-message loops
+// above. Same outputs as the device batch.
+#include <algorithm>
+#include <thread>
+#include <vector>
+
+#include "ambrycrc_ctx.h"
+
+namespace ambrycrc {
+namespace detail {
+
+namespace {
+// fn(a, b) over contiguous index ranges of [0, m) holding about equal sums of weight(i).
+template <class W, class F>
+void split_run(size_t m, int threads, W weight, F fn) {
+  threads = (int)std::max<size_t>(1, std::min<size_t>((size_t)std::max(threads, 1), m));
+  if (threads == 1) {
+    fn((size_t)0, m);
+    return;
+  }
+  std::vector<uint64_t> pre(m + 1, 0);
+  for (size_t i = 0; i < m; ++i) pre[i + 1] = pre[i] + weight(i) + 64;  // + a per-message cost
+  std::vector<size_t> cut(threads + 1, m);
+  cut[0] = 0;
+  for (int t = 1; t < threads; ++t)
+    cut[t] = (size_t)(std::lower_bound(pre.begin(), pre.end(), pre[m] * (uint64_t)t / (uint64_t)threads) - pre.begin());
+  std::vector<std::thread> th;
+  for (int t = 1; t < threads; ++t)
+    if (cut[t] < cut[t + 1]) th.emplace_back(fn, cut[t], cut[t + 1]);
+  fn(cut[0], cut[1]);
+  for (auto& x : th) x.join();
+}
+
+uint64_t extent_of(const uint8_t* region, uint64_t region_len, uint64_t off) {
+  return off >= region_len ? 0 : message_extent_of(region + off, region_len - off);
+}
+}  // namespace
+
+int verify_messages_cpu(const uint8_t* region, uint64_t region_len, const uint64_t* msg_off, size_t m,
+                        uint32_t* status, uint64_t* msg_end, int threads) {
+  int rc = AMBRYCRC_OK;
+  split_run(m, threads, [&](size_t i) { return extent_of(region, region_len, msg_off[i]); },
+            [&](size_t a, size_t b) {
+              for (size_t i = a; i < b; ++i) {
+                uint64_t e = 0;
+                if (ambrycrc_verify_message_cpu(region, region_len, msg_off[i], &status[i], &e) != AMBRYCRC_OK)
+                  rc = AMBRYCRC_EINVAL;
+                if (msg_end) msg_end[i] = e;
+              }
+            });
+  return rc;
+}
+
+int transform_messages_cpu(const uint8_t* region, uint64_t region_len, const uint64_t* msg_off, size_t m,
+                           const int16_t* life_version, int header_version, uint8_t* out, uint64_t out_cap,
+                           uint64_t* out_off, uint64_t* out_len, uint32_t* status, int threads) {
+  // each message into its own scratch span (its extent + the growth bound), in parallel; then packed
+  // in message order as the device batch packs it (NO_ROOM once the running sum passes out_cap)
+  std::vector<uint64_t> at(m + 1, 0);
+  for (size_t i = 0; i < m; ++i)
+    at[i + 1] = at[i] + extent_of(region, region_len, msg_off[i]) + AMBRYCRC_TRANSFORM_GROWTH_MAX;
+  std::vector<uint8_t> scratch(at[m]);
+  std::vector<uint64_t> len(m, 0);
+  int rc = AMBRYCRC_OK;
+  split_run(m, threads, [&](size_t i) { return at[i + 1] - at[i]; }, [&](size_t a, size_t b) {
+    for (size_t i = a; i < b; ++i) {
+      const int lv = life_version ? life_version[i] : -1;
+      if (ambrycrc_transform_message_cpu(region, region_len, msg_off[i], lv, header_version, scratch.data() + at[i],
+                                         at[i + 1] - at[i], &len[i], &status[i]) != AMBRYCRC_OK)
+        rc = AMBRYCRC_EINVAL;
+    }
+  });
+  if (rc) return rc;
+  uint64_t vpos = 0;
+  for (size_t i = 0; i < m; ++i) {
+    if (status[i] == 0 && len[i]) {
+      if (vpos + len[i] <= out_cap) {
+        memcpy(out + vpos, scratch.data() + at[i], len[i]);
+        if (out_off) out_off[i] = vpos;
+        out_len[i] = len[i];
+      } else {
+        status[i] = AMBRYCRC_MSG_NO_ROOM;
+        if (out_off) out_off[i] = ~0ull;
+        out_len[i] = 0;
+      }
+      vpos += len[i];
+      continue;
+    }
+    if (out_off) out_off[i] = ~0ull;
+    out_len[i] = 0;
+  }
+  return AMBRYCRC_OK;
+}
+
+}  // namespace detail
+}  // namespace ambrycrc

@@ -115,6 +115,28 @@ constexpr int kDiagNoFold = 100;  // diagnostic timing build, selectable via amb
 // region_runs_kernel), then one thread per message parses it and assembles its record CRCs from
 // the runs they cover (message_kernels.hip region_msg_kernel, region_crc.h). Runs are [base + 64k, base + 64k + 64) with
 // base = the region's start rounded down to 64 B; only 16-B pieces holding region bytes are read.
+// A record of more than region::kLongRuns runs (a multi-MiB blob among small messages) that
+// region_msg_kernel leaves to region_long_kernel: that kernel splits it into pieces of about
+// kLongPiece bytes over the whole grid -- each piece's zlib CRC by one wave from the run sums,
+// shifted to the record's end (crc(A||B) = crc(A) x^(8|B|) + crc(B)) and XORed into acc; the wave
+// that finishes the last piece compares acc with the stored CRC.
+struct LongRec {
+  uint64_t pa;       // base-relative start
+  uint64_t msg;      // message index
+  uint32_t len, ex;  // record length, stored CRC
+  uint32_t bit;      // the status bit of its record slot
+  uint32_t piece0;   // its first piece in the list's numbering
+  uint32_t pieces;
+  uint32_t acc, done;
+};
+struct LongList {
+  LongRec* rec = nullptr;              // [cap]
+  unsigned long long* ctr = nullptr;   // records << 32 | pieces, one atomic (piece0 ascending with the index)
+  uint32_t* claim = nullptr;           // pieces handed out by region_long_kernel
+  uint32_t cap = 0;                    // records the list holds (more: the old per-wave queue)
+};
+constexpr uint64_t kLongPiece = 256u << 10;
+
 struct RegionArgs {
   const uint8_t* base;   // region start rounded down to 64 B
   uint64_t reg0;         // region start - base (0..63)
@@ -124,6 +146,7 @@ struct RegionArgs {
   uint32_t* rk;          // [kRunPad + nsb * 64 + 256]: run k's raw CRC at rk[kRunPad + k]; then a
                          // 1 KiB spill line for the stores of lanes with no sums to write
   const uint32_t* img;   // the table image (kImgBytes)
+  LongList lng;          // two-pass region mode: long records (region_runs_kernel zeroes ctr / claim)
 };
 // Words ahead of run 0: a run group read before run 0 stays inside rk, and each super-block's 64
 // sums (one wave store) fill exactly two 128-B lines (a misaligned window left partial lines,
@@ -316,6 +339,9 @@ hipError_t launch_trailer_verify(const TrailerArgs& a, hipStream_t s);
 hipError_t launch_msg_parse(const MsgArgs& a, hipStream_t s);
 // Region mode, pass 2: parse, record CRCs from the run sums, status (a.job_* / expected / crc unused).
 hipError_t launch_region_msg(const MsgArgs& a, const RegionArgs& g, int num_cu, hipStream_t s);
+// Region mode, after pass 2: the long records of g.lng, split over the whole grid (returns at once
+// when there are none).
+hipError_t launch_region_long(const MsgArgs& a, const RegionArgs& g, int num_cu, hipStream_t s);
 hipError_t launch_msg_reduce(const MsgArgs& a, hipStream_t s);
 
 // Region mode in one pass: region_fused_kernel, one workgroup per CU over a

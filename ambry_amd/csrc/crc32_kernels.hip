@@ -1536,12 +1536,13 @@ hipError_t launch_sweep_copy(const SweepArgs& a, int grid, int num_cu, int varia
 // runs that straddle the region's ends are never used; region_msg_kernel (region_crc.h) recomputes those
 // runs from the bytes). Runs have no loop-carried state, so consecutive super-blocks' chains
 // are independent.
+template <bool NT = true>
 __device__ __forceinline__ void region_sb_load(const RegionArgs& a, uint64_t s, uint32_t lane, u32x4 (&x)[4]) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const uint64_t p = s * kSuperBlock + (uint64_t)kBlockBytes * i + 16u * lane;
     const uint64_t q = p < a.lo16 ? a.lo16 : (p > a.hi16 ? a.hi16 : p);
-    x[i] = ld16<true>(reinterpret_cast<const u32x4*>(a.base + q));
+    x[i] = ld16<NT>(reinterpret_cast<const u32x4*>(a.base + q));
   }
 }
 
@@ -1557,6 +1558,10 @@ __device__ __forceinline__ void region_sb_zero(const RegionArgs& a, uint64_t s, 
 // 6 = every wave's stores to one 1 KiB line set (timing only, wrong sums); AMBRY_RUNS_STORE_NT 0 =
 // plain stores.
 __global__ __launch_bounds__(1024) void region_runs_kernel(RegionArgs a) {
+  if (a.lng.ctr && blockIdx.x == 0 && threadIdx.x == 0) {  // pass 2's long-record list starts empty
+    *a.lng.ctr = 0;
+    *a.lng.claim = 0;
+  }
   const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
   // Shares wave-major over workgroups, as the sweep kernel's (CU-major shares measured the same).
   const uint32_t wave = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * gridDim.x + blockIdx.x);
@@ -1776,10 +1781,10 @@ __global__ __launch_bounds__(64 * W) void region_fused_kernel(FusedArgs f) {
     if (mine_n) {
       u32x4 b0[4], b1[4], b2[4], b3[4];
       uint64_t g = gfirst;
-      region_sb_load(a, 4 * g, lane, b0);
-      region_sb_load(a, 4 * g + 1, lane, b1);
-      region_sb_load(a, 4 * g + 2, lane, b2);
-      region_sb_load(a, 4 * g + 3, lane, b3);
+      region_sb_load<AMBRY_FUSED_NT != 0>(a, 4 * g, lane, b0);
+      region_sb_load<AMBRY_FUSED_NT != 0>(a, 4 * g + 1, lane, b1);
+      region_sb_load<AMBRY_FUSED_NT != 0>(a, 4 * g + 2, lane, b2);
+      region_sb_load<AMBRY_FUSED_NT != 0>(a, 4 * g + 3, lane, b3);
       for (uint64_t j = 0; j < mine_n; ++j, g += gstep) {
         const uint64_t nx = j + 1 < mine_n ? g + gstep : g;  // the last group re-reads itself
         // COPY: a message that cannot take the fast path anywhere ends the pass (the general path
@@ -1798,19 +1803,19 @@ __global__ __launch_bounds__(64 * W) void region_fused_kernel(FusedArgs f) {
                              __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         __builtin_amdgcn_s_setprio(3);
-        region_sb_load(a, 4 * nx, lane, b0);
+        region_sb_load<AMBRY_FUSED_NT != 0>(a, 4 * nx, lane, b0);
         __builtin_amdgcn_s_setprio(0);
         hash(4 * g + 1, 1, b1);
         __builtin_amdgcn_s_setprio(3);
-        region_sb_load(a, 4 * nx + 1, lane, b1);
+        region_sb_load<AMBRY_FUSED_NT != 0>(a, 4 * nx + 1, lane, b1);
         __builtin_amdgcn_s_setprio(0);
         hash(4 * g + 2, 2, b2);
         __builtin_amdgcn_s_setprio(3);
-        region_sb_load(a, 4 * nx + 2, lane, b2);
+        region_sb_load<AMBRY_FUSED_NT != 0>(a, 4 * nx + 2, lane, b2);
         __builtin_amdgcn_s_setprio(0);
         hash(4 * g + 3, 3, b3);
         __builtin_amdgcn_s_setprio(3);
-        region_sb_load(a, 4 * nx + 3, lane, b3);
+        region_sb_load<AMBRY_FUSED_NT != 0>(a, 4 * nx + 3, lane, b3);
         __builtin_amdgcn_s_setprio(0);
         const u32x4 sums = *reinterpret_cast<const u32x4*>(buf + 4u * lane);
         if constexpr (AMBRY_FUSED_PROBE == 3) {  // A/B probe 3: no sum stores (timing only)

@@ -143,6 +143,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AMBRY_REGIO
       const uint32_t jl = slot[4 * k + 2], ex = slot[4 * k + 3];
       const uint64_t pa = g.reg0 + jo;
       if (jl && (int64_t)((((pa + jl + 63) & ~uint64_t(63)) - (pa & ~uint64_t(63))) >> 6) > region::kLongRuns) {
+        if (g.lng.ctr) {  // to region_long_kernel: the whole grid takes it, piece by piece
+          const uint32_t pieces = (uint32_t)((jl + kLongPiece - 1) / kLongPiece);
+          const unsigned long long was = atomicAdd(g.lng.ctr, (1ull << 32) | pieces);
+          const uint32_t at = (uint32_t)(was >> 32);
+          if (at < g.lng.cap) {
+            LongRec& lr = g.lng.rec[at];
+            lr.pa = pa;
+            lr.msg = i;
+            lr.len = jl;
+            lr.ex = ex;
+            lr.bit = AMBRYCRC_MSG_ENCKEY_CRC << k;
+            lr.piece0 = (uint32_t)was;
+            lr.pieces = pieces;
+            lr.acc = 0;
+            lr.done = 0;
+            continue;
+          }
+        }
         const uint32_t at = atomicAdd(&lq_n[wv], 1u);
         if (at < kLongQ) {  // the wave's, after the loop (its bit ORed into the status then)
           lq_jo[wv][at] = pa;
@@ -552,6 +570,63 @@ hipError_t launch_region_msg(const MsgArgs& a, const RegionArgs& g, int num_cu, 
   uint64_t blocks = (a.m + 255) / 256;
   if (bpc > 0 && blocks > (uint64_t)num_cu * bpc) blocks = (uint64_t)num_cu * bpc;
   hipLaunchKernelGGL(region_msg_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, a, g);
+  return hipGetLastError();
+}
+
+// The long records region_msg_kernel listed (LongList): a piece is handed out per wave round by one
+// atomic; the record holding piece q is found by a search of the ascending piece0; its zlib CRC
+// comes from record_crc_runs_wave over the piece's bytes [s, e), is shifted by x^(8(len - e)) to the
+// record's end (x^(8*2^k) words, gf2_mul) and XORed into acc. The wave that finishes a record's last
+// piece reads acc back (every XOR was made before its done increment) and flags a mismatch.
+// (Before: one wave walked each whole record after its messages -- ~100 us per 4 MiB blob, which
+// ended the kernel long after the rest; tools/probes/long_mix.py.)
+__global__ __launch_bounds__(256) void region_long_kernel(MsgArgs a, RegionArgs g) {
+  const unsigned long long ctr = __hip_atomic_load(g.lng.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t n = min((uint32_t)(ctr >> 32), g.lng.cap);
+  if (n == 0) return;
+  const uint32_t total = g.lng.rec[n - 1].piece0 + g.lng.rec[n - 1].pieces;
+  __shared__ uint32_t tbl[1024];
+  __shared__ uint32_t nib[region::kNibTotal];
+  __shared__ uint32_t dn[region::kDirSets * region::kNibWords];
+  stage_slice_tables(tbl, a.img);
+  region::stage_nib(nib, a.img);
+  region::stage_direct_nib(dn, a.img);
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t* rk = g.rk + kRunPad;
+  for (;;) {
+    uint32_t q = 0;
+    if (lane == 0) q = atomicAdd(g.lng.claim, 1u);
+    q = __builtin_amdgcn_readfirstlane(q);
+    if (q >= total) break;
+    uint32_t lo = 0, hi = n - 1;  // the last record with piece0 <= q
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1) / 2;
+      if (g.lng.rec[mid].piece0 <= q) lo = mid;
+      else hi = mid - 1;
+    }
+    LongRec& lr = g.lng.rec[lo];
+    const uint64_t len = lr.len;
+    const uint32_t p = q - lr.piece0, np = lr.pieces;
+    const uint64_t s = len * p / np, e = len * (p + 1) / np;
+    uint32_t c = region::record_crc_runs_wave(region::TabC{tbl}, nib, dn, g.base, rk, lr.pa + s, e - s, lane);
+    if (lane == 0) {
+      for (uint64_t d = len - e, k = 0; d; d >>= 1, ++k)  // c * x^(8(len - e))
+        if (d & 1) c = gf2_mul(c, nib[region::kXpOff + k]);
+      atomicXor(&lr.acc, c);
+      __threadfence();
+      if (atomicAdd(&lr.done, 1u) == np - 1) {
+        __threadfence();
+        const uint32_t crc = atomicOr(&lr.acc, 0u);
+        if (crc != lr.ex) atomicOr(&a.status[lr.msg], lr.bit);
+      }
+    }
+  }
+}
+
+hipError_t launch_region_long(const MsgArgs& a, const RegionArgs& g, int num_cu, hipStream_t s) {
+  if (a.m == 0 || !g.lng.ctr) return hipSuccess;
+  hipLaunchKernelGGL(region_long_kernel, dim3((uint32_t)num_cu * 2), dim3(256), 0, s, a, g);
   return hipGetLastError();
 }
 

@@ -190,6 +190,29 @@ def set_transform_verdict(device: int, host: bool) -> int:
     return check(lib().ambrycrc_set_transform_verdict(device, 1 if host else 0), "ambrycrc_set_transform_verdict")
 
 
+HOST_AUTO, HOST_GPU, HOST_CPU = 0, 1, 2
+
+
+def set_host_policy(device: int, policy: int) -> int:
+    """Host-resident dispatch of the *_host entries (ambrycrc_set_host_policy): HOST_AUTO (the
+    default: the CPU leg for pageable bytes when the CPU threads beat the GPU host path), HOST_GPU,
+    HOST_CPU. Returns the previous policy."""
+    return check(lib().ambrycrc_set_host_policy(device, int(policy)), "ambrycrc_set_host_policy")
+
+
+def host_rates(device: int = 0) -> dict:
+    """The rates the auto policy compares (ambrycrc_host_rates) and the leg it takes for pageable bytes."""
+    c, g, t = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
+    leg = check(lib().ambrycrc_host_rates(device, ctypes.byref(c), ctypes.byref(g), ctypes.byref(t)),
+                "ambrycrc_host_rates")
+    return {"cpu_gibps": c.value, "gpu_gibps": g.value, "cpu_threads": t.value, "auto_leg": "gpu" if leg else "cpu"}
+
+
+def last_host_path(device: int = 0) -> int:
+    """The leg the device's last host call took: 0 CPU, 1 GPU (-1: none yet)."""
+    return lib().ambrycrc_last_host_path(device)
+
+
 def set_grid(device: int, workgroups: int) -> None:
     check(lib().ambrycrc_set_grid(device, workgroups), "ambrycrc_set_grid")
 

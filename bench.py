@@ -274,13 +274,29 @@ def host_path_rate(torch, args):
     roof = best_of(lambda: dev.copy_(host, non_blocking=True))
     del dev
     res = {}
-    for name, base in (("pinned", host.data_ptr()), ("pageable", pageable.ctypes.data)):
-        chunks = [(base + i * chunk, chunk) for i in range(nchunks)]
-        res[name] = best_of(lambda: D.crc32_batch_host(chunks, device=0, pinned=name == "pinned"))
+    prev = D.set_host_policy(0, D.HOST_GPU)  # the GPU leg itself, whatever auto would pick
+    try:
+        for name, base in (("pinned", host.data_ptr()), ("pageable", pageable.ctypes.data)):
+            chunks = [(base + i * chunk, chunk) for i in range(nchunks)]
+            res[name] = best_of(lambda: D.crc32_batch_host(chunks, device=0, pinned=name == "pinned"))
+        # the CPU leg on the same pageable sample, and the leg the default (auto) policy takes
+        D.set_host_policy(0, D.HOST_CPU)
+        chunks = [(pageable.ctypes.data + i * chunk, chunk) for i in range(nchunks)]
+        res["cpu_leg"] = best_of(lambda: D.crc32_batch_host(chunks, device=0))
+        D.set_host_policy(0, D.HOST_AUTO)
+        res["auto"] = best_of(lambda: D.crc32_batch_host(chunks, device=0))
+        auto_leg = "gpu" if D.last_host_path(0) == 1 else "cpu"
+        rates = D.host_rates(0)
+    finally:
+        D.set_host_policy(0, prev)
     return {"value": round(res["pinned"], 2), "unit": "GiB/s",
             "pageable": round(res["pageable"], 2),
             "h2d_copy_roof": round(roof, 2),
             "frac_of_h2d_roof": round(res["pinned"] / roof, 4),
+            "dispatch": {"cpu_leg_pageable": round(res["cpu_leg"], 2), "auto_pageable": round(res["auto"], 2),
+                         "auto_leg": auto_leg, "cpu_threads": rates["cpu_threads"],
+                         "policy_cpu_estimate": round(rates["cpu_gibps"], 1),
+                         "policy_gpu_estimate": round(rates["gpu_gibps"], 1)},
             "sample": f"{nchunks} x 4 MiB host chunks (2 GiB), synchronous ambrycrc_batch_host (H2D + kernels + "
                       "D2H of CRCs), best of 3 after one untimed pass; pinned = hipHostMalloc'd source, "
                       "pageable = malloc'd source staged by the library's copy threads"}

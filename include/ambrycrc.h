@@ -385,6 +385,26 @@ int ambrycrc_transform_message_cpu(const uint8_t* region, uint64_t region_len, u
 int ambrycrc_batch_host(const void* const* ptrs, const uint64_t* lens, const uint32_t* crc_in, uint32_t* out,
                         size_t n, int device, int pinned);
 
+/* Host-resident dispatch of the *_host entries (ambrycrc_batch_host, _verify_messages_host,
+ * _transform_messages_host, and through them _verify_trailed_host and _range_checksums_host;
+ * ambrycrc_batch_multi decides once for its whole batch). Bytes that live in pageable host memory
+ * reach the GPU over PCIe (~51 GiB/s per GPU) while the CPU's CLMUL loop hashes them
+ * at ~9 GiB/s per thread: policy 0 (auto, the default) takes the CPU leg -- the same outputs, on
+ * ambrycrc_host_rates' CPU threads -- when their rate beats the GPU host path's, and the GPU for
+ * pinned bytes (pinned != 0: the caller registered them for DMA); 1 = always the GPU; 2 = always
+ * the CPU. device < 0 in those entries means the CPU leg (no context needed). Returns the previous
+ * policy. Replaces nothing in the reference, whose callers (NettyServerRequest.java:35,54,
+ * StoreMessageReadSet.java:170-188) hold exactly such host buffers. */
+int ambrycrc_set_host_policy(int device, int policy);
+/* The rates the auto policy compares: *cpu_gibps (CPU threads x per-thread CLMUL rate measured once
+ * per process x 0.85), *gpu_gibps (the GPU host path: 51 GiB/s measured, refreshed by each pageable
+ * GPU call of >= 64 MiB), *cpu_threads (AMBRYCRC_CPU_THREADS, else OMP_NUM_THREADS, else this
+ * process's CPUs). Returns the leg auto takes for pageable bytes (0 CPU, 1 GPU), or < 0. Any
+ * output may be NULL. */
+int ambrycrc_host_rates(int device, double* cpu_gibps, double* gpu_gibps, int* cpu_threads);
+/* The leg the device's last host call took: 0 CPU, 1 GPU, -1 none yet. */
+int ambrycrc_last_host_path(int device);
+
 /* ambrycrc_batch_host across several GPUs of this process: the n
  * chunks are split into ndev contiguous ranges by ambrycrc_shard_by_bytes, range g runs ambrycrc_batch_host on devices[g]
  * from its own host thread, and the calls are joined. devices == NULL means

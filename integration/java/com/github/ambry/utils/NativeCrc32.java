@@ -109,6 +109,7 @@ public final class NativeCrc32 implements Checksum {
    * copy, gfx950 kernels): out[i] = crc32(crcIn == null ? 0 : crcIn[i], bufs[i][pos[i], pos[i] + len[i])).
    */
   public static void batch(ByteBuffer[] bufs, int[] pos, int[] len, int[] crcIn, int[] out, int device) {
+    // device < 0: the CPU leg; otherwise the library's host-resident dispatch (ambrycrc_set_host_policy)
     nativeBatchDirect(bufs, pos, len, crcIn, out, device);
   }
 
@@ -119,6 +120,8 @@ public final class NativeCrc32 implements Checksum {
    * ends[i] (may be null) = end offset of message i, 0 when its layout is invalid.
    */
   public static void verifyMessages(ByteBuffer region, long[] offsets, int[] status, long[] ends, int device) {
+    // device < 0: the library's CPU leg; otherwise its host-resident dispatch picks the CPU threads or
+    // GPU `device` for these (pageable) bytes, whichever hashes them faster (ambrycrc_set_host_policy)
     nativeVerifyMessages(region, offsets, status, ends, device);
   }
 
@@ -166,6 +169,7 @@ public final class NativeCrc32 implements Checksum {
    */
   public static void transformMessages(ByteBuffer region, long[] offsets, short[] lifeVersions, int headerVersion,
       ByteBuffer out, long[] outOffsets, long[] outLens, int[] status, int device) {
+    // device < 0: the CPU leg; otherwise the library's host-resident dispatch (ambrycrc_set_host_policy)
     nativeTransformMessages(region, offsets, lifeVersions, headerVersion, out, outOffsets, outLens, status, device);
   }
 

@@ -146,4 +146,7 @@ def gpu():
 
     torch.cuda.init()
     device.init(0)
+    # the GPU suite tests the GPU leg of the *_host entries; the host-resident dispatch policy's own
+    # tests (test_host_policy.py, test_gpu_host_policy) set it themselves
+    device.set_host_policy(0, device.HOST_GPU)
     return device

@@ -287,7 +287,8 @@ def test_chain_messages_host_under_asan(tmp_path):
                     os.path.join(ROOT, "tests", "native", "chain_asan.cpp"), os.path.join(csrc, "ambrycrc.cpp"),
                     os.path.join(csrc, "ambrycrc_multi.cpp"), os.path.join(csrc, "crc32_kernels.hip"),
                     os.path.join(csrc, "message_kernels.hip"), os.path.join(csrc, "ambrycrc_put.cpp"),
-                    os.path.join(csrc, "put_kernels.hip"), "-ldl", "-o", str(exe)], check=True, timeout=900)
+                    os.path.join(csrc, "put_kernels.hip"), os.path.join(csrc, "ambrycrc_msg_cpu.cpp"), "-ldl", "-o",
+                    str(exe)], check=True, timeout=900)
     r = subprocess.run([str(exe), str(rf)], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "runs=" in r.stdout

@@ -369,3 +369,36 @@ def test_unsorted_offsets_take_the_tail(gpu, msg_mode):
     st, end = run(gpu, region, [offs[j] for j in perm])
     assert st == [expect[j][0] for j in perm]
     assert end == [expect[j][1] for j in perm]
+
+
+def test_long_records_split_over_the_grid(gpu, msg_mode):
+    """Several multi-MiB blobs among small PUTs (tools/probes/long_mix.py's shape, scaled down): in
+    two-pass region mode each is split into ~256 KiB pieces that waves across the GPU hash from the
+    run sums and combine by x^(8d) shifts (region_long_kernel). Flips land in the first piece, one
+    byte either side of piece boundaries, and in the last 64-B run of a blob; a 3 MiB + 1 B blob (an
+    uneven last piece) and a 32 KiB + 1 B one (a single piece) stay clean. Every status and end
+    equals the oracle's."""
+    from datagen import stream_bytes
+
+    sizes = {300: (4 << 20) + 13, 900: (3 << 20) + 1, 1400: (32 << 10) + 1, 2100: (5 << 20) - 7, 2500: 9 << 20}
+    msgs = []
+    for i in range(6000):
+        size = sizes.get(i, 200 + (i * 37) % 1700)
+        msgs.append(MF.put_message(MF.store_key("G%d" % i), MF.blob_properties_bytes(size), b"q" * (i % 11),
+                                   stream_bytes(7000 + i, 0, size).tobytes(), version=1 + i % 3))
+    offs = np.cumsum([0] + [len(x) for x in msgs[:-1]]).tolist()
+    region = bytearray(b"".join(msgs))
+    blob_at = {i: offs[i] + len(msgs[i]) - 8 - sizes[i] for i in sizes}  # blob content start
+    # (record = 13-B head + content + 8-B CRC; pieces split the record, so boundaries sit near k*len/np)
+    flips = {300: 100, 2100: ((5 << 20) + 13 + 8) // 20 * 3 - 13, 2500: (9 << 20) - 3}
+    for i, d in flips.items():
+        region[blob_at[i] + d] ^= 0x04
+    region[blob_at[2100] + ((5 << 20) + 21) * 7 // 20 - 12] ^= 0x80  # one byte past another boundary
+    region = bytes(region)
+    expect = [MF.verify_message(region, o) for o in offs]
+    assert len(region) <= 6144 * len(offs)  # region mode engages
+    st, end = run(gpu, region, offs, shift=3)
+    _expect_mode(gpu, msg_mode, len(region), len(offs))
+    assert st == [s for s, _ in expect]
+    assert end == [e for _, e in expect]
+    assert st[300] == st[2100] == st[2500] == MF.BLOB_CRC and st[900] == st[1400] == 0

@@ -1,0 +1,90 @@
+"""Host-resident dispatch (include/ambrycrc.h ambrycrc_set_host_policy): the
+*_host entries' CPU leg. device = -1 runs it without any GPU context, so this file runs on the CPU:
+ambrycrc_batch_host, _verify_messages_host and _transform_messages_host on the CPU leg against
+zlib and oracle/message_format.py (the same outputs the GPU leg's tests check), and the argument
+rules of the policy calls."""
+import zlib
+
+import numpy as np
+import pytest
+
+from datagen import stream_bytes
+from test_message_format import MF, build_region
+
+
+@pytest.fixture(scope="module")
+def ambry():
+    from conftest import _build_if_missing
+
+    _build_if_missing()
+    import ambry_amd
+
+    return ambry_amd
+
+
+def test_batch_host_cpu_leg(ambry):
+    """ambrycrc_batch_host(device = -1): every chunk's CRC (with and without crc_in) equals zlib's,
+    empty chunks included -- Crc32.update over each buffer (Crc32.java:55-98)."""
+    from ambry_amd import device as D
+
+    mem = stream_bytes(3, 0, 6 << 20)
+    rng = np.random.default_rng(4)
+    offs = rng.integers(0, (6 << 20) - (1 << 20), size=300)
+    lens = rng.integers(0, 1 << 20, size=300)
+    lens[:3] = [0, 1, 4095]
+    chunks = [(mem.ctypes.data + int(o), int(n)) for o, n in zip(offs, lens)]
+    got = D.crc32_batch_host(chunks, device=-1)
+    assert got == [zlib.crc32(mem[o:o + n].tobytes()) for o, n in zip(offs, lens)]
+    cin = rng.integers(0, 1 << 32, size=300, dtype=np.uint64).astype(np.uint32)
+    got = D.crc32_batch_host(chunks, device=-1, crc_in=cin)
+    assert got == [zlib.crc32(mem[o:o + n].tobytes(), int(c)) for o, n, c in zip(offs, lens, cin)]
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_verify_messages_host_cpu_leg(ambry, seed):
+    """ambrycrc_verify_messages_host(device = -1) over a region of PUT / update messages (headers
+    V1-V3, corrupt bytes, a bad version, a truncated tail): every status and message end equals the
+    oracle's deserializeBlobAll reading, as the GPU leg's test_verify_messages_host_matches_oracle."""
+    from ambry_amd import device as D
+
+    region, offs, expect = build_region(n=400, seed=seed, corrupt_frac=0.1)
+    st, end = D.verify_messages_host(region, offs, device=-1)
+    assert list(st) == [s for s, _ in expect]
+    assert list(end) == [e for _, e in expect]
+
+
+def test_transform_messages_host_cpu_leg(ambry):
+    """ambrycrc_transform_messages_host(device = -1): ValidatingTransformer.transform over a batch
+    (ValidatingTransformer.java:46-104) -- clean PUTs of every header version re-serialized at V3
+    with index life versions, corrupt ones and update records refused -- packed in message order;
+    then a cap that holds only the first 20 outputs gives NO_ROOM after them, as the device batch."""
+    from ambry_amd.messages import transform_host
+
+    region, offs, _ = build_region(n=300, seed=9, corrupt_frac=0.1)
+    life = np.random.default_rng(2).integers(0, 7, size=len(offs)).astype(np.int16)
+    out, oo, ol, st = transform_host(region, offs, life_version=life, device=-1)
+    pos = 0
+    for i, o in enumerate(offs):
+        exp_st, exp = MF.transform_message(region, o, life=int(life[i]), version=3)
+        assert int(st[i]) == exp_st, i
+        if exp is None:
+            assert ol[i] == 0 and oo[i] == -1
+            continue
+        assert oo[i] == pos and ol[i] == len(exp) and out[pos:pos + len(exp)] == exp, i
+        pos += len(exp)
+    ok = [i for i in range(len(offs)) if st[i] == 0]
+    cap = int(oo[ok[20]])
+    _, oo2, ol2, st2 = transform_host(region, offs, life_version=life, device=-1, out_cap=cap)
+    assert all(st2[i] == 0 for i in ok[:20]) and all(st2[i] == (1 << 12) for i in ok[20:])  # AMBRYCRC_MSG_NO_ROOM
+    assert all(oo2[i] == -1 and ol2[i] == 0 for i in ok[20:])
+
+
+def test_policy_calls_without_context(ambry):
+    """Policy calls need a context (ENOINIT without one); the CPU leg does not."""
+    from ambry_amd._lib import lib
+
+    L = lib()
+    dev = 63  # never initialised here
+    assert L.ambrycrc_set_host_policy(dev, 1) == -4
+    assert L.ambrycrc_last_host_path(dev) == -4
+    assert L.ambrycrc_host_rates(dev, None, None, None) == -4

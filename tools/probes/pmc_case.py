@@ -11,8 +11,8 @@ untimed; the profiler's per-dispatch counters are the measurement.
   batch16k   16 KiB chunks, aligned                                               -- class 3
   msg4k      ambrycrc_verify_messages_dev over 262,144 x PUT(4 KiB blob), 1.29 GiB (the default: region
              mode, two passes)
-  msg1k      the same over 524,288 x PUT(1 KiB blob); msg3k with 3000 B blobs
-  msg4k_1pass / msg4k_jobs   msg4k in region mode's one-pass form / in job mode (msg4k_2pass = msg4k)
+  msg1k      the same over 524,288 x PUT(1 KiB blob); msg3k with 3000 B blobs; msg100: 1,048,576 x 100 B
+  <msg>_1pass / <msg>_jobs   in region mode's one-pass form / in job mode (<msg>_2pass = <msg>)
   scatter16 / scatter4 / scatter8   FETCH_SIZE calibration: every 128-B line of 1 GiB read once in
              scattered order by one 16-B / 4-B / unaligned 8-B load (ambrycrc_debug_readbw_dev 60-62)
   put4k      ambrycrc_serialize_puts_dev, copy mode, 262,144 x PUT(4 KiB blob); put4k_inplace in place
@@ -85,10 +85,12 @@ def main():
         for _ in range(args.reps):
             D.crc32_batch(buf, off, ln, out=out, workspace=ws)
         info.update(chunks=1, chunk_bytes=size, alg_bytes_per_launch=size + 4)
-    elif args.case in ("msg4k", "msg3k", "msg1k", "msg4k_2pass", "msg4k_1pass", "msg4k_jobs"):
+    elif args.case.split("_")[0] in ("msg4k", "msg3k", "msg1k", "msg100") and \
+            args.case.split("_")[-1] in ("msg4k", "msg3k", "msg1k", "msg100", "2pass", "1pass", "jobs"):
         from bench_messages import gpu_region, load_mf
 
-        m, blob = {"msg3k": (262144, 3000), "msg1k": (524288, 1024)}.get(args.case, (262144, 4096))
+        m, blob = {"msg3k": (262144, 3000), "msg1k": (524288, 1024),
+                   "msg100": (1048576, 100)}.get(args.case.split("_")[0], (262144, 4096))
         mode = "region" if args.case.endswith("_1pass") else "jobs" if args.case.endswith("_jobs") else "region2"
         res = gpu_region(load_mf(), m, blob, args.reps, mode=mode)
         info.update(res)
