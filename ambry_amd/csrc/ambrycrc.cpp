@@ -1731,7 +1731,7 @@ int ambrycrc_host_rates(int device, double* cpu_gibps, double* gpu_gibps, int* c
   if (cpu_gibps) *cpu_gibps = host_cpu_gibps();
   if (gpu_gibps) *gpu_gibps = c->gpu_host_gibps.load();
   if (cpu_threads) *cpu_threads = host_cpu_threads();
-  return host_take_cpu(c, device, 0) ? 0 : 1;
+  return host_cpu_gibps() > c->gpu_host_gibps.load() ? 0 : 1;  // auto's leg for pageable bytes, whatever the policy
 }
 
 int ambrycrc_last_host_path(int device) {

@@ -56,6 +56,9 @@
 #ifndef AMBRY_RUNS_STORE_NT  // region pass 1: nontemporal run-sum stores
 #define AMBRY_RUNS_STORE_NT 0
 #endif
+#ifndef AMBRY_RUNS_NT  // region pass 1: nontemporal loads (0: temporal -- pass 2's re-reads may then hit L2 / MALL)
+#define AMBRY_RUNS_NT 1
+#endif
 #ifndef AMBRY_RUNS_GIL  // region pass 1: super-blocks in flight per wave beyond the current one
 #define AMBRY_RUNS_GIL 1
 #endif
@@ -91,7 +94,7 @@
   X(AMBRY_FUSED_WAVES_VERIFY, 12)                                                                               \
   X(AMBRY_FUSED_WAVES_COPY, 8) X(AMBRY_FUSED_NT, 1)                                                                 \
   X(AMBRY_GRP_PRIO, 0) X(AMBRY_GRP_IL, 4) X(AMBRY_C0_G, 2) X(AMBRY_C0_NB, 8) X(AMBRY_C1_MAX, 1024)           \
-  X(AMBRY_RUNS_STORE_NT, 0) X(AMBRY_RUNS_GIL, 1) X(AMBRY_PLAN_PER_BLOCK, 2048) X(AMBRY_DEFAULT_VARIANT, 29) \
+  X(AMBRY_RUNS_STORE_NT, 0) X(AMBRY_RUNS_NT, 1) X(AMBRY_RUNS_GIL, 1) X(AMBRY_PLAN_PER_BLOCK, 2048) X(AMBRY_DEFAULT_VARIANT, 29) \
   X(AMBRY_REGION_PROBE, 0) X(AMBRY_RUNS_PROBE, 0) X(AMBRY_FUSED_PROBE, 0)
 
 #if defined(AMBRY_AB_PROBE_BUILD)

@@ -132,7 +132,7 @@ struct LongRec {
 struct LongList {
   LongRec* rec = nullptr;              // [cap]
   unsigned long long* ctr = nullptr;   // records << 32 | pieces, one atomic (piece0 ascending with the index)
-  uint32_t* claim = nullptr;           // pieces handed out by region_long_kernel
+  uint32_t* claim = nullptr;           // (zeroed with ctr; reserved)
   uint32_t cap = 0;                    // records the list holds (more: the old per-wave queue)
 };
 constexpr uint64_t kLongPiece = 256u << 10;

@@ -1602,28 +1602,28 @@ __global__ __launch_bounds__(1024) void region_runs_kernel(RegionArgs a) {
     if (AMBRY_RUNS_PROBE == 0 || r == 0x9E3779B9u) buf[64u * u + slot] = r;
   };
   u32x4 b0[4], b1[4], b2[4], b3[4];
-  region_sb_load(a, first, lane, b0);
-  region_sb_load(a, at(first + 1), lane, b1);
-  region_sb_load(a, at(first + 2), lane, b2);
-  region_sb_load(a, at(first + 3), lane, b3);
+  region_sb_load<AMBRY_RUNS_NT != 0>(a, first, lane, b0);
+  region_sb_load<AMBRY_RUNS_NT != 0>(a, at(first + 1), lane, b1);
+  region_sb_load<AMBRY_RUNS_NT != 0>(a, at(first + 2), lane, b2);
+  region_sb_load<AMBRY_RUNS_NT != 0>(a, at(first + 3), lane, b3);
   u32x4* spill = reinterpret_cast<u32x4*>(a.rk + kRunPad + a.nsb * 64) + lane;
   for (uint64_t g = first; g < end; g += step) {
     const uint64_t nx = g + step;
     hash(g, 0, b0);
     __builtin_amdgcn_s_setprio(3);
-    region_sb_load(a, at(nx), lane, b0);
+    region_sb_load<AMBRY_RUNS_NT != 0>(a, at(nx), lane, b0);
     __builtin_amdgcn_s_setprio(0);
     if (g + 1 < end) hash(g + 1, 1, b1);
     __builtin_amdgcn_s_setprio(3);
-    region_sb_load(a, at(nx + 1), lane, b1);
+    region_sb_load<AMBRY_RUNS_NT != 0>(a, at(nx + 1), lane, b1);
     __builtin_amdgcn_s_setprio(0);
     if (g + 2 < end) hash(g + 2, 2, b2);
     __builtin_amdgcn_s_setprio(3);
-    region_sb_load(a, at(nx + 2), lane, b2);
+    region_sb_load<AMBRY_RUNS_NT != 0>(a, at(nx + 2), lane, b2);
     __builtin_amdgcn_s_setprio(0);
     if (g + 3 < end) hash(g + 3, 3, b3);
     __builtin_amdgcn_s_setprio(3);
-    region_sb_load(a, at(nx + 3), lane, b3);
+    region_sb_load<AMBRY_RUNS_NT != 0>(a, at(nx + 3), lane, b3);
     __builtin_amdgcn_s_setprio(0);
     const u32x4 v = *reinterpret_cast<const u32x4*>(buf + 4u * lane);
     u32x4* dst = 4u * lane < 64u * (end - g) ? reinterpret_cast<u32x4*>(a.rk + kRunPad + g * 64) + lane : spill;

@@ -584,7 +584,11 @@ __global__ __launch_bounds__(256) void region_long_kernel(MsgArgs a, RegionArgs 
   const unsigned long long ctr = __hip_atomic_load(g.lng.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t n = min((uint32_t)(ctr >> 32), g.lng.cap);
   if (n == 0) return;
-  const uint32_t total = g.lng.rec[n - 1].piece0 + g.lng.rec[n - 1].pieces;
+  // pieces of the listed records (the counter's low word counts those of unlisted ones too)
+  const uint32_t total = min(g.lng.rec[n - 1].piece0 + g.lng.rec[n - 1].pieces, (uint32_t)ctr);
+  const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+  const uint32_t w0 = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (blockIdx.x * (blockDim.x >> 6) >= total) return;  // no piece for this block
   __shared__ uint32_t tbl[1024];
   __shared__ uint32_t nib[region::kNibTotal];
   __shared__ uint32_t dn[region::kDirSets * region::kNibWords];
@@ -594,11 +598,8 @@ __global__ __launch_bounds__(256) void region_long_kernel(MsgArgs a, RegionArgs 
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t* rk = g.rk + kRunPad;
-  for (;;) {
-    uint32_t q = 0;
-    if (lane == 0) q = atomicAdd(g.lng.claim, 1u);
-    q = __builtin_amdgcn_readfirstlane(q);
-    if (q >= total) break;
+  // wave w takes pieces w, w + waves, ... (no claim counter: a static split)
+  for (uint32_t q = w0; q < total; q += waves) {
     uint32_t lo = 0, hi = n - 1;  // the last record with piece0 <= q
     while (lo < hi) {
       const uint32_t mid = (lo + hi + 1) / 2;
@@ -610,9 +611,9 @@ __global__ __launch_bounds__(256) void region_long_kernel(MsgArgs a, RegionArgs 
     const uint32_t p = q - lr.piece0, np = lr.pieces;
     const uint64_t s = len * p / np, e = len * (p + 1) / np;
     uint32_t c = region::record_crc_runs_wave(region::TabC{tbl}, nib, dn, g.base, rk, lr.pa + s, e - s, lane);
+    for (uint64_t d = len - e, k = 0; d; d >>= 1, ++k)  // c * x^(8(len - e)) (wave-uniform)
+      if (d & 1) c = gf2_mul(c, nib[region::kXpOff + k]);
     if (lane == 0) {
-      for (uint64_t d = len - e, k = 0; d; d >>= 1, ++k)  // c * x^(8(len - e))
-        if (d & 1) c = gf2_mul(c, nib[region::kXpOff + k]);
       atomicXor(&lr.acc, c);
       __threadfence();
       if (atomicAdd(&lr.done, 1u) == np - 1) {

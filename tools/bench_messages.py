@@ -174,7 +174,9 @@ def main():
     if args.no_gpu:
         return
     cases = {"64k": (65536, 64 << 10), "4m": (4096, 4 << 20), "4k": (262144, 4 << 10), "3k": (327680, 3 << 10),
-             "2k": (393216, 2 << 10), "1k": (524288, 1 << 10), "100": (1048576, 100)}
+             "2k": (393216, 2 << 10), "1k": (524288, 1 << 10), "100": (1048576, 100),
+             # 4 KiB blobs over smaller regions (~87 / 175 / 350 MB: inside / around the 256 MB MALL)
+             "4k16k": (16384, 4 << 10), "4k32k": (32768, 4 << 10), "4k64k": (65536, 4 << 10)}
     for m, s in (cases[c] for c in args.cases.split(",")):
         for v in [int(x) for x in args.variants.split(",")]:
             for mode in args.modes.split(","):

@@ -34,6 +34,9 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
+# message-verify regions: (messages, blob bytes); msg4k16k / 32k / 64k: 4 KiB blobs over ~87 / 175 / 350 MB
+MSG_CASES = {"msg4k": (262144, 4096), "msg3k": (262144, 3000), "msg1k": (524288, 1024), "msg100": (1048576, 100),
+             "msg4k16k": (16384, 4096), "msg4k32k": (32768, 4096), "msg4k64k": (65536, 4096)}
 SIZES = {"batch100": (100, 112), "batch1k": (1024, 1024), "batch4k": (4096, 4096), "batch4109": (4109, 4112),
          "batch2000": (2000, 2000), "batch3000": (3000, 3008), "batch16k": (16384, 16384)}
 
@@ -85,12 +88,10 @@ def main():
         for _ in range(args.reps):
             D.crc32_batch(buf, off, ln, out=out, workspace=ws)
         info.update(chunks=1, chunk_bytes=size, alg_bytes_per_launch=size + 4)
-    elif args.case.split("_")[0] in ("msg4k", "msg3k", "msg1k", "msg100") and \
-            args.case.split("_")[-1] in ("msg4k", "msg3k", "msg1k", "msg100", "2pass", "1pass", "jobs"):
+    elif args.case.split("_")[0] in MSG_CASES and args.case.split("_")[-1] in tuple(MSG_CASES) + ("2pass", "1pass", "jobs"):
         from bench_messages import gpu_region, load_mf
 
-        m, blob = {"msg3k": (262144, 3000), "msg1k": (524288, 1024),
-                   "msg100": (1048576, 100)}.get(args.case.split("_")[0], (262144, 4096))
+        m, blob = MSG_CASES[args.case.split("_")[0]]
         mode = "region" if args.case.endswith("_1pass") else "jobs" if args.case.endswith("_jobs") else "region2"
         res = gpu_region(load_mf(), m, blob, args.reps, mode=mode)
         info.update(res)
