@@ -268,10 +268,16 @@ void reap_retired_ws(DevCtx* c) {
 // (A destroyed stream's handle may be reused by a new stream; hipStreamDestroy drains the old
 // stream's work first, so the buffer is idle by then.)
 int stream_ws(DevCtx* c, hipStream_t s, size_t need, void** out, size_t* entry) {
-  reap_retired_ws(c);
+  // Under stream capture (a HIP graph) nothing here may query events, synchronize or allocate: a
+  // capture uses the stream's buffer as an earlier uncaptured call sized it, or gets EINVAL.
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cap) != hipSuccess) return AMBRYCRC_EHIP;
+  const bool capturing = cap != hipStreamCaptureStatusNone;
+  if (!capturing) reap_retired_ws(c);
   DevCtx::StreamWs* w = nullptr;
   for (auto& e : c->ws_list)
     if (e.stream == s) w = &e;
+  if (capturing && (!w || w->bytes < need)) return AMBRYCRC_EINVAL;
   if (!w && c->ws_list.size() >= kMaxStreamWs) {
     // evict the least recently used stream's buffer: retired behind its last call's event
     // (the entry's event moves with it), the entry reused for s
@@ -411,11 +417,12 @@ int host_cpu_threads() {
 
 double host_cpu_gibps() {
   static const double per_thread = [] {
-    std::vector<uint8_t> buf(4u << 20);
+    // 32 MiB: past a CCD's L3, so the rate is the DRAM-fed one the host entries see (~2 ms once)
+    std::vector<uint8_t> buf(32u << 20);
     for (size_t i = 0; i < buf.size(); ++i) buf[i] = (uint8_t)(i * 131u + 7u);
     double best = 1e30;
     volatile uint32_t sink = 0;
-    for (int r = 0; r < 3; ++r) {
+    for (int r = 0; r < 2; ++r) {
       const auto t0 = std::chrono::steady_clock::now();
       sink = sink ^ ambrycrc_update(0, buf.data(), buf.size());
       best = std::min(best, std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());

@@ -161,7 +161,7 @@ struct DevCtx {
 int hip_err(hipError_t e);
 // Host-resident dispatch: the CPU threads the CPU leg uses (AMBRYCRC_CPU_THREADS, else
 // OMP_NUM_THREADS, else the CPUs this process may run on) and their combined CRC rate in GiB/s
-// (measured once per process on a 4 MiB buffer, x threads x 0.85).
+// (measured once per process on a 32 MiB buffer, x threads x 0.85).
 int host_cpu_threads();
 double host_cpu_gibps();
 // True when a host call over `bytes` of host memory should take the CPU leg (device < 0, the

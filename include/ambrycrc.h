@@ -26,7 +26,9 @@
  * enqueues on the caller's stream. With d_ws == NULL a call uses the default
  * workspace of its stream (one per stream, so calls on different streams never
  * share one); a caller workspace (ambrycrc_workspace_bytes) must not be used by
- * two calls whose work overlaps.
+ * two calls whose work overlaps. Under stream capture (a HIP graph) a call with
+ * d_ws == NULL uses its stream's default workspace as an earlier uncaptured call
+ * on that stream sized it, and returns AMBRYCRC_EINVAL if that is too small.
  */
 #ifndef AMBRYCRC_H
 #define AMBRYCRC_H
@@ -397,7 +399,7 @@ int ambrycrc_batch_host(const void* const* ptrs, const uint64_t* lens, const uin
  * StoreMessageReadSet.java:170-188) hold exactly such host buffers. */
 int ambrycrc_set_host_policy(int device, int policy);
 /* The rates the auto policy compares: *cpu_gibps (CPU threads x per-thread CLMUL rate measured once
- * per process x 0.85), *gpu_gibps (the GPU host path: 51 GiB/s measured, refreshed by each pageable
+ * per process over 32 MiB x 0.85), *gpu_gibps (the GPU host path: 51 GiB/s measured, refreshed by each pageable
  * GPU call of >= 64 MiB), *cpu_threads (AMBRYCRC_CPU_THREADS, else OMP_NUM_THREADS, else this
  * process's CPUs). Returns the leg auto takes for pageable bytes (0 CPU, 1 GPU), or < 0. Any
  * output may be NULL. */

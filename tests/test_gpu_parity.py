@@ -618,7 +618,9 @@ def test_shutdown_and_reinit(gpu, oracle):
     assert lib().ambrycrc_batch_host((ctypes.c_void_p * 1)(mem.ctypes.data), (ctypes.c_uint64 * 1)(10), None,
                                      (ctypes.c_uint32 * 1)(), 1, 0, 0) == -4  # ENOINIT
     gpu.init(0)
+    gpu.set_host_policy(0, gpu.HOST_GPU)  # a new context starts at the auto policy (conftest's gpu fixture)
     assert gpu.crc32_batch_host(chunks) == before == list(oracle.batch(mem, [5, 0], [3 << 20, 1000]))
+    assert gpu.last_host_path(0) == 1
 
 
 def test_timing_with_host_paths(gpu, oracle):

@@ -45,6 +45,7 @@ def main():
 
     torch.cuda.set_device(0)
     D.init(0)
+    D.set_host_policy(0, D.HOST_GPU)  # the GPU host path itself (the auto policy may pick the CPU leg)
     L = lib()
     total = args.mib << 20
     chunk = args.chunk_kib << 10

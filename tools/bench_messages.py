@@ -140,6 +140,7 @@ def host_region_rate(D, region, base, m, L):
 
     host = region.cpu().numpy()
     offs = base.cpu().numpy().astype(np.uint64)
+    D.set_host_policy(0, D.HOST_GPU)  # the GPU host path itself (the auto policy may pick the CPU leg)
     out = {}
     for name, src, pinned in (("pageable", host, False), ("pinned", None, True)):
         if pinned:
