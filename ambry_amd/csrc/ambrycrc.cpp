@@ -1108,6 +1108,16 @@ uint32_t fused_proc_waves(const DevCtx* c, size_t m, bool copy) {
   return (uint32_t)std::min(p, most);
 }
 
+// The long-record list in the job arrays' space (unused in region mode), `bytes` long: records from
+// byte 64 (at most 4,096), then the piece slots.
+static void set_long_list(LongList& l, uint8_t* w, size_t bytes) {
+  l.rec = reinterpret_cast<LongRec*>(w + 64);
+  l.cap = (uint32_t)std::min<size_t>(4096, (bytes - 64) / 2 / sizeof(LongRec));
+  const size_t sb = (64 + l.cap * sizeof(LongRec) + 255) & ~size_t(255);
+  l.slot = reinterpret_cast<uint32_t*>(w + sb);
+  l.pcap = (uint32_t)std::min<size_t>(1u << 30, (bytes - sb) / sizeof(uint32_t));
+}
+
 int enqueue_messages(DevCtx* c, const uint8_t* d_region, uint64_t region_len, const uint64_t* d_msg_off, size_t m,
                      uint32_t* d_status, uint64_t* d_msg_end, void* d_ws, size_t ws_bytes, hipStream_t stream) {
   const bool region = c->region_mode && region_len > 0 && region_len <= c->region_max * (uint64_t)m &&
@@ -1145,8 +1155,7 @@ int enqueue_messages(DevCtx* c, const uint8_t* d_region, uint64_t region_len, co
     uint8_t* lw = static_cast<uint8_t*>(d_ws);
     r.lng.ctr = reinterpret_cast<unsigned long long*>(lw);
     r.lng.claim = reinterpret_cast<uint32_t*>(lw + 8);
-    r.lng.rec = reinterpret_cast<LongRec*>(lw + 64);
-    r.lng.cap = (uint32_t)std::min<size_t>(4096, (msg_jobs_bytes(m) - 64) / sizeof(LongRec));
+    set_long_list(r.lng, lw, msg_jobs_bytes(m));
     if (launch_region_runs(r, c->grid, stream) != hipSuccess ||
         launch_region_msg(st.a, r, c->num_cu, stream) != hipSuccess)
       return AMBRYCRC_EHIP;
@@ -1159,7 +1168,12 @@ int enqueue_messages(DevCtx* c, const uint8_t* d_region, uint64_t region_len, co
   f.ctl = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(st.batch_ws) + region_rk_bytes(d_region, region_len));
   f.defer = f.ctl + 64;
   f.nproc = fused_proc_waves(c, m, false);
-  if (hipMemsetAsync(f.ctl, 0, 8, stream) != hipSuccess) return AMBRYCRC_EHIP;
+  // long records: listed by the processors (records in the job arrays' space, as the two-pass
+  // form's; the counters in ctl, zeroed with it), taken by region_long_kernel after the tail
+  f.g.lng.ctr = reinterpret_cast<unsigned long long*>(f.ctl + 4);
+  f.g.lng.claim = f.ctl + 6;
+  set_long_list(f.g.lng, static_cast<uint8_t*>(d_ws), msg_jobs_bytes(m));
+  if (hipMemsetAsync(f.ctl, 0, 32, stream) != hipSuccess) return AMBRYCRC_EHIP;
   return hip_err(launch_region_fused(f, c->num_cu, stream));
 }
 

@@ -115,27 +115,33 @@ constexpr int kDiagNoFold = 100;  // diagnostic timing build, selectable via amb
 // region_runs_kernel), then one thread per message parses it and assembles its record CRCs from
 // the runs they cover (message_kernels.hip region_msg_kernel, region_crc.h). Runs are [base + 64k, base + 64k + 64) with
 // base = the region's start rounded down to 64 B; only 16-B pieces holding region bytes are read.
-// A record of more than region::kLongRuns runs (a multi-MiB blob among small messages) that
-// region_msg_kernel leaves to region_long_kernel: that kernel splits it into pieces of about
-// kLongPiece bytes over the whole grid -- each piece's zlib CRC by one wave from the run sums,
-// shifted to the record's end (crc(A||B) = crc(A) x^(8|B|) + crc(B)) and XORed into acc; the wave
-// that finishes the last piece compares acc with the stored CRC.
+// A record of more than region::kLongRuns runs (a multi-MiB blob among small messages) that the
+// region kernels leave to region_long_kernel: that kernel splits it into kLongPiece-byte pieces
+// over the whole grid, each piece's zlib CRC by one wave from the run sums into slot[piece0 + p];
+// region_long_combine_kernel then folds a record's pieces in order (crc(A||B) = crc(A) x^(8|B|) +
+// crc(B); x^(8 kLongPiece) from the LDS nibble sets) and compares.
 struct LongRec {
   uint64_t pa;       // base-relative start
   uint64_t msg;      // message index
   uint32_t len, ex;  // record length, stored CRC
   uint32_t bit;      // the status bit of its record slot
   uint32_t piece0;   // its first piece in the list's numbering
-  uint32_t pieces;
-  uint32_t acc, done;
+  uint32_t pieces;   // 0: not listed (the slots ran out; the caller took the record)
+  uint32_t pad;
 };
 struct LongList {
   LongRec* rec = nullptr;              // [cap]
   unsigned long long* ctr = nullptr;   // records << 32 | pieces, one atomic (piece0 ascending with the index)
   uint32_t* claim = nullptr;           // (zeroed with ctr; reserved)
-  uint32_t cap = 0;                    // records the list holds (more: the old per-wave queue)
+  uint32_t cap = 0;                    // records the list holds (more: the caller's own path)
+  uint32_t* slot = nullptr;            // [pcap] piece CRCs
+  uint32_t pcap = 0;
 };
-constexpr uint64_t kLongPiece = 256u << 10;
+// Records of more pieces than this stay with their caller (the combine is one wave's Horner chain).
+constexpr uint32_t kLongMaxPieces = 4096;
+// Pieces of 64 KiB (x^(8*65536) is the nibble set record_crc_runs_wave folds its streams by): a
+// 4 MiB blob is 64 waves' work.
+constexpr uint64_t kLongPiece = 64u << 10;
 
 struct RegionArgs {
   const uint8_t* base;   // region start rounded down to 64 B
@@ -339,8 +345,8 @@ hipError_t launch_trailer_verify(const TrailerArgs& a, hipStream_t s);
 hipError_t launch_msg_parse(const MsgArgs& a, hipStream_t s);
 // Region mode, pass 2: parse, record CRCs from the run sums, status (a.job_* / expected / crc unused).
 hipError_t launch_region_msg(const MsgArgs& a, const RegionArgs& g, int num_cu, hipStream_t s);
-// Region mode, after pass 2: the long records of g.lng, split over the whole grid (returns at once
-// when there are none).
+// Region mode, after pass 2 (or the one-pass tail): the long records of g.lng, split over the whole
+// grid, then combined (two kernels; both return at once when there are none).
 hipError_t launch_region_long(const MsgArgs& a, const RegionArgs& g, int num_cu, hipStream_t s);
 hipError_t launch_msg_reduce(const MsgArgs& a, hipStream_t s);
 

@@ -1929,7 +1929,7 @@ __global__ __launch_bounds__(256) void region_tail_kernel(FusedArgs f) {
       const uint64_t i = all ? w : f.defer[w];
       uint32_t st;
       uint64_t mend;
-      region::process_message_direct(f.a, f.g, tbl, nib, dn, i, lane, st, mend);
+      region::process_message_direct(f.a, f.g, tbl, nib, dn, i, lane, st, mend, COPY ? nullptr : &f.g.lng);
       if constexpr (COPY) region::transform_fast(f, tbl, lane == 0, i, st, mend);
     }
     return;
@@ -1996,6 +1996,10 @@ hipError_t launch_region_fused(const FusedArgs& f, int num_cu, hipStream_t s) {
   if (blocks > (uint64_t)num_cu * 4) blocks = (uint64_t)num_cu * 4;
   if (copy) hipLaunchKernelGGL(region_tail_kernel<true>, dim3((uint32_t)blocks), dim3(256), 0, s, f);
   else hipLaunchKernelGGL(region_tail_kernel<false>, dim3((uint32_t)blocks), dim3(256), 0, s, f);
+  if (!copy && f.g.lng.ctr) {  // the long records the tail listed, over the whole grid
+    const hipError_t e = launch_region_long(f.a, f.g, num_cu, s);
+    if (e != hipSuccess) return e;
+  }
   if (copy && (f.life || f.path_out)) {
     uint64_t pb = f.life ? (f.a.m + 255) / 256 : 1;
     if (pb > (uint64_t)num_cu * 8) pb = (uint64_t)num_cu * 8;

@@ -143,24 +143,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AMBRY_REGIO
       const uint32_t jl = slot[4 * k + 2], ex = slot[4 * k + 3];
       const uint64_t pa = g.reg0 + jo;
       if (jl && (int64_t)((((pa + jl + 63) & ~uint64_t(63)) - (pa & ~uint64_t(63))) >> 6) > region::kLongRuns) {
-        if (g.lng.ctr) {  // to region_long_kernel: the whole grid takes it, piece by piece
-          const uint32_t pieces = (uint32_t)((jl + kLongPiece - 1) / kLongPiece);
-          const unsigned long long was = atomicAdd(g.lng.ctr, (1ull << 32) | pieces);
-          const uint32_t at = (uint32_t)(was >> 32);
-          if (at < g.lng.cap) {
-            LongRec& lr = g.lng.rec[at];
-            lr.pa = pa;
-            lr.msg = i;
-            lr.len = jl;
-            lr.ex = ex;
-            lr.bit = AMBRYCRC_MSG_ENCKEY_CRC << k;
-            lr.piece0 = (uint32_t)was;
-            lr.pieces = pieces;
-            lr.acc = 0;
-            lr.done = 0;
-            continue;
-          }
-        }
+        // to region_long_kernel (the whole grid takes it, piece by piece) unless the list is full
+        if (g.lng.ctr && region::list_long(g.lng, pa, jl, ex, i, AMBRYCRC_MSG_ENCKEY_CRC << k)) continue;
         const uint32_t at = atomicAdd(&lq_n[wv], 1u);
         if (at < kLongQ) {  // the wave's, after the loop (its bit ORed into the status then)
           lq_jo[wv][at] = pa;
@@ -573,22 +557,24 @@ hipError_t launch_region_msg(const MsgArgs& a, const RegionArgs& g, int num_cu, 
   return hipGetLastError();
 }
 
-// The long records region_msg_kernel listed (LongList): a piece is handed out per wave round by one
-// atomic; the record holding piece q is found by a search of the ascending piece0; its zlib CRC
-// comes from record_crc_runs_wave over the piece's bytes [s, e), is shifted by x^(8(len - e)) to the
-// record's end (x^(8*2^k) words, gf2_mul) and XORed into acc. The wave that finishes a record's last
-// piece reads acc back (every XOR was made before its done increment) and flags a mismatch.
-// (Before: one wave walked each whole record after its messages -- ~100 us per 4 MiB blob, which
-// ended the kernel long after the rest; tools/probes/long_mix.py.)
-__global__ __launch_bounds__(256) void region_long_kernel(MsgArgs a, RegionArgs g) {
+// The long records the region kernels listed (LongList), piece by piece: wave w hashes pieces w,
+// w + waves, ... (a static split; a claim loop through one atomic counter hung a two-pass verify on
+// the GPU), each from the run sums (record_crc_runs_wave) into its slot. No atomics on a record's
+// words: 64 waves updating one record's accumulator and counter serialized at L2 (28 us for eight
+// 4 MiB blobs; tools/probes/long_mix.py).
+__device__ __forceinline__ uint32_t long_count(const RegionArgs& g, uint32_t* total) {
   const unsigned long long ctr = __hip_atomic_load(g.lng.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t n = min((uint32_t)(ctr >> 32), g.lng.cap);
-  if (n == 0) return;
-  // pieces of the listed records (the counter's low word counts those of unlisted ones too)
-  const uint32_t total = min(g.lng.rec[n - 1].piece0 + g.lng.rec[n - 1].pieces, (uint32_t)ctr);
+  *total = n ? min(g.lng.rec[n - 1].piece0 + g.lng.rec[n - 1].pieces, min((uint32_t)ctr, g.lng.pcap)) : 0u;
+  return n;
+}
+
+__global__ __launch_bounds__(256) void region_long_kernel(MsgArgs a, RegionArgs g) {
+  uint32_t total;
+  const uint32_t n = long_count(g, &total);
   const uint32_t waves = gridDim.x * (blockDim.x >> 6);
   const uint32_t w0 = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (blockIdx.x * (blockDim.x >> 6) >= total) return;  // no piece for this block
+  if (n == 0 || blockIdx.x * (blockDim.x >> 6) >= total) return;  // no piece for this block
   __shared__ uint32_t tbl[1024];
   __shared__ uint32_t nib[region::kNibTotal];
   __shared__ uint32_t dn[region::kDirSets * region::kNibWords];
@@ -598,36 +584,68 @@ __global__ __launch_bounds__(256) void region_long_kernel(MsgArgs a, RegionArgs 
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t* rk = g.rk + kRunPad;
-  // wave w takes pieces w, w + waves, ... (no claim counter: a static split)
   for (uint32_t q = w0; q < total; q += waves) {
-    uint32_t lo = 0, hi = n - 1;  // the last record with piece0 <= q
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi + 1) / 2;
-      if (g.lng.rec[mid].piece0 <= q) lo = mid;
-      else hi = mid - 1;
+    // the last record with piece0 <= q: 64 records a probe, one ballot each (one round trip for
+    // up to 64 records)
+    uint32_t lo = 0;
+    for (uint32_t b = 0; b < n; b += 64) {
+      const uint32_t r = b + lane;
+      const uint64_t ball = __ballot(r < n && g.lng.rec[r].piece0 <= q);
+      if (ball == 0) break;
+      lo = b + 63u - (uint32_t)__builtin_clzll(ball);
+      if (ball != ~0ull) break;
     }
-    LongRec& lr = g.lng.rec[lo];
-    const uint64_t len = lr.len;
-    const uint32_t p = q - lr.piece0, np = lr.pieces;
-    const uint64_t s = len * p / np, e = len * (p + 1) / np;
-    uint32_t c = region::record_crc_runs_wave(region::TabC{tbl}, nib, dn, g.base, rk, lr.pa + s, e - s, lane);
-    for (uint64_t d = len - e, k = 0; d; d >>= 1, ++k)  // c * x^(8(len - e)) (wave-uniform)
-      if (d & 1) c = gf2_mul(c, nib[region::kXpOff + k]);
-    if (lane == 0) {
-      atomicXor(&lr.acc, c);
-      __threadfence();
-      if (atomicAdd(&lr.done, 1u) == np - 1) {
-        __threadfence();
-        const uint32_t crc = atomicOr(&lr.acc, 0u);
-        if (crc != lr.ex) atomicOr(&a.status[lr.msg], lr.bit);
-      }
+    lo = __builtin_amdgcn_readfirstlane(lo);
+    const LongRec& lr = g.lng.rec[lo];
+    const uint32_t p = q - lr.piece0;
+    if (p >= lr.pieces) continue;  // a record listed empty
+    const uint64_t s = (uint64_t)p * kLongPiece, e = min((uint64_t)lr.len, s + kLongPiece);
+    const uint32_t c = region::record_crc_runs_wave(region::TabC{tbl}, nib, dn, g.base, rk, lr.pa + s, e - s, lane);
+    if (lane == 0) g.lng.slot[q] = c;
+  }
+}
+
+// One wave per listed record: its pieces folded in order -- acc = acc x^(8 kLongPiece) + crc(piece)
+// (the x^(8*65536) nibble set), the last piece's length by the x^(8*2^k) words -- and compared.
+__global__ __launch_bounds__(256) void region_long_combine_kernel(MsgArgs a, RegionArgs g) {
+  uint32_t total;
+  const uint32_t n = long_count(g, &total);
+  const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+  const uint32_t w0 = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (n == 0 || blockIdx.x * (blockDim.x >> 6) >= n) return;
+  __shared__ uint32_t nib[region::kNibTotal];
+  __shared__ uint32_t dn[region::kDirSets * region::kNibWords];
+  region::stage_nib(nib, a.img);
+  region::stage_direct_nib(dn, a.img);
+  __syncthreads();
+  for (uint32_t r = w0; r < n; r += waves) {
+    const LongRec& lr = g.lng.rec[r];
+    const uint32_t np = lr.pieces;
+    if (np == 0) continue;
+    const uint32_t* sl = g.lng.slot + lr.piece0;
+    const uint32_t lane = threadIdx.x & 63u;
+    // Horner over the slots, 64 at a time: each lane loads one slot, the wave takes them in turn
+    uint32_t acc = 0;
+    for (uint32_t b = 0; b + 1 < np; b += 64) {
+      const uint32_t v = b + lane + 1 < np ? sl[b + lane] : 0u;  // pieces 0 .. np-2 (the last apart)
+      const uint32_t cnt = min(64u, np - 1 - b);
+      for (uint32_t j = 0; j < cnt; ++j)
+        acc = region::nmul(dn, acc, region::kDirStream) ^ (uint32_t)__builtin_amdgcn_readlane((int)v, (int)j);
     }
+    if (np > 1) {
+      const uint64_t last = (uint64_t)lr.len - (uint64_t)(np - 1) * kLongPiece;  // 1 .. kLongPiece
+      for (uint64_t d = last, k = 0; d; d >>= 1, ++k)  // acc x^(8 last)
+        if (d & 1) acc = gf2_mul(acc, nib[region::kXpOff + k]);
+    }
+    acc ^= sl[np - 1];
+    if ((threadIdx.x & 63u) == 0 && acc != lr.ex) atomicOr(&a.status[lr.msg], lr.bit);
   }
 }
 
 hipError_t launch_region_long(const MsgArgs& a, const RegionArgs& g, int num_cu, hipStream_t s) {
   if (a.m == 0 || !g.lng.ctr) return hipSuccess;
   hipLaunchKernelGGL(region_long_kernel, dim3((uint32_t)num_cu * 2), dim3(256), 0, s, a, g);
+  hipLaunchKernelGGL(region_long_combine_kernel, dim3((uint32_t)num_cu), dim3(256), 0, s, a, g);
   return hipGetLastError();
 }
 

@@ -331,5 +331,26 @@ __device__ __forceinline__ uint32_t record_crc(const uint32_t* __restrict__ t, c
   return record_crc(TabC{t}, nib, base, rk, pa, len);
 }
 
+// Appends a long record to the grid-wide list (region_long_kernel, message_kernels.hip); false when
+// the list is full (the caller then takes the record itself).
+__device__ __forceinline__ bool list_long(const LongList& l, uint64_t pa, uint64_t len, uint32_t ex, uint64_t msg,
+                                          uint32_t bit) {
+  const uint32_t pieces = (uint32_t)((len + kLongPiece - 1) / kLongPiece);
+  if (pieces > kLongMaxPieces) return false;
+  const unsigned long long was = atomicAdd(l.ctr, (1ull << 32) | pieces);
+  const uint32_t at = (uint32_t)(was >> 32);
+  if (at >= l.cap) return false;
+  const bool room = (uint64_t)(uint32_t)was + pieces <= l.pcap;
+  LongRec& lr = l.rec[at];
+  lr.pa = pa;
+  lr.msg = msg;
+  lr.len = (uint32_t)len;
+  lr.ex = ex;
+  lr.bit = bit;
+  lr.piece0 = (uint32_t)was;
+  lr.pieces = room ? pieces : 0;  // no slots left: listed empty, taken by the caller
+  return room;
+}
+
 }  // namespace region
 }  // namespace ambrycrc

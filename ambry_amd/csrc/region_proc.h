@@ -147,7 +147,8 @@ __device__ __forceinline__ uint32_t record_crc_direct(const TabC& tc, const uint
 __device__ __forceinline__ void process_message_direct(const MsgArgs& a, const RegionArgs& g,
                                                        const uint32_t* __restrict__ t, const uint32_t* __restrict__ nib,
                                                        const uint32_t* __restrict__ dn, uint64_t i, uint32_t lane,
-                                                       uint32_t& st_ret, uint64_t& end_ret) {
+                                                       uint32_t& st_ret, uint64_t& end_ret,
+                                                       const LongList* lng = nullptr) {
   const uint32_t* rk = g.rk + kRunPad;
   const uint64_t off = a.msg_off[i];
   const bool in_region = off <= a.region_len;
@@ -174,6 +175,11 @@ __device__ __forceinline__ void process_message_direct(const MsgArgs& a, const R
     if (jl == 0) continue;
     const uint64_t pa = g.reg0 + jo;
     const int64_t runs = (int64_t)((((pa + jl + 63) & ~uint64_t(63)) - (pa & ~uint64_t(63))) >> 6);
+    if (runs > kLongRuns && lng && lng->ctr) {  // a multi-MiB record: the whole grid's, after this kernel
+      bool ok = false;
+      if (lane == 0) ok = list_long(*lng, pa, jl, ex, i, record_bit(k));
+      if (__builtin_amdgcn_readfirstlane((uint32_t)ok)) continue;
+    }
     const uint32_t c = runs > kLongRuns ? record_crc_runs_wave(tc, nib, dn, g.base, rk, pa, jl, lane)
                                         : record_crc_direct(tc, nib, dn, g, pa, jl, lane);
     if (c != ex) status |= record_bit(k);
