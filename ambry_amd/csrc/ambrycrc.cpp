@@ -87,6 +87,43 @@ std::vector<uint32_t> build_table_image() {
       for (int x = 0; x < 16; ++x) img[(kImgInvOff + kNibSetBytes * k + 64u * n + 4u * x) / 4] = nt[n][x];
     inv = gf2_mul(inv, inv);
   }
+  // region pass 2's words (crc32_layout.h kImgRegOff)
+  uint32_t* reg = img.data() + kImgRegOff / 4;
+  for (uint32_t lo = 0; lo < 64; ++lo) {
+    const uint32_t ni = 64 - lo < 4 ? 64 - lo : 4;
+    uint32_t r = 0;
+    for (uint32_t i = 0; i < 64; ++i) r = t[0][(r ^ (i >= lo && i < lo + ni ? 0xFFu : 0u)) & 0xFFu] ^ (r >> 8);
+    reg[kRegH0 + lo] = r;
+  }
+  for (uint32_t a = 0; a <= 4; ++a) {
+    reg[kRegGe + a] = a < 4 ? 0xFFFFFFFFu << (8 * a) : 0u;
+    reg[kRegLt + a] = a < 4 ? (1u << (8 * a)) - 1u : 0xFFFFFFFFu;
+  }
+  {
+    uint32_t nt[8][16];
+    nibble_tables(host_xpow8(256), nt);
+    for (uint32_t j = 0; j < 4; ++j)
+      for (uint32_t b = 0; b < 256; ++b)
+        reg[kRegAuxWords + 256 * j + b] = nt[2 * j][b & 15] ^ nt[2 * j + 1][b >> 4];
+  }
+  {
+    uint32_t inv8 = kOne;  // x^-8
+    for (int i = 0; i < 8; ++i) inv8 = (inv8 & 0x80000000u) ? (((inv8 ^ kPoly) << 1) | 1u) : (inv8 << 1);
+    uint32_t inv64 = kOne;
+    for (int i = 0; i < 8; ++i) inv64 = gf2_mul(inv64, inv8);
+    uint32_t u0 = kOne, u1 = kOne;  // x^(-8 d0), x^(-64 d1)
+    for (uint32_t d = 0; d < 8; ++d) {
+      uint32_t nt[8][16];
+      nibble_tables(u0, nt);
+      for (int n = 0; n < 8; ++n)
+        for (int x = 0; x < 16; ++x) reg[kRegAuxWords + kRegByteWords + 128u * d + 16u * n + x] = nt[n][x];
+      nibble_tables(u1, nt);
+      for (int n = 0; n < 8; ++n)
+        for (int x = 0; x < 16; ++x) reg[kRegAuxWords + kRegByteWords + 128u * (8 + d) + 16u * n + x] = nt[n][x];
+      u0 = gf2_mul(u0, inv8);
+      u1 = gf2_mul(u1, inv64);
+    }
+  }
   return img;
 }
 

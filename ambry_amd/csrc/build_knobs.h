@@ -19,10 +19,13 @@
 #define AMBRY_REGION_WPE 2
 #endif
 #ifndef AMBRY_REGION_BPC_SMALL  // the same for regions of <= 1.5 KiB per message
-#define AMBRY_REGION_BPC_SMALL 3
+#define AMBRY_REGION_BPC_SMALL 2
 #endif
 #ifndef AMBRY_REGION_BPC  // region pass 2: blocks per CU (0: one thread per message)
 #define AMBRY_REGION_BPC 2
+#endif
+#ifndef AMBRY_REGION_AUX  // region pass 2's LDS helpers (region_crc.h Aux): 1 = LDS byte masks + H0, 2 = x^(8*256)
+#define AMBRY_REGION_AUX 7  // byte tables for the Horner steps, 4 = two-multiply un-shift
 #endif
 #ifndef AMBRY_FUSED_PROC  // one-pass region verify: processor waves per workgroup (0: per call)
 #define AMBRY_FUSED_PROC 0
@@ -89,7 +92,7 @@
 // X(name, default) for every knob above: ambrycrc_version() reports those that differ.
 #define AMBRY_KNOB_LIST(X)                                                                                  \
   X(AMBRY_PROPS_WIN, 96) X(AMBRY_PARSE_BPC, 2) X(AMBRY_REGION_WPE, 2) X(AMBRY_REGION_BPC, 2)                  \
-  X(AMBRY_REGION_BPC_SMALL, 3)                                                                              \
+  X(AMBRY_REGION_BPC_SMALL, 2) X(AMBRY_REGION_AUX, 7)                                                                          \
   X(AMBRY_FUSED_PROC, 0)                                                                                      \
   X(AMBRY_FUSED_WAVES_VERIFY, 12)                                                                               \
   X(AMBRY_FUSED_WAVES_COPY, 8) X(AMBRY_FUSED_NT, 1)                                                                 \

@@ -118,8 +118,8 @@ constexpr int kDiagNoFold = 100;  // diagnostic timing build, selectable via amb
 // A record of more than region::kLongRuns runs (a multi-MiB blob among small messages) that the
 // region kernels leave to region_long_kernel: that kernel splits it into kLongPiece-byte pieces
 // over the whole grid, each piece's zlib CRC by one wave from the run sums into slot[piece0 + p];
-// region_long_combine_kernel then folds a record's pieces in order (crc(A||B) = crc(A) x^(8|B|) +
-// crc(B); x^(8 kLongPiece) from the LDS nibble sets) and compares.
+// the wave that finishes a record's last piece (done counts them) folds its pieces (crc(A||B) =
+// crc(A) x^(8|B|) + crc(B): a tree over the lanes by x^(8 kLongPiece 2^k)) and compares.
 struct LongRec {
   uint64_t pa;       // base-relative start
   uint64_t msg;      // message index
@@ -127,7 +127,7 @@ struct LongRec {
   uint32_t bit;      // the status bit of its record slot
   uint32_t piece0;   // its first piece in the list's numbering
   uint32_t pieces;   // 0: not listed (the slots ran out; the caller took the record)
-  uint32_t pad;
+  uint32_t done;     // pieces hashed (region_long_kernel; list_long zeroes it)
 };
 struct LongList {
   LongRec* rec = nullptr;              // [cap]
@@ -137,7 +137,7 @@ struct LongList {
   uint32_t* slot = nullptr;            // [pcap] piece CRCs
   uint32_t pcap = 0;
 };
-// Records of more pieces than this stay with their caller (the combine is one wave's Horner chain).
+// Records of more pieces than this stay with their caller (the combine: one wave, 64 pieces a round).
 constexpr uint32_t kLongMaxPieces = 4096;
 // Pieces of 64 KiB (x^(8*65536) is the nibble set record_crc_runs_wave folds its streams by): a
 // 4 MiB blob is 64 waves' work.

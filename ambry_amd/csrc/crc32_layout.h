@@ -35,7 +35,18 @@ static_assert(kPowOff + kPowTables * kNibSetBytes < 65536u, "nibble offsets must
 // region_crc.h).
 constexpr uint32_t kImgInvOff = kLdsBytes + 256u;
 constexpr uint32_t kInvPowSets = 6;
-constexpr uint32_t kImgBytes = kImgInvOff + kInvPowSets * kNibSetBytes;
+// Then region pass 2's words (region_crc.h Aux, staged by region_msg_kernel): H0[lo] (64 words:
+// the raw register at a 64-B run's end of 0xFF in bytes [lo, lo + min(64 - lo, 4)), i.e. the
+// initial register of a record starting at run offset lo, by linearity), GE[a] = the bytes >= a
+// of a word and LT[b] = the bytes < b (a, b = 0..4; 8 words each), then the byte tables of
+// x^(8*256): B[256j + b] = (b << 8j) * x^(8*256), j = 0..3, then 16 nibble sets for the final
+// un-shift by x^(-8d), d = 0..63, in two multiplies: x^(-8 d0) (d0 = 0..7), then x^(-64 d1).
+constexpr uint32_t kImgRegOff = kImgInvOff + kInvPowSets * kNibSetBytes;
+constexpr uint32_t kRegH0 = 0, kRegGe = 64, kRegLt = 72, kRegAuxWords = 80;
+constexpr uint32_t kRegByteWords = 1024;
+constexpr uint32_t kRegUnSets = 16, kRegUnWords = kRegUnSets * (kNibSetBytes / 4);
+constexpr uint32_t kRegWords = kRegAuxWords + kRegByteWords + kRegUnWords;
+constexpr uint32_t kImgBytes = kImgRegOff + 4u * kRegWords;
 
 constexpr uint32_t kBlockBytes = 1024;  // one wave-wide 16 B/lane load
 constexpr uint32_t kWaveLanes = 64;

@@ -94,7 +94,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AMBRY_REGIO
   __shared__ uint32_t tbl[1024];
   __shared__ uint32_t pwin[256 * kPropsSlotWords];
   __shared__ uint32_t nib[region::kNibTotal];
-  __shared__ uint32_t dn[region::kDirSets * region::kNibWords];
+  __shared__ uint32_t hm[kRegAuxWords], bt[kRegByteWords], un[kRegUnWords];
   // Long records (more than region::kLongRuns runs: a 4 MiB blob among small messages) are queued
   // per wave and taken by the whole wave after its messages (record_crc_runs_wave): one thread
   // walking 65,536 run sums would hold the kernel for milliseconds.
@@ -103,9 +103,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AMBRY_REGIO
   __shared__ uint32_t lq_jl[4][kLongQ], lq_ex[4][kLongQ], lq_bit[4][kLongQ], lq_n[4];
   stage_slice_tables(tbl, a.img);
   region::stage_nib(nib, a.img);
-  region::stage_direct_nib(dn, a.img);
+  region::stage_aux(hm, bt, un, a.img);
   if (threadIdx.x < 4) lq_n[threadIdx.x] = 0;
   __syncthreads();
+  const region::Aux aux{hm, bt, un};
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   uint32_t* slot = pwin + threadIdx.x * kPropsSlotWords;
   const uint32_t* rk = g.rk + kRunPad;
@@ -158,14 +159,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AMBRY_REGIO
 #if AMBRY_REGION_PROBE == 1
       const uint32_t c = ex;
 #else
-      const uint32_t c = jl ? region::record_crc(region::TabC{tbl}, nib, g.base, rk, pa, jl) : 0u;
+      const uint32_t c = jl ? region::record_crc(region::TabC{tbl}, nib, g.base, rk, pa, jl, aux) : 0u;
 #endif
       if (c != ex) status |= AMBRYCRC_MSG_ENCKEY_CRC << k;
     }
     a.status[i] = status;
     if (a.msg_end) a.msg_end[i] = end ? off + end : 0;
   }
-  // the wave's long records (the loop above ended in every lane: the wave is whole again)
+  // the waves' long records (the loop above ended in every thread; the list was full): the direct
+  // nibble sets staged over the properties windows, which no thread uses any more
+  static_assert(region::kDirSets * region::kNibWords <= 256 * kPropsSlotWords, "dn fits the windows");
+  __syncthreads();
+  if ((lq_n[0] | lq_n[1] | lq_n[2] | lq_n[3]) == 0) return;
+  uint32_t* dn = pwin;
+  region::stage_direct_nib(dn, a.img);
+  __syncthreads();
   const uint32_t nq = min(__builtin_amdgcn_readfirstlane(lq_n[wv]), kLongQ);
   for (uint32_t q = 0; q < nq; ++q) {
     const uint64_t pa = lq_jo[wv][q];
@@ -559,14 +567,68 @@ hipError_t launch_region_msg(const MsgArgs& a, const RegionArgs& g, int num_cu, 
 
 // The long records the region kernels listed (LongList), piece by piece: wave w hashes pieces w,
 // w + waves, ... (a static split; a claim loop through one atomic counter hung a two-pass verify on
-// the GPU), each from the run sums (record_crc_runs_wave) into its slot. No atomics on a record's
-// words: 64 waves updating one record's accumulator and counter serialized at L2 (28 us for eight
-// 4 MiB blobs; tools/probes/long_mix.py).
+// the GPU), each from the run sums (record_crc_runs_wave) into its slot, then counts it in the
+// record's done word (release: fence, then the add); the wave that counts the last piece folds the
+// record (acquire: fence after the add) -- no wave waits on another. Round 5's first form kept a
+// per-record accumulator that 64 waves XORed into (28 us for eight 4 MiB blobs; then a second
+// kernel folded each record in a 63-step Horner chain, 12.5 us).
 __device__ __forceinline__ uint32_t long_count(const RegionArgs& g, uint32_t* total) {
   const unsigned long long ctr = __hip_atomic_load(g.lng.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t n = min((uint32_t)(ctr >> 32), g.lng.cap);
   *total = n ? min(g.lng.rec[n - 1].piece0 + g.lng.rec[n - 1].pieces, min((uint32_t)ctr, g.lng.pcap)) : 0u;
   return n;
+}
+
+// POW[k] = x^(8*2^k) nibble sets, k = 0..kLongPow-1, staged by region_long_kernel: the tree over
+// 64 KiB pieces (k = 16..21), the fold over rounds of 64 pieces (22) and the last piece's length
+// (0..16).
+constexpr uint32_t kLongPow = 23;
+
+// A record's CRC from its piece CRCs sl[0 .. np-1] (pieces 0 .. np-2 of kLongPiece bytes, the last
+// of `last`), by the whole wave: the full pieces in rounds of 64 aligned so that piece np-2 is lane
+// 63's, folded in-lane by x^(8*2^22) over the rounds, merged by the DPP tree (lane l takes lane
+// l - 2^k's value times x^(8*2^(16+k))), then lane 63's register shifted by the last piece's length
+// and the last piece's CRC added.
+__device__ __forceinline__ uint32_t long_fold(const uint32_t* __restrict__ sl, uint32_t np, uint64_t last,
+                                              const uint32_t* __restrict__ pw, uint32_t lane) {
+  const uint32_t M = np - 1;  // full pieces
+  uint32_t acc = 0;
+  if (M) {
+    const uint32_t V = (M + 63) / 64;
+    for (uint32_t v = 0; v < V; ++v) {
+      const int64_t j = (int64_t)64 * v + lane - ((int64_t)64 * V - M);
+      const uint32_t x = j >= 0 ? sl[j] : 0u;
+      acc = (v ? region::nmul(pw, acc, 22) : 0u) ^ x;
+    }
+    {
+      const uint32_t pt = region::left_partner<0>(acc);
+      if (lane & 1u) acc ^= region::nmul(pw, pt, 16);
+    }
+    {
+      const uint32_t pt = region::left_partner<1>(acc);
+      if (lane & 2u) acc ^= region::nmul(pw, pt, 17);
+    }
+    {
+      const uint32_t pt = region::left_partner<2>(acc);
+      if (lane & 4u) acc ^= region::nmul(pw, pt, 18);
+    }
+    {
+      const uint32_t pt = region::left_partner<3>(acc);
+      if (lane & 8u) acc ^= region::nmul(pw, pt, 19);
+    }
+    {
+      const uint32_t pt = region::left_partner<4>(acc);
+      if (lane & 16u) acc ^= region::nmul(pw, pt, 20);
+    }
+    {
+      const uint32_t pt = region::left_partner<5>(acc);
+      if (lane & 32u) acc ^= region::nmul(pw, pt, 21);
+    }
+    acc = (uint32_t)__builtin_amdgcn_readlane((int)acc, 63);
+    for (uint32_t k = 0; k <= 16; ++k)  // acc x^(8 last), last = 1 .. kLongPiece (wave-uniform)
+      if ((last >> k) & 1u) acc = region::nmul(pw, acc, k);
+  }
+  return acc ^ sl[np - 1];
 }
 
 __global__ __launch_bounds__(256) void region_long_kernel(MsgArgs a, RegionArgs g) {
@@ -578,9 +640,12 @@ __global__ __launch_bounds__(256) void region_long_kernel(MsgArgs a, RegionArgs 
   __shared__ uint32_t tbl[1024];
   __shared__ uint32_t nib[region::kNibTotal];
   __shared__ uint32_t dn[region::kDirSets * region::kNibWords];
+  __shared__ uint32_t pw[kLongPow * region::kNibWords];
   stage_slice_tables(tbl, a.img);
   region::stage_nib(nib, a.img);
   region::stage_direct_nib(dn, a.img);
+  for (uint32_t i = threadIdx.x; i < kLongPow * region::kNibWords; i += blockDim.x)
+    pw[i] = a.img[(kNibBase + kPowOff) / 4 + i];  // POW[k] sets are consecutive, kNibWords apart
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t* rk = g.rk + kRunPad;
@@ -596,56 +661,29 @@ __global__ __launch_bounds__(256) void region_long_kernel(MsgArgs a, RegionArgs 
       if (ball != ~0ull) break;
     }
     lo = __builtin_amdgcn_readfirstlane(lo);
-    const LongRec& lr = g.lng.rec[lo];
-    const uint32_t p = q - lr.piece0;
-    if (p >= lr.pieces) continue;  // a record listed empty
+    LongRec& lr = g.lng.rec[lo];
+    const uint32_t p = q - lr.piece0, np = lr.pieces;
+    if (p >= np) continue;  // a record listed empty
     const uint64_t s = (uint64_t)p * kLongPiece, e = min((uint64_t)lr.len, s + kLongPiece);
     const uint32_t c = region::record_crc_runs_wave(region::TabC{tbl}, nib, dn, g.base, rk, lr.pa + s, e - s, lane);
-    if (lane == 0) g.lng.slot[q] = c;
-  }
-}
-
-// One wave per listed record: its pieces folded in order -- acc = acc x^(8 kLongPiece) + crc(piece)
-// (the x^(8*65536) nibble set), the last piece's length by the x^(8*2^k) words -- and compared.
-__global__ __launch_bounds__(256) void region_long_combine_kernel(MsgArgs a, RegionArgs g) {
-  uint32_t total;
-  const uint32_t n = long_count(g, &total);
-  const uint32_t waves = gridDim.x * (blockDim.x >> 6);
-  const uint32_t w0 = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (n == 0 || blockIdx.x * (blockDim.x >> 6) >= n) return;
-  __shared__ uint32_t nib[region::kNibTotal];
-  __shared__ uint32_t dn[region::kDirSets * region::kNibWords];
-  region::stage_nib(nib, a.img);
-  region::stage_direct_nib(dn, a.img);
-  __syncthreads();
-  for (uint32_t r = w0; r < n; r += waves) {
-    const LongRec& lr = g.lng.rec[r];
-    const uint32_t np = lr.pieces;
-    if (np == 0) continue;
-    const uint32_t* sl = g.lng.slot + lr.piece0;
-    const uint32_t lane = threadIdx.x & 63u;
-    // Horner over the slots, 64 at a time: each lane loads one slot, the wave takes them in turn
-    uint32_t acc = 0;
-    for (uint32_t b = 0; b + 1 < np; b += 64) {
-      const uint32_t v = b + lane + 1 < np ? sl[b + lane] : 0u;  // pieces 0 .. np-2 (the last apart)
-      const uint32_t cnt = min(64u, np - 1 - b);
-      for (uint32_t j = 0; j < cnt; ++j)
-        acc = region::nmul(dn, acc, region::kDirStream) ^ (uint32_t)__builtin_amdgcn_readlane((int)v, (int)j);
+    uint32_t prev = 0;
+    if (lane == 0) {
+      g.lng.slot[q] = c;
+      __threadfence();  // the slot before the count
+      prev = atomicAdd(&lr.done, 1u);
     }
-    if (np > 1) {
-      const uint64_t last = (uint64_t)lr.len - (uint64_t)(np - 1) * kLongPiece;  // 1 .. kLongPiece
-      for (uint64_t d = last, k = 0; d; d >>= 1, ++k)  // acc x^(8 last)
-        if (d & 1) acc = gf2_mul(acc, nib[region::kXpOff + k]);
-    }
-    acc ^= sl[np - 1];
-    if ((threadIdx.x & 63u) == 0 && acc != lr.ex) atomicOr(&a.status[lr.msg], lr.bit);
+    prev = __builtin_amdgcn_readfirstlane(prev);
+    if (prev + 1 != np) continue;
+    __threadfence();  // every other piece's slot after its count
+    const uint64_t last = (uint64_t)lr.len - (uint64_t)(np - 1) * kLongPiece;  // 1 .. kLongPiece
+    const uint32_t crc = long_fold(g.lng.slot + lr.piece0, np, last, pw, lane);
+    if (lane == 0 && crc != lr.ex) atomicOr(&a.status[lr.msg], lr.bit);
   }
 }
 
 hipError_t launch_region_long(const MsgArgs& a, const RegionArgs& g, int num_cu, hipStream_t s) {
   if (a.m == 0 || !g.lng.ctr) return hipSuccess;
   hipLaunchKernelGGL(region_long_kernel, dim3((uint32_t)num_cu * 2), dim3(256), 0, s, a, g);
-  hipLaunchKernelGGL(region_long_combine_kernel, dim3((uint32_t)num_cu), dim3(256), 0, s, a, g);
   return hipGetLastError();
 }
 

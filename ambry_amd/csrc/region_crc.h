@@ -141,6 +141,68 @@ __device__ __forceinline__ void stage_nib(uint32_t* __restrict__ nib, const uint
   }
 }
 
+// Pass 2's extra LDS words (crc32_layout.h kImgRegOff; region_msg_kernel stages them): hm = H0,
+// GE, LT (kRegAuxWords), bt = the byte tables of x^(8*256). NoAux: nibble forms only (the
+// one-pass processors, whose LDS holds the streamers' replicated tables).
+struct NoAux {
+  static constexpr bool kOn = false, kMask = false, kByte = false, kUn = false;
+  const uint32_t* hm = nullptr;
+  const uint32_t* bt = nullptr;
+  const uint32_t* un = nullptr;
+};
+struct Aux {
+  static constexpr bool kOn = true, kMask = (AMBRY_REGION_AUX & 1) != 0, kByte = (AMBRY_REGION_AUX & 2) != 0,
+                        kUn = (AMBRY_REGION_AUX & 4) != 0;
+  const uint32_t* __restrict__ hm;
+  const uint32_t* __restrict__ bt;
+  const uint32_t* __restrict__ un;  // un-shift sets: x^(-8 d0) (0..7), x^(-64 d1) (8..15)
+};
+
+// The image's kRegWords region words into hm, bt and un (the caller syncs).
+__device__ __forceinline__ void stage_aux(uint32_t* __restrict__ hm, uint32_t* __restrict__ bt,
+                                          uint32_t* __restrict__ un, const uint32_t* __restrict__ img) {
+  const uint32_t* src = img + kImgRegOff / 4;
+  for (uint32_t i = threadIdx.x; i < kRegWords; i += blockDim.x) {
+    if (i < kRegAuxWords)
+      hm[i] = src[i];
+    else if (i < kRegAuxWords + kRegByteWords)
+      bt[i - kRegAuxWords] = src[i];
+    else
+      un[i - kRegAuxWords - kRegByteWords] = src[i];
+  }
+}
+
+// v * x^(8*256) from the byte tables: four lookups (byte-indexed, one VALU address each) where
+// the nibble sets take eight.
+__device__ __forceinline__ uint32_t bmul(const uint32_t* __restrict__ bt, uint32_t v) {
+  return bt[v & 0xffu] ^ bt[256 + ((v >> 8) & 0xffu)] ^ bt[512 + ((v >> 16) & 0xffu)] ^ bt[768 + (v >> 24)];
+}
+
+// hash_run with each word's byte mask read from LDS -- LT / GE at the byte offset clamped into
+// the word, one v_med3 and one broadcast read per mask -- in place of the compares and shifts of
+// keep_ge / keep_lt (about half of a record's VALU work in pass 2), and without the initial-register
+// bytes: the caller XORs H0[lo] (the raw register is linear in the bytes). LO0: bytes from 0 (tail
+// runs, no GE mask).
+template <bool LO0, class Tab>
+__device__ __forceinline__ uint32_t hash_run_m(const Tab& t, const uint32_t* __restrict__ nib,
+                                               const uint32_t* __restrict__ hm, const u32x4 (&w)[4], int lo, int hi) {
+  const int lo4 = 4 * lo, hi4 = 4 * hi;
+  uint32_t p[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t s = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const int c = 16 * (4 * q + d);  // 4 x the word's first byte offset
+      uint32_t v = w[q][d] & hm[kRegLt + ((min(max(hi4, c), c + 16) - c) >> 2)];
+      if (!LO0) v &= hm[kRegGe + ((min(max(lo4, c), c + 16) - c) >> 2)];
+      s = t.step4(s ^ v);
+    }
+    p[q] = s;
+  }
+  return nmul(nib, nmul(nib, p[0], kP16) ^ p[1], kP32) ^ nmul(nib, p[2], kP16) ^ p[3];
+}
+
 // Four run groups (16 run sums) from group g on, as 16-B loads; groups past ng are not read.
 __device__ __forceinline__ void load_groups(const uint32_t* __restrict__ rk, int64_t e0, int64_t g, int64_t ng,
                                             u32x4 (&r)[4]) {
@@ -157,10 +219,11 @@ __device__ __forceinline__ void load_groups(const uint32_t* __restrict__ rk, int
 // zlib CRC-32 of the len bytes at offset pa from base; rk = RegionArgs::rk + kRunPad. Every load
 // is issued before the first is used (head and tail runs, the first 16 run sums), and each
 // Horner step group prefetches the next 16 sums.
-template <class Tab>
+// X = Aux: head / tail runs by hash_run_m plus H0[lo], Horner steps by the byte tables.
+template <class Tab, class X = NoAux>
 __device__ __forceinline__ uint32_t record_crc(const Tab& t, const uint32_t* __restrict__ nib,
                                                const uint8_t* __restrict__ base, const uint32_t* __restrict__ rk,
-                                               uint64_t pa, uint64_t len) {
+                                               uint64_t pa, uint64_t len, const X& x = X{}) {
   if (len == 0) return 0;
   const uint64_t pb = pa + len;
   if (len < 4) {
@@ -174,29 +237,44 @@ __device__ __forceinline__ uint32_t record_crc(const Tab& t, const uint32_t* __r
   const int tin = hi - lo;
   const bool tail_bytes = n >= 2 && (pb & 63u) != 0;
   const int thi = (int)(pb - (B1 - 64));
-  const int64_t ng = (n + 3) >> 2, e0 = k0 + n - 4 * ng, elast = k0 + n - 1;
+  const int64_t ng = (n + 3) >> 2, e0 = k0 + n - 4 * ng;
   u32x4 hw[4], tw[4], nxt[4];
   load_run(base, A0, lo, hi, hw);
   load_run(base, B1 - 64, 0, tail_bytes ? thi : 0, tw);
   load_groups(rk, e0, 0, ng, nxt);
-  uint32_t H = hash_run(t, nib, hw, lo, hi, tin < 4 ? tin : 4);
+  uint32_t H, T;
+  if constexpr (X::kMask) {
+    H = hash_run_m<false>(t, nib, x.hm, hw, lo, hi) ^ x.hm[kRegH0 + lo];
+    T = tail_bytes ? hash_run_m<true>(t, nib, x.hm, tw, 0, thi) : 0u;
+  } else {
+    H = hash_run(t, nib, hw, lo, hi, tin < 4 ? tin : 4);
+    T = tail_bytes ? hash_run(t, nib, tw, 0, thi, 0) : 0u;
+  }
   if (tin < 4) H ^= 0xFFFFFFFFu >> (8 * tin);
-  const uint32_t T = tail_bytes ? hash_run(t, nib, tw, 0, thi, 0) : 0u;
-  // Horner over runs k0 .. k0+n-1 in groups of four ending at the last run.
+  // Horner over runs k0 .. k0+n-1 in groups of four ending at the last run. The head run and the
+  // first group's padding (runs before k0, zero) are patched into group 0's sums once; the tail
+  // run enters with factor 1 (it is the last), so the raw sum the loop folds in is swapped for T
+  // after it. The loop itself is four lookups and four XORs per run.
+  const int32_t n32 = (int32_t)n, ng32 = (int32_t)ng, rb = n32 - 4 * ng32;  // rb: -3..0
+  const uint32_t rlast = tail_bytes ? rk[k0 + n - 1] : 0u;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) nxt[0][q] = rb + q < 0 ? 0u : rb + q == 0 ? H : nxt[0][q];
   uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;  // s3: the stream updated last
-  for (int64_t g = 0; g < ng; g += 4) {
+  for (int32_t g = 0; g < ng32; g += 4) {
     u32x4 r[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) r[u] = nxt[u];
-    if (g + 4 < ng) load_groups(rk, e0, g + 4, ng, nxt);
+    if (g + 4 < ng32) load_groups(rk, e0, g + 4, ng, nxt);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      if (g + u < ng) {
+      if (g + u < ng32) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const int64_t e = e0 + 4 * (g + u) + q;
-          const uint32_t v = e < k0 ? 0u : e == k0 ? H : (e == elast && tail_bytes) ? T : r[u][q];
-          const uint32_t nv = nmul(nib, s0, kP256) ^ v;
+          uint32_t nv;
+          if constexpr (X::kByte)
+            nv = bmul(x.bt, s0) ^ r[u][q];
+          else
+            nv = nmul(nib, s0, kP256) ^ r[u][q];
           s0 = s1;
           s1 = s2;
           s2 = s3;
@@ -205,11 +283,18 @@ __device__ __forceinline__ uint32_t record_crc(const Tab& t, const uint32_t* __r
       }
     }
   }
-  uint32_t V = s3 ^ nmul(nib, s2, kP64) ^ nmul(nib, s1, kP128) ^ nmul(nib, nmul(nib, s0, kP64), kP128);
+  s3 ^= T ^ rlast;
+  // streams merged by x^(8*64) (s0 * x^(8*192) ^ s1 * x^(8*128) ^ s2 * x^(8*64) ^ s3), then the
+  // register at B1 un-shifted to pb
+  uint32_t V = s3 ^ nmul(nib, s2 ^ nmul(nib, s1 ^ nmul(nib, s0, kP64), kP64), kP64);
   const uint32_t d = (uint32_t)(B1 - pb);
+  if constexpr (X::kUn) {
+    V = nmul(x.un, nmul(x.un, V, d & 7u), 8u + (d >> 3));
+  } else {
 #pragma unroll
-  for (uint32_t k = 0; k < kInvPowSets; ++k)
-    if (d & (1u << k)) V = nmul(nib, V, kInv0 + k);
+    for (uint32_t k = 0; k < kInvPowSets; ++k)
+      if (d & (1u << k)) V = nmul(nib, V, kInv0 + k);
+  }
   return ~V;
 }
 
@@ -349,6 +434,7 @@ __device__ __forceinline__ bool list_long(const LongList& l, uint64_t pa, uint64
   lr.bit = bit;
   lr.piece0 = (uint32_t)was;
   lr.pieces = room ? pieces : 0;  // no slots left: listed empty, taken by the caller
+  lr.done = 0;
   return room;
 }
 

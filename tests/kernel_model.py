@@ -24,7 +24,11 @@ K_POW_TABLES = 36
 K_LDS_BYTES = K_NIB_BASE + K_POW_OFF + K_POW_TABLES * K_NIB_SET
 K_IMG_INV_OFF = K_LDS_BYTES + 256  # nibble sets of x^(-8*2^k), k = 0..5 (crc32_layout.h)
 K_INV_SETS = 6
-K_IMG_BYTES = K_IMG_INV_OFF + K_INV_SETS * K_NIB_SET
+K_IMG_REG_OFF = K_IMG_INV_OFF + K_INV_SETS * K_NIB_SET  # region pass 2's words (crc32_layout.h)
+K_REG_H0, K_REG_GE, K_REG_LT, K_REG_AUX = 0, 64, 72, 80
+K_REG_BYTE = 1024
+K_REG_UN = 16 * (K_NIB_SET // 4)
+K_IMG_BYTES = K_IMG_REG_OFF + 4 * (K_REG_AUX + K_REG_BYTE + K_REG_UN)
 BLOCK = 1024
 LANES = np.arange(64, dtype=np.uint32)
 
@@ -492,6 +496,91 @@ class RegionModel:
                 V = self.inv(V, k)
         return V ^ 0xFFFFFFFF
 
+
+    def job_crc_aux(self, mem: bytes, reg0: int, rk, off: int, ln: int) -> int:
+        """record_crc with region_msg_kernel's Aux words (region_crc.h): head / tail runs masked by
+        the image's GE / LT words and no initial-register bytes, H0[lo] XORed into the head run,
+        group 0 patched (padding zero, head run H), Horner by the x^(8*256) byte tables with the
+        raw last-run sum swapped for T afterwards, streams merged by x^(8*64) three times, and the
+        un-shift as x^(-8 (d & 7)) then x^(-64 (d >> 3)) from the 16 un-shift sets."""
+        if ln == 0:
+            return 0
+        if ln < 4:
+            return self.job_crc(mem, reg0, rk, off, ln)
+        reg = self.img[K_IMG_REG_OFF // 4:]
+        bt = reg[K_REG_AUX:K_REG_AUX + K_REG_BYTE]
+        un = K_IMG_REG_OFF + 4 * (K_REG_AUX + K_REG_BYTE)
+
+        def bmul(v):
+            return int(bt[v & 0xFF] ^ bt[256 + ((v >> 8) & 0xFF)] ^ bt[512 + ((v >> 16) & 0xFF)] ^ bt[768 + (v >> 24)])
+
+        def masked(buf, r0, lo, hi):
+            p = []
+            for q in range(4):
+                s = 0
+                for d in range(4):
+                    w = 4 * q + d
+                    c = 16 * w
+                    v = int.from_bytes(buf[r0 + 4 * w:r0 + 4 * w + 4], "little")
+                    v &= int(reg[K_REG_LT + (min(max(4 * hi, c), c + 16) - c) // 4])
+                    v &= int(reg[K_REG_GE + (min(max(4 * lo, c), c + 16) - c) // 4])
+                    s = self.step4(s ^ v)
+                p.append(s)
+            return self.pow_(self.pow_(p[0], 4) ^ p[1], 5) ^ self.pow_(p[2], 4) ^ p[3]
+
+        nruns = len(rk)
+        buf = bytes(reg0) + mem + bytes(nruns * 64 - reg0 - len(mem))
+        pa = reg0 + off
+        pb = pa + ln
+        A0, B1 = pa & ~63, (pb + 63) & ~63
+        n, k0 = (B1 - A0) >> 6, A0 >> 6
+        lo, hi = pa - A0, min(pb - A0, 64)
+        tin = hi - lo
+        tail = n >= 2 and pb & 63 != 0
+        H = masked(buf, A0, lo, hi) ^ int(reg[K_REG_H0 + lo])
+        if tin < 4:
+            H ^= 0xFFFFFFFF >> (8 * tin)
+        T = masked(buf, B1 - 64, 0, pb - (B1 - 64)) if tail else 0
+        ng = (n + 3) >> 2
+        e0 = k0 + n - 4 * ng
+        vals = [rk[e] if e >= 0 else 0 for e in range(e0, e0 + 4 * ng)]
+        rb = n - 4 * ng
+        for q in range(4):
+            vals[q] = 0 if rb + q < 0 else H if rb + q == 0 else vals[q]
+        s = [0, 0, 0, 0]
+        for v in vals:
+            s = [s[1], s[2], s[3], bmul(s[0]) ^ v]
+        if tail:
+            s[3] ^= T ^ rk[k0 + n - 1]
+        V = s[3] ^ self.pow_(s[2] ^ self.pow_(s[1] ^ self.pow_(s[0], 6), 6), 6)
+        d = B1 - pb
+        V = self._nib(self._nib(V, un + K_NIB_SET * (d & 7)), un + K_NIB_SET * (8 + (d >> 3)))
+        return V ^ 0xFFFFFFFF
+
+    def long_fold(self, sl, last: int) -> int:
+        """message_kernels.hip long_fold: a long record's CRC from its 64 KiB pieces' CRCs sl (the
+        last piece `last` bytes) -- full pieces in rounds of 64 lanes aligned so that the last full
+        piece is lane 63's, folded in-lane by POW[22] over rounds, the DPP tree (lane l takes lane
+        l - 2^k's value times POW[16 + k]; lane 63 read), x^(8 last), plus the last piece's CRC."""
+        np_ = len(sl)
+        M = np_ - 1
+        acc = 0
+        if M:
+            V = (M + 63) // 64
+            lanes = [0] * 64
+            for v in range(V):
+                for l in range(64):
+                    j = 64 * v + l - (64 * V - M)
+                    x = sl[j] if j >= 0 else 0
+                    lanes[l] = (self.pow_(lanes[l], 22) if v else 0) ^ x
+            for k in range(6):
+                lanes = [lanes[l] ^ self.pow_(lanes[l - (1 << k)], 16 + k) if l & (1 << k) else lanes[l]
+                         for l in range(64)]
+            acc = lanes[63]
+            for k in range(17):
+                if last >> k & 1:
+                    acc = self.pow_(acc, k)
+        return acc ^ sl[np_ - 1]
 
     def job_crc_wave(self, mem: bytes, reg0: int, rk, off: int, ln: int) -> int:
         """region_crc.h record_crc_runs_wave: a long record by the whole wave from the run sums --

@@ -117,6 +117,7 @@ def test_region_model_matches_zlib(ambry):
             if a + ln > len(mem):
                 continue
             assert rm.job_crc(mem, reg0, rk, a, ln) == zlib.crc32(mem[a:a + ln]), (reg0, a, ln)
+            assert rm.job_crc_aux(mem, reg0, rk, a, ln) == zlib.crc32(mem[a:a + ln]), (reg0, a, ln)
 
 
 def test_region_wave_model_matches_zlib(ambry):
@@ -171,3 +172,21 @@ def test_direct_record_model_matches_zlib(ambry):
     for reg0 in (0, 13):
         for a, ln in ((0, 4), (1, 5), (63, 64), (7, 65), (100, 1006), (33, 4109), (5, 4096), (9, 9000)):
             assert rm.direct_crc(mem, reg0, a, ln) == zlib.crc32(mem[a:a + ln]), (reg0, a, ln)
+
+
+def test_long_fold_model_matches_zlib(ambry):
+    """region_long_kernel's fold of a long record's 64 KiB piece CRCs (message_kernels.hip long_fold:
+    rounds of 64 lanes, the DPP tree by x^(8*2^(16+k)), the last piece's length) against zlib, for
+    1, 2, 64, 65 and 130 pieces and last pieces of 1 B, a few bytes and a full 64 KiB."""
+    import zlib
+
+    from kernel_model import RegionModel, table_image
+
+    rm = RegionModel(table_image())
+    P = 64 << 10
+    for npieces, last in ((1, 5), (2, 1), (2, P), (64, P), (65, 3), (130, 777)):
+        ln = (npieces - 1) * P + last
+        mem = stream_bytes(npieces * 31 + last, 0, ln).tobytes()
+        sl = [zlib.crc32(mem[i:i + P]) for i in range(0, ln, P)]
+        assert len(sl) == npieces
+        assert rm.long_fold(sl, last) == zlib.crc32(mem), (npieces, last)

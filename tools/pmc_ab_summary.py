@@ -7,8 +7,11 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 
+# kernels summarized (regex on the short name; KMATCH=region_ for the message verify kernels)
+KMATCH = os.environ.get("KMATCH", "sweep_kernel|group_kernel")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 src = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "pmc_ab")
 res = {}
@@ -18,7 +21,7 @@ for f in sorted(glob.glob(os.path.join(src, "*", "*", "p*.csv"))):
     rows = list(csv.DictReader(open(f)))
     for r in rows:
         k = r["Kernel_Name"].split("(")[0].split("<")[0].split("::")[-1]
-        if "sweep_kernel" not in k and "group_kernel" not in k:
+        if not re.search(KMATCH, k):
             continue
         per[(k, r["Dispatch_Id"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
