@@ -591,8 +591,9 @@ int ambrycrc_fill_random_dev(uint8_t* d_dst, uint64_t nbytes, uint64_t seed, uin
 int ambrycrc_debug_readbw_dev(const uint8_t* d_base, uint64_t nbytes, uint32_t* d_out, int variant,
                               hipStream_t stream);
 
-/* Copy of the table image (the LDS image kLdsBytes, 64 words x^(8*2^k), then the nibble sets
- * of x^(-8*2^k), k = 0..5: kImgBytes in all) into host memory `out` (for
+/* Copy of the table image (the LDS image kLdsBytes, 64 words x^(8*2^k), the nibble sets of
+ * x^(-8*2^k), k = 0..5, then region pass 2's words -- head-run initial registers, byte masks, the
+ * x^(8*256) byte tables and the un-shift sets: kImgBytes in all) into host memory `out` (for
  * tests that model the kernel on the CPU). Returns the byte size, or <0. */
 long ambrycrc_debug_table_image(uint32_t* out, size_t max_words);
 
