@@ -354,7 +354,8 @@ int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len
   } else {
     c->last_xform_path.store(0);
   }
-  if (hipMemsetAsync(fail, 0, sizeof(uint32_t), stream) != hipSuccess) return AMBRYCRC_EHIP;
+  // fail[0] is written only by the general path below; the fast path zeroed it with xfail
+  if (!fast && hipMemsetAsync(fail, 0, sizeof(uint32_t), stream) != hipSuccess) return AMBRYCRC_EHIP;
   p.gate = general;
   t.gate = general;
   t.gate_when = 1;

@@ -120,8 +120,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AMBRY_REGIO
     const uint64_t rem = in_region ? a.region_len - off : 0;
     const uint8_t* p = a.region + (in_region ? off : 0);
     const HeaderWords hw = load_header(p, rem);
-    uint32_t status;
+    uint32_t status = 0;
     uint64_t end;
+    // One record's CRC from the run sums (long records to region_long_kernel's list, else to the
+    // wave's queue), its bit into `status` on a mismatch.
+    auto take = [&](int k, uint64_t jo, uint64_t jl, uint32_t ex) {
+      const uint64_t pa = g.reg0 + jo;
+      if (jl && (int64_t)((((pa + jl + 63) & ~uint64_t(63)) - (pa & ~uint64_t(63))) >> 6) > region::kLongRuns) {
+        // to region_long_kernel (the whole grid takes it, piece by piece) unless the list is full
+        if (g.lng.ctr && region::list_long(g.lng, pa, jl, ex, i, AMBRYCRC_MSG_ENCKEY_CRC << k)) return;
+        const uint32_t at = atomicAdd(&lq_n[wv], 1u);
+        if (at < kLongQ) {  // the wave's, after the loop (its bit ORed into the status then)
+          lq_jo[wv][at] = pa;
+          lq_i[wv][at] = i;
+          lq_jl[wv][at] = (uint32_t)jl;
+          lq_ex[wv][at] = ex;
+          lq_bit[wv][at] = AMBRYCRC_MSG_ENCKEY_CRC << k;
+          return;
+        }
+      }
+#if AMBRY_REGION_PROBE == 1
+      const uint32_t c = ex;
+#else
+      const uint32_t c = jl ? region::record_crc(region::TabC{tbl}, nib, g.base, rk, pa, jl, aux) : 0u;
+#endif
+      if (c != ex) status |= AMBRYCRC_MSG_ENCKEY_CRC << k;
+    };
     {
       MsgParse r;
       parse_message<false>(off, in_region, rem, p, hw, tbl, slot, 0, r, pf, pf_ok);
@@ -139,30 +163,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AMBRY_REGIO
       end = r.end;
     }
     static_assert(4 * kMsgSlots <= kPropsSlotWords, "job slots fit the properties window");
-    for (int k = 0; k < kMsgSlots; ++k) {
-      const uint64_t jo = off + ((uint64_t)slot[4 * k + 1] << 32 | slot[4 * k]);
-      const uint32_t jl = slot[4 * k + 2], ex = slot[4 * k + 3];
-      const uint64_t pa = g.reg0 + jo;
-      if (jl && (int64_t)((((pa + jl + 63) & ~uint64_t(63)) - (pa & ~uint64_t(63))) >> 6) > region::kLongRuns) {
-        // to region_long_kernel (the whole grid takes it, piece by piece) unless the list is full
-        if (g.lng.ctr && region::list_long(g.lng, pa, jl, ex, i, AMBRYCRC_MSG_ENCKEY_CRC << k)) continue;
-        const uint32_t at = atomicAdd(&lq_n[wv], 1u);
-        if (at < kLongQ) {  // the wave's, after the loop (its bit ORed into the status then)
-          lq_jo[wv][at] = pa;
-          lq_i[wv][at] = i;
-          lq_jl[wv][at] = jl;
-          lq_ex[wv][at] = ex;
-          lq_bit[wv][at] = AMBRYCRC_MSG_ENCKEY_CRC << k;
-          continue;
-        }
-      }
-#if AMBRY_REGION_PROBE == 1
-      const uint32_t c = ex;
-#else
-      const uint32_t c = jl ? region::record_crc(region::TabC{tbl}, nib, g.base, rk, pa, jl, aux) : 0u;
-#endif
-      if (c != ex) status |= AMBRYCRC_MSG_ENCKEY_CRC << k;
-    }
+    for (int k = 0; k < kMsgSlots; ++k)
+      take(k, off + ((uint64_t)slot[4 * k + 1] << 32 | slot[4 * k]), slot[4 * k + 2], slot[4 * k + 3]);
     a.status[i] = status;
     if (a.msg_end) a.msg_end[i] = end ? off + end : 0;
   }
