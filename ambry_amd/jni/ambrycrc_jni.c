@@ -29,6 +29,9 @@
  *                               ByteBuffer out, long[] outLen)
  *   void nativeTransformMessages(ByteBuffer region, long[] offsets, short[] lifeVersions, int headerVersion,
  *                                ByteBuffer out, long[] outOffsets, long[] outLens, int[] status, int device)
+ *   int  nativeSetHostPolicy(int device, int policy)
+ *   int  nativeHostRates(int device, double[] out)
+ *   int  nativeLastHostPath(int device)
  * CRC values travel as Java ints holding the uint32 bit pattern.
  */
 #include <jni.h>
@@ -362,4 +365,36 @@ JNIEXPORT void JNICALL JNI_FN(nativeTransformMessages)(JNIEnv* env, jclass cls, 
   free(ol);
   free(st);
   raise(env, rc);
+}
+
+/* NativeCrc32.setHostPolicy: the host-resident dispatch policy of `device` (ambrycrc_set_host_policy:
+ * 0 auto, 1 GPU, 2 CPU); returns the previous one. */
+JNIEXPORT jint JNICALL JNI_FN(nativeSetHostPolicy)(JNIEnv* env, jclass cls, jint device, jint policy) {
+  (void)cls;
+  const int r = ambrycrc_set_host_policy(device, policy);
+  if (r < 0) return raise(env, r), -1;
+  return r;
+}
+
+/* NativeCrc32.hostRates: out[0] = the CPU leg's GiB/s, out[1] = the GPU host path's, out[2] = the CPU
+ * threads (ambrycrc_host_rates); returns the leg auto takes for pageable bytes (0 CPU, 1 GPU). */
+JNIEXPORT jint JNICALL JNI_FN(nativeHostRates)(JNIEnv* env, jclass cls, jint device, jdoubleArray out) {
+  (void)cls;
+  if (!out) return raise(env, AJC_ENULL), -1;
+  if ((*env)->GetArrayLength(env, out) < 3) return raise(env, AJC_ESHORT), -1;
+  double cpu = 0, gpu = 0;
+  int threads = 0;
+  const int r = ambrycrc_host_rates(device, &cpu, &gpu, &threads);
+  if (r < 0) return raise(env, r), -1;
+  const jdouble v[3] = {cpu, gpu, (jdouble)threads};
+  (*env)->SetDoubleArrayRegion(env, out, 0, 3, v);
+  return r;
+}
+
+/* NativeCrc32.lastHostPath: the leg `device`'s last host-resident call took (0 CPU, 1 GPU, -1 none). */
+JNIEXPORT jint JNICALL JNI_FN(nativeLastHostPath)(JNIEnv* env, jclass cls, jint device) {
+  (void)cls;
+  const int r = ambrycrc_last_host_path(device);
+  if (r < -1) return raise(env, r), -1;
+  return r;
 }

@@ -185,6 +185,36 @@ public final class NativeCrc32 implements Checksum {
     return regionBytes + (long) m * TRANSFORM_GROWTH_MAX;
   }
 
+  /** Host-resident dispatch policies (ambrycrc_set_host_policy): auto, always the GPU, always the CPU leg. */
+  public static final int HOST_AUTO = 0;
+  public static final int HOST_GPU = 1;
+  public static final int HOST_CPU = 2;
+
+  /**
+   * Sets how batch / verifyMessages / transformMessages on `device` run host-resident bytes (HOST_AUTO: the
+   * CPU leg for pageable bytes when its threads beat the GPU host path, see hostRates); returns the
+   * previous policy. Throws IllegalStateException for a device not initialised, IllegalArgumentException
+   * for an unknown policy.
+   */
+  public static int setHostPolicy(int device, int policy) {
+    return nativeSetHostPolicy(device, policy);
+  }
+
+  /**
+   * The rates HOST_AUTO compares on `device`: {CPU leg GiB/s, GPU host path GiB/s, CPU threads}
+   * (ambrycrc_host_rates).
+   */
+  public static double[] hostRates(int device) {
+    double[] out = new double[3];
+    nativeHostRates(device, out);
+    return out;
+  }
+
+  /** The leg `device`'s last host-resident call took: 0 the CPU, 1 the GPU, -1 none yet. */
+  public static int lastHostPath(int device) {
+    return nativeLastHostPath(device);
+  }
+
   /** AMBRYCRC_MSG_* status bits of verifyMessages (include/ambrycrc.h). */
   public static final int MSG_HEADER_CRC = 1;
   public static final int MSG_ENCKEY_CRC = 1 << 1;
@@ -227,4 +257,10 @@ public final class NativeCrc32 implements Checksum {
 
   private static native void nativeTransformMessages(ByteBuffer region, long[] offsets, short[] lifeVersions,
       int headerVersion, ByteBuffer out, long[] outOffsets, long[] outLens, int[] status, int device);
+
+  private static native int nativeSetHostPolicy(int device, int policy);
+
+  private static native int nativeHostRates(int device, double[] out);
+
+  private static native int nativeLastHostPath(int device);
 }

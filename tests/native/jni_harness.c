@@ -15,7 +15,7 @@
 
 #include "../../include/ambrycrc.h"
 
-enum Kind { K_CLASS, K_BYTES, K_INTS, K_LONGS, K_SHORTS, K_OBJS, K_BUFFER };
+enum Kind { K_CLASS, K_BYTES, K_INTS, K_LONGS, K_SHORTS, K_OBJS, K_BUFFER, K_DOUBLES };
 
 struct _jobject {
   enum Kind kind;
@@ -122,11 +122,16 @@ static jlong direct_capacity(JNIEnv* env, jobject b) {
   return b->kind == K_BUFFER && b->data ? b->len : -1;
 }
 
+static void set_double_region(JNIEnv* env, jdoubleArray a, jsize s, jsize n, const jdouble* buf) {
+  (void)env;
+  region_check(a, s, n);
+  memcpy((jdouble*)a->data + s, buf, (size_t)n * sizeof(jdouble));
+}
 static const struct JNINativeInterface_ g_fns = {
     find_class,         throw_new,       exception_check, delete_local_ref, get_method_id,
     call_int_method,    get_array_length, get_object_array_element, get_int_region, set_int_region,
     get_long_region,    set_long_region, get_short_region, get_critical,   release_critical,
-    direct_address,     direct_capacity,
+    direct_address,     direct_capacity, set_double_region,
 };
 static JNIEnv g_env = &g_fns;
 
@@ -223,6 +228,9 @@ static int msg_cases(const char* path) {
 }
 
 JNIEXPORT jint JNICALL FN(nativeChainMessages)(JNIEnv*, jclass, jobject, jlong, jlongArray);
+JNIEXPORT jint JNICALL FN(nativeSetHostPolicy)(JNIEnv*, jclass, jint, jint);
+JNIEXPORT jint JNICALL FN(nativeHostRates)(JNIEnv*, jclass, jint, jdoubleArray);
+JNIEXPORT jint JNICALL FN(nativeLastHostPath)(JNIEnv*, jclass, jint);
 
 static uint8_t* slurp(const char* path, size_t* n) {
   FILE* f = fopen(path, "rb");
@@ -384,6 +392,24 @@ static int gpu_cases(void) {
   report("gpu_verify_0", st[0]);
   report("gpu_verify_1", st[1]);
   report("gpu_verify_end", (jint)(ends[0] + ends[1]));
+  /* host-resident dispatch: the rates auto compares, then the batch above on each forced leg */
+  jdouble rates[3] = {0, 0, 0};
+  struct _jobject jrates = arr(K_DOUBLES, rates, 3);
+  report("gpu_rates_leg", FN(nativeHostRates)(&g_env, NULL, 0, &jrates));
+  report("gpu_rates_positive", rates[0] > 0 && rates[1] > 0 && rates[2] >= 1);
+  report("gpu_policy_bad", FN(nativeSetHostPolicy)(&g_env, NULL, 0, 7));
+  const jint prev = FN(nativeSetHostPolicy)(&g_env, NULL, 0, 2);
+  report("gpu_policy_cpu", prev >= 0 && prev <= 2);
+  out[0] = out[1] = out[2] = 0;
+  FN(nativeBatchDirect)(&g_env, NULL, &lst, &jpos, &jlen, &jcin, &jout, 0);
+  report("gpu_cpu_leg_batch_1", out[1]);
+  report("gpu_cpu_leg_path", FN(nativeLastHostPath)(&g_env, NULL, 0));
+  report("gpu_policy_gpu", FN(nativeSetHostPolicy)(&g_env, NULL, 0, 1));
+  out[0] = out[1] = out[2] = 0;
+  FN(nativeBatchDirect)(&g_env, NULL, &lst, &jpos, &jlen, &jcin, &jout, 0);
+  report("gpu_gpu_leg_batch_1", out[1]);
+  report("gpu_gpu_leg_path", FN(nativeLastHostPath)(&g_env, NULL, 0));
+  FN(nativeSetHostPolicy)(&g_env, NULL, 0, prev);
   return 0;
 }
 
@@ -474,6 +500,15 @@ int main(int argc, char** argv) {
   report("chain_heap", FN(nativeChainMessages)(&g_env, NULL, &heap_buf, 0, &jco));
   report("chain_negative", FN(nativeChainMessages)(&g_env, NULL, &direct_buf, -1, &jco));
   report("chain_none", FN(nativeChainMessages)(&g_env, NULL, &direct_buf, 0, &jco)); /* "123456789": no header */
+
+  /* host-resident dispatch policy: argument errors, and no context (no GPU initialised yet) */
+  jdouble rates[3] = {0, 0, 0};
+  struct _jobject jrates = arr(K_DOUBLES, rates, 3), jrates2 = arr(K_DOUBLES, rates, 2);
+  report("policy_no_context", FN(nativeSetHostPolicy)(&g_env, NULL, 0, 1));
+  report("rates_null", FN(nativeHostRates)(&g_env, NULL, 0, NULL));
+  report("rates_short", FN(nativeHostRates)(&g_env, NULL, 0, &jrates2));
+  report("rates_no_context", FN(nativeHostRates)(&g_env, NULL, 0, &jrates));
+  report("last_path_no_context", FN(nativeLastHostPath)(&g_env, NULL, 0));
 
   FN(nativeInit)(&g_env, NULL, 0); /* no GPU in the build container: the init error is thrown */
   report("init_no_gpu", 0);

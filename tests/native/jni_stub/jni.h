@@ -22,6 +22,7 @@ typedef int32_t jint;
 typedef int64_t jlong;
 typedef int8_t jbyte;
 typedef int16_t jshort;
+typedef double jdouble;
 typedef uint8_t jboolean;
 typedef jint jsize;
 
@@ -33,6 +34,7 @@ typedef jarray jbyteArray;
 typedef jarray jintArray;
 typedef jarray jlongArray;
 typedef jarray jshortArray;
+typedef jarray jdoubleArray;
 typedef jarray jobjectArray;
 typedef jobject jthrowable;
 struct _jmethodID;
@@ -59,6 +61,7 @@ struct JNINativeInterface_ {
   void (*ReleasePrimitiveArrayCritical)(JNIEnv* env, jarray array, void* carray, jint mode);
   void* (*GetDirectBufferAddress)(JNIEnv* env, jobject buf);
   jlong (*GetDirectBufferCapacity)(JNIEnv* env, jobject buf);
+  void (*SetDoubleArrayRegion)(JNIEnv* env, jdoubleArray array, jsize start, jsize len, const jdouble* buf);
 };
 
 #endif

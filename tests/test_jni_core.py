@@ -142,7 +142,7 @@ def test_jni_shim_against_fake_jvm(core, tmp_path):
     got = _run_harness(tmp_path)
     crc = lambda b: zlib.crc32(b)  # noqa: E731
     NPE, IOOBE = "java/lang/NullPointerException", "java/lang/IndexOutOfBoundsException"
-    IAE = "java/lang/IllegalArgumentException"
+    IAE, ISE = "java/lang/IllegalArgumentException", "java/lang/IllegalStateException"
     expect = {
         "array_full": (crc(b"123456789"), "-"), "array_tail": (crc(b"56789"), "-"),
         "array_bounds": (0x1234, IOOBE), "array_negative": (0x1234, IOOBE), "array_null": (0x1234, NPE),
@@ -155,6 +155,8 @@ def test_jni_shim_against_fake_jvm(core, tmp_path):
         "xform_null_out": (0, NPE), "xform_heap": (0, IAE),
         "xform_no_context": (0, "java/lang/IllegalStateException"),
         "chain_null": (0, NPE), "chain_heap": (0, IAE), "chain_negative": (0, IOOBE), "chain_none": (0, "-"),
+        "policy_no_context": (0xFFFFFFFF, ISE), "rates_null": (0xFFFFFFFF, NPE), "rates_short": (0xFFFFFFFF, IAE),
+        "rates_no_context": (0xFFFFFFFF, ISE), "last_path_no_context": (0xFFFFFFFF, ISE),
     }
     for name, want in expect.items():
         assert got[name] == want, name
@@ -174,6 +176,13 @@ def test_jni_shim_device_entries(core, tmp_path):
     assert got["gpu_batch_2"] == (zlib.crc32(b"89yy"), "-")
     assert got["gpu_verify_0"] == (1 << 8, "-") and got["gpu_verify_1"] == (1 << 8, "-")
     assert got["gpu_verify_end"] == (0, "-")
+    # host-resident dispatch (nativeSetHostPolicy / nativeHostRates / nativeLastHostPath)
+    assert got["gpu_rates_leg"] in ((0, "-"), (1, "-")) and got["gpu_rates_positive"] == (1, "-")
+    assert got["gpu_policy_bad"] == (0xFFFFFFFF, "java/lang/IllegalArgumentException")
+    assert got["gpu_policy_cpu"] == (1, "-")
+    assert got["gpu_cpu_leg_batch_1"] == (zlib.crc32(b"456"), "-") and got["gpu_cpu_leg_path"] == (0, "-")
+    assert got["gpu_policy_gpu"] == (2, "-")
+    assert got["gpu_gpu_leg_batch_1"] == (zlib.crc32(b"456"), "-") and got["gpu_gpu_leg_path"] == (1, "-")
 
 
 def test_jni_shim_message_entries(core, tmp_path):
