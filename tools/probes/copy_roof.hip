@@ -1,0 +1,76 @@
+// copy_roof.hip -- probe: device-to-device copy bandwidth on this GPU for the transform's size
+// (1.39 GB region -> separate output): hipMemcpyAsync, and a grid-stride 16-B-per-lane kernel with
+// plain / nontemporal loads and stores at a few unroll depths. Prints JSON lines (GB/s of read +
+// write). Build: hipcc -O3 --offload-arch=gfx950 -o copy_roof tools/probes/copy_roof.hip
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <int U, bool NTL, bool NTS>
+__global__ __launch_bounds__(256) void copy_k(const u32x4* __restrict__ src, u32x4* __restrict__ dst, size_t n) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + (U - 1) * stride < n; i += U * stride) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = NTL ? __builtin_nontemporal_load(src + i + u * stride) : src[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (NTS) __builtin_nontemporal_store(v[u], dst + i + u * stride);
+      else dst[i + u * stride] = v[u];
+    }
+  }
+  for (; i < n; i += stride) dst[i] = src[i];
+}
+
+#define CK(e) do { hipError_t r_ = (e); if (r_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(r_), __LINE__); exit(1); } } while (0)
+
+template <int U, bool NTL, bool NTS>
+static void run(const char* name, const u32x4* s, u32x4* d, size_t n, int grid, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+  float best = 1e9, sum = 0;
+  const int reps = 10;
+  for (int r = 0; r < reps + 2; ++r) {
+    CK(hipEventRecord(e0, st));
+    hipLaunchKernelGGL((copy_k<U, NTL, NTS>), dim3(grid), dim3(256), 0, st, s, d, n);
+    CK(hipEventRecord(e1, st));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    if (r >= 2) { sum += ms; if (ms < best) best = ms; }
+  }
+  const double bytes = 2.0 * n * 16;
+  printf("{\"copy\": \"%s\", \"grid\": %d, \"ms_avg\": %.4f, \"GBps_avg\": %.1f, \"GBps_best\": %.1f}\n", name, grid,
+         sum / reps, bytes / (sum / reps) / 1e6, bytes / best / 1e6);
+}
+
+int main() {
+  const size_t bytes = 1389101056;  // 262,144 x 4 KiB PUT messages (bench_put.py's transform case)
+  const size_t n = bytes / 16;
+  u32x4 *s, *d;
+  CK(hipMalloc(&s, bytes)); CK(hipMalloc(&d, bytes));
+  CK(hipMemset(s, 1, bytes)); CK(hipMemset(d, 0, bytes));
+  hipStream_t st; CK(hipStreamCreate(&st));
+  hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  {
+    float sum = 0;
+    for (int r = 0; r < 12; ++r) {
+      CK(hipEventRecord(e0, st));
+      CK(hipMemcpyAsync(d, s, bytes, hipMemcpyDeviceToDevice, st));
+      CK(hipEventRecord(e1, st));
+      CK(hipEventSynchronize(e1));
+      float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+      if (r >= 2) sum += ms;
+    }
+    printf("{\"copy\": \"hipMemcpyAsync\", \"ms_avg\": %.4f, \"GBps_avg\": %.1f}\n", sum / 10, 2.0 * bytes / (sum / 10) / 1e6);
+  }
+  int cu = 256;
+  for (int g : {cu * 4, cu * 8, cu * 16}) {
+    run<4, false, false>("plain_u4", s, d, n, g, st, e0, e1);
+    run<4, true, true>("nt_u4", s, d, n, g, st, e0, e1);
+    run<4, true, false>("ntload_u4", s, d, n, g, st, e0, e1);
+    run<8, true, true>("nt_u8", s, d, n, g, st, e0, e1);
+  }
+  return 0;
+}
