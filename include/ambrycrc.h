@@ -398,9 +398,9 @@ int ambrycrc_batch_host(const void* const* ptrs, const uint64_t* lens, const uin
  * policy. Replaces nothing in the reference, whose callers (NettyServerRequest.java:35,54,
  * StoreMessageReadSet.java:170-188) hold exactly such host buffers. */
 int ambrycrc_set_host_policy(int device, int policy);
-/* The rates the auto policy compares: *cpu_gibps (CPU threads x per-thread CLMUL rate measured once
- * per process over 32 MiB x 0.85), *gpu_gibps (the GPU host path: 51 GiB/s measured, refreshed by each pageable
- * GPU call of >= 64 MiB), *cpu_threads (AMBRYCRC_CPU_THREADS, else OMP_NUM_THREADS, else this
+/* The rates the auto policy compares: *cpu_gibps (the CLMUL CPU leg's rate measured once per process
+ * with all its threads, each over its own 16 MiB slice of a buffer past the L3), *gpu_gibps (the
+ * GPU host path: 51 GiB/s measured, refreshed by each pageable GPU call of >= 64 MiB), *cpu_threads (AMBRYCRC_CPU_THREADS, else OMP_NUM_THREADS, else this
  * process's CPUs). Returns the leg auto takes for pageable bytes (0 CPU, 1 GPU), or < 0. Any
  * output may be NULL. */
 int ambrycrc_host_rates(int device, double* cpu_gibps, double* gpu_gibps, int* cpu_threads);
