@@ -373,11 +373,11 @@ def test_unsorted_offsets_take_the_tail(gpu, msg_mode):
 
 def test_long_records_split_over_the_grid(gpu, msg_mode):
     """Several multi-MiB blobs among small PUTs (tools/probes/long_mix.py's shape, scaled down): in
-    two-pass region mode each is split into ~256 KiB pieces that waves across the GPU hash from the
-    run sums and combine by x^(8d) shifts (region_long_kernel). Flips land in the first piece, one
-    byte either side of piece boundaries, and in the last 64-B run of a blob; a 3 MiB + 1 B blob (an
-    uneven last piece) and a 32 KiB + 1 B one (a single piece) stay clean. Every status and end
-    equals the oracle's."""
+    region mode each is split into 64 KiB pieces that waves across the GPU hash from the run sums;
+    the wave that finishes a record's last piece folds them (region_long_kernel, long_fold). Flips
+    land in the first piece, on the last byte of one piece and the first byte of another, and in the
+    last 64-B run of a blob; a 3 MiB + 1 B blob (an uneven last piece) and a 32 KiB + 1 B one (a
+    single piece) stay clean. Every status and end equals the oracle's."""
     from datagen import stream_bytes
 
     sizes = {300: (4 << 20) + 13, 900: (3 << 20) + 1, 1400: (32 << 10) + 1, 2100: (5 << 20) - 7, 2500: 9 << 20}
@@ -389,11 +389,11 @@ def test_long_records_split_over_the_grid(gpu, msg_mode):
     offs = np.cumsum([0] + [len(x) for x in msgs[:-1]]).tolist()
     region = bytearray(b"".join(msgs))
     blob_at = {i: offs[i] + len(msgs[i]) - 8 - sizes[i] for i in sizes}  # blob content start
-    # (record = 13-B head + content + 8-B CRC; pieces split the record, so boundaries sit near k*len/np)
-    flips = {300: 100, 2100: ((5 << 20) + 13 + 8) // 20 * 3 - 13, 2500: (9 << 20) - 3}
+    # (record = 13-B head + content + 8-B CRC; piece p = record bytes [p * 64 KiB, (p + 1) * 64 KiB))
+    flips = {300: 100, 2100: 3 * 65536 - 13 - 1, 2500: (9 << 20) - 3}  # 2100: piece 2's last byte
     for i, d in flips.items():
         region[blob_at[i] + d] ^= 0x04
-    region[blob_at[2100] + ((5 << 20) + 21) * 7 // 20 - 12] ^= 0x80  # one byte past another boundary
+    region[blob_at[2100] + 7 * 65536 - 13] ^= 0x80  # piece 7's first byte
     region = bytes(region)
     expect = [MF.verify_message(region, o) for o in offs]
     assert len(region) <= 6144 * len(offs)  # region mode engages
@@ -402,3 +402,52 @@ def test_long_records_split_over_the_grid(gpu, msg_mode):
     assert st == [s for s, _ in expect]
     assert end == [e for _, e in expect]
     assert st[300] == st[2100] == st[2500] == MF.BLOB_CRC and st[900] == st[1400] == 0
+
+
+def test_verify_graph_capture_and_replay(gpu, msg_mode):
+    """ambrycrc_verify_messages_dev only enqueues work (the form is chosen on the host from the
+    region's size, the long-record list is reset on the device by pass 1), so it can be captured
+    into a HIP graph. Captured once over small PUTs with two multi-MiB blobs and replayed after the
+    bytes change -- a flip in a small message, then one in a long blob's middle piece: every
+    replay's statuses and ends equal the oracle's."""
+    import torch
+
+    from datagen import stream_bytes
+
+    sizes = {200: (3 << 20) + 5, 700: (2 << 20) + 77}
+    msgs = []
+    for i in range(1500):
+        size = sizes.get(i, 100 + (i * 53) % 2500)
+        msgs.append(MF.put_message(MF.store_key("C%d" % i), MF.blob_properties_bytes(size), b"m" * (i % 7),
+                                   stream_bytes(9100 + i, 0, size).tobytes(), version=1 + i % 3))
+    offs = np.cumsum([0] + [len(x) for x in msgs[:-1]]).tolist()
+    region = bytearray(b"".join(msgs))
+    dev = torch.frombuffer(bytearray(region), dtype=torch.uint8).cuda()
+    o = torch.tensor(np.asarray(offs, dtype=np.int64), device="cuda")
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        gpu.verify_messages(dev, o)  # sizes the stream's default workspace outside the capture
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            st, end = gpu.verify_messages(dev, o)
+    torch.cuda.synchronize()
+
+    def replay_check(b):
+        dev.copy_(torch.frombuffer(bytearray(b), dtype=torch.uint8).cuda())
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        expect = [MF.verify_message(bytes(b), x) for x in offs]
+        assert st.cpu().numpy().view(np.uint32).tolist() == [e for e, _ in expect]
+        assert end.cpu().numpy().tolist() == [e for _, e in expect]
+        return expect
+
+    assert all(e == 0 for e, _ in replay_check(region))
+    region[offs[50] + len(msgs[50]) - 20] ^= 0x01
+    assert replay_check(region)[50][0] != 0
+    blob200 = offs[200] + len(msgs[200]) - 8 - sizes[200]
+    region[blob200 + 21 * 65536 + 5] ^= 0x40
+    got = replay_check(region)
+    assert got[200][0] == MF.BLOB_CRC and got[700][0] == 0
