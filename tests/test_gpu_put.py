@@ -167,3 +167,49 @@ def test_serialize_6k_messages(gpu, mf):
         assert layout(m)[0] == want
         msgs.append(m)
     _run(gpu, mf, msgs, 1, 3, 5)
+
+
+def test_serialize_graph_capture_and_replay(gpu, mf):
+    """ambrycrc_serialize_puts_dev only enqueues work, so it can be captured into a HIP graph:
+    captured once over 300 PUTs in copy mode and replayed after every blob's bytes change (same
+    sizes); each replay's output is the oracle's layout of the current bytes, every CRC trailer
+    included."""
+    import dataclasses
+
+    import torch
+
+    from ambry_amd.messages import pack_batch, serialize_dev
+    from datagen import stream_bytes
+
+    msgs = random_messages(mf, 300, seed=21, max_blob=9000)
+    descs, fields, blobs, offs, total = pack_batch(msgs, out_align=1, field_align=3, gap=2)
+    d, f, b = _dev(descs.tobytes()), _dev(fields), _dev(blobs)
+    out = _dev(b"\xAA" * total)
+    mlen = torch.empty(len(msgs), dtype=torch.int64, device="cuda")
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        serialize_dev(d, out, f, b, msg_len=mlen)  # sizes the stream's default workspace outside the capture
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            serialize_dev(d, out, f, b, msg_len=mlen)
+    torch.cuda.synchronize()
+
+    def check(ms):
+        g.replay()
+        torch.cuda.synchronize()
+        exp = bytearray(b"\xAA" * total)
+        for m, o in zip(ms, offs):
+            e = expected(mf, m)
+            exp[o:o + len(e)] = e
+        assert out.cpu().numpy().tobytes() == bytes(exp)
+        assert mlen.cpu().numpy().tolist() == [len(expected(mf, m)) for m in ms]
+
+    check(msgs)
+    msgs2 = [dataclasses.replace(m, blob=stream_bytes(500 + i, 11, len(m.blob)).tobytes()) if m.blob else m
+             for i, m in enumerate(msgs)]
+    _, _, blobs2, offs2, total2 = pack_batch(msgs2, out_align=1, field_align=3, gap=2)
+    assert offs2 == offs and total2 == total and len(blobs2) == len(blobs)
+    b.copy_(_dev(blobs2))
+    check(msgs2)
