@@ -454,12 +454,12 @@ int host_cpu_threads() {
 
 double host_cpu_gibps() {
   // The CPU leg's rate with all its threads at once, measured once per process: each thread hashes
-  // its own slice of a buffer larger than the L3 (16 MiB a thread, 1 GiB at most), twice, and the
+  // its own slice of a buffer larger than the L3 (16 MiB a thread, 512 MiB at most), twice, and the
   // faster pass counts. A single thread times threads (round 5's first form) read the L3-fed rate:
   // 662 GiB/s estimated against 262 measured on 16 CPUs, where the threads share DRAM bandwidth.
   static const double rate = [] {
     const int t = host_cpu_threads();
-    const size_t slice = std::min<size_t>(16u << 20, ((size_t)1 << 30) / (size_t)t) & ~size_t(4095);
+    const size_t slice = std::min<size_t>(16u << 20, ((size_t)512 << 20) / (size_t)t) & ~size_t(4095);
     std::vector<uint8_t> buf(slice * (size_t)t);
     std::vector<std::thread> th;
     th.reserve(t);

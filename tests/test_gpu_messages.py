@@ -451,3 +451,54 @@ def test_verify_graph_capture_and_replay(gpu, msg_mode):
     region[blob200 + 21 * 65536 + 5] ^= 0x40
     got = replay_check(region)
     assert got[200][0] == MF.BLOB_CRC and got[700][0] == 0
+
+
+def test_long_record_list_overflow(gpu, msg_mode):
+    """More long records than region mode's grid-wide list holds (4,096): 4,200 PUTs with 33 KiB blobs
+    (528 runs each, over the 512-run cut) among 100,800 small PUTs, so the records listed past the
+    list's capacity fall back to their wave's queue (and past that to their own thread). One long
+    record in ten has a flipped content bit, spread over the whole region (which records reach the
+    list is decided by the device's atomics). Statuses and ends against the construction, and a
+    sample of messages against the oracle."""
+    import torch
+
+    from datagen import stream_bytes
+
+    small = MF.put_message(MF.store_key("s"), MF.blob_properties_bytes(300), b"u" * 200,
+                           stream_bytes(77, 0, 300).tobytes(), version=3)
+    longs = []
+    for j in range(4200):
+        blob = stream_bytes(50000 + j, 0, 33 << 10).tobytes()
+        longs.append(MF.put_message(MF.store_key("L%d" % j), MF.blob_properties_bytes(len(blob)), b"", blob,
+                                    version=1 + j % 3))
+    parts, offs, is_long = [], [], []
+    pos = 0
+    for j in range(4200):
+        for _ in range(24):
+            parts.append(small)
+            offs.append(pos)
+            is_long.append(-1)
+            pos += len(small)
+        parts.append(longs[j])
+        offs.append(pos)
+        is_long.append(j)
+        pos += len(longs[j])
+    region = bytearray(b"".join(parts))
+    flipped = set(range(3, 4200, 10))
+    for j in flipped:
+        i = 25 * j + 24
+        region[offs[i] + len(longs[j]) - 8 - 1000] ^= 0x02  # inside the blob content
+    region = bytes(region)
+    assert len(region) <= 6144 * len(offs)
+    r = torch.frombuffer(bytearray(region), dtype=torch.uint8).cuda()
+    o = torch.tensor(np.asarray(offs, dtype=np.int64), device="cuda")
+    st, end = gpu.verify_messages(r, o)
+    torch.cuda.synchronize()
+    st = st.cpu().numpy().view(np.uint32)
+    end = end.cpu().numpy()
+    want_st = np.array([MF.BLOB_CRC if k in flipped else 0 for k in is_long], dtype=np.uint32)
+    lens = np.array([len(small) if k < 0 else len(longs[k]) for k in is_long], dtype=np.int64)
+    assert np.array_equal(st, want_st)
+    assert np.array_equal(end, np.asarray(offs, dtype=np.int64) + lens)
+    for i in list(range(0, len(offs), 997)) + [25 * j + 24 for j in (3, 4095, 4096, 4193, 4199)]:
+        assert (int(st[i]), int(end[i])) == MF.verify_message(region, offs[i]), i
