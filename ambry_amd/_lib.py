@@ -145,6 +145,8 @@ _SIGNATURES = [
     ("ambrycrc_host_rates", ctypes.c_int,
      [ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),
     ("ambrycrc_last_host_path", ctypes.c_int, [ctypes.c_int]),
+    ("ambrycrc_host_msg_rates", ctypes.c_int,
+     [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     ("ambrycrc_set_grid", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     ("ambrycrc_set_window", ctypes.c_int, [ctypes.c_int, ctypes.c_uint64]),
     ("ambrycrc_timing_enable", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),

@@ -120,6 +120,15 @@ struct DevCtx {
   int host_policy = 0;
   std::atomic<double> gpu_host_gibps{51.0};
   std::atomic<int> last_host_path{-1};
+  // The message entries (kMsgVerify, kMsgTransform) compare their own legs' rates over region
+  // bytes, GiB/s: a CPU leg parses and (transform) copies each message, so the CRC rate above does
+  // not stand for it. Each leg's rate is refreshed by its calls of >= 64 MiB (EWMA); the CPU legs
+  // start from a fraction of the CRC rate (-1 until measured), the GPU legs from round 5's
+  // measurements (bench_put --transform-host, 4 KiB PUTs); under auto every 16th large pageable call
+  // takes the other leg, so a rate that changes is seen.
+  std::atomic<double> msg_gpu_gibps[2] = {{44.0}, {22.0}};
+  std::atomic<double> msg_cpu_gibps[2] = {{-1.0}, {-1.0}};
+  std::atomic<uint32_t> msg_calls[2] = {{0u}, {0u}};
   // Processor waves of the one-pass kernels (0: per call, fused_proc_waves); AMBRYCRC_FUSED_PROC.
   int fused_proc = AMBRY_FUSED_PROC;
   uint64_t region_max = kRegionMaxPerMessage;  // region bytes per message up to which it applies
@@ -169,6 +178,11 @@ double host_cpu_gibps();
 bool host_take_cpu(DevCtx* c, int device, int pinned);
 // After a GPU host call over `bytes` that took `seconds`: refresh c->gpu_host_gibps.
 void host_note_gpu(DevCtx* c, uint64_t bytes, double seconds);
+// The message entries' leg choice and rate tracking (DevCtx::msg_*_gibps).
+constexpr int kMsgVerify = 0, kMsgTransform = 1;
+bool host_take_cpu_msg(DevCtx* c, int device, int pinned, int op, uint64_t bytes);
+void host_note_msg(DevCtx* c, int op, bool cpu, uint64_t bytes, double seconds);
+double host_msg_cpu_gibps(const DevCtx* c, int op);
 DevCtx* ctx_for(int device);
 DevCtx* ctx_current();
 // Bytes of batch workspace for n chunks (ambrycrc_workspace_bytes).

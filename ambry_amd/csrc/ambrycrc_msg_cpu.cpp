@@ -117,6 +117,95 @@ uint32_t verify(const uint8_t* p, uint64_t rem, Parsed* m) {
   return status;
 }
 
+// ValidatingTransformer.transform of one message, split for the batch: transform_plan verifies the
+// message and decides its output (status, length, and how to write it) without writing; transform_emit
+// writes it. The batch plans every message, places them by one prefix sum and emits each straight
+// into the output, with no scratch copy.
+struct XPlan {
+  uint64_t len = 0;      // output bytes
+  bool fast = false;     // the message's own bytes, life version and header CRC rewritten
+  int life = -1;         // fast: the life version to write (-1: keep the stored one)
+  ambrycrc_put_desc d;   // general: the re-serialization
+  ambrycrc::PropsFix fx;
+};
+
+uint32_t transform_plan(const uint8_t* region, uint64_t region_len, uint64_t off, int life_version, int header_version,
+                        XPlan* x) {
+  Parsed m;
+  m.end = 0;
+  const uint32_t st = off <= region_len ? verify(region + off, region_len - off, &m) : (uint32_t)AMBRYCRC_MSG_BAD_LAYOUT;
+  if (st) return st;
+  const uint8_t* p = region + off;
+  const int32_t enc = m.rel[0], bp = m.rel[1], upd = m.rel[2], um = m.rel[3], blob = m.rel[4];
+  if (upd != -1 || bp == -1 || um == -1 || blob == -1) return AMBRYCRC_MSG_NOT_PUT;  // "cannot be anything rather than put record"
+  // the deserializers' field reads (deserializeBlobEncryptionKey / Properties / UserMetadata / Blob,
+  // MessageFormatRecord.java:1568-1833); verify's record checks already hold for them
+  const int64_t first = enc != -1 ? enc : bp;
+  const uint32_t bv = rd16(p + blob);
+  const uint32_t head = bv == 1 ? 10u : bv == 2 ? 12u : 13u;
+  // deserializeBlobProperties, re-serialized at VERSION_5 (record_fields.h; verify parsed it)
+  const uint32_t stored = (uint32_t)(um - bp - 2 - 8);
+  ambrycrc::PropsFields pf;
+  if (ambrycrc::props_parse<true>(p + bp + 2, stored, &pf) != 0) return AMBRYCRC_MSG_BAD_RECORD;
+  if (!pf.ascii) return AMBRYCRC_MSG_NOT_ENCODABLE;
+  x->fx = ambrycrc::props_fix_of(pf, stored);
+  // A V3 message with a V3 blob record and properties already canonical VERSION_5 bytes re-serializes
+  // at V3 to its own bytes but for the life version and the header CRC (the GPU fast path's rule,
+  // region_proc.h transform_fast): one copy and the 32-byte header's CRC, instead of the layout,
+  // copy and every record CRC again.
+  if (header_version == 3 && m.version == 3 && bv == 3 && x->fx.version == 0) {
+    x->fast = true;
+    x->len = m.end;
+    x->life = life_version >= 0 && (uint32_t)life_version != m.life ? life_version : -1;
+    return 0;
+  }
+  ambrycrc_put_desc& d = x->d;
+  memset(&d, 0, sizeof d);
+  const bool keep_enc = enc != -1 && header_version >= 2;
+  d.out_off = 0;
+  d.key_src = off + m.hsize;
+  d.key_len = (uint32_t)(first - m.hsize);
+  d.enckey_src = keep_enc ? off + enc + 6 : 0;
+  d.enckey_len = keep_enc ? (int32_t)rd32(p + enc + 2) : -1;
+  d.props_src = off + bp + 2;
+  d.props_len = ambrycrc::props_v5_len(x->fx);
+  d.usermeta_src = off + um + 6;
+  d.usermeta_len = rd32(p + um + 2);
+  d.blob_src = off + blob + head;
+  d.blob_len = rd64(p + blob + (bv == 1 ? 2 : bv == 2 ? 4 : 5));
+  d.life_version = (int16_t)(life_version >= 0 ? life_version : (int)m.life);
+  d.blob_type = (int16_t)(bv == 1 ? 0u : rd16(p + blob + 2));
+  d.compressed = (uint8_t)(bv == 3 && p[blob + 4] == 1 ? 1 : 0);
+  d.header_version = (uint8_t)header_version;
+  x->len = ambrycrc_put_layout(&d, nullptr);
+  return x->len ? 0u : (uint32_t)AMBRYCRC_MSG_BAD_RECORD;
+}
+
+// Writes the planned message at out (x.len bytes of room).
+int transform_emit(const uint8_t* region, uint64_t off, const XPlan& x, uint8_t* out) {
+  if (x.fast) {
+    memcpy(out, region + off, x.len);
+    if (x.life >= 0) {
+      ambrycrc::put_be16(out + 2, (uint32_t)x.life);
+      ambrycrc::put_be64(out + 32, (uint64_t)ambrycrc_update(0, out, 32));
+    }
+    return AMBRYCRC_OK;
+  }
+  // the stored payload is copied (props_len bytes from props_src: the appendix's share of them comes
+  // from the user-metadata record that follows, inside the message), then rewritten as V5 and its
+  // record CRC recomputed
+  const int rc = ambrycrc_serialize_put_host(&x.d, region, region, out, x.len, nullptr);
+  if (rc) return rc;
+  if (x.fx.version) {
+    uint64_t fo[5];
+    ambrycrc_put_layout(&x.d, fo);
+    uint8_t* rec = out + fo[2] - 2;
+    ambrycrc::props_apply_fix(rec + 2, x.fx);
+    ambrycrc::put_be64(rec + 2 + x.d.props_len, (uint64_t)ambrycrc_update(0, rec, 2ull + x.d.props_len));
+  }
+  return AMBRYCRC_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -136,77 +225,16 @@ int ambrycrc_transform_message_cpu(const uint8_t* region, uint64_t region_len, u
   if (!region || !out_len || !status || header_version < 1 || header_version > 3 || life_version > 32767)
     return AMBRYCRC_EINVAL;
   *out_len = 0;
-  Parsed m;
-  m.end = 0;
-  uint32_t st = off <= region_len ? verify(region + off, region_len - off, &m) : (uint32_t)AMBRYCRC_MSG_BAD_LAYOUT;
-  if (st) {
-    *status = st;
-    return AMBRYCRC_OK;
-  }
-  const uint8_t* p = region + off;
-  const int32_t enc = m.rel[0], bp = m.rel[1], upd = m.rel[2], um = m.rel[3], blob = m.rel[4];
-  if (upd != -1 || bp == -1 || um == -1 || blob == -1) {  // "cannot be anything rather than put record"
-    *status = AMBRYCRC_MSG_NOT_PUT;
-    return AMBRYCRC_OK;
-  }
-  // the deserializers' field reads (deserializeBlobEncryptionKey / Properties / UserMetadata / Blob,
-  // MessageFormatRecord.java:1568-1833); verify's record checks already hold for them
-  const int64_t first = enc != -1 ? enc : bp;
-  const uint32_t bv = rd16(p + blob);
-  const uint32_t head = bv == 1 ? 10u : bv == 2 ? 12u : 13u;
-  ambrycrc_put_desc d;
-  memset(&d, 0, sizeof d);
-  const bool keep_enc = enc != -1 && header_version >= 2;
-  d.out_off = 0;
-  d.key_src = off + m.hsize;
-  d.key_len = (uint32_t)(first - m.hsize);
-  d.enckey_src = keep_enc ? off + enc + 6 : 0;
-  d.enckey_len = keep_enc ? (int32_t)rd32(p + enc + 2) : -1;
-  // deserializeBlobProperties, re-serialized at VERSION_5 (record_fields.h; verify parsed it)
-  const uint32_t stored = (uint32_t)(um - bp - 2 - 8);
-  ambrycrc::PropsFields pf;
-  if (ambrycrc::props_parse<true>(p + bp + 2, stored, &pf) != 0) {
-    *status = AMBRYCRC_MSG_BAD_RECORD;
-    return AMBRYCRC_OK;
-  }
-  if (!pf.ascii) {
-    *status = AMBRYCRC_MSG_NOT_ENCODABLE;
-    return AMBRYCRC_OK;
-  }
-  const ambrycrc::PropsFix fx = ambrycrc::props_fix_of(pf, stored);
-  d.props_src = off + bp + 2;
-  d.props_len = ambrycrc::props_v5_len(fx);
-  d.usermeta_src = off + um + 6;
-  d.usermeta_len = rd32(p + um + 2);
-  d.blob_src = off + blob + head;
-  d.blob_len = rd64(p + blob + (bv == 1 ? 2 : bv == 2 ? 4 : 5));
-  d.life_version = (int16_t)(life_version >= 0 ? life_version : (int)m.life);
-  d.blob_type = (int16_t)(bv == 1 ? 0u : rd16(p + blob + 2));
-  d.compressed = (uint8_t)(bv == 3 && p[blob + 4] == 1 ? 1 : 0);
-  d.header_version = (uint8_t)header_version;
-  const uint64_t n = ambrycrc_put_layout(&d, nullptr);
-  if (n == 0) {
-    *status = AMBRYCRC_MSG_BAD_RECORD;
-    return AMBRYCRC_OK;
-  }
-  if (!out || n > out_cap) {
+  XPlan x;
+  *status = transform_plan(region, region_len, off, life_version, header_version, &x);
+  if (*status) return AMBRYCRC_OK;
+  if (!out || x.len > out_cap) {
     *status = AMBRYCRC_MSG_NO_ROOM;
     return AMBRYCRC_OK;
   }
-  // the stored payload is copied (props_len bytes from props_src: the appendix's share of them comes
-  // from the user-metadata record that follows, inside the message), then rewritten as V5 and its
-  // record CRC recomputed
-  const int rc = ambrycrc_serialize_put_host(&d, region, region, out, out_cap, nullptr);
+  const int rc = transform_emit(region, off, x, out);
   if (rc) return rc;
-  if (fx.version) {
-    uint64_t fo[5];
-    ambrycrc_put_layout(&d, fo);
-    uint8_t* rec = out + fo[2] - 2;
-    ambrycrc::props_apply_fix(rec + 2, fx);
-    ambrycrc::put_be64(rec + 2 + d.props_len, (uint64_t)ambrycrc_update(0, rec, 2ull + d.props_len));
-  }
-  *out_len = n;
-  *status = 0;
+  *out_len = x.len;
   return AMBRYCRC_OK;
 }
 
@@ -219,6 +247,8 @@ int ambrycrc_transform_message_cpu(const uint8_t* region, uint64_t region_len, u
 // above. Same outputs as the device batch.
 #include <algorithm>
 #include <thread>
+#include <memory>
+#include <new>
 #include <vector>
 
 #include "ambrycrc_ctx.h"
@@ -271,42 +301,35 @@ int verify_messages_cpu(const uint8_t* region, uint64_t region_len, const uint64
 int transform_messages_cpu(const uint8_t* region, uint64_t region_len, const uint64_t* msg_off, size_t m,
                            const int16_t* life_version, int header_version, uint8_t* out, uint64_t out_cap,
                            uint64_t* out_off, uint64_t* out_len, uint32_t* status, int threads) {
-  // each message into its own scratch span (its extent + the growth bound), in parallel; then packed
-  // in message order as the device batch packs it (NO_ROOM once the running sum passes out_cap)
-  std::vector<uint64_t> at(m + 1, 0);
-  for (size_t i = 0; i < m; ++i)
-    at[i + 1] = at[i] + extent_of(region, region_len, msg_off[i]) + AMBRYCRC_TRANSFORM_GROWTH_MAX;
-  std::vector<uint8_t> scratch(at[m]);
-  std::vector<uint64_t> len(m, 0);
-  int rc = AMBRYCRC_OK;
-  split_run(m, threads, [&](size_t i) { return at[i + 1] - at[i]; }, [&](size_t a, size_t b) {
-    for (size_t i = a; i < b; ++i) {
-      const int lv = life_version ? life_version[i] : -1;
-      if (ambrycrc_transform_message_cpu(region, region_len, msg_off[i], lv, header_version, scratch.data() + at[i],
-                                         at[i + 1] - at[i], &len[i], &status[i]) != AMBRYCRC_OK)
-        rc = AMBRYCRC_EINVAL;
-    }
+  // every message planned in parallel (verified, its output length known), placed in message order
+  // as the device batch packs it (NO_ROOM once the running sum passes out_cap), then emitted in
+  // parallel straight into `out` (round 5's first form transformed into a scratch copy of the region
+  // and packed it after: two more passes over the bytes and a fresh allocation's page faults)
+  std::vector<XPlan> plan(m);
+  split_run(m, threads, [&](size_t i) { return extent_of(region, region_len, msg_off[i]); }, [&](size_t a, size_t b) {
+    for (size_t i = a; i < b; ++i)
+      status[i] = transform_plan(region, region_len, msg_off[i], life_version ? life_version[i] : -1, header_version,
+                                 &plan[i]);
   });
-  if (rc) return rc;
+  std::vector<uint64_t> pos(m, ~0ull);  // output position, ~0: not placed
   uint64_t vpos = 0;
   for (size_t i = 0; i < m; ++i) {
-    if (status[i] == 0 && len[i]) {
-      if (vpos + len[i] <= out_cap) {
-        memcpy(out + vpos, scratch.data() + at[i], len[i]);
-        if (out_off) out_off[i] = vpos;
-        out_len[i] = len[i];
-      } else {
+    if (status[i] == 0 && plan[i].len) {
+      if (vpos + plan[i].len <= out_cap)
+        pos[i] = vpos;
+      else
         status[i] = AMBRYCRC_MSG_NO_ROOM;
-        if (out_off) out_off[i] = ~0ull;
-        out_len[i] = 0;
-      }
-      vpos += len[i];
-      continue;
+      vpos += plan[i].len;
     }
-    if (out_off) out_off[i] = ~0ull;
-    out_len[i] = 0;
+    if (out_off) out_off[i] = pos[i];
+    out_len[i] = pos[i] == ~0ull ? 0 : plan[i].len;
   }
-  return AMBRYCRC_OK;
+  int rc = AMBRYCRC_OK;
+  split_run(m, threads, [&](size_t i) { return pos[i] == ~0ull ? 0 : plan[i].len; }, [&](size_t a, size_t b) {
+    for (size_t i = a; i < b; ++i)
+      if (pos[i] != ~0ull && transform_emit(region, msg_off[i], plan[i], out + pos[i]) != AMBRYCRC_OK) rc = AMBRYCRC_EINVAL;
+  });
+  return rc;
 }
 
 }  // namespace detail

@@ -208,6 +208,15 @@ def host_rates(device: int = 0) -> dict:
     return {"cpu_gibps": c.value, "gpu_gibps": g.value, "cpu_threads": t.value, "auto_leg": "gpu" if leg else "cpu"}
 
 
+def host_msg_rates(device: int = 0, op: str = "verify") -> dict:
+    """The rates auto compares for the host message entries (op "verify" / "transform";
+    ambrycrc_host_msg_rates) and the leg it takes for pageable bytes."""
+    c, g = ctypes.c_double(), ctypes.c_double()
+    leg = check(lib().ambrycrc_host_msg_rates(device, {"verify": 0, "transform": 1}[op], ctypes.byref(c),
+                                              ctypes.byref(g)), "ambrycrc_host_msg_rates")
+    return {"cpu_gibps": c.value, "gpu_gibps": g.value, "auto_leg": "gpu" if leg else "cpu"}
+
+
 def last_host_path(device: int = 0) -> int:
     """The leg the device's last host call took: 0 CPU, 1 GPU (-1: none yet)."""
     return lib().ambrycrc_last_host_path(device)

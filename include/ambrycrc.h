@@ -398,7 +398,7 @@ int ambrycrc_batch_host(const void* const* ptrs, const uint64_t* lens, const uin
  * policy. Replaces nothing in the reference, whose callers (NettyServerRequest.java:35,54,
  * StoreMessageReadSet.java:170-188) hold exactly such host buffers. */
 int ambrycrc_set_host_policy(int device, int policy);
-/* The rates the auto policy compares: *cpu_gibps (the CLMUL CPU leg's rate measured once per process
+/* The rates the auto policy compares for ambrycrc_batch_host: *cpu_gibps (the CLMUL CPU leg's rate measured once per process
  * with all its threads, each over its own 16 MiB slice of a buffer past the L3), *gpu_gibps (the
  * GPU host path: 51 GiB/s measured, refreshed by each pageable GPU call of >= 64 MiB), *cpu_threads (AMBRYCRC_CPU_THREADS, else OMP_NUM_THREADS, else this
  * process's CPUs). Returns the leg auto takes for pageable bytes (0 CPU, 1 GPU), or < 0. Any
@@ -406,6 +406,12 @@ int ambrycrc_set_host_policy(int device, int policy);
 int ambrycrc_host_rates(int device, double* cpu_gibps, double* gpu_gibps, int* cpu_threads);
 /* The leg the device's last host call took: 0 CPU, 1 GPU, -1 none yet. */
 int ambrycrc_last_host_path(int device);
+/* The rates auto compares for the host message entries (op 0: ambrycrc_verify_messages_host, 1:
+ * ambrycrc_transform_messages_host), GiB/s of region bytes: each leg's rate as its calls of >= 64 MiB
+ * measured it (an EWMA; the CPU leg starts at a share of the CRC rate, the GPU leg at round 5's
+ * measurement); under auto every 16th such pageable call takes the other leg to refresh it.
+ * Returns the leg auto takes for pageable bytes (0 CPU, 1 GPU), or < 0. */
+int ambrycrc_host_msg_rates(int device, int op, double* cpu_gibps, double* gpu_gibps);
 
 /* ambrycrc_batch_host across several GPUs of this process: the n
  * chunks are split into ndev contiguous ranges by ambrycrc_shard_by_bytes, range g runs ambrycrc_batch_host on devices[g]

@@ -46,3 +46,29 @@ def test_verify_messages_host_both_legs(gpu, policy):
     finally:
         gpu.set_host_policy(0, prev)
     assert list(st) == [s for s, _ in expect] and list(end) == [e for _, e in expect]
+
+
+@pytest.mark.parametrize("op", ["verify", "transform"])
+def test_auto_policy_message_legs(gpu, op):
+    """The message entries under auto take the leg ambrycrc_host_msg_rates names for their own op
+    (not the CRC batch's rates: a CPU leg parses, and for the transform copies, each message);
+    results equal the oracle's either way."""
+    from test_gpu_transform import dense_v3_region
+    from test_message_format import MF
+
+    from ambry_amd.messages import transform_host
+
+    region, offs = dense_v3_region(MF, 400, seed=71)
+    rates = gpu.host_msg_rates(0, op)
+    assert rates["cpu_gibps"] > 0 and rates["gpu_gibps"] > 0
+    prev = gpu.set_host_policy(0, gpu.HOST_AUTO)
+    try:
+        if op == "verify":
+            st, end = gpu.verify_messages_host(region, offs)
+            assert list(st) == [0] * len(offs)
+        else:
+            out, oo, ol, st = transform_host(region, offs)
+            assert list(st) == [0] * len(offs) and out == region  # V3 -> V3, no life versions: the same bytes
+        assert gpu.last_host_path(0) == (1 if rates["auto_leg"] == "gpu" else 0)
+    finally:
+        gpu.set_host_policy(0, prev)

@@ -88,3 +88,4 @@ def test_policy_calls_without_context(ambry):
     assert L.ambrycrc_set_host_policy(dev, 1) == -4
     assert L.ambrycrc_last_host_path(dev) == -4
     assert L.ambrycrc_host_rates(dev, None, None, None) == -4
+    assert L.ambrycrc_host_msg_rates(dev, 0, None, None) == -4

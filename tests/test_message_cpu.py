@@ -51,6 +51,22 @@ def test_transform_matches_oracle(ambry, version, life):
     assert 0 in kinds and MF.NOT_PUT in kinds and MF.BAD_RECORD in kinds and MF.NOT_ENCODABLE in kinds
 
 
+@pytest.mark.parametrize("life", [None, 0, 7])
+def test_transform_fast_form_matches_oracle(ambry, life):
+    """The CPU transform's fast form (V3 header, V3 blob record, properties already canonical
+    VERSION_5 bytes: the message's own bytes with the life version and header CRC rewritten, as the
+    GPU fast path does) against the oracle's full re-serialization, message by message."""
+    from test_gpu_transform import dense_v3_region
+
+    from ambry_amd.messages import transform_message_cpu
+
+    region, offs = dense_v3_region(MF, 200, seed=61)
+    for o in offs:
+        exp_st, exp = MF.transform_message(region, o, life=life, version=3)
+        st, got = transform_message_cpu(region, o, header_version=3, life=life)
+        assert exp_st == 0 and st == 0 and got == exp, o
+
+
 def test_transform_no_room_and_args(ambry):
     from ambry_amd._lib import AmbryCrcError
     from ambry_amd.messages import MSG_NO_ROOM, transform_message_cpu

@@ -177,6 +177,85 @@ def run_transform(m, blob_bytes, reps, verdict="device"):
             "path_taken": {1: "one-pass fast path", 0: "general path"}.get(path)}
 
 
+def run_transform_host(m, blob_bytes, reps, leg="gpu", verdict="device", op="transform"):
+    """ambrycrc_transform_messages_host over the same region in pageable host memory (the replication
+    sieve's case: a GetResponse read into a heap or direct buffer), output into host memory: the GPU
+    leg streams it through the pinned slabs (H2D, the fast path per slab, D2H), the CPU leg runs the
+    per-message transform on the CPU threads. verdict=host is round 4's blocking per-slab verdict.
+    Wall time per synchronous call, buffers preallocated."""
+    import ctypes
+
+    import numpy as np
+    import torch
+
+    from ambry_amd import device as D
+    from ambry_amd._lib import check, lib
+    from ambry_amd.messages import PUT_DESC_DTYPE, PutMessage, layout, out_bound, serialize_dev
+
+    key_len, props_len, um_len = 24, 94, 1000
+    L, fo = layout(PutMessage(key=bytes(key_len), props=bytes(props_len), usermeta=bytes(um_len),
+                              blob=bytes(blob_bytes)))
+    descs = np.zeros(m, dtype=PUT_DESC_DTYPE)
+    idx = np.arange(m, dtype=np.uint64)
+    descs["out_off"] = idx * L
+    descs["blob_len"] = blob_bytes
+    descs["key_len"], descs["props_len"], descs["usermeta_len"] = key_len, props_len, um_len
+    descs["enckey_len"] = -1
+    descs["header_version"] = 3
+    region = torch.empty(m * L, dtype=torch.uint8, device="cuda")
+    D.fill_random(region[: (m * L) // 16 * 16], 3, 0)
+    p0 = fo["props"]
+    region.view(m, L)[:, p0:p0 + props_len] = _props_tensor(torch)
+    serialize_dev(torch.from_numpy(descs.view(np.uint8).copy()).cuda(), region)
+    torch.cuda.synchronize()
+    host = region.cpu().numpy()  # pageable
+    del region
+    offs = (idx * L).astype(np.uint64)
+    cap = out_bound(m * L, m)
+    out = np.empty(cap, dtype=np.uint8)
+    oo, ol = np.zeros(m, dtype=np.uint64), np.zeros(m, dtype=np.uint64)
+    st = np.zeros(m, dtype=np.uint32)
+    u64p = ctypes.POINTER(ctypes.c_uint64)
+    prev_policy = D.set_host_policy(0, D.HOST_GPU if leg == "gpu" else D.HOST_CPU)
+    prev_verdict = D.set_transform_verdict(0, verdict == "host")
+
+    def call():
+        if op == "verify":
+            check(lib().ambrycrc_verify_messages_host(
+                ctypes.c_void_p(host.ctypes.data), host.size, offs.ctypes.data_as(u64p), m,
+                st.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), oo.ctypes.data_as(u64p), 0, 0),
+                "ambrycrc_verify_messages_host")
+            return
+        check(lib().ambrycrc_transform_messages_host(
+            ctypes.c_void_p(host.ctypes.data), host.size, offs.ctypes.data_as(u64p), m, None, 3, out.ctypes.data, cap,
+            oo.ctypes.data_as(u64p), ol.ctypes.data_as(u64p), st.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), 0, 0),
+            "ambrycrc_transform_messages_host")
+
+    try:
+        call()
+        if op == "verify":  # every message clean, each ending where the next starts
+            assert int(st.max()) == 0 and np.array_equal(oo, offs + L)
+        else:
+            assert int(st.max()) == 0 and np.array_equal(out[: m * L], host)  # V3 -> V3: identical
+        times = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            call()
+            times.append(time.perf_counter() - t0)
+        path = D.last_host_path(0)
+    finally:
+        D.set_host_policy(0, prev_policy)
+        D.set_transform_verdict(0, bool(prev_verdict))
+    times.sort()
+    ms = 1e3 * times[len(times) // 2]
+    nbytes = m * L
+    what = "verify_host" if op == "verify" else "transform_host"
+    return {"case": f"{what} {m} x PUT({blob_bytes} B blob) V3 -> V3, pageable", "leg": leg,
+            "verdict": verdict, "messages": m, "message_bytes": nbytes, "ms_median": round(ms, 3),
+            "GiBps_messages": round(nbytes / (ms / 1e3) / 2**30, 2), "leg_taken": {0: "cpu", 1: "gpu"}.get(path),
+            "parity": "every message verifies and the V3 -> V3 output equals the input region byte for byte"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
@@ -186,6 +265,7 @@ def main():
     ap.add_argument("--transform", default="64k,4k,4m", help="ValidatingTransformer cases ('' for none)")
     ap.add_argument("--verdict", default="device,host",
                     help="how the transform learns its fast path's verdict: device (async, the default), host")
+    ap.add_argument("--transform-host", default="", help="host-resident transform cases (pageable region, both legs)")
     args = ap.parse_args()
     import torch
 
@@ -208,6 +288,14 @@ def main():
         m, s = cases[c]
         for v in [x for x in args.verdict.split(",") if x]:
             print(json.dumps(run_transform(m, s, args.reps, v)), flush=True)
+            torch.cuda.empty_cache()
+    for c in [x for x in args.transform_host.split(",") if x]:
+        m, s = cases[c]
+        for leg, v in (("gpu", "device"), ("gpu", "host"), ("cpu", "device")):
+            print(json.dumps(run_transform_host(m, s, max(3, args.reps // 2), leg, v)), flush=True)
+            torch.cuda.empty_cache()
+        for leg in ("gpu", "cpu"):
+            print(json.dumps(run_transform_host(m, s, max(3, args.reps // 2), leg, "device", op="verify")), flush=True)
             torch.cuda.empty_cache()
 
 
