@@ -89,3 +89,22 @@ def test_policy_calls_without_context(ambry):
     assert L.ambrycrc_last_host_path(dev) == -4
     assert L.ambrycrc_host_rates(dev, None, None, None) == -4
     assert L.ambrycrc_host_msg_rates(dev, 0, None, None) == -4
+
+
+def test_transform_messages_host_cpu_leg_fast_form(ambry):
+    """The CPU leg over a dense region of canonical V3 PUTs (every message takes the fast form: its own
+    bytes, life version and header CRC rewritten), with index life versions, against the oracle;
+    then with no life versions, where the output is the region itself."""
+    from test_gpu_transform import dense_v3_region
+
+    from ambry_amd.messages import transform_host
+
+    region, offs = dense_v3_region(MF, 300, seed=19)
+    life = np.random.default_rng(4).integers(0, 9, size=len(offs)).astype(np.int16)
+    out, oo, ol, st = transform_host(region, offs, life_version=life, device=-1)
+    assert list(st) == [0] * len(offs)
+    for i, o in enumerate(offs):
+        exp_st, exp = MF.transform_message(region, o, life=int(life[i]), version=3)
+        assert exp_st == 0 and oo[i] == o - offs[0] and out[oo[i]:oo[i] + ol[i]] == exp, i
+    out2, _, _, st2 = transform_host(region, offs, device=-1)
+    assert list(st2) == [0] * len(offs) and out2 == region[offs[0]:]
