@@ -246,6 +246,7 @@ int ambrycrc_transform_message_cpu(const uint8_t* region, uint64_t region_len, u
 // across `threads` CPU threads by region bytes, each message through the single-message loops
 // above. Same outputs as the device batch.
 #include <algorithm>
+#include <atomic>
 #include <thread>
 #include <memory>
 #include <new>
@@ -285,17 +286,17 @@ uint64_t extent_of(const uint8_t* region, uint64_t region_len, uint64_t off) {
 
 int verify_messages_cpu(const uint8_t* region, uint64_t region_len, const uint64_t* msg_off, size_t m,
                         uint32_t* status, uint64_t* msg_end, int threads) {
-  int rc = AMBRYCRC_OK;
+  std::atomic<int> rc{AMBRYCRC_OK};  // written by any worker
   split_run(m, threads, [&](size_t i) { return extent_of(region, region_len, msg_off[i]); },
             [&](size_t a, size_t b) {
               for (size_t i = a; i < b; ++i) {
                 uint64_t e = 0;
                 if (ambrycrc_verify_message_cpu(region, region_len, msg_off[i], &status[i], &e) != AMBRYCRC_OK)
-                  rc = AMBRYCRC_EINVAL;
+                  rc.store(AMBRYCRC_EINVAL);
                 if (msg_end) msg_end[i] = e;
               }
             });
-  return rc;
+  return rc.load();
 }
 
 int transform_messages_cpu(const uint8_t* region, uint64_t region_len, const uint64_t* msg_off, size_t m,
@@ -324,12 +325,13 @@ int transform_messages_cpu(const uint8_t* region, uint64_t region_len, const uin
     if (out_off) out_off[i] = pos[i];
     out_len[i] = pos[i] == ~0ull ? 0 : plan[i].len;
   }
-  int rc = AMBRYCRC_OK;
+  std::atomic<int> rc{AMBRYCRC_OK};  // written by any worker
   split_run(m, threads, [&](size_t i) { return pos[i] == ~0ull ? 0 : plan[i].len; }, [&](size_t a, size_t b) {
     for (size_t i = a; i < b; ++i)
-      if (pos[i] != ~0ull && transform_emit(region, msg_off[i], plan[i], out + pos[i]) != AMBRYCRC_OK) rc = AMBRYCRC_EINVAL;
+      if (pos[i] != ~0ull && transform_emit(region, msg_off[i], plan[i], out + pos[i]) != AMBRYCRC_OK)
+        rc.store(AMBRYCRC_EINVAL);
   });
-  return rc;
+  return rc.load();
 }
 
 }  // namespace detail
