@@ -465,38 +465,44 @@ double host_cpu_gibps() {
     const size_t total = slice * (size_t)t;
     std::unique_ptr<uint8_t[]> buf(new (std::nothrow) uint8_t[total]);  // not zero-filled: first touch below
     if (!buf) return 1.0;
+    // Each thread first-touches its own slice, then hashes it twice from a common start (all threads
+    // spawned and waiting: spawning inside the timed span read ~half the rate on a 16-CPU box);
+    // each pass is timed from its start to the last thread's end.
+    std::atomic<int> ready{0};
+    std::atomic<int> go{0};  // pass number released
+    std::atomic<int64_t> last_end[2];
+    last_end[0] = 0;
+    last_end[1] = 0;
+    std::atomic<uint32_t> sink{0};
     std::vector<std::thread> th;
     th.reserve(t);
-    for (int k = 0; k < t; ++k)  // first touch by the thread that hashes the slice (NUMA placement)
+    for (int k = 0; k < t; ++k)
       th.emplace_back([&, k] {
         uint8_t* p = buf.get() + slice * (size_t)k;
         for (size_t i = 0; i < slice; ++i) p[i] = (uint8_t)(i * 131u + 7u + k);
-      });
-    for (auto& x : th) x.join();
-    // timed from a common start to the last thread's end (the threads are spawned and waiting
-    // first: spawning them inside the timed span read ~half the rate on a 16-CPU box)
-    double best = 1e30;
-    std::atomic<uint32_t> sink{0};
-    for (int r = 0; r < 2; ++r) {
-      th.clear();
-      std::atomic<int> ready{0};
-      std::atomic<bool> go{false};
-      std::atomic<int64_t> last_end{0};
-      for (int k = 0; k < t; ++k)
-        th.emplace_back([&, k] {
+        for (int r = 0; r < 2; ++r) {
           ready.fetch_add(1);
-          while (!go.load(std::memory_order_acquire)) std::this_thread::yield();
-          sink ^= ambrycrc_update(0, buf.get() + slice * (size_t)k, slice);
+          while (go.load(std::memory_order_acquire) <= r) std::this_thread::yield();
+          sink ^= ambrycrc_update(0, p, slice);
           const int64_t e = std::chrono::steady_clock::now().time_since_epoch().count();
-          int64_t cur = last_end.load();
-          while (e > cur && !last_end.compare_exchange_weak(cur, e)) {
+          int64_t cur = last_end[r].load();
+          while (e > cur && !last_end[r].compare_exchange_weak(cur, e)) {
           }
-        });
-      while (ready.load() < t) std::this_thread::yield();
+        }
+      });
+    double best = 1e30;
+    // (the main thread sleeps while it waits: spinning would take a CPU from the hashing threads)
+    for (int r = 0; r < 2; ++r) {
+      while (ready.load() < t * (r + 1)) std::this_thread::sleep_for(std::chrono::microseconds(20));
+      // the previous pass has ended in every thread once all have re-armed
       const int64_t t0 = std::chrono::steady_clock::now().time_since_epoch().count();
-      go.store(true, std::memory_order_release);
-      for (auto& x : th) x.join();
-      const double sec = std::chrono::duration<double>(std::chrono::steady_clock::duration(last_end.load() - t0)).count();
+      go.store(r + 1, std::memory_order_release);
+      if (r == 1) {
+        for (auto& x : th) x.join();
+      } else {
+        while (ready.load() < 2 * t) std::this_thread::sleep_for(std::chrono::microseconds(20));  // pass 0 done
+      }
+      const double sec = std::chrono::duration<double>(std::chrono::steady_clock::duration(last_end[r].load() - t0)).count();
       if (sec > 0) best = std::min(best, sec);
     }
     return (double)total / best / (double)(1ull << 30);
