@@ -209,7 +209,11 @@ class CopyPool {
     int t = 8;
     if (const char* e = getenv("AMBRYCRC_COPY_THREADS")) t = atoi(e);
     nthreads_ = std::max(1, std::min(t, 64));
-    for (int i = 1; i < nthreads_; ++i) workers_.emplace_back([this] { loop(); });
+    try {
+      for (int i = 1; i < nthreads_; ++i) workers_.emplace_back([this] { loop(); });
+    } catch (...) {  // fewer workers than asked (the C ABI does not throw): the parts queue on those started
+    }
+    nthreads_ = (int)workers_.size() + 1;
   }
   static void finish_one(Batch& b) {
     std::lock_guard<std::mutex> g(b.mu);
@@ -476,20 +480,26 @@ double host_cpu_gibps() {
     std::atomic<uint32_t> sink{0};
     std::vector<std::thread> th;
     th.reserve(t);
-    for (int k = 0; k < t; ++k)
-      th.emplace_back([&, k] {
-        uint8_t* p = buf.get() + slice * (size_t)k;
-        for (size_t i = 0; i < slice; ++i) p[i] = (uint8_t)(i * 131u + 7u + k);
-        for (int r = 0; r < 2; ++r) {
-          ready.fetch_add(1);
-          while (go.load(std::memory_order_acquire) <= r) std::this_thread::yield();
-          sink ^= ambrycrc_update(0, p, slice);
-          const int64_t e = std::chrono::steady_clock::now().time_since_epoch().count();
-          int64_t cur = last_end[r].load();
-          while (e > cur && !last_end[r].compare_exchange_weak(cur, e)) {
-          }
+    auto body = [&](int k) {
+      uint8_t* p = buf.get() + slice * (size_t)k;
+      for (size_t i = 0; i < slice; ++i) p[i] = (uint8_t)(i * 131u + 7u + k);
+      for (int r = 0; r < 2; ++r) {
+        ready.fetch_add(1);
+        while (go.load(std::memory_order_acquire) <= r) std::this_thread::yield();
+        sink ^= ambrycrc_update(0, p, slice);
+        const int64_t e = std::chrono::steady_clock::now().time_since_epoch().count();
+        int64_t cur = last_end[r].load();
+        while (e > cur && !last_end[r].compare_exchange_weak(cur, e)) {
         }
-      });
+      }
+    };
+    try {
+      for (int k = 0; k < t; ++k) th.emplace_back(body, k);
+    } catch (...) {  // no thread for every slice (the C ABI must not throw): release them, no estimate
+      go.store(2, std::memory_order_release);
+      for (auto& x : th) x.join();
+      return 1.0;
+    }
     double best = 1e30;
     // (the main thread sleeps while it waits: spinning would take a CPU from the hashing threads)
     for (int r = 0; r < 2; ++r) {
@@ -700,8 +710,14 @@ int ambrycrc_batch_cpu(const void* const* ptrs, const uint64_t* lens, const uint
   if (rc) return rc;
   std::vector<std::thread> th;
   th.reserve(threads - 1);
-  for (int t = 1; t < threads; ++t)
-    if (cut[t] < cut[t + 1]) th.emplace_back(run, cut[t], cut[t + 1]);
+  for (int t = 1; t < threads; ++t) {
+    if (cut[t] >= cut[t + 1]) continue;
+    try {
+      th.emplace_back(run, cut[t], cut[t + 1]);
+    } catch (...) {  // no thread (the C ABI does not throw): the part runs here
+      run(cut[t], cut[t + 1]);
+    }
+  }
   run(cut[0], cut[1]);
   for (auto& t : th) t.join();
   return AMBRYCRC_OK;
@@ -989,10 +1005,15 @@ int ambrycrc_batch_multi(const void* const* ptrs, const uint64_t* lens, const ui
   for (int r = 0; r < ndev; ++r) {
     const size_t a = cut[r], b = cut[r + 1];
     if (a >= b) continue;
-    th.emplace_back([&, r, a, b] {
+    auto part = [&, r, a, b] {
       rc[r] = batch_host_gpu(ctx_for(dev[r]), ptrs + a, lens + a, crc_in ? crc_in + a : nullptr, out + a, b - a, dev[r],
                              pinned);
-    });
+    };
+    try {
+      th.emplace_back(part);
+    } catch (...) {  // no thread (the C ABI does not throw): this device's share runs here
+      part();
+    }
   }
   for (auto& t : th) t.join();
   for (int r = 0; r < ndev; ++r)

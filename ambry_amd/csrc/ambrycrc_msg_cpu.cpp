@@ -273,8 +273,14 @@ void split_run(size_t m, int threads, W weight, F fn) {
   for (int t = 1; t < threads; ++t)
     cut[t] = (size_t)(std::lower_bound(pre.begin(), pre.end(), pre[m] * (uint64_t)t / (uint64_t)threads) - pre.begin());
   std::vector<std::thread> th;
-  for (int t = 1; t < threads; ++t)
-    if (cut[t] < cut[t + 1]) th.emplace_back(fn, cut[t], cut[t + 1]);
+  for (int t = 1; t < threads; ++t) {
+    if (cut[t] >= cut[t + 1]) continue;
+    try {
+      th.emplace_back(fn, cut[t], cut[t + 1]);
+    } catch (...) {  // no thread (the C ABI does not throw): the part runs here
+      fn(cut[t], cut[t + 1]);
+    }
+  }
   fn(cut[0], cut[1]);
   for (auto& x : th) x.join();
 }
