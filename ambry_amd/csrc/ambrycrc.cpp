@@ -8,6 +8,9 @@
 #include <string.h>
 
 #include <sched.h>
+#if defined(__x86_64__)
+#include <emmintrin.h>
+#endif
 
 #include <algorithm>
 #include <chrono>
@@ -460,61 +463,58 @@ int host_cpu_threads() {
 
 double host_cpu_gibps() {
   // The CPU leg's rate with all its threads at once, measured once per process: each thread hashes
-  // its own slice of a buffer larger than the L3 (16 MiB a thread, 512 MiB at most), twice, and the
-  // faster pass counts. A single thread times threads (round 5's first form) read the L3-fed rate:
-  // 662 GiB/s estimated against 262 measured on 16 CPUs, where the threads share DRAM bandwidth.
+  // its own slice (16 MiB a thread, 512 MiB at most), written with nontemporal stores so that the
+  // timed pass reads DRAM, not the L3 (16 threads spread over CCDs hold a 16 MiB slice each in their
+  // CCD's 32 MiB: 679 GiB/s estimated against 246 measured, r05ao). A single thread times threads
+  // (round 5's first form) read the L3-fed rate too: 662 against 262 on 16 CPUs.
   static const double rate = [] {
     const int t = host_cpu_threads();
     const size_t slice = std::min<size_t>(16u << 20, ((size_t)512 << 20) / (size_t)t) & ~size_t(4095);
     const size_t total = slice * (size_t)t;
     std::unique_ptr<uint8_t[]> buf(new (std::nothrow) uint8_t[total]);  // not zero-filled: first touch below
     if (!buf) return 1.0;
-    // Each thread first-touches its own slice, then hashes it twice from a common start (all threads
-    // spawned and waiting: spawning inside the timed span read ~half the rate on a 16-CPU box);
-    // each pass is timed from its start to the last thread's end.
+    // Each thread first-touches its own slice, then hashes it once from a common start (all threads
+    // spawned and waiting: spawning inside the timed span read ~half the rate on a 16-CPU box),
+    // timed from the start to the last thread's end. (A second pass would read the L3.)
     std::atomic<int> ready{0};
-    std::atomic<int> go{0};  // pass number released
-    std::atomic<int64_t> last_end[2];
-    last_end[0] = 0;
-    last_end[1] = 0;
+    std::atomic<int> go{0};
+    std::atomic<int64_t> last_end{0};
     std::atomic<uint32_t> sink{0};
     std::vector<std::thread> th;
     th.reserve(t);
     auto body = [&](int k) {
       uint8_t* p = buf.get() + slice * (size_t)k;
+#if defined(__x86_64__)
+      for (size_t i = 0; i < slice; i += 16) {  // slice and buffer 16-B aligned (new[] of >= 16 MiB, 4 KiB slices)
+        const __m128i v = _mm_set_epi32((int)(i * 131u + k), (int)(i * 7u), (int)(i ^ 0x5bd1e995u), (int)i);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(p + i), v);
+      }
+      _mm_sfence();
+#else
       for (size_t i = 0; i < slice; ++i) p[i] = (uint8_t)(i * 131u + 7u + k);
-      for (int r = 0; r < 2; ++r) {
-        ready.fetch_add(1);
-        while (go.load(std::memory_order_acquire) <= r) std::this_thread::yield();
-        sink ^= ambrycrc_update(0, p, slice);
-        const int64_t e = std::chrono::steady_clock::now().time_since_epoch().count();
-        int64_t cur = last_end[r].load();
-        while (e > cur && !last_end[r].compare_exchange_weak(cur, e)) {
-        }
+#endif
+      ready.fetch_add(1);
+      while (go.load(std::memory_order_acquire) == 0) std::this_thread::yield();
+      sink ^= ambrycrc_update(0, p, slice);
+      const int64_t e = std::chrono::steady_clock::now().time_since_epoch().count();
+      int64_t cur = last_end.load();
+      while (e > cur && !last_end.compare_exchange_weak(cur, e)) {
       }
     };
     try {
       for (int k = 0; k < t; ++k) th.emplace_back(body, k);
     } catch (...) {  // no thread for every slice (the C ABI must not throw): release them, no estimate
-      go.store(2, std::memory_order_release);
+      go.store(1, std::memory_order_release);
       for (auto& x : th) x.join();
       return 1.0;
     }
-    double best = 1e30;
     // (the main thread sleeps while it waits: spinning would take a CPU from the hashing threads)
-    for (int r = 0; r < 2; ++r) {
-      while (ready.load() < t * (r + 1)) std::this_thread::sleep_for(std::chrono::microseconds(20));
-      // the previous pass has ended in every thread once all have re-armed
-      const int64_t t0 = std::chrono::steady_clock::now().time_since_epoch().count();
-      go.store(r + 1, std::memory_order_release);
-      if (r == 1) {
-        for (auto& x : th) x.join();
-      } else {
-        while (ready.load() < 2 * t) std::this_thread::sleep_for(std::chrono::microseconds(20));  // pass 0 done
-      }
-      const double sec = std::chrono::duration<double>(std::chrono::steady_clock::duration(last_end[r].load() - t0)).count();
-      if (sec > 0) best = std::min(best, sec);
-    }
+    while (ready.load() < t) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    const int64_t t0 = std::chrono::steady_clock::now().time_since_epoch().count();
+    go.store(1, std::memory_order_release);
+    for (auto& x : th) x.join();
+    const double best = std::chrono::duration<double>(std::chrono::steady_clock::duration(last_end.load() - t0)).count();
+    if (!(best > 0)) return 1.0;
     return (double)total / best / (double)(1ull << 30);
   }();
   return rate;
