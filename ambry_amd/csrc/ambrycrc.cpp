@@ -463,36 +463,40 @@ int host_cpu_threads() {
 
 double host_cpu_gibps() {
   // The CPU leg's rate with all its threads at once, measured once per process: each thread hashes
-  // its own slice (16 MiB a thread, 512 MiB at most), written with nontemporal stores so that the
-  // timed pass reads DRAM, not the L3 (16 threads spread over CCDs hold a 16 MiB slice each in their
-  // CCD's 32 MiB: 679 GiB/s estimated against 246 measured, r05ao). A single thread times threads
-  // (round 5's first form) read the L3-fed rate too: 662 against 262 on 16 CPUs.
+  // a slice (16 MiB a thread, 512 MiB at most) of a buffer the calling thread wrote with nontemporal
+  // stores -- so the timed pass reads DRAM, not the L3, from the pages one writer placed, as a
+  // caller's buffer is. Slices each thread wrote itself read 440-679 GiB/s against 172-246 measured
+  // on a 2 GiB sample the main thread wrote (r05ao, r05aq: 16 threads, their own slices near them
+  // and in their CCDs' L3); a single thread times threads (round 5's first form): 662 against 262.
   static const double rate = [] {
     const int t = host_cpu_threads();
     const size_t slice = std::min<size_t>(16u << 20, ((size_t)512 << 20) / (size_t)t) & ~size_t(4095);
     const size_t total = slice * (size_t)t;
     std::unique_ptr<uint8_t[]> buf(new (std::nothrow) uint8_t[total]);  // not zero-filled: first touch below
     if (!buf) return 1.0;
-    // Each thread first-touches its own slice, then hashes it once from a common start (all threads
-    // spawned and waiting: spawning inside the timed span read ~half the rate on a 16-CPU box),
-    // timed from the start to the last thread's end. (A second pass would read the L3.)
+    // The threads hash their slices once from a common start (all spawned and waiting: spawning
+    // inside the timed span read ~half the rate on a 16-CPU box), timed from the start to the last
+    // thread's end. (A second pass would read the L3.)
     std::atomic<int> ready{0};
     std::atomic<int> go{0};
     std::atomic<int64_t> last_end{0};
     std::atomic<uint32_t> sink{0};
     std::vector<std::thread> th;
     th.reserve(t);
-    auto body = [&](int k) {
-      uint8_t* p = buf.get() + slice * (size_t)k;
+    {
+      uint8_t* p = buf.get();
 #if defined(__x86_64__)
-      for (size_t i = 0; i < slice; i += 16) {  // slice and buffer 16-B aligned (new[] of >= 16 MiB, 4 KiB slices)
-        const __m128i v = _mm_set_epi32((int)(i * 131u + k), (int)(i * 7u), (int)(i ^ 0x5bd1e995u), (int)i);
+      for (size_t i = 0; i < total; i += 16) {  // 16-B aligned (new[] of >= 16 MiB, 4 KiB slices)
+        const __m128i v = _mm_set_epi32((int)(i * 131u), (int)(i * 7u), (int)(i ^ 0x5bd1e995u), (int)i);
         _mm_stream_si128(reinterpret_cast<__m128i*>(p + i), v);
       }
       _mm_sfence();
 #else
-      for (size_t i = 0; i < slice; ++i) p[i] = (uint8_t)(i * 131u + 7u + k);
+      for (size_t i = 0; i < total; ++i) p[i] = (uint8_t)(i * 131u + 7u);
 #endif
+    }
+    auto body = [&](int k) {
+      const uint8_t* p = buf.get() + slice * (size_t)k;
       ready.fetch_add(1);
       while (go.load(std::memory_order_acquire) == 0) std::this_thread::yield();
       sink ^= ambrycrc_update(0, p, slice);

@@ -1878,7 +1878,8 @@ __global__ __launch_bounds__(64 * W) void region_fused_kernel(FusedArgs f) {
     uint32_t st;
     uint64_t mend;
     const region::TabR tr{reinterpret_cast<const uint8_t*>(g_lds_runs), (lane & 31u) << 2};
-    region::process_message(f.a, f.g, tbl, tr, nib, have, i, lane, st, mend, [&](uint64_t pos, uint64_t end) -> bool {
+    constexpr bool kEnds = COPY ? AMBRY_FUSED_ENDS >= 1 : AMBRY_FUSED_ENDS >= 2;
+    region::process_message<kEnds>(f.a, f.g, tbl, tr, nib, have, i, lane, st, mend, [&](uint64_t pos, uint64_t end) -> bool {
       // the lane's message ends at pos + end (base-relative): before the share, or past it (the
       // copy form: more than kDirectSpan past it; its records past the share are hashed from the
       // bytes) -> the tail's. (Measured: the copy form 0.713 -> 0.695 ms per 262,144 4 KiB PUTs;

@@ -298,6 +298,82 @@ __device__ __forceinline__ uint32_t record_crc(const Tab& t, const uint32_t* __r
   return ~V;
 }
 
+// record_crc in two steps, for the one-pass processors (AMBRY_FUSED_ENDS): record_ends hashes the
+// head and tail runs from the bytes -- right after the parse, whose loads fetched those lines, and
+// before the wait for the run sums, which the streamers' nontemporal loads outlast in L2 -- and
+// record_crc_from_ends does the rest once the sums exist. Records under 4 bytes: the CRC itself
+// in h.
+struct RecEnds {
+  uint32_t h, t;
+};
+template <class Tab>
+__device__ __forceinline__ RecEnds record_ends(const Tab& t, const uint32_t* __restrict__ nib,
+                                               const uint8_t* __restrict__ base, uint64_t pa, uint64_t len) {
+  if (len == 0) return RecEnds{0u, 0u};
+  const uint64_t pb = pa + len;
+  if (len < 4) {
+    uint32_t c = 0xFFFFFFFFu;
+    for (uint64_t i = pa; i < pb; ++i) c = t.t0((c ^ base[i]) & 0xffu) ^ (c >> 8);
+    return RecEnds{~c, 0u};
+  }
+  const uint64_t A0 = pa & ~uint64_t(63), B1 = (pb + 63) & ~uint64_t(63);
+  const int64_t n = (int64_t)((B1 - A0) >> 6);
+  const int lo = (int)(pa - A0), hi = pb - A0 < 64 ? (int)(pb - A0) : 64;
+  const int tin = hi - lo;
+  const bool tail_bytes = n >= 2 && (pb & 63u) != 0;
+  const int thi = (int)(pb - (B1 - 64));
+  u32x4 hw[4], tw[4];
+  load_run(base, A0, lo, hi, hw);
+  load_run(base, B1 - 64, 0, tail_bytes ? thi : 0, tw);
+  uint32_t H = hash_run(t, nib, hw, lo, hi, tin < 4 ? tin : 4);
+  if (tin < 4) H ^= 0xFFFFFFFFu >> (8 * tin);
+  return RecEnds{H, tail_bytes ? hash_run(t, nib, tw, 0, thi, 0) : 0u};
+}
+
+__device__ __forceinline__ uint32_t record_crc_from_ends(const uint32_t* __restrict__ nib,
+                                                         const uint32_t* __restrict__ rk, uint64_t pa, uint64_t len,
+                                                         RecEnds e) {
+  if (len < 4) return e.h;
+  const uint64_t pb = pa + len;
+  const uint64_t A0 = pa & ~uint64_t(63), B1 = (pb + 63) & ~uint64_t(63);
+  const int64_t n = (int64_t)((B1 - A0) >> 6), k0 = (int64_t)(A0 >> 6);
+  const bool tail_bytes = n >= 2 && (pb & 63u) != 0;
+  const int64_t ng = (n + 3) >> 2, e0 = k0 + n - 4 * ng;
+  u32x4 nxt[4];
+  load_groups(rk, e0, 0, ng, nxt);
+  const int32_t n32 = (int32_t)n, ng32 = (int32_t)ng, rb = n32 - 4 * ng32;
+  const uint32_t rlast = tail_bytes ? rk[k0 + n - 1] : 0u;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) nxt[0][q] = rb + q < 0 ? 0u : rb + q == 0 ? e.h : nxt[0][q];
+  uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+  for (int32_t g = 0; g < ng32; g += 4) {
+    u32x4 r[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) r[u] = nxt[u];
+    if (g + 4 < ng32) load_groups(rk, e0, g + 4, ng, nxt);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (g + u < ng32) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t nv = nmul(nib, s0, kP256) ^ r[u][q];
+          s0 = s1;
+          s1 = s2;
+          s2 = s3;
+          s3 = nv;
+        }
+      }
+    }
+  }
+  s3 ^= e.t ^ rlast;
+  uint32_t V = s3 ^ nmul(nib, s2 ^ nmul(nib, s1 ^ nmul(nib, s0, kP64), kP64), kP64);
+  const uint32_t d = (uint32_t)(B1 - pb);
+#pragma unroll
+  for (uint32_t k = 0; k < kInvPowSets; ++k)
+    if (d & (1u << k)) V = nmul(nib, V, kInv0 + k);
+  return ~V;
+}
+
 // LDS sets: x^(8*64*2^k) for k = 0..5 (the tree), x^(8*4096) (the fold): the image's POW[6..12].
 // x^(8*2^(6+s)) for s = 0..10 (the image's POW[6..16]): record_crc_direct's tree (s = 0..5,
 // 64-B runs) and fold (s = 6); record_crc_runs_wave's in-lane fold of 64-B runs (s = 0), tree of

@@ -204,7 +204,10 @@ __device__ __forceinline__ void process_message_direct(const MsgArgs& a, const R
 // the next CU's share) and is hashed by the wave straight from the region's bytes
 // (record_crc_direct with dn's sets), without waiting -- so the message that straddles a share's
 // end is finished by its own share's processor instead of the tail kernel.
-template <class Tab, class Keep, class Wait>
+// ENDS: the lane's own records' head / tail runs hashed right after the parse (record_ends), the
+// rest after the wait (AMBRY_FUSED_ENDS: the copy form's 4 KiB PUTs 617 -> 609 us, the verify
+// form's 371 -> 392 at 4 KiB blobs, profiles/r05aq_fused_ends_ab.txt).
+template <bool ENDS = false, class Tab, class Keep, class Wait>
 __device__ __forceinline__ void process_message(const MsgArgs& a, const RegionArgs& g,
                                                 const uint32_t* __restrict__ t, const Tab& tr,
                                                 const uint32_t* __restrict__ nib, bool have, uint64_t i,
@@ -274,6 +277,14 @@ __device__ __forceinline__ void process_message(const MsgArgs& a, const RegionAr
   }
   longs |= direct;
   const uint32_t own_long = longs;
+  // ENDS: the lane's own records' head / tail runs now, while the parse's lines are in L2
+  RecEnds ends[kMsgSlots];
+#pragma unroll
+  for (int k = 0; k < kMsgSlots; ++k) {
+    ends[k] = RecEnds{0u, 0u};
+    if (ENDS && have && jl[k] != 0 && !(own_long & (1u << k)))
+      ends[k] = record_ends(tr, nib, g.base, g.reg0 + jo[k], jl[k]);
+  }
   for (;;) {
     const uint64_t ball = __ballot(longs != 0);
     if (ball == 0) break;
@@ -312,7 +323,9 @@ __device__ __forceinline__ void process_message(const MsgArgs& a, const RegionAr
 #pragma unroll
   for (int k = 0; k < kMsgSlots; ++k) {
     if (!have || jl[k] == 0 || (own_long & (1u << k))) continue;
-    if (record_crc(tr, nib, g.base, rk, g.reg0 + jo[k], jl[k]) != ex[k]) status |= record_bit(k);
+    const uint32_t c = ENDS ? record_crc_from_ends(nib, rk, g.reg0 + jo[k], jl[k], ends[k])
+                            : record_crc(tr, nib, g.base, rk, g.reg0 + jo[k], jl[k]);
+    if (c != ex[k]) status |= record_bit(k);
   }
   if (have) {
     a.status[i] = status;
