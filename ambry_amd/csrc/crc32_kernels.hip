@@ -1879,6 +1879,7 @@ __global__ __launch_bounds__(64 * W) void region_fused_kernel(FusedArgs f) {
     uint64_t mend;
     const region::TabR tr{reinterpret_cast<const uint8_t*>(g_lds_runs), (lane & 31u) << 2};
     constexpr bool kEnds = COPY ? AMBRY_FUSED_ENDS >= 1 : AMBRY_FUSED_ENDS >= 2;
+    region::FastPre pre{false, 0};  // COPY: the fast path's shape checks, right after the parse
     region::process_message<kEnds>(f.a, f.g, tbl, tr, nib, have, i, lane, st, mend, [&](uint64_t pos, uint64_t end) -> bool {
       // the lane's message ends at pos + end (base-relative): before the share, or past it (the
       // copy form: more than kDirectSpan past it; its records past the share are hashed from the
@@ -1889,9 +1890,10 @@ __global__ __launch_bounds__(64 * W) void region_fused_kernel(FusedArgs f) {
         if (at < f.a.m) f.defer[at] = (uint32_t)i;  // (unsorted offsets may defer more: ctl[0] covers them)
         return false;
       }
+      if constexpr (COPY) pre = region::transform_fast_pre(f, tbl, i, end);
       return true;
     }, [&](uint64_t need) { wait_for(need); }, dn, COPY ? s_hi : ~0ull);
-    if constexpr (COPY) region::transform_fast(f, tbl, st != ~0u, i, st, mend);  // `out` untouched
+    if constexpr (COPY) region::transform_fast_post(f, st != ~0u, i, st, mend, pre);  // `out` untouched
   }
 #if AMBRY_FUSED_PROBE == 2
   if (lane == 0) atomicMax(&g_fused_t[3 * blockIdx.x + 2], (unsigned long long)__builtin_amdgcn_s_memrealtime());

@@ -344,45 +344,69 @@ __device__ __forceinline__ void process_message(const MsgArgs& a, const RegionAr
 // out + (offset - msg_off[0]); this records the header's new life version and CRC in patch[i]
 // (applied by region_patch_kernel once the copy is complete) and writes the outputs.
 // Anything else sets *xfail: the general path then redoes the whole batch.
-__device__ __forceinline__ void transform_fast(const FusedArgs& f, const uint32_t* __restrict__ t, bool have,
-                                               uint64_t i, uint32_t st, uint64_t end) {
+// In two steps: transform_fast_pre reads the message's shape (header, properties, blob record
+// version) and computes the patch -- the one-pass kernel calls it right after the parse, while
+// those lines are in L2, instead of after the wait for the run sums -- and transform_fast_post
+// decides with the verify status.
+struct FastPre {
+  bool ok;
+  uint64_t patch;
+};
+__device__ __forceinline__ FastPre transform_fast_pre(const FusedArgs& f, const uint32_t* __restrict__ t, uint64_t i,
+                                                      uint64_t end) {
+  const MsgArgs& a = f.a;
+  const uint64_t off = a.msg_off[i];
+  FastPre r{false, 0};
+  // not verified yet: every read below stays inside the message's parsed extent
+  if (off > a.region_len || a.region_len - off < end || end < 40) return r;
+  const uint8_t* p = a.region + off;
+  HeaderWords hw = load_header(p, 40);
+  if (be16(p) != 3) return r;
+  int32_t rel[kMsgSlots];
+#pragma unroll
+  for (int k = 0; k < kMsgSlots; ++k) rel[k] = (int32_t)be32_w0(hw, 3 + k);
+  bool ok = rel[2] == -1 && rel[1] >= 0 && rel[3] >= 0 && rel[4] >= 0 && (int64_t)rel[3] >= (int64_t)rel[1] + 10 &&
+            (uint64_t)rel[3] <= end && (uint64_t)rel[4] + 2 <= end;
+  if (ok) ok = be16(p + rel[4]) == 3;
+  if (ok) {  // properties already canonical VERSION_5 bytes, every string ASCII (record_fields.h)
+    const uint32_t stored = (uint32_t)(rel[3] - rel[1] - 10);
+    PropsFields pf;
+    ok = props_parse<true>(p + rel[1] + 2, stored, &pf) == 0 && pf.ascii && props_fix_of(pf, stored).version == 0;
+  }
+  if (ok && f.life && f.life[i] < 0) ok = false;  // not a life version a V3 header holds
+  if (ok && f.life) {  // the index's life version (MessageInfo.getLifeVersion), header CRC recomputed
+    const uint32_t lv = (uint16_t)f.life[i];
+    hw.w[0] = (hw.w[0] & 0xFFFFu) | (((lv >> 8) | ((lv & 0xFFu) << 8)) << 16);
+    r.patch = (uint64_t)lv | ((uint64_t)header_crc(hw, 32, t) << 32);
+  }
+  r.ok = ok;
+  return r;
+}
+
+__device__ __forceinline__ void transform_fast_post(const FusedArgs& f, bool have, uint64_t i, uint32_t st,
+                                                    uint64_t end, FastPre pre) {
   if (!have || st == ~0u) return;  // no message, or deferred to the tail kernel
   const MsgArgs& a = f.a;
   const uint64_t off = a.msg_off[i], off0 = a.msg_off[0];
-  bool ok = st == 0 && end != 0 && off >= off0 && off - off0 + end <= f.out_cap &&
-            (i + 1 == a.m || a.msg_off[i + 1] == off + end);
-  const uint8_t* p = a.region + off;
-  HeaderWords hw;
-  if (ok) {  // verified: the header and every record lie inside the region
-    hw = load_header(p, 40);
-    ok = be16(p) == 3;
-  }
-  if (ok) {
-    int32_t rel[kMsgSlots];
-#pragma unroll
-    for (int k = 0; k < kMsgSlots; ++k) rel[k] = (int32_t)be32_w0(hw, 3 + k);
-    ok = rel[2] == -1 && rel[1] != -1 && rel[3] != -1 && rel[4] != -1 && be16(p + rel[4]) == 3;
-    if (ok) {  // properties already canonical VERSION_5 bytes, every string ASCII (record_fields.h)
-      const uint32_t stored = (uint32_t)(rel[3] - rel[1] - 10);
-      PropsFields pf;
-      ok = props_parse<true>(p + rel[1] + 2, stored, &pf) == 0 && pf.ascii && props_fix_of(pf, stored).version == 0;
-    }
-  }
-  if (ok && f.life && f.life[i] < 0) ok = false;  // not a life version a V3 header holds
+  const bool ok = pre.ok && st == 0 && end != 0 && off >= off0 && off - off0 + end <= f.out_cap &&
+                  (i + 1 == a.m || a.msg_off[i + 1] == off + end);
   if (!ok) {
     atomicOr(f.xfail, 1u);
     return;
   }
-  if (f.life) {  // the index's life version (MessageInfo.getLifeVersion), header CRC recomputed
-    const uint32_t lv = (uint16_t)f.life[i];
-    hw.w[0] = (hw.w[0] & 0xFFFFu) | (((lv >> 8) | ((lv & 0xFFu) << 8)) << 16);
-    // region_patch_kernel writes it into `out` after the copy has completed (kernel order, no
-    // store-ordering argument between this wave and the waves copying the header's bytes)
-    f.patch[i] = (uint64_t)lv | ((uint64_t)header_crc(hw, 32, t) << 32);
-  }
+  // region_patch_kernel writes the patch into `out` after the copy has completed (kernel order, no
+  // store-ordering argument between this wave and the waves copying the header's bytes)
+  if (f.life) f.patch[i] = pre.patch;
   if (f.out_off) f.out_off[i] = off - off0;
   f.out_len[i] = end;
   f.xstatus[i] = 0;
+}
+
+__device__ __forceinline__ void transform_fast(const FusedArgs& f, const uint32_t* __restrict__ t, bool have,
+                                               uint64_t i, uint32_t st, uint64_t end) {
+  if (!have || st == ~0u) return;
+  const FastPre pre = st == 0 && end != 0 ? transform_fast_pre(f, t, i, end) : FastPre{false, 0};
+  transform_fast_post(f, have, i, st, end, pre);
 }
 
 }  // namespace region
