@@ -45,9 +45,6 @@
 #ifndef AMBRY_FUSED_NT  // one-pass region kernel: nontemporal streamer loads (0: temporal, the lines stay in L2)
 #define AMBRY_FUSED_NT 1
 #endif
-#ifndef AMBRY_FUSED_LEAD  // one-pass processors: parse a batch only once the stream is within this many bytes (0: at once)
-#define AMBRY_FUSED_LEAD 0
-#endif
 #ifndef AMBRY_FUSED_ENDS  // one-pass processors hash a record's head / tail runs right after the parse, before
 #define AMBRY_FUSED_ENDS 1  // the wait for its run sums: 0 = never, 1 = the transform's copy form, 2 = also the verify
 #endif
@@ -107,7 +104,7 @@
   X(AMBRY_REGION_BPC_SMALL, 2) X(AMBRY_REGION_AUX, 7) X(AMBRY_HOST_VERIFY_CPU_PCT, 50) X(AMBRY_HOST_XFORM_CPU_PCT, 25)                                                                          \
   X(AMBRY_FUSED_PROC, 0)                                                                                      \
   X(AMBRY_FUSED_WAVES_VERIFY, 12)                                                                               \
-  X(AMBRY_FUSED_WAVES_COPY, 8) X(AMBRY_FUSED_NT, 1) X(AMBRY_FUSED_ENDS, 1) X(AMBRY_FUSED_LEAD, 0)                                                                 \
+  X(AMBRY_FUSED_WAVES_COPY, 8) X(AMBRY_FUSED_NT, 1) X(AMBRY_FUSED_ENDS, 1)                                                                 \
   X(AMBRY_GRP_PRIO, 0) X(AMBRY_GRP_IL, 4) X(AMBRY_C0_G, 2) X(AMBRY_C0_NB, 8) X(AMBRY_C1_MAX, 1024)           \
   X(AMBRY_RUNS_STORE_NT, 0) X(AMBRY_RUNS_NT, 1) X(AMBRY_RUNS_GIL, 1) X(AMBRY_PLAN_PER_BLOCK, 2048) X(AMBRY_DEFAULT_VARIANT, 29) \
   X(AMBRY_REGION_PROBE, 0) X(AMBRY_RUNS_PROBE, 0) X(AMBRY_FUSED_PROBE, 0)

@@ -1878,10 +1878,6 @@ __global__ __launch_bounds__(64 * W) void region_fused_kernel(FusedArgs f) {
     uint32_t st;
     uint64_t mend;
     const region::TabR tr{reinterpret_cast<const uint8_t*>(g_lds_runs), (lane & 31u) << 2};
-    if constexpr (AMBRY_FUSED_LEAD > 0) {  // A/B: parse no further than LEAD bytes ahead of the stream
-      const uint64_t p0 = msg_pos(f, b);
-      if (p0 > s_lo + AMBRY_FUSED_LEAD) wait_for(p0 - AMBRY_FUSED_LEAD);
-    }
     constexpr bool kEnds = COPY ? AMBRY_FUSED_ENDS >= 1 : AMBRY_FUSED_ENDS >= 2;
     region::FastPre pre{false, 0};  // COPY: the fast path's shape checks, right after the parse
     region::process_message<kEnds>(f.a, f.g, tbl, tr, nib, have, i, lane, st, mend, [&](uint64_t pos, uint64_t end) -> bool {
