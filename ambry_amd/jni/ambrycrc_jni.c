@@ -29,6 +29,10 @@
  *                               ByteBuffer out, long[] outLen)
  *   void nativeTransformMessages(ByteBuffer region, long[] offsets, short[] lifeVersions, int headerVersion,
  *                                ByteBuffer out, long[] outOffsets, long[] outLens, int[] status, int device)
+ *   void nativePutCrcs(ByteBuffer[] fields, ByteBuffer[] prefixes, int[] blobCrc, long[] blobLen,
+ *                      int[] wireOut, int[] recordOut)                  PutRequest.java:238-283
+ *   void nativeRangeChecksums(ByteBuffer file, long[] first, long[] second, int[] out, int device)
+ *                                                                      FileStore.java:567-595
  *   int  nativeSetHostPolicy(int device, int policy)
  *   int  nativeHostRates(int device, double[] out)
  *   int  nativeLastHostPath(int device)
@@ -201,27 +205,19 @@ JNIEXPORT void JNICALL JNI_FN(nativeVerifyMessages)(JNIEnv* env, jclass cls, job
   raise(env, rc);
 }
 
-/* The loop of PutOperation.PutChunk.verifyCRC (PutOperation.java:2041-2043) over a Netty
- * CompositeByteBuf's nioBuffers(), all direct: one JNI crossing for the whole gather list
- * (ambrycrc_update_iov). Each buffer's position..limit is used; the Java side consumes them. */
-JNIEXPORT jint JNICALL JNI_FN(nativeUpdateDirectAll)(JNIEnv* env, jclass cls, jint crc, jobjectArray bufs) {
-  (void)cls;
-  if (!bufs) return raise(env, AJC_ENULL), crc;
-  const jsize n = (*env)->GetArrayLength(env, bufs);
-  if (n == 0) return crc;
+/* position..limit of buffers[0 .. n) (each non-null and direct) into ptrs / lens; a status. */
+static int gather_list(JNIEnv* env, jobjectArray bufs, jsize n, const void** ptrs, size_t* lens) {
+  if (n == 0) return AJC_OK;
   jclass bc = (*env)->FindClass(env, "java/nio/Buffer");
   jmethodID mpos = bc ? (*env)->GetMethodID(env, bc, "position", "()I") : NULL;
   jmethodID mlim = bc ? (*env)->GetMethodID(env, bc, "limit", "()I") : NULL;
-  if (!mpos || !mlim) return raise(env, AMBRYCRC_EINVAL), crc;
+  if (!mpos || !mlim) return AMBRYCRC_EINVAL;
   const uint8_t** bases = (const uint8_t**)malloc(sizeof(void*) * (size_t)n);
   int64_t* caps = (int64_t*)malloc(sizeof(int64_t) * (size_t)n);
   jint* jpos = (jint*)malloc(sizeof(jint) * (size_t)n);
   jint* jlim = (jint*)malloc(sizeof(jint) * (size_t)n);
-  const void** ptrs = (const void**)malloc(sizeof(void*) * (size_t)n);
-  size_t* lens = (size_t*)malloc(sizeof(size_t) * (size_t)n);
   int st = AMBRYCRC_ENOMEM;
-  jint result = crc;
-  if (bases && caps && jpos && jlim && ptrs && lens) {
+  if (bases && caps && jpos && jlim) {
     st = AJC_OK;
     for (jsize i = 0; i < n && st == AJC_OK; ++i) {
       jobject b = (*env)->GetObjectArrayElement(env, bufs, i);
@@ -237,16 +233,137 @@ JNIEXPORT jint JNICALL JNI_FN(nativeUpdateDirectAll)(JNIEnv* env, jclass cls, ji
     }
     size_t bad = 0;
     if (st == AJC_OK) st = ajc_iov_args((size_t)n, bases, caps, jpos, jlim, ptrs, lens, &bad);
-    if (st == AJC_OK) result = (jint)ambrycrc_update_iov((uint32_t)crc, ptrs, lens, (size_t)n);
   }
   free(bases);
   free(caps);
   free(jpos);
   free(jlim);
+  return st;
+}
+
+/* The loop of PutOperation.PutChunk.verifyCRC (PutOperation.java:2041-2043) over a Netty
+ * CompositeByteBuf's nioBuffers(), all direct: one JNI crossing for the whole gather list
+ * (ambrycrc_update_iov). Each buffer's position..limit is used; the Java side consumes them. */
+JNIEXPORT jint JNICALL JNI_FN(nativeUpdateDirectAll)(JNIEnv* env, jclass cls, jint crc, jobjectArray bufs) {
+  (void)cls;
+  if (!bufs) return raise(env, AJC_ENULL), crc;
+  const jsize n = (*env)->GetArrayLength(env, bufs);
+  if (n == 0) return crc;
+  const void** ptrs = (const void**)malloc(sizeof(void*) * (size_t)n);
+  size_t* lens = (size_t*)malloc(sizeof(size_t) * (size_t)n);
+  jint result = crc;
+  int st = AMBRYCRC_ENOMEM;
+  if (ptrs && lens) {
+    st = gather_list(env, bufs, n, ptrs, lens);
+    if (st == AJC_OK) result = (jint)ambrycrc_update_iov((uint32_t)crc, ptrs, lens, (size_t)n);
+  }
   free(ptrs);
   free(lens);
   raise(env, st);
   return result;
+}
+
+/* NativeCrc32.putCrcs -> ambrycrc_put_crcs: PutRequest.prepareBuffer's wire CRC
+ * (PutRequest.java:238-283) and the Blob_Format_V3 record CRC (MessageFormatRecord.java:1789-1795,
+ * PutMessageFormatInputStream.java:116-120) of n PUTs from their known blob CRCs, by GF(2) combine.
+ * fields[i] / prefixes[i]: direct buffers, position..limit used (not consumed). */
+JNIEXPORT void JNICALL JNI_FN(nativePutCrcs)(JNIEnv* env, jclass cls, jobjectArray fields, jobjectArray prefixes,
+                                             jintArray blob_crc, jlongArray blob_len, jintArray wire_out,
+                                             jintArray record_out) {
+  (void)cls;
+  if (!blob_crc || !blob_len) {
+    raise(env, AJC_ENULL);
+    return;
+  }
+  const jsize n = (*env)->GetArrayLength(env, blob_crc);
+  if (raise(env, ajc_put_lengths(n, (*env)->GetArrayLength(env, blob_len),
+                                 fields ? (*env)->GetArrayLength(env, fields) : -1,
+                                 wire_out ? (*env)->GetArrayLength(env, wire_out) : -1,
+                                 prefixes ? (*env)->GetArrayLength(env, prefixes) : -1,
+                                 record_out ? (*env)->GetArrayLength(env, record_out) : -1)))
+    return;
+  if (n == 0 || (!wire_out && !record_out)) return;
+  uint32_t* crc = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n);
+  uint64_t* blen = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)n);
+  const void** fp = (const void**)malloc(sizeof(void*) * (size_t)n);
+  size_t* fl = (size_t*)malloc(sizeof(size_t) * (size_t)n);
+  const void** pp = (const void**)malloc(sizeof(void*) * (size_t)n);
+  size_t* pl = (size_t*)malloc(sizeof(size_t) * (size_t)n);
+  uint64_t* fl64 = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)n);
+  uint64_t* pl64 = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)n);
+  uint32_t* wire = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n);
+  uint32_t* rec = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n);
+  int st = AMBRYCRC_ENOMEM;
+  if (crc && blen && fp && fl && pp && pl && fl64 && pl64 && wire && rec) {
+    (*env)->GetIntArrayRegion(env, blob_crc, 0, n, (jint*)crc);
+    (*env)->GetLongArrayRegion(env, blob_len, 0, n, (jlong*)blen);
+    st = AJC_OK;
+    for (jsize i = 0; i < n && st == AJC_OK; ++i)
+      if ((int64_t)blen[i] < 0) st = AMBRYCRC_EINVAL;
+    if (st == AJC_OK && wire_out) st = gather_list(env, fields, n, fp, fl);
+    if (st == AJC_OK && record_out) st = gather_list(env, prefixes, n, pp, pl);
+    if (st == AJC_OK) {
+      for (jsize i = 0; i < n; ++i) {
+        fl64[i] = wire_out ? (uint64_t)fl[i] : 0;
+        pl64[i] = record_out ? (uint64_t)pl[i] : 0;
+      }
+      st = ambrycrc_put_crcs((const uint8_t* const*)fp, fl64, (const uint8_t* const*)pp, pl64, crc, blen, (size_t)n,
+                             wire_out ? wire : NULL, record_out ? rec : NULL);
+    }
+    if (st == AJC_OK && wire_out) (*env)->SetIntArrayRegion(env, wire_out, 0, n, (const jint*)wire);
+    if (st == AJC_OK && record_out) (*env)->SetIntArrayRegion(env, record_out, 0, n, (const jint*)rec);
+  }
+  free(crc);
+  free(blen);
+  free(fp);
+  free(fl);
+  free(pp);
+  free(pl);
+  free(fl64);
+  free(pl64);
+  free(wire);
+  free(rec);
+  raise(env, st);
+}
+
+/* NativeCrc32.rangeChecksums -> ambrycrc_range_checksums_host: FileStore.getChecksumsForRanges
+ * (FileStore.java:567-595) over a file image in a direct buffer (a MappedByteBuffer: capacity = file length).
+ * out[i] = CRC of [first[i], second[i]) truncated at the image's end; an invalid range throws
+ * IllegalArgumentException before anything is computed. A direct buffer of capacity 0 (an empty file's
+ * mapping, which has no address) is an empty image. */
+JNIEXPORT void JNICALL JNI_FN(nativeRangeChecksums)(JNIEnv* env, jclass cls, jobject file, jlongArray first,
+                                                    jlongArray second, jintArray out, jint device) {
+  (void)cls;
+  if (!file || !first || !second || !out) {
+    raise(env, AJC_ENULL);
+    return;
+  }
+  const jsize n = (*env)->GetArrayLength(env, first);
+  if (raise(env, ajc_range_lengths(n, (*env)->GetArrayLength(env, second), (*env)->GetArrayLength(env, out)))) return;
+  int64_t cap;
+  const uint8_t* base = direct(env, file, &cap);
+  if (!base) {
+    if ((*env)->GetDirectBufferCapacity(env, file) != 0) {
+      raise(env, AJC_ENOTDIRECT);
+      return;
+    }
+    cap = 0;
+  }
+  if (n == 0) return;
+  int64_t* f = (int64_t*)malloc(sizeof(int64_t) * (size_t)n);
+  int64_t* s = (int64_t*)malloc(sizeof(int64_t) * (size_t)n);
+  uint32_t* res = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n);
+  int st = AMBRYCRC_ENOMEM;
+  if (f && s && res) {
+    (*env)->GetLongArrayRegion(env, first, 0, n, (jlong*)f);
+    (*env)->GetLongArrayRegion(env, second, 0, n, (jlong*)s);
+    st = ambrycrc_range_checksums_host(base, (uint64_t)cap, f, s, (size_t)n, res, device);
+    if (st == AMBRYCRC_OK) (*env)->SetIntArrayRegion(env, out, 0, n, (const jint*)res);
+  }
+  free(f);
+  free(s);
+  free(res);
+  raise(env, st);
 }
 
 /* One message on the CPU (ambrycrc_verify_message_cpu): MessageFormatSend / BlobStoreRecovery's

@@ -87,3 +87,19 @@ int ajc_transform_lengths(int64_t m, int64_t life_len, int64_t out_off_len, int6
     return AJC_ESHORT;
   return AJC_OK;
 }
+
+int ajc_put_lengths(int64_t n, int64_t blob_len_len, int64_t fields_len, int64_t wire_len, int64_t prefixes_len,
+                    int64_t record_len) {
+  if (n < 0 || blob_len_len < 0) return AJC_ENULL;
+  if ((wire_len >= 0 && fields_len < 0) || (record_len >= 0 && prefixes_len < 0)) return AJC_ENULL;
+  if (blob_len_len < n) return AJC_ESHORT;
+  if (wire_len >= 0 && (wire_len < n || fields_len < n)) return AJC_ESHORT;
+  if (record_len >= 0 && (record_len < n || prefixes_len < n)) return AJC_ESHORT;
+  return AJC_OK;
+}
+
+int ajc_range_lengths(int64_t n, int64_t second_len, int64_t out_len) {
+  if (n < 0 || second_len < 0 || out_len < 0) return AJC_ENULL;
+  if (second_len < n || out_len < n) return AJC_ESHORT;
+  return AJC_OK;
+}

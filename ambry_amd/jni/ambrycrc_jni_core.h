@@ -61,6 +61,14 @@ int ajc_verify_lengths(int64_t m, int64_t status_len, int64_t ends_len);
  * hold >= m entries each. */
 int ajc_transform_lengths(int64_t m, int64_t life_len, int64_t out_off_len, int64_t out_len_len, int64_t status_len);
 
+/* nativePutCrcs: n = blobCrc.length; blobLen holds >= n; wireOut and its fields list (-1 each: null), recordOut
+ * and its prefixes list likewise hold >= n entries. An output without its input list is AJC_ENULL. */
+int ajc_put_lengths(int64_t n, int64_t blob_len_len, int64_t fields_len, int64_t wire_len, int64_t prefixes_len,
+                    int64_t record_len);
+
+/* nativeRangeChecksums: n = first.length; second and out hold >= n entries. */
+int ajc_range_lengths(int64_t n, int64_t second_len, int64_t out_len);
+
 #ifdef __cplusplus
 }
 #endif

@@ -19,8 +19,36 @@ import java.util.zip.Checksum;
 
 
 public final class NativeCrc32 implements Checksum {
-  static {
-    System.loadLibrary("ambrycrc_jni");
+  /** Whether libambrycrc_jni loaded. Crc32 consults it, so a JVM without the library keeps the pure-Java loop. */
+  private static final boolean LOADED = load();
+
+  /**
+   * com.github.ambry.utils.Crc32 runs updates of at least this many bytes through the library
+   * (ambry-utils-crc32-native.patch); Integer.MAX_VALUE when the library did not load or
+   * -Dambry.crc32.native=false. Below it the JNI crossing costs more than the Java slice-by-8
+   * loop (-Dambry.crc32.native.min.bytes, default 256).
+   */
+  static final int CRC32_MIN_BYTES = crc32MinBytes();
+
+  private static boolean load() {
+    try {
+      System.loadLibrary("ambrycrc_jni");
+      return true;
+    } catch (UnsatisfiedLinkError | SecurityException e) {
+      return false;
+    }
+  }
+
+  private static int crc32MinBytes() {
+    if (!LOADED || "false".equals(System.getProperty("ambry.crc32.native"))) {
+      return Integer.MAX_VALUE;
+    }
+    return Math.max(1, Integer.getInteger("ambry.crc32.native.min.bytes", 256));
+  }
+
+  /** True when libambrycrc_jni loaded; every other method throws UnsatisfiedLinkError otherwise. */
+  public static boolean isAvailable() {
+    return LOADED;
   }
 
   /** Finalized value (zlib convention, starts at 0); Crc32.java keeps the inverted register. */
@@ -47,10 +75,18 @@ public final class NativeCrc32 implements Checksum {
   /** Crc32.update(ByteBuffer), Crc32.java:100-143: consumes position..limit. */
   @Override
   public void update(ByteBuffer buffer) {
+    crc = updateBuffer(crc, buffer);
+  }
+
+  /**
+   * The finalized CRC `crc` continued over buffer's position..limit, which it consumes (Crc32.java:100-143).
+   * Crc32 calls it with its register inverted.
+   */
+  static int updateBuffer(int crc, ByteBuffer buffer) {
     int pos = buffer.position();
     int len = buffer.remaining();
     if (len == 0) {
-      return;
+      return crc;
     }
     if (buffer.isDirect()) {
       crc = nativeUpdateDirect(crc, buffer, pos, len);
@@ -62,6 +98,12 @@ public final class NativeCrc32 implements Checksum {
       crc = nativeUpdateArray(crc, tmp, 0, len);
     }
     buffer.position(buffer.limit());
+    return crc;
+  }
+
+  /** The finalized CRC `crc` continued over b[off, off + len); Crc32 checks the bounds first. */
+  static int updateArray(int crc, byte[] b, int off, int len) {
+    return nativeUpdateArray(crc, b, off, len);
   }
 
   /** update(ByteBuffer) over a gather list, e.g. PutChunk.verifyCRC's nioBuffers() (PutOperation.java:2041-2043). */
@@ -185,6 +227,61 @@ public final class NativeCrc32 implements Checksum {
     return regionBytes + (long) m * TRANSFORM_GROWTH_MAX;
   }
 
+  /**
+   * One-pass PUT CRCs (ambrycrc_put_crcs, SURVEY.md §8f row 2) for n = blobCrc.length PUTs whose blob CRC
+   * blobCrc[i] over blobLen[i] bytes is already known (the router's chunk CRC, a batch call's output):
+   * wireOut[i] = CRC of fields[i] followed by the blob -- PutRequest.prepareBuffer's wire CRC over the
+   * serialized blobId ... blobSize fields and the blob (PutRequest.java:238-283) -- and recordOut[i] = CRC of
+   * prefixes[i] followed by the blob -- the Blob_Format_V3 record CRC seeded by its 13-B prefix
+   * (MessageFormatRecord.java:1789-1795, PutMessageFormatInputStream.java:116-120). Each field / prefix
+   * buffer's position..limit is used and left unconsumed; heap buffers are copied out. Either output (with
+   * its input list) may be null. No blob byte is read: both CRCs come from blobCrc by GF(2) combine.
+   */
+  public static void putCrcs(ByteBuffer[] fields, ByteBuffer[] prefixes, int[] blobCrc, long[] blobLen,
+      int[] wireOut, int[] recordOut) {
+    nativePutCrcs(directOrCopy(fields), directOrCopy(prefixes), blobCrc, blobLen, wireOut, recordOut);
+  }
+
+  /** The list with every heap buffer replaced by a direct copy of its position..limit (same position). */
+  private static ByteBuffer[] directOrCopy(ByteBuffer[] bufs) {
+    if (bufs == null) {
+      return null;
+    }
+    ByteBuffer[] out = bufs;
+    for (int i = 0; i < bufs.length; i++) {
+      ByteBuffer b = bufs[i];
+      if (b != null && !b.isDirect()) {
+        if (out == bufs) {
+          out = bufs.clone();
+        }
+        ByteBuffer copy = ByteBuffer.allocateDirect(b.remaining());
+        copy.put(b.duplicate());
+        copy.flip();
+        out[i] = copy;
+      }
+    }
+    return out;
+  }
+
+  /**
+   * FileStore.getChecksumsForRanges (FileStore.java:567-595) over a file image in a direct buffer -- a
+   * MappedByteBuffer of the file, whose capacity is the file length (ambrycrc_range_checksums_host):
+   * checksum i = CRC-32 of bytes [first[i], second[i]), truncated at the end of the image and empty past it,
+   * as the reference's FileChannel read gives them. Returned as unsigned values, the numbers the reference
+   * renders with Long.toString. A range with first < 0, second < 0 or first > second throws
+   * IllegalArgumentException and computes nothing. device < 0: the library's CPU threads; otherwise its
+   * host-resident dispatch on that (initialised) GPU.
+   */
+  public static long[] rangeChecksums(ByteBuffer file, long[] first, long[] second, int device) {
+    int[] out = new int[first.length];
+    nativeRangeChecksums(file, first, second, out, device);
+    long[] values = new long[out.length];
+    for (int i = 0; i < out.length; i++) {
+      values[i] = out[i] & 0xffffffffL;
+    }
+    return values;
+  }
+
   /** Host-resident dispatch policies (ambrycrc_set_host_policy): auto, always the GPU, always the CPU leg. */
   public static final int HOST_AUTO = 0;
   public static final int HOST_GPU = 1;
@@ -257,6 +354,11 @@ public final class NativeCrc32 implements Checksum {
 
   private static native void nativeTransformMessages(ByteBuffer region, long[] offsets, short[] lifeVersions,
       int headerVersion, ByteBuffer out, long[] outOffsets, long[] outLens, int[] status, int device);
+
+  private static native void nativePutCrcs(ByteBuffer[] fields, ByteBuffer[] prefixes, int[] blobCrc, long[] blobLen,
+      int[] wireOut, int[] recordOut);
+
+  private static native void nativeRangeChecksums(ByteBuffer file, long[] first, long[] second, int[] out, int device);
 
   private static native int nativeSetHostPolicy(int device, int policy);
 

@@ -106,4 +106,46 @@ public class NativeCrc32Test {
     }
     assertEquals(v, n.getValue());
   }
+
+  /**
+   * With ambry-utils-crc32-native.patch applied, Crc32 itself delegates updates of CRC32_MIN_BYTES and more to the
+   * library: the same values as java.util.zip.CRC32 across the threshold, for arrays and heap / direct / read-only
+   * buffers (consumed), in pieces straddling it, and the same exception for a bad range with the value unchanged.
+   */
+  @Test
+  public void crc32DelegatesAcrossTheThreshold() {
+    assertTrue(NativeCrc32.isAvailable());
+    int t = NativeCrc32.CRC32_MIN_BYTES;
+    byte[] b = new byte[4 * t + 11];
+    new Random(7).nextBytes(b);
+    for (int len : new int[]{t - 1, t, t + 1, 4 * t}) {
+      Crc32 c = new Crc32();
+      c.update(b, 5, len);
+      assertEquals(jdk(b, 5, len), c.getValue());
+      for (ByteBuffer buf : new ByteBuffer[]{ByteBuffer.wrap(b), ByteBuffer.allocateDirect(b.length),
+          ByteBuffer.wrap(b).asReadOnlyBuffer()}) {
+        if (buf.isDirect()) {
+          buf.put(b).flip();
+        }
+        buf.position(5).limit(5 + len);
+        Crc32 d = new Crc32();
+        d.update(buf);
+        assertEquals(jdk(b, 5, len), d.getValue());
+        assertEquals(buf.limit(), buf.position());
+      }
+    }
+    Crc32 pieces = new Crc32();
+    pieces.update(b, 0, 3);
+    pieces.update(b, 3, t + 2);
+    pieces.update(b[t + 5]);
+    pieces.update(b, t + 6, b.length - t - 6);
+    assertEquals(jdk(b, 0, b.length), pieces.getValue());
+    long before = pieces.getValue();
+    try {
+      pieces.update(b, b.length - t + 1, t);
+      fail("expected ArrayIndexOutOfBoundsException");
+    } catch (ArrayIndexOutOfBoundsException e) {
+      assertEquals(before, pieces.getValue());
+    }
+  }
 }

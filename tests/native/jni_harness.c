@@ -238,8 +238,9 @@ static uint8_t* slurp(const char* path, size_t* n) {
   fseek(f, 0, SEEK_END);
   const long len = ftell(f);
   fseek(f, 0, SEEK_SET);
-  uint8_t* b = (uint8_t*)malloc(len > 0 ? (size_t)len : 1);
+  uint8_t* b = (uint8_t*)malloc((len > 0 ? (size_t)len : 0) + 1); /* NUL-terminated: putcrcs_cases scans text */
   *n = b ? fread(b, 1, (size_t)len, f) : 0;
+  if (b) b[*n] = 0;
   fclose(f);
   return b;
 }
@@ -369,6 +370,192 @@ static int recover_cases(const char* rpath, int batch) {
   return 0;
 }
 
+JNIEXPORT void JNICALL FN(nativePutCrcs)(JNIEnv*, jclass, jobjectArray, jobjectArray, jintArray, jlongArray, jintArray,
+                                         jintArray);
+JNIEXPORT void JNICALL FN(nativeRangeChecksums)(JNIEnv*, jclass, jobject, jlongArray, jlongArray, jintArray, jint);
+
+/* com.github.ambry.utils.Crc32 with ambry-utils-crc32-native.patch: the register is kept inverted, updates of at
+ * least min_bytes go through NativeCrc32.updateBuffer (nativeUpdateDirect on a direct buffer, which is then
+ * consumed), shorter ones through the class's own table loop (Crc32.java:77-94, byte-wise). */
+struct crc32_obj {
+  jint crc;
+};
+static uint32_t g_t0[256];
+static void crc32_reset(struct crc32_obj* c) { c->crc = (jint)0xffffffffu; }
+static void crc32_update_buffer(struct crc32_obj* c, struct _jobject* buf, int min_bytes) {
+  const jint len = buf->lim - buf->pos;
+  if (len == 0) return;
+  if (len >= min_bytes) {
+    c->crc = ~FN(nativeUpdateDirect)(&g_env, NULL, ~c->crc, buf, buf->pos, len);
+    if (!g_pending) buf->pos = buf->lim;
+    return;
+  }
+  uint32_t r = (uint32_t)c->crc;
+  for (; buf->pos < buf->lim; ++buf->pos) r = (r >> 8) ^ g_t0[(r ^ ((const uint8_t*)buf->data)[buf->pos]) & 0xff];
+  c->crc = (jint)r;
+}
+static jint crc32_value(const struct crc32_obj* c) { return ~c->crc; }
+
+/* argv[1] == "putchunk", argv[2] = a chunk's bytes, argv[3..] = the lengths of the slices fillFrom receives: the
+ * PutChunk call sequence of PutOperation.java with the patched Crc32 (min_bytes 256). fillFrom updates chunkCrc32
+ * with each slice's nioBuffer (:1700-1703); verifyCRC runs a fresh Crc32 over buf.nioBuffers() (:2033-2054) -- the
+ * composite's components, here the same slices; a byte mutated after the fill (PutOperationTest.java:629-679) must
+ * then fail the comparison; a compressed chunk resets chunkCrc32 and recomputes it over the new buffer
+ * (:1595-1599). Prints fill / verify values and the verify outcomes. */
+static int putchunk_cases(const char* path, int nslices, char** slices) {
+  for (uint32_t i = 0; i < 256; ++i) {
+    uint32_t r = i;
+    for (int k = 0; k < 8; ++k) r = (r >> 1) ^ (0xEDB88320u & (0u - (r & 1)));
+    g_t0[i] = r;
+  }
+  size_t n = 0;
+  uint8_t* chunk = slurp(path, &n);
+  if (!chunk || nslices > 256) return 2;
+  static struct _jobject bufs[256];
+  size_t at = 0;
+  for (int i = 0; i < nslices; ++i) {
+    const size_t len = (size_t)atol(slices[i]);
+    if (at + len > n) return 3;
+    bufs[i] = arr(K_BUFFER, chunk + at, (jsize)len); /* slice.nioBuffer(): a direct buffer over the slice */
+    bufs[i].pos = 0, bufs[i].lim = (jint)len;
+    at += len;
+  }
+  struct crc32_obj chunk_crc, computed;
+  crc32_reset(&chunk_crc);
+  for (int i = 0; i < nslices; ++i) crc32_update_buffer(&chunk_crc, &bufs[i], 256); /* fillFrom */
+  report("putchunk_fill", crc32_value(&chunk_crc));
+  report("putchunk_fill_consumed", bufs[0].pos == bufs[0].lim && bufs[nslices - 1].pos == bufs[nslices - 1].lim);
+  /* verifyCRC: buf.nioBuffers() hands out fresh buffers over the components */
+  crc32_reset(&computed);
+  for (int i = 0; i < nslices; ++i) {
+    bufs[i].pos = 0;
+    crc32_update_buffer(&computed, &bufs[i], 256);
+  }
+  report("putchunk_verify", crc32_value(&computed));
+  report("putchunk_verify_match", crc32_value(&computed) == crc32_value(&chunk_crc));
+  chunk[n / 2] ^= 0x10; /* the buffer mutated after the fill */
+  crc32_reset(&computed);
+  for (int i = 0; i < nslices; ++i) {
+    bufs[i].pos = 0;
+    crc32_update_buffer(&computed, &bufs[i], 256);
+  }
+  report("putchunk_mutated_match", crc32_value(&computed) == crc32_value(&chunk_crc));
+  /* compression: chunkCrc32.reset(), then the compressed buffer's nioBuffers (one direct buffer here) */
+  struct _jobject whole = arr(K_BUFFER, chunk, (jsize)n);
+  whole.pos = 0, whole.lim = (jint)n;
+  crc32_reset(&chunk_crc);
+  crc32_update_buffer(&chunk_crc, &whole, 256);
+  report("putchunk_recomputed", crc32_value(&chunk_crc));
+  free(chunk);
+  return 0;
+}
+
+/* argv[1] == "ranges", argv[2] = a file image, argv[3] = ranges "first second" per line, argv[4] = the device (-1 the
+ * CPU): FileStore.getChecksumsForRanges with ambry-store-filestore-ranges.patch -- NativeCrc32.rangeChecksums over a
+ * mapping of the file. Prints range_<i> per range (or the exception). An empty file image is a capacity-0 direct
+ * buffer. */
+static int ranges_cases(const char* fpath, const char* rpath, int device) {
+  size_t n = 0;
+  uint8_t* image = slurp(fpath, &n);
+  FILE* f = fopen(rpath, "r");
+  if (!image || !f) return 2;
+  static jlong first[4096], second[4096];
+  static jint out[4096];
+  int k = 0;
+  long long a, b;
+  while (k < 4096 && fscanf(f, "%lld %lld", &a, &b) == 2) first[k] = a, second[k] = b, ++k;
+  fclose(f);
+  if (device >= 0) {
+    FN(nativeInit)(&g_env, NULL, device);
+    report("ranges_init", 0);
+  }
+  struct _jobject file = arr(K_BUFFER, image, (jsize)n);
+  struct _jobject jf = arr(K_LONGS, first, k), js = arr(K_LONGS, second, k), jo = arr(K_INTS, out, k);
+  for (int i = 0; i < k; ++i) out[i] = 0x5a5a5a5a;
+  FN(nativeRangeChecksums)(&g_env, NULL, &file, &jf, &js, &jo, device);
+  report("ranges_call", 0);
+  char name[64];
+  for (int i = 0; i < k; ++i) {
+    snprintf(name, sizeof name, "range_%d", i);
+    report(name, out[i]);
+  }
+  /* argument errors: a short output array, a heap buffer, a null list */
+  struct _jobject jshort = arr(K_INTS, out, k > 0 ? k - 1 : 0), heap = arr(K_BUFFER, NULL, (jsize)n);
+  if (k > 0) {
+    FN(nativeRangeChecksums)(&g_env, NULL, &file, &jf, &js, &jshort, device);
+    report("ranges_short", 0);
+  }
+  FN(nativeRangeChecksums)(&g_env, NULL, &heap, &jf, &js, &jo, device);
+  report("ranges_heap", 0);
+  FN(nativeRangeChecksums)(&g_env, NULL, &file, NULL, &js, &jo, device);
+  report("ranges_null", 0);
+  free(image);
+  return 0;
+}
+
+/* argv[1] == "putcrcs", argv[2] = a file of PUTs, each "<fields len> <prefix len> <blob len>\n" then those bytes:
+ * NativeCrc32.putCrcs -- the blob CRCs first (nativeUpdateDirect over each blob), then both CRCs of every PUT from
+ * them (ambrycrc_put_crcs: no blob byte read). Prints wire_<i> and record_<i>, then the argument errors. */
+static int putcrcs_cases(const char* path) {
+  size_t n = 0;
+  uint8_t* data = slurp(path, &n);
+  if (!data) return 2;
+  static struct _jobject fb[512], pb[512];
+  static jobject fl[512], pl[512];
+  static jint bcrc[512], wire[512], rec[512];
+  static jlong blen[512];
+  int k = 0;
+  size_t at = 0;
+  while (at < n && k < 512) {
+    unsigned long long a, b, c;
+    int used = 0;
+    if (sscanf((const char*)data + at, "%llu %llu %llu%n", &a, &b, &c, &used) != 3) return 3;
+    at += (size_t)used + 1; /* the newline */
+    fb[k] = arr(K_BUFFER, data + at, (jsize)a), fb[k].pos = 0, fb[k].lim = (jint)a;
+    pb[k] = arr(K_BUFFER, data + at + a, (jsize)b), pb[k].pos = 0, pb[k].lim = (jint)b;
+    struct _jobject blob = arr(K_BUFFER, data + at + a + b, (jsize)c);
+    bcrc[k] = c ? FN(nativeUpdateDirect)(&g_env, NULL, 0, &blob, 0, (jint)c) : 0;
+    blen[k] = (jlong)c;
+    fl[k] = &fb[k], pl[k] = &pb[k];
+    at += a + b + c;
+    ++k;
+  }
+  struct _jobject jfl = arr(K_OBJS, fl, k), jpl = arr(K_OBJS, pl, k), jcrc = arr(K_INTS, bcrc, k);
+  struct _jobject jlen = arr(K_LONGS, blen, k), jw = arr(K_INTS, wire, k), jr = arr(K_INTS, rec, k);
+  FN(nativePutCrcs)(&g_env, NULL, &jfl, &jpl, &jcrc, &jlen, &jw, &jr);
+  report("putcrcs_call", 0);
+  char name[64];
+  for (int i = 0; i < k; ++i) {
+    snprintf(name, sizeof name, "wire_%d", i);
+    report(name, wire[i]);
+    snprintf(name, sizeof name, "record_%d", i);
+    report(name, rec[i]);
+  }
+  /* the record CRCs alone (no field list), then the argument errors */
+  for (int i = 0; i < k; ++i) rec[i] = 0;
+  FN(nativePutCrcs)(&g_env, NULL, NULL, &jpl, &jcrc, &jlen, NULL, &jr);
+  report("putcrcs_record_only_0", rec[0]);
+  FN(nativePutCrcs)(&g_env, NULL, NULL, &jpl, &jcrc, &jlen, &jw, &jr);
+  report("putcrcs_wire_without_fields", 0);
+  struct _jobject jshort = arr(K_INTS, wire, k - 1);
+  FN(nativePutCrcs)(&g_env, NULL, &jfl, &jpl, &jcrc, &jlen, &jshort, &jr);
+  report("putcrcs_short_out", 0);
+  blen[0] = -1;
+  FN(nativePutCrcs)(&g_env, NULL, &jfl, &jpl, &jcrc, &jlen, &jw, &jr);
+  report("putcrcs_negative_len", 0);
+  blen[0] = 0;
+  struct _jobject heap = arr(K_BUFFER, NULL, 4);
+  fl[0] = &heap;
+  FN(nativePutCrcs)(&g_env, NULL, &jfl, &jpl, &jcrc, &jlen, &jw, &jr);
+  report("putcrcs_heap_field", 0);
+  fb[1].lim = fb[1].len + 1;
+  fl[0] = &fb[0];
+  FN(nativePutCrcs)(&g_env, NULL, &jfl, &jpl, &jcrc, &jlen, &jw, &jr);
+  report("putcrcs_field_bounds", 0);
+  free(data);
+  return 0;
+}
+
 /* With a GPU (argv[1] == "gpu"): the device entries on valid arguments. */
 static int gpu_cases(void) {
   FN(nativeInit)(&g_env, NULL, 0);
@@ -419,6 +606,9 @@ int main(int argc, char** argv) {
   if (argc > 2 && strcmp(argv[1], "gpumsg") == 0) return gpumsg_cases(argv[2]);
   if (argc > 3 && strcmp(argv[1], "sieve") == 0) return sieve_cases(argv[2], argv[3]);
   if (argc > 3 && strcmp(argv[1], "recover") == 0) return recover_cases(argv[2], atoi(argv[3]));
+  if (argc > 3 && strcmp(argv[1], "putchunk") == 0) return putchunk_cases(argv[2], argc - 3, argv + 3);
+  if (argc > 4 && strcmp(argv[1], "ranges") == 0) return ranges_cases(argv[2], argv[3], atoi(argv[4]));
+  if (argc > 2 && strcmp(argv[1], "putcrcs") == 0) return putcrcs_cases(argv[2]);
   static uint8_t digits[] = "123456789";
   struct _jobject b9 = arr(K_BYTES, digits, 9);
   report("array_full", FN(nativeUpdateArray)(&g_env, NULL, 0, &b9, 0, 9));

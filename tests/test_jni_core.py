@@ -348,3 +348,128 @@ def test_jni_recovery_call_sequence(core, tmp_path, case):
     assert got["recover_init"] == (0, "-")
     assert (got["recover_count"][0], got["recover_stop"][0], got["recover_failed"][0]) == (count, stop, failed)
     assert failed == (case != "clean") and count == {"clean": 30, "corrupt": 13, "truncated": 29}[case]
+
+
+def test_jni_putchunk_call_sequence(core, tmp_path):
+    """com.github.ambry.utils.Crc32 with ambry-utils-crc32-native.patch, as PutOperation.PutChunk calls it, in the
+    fake JVM: fillFrom's update(slice.nioBuffer()) per slice (PutOperation.java:1700-1703) -- slices of 256 B and
+    more through nativeUpdateDirect on the inverted register, shorter ones through the class's own loop -- then
+    verifyCRC's fresh Crc32 over nioBuffers() (:2033-2054). Both equal zlib's CRC of the 4 MiB chunk (the C3 chunk
+    size), the slices are consumed, a byte mutated after the fill fails verifyCRC (PutOperationTest.java:629-679),
+    and the post-compression reset + recompute (:1595-1599) sees the new bytes."""
+    from datagen import stream_bytes
+
+    chunk = bytearray(stream_bytes(0xC3, 0, 4 << 20).tobytes())
+    (tmp_path / "chunk.bin").write_bytes(bytes(chunk))
+    rng = __import__("numpy").random.default_rng(11)
+    slices, left = [], len(chunk)
+    while left:
+        s = min(left, int(rng.choice([1, 7, 255, 256, 257, 4096, 65536, 1 << 20])))
+        slices.append(s)
+        left -= s
+    slices = slices[:200] + [sum(slices[200:])] if len(slices) > 201 else slices
+    got = _run_harness(tmp_path, "putchunk", str(tmp_path / "chunk.bin"), *map(str, slices))
+    want = zlib.crc32(bytes(chunk))
+    assert got["putchunk_fill"] == (want, "-") and got["putchunk_verify"] == (want, "-")
+    assert got["putchunk_fill_consumed"] == (1, "-") and got["putchunk_verify_match"] == (1, "-")
+    assert got["putchunk_mutated_match"] == (0, "-")
+    chunk[len(chunk) // 2] ^= 0x10
+    assert got["putchunk_recomputed"] == (zlib.crc32(bytes(chunk)), "-")
+
+
+def _filestore_ranges(image, ranges):
+    """FileStore.getChecksumsForRanges (FileStore.java:567-595) restated: each range read from `first` for
+    `second - first` bytes by FileChannel.read, so cut at the end of the file and empty past it."""
+    n = len(image)
+    return [zlib.crc32(image[min(a, n):min(b, n)]) for a, b in ranges]
+
+
+def _ranges_case(tmp_path, image, ranges, device):
+    (tmp_path / "file.bin").write_bytes(image)
+    (tmp_path / "ranges.txt").write_text("".join("%d %d\n" % r for r in ranges))
+    return _run_harness(tmp_path, "ranges", str(tmp_path / "file.bin"), str(tmp_path / "ranges.txt"), str(device))
+
+
+def _check_ranges(got, image, ranges):
+    IAE, NPE = "java/lang/IllegalArgumentException", "java/lang/NullPointerException"
+    assert got["ranges_call"] == (0, "-")
+    for i, want in enumerate(_filestore_ranges(image, ranges)):
+        assert got["range_%d" % i] == (want, "-"), i
+    assert got["ranges_short"] == (0, IAE) and got["ranges_heap"] == (0, IAE) and got["ranges_null"] == (0, NPE)
+
+
+def _file_and_ranges():
+    from datagen import stream_bytes
+
+    image = stream_bytes(0xF5, 0, 3 << 20).tobytes()
+    n = len(image)
+    # StoreFileCopyHandler.getChecksumRanges' shape (start, start + size - 1), plus empty, straddling and past-EOF
+    ranges = [(i * (256 << 10), i * (256 << 10) + (256 << 10) - 1) for i in range(12)]
+    ranges += [(0, 0), (5, 5), (1, 2), (n - 100, n + 100), (n, n + 10), (n + 50, n + 60), (7, n), (0, n)]
+    return image, ranges
+
+
+def test_jni_filestore_ranges_cpu(core, tmp_path):
+    """ambry-store-filestore-ranges.patch's call, in the fake JVM on the library's CPU threads (device -1):
+    nativeRangeChecksums over the file image equals FileStore's per-range reads -- the copy handler's ranges,
+    empty ranges, ranges straddling and past the end of the file -- and an empty file image (capacity-0 mapping)
+    gives 0 for every range, as the reference's empty reads do. An invalid range throws IllegalArgumentException
+    and computes nothing."""
+    image, ranges = _file_and_ranges()
+    _check_ranges(_ranges_case(tmp_path, image, ranges, -1), image, ranges)
+    got = _ranges_case(tmp_path, b"", [(0, 10), (3, 3)], -1)
+    assert got["range_0"] == (0, "-") and got["range_1"] == (0, "-")
+    got = _ranges_case(tmp_path, image, [(0, 10), (9, 3)], -1)
+    assert got["ranges_call"] == (0, "java/lang/IllegalArgumentException")
+    assert got["range_0"] == (0x5A5A5A5A, "-")  # nothing computed
+
+
+@pytest.mark.gpu
+def test_jni_filestore_ranges_gpu(core, tmp_path):
+    """The same FileStore ranges through the library's host-resident dispatch on GPU 0 (nativeInit first)."""
+    image, ranges = _file_and_ranges()
+    got = _ranges_case(tmp_path, image, ranges, 0)
+    assert got["ranges_init"] == (0, "-")
+    _check_ranges(got, image, ranges)
+
+
+def test_jni_put_crcs(core, tmp_path):
+    """NativeCrc32.putCrcs (ambrycrc_put_crcs, §8f row 2) in the fake JVM: from each blob's CRC alone, the PutRequest
+    wire CRC over the V5 fields and the blob (PutRequest.java:238-283) and the Blob_Format_V3 record CRC over its
+    13-B prefix and the blob (MessageFormatRecord.java:1789-1795), equal to zlib over the concatenations; then the
+    record CRCs alone, and the argument errors (a wire output without fields, a short output, a negative blob
+    length, a heap field buffer, a limit past the capacity) thrown."""
+    from ambry_amd.protocol import blob_record_prefix_v3
+    from test_protocol import make_requests
+
+    reqs = make_requests(n=12, seed=9)
+    prefixes = [blob_record_prefix_v3(len(b), t, c) for _, b, c, t in reqs]
+    blob = b"".join(b"%d %d %d\n" % (len(f), len(p), len(b)) + f + p + b for (f, b, _, _), p in zip(reqs, prefixes))
+    (tmp_path / "puts.bin").write_bytes(blob)
+    got = _run_harness(tmp_path, "putcrcs", str(tmp_path / "puts.bin"))
+    assert got["putcrcs_call"] == (0, "-")
+    for i, ((f, b, _, _), p) in enumerate(zip(reqs, prefixes)):
+        assert got["wire_%d" % i] == (zlib.crc32(f + b), "-"), i
+        assert got["record_%d" % i] == (zlib.crc32(p + b), "-"), i
+    assert got["putcrcs_record_only_0"] == (zlib.crc32(prefixes[0] + reqs[0][1]), "-")
+    NPE, IAE, IOOBE = ("java/lang/NullPointerException", "java/lang/IllegalArgumentException",
+                       "java/lang/IndexOutOfBoundsException")
+    assert got["putcrcs_wire_without_fields"] == (0, NPE) and got["putcrcs_short_out"] == (0, IAE)
+    assert got["putcrcs_negative_len"] == (0, IAE) and got["putcrcs_heap_field"] == (0, IAE)
+    assert got["putcrcs_field_bounds"] == (0, IOOBE)
+
+
+def test_integration_patches_apply(tmp_path):
+    """Every integration/*.patch applies to the reference tree (git apply --check; read-only). Skipped where the
+    reference is absent (the GPU box)."""
+    import glob
+    import subprocess
+
+    ref = "/root/reference"
+    if not os.path.isdir(os.path.join(ref, "ambry-utils")):
+        pytest.skip("reference tree not present")
+    patches = sorted(glob.glob(os.path.join(ROOT, "integration", "*.patch")))
+    assert len(patches) >= 5
+    for p in patches:
+        r = subprocess.run(["git", "apply", "--check", p], cwd=ref, capture_output=True, text=True)
+        assert r.returncode == 0, (p, r.stderr)
