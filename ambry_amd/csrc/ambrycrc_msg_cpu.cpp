@@ -124,13 +124,16 @@ uint32_t verify(const uint8_t* p, uint64_t rem, Parsed* m) {
 struct XPlan {
   uint64_t len = 0;      // output bytes
   bool fast = false;     // the message's own bytes, life version and header CRC rewritten
-  int life = -1;         // fast: the life version to write (-1: keep the stored one)
+  int life = -1;         // fast: the life version to write, as the header's 16 bits (-1: keep the stored one)
   ambrycrc_put_desc d;   // general: the re-serialization
   ambrycrc::PropsFix fx;
 };
 
-uint32_t transform_plan(const uint8_t* region, uint64_t region_len, uint64_t off, int life_version, int header_version,
-                        XPlan* x) {
+// have_life: write life_version into the new header as given -- a batch's index value, negatives
+// included (MessageInfo.LIFE_VERSION_FROM_FRONTEND is -1; ValidatingTransformer.java:90 writes
+// msgInfo.getLifeVersion() unchanged, as the device batch does); otherwise keep the stored one.
+uint32_t transform_plan(const uint8_t* region, uint64_t region_len, uint64_t off, bool have_life, int life_version,
+                        int header_version, XPlan* x) {
   Parsed m;
   m.end = 0;
   const uint32_t st = off <= region_len ? verify(region + off, region_len - off, &m) : (uint32_t)AMBRYCRC_MSG_BAD_LAYOUT;
@@ -156,7 +159,7 @@ uint32_t transform_plan(const uint8_t* region, uint64_t region_len, uint64_t off
   if (header_version == 3 && m.version == 3 && bv == 3 && x->fx.version == 0) {
     x->fast = true;
     x->len = m.end;
-    x->life = life_version >= 0 && (uint32_t)life_version != m.life ? life_version : -1;
+    x->life = have_life && (uint32_t)(uint16_t)life_version != m.life ? (int)(uint16_t)life_version : -1;
     return 0;
   }
   ambrycrc_put_desc& d = x->d;
@@ -173,7 +176,7 @@ uint32_t transform_plan(const uint8_t* region, uint64_t region_len, uint64_t off
   d.usermeta_len = rd32(p + um + 2);
   d.blob_src = off + blob + head;
   d.blob_len = rd64(p + blob + (bv == 1 ? 2 : bv == 2 ? 4 : 5));
-  d.life_version = (int16_t)(life_version >= 0 ? life_version : (int)m.life);
+  d.life_version = (int16_t)(have_life ? life_version : (int)m.life);
   d.blob_type = (int16_t)(bv == 1 ? 0u : rd16(p + blob + 2));
   d.compressed = (uint8_t)(bv == 3 && p[blob + 4] == 1 ? 1 : 0);
   d.header_version = (uint8_t)header_version;
@@ -226,7 +229,7 @@ int ambrycrc_transform_message_cpu(const uint8_t* region, uint64_t region_len, u
     return AMBRYCRC_EINVAL;
   *out_len = 0;
   XPlan x;
-  *status = transform_plan(region, region_len, off, life_version, header_version, &x);
+  *status = transform_plan(region, region_len, off, life_version >= 0, life_version, header_version, &x);
   if (*status) return AMBRYCRC_OK;
   if (!out || x.len > out_cap) {
     *status = AMBRYCRC_MSG_NO_ROOM;
@@ -315,8 +318,8 @@ int transform_messages_cpu(const uint8_t* region, uint64_t region_len, const uin
   std::vector<XPlan> plan(m);
   split_run(m, threads, [&](size_t i) { return extent_of(region, region_len, msg_off[i]); }, [&](size_t a, size_t b) {
     for (size_t i = a; i < b; ++i)
-      status[i] = transform_plan(region, region_len, msg_off[i], life_version ? life_version[i] : -1, header_version,
-                                 &plan[i]);
+      status[i] = transform_plan(region, region_len, msg_off[i], life_version != nullptr,
+                                 life_version ? life_version[i] : 0, header_version, &plan[i]);
   });
   std::vector<uint64_t> pos(m, ~0ull);  // output position, ~0: not placed
   uint64_t vpos = 0;

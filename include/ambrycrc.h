@@ -259,8 +259,9 @@ int ambrycrc_serialize_puts_dev(const ambrycrc_put_desc* d_desc, size_t m, const
  * BlobPropertiesSerDe VERSION_5 (ValidatingTransformer.java:77,87-89; AMBRYCRC_MSG_NOT_ENCODABLE
  * when a property string is not ASCII), blob record at Blob_Format_V3 -- with header version
  * `header_version` (1, 2 or 3: MessageFormatRecord.headerVersionToUse; V1 drops the encryption key,
- * as createStreamWithMessageHeaderV1 does) and life version d_life_version[i] (nullable: the
- * stored header's, 0 for V1/V2) -- all CRCs recomputed -- packed in message order into
+ * as createStreamWithMessageHeaderV1 does) and life version d_life_version[i], written as given,
+ * negatives included (ValidatingTransformer.java:90; nullable: the stored header's, 0 for V1/V2)
+ * -- all CRCs recomputed -- packed in message order into
  * [d_out, d_out + out_cap). Outputs (device arrays of m): d_status (AMBRYCRC_MSG_* bits, 0 =
  * transformed), d_out_len (0 when not transformed), d_out_off (nullable; the message's offset in
  * d_out). Bytes of d_out outside the returned spans are unspecified (a clean batch is copied while
@@ -338,7 +339,7 @@ int ambrycrc_verify_messages_host(const uint8_t* region, uint64_t region_len, co
  * slab's re-serialized messages come back through pinned memory. Outputs equal those of one
  * ambrycrc_transform_messages_dev call over the whole region: out[0 .. out_cap) packed in message
  * order, out_off[i] (nullable; UINT64_MAX when not transformed), out_len[i], status[i] (host arrays);
- * life_version (nullable) host int16[m]. out_cap = ambrycrc_transform_out_bound(region_len, m)
+ * life_version (nullable) host int16[m], written as given on either leg. out_cap = ambrycrc_transform_out_bound(region_len, m)
  * never yields AMBRYCRC_MSG_NO_ROOM for messages that share no bytes. pinned != 0: region is
  * hipHostMalloc'd / registered. Synchronous. */
 int ambrycrc_transform_messages_host(const uint8_t* region, uint64_t region_len, const uint64_t* msg_off, size_t m,

@@ -696,3 +696,32 @@ def test_transform_host_shared_bytes_matches_dev(gpu, mf):
     for i in (0, 1, 9):
         exp_st, exp = mf.transform_message(region, offs[i], version=3)
         assert exp_st == 0 and out_h[oo_h[i]:oo_h[i] + ol_h[i]] == exp
+
+
+@pytest.mark.parametrize("dense", [True, False])
+def test_transform_negative_life_versions_device_and_cpu_leg(gpu, mf, dense):
+    """Index life versions below zero (MessageInfo.LIFE_VERSION_FROM_FRONTEND = -1) are written unchanged by
+    the device batch (the fast path declines them, the general path writes them) and by the host entry's CPU
+    leg alike, so the auto policy's choice of leg never changes a byte: both against the oracle."""
+    import torch
+
+    from ambry_amd.messages import transform_dev, transform_host
+
+    region, offs = dense_v3_region(mf, 80, seed=31) if dense else build_region(mf, 150, seed=32)
+    life = np.random.default_rng(9).integers(-2, 4, size=len(offs)).astype(np.int16)
+    life[::4] = -1
+    dev = torch.frombuffer(bytearray(region), dtype=torch.uint8).cuda()
+    dout, doo, dol, dst = transform_dev(dev, torch.tensor(offs, dtype=torch.int64, device="cuda"),
+                                        header_version=3, life_version=torch.from_numpy(life).cuda())
+    torch.cuda.synchronize()
+    cout, coo, col, cst = transform_host(region, offs, header_version=3, life_version=life, device=-1)
+    assert np.array_equal(cst, dst.cpu().numpy().view(np.uint32))
+    assert np.array_equal(coo, doo.cpu().numpy()) and np.array_equal(col, dol.cpu().numpy())
+    assert cout == dout.cpu().numpy().tobytes()[:len(cout)]
+    pos = 0
+    for i, o in enumerate(offs):
+        exp_st, exp = mf.transform_message(region, o, life=int(life[i]), version=3)
+        assert int(cst[i]) == exp_st, i
+        if exp is not None:
+            assert coo[i] == pos and cout[pos:pos + len(exp)] == exp, i
+            pos += len(exp)

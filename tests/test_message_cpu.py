@@ -143,3 +143,25 @@ def test_transform_host_argument_errors(ambry):
     assert f(region, 64, offs, 1, None, 3, out, 128, None, None, st, 0, 0) == -1
     assert f(region, 64, offs, 1, None, 3, None, 128, None, ol, st, 0, 0) == -1  # out NULL with a capacity
     assert f(region, 64, offs, 1, None, 3, out, 128, None, ol, st, 63, 0) == -4  # no context
+
+
+def test_transform_host_cpu_leg_writes_negative_life_versions(ambry):
+    """The CPU leg of ambrycrc_transform_messages_host (device -1) writes each index life version as given,
+    -1 (MessageInfo.LIFE_VERSION_FROM_FRONTEND) included, as ValidatingTransformer.java:90 writes
+    msgInfo.getLifeVersion() and the device batch does: dense clean V3 messages (the CPU fast form) and
+    the mixed region (the general form), against the oracle."""
+    from test_gpu_transform import build_region, dense_v3_region
+
+    from ambry_amd.messages import transform_host
+
+    for region, offs in (dense_v3_region(MF, 60, seed=21), build_region(MF, 120, seed=22)):
+        life = np.random.default_rng(8).integers(-2, 4, size=len(offs)).astype(np.int16)
+        life[::5] = -1
+        out, oo, ol, st = transform_host(region, offs, header_version=3, life_version=life, device=-1)
+        pos = 0
+        for i, o in enumerate(offs):
+            exp_st, exp = MF.transform_message(region, o, life=int(life[i]), version=3)
+            assert int(st[i]) == exp_st, i
+            if exp is not None:
+                assert oo[i] == pos and out[pos:pos + len(exp)] == exp, i
+                pos += len(exp)
