@@ -145,6 +145,8 @@ _SIGNATURES = [
     ("ambrycrc_host_rates", ctypes.c_int,
      [ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),
     ("ambrycrc_last_host_path", ctypes.c_int, [ctypes.c_int]),
+    ("ambrycrc_set_host_cpu_threads", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    ("ambrycrc_host_calibrate", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),
     ("ambrycrc_host_msg_rates", ctypes.c_int,
      [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     ("ambrycrc_set_grid", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),

@@ -4,6 +4,7 @@
 #include "../../include/ambrycrc.h"
 
 #include <hip/hip_runtime.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -313,24 +314,39 @@ void reap_retired_ws(DevCtx* c) {
 // event on the stream (work already queued there may still read it), never freed in place.
 // (A destroyed stream's handle may be reused by a new stream; hipStreamDestroy drains the old
 // stream's work first, so the buffer is idle by then.)
-int stream_ws(DevCtx* c, hipStream_t s, size_t need, void** out, size_t* entry) {
-  // Under stream capture (a HIP graph) nothing here may query events, synchronize or allocate: a
-  // capture uses the stream's buffer as an earlier uncaptured call sized it, or gets EINVAL.
+//
+// Under stream capture (a HIP graph) nothing here may query events, synchronize or allocate: a
+// capture uses the stream's buffer as an earlier uncaptured call sized it, or gets EINVAL. The graph
+// then holds that buffer's address, so the entry is marked captured: when a later call grows it, or
+// the entry is evicted, the buffer is kept (c->ws_kept) until shutdown instead of being freed, and
+// replays stay valid. Replays share it with later calls on the stream, so they must be ordered with
+// them (launched on that stream), as any two calls on one stream are.
+int stream_ws(DevCtx* c, hipStream_t s, size_t need, void** out, size_t* entry, bool* capturing_out) {
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(s, &cap) != hipSuccess) return AMBRYCRC_EHIP;
   const bool capturing = cap != hipStreamCaptureStatusNone;
+  if (capturing_out) *capturing_out = capturing;
   if (!capturing) reap_retired_ws(c);
   DevCtx::StreamWs* w = nullptr;
   for (auto& e : c->ws_list)
     if (e.stream == s) w = &e;
   if (capturing && (!w || w->bytes < need)) return AMBRYCRC_EINVAL;
+  if (capturing) {
+    w->captured = true;
+    *entry = (size_t)(w - c->ws_list.data());
+    *out = w->ptr;
+    return AMBRYCRC_OK;
+  }
   if (!w && c->ws_list.size() >= kMaxStreamWs) {
     // evict the least recently used stream's buffer: retired behind its last call's event
     // (the entry's event moves with it), the entry reused for s
     w = &c->ws_list[0];
     for (auto& e : c->ws_list)
       if (e.tick < w->tick) w = &e;
-    if (w->ptr) {
+    if (w->ptr && w->captured) {
+      c->ws_kept.push_back(w->ptr);
+      if (w->last) (void)hipEventDestroy(w->last);
+    } else if (w->ptr) {
       if (w->last) {
         c->ws_retired.push_back({w->ptr, w->last});
       } else {
@@ -340,10 +356,10 @@ int stream_ws(DevCtx* c, hipStream_t s, size_t need, void** out, size_t* entry) 
     } else if (w->last) {
       (void)hipEventDestroy(w->last);
     }
-    *w = {s, nullptr, 0, nullptr, 0};
+    *w = {s, nullptr, 0, nullptr, 0, false};
   }
   if (!w) {
-    c->ws_list.push_back({s, nullptr, 0, nullptr, 0});
+    c->ws_list.push_back({s, nullptr, 0, nullptr, 0, false});
     w = &c->ws_list.back();
   }
   w->tick = ++c->ws_tick;
@@ -352,7 +368,11 @@ int stream_ws(DevCtx* c, hipStream_t s, size_t need, void** out, size_t* entry) 
     *out = w->ptr;
     return AMBRYCRC_OK;
   }
-  if (w->ptr) {
+  if (w->ptr && w->captured) {
+    c->ws_kept.push_back(w->ptr);
+    w->ptr = nullptr;
+    w->captured = false;
+  } else if (w->ptr) {
     hipEvent_t ev = nullptr;
     if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return AMBRYCRC_EHIP;
     if (hipEventRecord(ev, s) != hipSuccess) {
@@ -451,84 +471,138 @@ bool same_or_disjoint(const uint32_t* a, const uint32_t* b, size_t n) {
   return x + 4 * n <= y || y + 4 * n <= x;
 }
 
-int host_cpu_threads() {
-  for (const char* name : {"AMBRYCRC_CPU_THREADS", "OMP_NUM_THREADS"})
-    if (const char* v = getenv(name)) {
-      const int t = atoi(v);
-      if (t > 0) return std::min(t, 256);
+std::atomic<int> g_cpu_threads{0};  // the process's CPU-leg budget (ambrycrc_set_host_cpu_threads(-1, n)); 0: default
+
+int host_cpu_share() {
+  static const int share = [] {
+    int n = 1;
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) n = std::max(1, CPU_COUNT(&set));
+    // a cgroup v2 CPU quota ("max 100000" when unlimited): a container's share of a larger machine
+    if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+      char q[32] = {0};
+      long long period = 0;
+      if (fscanf(f, "%31s %lld", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0) {
+        const long long quota = atoll(q);
+        if (quota > 0) n = std::min<long long>(n, std::max<long long>(1, (quota + period - 1) / period));
+      }
+      fclose(f);
     }
-  cpu_set_t set;
-  return sched_getaffinity(0, sizeof(set), &set) == 0 ? std::max(1, CPU_COUNT(&set)) : 1;
+    if (const char* v = getenv("OMP_NUM_THREADS")) {
+      const int t = atoi(v);
+      if (t > 0) n = std::min(n, t);
+    }
+    return std::min(n, 256);
+  }();
+  return share;
 }
 
-double host_cpu_gibps() {
-  // The CPU leg's rate with all its threads at once, measured once per process: each thread hashes
-  // a slice (16 MiB a thread, 512 MiB at most) of a buffer the calling thread wrote with nontemporal
-  // stores -- so the timed pass reads DRAM, not the L3, from the pages one writer placed, as a
-  // caller's buffer is. Slices each thread wrote itself read 440-679 GiB/s against 172-246 measured
-  // on a 2 GiB sample the main thread wrote (r05ao, r05aq: 16 threads, their own slices near them
-  // and in their CCDs' L3); a single thread times threads (round 5's first form): 662 against 262.
-  static const double rate = [] {
-    const int t = host_cpu_threads();
-    const size_t slice = std::min<size_t>(16u << 20, ((size_t)512 << 20) / (size_t)t) & ~size_t(4095);
-    const size_t total = slice * (size_t)t;
-    std::unique_ptr<uint8_t[]> buf(new (std::nothrow) uint8_t[total]);  // not zero-filled: first touch below
-    if (!buf) return 1.0;
-    // The threads hash their slices once from a common start (all spawned and waiting: spawning
-    // inside the timed span read ~half the rate on a 16-CPU box), timed from the start to the last
-    // thread's end. (A second pass would read the L3.)
-    std::atomic<int> ready{0};
-    std::atomic<int> go{0};
-    std::atomic<int64_t> last_end{0};
-    std::atomic<uint32_t> sink{0};
-    std::vector<std::thread> th;
-    th.reserve(t);
-    {
-      uint8_t* p = buf.get();
+int host_cpu_threads(const DevCtx* c) {
+  int t = c ? c->cpu_threads.load(std::memory_order_relaxed) : 0;
+  if (t <= 0) t = g_cpu_threads.load(std::memory_order_relaxed);
+  if (t > 0) return t;
+  if (const char* v = getenv("AMBRYCRC_CPU_THREADS")) {
+    const int e = atoi(v);
+    if (e > 0) return std::min(e, 256);
+  }
+  return std::max(1, host_cpu_share() / 2);
+}
+
+namespace {
+// The calibration for `t` threads: each thread hashes its own slice (16 MiB, 256 MiB in all at most,
+// 1 MiB at least) of a buffer the calling thread wrote with nontemporal stores -- so the timed pass
+// reads DRAM, not the L3, from the pages one writer placed, as a caller's buffer is. Slices each
+// thread wrote itself read 440-679 GiB/s against 172-246 measured on a 2 GiB sample the main thread
+// wrote (r05ao, r05aq: 16 threads, their own slices near them and in their CCDs' L3); a single
+// thread times threads (round 5's first form): 662 against 262.
+double calibrate_cpu(int t) {
+  const size_t slice = std::max<size_t>(1u << 20, std::min<size_t>(16u << 20, ((size_t)256 << 20) / (size_t)t)) &
+                       ~size_t(4095);
+  const size_t total = slice * (size_t)t;
+  std::unique_ptr<uint8_t[]> buf(new (std::nothrow) uint8_t[total]);  // not zero-filled: first touch below
+  if (!buf) return 1.0;
+  // The threads hash their slices once from a common start (all spawned and waiting: spawning
+  // inside the timed span read ~half the rate on a 16-CPU box), timed from the start to the last
+  // thread's end. (A second pass would read the L3.)
+  std::atomic<int> ready{0};
+  std::atomic<int> go{0};
+  std::atomic<int64_t> last_end{0};
+  std::atomic<uint32_t> sink{0};
+  std::vector<std::thread> th;
+  th.reserve(t);
+  {
+    uint8_t* p = buf.get();
 #if defined(__x86_64__)
-      for (size_t i = 0; i < total; i += 16) {  // 16-B aligned (new[] of >= 16 MiB, 4 KiB slices)
-        const __m128i v = _mm_set_epi32((int)(i * 131u), (int)(i * 7u), (int)(i ^ 0x5bd1e995u), (int)i);
-        _mm_stream_si128(reinterpret_cast<__m128i*>(p + i), v);
-      }
-      _mm_sfence();
+    for (size_t i = 0; i < total; i += 16) {  // 16-B aligned (new[] of >= 1 MiB, 4 KiB slices)
+      const __m128i v = _mm_set_epi32((int)(i * 131u), (int)(i * 7u), (int)(i ^ 0x5bd1e995u), (int)i);
+      _mm_stream_si128(reinterpret_cast<__m128i*>(p + i), v);
+    }
+    _mm_sfence();
 #else
-      for (size_t i = 0; i < total; ++i) p[i] = (uint8_t)(i * 131u + 7u);
+    for (size_t i = 0; i < total; ++i) p[i] = (uint8_t)(i * 131u + 7u);
 #endif
+  }
+  auto body = [&](int k) {
+    const uint8_t* p = buf.get() + slice * (size_t)k;
+    ready.fetch_add(1);
+    while (go.load(std::memory_order_acquire) == 0) std::this_thread::yield();
+    sink ^= ambrycrc_update(0, p, slice);
+    const int64_t e = std::chrono::steady_clock::now().time_since_epoch().count();
+    int64_t cur = last_end.load();
+    while (e > cur && !last_end.compare_exchange_weak(cur, e)) {
     }
-    auto body = [&](int k) {
-      const uint8_t* p = buf.get() + slice * (size_t)k;
-      ready.fetch_add(1);
-      while (go.load(std::memory_order_acquire) == 0) std::this_thread::yield();
-      sink ^= ambrycrc_update(0, p, slice);
-      const int64_t e = std::chrono::steady_clock::now().time_since_epoch().count();
-      int64_t cur = last_end.load();
-      while (e > cur && !last_end.compare_exchange_weak(cur, e)) {
-      }
-    };
-    try {
-      for (int k = 0; k < t; ++k) th.emplace_back(body, k);
-    } catch (...) {  // no thread for every slice (the C ABI must not throw): release them, no estimate
-      go.store(1, std::memory_order_release);
-      for (auto& x : th) x.join();
-      return 1.0;
-    }
-    // (the main thread sleeps while it waits: spinning would take a CPU from the hashing threads)
-    while (ready.load() < t) std::this_thread::sleep_for(std::chrono::microseconds(20));
-    const int64_t t0 = std::chrono::steady_clock::now().time_since_epoch().count();
+  };
+  try {
+    for (int k = 0; k < t; ++k) th.emplace_back(body, k);
+  } catch (...) {  // no thread for every slice (the C ABI must not throw): release them, no estimate
     go.store(1, std::memory_order_release);
     for (auto& x : th) x.join();
-    const double best = std::chrono::duration<double>(std::chrono::steady_clock::duration(last_end.load() - t0)).count();
-    if (!(best > 0)) return 1.0;
-    return (double)total / best / (double)(1ull << 30);
-  }();
-  return rate;
+    return 1.0;
+  }
+  // (the main thread sleeps while it waits: spinning would take a CPU from the hashing threads)
+  while (ready.load() < t) std::this_thread::sleep_for(std::chrono::microseconds(20));
+  const int64_t t0 = std::chrono::steady_clock::now().time_since_epoch().count();
+  go.store(1, std::memory_order_release);
+  for (auto& x : th) x.join();
+  const double best = std::chrono::duration<double>(std::chrono::steady_clock::duration(last_end.load() - t0)).count();
+  if (!(best > 0)) return 1.0;
+  return (double)total / best / (double)(1ull << 30);
+}
+}  // namespace
+
+double host_cpu_gibps(int threads) {
+  static std::mutex mu;
+  static std::vector<std::pair<int, double>> cache;  // (threads, GiB/s), one calibration per budget
+  threads = std::max(1, std::min(threads, 256));
+  std::lock_guard<std::mutex> g(mu);  // one calibration at a time: concurrent ones would share the CPUs
+  for (const auto& e : cache)
+    if (e.first == threads) return e.second;
+  const double r = calibrate_cpu(threads);
+  cache.emplace_back(threads, r);
+  return r;
 }
 
-bool host_take_cpu(DevCtx* c, int device, int pinned) {
+// The CPU leg's CRC rate on c: as its large calls measured it, else the calibration at c's budget.
+double host_batch_cpu_gibps(const DevCtx* c) {
+  const double r = c ? c->cpu_batch_gibps.load() : -1.0;
+  return r >= 0 ? r : host_cpu_gibps(host_cpu_threads(c));
+}
+
+bool host_take_cpu(DevCtx* c, int device, int pinned, uint64_t bytes) {
   if (device < 0) return true;
   if (!c || c->host_policy == 1) return false;
   if (c->host_policy == 2) return true;
-  return !pinned && host_cpu_gibps() > c->gpu_host_gibps.load();
+  if (pinned) return false;
+  const bool cpu = host_batch_cpu_gibps(c) > c->gpu_host_gibps.load();
+  if (bytes >= (64ull << 20) && c->batch_calls.fetch_add(1) % 16 == 15) return !cpu;  // the other leg's rate
+  return cpu;
+}
+
+void host_note_cpu(DevCtx* c, uint64_t bytes, double seconds) {
+  if (!c || bytes < (64ull << 20) || seconds <= 0) return;
+  const double r = (double)bytes / seconds / (double)(1ull << 30);
+  const double old = c->cpu_batch_gibps.load();
+  c->cpu_batch_gibps.store(old < 0 ? r : 0.5 * old + 0.5 * r);
 }
 
 // The CPU leg of a message entry before it has been measured: verify parses and CRCs each
@@ -536,7 +610,9 @@ bool host_take_cpu(DevCtx* c, int device, int pinned) {
 // transform 40 / 60 GiB/s for 4 KiB / 64 KiB PUTs, against a CRC rate of 146-262: ~50 % and ~25 %).
 double host_msg_cpu_gibps(const DevCtx* c, int op) {
   const double r = c->msg_cpu_gibps[op].load();
-  return r >= 0 ? r : host_cpu_gibps() * 0.01 * (op == kMsgVerify ? AMBRY_HOST_VERIFY_CPU_PCT : AMBRY_HOST_XFORM_CPU_PCT);
+  return r >= 0 ? r
+                : host_cpu_gibps(host_cpu_threads(c)) * 0.01 *
+                      (op == kMsgVerify ? AMBRY_HOST_VERIFY_CPU_PCT : AMBRY_HOST_XFORM_CPU_PCT);
 }
 
 bool host_take_cpu_msg(DevCtx* c, int device, int pinned, int op, uint64_t bytes) {
@@ -597,6 +673,7 @@ void free_ctx(DevCtx* c) {
     (void)hipFree(r.ptr);
     (void)hipEventDestroy(r.done);
   }
+  for (void* p : c->ws_kept) (void)hipFree(p);
   for (auto& e : c->pending) {
     (void)hipEventDestroy(e.a);
     (void)hipEventDestroy(e.b);
@@ -996,9 +1073,10 @@ int ambrycrc_batch_multi(const void* const* ptrs, const uint64_t* lens, const ui
     DevCtx* c0 = ctx_for(dev[0]);
     double gpus = 0;
     for (int g = 0; g < ndev; ++g) gpus += ctx_for(dev[g])->gpu_host_gibps.load();
-    const bool cpu = c0->host_policy == 2 || (c0->host_policy == 0 && !pinned && host_cpu_gibps() > gpus);
+    const int policy = c0->host_policy.load();
+    const bool cpu = policy == 2 || (policy == 0 && !pinned && host_batch_cpu_gibps(c0) > gpus);
     c0->last_host_path.store(cpu ? 0 : 1);
-    if (cpu) return ambrycrc_batch_cpu(ptrs, lens, crc_in, out, n, host_cpu_threads());
+    if (cpu) return ambrycrc_batch_cpu(ptrs, lens, crc_in, out, n, host_cpu_threads(c0));
   }
   std::vector<size_t> cut(ndev + 1, n);
   const int src = ambrycrc_shard_by_bytes(lens, n, ndev, cut.data());
@@ -1106,8 +1184,7 @@ int ambrycrc_set_transform_verdict(int device, int host) {
   DevCtx* c = ctx_for(device);
   if (!c) return AMBRYCRC_ENOINIT;
   if (host != 0 && host != 1) return AMBRYCRC_EINVAL;
-  const int prev = c->xform_host_verdict;
-  c->xform_host_verdict = host;
+  const int prev = c->xform_host_verdict.exchange(host);
   return prev;
 }
 
@@ -1820,14 +1897,16 @@ int ambrycrc_batch_host(const void* const* ptrs, const uint64_t* lens, const uin
   if (!ptrs || !lens || !out) return AMBRYCRC_EINVAL;
   DevCtx* c;
   if (const int rc = host_ctx(device, &c)) return rc;
-  if (host_take_cpu(c, device, pinned)) {
-    if (c) c->last_host_path.store(0);
-    return ambrycrc_batch_cpu(ptrs, lens, crc_in, out, n, host_cpu_threads());
-  }
-  c->last_host_path.store(1);
   uint64_t bytes = 0;
   for (size_t i = 0; i < n; ++i) bytes += lens[i];
   const auto t0 = std::chrono::steady_clock::now();
+  if (host_take_cpu(c, device, pinned, bytes)) {
+    if (c) c->last_host_path.store(0);
+    const int rc = ambrycrc_batch_cpu(ptrs, lens, crc_in, out, n, host_cpu_threads(c));
+    if (rc == AMBRYCRC_OK && device >= 0) host_note_cpu(c, bytes, seconds_since(t0));
+    return rc;
+  }
+  c->last_host_path.store(1);
   const int rc = batch_host_gpu(c, ptrs, lens, crc_in, out, n, device, pinned);
   if (rc == AMBRYCRC_OK && !pinned) host_note_gpu(c, bytes, seconds_since(t0));
   return rc;
@@ -1842,7 +1921,7 @@ int ambrycrc_verify_messages_host(const uint8_t* region, uint64_t region_len, co
   const bool cpu = host_take_cpu_msg(c, device, pinned, kMsgVerify, region_len);
   if (c) c->last_host_path.store(cpu ? 0 : 1);
   const auto t0 = std::chrono::steady_clock::now();
-  const int rc = cpu ? verify_messages_cpu(region, region_len, msg_off, m, status, msg_end, host_cpu_threads())
+  const int rc = cpu ? verify_messages_cpu(region, region_len, msg_off, m, status, msg_end, host_cpu_threads(c))
                      : verify_messages_host_gpu(c, region, region_len, msg_off, m, status, msg_end, device, pinned);
   if (rc == AMBRYCRC_OK && !pinned && device >= 0) host_note_msg(c, kMsgVerify, cpu, region_len, seconds_since(t0));
   return rc;
@@ -1861,7 +1940,7 @@ int ambrycrc_transform_messages_host(const uint8_t* region, uint64_t region_len,
   if (c) c->last_host_path.store(cpu ? 0 : 1);
   const auto t0 = std::chrono::steady_clock::now();
   const int rc = cpu ? transform_messages_cpu(region, region_len, msg_off, m, life_version, header_version, out, out_cap,
-                                              out_off, out_len, status, host_cpu_threads())
+                                              out_off, out_len, status, host_cpu_threads(c))
                      : transform_messages_host_gpu(c, region, region_len, msg_off, m, life_version, header_version, out,
                                                    out_cap, out_off, out_len, status, device, pinned);
   if (rc == AMBRYCRC_OK && !pinned && device >= 0) host_note_msg(c, kMsgTransform, cpu, region_len, seconds_since(t0));
@@ -1872,18 +1951,38 @@ int ambrycrc_set_host_policy(int device, int policy) {
   DevCtx* c = ctx_for(device);
   if (!c) return AMBRYCRC_ENOINIT;
   if (policy < 0 || policy > 2) return AMBRYCRC_EINVAL;
-  const int prev = c->host_policy;
-  c->host_policy = policy;
-  return prev;
+  return c->host_policy.exchange(policy);
 }
 
 int ambrycrc_host_rates(int device, double* cpu_gibps, double* gpu_gibps, int* cpu_threads) {
+  DevCtx* c = device < 0 ? nullptr : ctx_for(device);
+  if (!c && device >= 0) return AMBRYCRC_ENOINIT;
+  const double cpu = host_batch_cpu_gibps(c), gpu = c ? c->gpu_host_gibps.load() : 0.0;
+  if (cpu_gibps) *cpu_gibps = cpu;
+  if (gpu_gibps) *gpu_gibps = gpu;
+  if (cpu_threads) *cpu_threads = host_cpu_threads(c);
+  return cpu > gpu ? 0 : 1;  // auto's leg for pageable bytes, whatever the policy
+}
+
+int ambrycrc_set_host_cpu_threads(int device, int threads) {
+  if (threads < 0 || threads > 256) return AMBRYCRC_EINVAL;
+  if (device < 0) return g_cpu_threads.exchange(threads);
   DevCtx* c = ctx_for(device);
   if (!c) return AMBRYCRC_ENOINIT;
-  if (cpu_gibps) *cpu_gibps = host_cpu_gibps();
-  if (gpu_gibps) *gpu_gibps = c->gpu_host_gibps.load();
-  if (cpu_threads) *cpu_threads = host_cpu_threads();
-  return host_cpu_gibps() > c->gpu_host_gibps.load() ? 0 : 1;  // auto's leg for pageable bytes, whatever the policy
+  const int prev = c->cpu_threads.exchange(threads);
+  if (prev != threads) {  // the CPU legs' measured rates were at the old budget
+    c->cpu_batch_gibps.store(-1.0);
+    for (auto& r : c->msg_cpu_gibps) r.store(-1.0);
+  }
+  return prev;
+}
+
+int ambrycrc_host_calibrate(int device, double* cpu_gibps) {
+  DevCtx* c = device < 0 ? nullptr : ctx_for(device);
+  if (!c && device >= 0) return AMBRYCRC_ENOINIT;
+  const double r = host_cpu_gibps(host_cpu_threads(c));
+  if (cpu_gibps) *cpu_gibps = r;
+  return AMBRYCRC_OK;
 }
 
 int ambrycrc_host_msg_rates(int device, int op, double* cpu_gibps, double* gpu_gibps) {

@@ -96,7 +96,7 @@ struct DevCtx {
   uint32_t* d_path = nullptr;  // (inside the d_img allocation)
   // The transform fast path's verdict read by the host (ambrycrc_set_transform_verdict): off by
   // default -- the general path is then enqueued behind a device gate, and the call never blocks.
-  int xform_host_verdict = 0;
+  std::atomic<int> xform_host_verdict{0};
   // Pinned words for one-word device-to-host reads (the host verdict): a call holds slot k (busy[k])
   // from its copy until it has read the word, so no two calls in flight share one; with every slot
   // held the call takes the device-gated form instead.
@@ -117,9 +117,17 @@ struct DevCtx {
   // pageable host bytes to the CPU leg when the CPU threads' CRC rate beats gpu_host_gibps, the
   // GPU host path's rate (PCIe-bound: 51 GiB/s measured, BENCH_r04 host_path; refreshed by every
   // GPU host call of >= 64 MiB). last_host_path: 0 CPU, 1 GPU, -1 none yet.
-  int host_policy = 0;
+  std::atomic<int> host_policy{0};
   std::atomic<double> gpu_host_gibps{51.0};
   std::atomic<int> last_host_path{-1};
+  // The CPU leg's thread budget on this device (ambrycrc_set_host_cpu_threads; 0: the process's,
+  // host_cpu_threads). Auto compares the CPU leg's rate AT this budget with the GPU's.
+  std::atomic<int> cpu_threads{0};
+  // ambrycrc_batch_host's CPU leg as its calls of >= 64 MiB measured it (EWMA; -1: not yet, the
+  // calibration at the budget stands for it); under auto every 16th such pageable call takes the other
+  // leg, so both rates stay current.
+  std::atomic<double> cpu_batch_gibps{-1.0};
+  std::atomic<uint32_t> batch_calls{0};
   // The message entries (kMsgVerify, kMsgTransform) compare their own legs' rates over region
   // bytes, GiB/s: a CPU leg parses and (transform) copies each message, so the CRC rate above does
   // not stand for it. Each leg's rate is refreshed by its calls of >= 64 MiB (EWMA); the CPU legs
@@ -146,6 +154,7 @@ struct DevCtx {
     size_t bytes;
     hipEvent_t last;  // recorded on `stream` after each call's work (WsLease), null before the first
     uint64_t tick;    // last use, for eviction
+    bool captured;    // a stream capture (HIP graph) recorded this buffer: never freed before shutdown
   };
   struct RetiredWs {
     void* ptr;
@@ -154,6 +163,7 @@ struct DevCtx {
   std::mutex ws_mu;
   std::vector<StreamWs> ws_list;  // at most kMaxStreamWs: the least recently used is evicted
   std::vector<RetiredWs> ws_retired;
+  std::vector<void*> ws_kept;  // buffers a captured graph may still use, replaced or evicted: freed at shutdown
   uint64_t ws_tick = 0;
   bool timing = false;
   std::vector<EventPair> pending, free_events;
@@ -168,14 +178,19 @@ struct DevCtx {
 };
 
 int hip_err(hipError_t e);
-// Host-resident dispatch: the CPU threads the CPU leg uses (AMBRYCRC_CPU_THREADS, else
-// OMP_NUM_THREADS, else the CPUs this process may run on) and their combined CRC rate in GiB/s
-// (measured once per process on a 32 MiB buffer, x threads x 0.85).
-int host_cpu_threads();
-double host_cpu_gibps();
+// Host-resident dispatch: the CPU threads the CPU leg of device c uses -- its budget
+// (ambrycrc_set_host_cpu_threads), else the process's (the same call with device -1), else
+// AMBRYCRC_CPU_THREADS, else half this process's CPU share (host_cpu_share: affinity, cgroup quota,
+// OMP_NUM_THREADS), so the server's own network and disk threads keep the other half.
+int host_cpu_share();
+int host_cpu_threads(const DevCtx* c = nullptr);
+// The CPU leg's CRC rate in GiB/s with `threads` threads hashing DRAM-resident bytes at once
+// (calibrated once per thread count: ambrycrc_host_calibrate, or the first auto decision needing it).
+double host_cpu_gibps(int threads);
 // True when a host call over `bytes` of host memory should take the CPU leg (device < 0, the
 // CPU policy, or auto with pageable bytes the CPU threads hash faster than the GPU host path).
-bool host_take_cpu(DevCtx* c, int device, int pinned);
+bool host_take_cpu(DevCtx* c, int device, int pinned, uint64_t bytes);
+void host_note_cpu(DevCtx* c, uint64_t bytes, double seconds);
 // After a GPU host call over `bytes` that took `seconds`: refresh c->gpu_host_gibps.
 void host_note_gpu(DevCtx* c, uint64_t bytes, double seconds);
 // The message entries' leg choice and rate tracking (DevCtx::msg_*_gibps).
@@ -191,7 +206,7 @@ size_t ws_need(size_t n);
 // request) holds at most this many buffers; the least recently used one is retired behind its
 // last call's event and freed once that work has completed.
 constexpr size_t kMaxStreamWs = 16;
-int stream_ws(DevCtx* c, hipStream_t s, size_t need, void** out, size_t* entry);
+int stream_ws(DevCtx* c, hipStream_t s, size_t need, void** out, size_t* entry, bool* capturing);
 // Largest chunk the group phase takes whole for a batch of n chunks on c's variant (0: none).
 uint64_t batch_small_max(const DevCtx* c, size_t n);
 // Plan + CRC kernels for n chunks on stream s (ws: >= ws_need(n) bytes). exp_fill, copy_dst,
@@ -254,20 +269,22 @@ struct WsLease {
   DevCtx* ctx = nullptr;
   hipStream_t stream = nullptr;
   size_t entry = ~size_t(0);
+  bool capturing = false;
   // On return *ws is the caller's buffer (checked against need) or the stream's default one.
   int acquire(DevCtx* c, hipStream_t s, void** ws, size_t ws_bytes, size_t need) {
     if (*ws) return ws_bytes < need ? AMBRYCRC_EINVAL : AMBRYCRC_OK;
     lk = std::unique_lock<std::mutex>(c->ws_mu);
-    const int rc = stream_ws(c, s, need, ws, &entry);
+    const int rc = stream_ws(c, s, need, ws, &entry, &capturing);
     if (rc == AMBRYCRC_OK) {
       ctx = c;
       stream = s;
     }
     return rc;
   }
-  // The call's work is enqueued: mark the buffer's last use on its stream (still under ws_mu).
+  // The call's work is enqueued: mark the buffer's last use on its stream (still under ws_mu). Not
+  // under capture: an event recorded there would belong to the graph, not to its replays.
   ~WsLease() {
-    if (!ctx || entry >= ctx->ws_list.size()) return;
+    if (!ctx || capturing || entry >= ctx->ws_list.size()) return;
     DevCtx::StreamWs& w = ctx->ws_list[entry];
     if (!w.last && hipEventCreateWithFlags(&w.last, hipEventDisableTiming) != hipSuccess) w.last = nullptr;
     if (w.last) (void)hipEventRecord(w.last, stream);

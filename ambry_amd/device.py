@@ -208,6 +208,19 @@ def host_rates(device: int = 0) -> dict:
     return {"cpu_gibps": c.value, "gpu_gibps": g.value, "cpu_threads": t.value, "auto_leg": "gpu" if leg else "cpu"}
 
 
+def set_host_cpu_threads(device: int, threads: int) -> int:
+    """The CPU leg's thread budget on `device` (-1: the process's; 0: the default, half this process's CPU
+    share) -- ambrycrc_set_host_cpu_threads. Returns the previous setting (0 = default)."""
+    return check(lib().ambrycrc_set_host_cpu_threads(device, int(threads)), "ambrycrc_set_host_cpu_threads")
+
+
+def host_calibrate(device: int = -1) -> float:
+    """Calibrates the CPU leg at `device`'s budget now (ambrycrc_host_calibrate); returns its GiB/s."""
+    r = ctypes.c_double()
+    check(lib().ambrycrc_host_calibrate(device, ctypes.byref(r)), "ambrycrc_host_calibrate")
+    return r.value
+
+
 def host_msg_rates(device: int = 0, op: str = "verify") -> dict:
     """The rates auto compares for the host message entries (op "verify" / "transform";
     ambrycrc_host_msg_rates) and the leg it takes for pageable bytes."""

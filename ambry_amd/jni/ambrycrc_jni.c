@@ -34,6 +34,7 @@
  *   void nativeRangeChecksums(ByteBuffer file, long[] first, long[] second, int[] out, int device)
  *                                                                      FileStore.java:567-595
  *   int  nativeSetHostPolicy(int device, int policy)
+ *   int  nativeSetHostCpuThreads(int device, int threads)
  *   int  nativeHostRates(int device, double[] out)
  *   int  nativeLastHostPath(int device)
  * CRC values travel as Java ints holding the uint32 bit pattern.
@@ -513,5 +514,14 @@ JNIEXPORT jint JNICALL JNI_FN(nativeLastHostPath)(JNIEnv* env, jclass cls, jint 
   (void)cls;
   const int r = ambrycrc_last_host_path(device);
   if (r < -1) return raise(env, r), -1;
+  return r;
+}
+
+/* NativeCrc32.setHostCpuThreads: the CPU leg's thread budget (ambrycrc_set_host_cpu_threads; device -1: the
+ * process's, threads 0: the default); returns the previous one. */
+JNIEXPORT jint JNICALL JNI_FN(nativeSetHostCpuThreads)(JNIEnv* env, jclass cls, jint device, jint threads) {
+  (void)cls;
+  const int r = ambrycrc_set_host_cpu_threads(device, threads);
+  if (r < 0) return raise(env, r), -1;
   return r;
 }

@@ -27,6 +27,7 @@ import argparse
 import json
 import os
 import sys
+import resource
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -259,15 +260,24 @@ def host_path_rate(torch, args):
     host.view(torch.int64).random_()
     pageable = host.numpy().copy()
 
-    def best_of(fn, reps=3):
+    cpu_cost = {}
+
+    def best_of(fn, reps=3, name=None):
+        """Best-of-reps GiB/s; with `name`, also this process's CPU-seconds per GiB over the reps
+        (getrusage user + system: the CPU leg's threads, or the GPU leg's staging copies and waits)."""
         fn()
         best = None
+        r0 = resource.getrusage(resource.RUSAGE_SELF)
         for _ in range(reps):
             t0 = time.perf_counter()
             fn()
             torch.cuda.synchronize()
             el = time.perf_counter() - t0
             best = el if best is None else min(best, el)
+        r1 = resource.getrusage(resource.RUSAGE_SELF)
+        if name:
+            cpu_s = (r1.ru_utime - r0.ru_utime) + (r1.ru_stime - r0.ru_stime)
+            cpu_cost[name] = round(cpu_s / (reps * total / 2**30), 4)
         return total / best / 2**30
 
     dev = torch.empty(total, dtype=torch.uint8, device="cuda")
@@ -278,11 +288,18 @@ def host_path_rate(torch, args):
     try:
         for name, base in (("pinned", host.data_ptr()), ("pageable", pageable.ctypes.data)):
             chunks = [(base + i * chunk, chunk) for i in range(nchunks)]
-            res[name] = best_of(lambda: D.crc32_batch_host(chunks, device=0, pinned=name == "pinned"))
-        # the CPU leg on the same pageable sample, and the leg the default (auto) policy takes
+            res[name] = best_of(lambda: D.crc32_batch_host(chunks, device=0, pinned=name == "pinned"),
+                                name="gpu_leg_" + name)
+        # the CPU leg on the same pageable sample at its default budget (half the CPU share) and at the
+        # whole share, and the leg the default (auto) policy takes at the default budget
         D.set_host_policy(0, D.HOST_CPU)
         chunks = [(pageable.ctypes.data + i * chunk, chunk) for i in range(nchunks)]
-        res["cpu_leg"] = best_of(lambda: D.crc32_batch_host(chunks, device=0))
+        res["cpu_leg"] = best_of(lambda: D.crc32_batch_host(chunks, device=0), name="cpu_leg_budget")
+        budget = D.host_rates(0)["cpu_threads"]
+        share = D.set_host_cpu_threads(0, 0) or 0  # (0: it was the default)
+        D.set_host_cpu_threads(0, max(1, 2 * budget))
+        res["cpu_leg_share"] = best_of(lambda: D.crc32_batch_host(chunks, device=0), name="cpu_leg_share")
+        D.set_host_cpu_threads(0, share)
         D.set_host_policy(0, D.HOST_AUTO)
         res["auto"] = best_of(lambda: D.crc32_batch_host(chunks, device=0))
         auto_leg = "gpu" if D.last_host_path(0) == 1 else "cpu"
@@ -295,8 +312,10 @@ def host_path_rate(torch, args):
             "frac_of_h2d_roof": round(res["pinned"] / roof, 4),
             "dispatch": {"cpu_leg_pageable": round(res["cpu_leg"], 2), "auto_pageable": round(res["auto"], 2),
                          "auto_leg": auto_leg, "cpu_threads": rates["cpu_threads"],
+                         "cpu_leg_pageable_2x_threads": round(res["cpu_leg_share"], 2),
                          "policy_cpu_estimate": round(rates["cpu_gibps"], 1),
-                         "policy_gpu_estimate": round(rates["gpu_gibps"], 1)},
+                         "policy_gpu_estimate": round(rates["gpu_gibps"], 1),
+                         "host_cpu_s_per_gib": cpu_cost},
             "sample": f"{nchunks} x 4 MiB host chunks (2 GiB), synchronous ambrycrc_batch_host (H2D + kernels + "
                       "D2H of CRCs), best of 3 after one untimed pass; pinned = hipHostMalloc'd source, "
                       "pageable = malloc'd source staged by the library's copy threads"}

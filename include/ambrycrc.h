@@ -399,12 +399,28 @@ int ambrycrc_batch_host(const void* const* ptrs, const uint64_t* lens, const uin
  * policy. Replaces nothing in the reference, whose callers (NettyServerRequest.java:35,54,
  * StoreMessageReadSet.java:170-188) hold exactly such host buffers. */
 int ambrycrc_set_host_policy(int device, int policy);
-/* The rates the auto policy compares for ambrycrc_batch_host: *cpu_gibps (the CLMUL CPU leg's rate measured once per process
- * with all its threads, each over its own 16 MiB slice of a buffer past the L3), *gpu_gibps (the
- * GPU host path: 51 GiB/s measured, refreshed by each pageable GPU call of >= 64 MiB), *cpu_threads (AMBRYCRC_CPU_THREADS, else OMP_NUM_THREADS, else this
- * process's CPUs). Returns the leg auto takes for pageable bytes (0 CPU, 1 GPU), or < 0. Any
- * output may be NULL. */
+/* The rates the auto policy compares for ambrycrc_batch_host: *cpu_gibps (the CLMUL CPU leg's rate
+ * at the device's thread budget: as its pageable calls of >= 64 MiB measured it, else the calibration
+ * at that budget -- each thread over its own slice of a buffer past the L3), *gpu_gibps (the GPU host
+ * path: 51 GiB/s measured, refreshed by each pageable GPU call of >= 64 MiB; under auto every 16th
+ * such call takes the other leg, so both stay current), *cpu_threads (the budget,
+ * ambrycrc_set_host_cpu_threads). Returns the leg auto takes for pageable bytes (0 CPU, 1 GPU), or
+ * < 0. Any output may be NULL. device -1: the process's budget and CPU rate, no GPU (gpu 0). */
 int ambrycrc_host_rates(int device, double* cpu_gibps, double* gpu_gibps, int* cpu_threads);
+/* The CPU budget of the host-resident CPU leg: how many threads ambrycrc_batch_host,
+ * _verify_messages_host and _transform_messages_host use on `device` when they take it, and the budget
+ * at which auto rates that leg. threads 0 = the default: the process's budget (this call with device
+ * -1), else AMBRYCRC_CPU_THREADS, else half the CPUs this process may use (affinity, cgroup v2 quota,
+ * OMP_NUM_THREADS) -- the other half stays with the server's own network and disk threads, which the
+ * reference runs on the same cores (NettyServerRequest.java:35,54, StoreMessageReadSet.java:170-188).
+ * Returns the previous setting (0 = default), AMBRYCRC_EINVAL (threads outside 0..256) or
+ * AMBRYCRC_ENOINIT. A change forgets the CPU legs' measured rates (they were at the old budget). */
+int ambrycrc_set_host_cpu_threads(int device, int threads);
+/* Runs the CPU leg's calibration at `device`'s budget now (once per thread count per process; up to
+ * 256 MiB written and hashed by the budget's threads, ~50-200 ms) instead of inside the first auto
+ * decision that needs it, and returns the rate in *cpu_gibps (may be NULL). device -1: the process's
+ * budget. A server calls it at start-up, before traffic. */
+int ambrycrc_host_calibrate(int device, double* cpu_gibps);
 /* The leg the device's last host call took: 0 CPU, 1 GPU, -1 none yet. */
 int ambrycrc_last_host_path(int device);
 /* The rates auto compares for the host message entries (op 0: ambrycrc_verify_messages_host, 1:
@@ -544,10 +560,13 @@ int ambrycrc_get_variant(int device);
 int ambrycrc_set_region_mode(int device, int enable);
 int ambrycrc_get_region_mode(int device);
 int ambrycrc_last_message_mode(int device);
-/* The path the device's last ambrycrc_transform_messages_dev call (or _host slab) took: 1 = the one-pass
- * fast path alone (header V3, every message a clean dense V3 PUT with canonical properties), 0 = the
- * general path (after the fast pass gave up, or without it), -1 = none yet. When that call left
- * the verdict on the device (the default), this waits for the device to go idle and reads it. */
+/* Diagnostic, for tests and profiles only: the path the device's last ambrycrc_transform_messages_dev
+ * call (or _host slab) took: 1 = the one-pass fast path alone (header V3, every message a clean dense V3
+ * PUT with canonical properties), 0 = the general path (after the fast pass gave up, or without it),
+ * -1 = none yet. One word per device, written by every transform on every stream: with concurrent
+ * transforms it names whichever finished last. When that call left the verdict on the device (the
+ * default), this waits for the whole device to go idle (hipDeviceSynchronize) and reads it -- do not
+ * call it while another thread captures a graph. */
 int ambrycrc_last_transform_path(int device);
 /* How ambrycrc_transform_messages_dev learns whether its fast path took the batch: 0 (the default;
  * AMBRYCRC_XFORM_HOST_VERDICT=1 at init sets 1) = on the device, the general path enqueued behind a

@@ -307,6 +307,15 @@ public final class NativeCrc32 implements Checksum {
     return out;
   }
 
+  /**
+   * The CPU leg's thread budget on `device` (-1: the process's; 0: the default, half the CPUs this process may
+   * use, leaving the rest to the server's network and disk threads) -- ambrycrc_set_host_cpu_threads. HOST_AUTO
+   * rates the CPU leg at this budget. Returns the previous setting.
+   */
+  public static int setHostCpuThreads(int device, int threads) {
+    return nativeSetHostCpuThreads(device, threads);
+  }
+
   /** The leg `device`'s last host-resident call took: 0 the CPU, 1 the GPU, -1 none yet. */
   public static int lastHostPath(int device) {
     return nativeLastHostPath(device);
@@ -363,6 +372,8 @@ public final class NativeCrc32 implements Checksum {
   private static native int nativeSetHostPolicy(int device, int policy);
 
   private static native int nativeHostRates(int device, double[] out);
+
+  private static native int nativeSetHostCpuThreads(int device, int threads);
 
   private static native int nativeLastHostPath(int device);
 }

@@ -231,6 +231,7 @@ JNIEXPORT jint JNICALL FN(nativeChainMessages)(JNIEnv*, jclass, jobject, jlong, 
 JNIEXPORT jint JNICALL FN(nativeSetHostPolicy)(JNIEnv*, jclass, jint, jint);
 JNIEXPORT jint JNICALL FN(nativeHostRates)(JNIEnv*, jclass, jint, jdoubleArray);
 JNIEXPORT jint JNICALL FN(nativeLastHostPath)(JNIEnv*, jclass, jint);
+JNIEXPORT jint JNICALL FN(nativeSetHostCpuThreads)(JNIEnv*, jclass, jint, jint);
 
 static uint8_t* slurp(const char* path, size_t* n) {
   FILE* f = fopen(path, "rb");
@@ -699,6 +700,10 @@ int main(int argc, char** argv) {
   report("rates_short", FN(nativeHostRates)(&g_env, NULL, 0, &jrates2));
   report("rates_no_context", FN(nativeHostRates)(&g_env, NULL, 0, &jrates));
   report("last_path_no_context", FN(nativeLastHostPath)(&g_env, NULL, 0));
+  report("cpu_threads_set", FN(nativeSetHostCpuThreads)(&g_env, NULL, -1, 3));
+  report("cpu_threads_prev", FN(nativeSetHostCpuThreads)(&g_env, NULL, -1, 0));
+  report("cpu_threads_bad", FN(nativeSetHostCpuThreads)(&g_env, NULL, -1, -1));
+  report("cpu_threads_no_context", FN(nativeSetHostCpuThreads)(&g_env, NULL, 0, 2));
 
   FN(nativeInit)(&g_env, NULL, 0); /* no GPU in the build container: the init error is thrown */
   report("init_no_gpu", 0);

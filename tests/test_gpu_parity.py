@@ -537,6 +537,55 @@ def test_hip_graph_capture_and_replay(gpu, oracle):
         assert np.array_equal(host_u32(out), oracle.batch(new, offs, lens)), seed
 
 
+def test_hip_graph_default_workspace_outlives_growth_and_eviction(gpu, oracle):
+    """A graph captured with the stream's DEFAULT workspace (d_ws = NULL) stays valid after that workspace
+    is replaced: a later, larger uncaptured call on the same stream grows it, and calls on 17 other streams
+    evict the stream's entry (kMaxStreamWs = 16). The captured buffer is kept until shutdown, so every
+    replay still CRCs the current bytes exactly (a freed buffer would be read by the replay)."""
+    torch = _torch()
+    offs, lens = [0, 5, 4096, 1 << 20], [100, 70000, 1 << 20, (2 << 20) - 3]
+    mem = stream_bytes(41, 0, 3 << 20)
+    base = dev_bytes(mem)
+    off, ln = dev_u64(offs), dev_u64(lens)
+    out = torch.empty(4, dtype=torch.int32, device="cuda")
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        gpu.crc32_batch(base, off, ln, out=out)  # sizes the stream's default workspace
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g, stream=s):
+            gpu.crc32_batch(base, off, ln, out=out)
+    torch.cuda.synchronize()
+
+    def replay_and_check(seed):
+        new = stream_bytes(seed, 0, 3 << 20)
+        base.copy_(torch.from_numpy(new).cuda())
+        with torch.cuda.stream(s):
+            g.replay()
+        torch.cuda.synchronize()
+        assert np.array_equal(host_u32(out), oracle.batch(new, offs, lens)), seed
+
+    replay_and_check(42)
+    # growth: 300,000 chunks need a far larger workspace on the same stream
+    n = 300_000
+    big_off = dev_u64(np.arange(n, dtype=np.int64) * 7)
+    big_ln = dev_u64(np.full(n, 9, dtype=np.int64))
+    with torch.cuda.stream(s):
+        big = gpu.crc32_batch(base, big_off, big_ln)
+    torch.cuda.synchronize()
+    cur = base.cpu().numpy()
+    assert np.array_equal(host_u32(big)[:1000], oracle.batch(cur, np.arange(1000) * 7, np.full(1000, 9)))
+    replay_and_check(43)
+    # eviction: more streams than the context keeps default workspaces for
+    for _ in range(17):
+        t = torch.cuda.Stream()
+        with torch.cuda.stream(t):
+            gpu.crc32_batch(base, off, ln)
+    torch.cuda.synchronize()
+    replay_and_check(44)
+
+
 def test_host_path_concurrent_threads(gpu, oracle):
     """Host entry points called from several host threads at once (the reference calls Crc32
     from the ChunkFiller, network and crypto threads): batch_host, verify_trailed_host and the

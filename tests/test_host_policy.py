@@ -108,3 +108,44 @@ def test_transform_messages_host_cpu_leg_fast_form(ambry):
         assert exp_st == 0 and oo[i] == o - offs[0] and out[oo[i]:oo[i] + ol[i]] == exp, i
     out2, _, _, st2 = transform_host(region, offs, device=-1)
     assert list(st2) == [0] * len(offs) and out2 == region[offs[0]:]
+
+
+def test_cpu_budget_process_default_and_calibration(ambry):
+    """The CPU leg's budget (ambrycrc_set_host_cpu_threads): the default is half this process's CPU share
+    (the rest stays with the server's own threads), a process budget set with device -1 is what device -1
+    calls and ambrycrc_host_rates report, the calibration is per budget (more threads, a higher rate, up to
+    the memory bound), and the CPU leg's results do not depend on it."""
+    import os
+
+    from ambry_amd import device as D
+
+    share = len(os.sched_getaffinity(0))
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit() and int(os.environ["OMP_NUM_THREADS"]) > 0:
+        share = min(share, int(os.environ["OMP_NUM_THREADS"]))
+    prev = D.set_host_cpu_threads(-1, 0)
+    try:
+        default = D.host_rates(-1)["cpu_threads"]
+        if "AMBRYCRC_CPU_THREADS" not in os.environ:
+            assert 1 <= default <= max(1, share // 2)
+        assert D.set_host_cpu_threads(-1, 1) == 0
+        one = D.host_calibrate(-1)
+        r1 = D.host_rates(-1)
+        assert r1["cpu_threads"] == 1 and r1["gpu_gibps"] == 0 and r1["auto_leg"] == "cpu" and one > 0
+        assert r1["cpu_gibps"] == one  # the calibration at this budget is what auto compares
+        mem = stream_bytes(5, 0, 4 << 20)
+        chunks = [(mem.ctypes.data + 997 * i, 30000 + i) for i in range(64)]
+        want = [zlib.crc32(mem[997 * i:997 * i + 30000 + i].tobytes()) for i in range(64)]
+        assert D.crc32_batch_host(chunks, device=-1) == want
+        if share >= 4:
+            assert D.set_host_cpu_threads(-1, 4) == 1
+            four = D.host_calibrate(-1)
+            assert four > one  # four threads hash DRAM faster than one
+            assert D.crc32_batch_host(chunks, device=-1) == want
+        with pytest.raises(Exception):
+            D.set_host_cpu_threads(-1, -2)
+        with pytest.raises(Exception):
+            D.set_host_cpu_threads(-1, 257)
+        with pytest.raises(Exception):
+            D.set_host_cpu_threads(63, 2)  # no context for device 63
+    finally:
+        D.set_host_cpu_threads(-1, prev)

@@ -157,6 +157,8 @@ def test_jni_shim_against_fake_jvm(core, tmp_path):
         "chain_null": (0, NPE), "chain_heap": (0, IAE), "chain_negative": (0, IOOBE), "chain_none": (0, "-"),
         "policy_no_context": (0xFFFFFFFF, ISE), "rates_null": (0xFFFFFFFF, NPE), "rates_short": (0xFFFFFFFF, IAE),
         "rates_no_context": (0xFFFFFFFF, ISE), "last_path_no_context": (0xFFFFFFFF, ISE),
+        "cpu_threads_set": (0, "-"), "cpu_threads_prev": (3, "-"), "cpu_threads_bad": (0xFFFFFFFF, IAE),
+        "cpu_threads_no_context": (0xFFFFFFFF, ISE),
     }
     for name, want in expect.items():
         assert got[name] == want, name
