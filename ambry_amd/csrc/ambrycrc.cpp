@@ -584,8 +584,9 @@ double host_cpu_gibps(int threads) {
 
 // The CPU leg's CRC rate on c: as its large calls measured it, else the calibration at c's budget.
 double host_batch_cpu_gibps(const DevCtx* c) {
-  const double r = c ? c->cpu_batch_gibps.load() : -1.0;
-  return r >= 0 ? r : host_cpu_gibps(host_cpu_threads(c));
+  const int t = host_cpu_threads(c);
+  const double r = c ? c->cpu_batch_gibps[std::min(t, DevCtx::kMaxCpuThreads)].load() : -1.0;
+  return r >= 0 ? r : host_cpu_gibps(t);
 }
 
 bool host_take_cpu(DevCtx* c, int device, int pinned, uint64_t bytes) {
@@ -601,8 +602,9 @@ bool host_take_cpu(DevCtx* c, int device, int pinned, uint64_t bytes) {
 void host_note_cpu(DevCtx* c, uint64_t bytes, double seconds) {
   if (!c || bytes < (64ull << 20) || seconds <= 0) return;
   const double r = (double)bytes / seconds / (double)(1ull << 30);
-  const double old = c->cpu_batch_gibps.load();
-  c->cpu_batch_gibps.store(old < 0 ? r : 0.5 * old + 0.5 * r);
+  std::atomic<double>& a = c->cpu_batch_gibps[std::min(host_cpu_threads(c), DevCtx::kMaxCpuThreads)];
+  const double old = a.load();
+  a.store(old < 0 ? r : 0.5 * old + 0.5 * r);
 }
 
 // The CPU leg of a message entry before it has been measured: verify parses and CRCs each
@@ -1970,10 +1972,8 @@ int ambrycrc_set_host_cpu_threads(int device, int threads) {
   DevCtx* c = ctx_for(device);
   if (!c) return AMBRYCRC_ENOINIT;
   const int prev = c->cpu_threads.exchange(threads);
-  if (prev != threads) {  // the CPU legs' measured rates were at the old budget
-    c->cpu_batch_gibps.store(-1.0);
+  if (prev != threads)  // the message legs' measured rates were at the old budget (the batch's are kept per budget)
     for (auto& r : c->msg_cpu_gibps) r.store(-1.0);
-  }
   return prev;
 }
 

@@ -123,10 +123,14 @@ struct DevCtx {
   // The CPU leg's thread budget on this device (ambrycrc_set_host_cpu_threads; 0: the process's,
   // host_cpu_threads). Auto compares the CPU leg's rate AT this budget with the GPU's.
   std::atomic<int> cpu_threads{0};
-  // ambrycrc_batch_host's CPU leg as its calls of >= 64 MiB measured it (EWMA; -1: not yet, the
-  // calibration at the budget stands for it); under auto every 16th such pageable call takes the other
-  // leg, so both rates stay current.
-  std::atomic<double> cpu_batch_gibps{-1.0};
+  // ambrycrc_batch_host's CPU leg as its calls of >= 64 MiB measured it, per thread budget (EWMA;
+  // -1: not yet, the calibration at that budget stands for it); under auto every 16th such pageable
+  // call takes the other leg, so both rates stay current.
+  static constexpr int kMaxCpuThreads = 256;
+  std::atomic<double> cpu_batch_gibps[kMaxCpuThreads + 1];
+  DevCtx() {
+    for (auto& r : cpu_batch_gibps) r.store(-1.0, std::memory_order_relaxed);
+  }
   std::atomic<uint32_t> batch_calls{0};
   // The message entries (kMsgVerify, kMsgTransform) compare their own legs' rates over region
   // bytes, GiB/s: a CPU leg parses and (transform) copies each message, so the CRC rate above does

@@ -280,6 +280,10 @@ def host_path_rate(torch, args):
             cpu_cost[name] = round(cpu_s / (reps * total / 2**30), 4)
         return total / best / 2**30
 
+    # the CPU leg's calibration at its default budget, at a quiet moment: after the CPU baseline's threads,
+    # a pause of a few cgroup quota periods (the box's CPU share is a CFS quota, which that leg exhausts)
+    time.sleep(0.3)
+    calib = D.host_calibrate(0)
     dev = torch.empty(total, dtype=torch.uint8, device="cuda")
     roof = best_of(lambda: dev.copy_(host, non_blocking=True))
     del dev
@@ -314,6 +318,7 @@ def host_path_rate(torch, args):
                          "auto_leg": auto_leg, "cpu_threads": rates["cpu_threads"],
                          "cpu_leg_pageable_2x_threads": round(res["cpu_leg_share"], 2),
                          "policy_cpu_estimate": round(rates["cpu_gibps"], 1),
+                         "cpu_calibration_at_budget": round(calib, 1),
                          "policy_gpu_estimate": round(rates["gpu_gibps"], 1),
                          "host_cpu_s_per_gib": cpu_cost},
             "sample": f"{nchunks} x 4 MiB host chunks (2 GiB), synchronous ambrycrc_batch_host (H2D + kernels + "

@@ -414,7 +414,8 @@ int ambrycrc_host_rates(int device, double* cpu_gibps, double* gpu_gibps, int* c
  * OMP_NUM_THREADS) -- the other half stays with the server's own network and disk threads, which the
  * reference runs on the same cores (NettyServerRequest.java:35,54, StoreMessageReadSet.java:170-188).
  * Returns the previous setting (0 = default), AMBRYCRC_EINVAL (threads outside 0..256) or
- * AMBRYCRC_ENOINIT. A change forgets the CPU legs' measured rates (they were at the old budget). */
+ * AMBRYCRC_ENOINIT. The CRC batch's measured CPU rates are kept per budget; a change forgets the message
+ * legs' (they were at the old budget). */
 int ambrycrc_set_host_cpu_threads(int device, int threads);
 /* Runs the CPU leg's calibration at `device`'s budget now (once per thread count per process; up to
  * 256 MiB written and hashed by the budget's threads, ~50-200 ms) instead of inside the first auto
