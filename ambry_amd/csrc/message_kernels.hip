@@ -668,13 +668,14 @@ __global__ __launch_bounds__(256) void region_long_kernel(MsgArgs a, RegionArgs 
     if (p >= np) continue;  // a record listed empty
     const uint64_t s = (uint64_t)p * kLongPiece, e = min((uint64_t)lr.len, s + kLongPiece);
     const uint32_t c = region::record_crc_runs_wave(region::TabC{tbl}, nib, dn, g.base, rk, lr.pa + s, e - s, lane);
-    uint32_t prev = 0;
-    if (lane == 0) {
-      g.lng.slot[q] = c;
-      __threadfence();  // the slot before the count
-      prev = atomicAdd(&lr.done, 1u);
-    }
-    prev = __builtin_amdgcn_readfirstlane(prev);
+    if (lane == 0) g.lng.slot[q] = c;
+    __threadfence();  // the slot before the count
+    // Every lane runs the count (lane 0 adds 1, the rest 0: one atomic after the compiler's merge) so
+    // the readfirstlane below follows no lane-0-only branch. A lane-0 atomic read back by readfirstlane
+    // inside a loop is what hung round 5's claim loop: the compiler let lanes 1..63 re-enter the loop
+    // without lane 0 and readfirstlane then read their own zero (DESIGN.md §11.3,
+    // profiles/r06_hang_isa.txt; tests/test_kernel_lint.py forbids the pattern).
+    const uint32_t prev = __builtin_amdgcn_readfirstlane(atomicAdd(&lr.done, lane == 0 ? 1u : 0u));
     if (prev + 1 != np) continue;
     __threadfence();  // every other piece's slot after its count
     const uint64_t last = (uint64_t)lr.len - (uint64_t)(np - 1) * kLongPiece;  // 1 .. kLongPiece

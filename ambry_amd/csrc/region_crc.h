@@ -492,8 +492,9 @@ __device__ __forceinline__ uint32_t record_crc(const uint32_t* __restrict__ t, c
   return record_crc(TabC{t}, nib, base, rk, pa, len);
 }
 
-// Appends a long record to the grid-wide list (region_long_kernel, message_kernels.hip); false when
-// the list is full (the caller then takes the record itself).
+// Appends a long record to the grid-wide list (region_long_kernel, message_kernels.hip) for one
+// thread's message (region_msg_kernel: a thread per message, its own atomic result, no broadcast);
+// false when the list is full (the caller then takes the record itself).
 __device__ __forceinline__ bool list_long(const LongList& l, uint64_t pa, uint64_t len, uint32_t ex, uint64_t msg,
                                           uint32_t bit) {
   const uint32_t pieces = (uint32_t)((len + kLongPiece - 1) / kLongPiece);
@@ -511,6 +512,35 @@ __device__ __forceinline__ bool list_long(const LongList& l, uint64_t pa, uint64
   lr.piece0 = (uint32_t)was;
   lr.pieces = room ? pieces : 0;  // no slots left: listed empty, taken by the caller
   lr.done = 0;
+  return room;
+}
+
+// The same for a whole wave with wave-uniform arguments (the region processors): every lane runs the
+// atomic (lane 0 adds, the rest add 0) and lane 0's result is broadcast, so the return value is
+// wave-uniform without a lane-0-only branch before a readfirstlane. Lane 0 writes
+// the record.
+__device__ __forceinline__ bool list_long_wave(const LongList& l, uint64_t pa, uint64_t len, uint32_t ex,
+                                               uint64_t msg, uint32_t bit, uint32_t lane) {
+  const uint32_t pieces = (uint32_t)((len + kLongPiece - 1) / kLongPiece);
+  if (pieces > kLongMaxPieces) return false;
+  const unsigned long long inc = lane == 0 ? ((1ull << 32) | pieces) : 0ull;
+  const unsigned long long raw = atomicAdd(l.ctr, inc);
+  const unsigned long long was = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(raw >> 32)) << 32) |
+                                 __builtin_amdgcn_readfirstlane((uint32_t)raw);
+  const uint32_t at = (uint32_t)(was >> 32);
+  if (at >= l.cap) return false;
+  const bool room = (uint64_t)(uint32_t)was + pieces <= l.pcap;
+  if (lane == 0) {
+    LongRec& lr = l.rec[at];
+    lr.pa = pa;
+    lr.msg = msg;
+    lr.len = (uint32_t)len;
+    lr.ex = ex;
+    lr.bit = bit;
+    lr.piece0 = (uint32_t)was;
+    lr.pieces = room ? pieces : 0;  // no slots left: listed empty, taken by the caller
+    lr.done = 0;
+  }
   return room;
 }
 

@@ -176,9 +176,7 @@ __device__ __forceinline__ void process_message_direct(const MsgArgs& a, const R
     const uint64_t pa = g.reg0 + jo;
     const int64_t runs = (int64_t)((((pa + jl + 63) & ~uint64_t(63)) - (pa & ~uint64_t(63))) >> 6);
     if (runs > kLongRuns && lng && lng->ctr) {  // a multi-MiB record: the whole grid's, after this kernel
-      bool ok = false;
-      if (lane == 0) ok = list_long(*lng, pa, jl, ex, i, record_bit(k));
-      if (__builtin_amdgcn_readfirstlane((uint32_t)ok)) continue;
+      if (list_long_wave(*lng, pa, jl, ex, i, record_bit(k), lane)) continue;
     }
     const uint32_t c = runs > kLongRuns ? record_crc_runs_wave(tc, nib, dn, g.base, rk, pa, jl, lane)
                                         : record_crc_direct(tc, nib, dn, g, pa, jl, lane);
