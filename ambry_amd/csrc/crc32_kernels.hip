@@ -1792,13 +1792,18 @@ __global__ __launch_bounds__(64 * W) void region_fused_kernel(FusedArgs f) {
         if (COPY && (j & 7) == 7 && __hip_atomic_load(f.xfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
         const uint32_t r0 = hash(4 * g, 0, b0);
         if (j >= 2) {
-          // Group j's first loads have landed (r0 used them), and vector memory operations retire in
-          // issue order, so the sum store of group j - 2 (issued before them) is in L2: groups
-          // 0 .. j - 2 of this wave are complete. z = 0, computed from r0, so the LDS store below
-          // cannot move above that wait; no s_waitcnt vmcnt(0), which would also drain the loads
-          // in flight.
+          // Publication of groups 0 .. j - 2 (their run-sum stores were issued before group j's
+          // loads): a workgroup-scope release fence, then the relaxed LDS store of done[v], paired
+          // with the acquire fence after the processors' poll (wait_for) -- release/acquire in the
+          // HIP memory model, the readers being waves of this workgroup. For gfx950 without
+          // threadgroup split the compiler implements it with s_waitcnt lgkmcnt(0) alone: a CU's
+          // vector memory operations go through its L1 in order, so a processor's later load of a
+          // published sum sees the store (ISA diff against the unfenced form: one s_nop became that
+          // wait). No s_waitcnt vmcnt(0), which would also drain the loads in flight.
+          // z = 0, computed from r0, keeps the store after group j's loads have landed.
           uint32_t z;
           asm volatile("v_mov_b32 %0, 0" : "=v"(z) : "v"(r0));
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
           __hip_atomic_store(&done[v], (uint32_t)j - 1u + __builtin_amdgcn_readfirstlane(z), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_WORKGROUP);
         }
@@ -1865,7 +1870,7 @@ __global__ __launch_bounds__(64 * W) void region_fused_kernel(FusedArgs f) {
   auto wait_for = [&](uint64_t target) {
     if (target > s_hi) target = s_hi;
     while (frontier() < target) __builtin_amdgcn_s_sleep(8);
-    asm volatile("" ::: "memory");  // no run-sum load above the poll
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   };
   for (uint64_t b = M0 + 64 * (uint64_t)p; b < M1; b += 64 * (uint64_t)f.nproc) {
     if (COPY && __hip_atomic_load(f.xfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;  // as the streamers
