@@ -88,12 +88,10 @@
 #ifndef AMBRY_RUNS_PROBE  // 1 = no run sums into LDS, 5 = no global stores, 6 = stores to one line set
 #define AMBRY_RUNS_PROBE 0
 #endif
-#ifndef AMBRY_FUSED_PROBE  // one-pass kernel: 1 = processors do nothing (the streaming alone), 2 = timestamps,
-                           // 3-5 = the streaming alone without sum stores / stores CU-interleaved / groups interleaved
-#define AMBRY_FUSED_PROBE 0
-#endif
+// (The one-pass kernel's timing probes, round 5's AMBRY_FUSED_PROBE 1-5, live in
+// tools/probes/fused_probe_branches.patch: `git apply` it to a scratch tree to rebuild them.)
 
-#if (AMBRY_REGION_PROBE != 0 || AMBRY_RUNS_PROBE != 0 || AMBRY_FUSED_PROBE != 0 || defined(AMBRYCRC_DIAGNOSTICS) || \
+#if (AMBRY_REGION_PROBE != 0 || AMBRY_RUNS_PROBE != 0 || defined(AMBRYCRC_DIAGNOSTICS) || \
      defined(AMBRY_AB_SPLIT_GROUP) || defined(AMBRY_AB_PUT_ASSEMBLE)) && !defined(AMBRY_AB_PROBE_BUILD)
 #error "probe / diagnostic knobs build a library that returns wrong CRCs or runs unshipped kernels: define AMBRY_AB_PROBE_BUILD (tools/ab_build.sh does)"
 #endif
@@ -107,7 +105,7 @@
   X(AMBRY_FUSED_WAVES_COPY, 8) X(AMBRY_FUSED_NT, 1) X(AMBRY_FUSED_ENDS, 1)                                                                 \
   X(AMBRY_GRP_PRIO, 0) X(AMBRY_GRP_IL, 4) X(AMBRY_C0_G, 2) X(AMBRY_C0_NB, 8) X(AMBRY_C1_MAX, 1024)           \
   X(AMBRY_RUNS_STORE_NT, 0) X(AMBRY_RUNS_NT, 1) X(AMBRY_RUNS_GIL, 1) X(AMBRY_PLAN_PER_BLOCK, 2048) X(AMBRY_DEFAULT_VARIANT, 29) \
-  X(AMBRY_REGION_PROBE, 0) X(AMBRY_RUNS_PROBE, 0) X(AMBRY_FUSED_PROBE, 0)
+  X(AMBRY_REGION_PROBE, 0) X(AMBRY_RUNS_PROBE, 0)
 
 #if defined(AMBRY_AB_PROBE_BUILD)
 #define AMBRY_IS_PROBE_BUILD 1

@@ -1695,17 +1695,8 @@ __device__ __forceinline__ uint64_t lower_bound_wave(const FusedArgs& f, uint64_
   return lo + (uint64_t)__popcll(ball);
 }
 
-#if AMBRY_FUSED_PROBE == 2
-// A/B probe: per workgroup, s_memrealtime (100 MHz) at entry, when its last streamer finished and
-// when its last processor finished (ambrycrc_debug_fused_times).
-__device__ unsigned long long g_fused_t[3 * 2048];
-#endif
-
 template <bool COPY, int W>
 __global__ __launch_bounds__(64 * W) void region_fused_kernel(FusedArgs f) {
-#if AMBRY_FUSED_PROBE == 2
-  if (threadIdx.x == 0) g_fused_t[3 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
-#endif
   __shared__ uint32_t tbl[1024];
   __shared__ uint32_t nib[region::kNibTotal];
   __shared__ uint32_t dn[region::kDirSets * region::kNibWords];
@@ -1768,16 +1759,7 @@ __global__ __launch_bounds__(64 * W) void region_fused_kernel(FusedArgs f) {
       buf[64u * u + slot] = r;
       return r;
     };
-    // A/B probe 5 (timing only, wrong sums): streamer v of workgroup b takes the region's groups
-    // (j*S + v)*grid + b -- every CU's reads and stores inside one window, as region_runs_kernel's
-    uint64_t gfirst = G0 + v, gstep = nstream;
-    uint64_t mine_n = mine;
-    if constexpr (AMBRY_FUSED_PROBE == 5) {
-      const uint64_t L = f.ngroups > blockIdx.x ? (f.ngroups - blockIdx.x + gridDim.x - 1) / gridDim.x : 0;
-      gfirst = (uint64_t)v * gridDim.x + blockIdx.x;
-      gstep = (uint64_t)nstream * gridDim.x;
-      mine_n = L > v ? (L - v + nstream - 1) / nstream : 0;
-    }
+    const uint64_t gfirst = G0 + v, gstep = nstream, mine_n = mine;
     if (mine_n) {
       u32x4 b0[4], b1[4], b2[4], b3[4];
       uint64_t g = gfirst;
@@ -1823,25 +1805,14 @@ __global__ __launch_bounds__(64 * W) void region_fused_kernel(FusedArgs f) {
         region_sb_load<AMBRY_FUSED_NT != 0>(a, 4 * nx + 3, lane, b3);
         __builtin_amdgcn_s_setprio(0);
         const u32x4 sums = *reinterpret_cast<const u32x4*>(buf + 4u * lane);
-        if constexpr (AMBRY_FUSED_PROBE == 3) {  // A/B probe 3: no sum stores (timing only)
-          if (sums.x == 0x9E3779B9u) *(reinterpret_cast<u32x4*>(a.rk + kRunPad + g * 256) + lane) = sums;
-        } else if constexpr (AMBRY_FUSED_PROBE == 4) {  // A/B probe 4: sums stored CU-interleaved (timing only)
-          const uint64_t gi = (g - G0) * gridDim.x + blockIdx.x;
-          *(reinterpret_cast<u32x4*>(a.rk + kRunPad + (gi < f.ngroups ? gi : g) * 256) + lane) = sums;
-        } else {
-          *(reinterpret_cast<u32x4*>(a.rk + kRunPad + g * 256) + lane) = sums;
-        }
+        *(reinterpret_cast<u32x4*>(a.rk + kRunPad + g * 256) + lane) = sums;
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __hip_atomic_store(&done[v], (uint32_t)mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#if AMBRY_FUSED_PROBE == 2
-    if (lane == 0) atomicMax(&g_fused_t[3 * blockIdx.x + 1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
-#endif
     return;
   }
   // ---- processor wave
-  if (AMBRY_FUSED_PROBE == 1 || AMBRY_FUSED_PROBE >= 3) return;  // A/B probes: the streaming alone (wrong statuses)
   const uint32_t p = v - nstream;
   const uint64_t s_lo = G0 * kGroupBytes, s_hi = G1 * kGroupBytes;  // the share, base-relative
   {  // this wave's slice of the global sortedness check
@@ -1900,9 +1871,6 @@ __global__ __launch_bounds__(64 * W) void region_fused_kernel(FusedArgs f) {
     }, [&](uint64_t need) { wait_for(need); }, dn, COPY ? s_hi : ~0ull);
     if constexpr (COPY) region::transform_fast_post(f, st != ~0u, i, st, mend, pre);  // `out` untouched
   }
-#if AMBRY_FUSED_PROBE == 2
-  if (lane == 0) atomicMax(&g_fused_t[3 * blockIdx.x + 2], (unsigned long long)__builtin_amdgcn_s_memrealtime());
-#endif
 }
 
 // The deferred messages (or, with ctl[0] set, every message) once all run sums exist: one lane
@@ -1977,12 +1945,6 @@ __global__ __launch_bounds__(256) void region_patch_kernel(FusedArgs f) {
   }
 }
 
-#if AMBRY_FUSED_PROBE == 2
-extern "C" int ambrycrc_debug_fused_times(unsigned long long* out, int n) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fused_t), sizeof(unsigned long long) * 3 * n) != hipSuccess) return -2;
-  return 0;
-}
-#endif
 
 hipError_t launch_region_fused(const FusedArgs& f, int num_cu, hipStream_t s) {
 

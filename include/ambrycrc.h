@@ -530,6 +530,16 @@ int ambrycrc_put_crcs(const uint8_t* const* fields, const uint64_t* field_len, c
 int ambrycrc_range_checksums_host(const uint8_t* file, uint64_t file_len, const int64_t* first, const int64_t* second,
                                   size_t n, uint32_t* out, int device);
 
+/* =====================================================================================
+ * DIAGNOSTICS -- for benchmarks, profiles and tests, not for production callers. Nothing in
+ * the reference corresponds to these entries. Every production path above is correct and
+ * tuned with their defaults; they select kernel shapes for A/B runs (set_variant, set_grid,
+ * set_window, set_region_mode, set_transform_verdict), time kernels (timing_*), report which
+ * form a call took (last_message_mode, last_transform_path), fill synthetic data
+ * (fill_random_dev), probe bandwidth (debug_readbw_dev) and expose the table image to the CPU
+ * kernel model (debug_table_image). The JNI shim binds none of them.
+ * ===================================================================================== */
+
 /* ------------------------------------------------------- tuning / telemetry */
 
 /* Kernel variant (0..29; crc32_kernels.h lists them). 0..13: sweep-kernel shapes (blocks in
@@ -594,7 +604,7 @@ int ambrycrc_timing_collect_each(int device, float* ms_out, int cap, int* launch
 /* Number of workgroups the sweep kernel launches with on `device` (0 if unknown). */
 int ambrycrc_grid_size(int device);
 
-/* ------------------------------------------------------- synthetic data */
+/* ------------------------------------------------------- synthetic data and probes (diagnostics) */
 
 /* Fill d_dst with the deterministic splitmix64 byte stream (byte i = byte i&7 of
  * splitmix64_mix(seed + ((stream_off+i)/8 + 1) * 0x9E3779B97F4A7C15)).
