@@ -274,7 +274,9 @@ def main():
     torch.cuda.set_device(0)
     D.init(0)
     cases = {"64k": (65536, 64 << 10), "32k": (32768, 32 << 10), "16k": (65536, 16 << 10), "8k": (131072, 8 << 10),
-             "4k": (262144, 4 << 10), "4m": (4096, 4 << 20)}
+             "4k": (262144, 4 << 10), "4m": (4096, 4 << 20),
+             # the 4 KiB case at 4x and 16x the region (5.6 / 22 GB): where the copy plateaus
+             "4kx4": (1048576, 4 << 10), "4kx16": (4194304, 4 << 10)}
     for c in [x for x in args.cases.split(",") if x]:
         m, s = cases[c]
         for in_place in (False, True):

@@ -1,7 +1,9 @@
-// copy_roof.hip -- probe: device-to-device copy bandwidth on this GPU for the transform's size
-// (1.39 GB region -> separate output): hipMemcpyAsync, and a grid-stride 16-B-per-lane kernel with
-// plain / nontemporal loads and stores at a few unroll depths. Prints JSON lines (GB/s of read +
-// write). Build: hipcc -O3 --offload-arch=gfx950 -o copy_roof tools/probes/copy_roof.hip
+// copy_roof.hip -- probe: device-to-device copy bandwidth on this GPU at a given size (argv[1] bytes;
+// default the transform's 1.39 GB region -> separate output): hipMemcpyAsync, a grid-stride
+// 16-B-per-lane kernel with plain / nontemporal loads and stores at a few unroll depths, and a
+// contiguous-share form (each wave copies its own contiguous 1/waves of the buffer, 4 KiB per
+// step). Prints JSON lines (GB/s of read + write).
+// Build: hipcc -O3 --offload-arch=gfx950 -o copy_roof tools/probes/copy_roof.hip
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -25,6 +27,24 @@ __global__ __launch_bounds__(256) void copy_k(const u32x4* __restrict__ src, u32
   for (; i < n; i += stride) dst[i] = src[i];
 }
 
+// each wave copies [w*per, (w+1)*per) 16 B per lane, U wave-loads in flight
+template <int U>
+__global__ __launch_bounds__(256) void copy_share(const u32x4* __restrict__ src, u32x4* __restrict__ dst, size_t n) {
+  const size_t waves = (size_t)gridDim.x * (blockDim.x / 64);
+  const size_t w = (size_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+  const size_t lane = threadIdx.x & 63;
+  const size_t lo = n * w / waves, hi = n * (w + 1) / waves;
+  size_t i = lo + lane;
+  for (; i + 64 * (U - 1) < hi; i += 64 * U) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(src + i + 64 * u);
+#pragma unroll
+    for (int u = 0; u < U; ++u) __builtin_nontemporal_store(v[u], dst + i + 64 * u);
+  }
+  for (; i < hi; i += 64) dst[i] = src[i];
+}
+
 #define CK(e) do { hipError_t r_ = (e); if (r_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(r_), __LINE__); exit(1); } } while (0)
 
 template <int U, bool NTL, bool NTS>
@@ -45,8 +65,26 @@ static void run(const char* name, const u32x4* s, u32x4* d, size_t n, int grid, 
          sum / reps, bytes / (sum / reps) / 1e6, bytes / best / 1e6);
 }
 
-int main() {
-  const size_t bytes = 1389101056;  // 262,144 x 4 KiB PUT messages (bench_put.py's transform case)
+template <int U>
+void run_share(const char* name, const u32x4* s, u32x4* d, size_t n, int grid, hipStream_t st, hipEvent_t e0,
+               hipEvent_t e1) {
+  float sum = 0, best = 1e30f;
+  for (int r = 0; r < 12; ++r) {
+    CK(hipEventRecord(e0, st));
+    hipLaunchKernelGGL(copy_share<U>, dim3(grid), dim3(256), 0, st, s, d, n);
+    CK(hipEventRecord(e1, st));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    if (r >= 2) sum += ms, best = ms < best ? ms : best;
+  }
+  printf("{\"copy\": \"%s\", \"bytes\": %zu, \"grid\": %d, \"ms_avg\": %.4f, \"GBps_avg\": %.1f, \"GBps_best\": %.1f}\n",
+         name, n * 16, grid, sum / 10, 2.0 * n * 16 / (sum / 10) / 1e6, 2.0 * n * 16 / best / 1e6);
+}
+
+int main(int argc, char** argv) {
+  // default: 262,144 x 4 KiB PUT messages (bench_put.py's transform case)
+  const size_t bytes = argc > 1 ? (size_t)strtoull(argv[1], nullptr, 10) & ~(size_t)4095 : 1389101056;
   const size_t n = bytes / 16;
   u32x4 *s, *d;
   CK(hipMalloc(&s, bytes)); CK(hipMalloc(&d, bytes));
@@ -63,7 +101,8 @@ int main() {
       float ms; CK(hipEventElapsedTime(&ms, e0, e1));
       if (r >= 2) sum += ms;
     }
-    printf("{\"copy\": \"hipMemcpyAsync\", \"ms_avg\": %.4f, \"GBps_avg\": %.1f}\n", sum / 10, 2.0 * bytes / (sum / 10) / 1e6);
+    printf("{\"copy\": \"hipMemcpyAsync\", \"bytes\": %zu, \"ms_avg\": %.4f, \"GBps_avg\": %.1f}\n", bytes, sum / 10,
+           2.0 * bytes / (sum / 10) / 1e6);
   }
   int cu = 256;
   for (int g : {cu * 4, cu * 8, cu * 16}) {
@@ -71,6 +110,10 @@ int main() {
     run<4, true, true>("nt_u4", s, d, n, g, st, e0, e1);
     run<4, true, false>("ntload_u4", s, d, n, g, st, e0, e1);
     run<8, true, true>("nt_u8", s, d, n, g, st, e0, e1);
+  }
+  for (int g : {cu * 2, cu * 4, cu * 8}) {
+    run_share<4>("share_nt_u4", s, d, n, g, st, e0, e1);
+    run_share<8>("share_nt_u8", s, d, n, g, st, e0, e1);
   }
   return 0;
 }
