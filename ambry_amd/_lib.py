@@ -141,6 +141,7 @@ _SIGNATURES = [
     ("ambrycrc_last_message_mode", ctypes.c_int, [ctypes.c_int]),
     ("ambrycrc_last_transform_path", ctypes.c_int, [ctypes.c_int]),
     ("ambrycrc_set_transform_verdict", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    ("ambrycrc_set_put_stream_max", ctypes.c_long, [ctypes.c_int, ctypes.c_long]),
     ("ambrycrc_set_host_policy", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     ("ambrycrc_host_rates", ctypes.c_int,
      [ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),

@@ -853,13 +853,11 @@ int ambrycrc_init(int device) {
     if (end != v && *end == '\0' && x >= 0 && x < 1000 && variant_supported((int)x)) c->variant = (int)x;
   }
   if (const char* v = getenv("AMBRYCRC_REGION")) c->region_mode = strcmp(v, "0") == 0 ? 0 : strcmp(v, "1") == 0 ? 1 : 2;
-#ifdef AMBRY_AB_PUT_ASSEMBLE
-  if (const char* v = getenv("AMBRYCRC_ASM_MAX")) {  // A/B: whole-message assembly cut-off
+  if (const char* v = getenv("AMBRYCRC_STREAM_PUT_MAX")) {  // A/B: serialize copy mode's streamed form (0: off)
     char* end = nullptr;
     const unsigned long x = strtoul(v, &end, 10);
-    if (end != v && *end == '\0' && x <= kAsmMaxBytes) c->asm_max = (uint32_t)x;
+    if (end != v && *end == '\0') c->stream_put_max = x < kStreamPutMax ? x : kStreamPutMax;
   }
-#endif
   if (const char* v = getenv("AMBRYCRC_XFORM_FAST_MAX")) {  // A/B: the transform fast path's cut-off
     char* end = nullptr;
     const unsigned long long x = strtoull(v, &end, 10);
@@ -1143,6 +1141,15 @@ int ambrycrc_set_variant(int device, int variant) {
   if (!variant_supported(variant)) return AMBRYCRC_EINVAL;
   c->variant = variant;
   return AMBRYCRC_OK;
+}
+
+long ambrycrc_set_put_stream_max(int device, long bytes) {
+  DevCtx* c = ctx_for(device);
+  if (!c) return AMBRYCRC_ENOINIT;
+  if (bytes < 0 || (uint64_t)bytes > kStreamPutMax) return AMBRYCRC_EINVAL;
+  const long prev = (long)c->stream_put_max;
+  c->stream_put_max = (uint64_t)bytes;
+  return prev;
 }
 
 int ambrycrc_set_region_mode(int device, int enable) {

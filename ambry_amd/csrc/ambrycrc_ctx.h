@@ -83,11 +83,9 @@ struct DevCtx {
   // mode is on and the region holds at most xform_fast_max bytes per message.
   int region_mode = 2;
   uint64_t xform_fast_max = kXformFastMaxPerMessage;
-#ifdef AMBRY_AB_PUT_ASSEMBLE
-  // A/B builds only (tools/probes/put_assemble.hip): serialize copy mode assembles messages of at
-  // most this many bytes whole; AMBRYCRC_ASM_MAX (0 = never, at most kAsmMaxBytes). DESIGN.md §10.4.
-  uint32_t asm_max = 0;
-#endif
+  // Serialize copy mode streams messages of at most this many bytes (put_stream_kernel, DESIGN.md
+  // §12.6); AMBRYCRC_STREAM_PUT_MAX at init: 0 = every message through the job path (A/B).
+  uint64_t stream_put_max = kStreamPutMax;
   // The form the last message verify on this device took (ambrycrc_last_message_mode).
   std::atomic<int> last_msg_mode{-1};
   // The path the last transform took (ambrycrc_last_transform_path): 1 fast, 0 general, 2 decided
@@ -252,7 +250,7 @@ int enqueue_messages_check(DevCtx* c, const MsgStage& st, hipStream_t stream, ui
 int enqueue_serialize(DevCtx* c, const ::ambrycrc_put_desc* d_desc, size_t m, const uint8_t* d_fields,
                       const uint8_t* d_blobs, uint8_t* d_out, uint64_t* d_msg_len, void* d_ws, hipStream_t stream,
                       const uint32_t* d_in_crc = nullptr, bool layout_only = false, const uint32_t* gate = nullptr,
-                      const PropsFix* pfix = nullptr);
+                      const PropsFix* pfix = nullptr, bool stream_ok = false);
 
 // Bytes from a message's start that its verify may read (the header window, or the whole message
 // when the header's sizes fit `rem`).

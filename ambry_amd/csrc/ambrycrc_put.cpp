@@ -25,6 +25,11 @@ size_t put_jobs_bytes(size_t m) {
   return (j * (4 * sizeof(uint64_t) + 2 * sizeof(uint64_t) + 2 * sizeof(uint32_t)) + 255) & ~size_t(255);
 }
 
+// The job path's workspace (copy and CRC jobs, the batch workspace, the streamed form's `big` word);
+// ambrycrc_serialize_puts_workspace_bytes adds the streamed form's run slots after it (the transform,
+// which never streams, uses this much).
+size_t put_core_bytes(size_t m) { return put_jobs_bytes(m) + ws_need((size_t)kPutSlots * m) + 256; }
+
 // A transform's own workspace: descriptors, the scan's per-message output, in_crc (4 per message),
 // the speculative pass's xstatus, its fail flag, the verify jobs' copy destinations (5 per message)
 // and the properties re-encodings (one PropsFix per message).
@@ -43,7 +48,8 @@ namespace detail {
 
 int enqueue_serialize(DevCtx* c, const ::ambrycrc_put_desc* d_desc, size_t m, const uint8_t* d_fields,
                       const uint8_t* d_blobs, uint8_t* d_out, uint64_t* d_msg_len, void* d_ws, hipStream_t stream,
-                      const uint32_t* d_in_crc, bool layout_only, const uint32_t* gate, const PropsFix* pfix) {
+                      const uint32_t* d_in_crc, bool layout_only, const uint32_t* gate, const PropsFix* pfix,
+                      bool stream_ok) {
   const size_t j = (size_t)kPutSlots * m;
   uint8_t* w = static_cast<uint8_t*>(d_ws);
   PutArgs a;
@@ -76,19 +82,32 @@ int enqueue_serialize(DevCtx* c, const ::ambrycrc_put_desc* d_desc, size_t m, co
   }
   a.pfix = pfix;
   void* batch_ws = w + put_jobs_bytes(m);
-#ifdef AMBRY_AB_PUT_ASSEMBLE
-  if (a.copy_through && d_fields && d_blobs && c->asm_max && !gate) {
-    // whole-message assembly for messages of at most asm_max bytes; the job path below runs (on
-    // the device) only if a longer one set *big, and skips the assembled ones
-    a.asm_max = c->asm_max;
+  // Copy mode with both sources (round 6): messages of at most stream_put_max bytes are
+  // streamed -- put_stream_kernel writes each whole and keeps its output runs' CRCs, put_stream_seal_kernel
+  // writes its trailers -- and the layout kernel gives them no jobs; a longer one sets `big`, which gates
+  // the job path below (CRC batch and seal) on the device.
+  const bool streamed = stream_ok && a.copy_through && d_fields && d_blobs && !gate && !pfix && c->stream_put_max;
+  StreamPutArgs sa;
+  if (streamed) {
+    a.stream_max = (uint32_t)c->stream_put_max;
     a.big = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(batch_ws) + ws_need(j));
     if (hipMemsetAsync(a.big, 0, sizeof(uint32_t), stream) != hipSuccess) return AMBRYCRC_EHIP;
-    if (launch_put_assemble(a, c->num_cu, stream) != hipSuccess) return AMBRYCRC_EHIP;
-    a.gate = a.big;
+    sa.desc = d_desc;
+    sa.m = m;
+    sa.obase = d_out - (reinterpret_cast<uintptr_t>(d_out) & 63u);
+    sa.oreg0 = reinterpret_cast<uintptr_t>(d_out) & 63u;
+    sa.fields = d_fields;
+    sa.blobs = d_blobs;
+    sa.rk = reinterpret_cast<uint32_t*>(w + put_core_bytes(m));
+    sa.img = c->d_img;
   }
-#endif
   if (launch_put_layout(a, stream) != hipSuccess) return AMBRYCRC_EHIP;
   if (layout_only) return AMBRYCRC_OK;
+  if (streamed) {
+    if (launch_put_stream(sa, c->num_cu, stream) != hipSuccess || launch_put_stream_seal(sa, c->num_cu, stream) != hipSuccess)
+      return AMBRYCRC_EHIP;
+    a.gate = a.big;  // the job path: only when a message was too long to stream
+  }
   if (a.copy_through) {
     // one pass over the fields: the copy-through sweep reads each from its source, writes it into
     // the message and CRCs it (job k*m+i = slot k of message i, as the CRC jobs)
@@ -173,9 +192,7 @@ int ambrycrc_serialize_put_host(const ambrycrc_put_desc* d, const uint8_t* field
   return AMBRYCRC_OK;
 }
 
-size_t ambrycrc_serialize_puts_workspace_bytes(size_t m) {
-  return put_jobs_bytes(m) + ws_need((size_t)kPutSlots * m) + 256;  // + the A/B assembly's `big` word
-}
+size_t ambrycrc_serialize_puts_workspace_bytes(size_t m) { return put_core_bytes(m) + stream_put_rk_bytes(m); }
 
 int ambrycrc_serialize_puts_dev(const ambrycrc_put_desc* d_desc, size_t m, const uint8_t* d_fields,
                                 const uint8_t* d_blobs, uint8_t* d_out, uint64_t* d_msg_len, void* d_ws,
@@ -187,12 +204,12 @@ int ambrycrc_serialize_puts_dev(const ambrycrc_put_desc* d_desc, size_t m, const
   WsLease lease;
   const int rc = lease.acquire(c, stream, &d_ws, ws_bytes, ambrycrc_serialize_puts_workspace_bytes(m));
   if (rc) return rc;
-  return enqueue_serialize(c, d_desc, m, d_fields, d_blobs, d_out, d_msg_len, d_ws, stream);
+  return enqueue_serialize(c, d_desc, m, d_fields, d_blobs, d_out, d_msg_len, d_ws, stream, nullptr, false, nullptr,
+                           nullptr, true);
 }
 
 size_t ambrycrc_transform_workspace_bytes(size_t m) {
-  return transform_own_bytes(m) + ws_need(m) +
-         std::max(ambrycrc_messages_workspace_bytes(m), ambrycrc_serialize_puts_workspace_bytes(m));
+  return transform_own_bytes(m) + ws_need(m) + std::max(ambrycrc_messages_workspace_bytes(m), put_core_bytes(m));
 }
 
 namespace {

@@ -92,7 +92,7 @@
 // tools/probes/fused_probe_branches.patch: `git apply` it to a scratch tree to rebuild them.)
 
 #if (AMBRY_REGION_PROBE != 0 || AMBRY_RUNS_PROBE != 0 || defined(AMBRYCRC_DIAGNOSTICS) || \
-     defined(AMBRY_AB_SPLIT_GROUP) || defined(AMBRY_AB_PUT_ASSEMBLE)) && !defined(AMBRY_AB_PROBE_BUILD)
+     defined(AMBRY_AB_SPLIT_GROUP)) && !defined(AMBRY_AB_PROBE_BUILD)
 #error "probe / diagnostic knobs build a library that returns wrong CRCs or runs unshipped kernels: define AMBRY_AB_PROBE_BUILD (tools/ab_build.sh does)"
 #endif
 

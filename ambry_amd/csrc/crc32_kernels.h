@@ -259,16 +259,13 @@ struct PutArgs {
   // is the record CRC; the layout kernel writes the header trailer itself. A slot with no source
   // buffer (fields or blobs null) re-reads its bytes in place (src = dst).
   bool copy_through;
-  // A/B builds only -- whole-message assembly (tools/probes/put_assemble.hip, copy mode with both field buffers): messages of
-  // at most asm_max bytes are written by it, and put_layout_kernel gives them no jobs; a longer one
-  // sets *big, which gates the job path (layout, plan + sweep, seal). 0: no assembly.
-  uint32_t asm_max = 0;
+  // Copy mode with both source buffers (round 6): messages of at most stream_max bytes are written by
+  // put_stream_kernel / put_stream_seal_kernel, and put_layout_kernel gives them no jobs (it writes
+  // their header and record prefixes); a longer one sets *big, which gates the job path (plan + sweep,
+  // seal). 0: every message through the job path.
+  uint32_t stream_max = 0;
   uint32_t* big = nullptr;
 };
-
-// A/B builds: messages of at most this many bytes are assembled whole by put_assemble_kernel (a wave
-// per message through a 7 KiB LDS image per wave: 4 waves and 37.5 KiB of LDS per block, 4 blocks per CU).
-constexpr uint32_t kAsmMaxBytes = 6144;
 
 // Each copy job costs its bytes plus kCopyJobCost: a wave pays about one memory round trip
 // (~2 us, ~1.6 KB of its share of HBM bandwidth) per job whatever its size, so balancing bytes
@@ -332,11 +329,33 @@ hipError_t launch_transform_finish(const TransformArgs& a, hipStream_t s);
 hipError_t launch_transform_merge(const TransformArgs& a, hipStream_t s);
 hipError_t launch_props_fix(const TransformArgs& a, hipStream_t s);
 
+// ---- copy-mode serialization of small messages by streaming the output (round 6)
+// put_stream_kernel: a wave per message writes the whole message -- header and record heads computed,
+// fields and blob gathered from their sources, trailers zero -- in 16-B output pieces (four 1 KiB wave
+// loads per 4 KiB super-block of output, stores whole pieces, the two it shares with its neighbours byte
+// by byte) and keeps the raw CRC of every 64-B output run (quad transpose + run_crc, as
+// region_runs_kernel does) in the message's run slots. put_stream_seal_kernel: a thread per message
+// assembles the header and record CRCs from those runs (region::record_crc; the partial runs at record
+// ends re-read from the output) and writes the trailers. Messages longer than kStreamPutMax take the
+// job path (put_layout_kernel sets *big, which gates it).
+constexpr uint64_t kStreamPutMax = 6144;
+constexpr uint64_t kStreamPutRuns = 100;  // run slots per message: ceil((63 + 6144) / 64) = 97, to a multiple of 4
+struct StreamPutArgs {
+  const ::ambrycrc_put_desc* desc;  // [m]
+  uint64_t m;
+  uint8_t* obase;         // the output pointer rounded down to 64 B
+  uint64_t oreg0;         // output pointer - obase
+  const uint8_t* fields;
+  const uint8_t* blobs;
+  uint32_t* rk;           // [kRunPad + m * kStreamPutRuns]: message i's run r at rk[kRunPad + i * kStreamPutRuns + r]
+  const uint32_t* img;
+};
+size_t stream_put_rk_bytes(size_t m);
+hipError_t launch_put_stream(const StreamPutArgs& a, int num_cu, hipStream_t s);
+hipError_t launch_put_stream_seal(const StreamPutArgs& a, int num_cu, hipStream_t s);
+
 hipError_t launch_put_layout(const PutArgs& a, hipStream_t s);
 hipError_t launch_put_seal(const PutArgs& a, hipStream_t s);
-#ifdef AMBRY_AB_PUT_ASSEMBLE
-hipError_t launch_put_assemble(const PutArgs& a, int num_cu, hipStream_t s);  // tools/probes/put_assemble.hip
-#endif
 hipError_t launch_gather_copy(const CopyArgs& a, int grid, hipStream_t s);
 
 hipError_t launch_trailer_parse(const TrailerArgs& a, hipStream_t s);

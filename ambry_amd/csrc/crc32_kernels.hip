@@ -31,6 +31,7 @@
 #include "crc32_layout.h"
 #include "crc32_kernels.h"
 #include "crc_img.h"
+#include "put_layout.h"
 #include "region_proc.h"
 
 // A/B knob: s_setprio 3 around the streamed group path's loads, as the wave-mode body has it.
@@ -1643,6 +1644,161 @@ hipError_t launch_region_runs(const RegionArgs& a, int grid, hipStream_t s) {
   hipLaunchKernelGGL(region_runs_kernel, dim3(grid), dim3(1024), 0, s, a);
   return hipGetLastError();
 }
+
+// ---- copy-mode serialization of small messages (put_stream_kernel; StreamPutArgs, crc32_kernels.h) ----
+// The uniform layout of one message (PutMessageFormatInputStream.java:76-124 through put_layout.h):
+// five data segments copied from their sources and six gaps between them -- the header, the record
+// prefixes and trailers -- whose bytes are computed (every CRC field zero here: put_stream_seal_kernel
+// writes them). Segments and gaps alternate: gap g = [hi[g-1], lo[g]) (hi[-1] = 0, lo[5] = len), an
+// absent encryption key an empty segment at the key's end.
+struct StreamMsg {
+  int32_t len;                    // message bytes (<= kStreamPutMax)
+  int32_t lo[5], hi[5];           // data segment k at [lo, hi) of the message (key, enc key, props, um, blob)
+  const uint8_t* src[5];          // its source
+};
+
+__device__ __forceinline__ bool stream_msg(const ambrycrc_put_desc& d, const uint8_t* fields, const uint8_t* blobs,
+                                           StreamMsg& M) {
+  PutLayout L;
+  if (!put_layout(d, L) || L.length > kStreamPutMax) return false;
+  M.len = (int32_t)L.length;
+  uint64_t fo[5];
+  put_field_offsets(d, L, fo);
+  const uint64_t ln[5] = {d.key_len, L.enc_rec ? (uint64_t)d.enckey_len : 0, d.props_len, d.usermeta_len, d.blob_len};
+  const uint64_t so[5] = {d.key_src, d.enckey_src, d.props_src, d.usermeta_src, d.blob_src};
+  if (!L.enc_rec) fo[1] = fo[0] + ln[0];  // the empty segment at the key's end
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    M.lo[k] = (int32_t)fo[k];
+    M.hi[k] = (int32_t)(fo[k] + ln[k]);
+    M.src[k] = (k == 4 ? blobs : fields) + so[k];
+  }
+  return true;
+}
+
+// The source of the 16-B output piece at message-relative dd (dd + m0 a multiple of 16) when the piece
+// lies inside one data segment, else 0 -- masked in arithmetically (a select chain on the segment
+// becomes a scratch table).
+__device__ __forceinline__ uint64_t stream_piece_src(const StreamMsg& M, int32_t dd) {
+  uint64_t src = 0;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const uint64_t in = 0 - (uint64_t)(dd >= M.lo[k] && dd + 16 <= M.hi[k]);
+    src |= in & (uint64_t)(M.src[k] + (dd - M.lo[k]));
+  }
+  return src;
+}
+
+constexpr uint32_t kStreamSbs = 2;  // super-blocks a message's runs span: ceil((63 + kStreamPutMax) / 4096)
+static_assert((63 + kStreamPutMax + kSuperBlock - 1) / kSuperBlock <= kStreamSbs, "streamed message spans");
+
+// A wave per message (grid-stride over the waves of one 1024-thread workgroup per CU; the next
+// message's descriptor loaded while this one runs). The message's output is 1 or 2 super-blocks of
+// 4 KiB from its first 64-B run, four 1 KiB wave pieces each. All loads go out first: the source of
+// each piece that lies inside one data segment, and the bytes of each segment whose piece is not
+// inside it (at most 15 at either end; a lane each). Then the stores: those pieces (16 B each) and
+// those edge bytes. Then the remaining pieces that touch the message are loaded back from the output,
+// where put_layout_kernel wrote the gaps' bytes (the header, record prefixes) and this wave the edge
+// bytes -- one wave's lanes, through the CU's one L1: no fence needed. Then, per super-block, the quad
+// transpose and run_crc as region_runs_kernel hashes them, the 64 sums stored (16-B stores of the lanes
+// whose runs overlap the message) into the message's run slots. A run that is not inside the message
+// (its neighbours' bytes), or that holds a CRC field, is never summed: put_stream_seal_kernel re-reads
+// those bytes once every field is written. (Software-pipelining two messages per wave measured slower:
+// 128 VGPRs and spills, 0.79 against 0.70 ms.)
+__global__ __launch_bounds__(1024) void put_stream_kernel(StreamPutArgs a) {
+  {  // LDS-DMA of the slice tables (image bytes [0, 128 KiB)), as region_runs_kernel
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (uint32_t c = wv; c < kSliceBytes / 1024; c += nw)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(reinterpret_cast<const uint8_t*>(a.img) + c * 1024 + lane * 16),
+          (__attribute__((address_space(3))) void*)(reinterpret_cast<uint8_t*>(g_lds_runs) + c * 1024), 16, 0, 0);
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+  }
+  const uint32_t lane = threadIdx.x & 63u;
+  const LaneConst k = make_lane_const(lane);
+  uint32_t* buf = g_lds_runs + kSliceBytes / 4 + (threadIdx.x >> 6) * (kRunsBufBytes / 4);
+  const uint32_t slot = 16u * (lane & 3u) + (lane >> 2);
+  const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  const uint32_t wave = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * gridDim.x + blockIdx.x);
+  ambrycrc_put_desc next{};
+  if (wave < a.m) next = a.desc[wave];
+  for (uint64_t i = wave; i < a.m; i += nwaves) {
+    const ambrycrc_put_desc d = next;
+    if (i + nwaves < a.m) next = a.desc[i + nwaves];
+    StreamMsg M;
+    if (!stream_msg(d, a.fields, a.blobs, M)) continue;  // the job path's (or invalid: nothing written)
+    const uint64_t m0 = a.oreg0 + d.out_off, S0 = m0 & ~uint64_t(63);
+    const int32_t mis = (int32_t)(m0 & 15u);
+    uint8_t* const out = a.obase + m0;
+    // edge bytes: slot j < 16 of segment s is byte lo + j (below the first inside piece), j >= 16 byte
+    // max(first inside piece, last piece's start) + j - 16 (the rest); 32 slots a segment
+    int32_t ee[3];
+    uint32_t eb[3];
+#pragma unroll
+    for (uint32_t it = 0; it < 3; ++it) {
+      const uint32_t idx = 64 * it + lane, s = idx >> 5, j = idx & 31u;
+      int32_t lo = M.lo[0], hi = M.hi[0];
+      uint64_t src = (uint64_t)M.src[0];
+#pragma unroll
+      for (uint32_t h = 1; h < 5; ++h) {
+        const bool is = s == h;
+        lo = is ? M.lo[h] : lo;
+        hi = is ? M.hi[h] : hi;
+        src = is ? (uint64_t)M.src[h] : src;
+      }
+      const int32_t up = ((lo + mis + 15) & ~15) - mis, dn = ((hi + mis) & ~15) - mis;
+      const int32_t e = j < 16 ? lo + (int32_t)j : (up > dn ? up : dn) + (int32_t)j - 16;
+      const bool live = s < 5 && (j < 16 ? e < (up < hi ? up : hi) : e < hi);
+      ee[it] = live ? e : -1;
+      eb[it] = live ? reinterpret_cast<const uint8_t*>(src)[e - lo] : 0u;
+    }
+    const int32_t p0 = (int32_t)(S0 - m0) + 16 * (int32_t)lane;
+    u32x4 x[kStreamSbs][4];
+    uint64_t ps[kStreamSbs][4];
+#pragma unroll
+    for (uint32_t sb = 0; sb < kStreamSbs; ++sb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        ps[sb][q] = stream_piece_src(M, p0 + (int32_t)(kSuperBlock * sb + kBlockBytes * q));
+        x[sb][q] = u32x4{0u, 0u, 0u, 0u};
+        if (ps[sb][q]) __builtin_memcpy(&x[sb][q], reinterpret_cast<const uint8_t*>(ps[sb][q]), 16);
+      }
+#pragma unroll
+    for (uint32_t it = 0; it < 3; ++it)
+      if (ee[it] >= 0) st8g(out + ee[it], eb[it]);
+#pragma unroll
+    for (uint32_t sb = 0; sb < kStreamSbs; ++sb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (ps[sb][q]) st16u_nt(out + p0 + (int32_t)(kSuperBlock * sb + kBlockBytes * q), x[sb][q]);
+#pragma unroll
+    for (uint32_t sb = 0; sb < kStreamSbs; ++sb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int32_t dd = p0 + (int32_t)(kSuperBlock * sb + kBlockBytes * q);
+        if (!ps[sb][q] && dd + 16 > 0 && dd < M.len) x[sb][q] = *reinterpret_cast<const u32x4*>(out + dd);
+      }
+    const uint64_t nruns = (m0 + M.len - S0 + 63) >> 6;
+    uint32_t* rk = a.rk + kRunPad + i * kStreamPutRuns;
+#pragma unroll
+    for (uint32_t sb = 0; sb < kStreamSbs; ++sb) {
+      if (64 * sb >= nruns) break;
+      quad_transpose_asm(x[sb]);
+      buf[slot] = run_crc<4, 1>(x[sb], k, 0u);
+      if (64 * sb + 4 * lane < nruns && lane < 16)  // runs 64 sb + 4 lane .. + 3, as region_runs_kernel's stores
+        *reinterpret_cast<u32x4*>(rk + 64 * sb + 4 * lane) = *reinterpret_cast<const u32x4*>(buf + 4u * lane);
+    }
+  }
+}
+
+hipError_t launch_put_stream(const StreamPutArgs& a, int num_cu, hipStream_t s) {
+  if (a.m == 0) return hipSuccess;
+  hipLaunchKernelGGL(put_stream_kernel, dim3((uint32_t)num_cu), dim3(1024), 0, s, a);
+  return hipGetLastError();
+}
+
+size_t stream_put_rk_bytes(size_t m) { return ((kRunPad + (size_t)m * kStreamPutRuns) * sizeof(uint32_t) + 255) & ~size_t(255); }
 
 // ---- region mode in one pass: region_fused_kernel (FusedArgs, crc32_kernels.h) ----
 // Workgroup b (one per CU) owns groups [G0, G1) of 16 KiB (4 super-blocks). Streaming wave v <

@@ -50,18 +50,21 @@ __global__ __launch_bounds__(256) void put_layout_kernel(PutArgs a) {
     if (a.msg_len) a.msg_len[i] = 0;
     return;
   }
-#ifdef AMBRY_AB_PUT_ASSEMBLE
-  if (a.asm_max && L.length <= a.asm_max) {  // put_assemble_kernel (tools/probes) wrote it: no jobs
-    for (uint32_t k = 0; k < kPutSlots; ++k) {
-      a.cp_len[k * m + i] = 0;
-      a.cp_cost[k * m + i] = 0;
-      a.crc_len[k * m + i] = 0;
-      a.crc_off[k * m + i] = 0;
-      a.crc_in[k * m + i] = 0;
+  if (a.stream_max) {  // copy mode: messages this short are the streamed kernels' (put_stream_kernel): no jobs
+    if (L.length <= a.stream_max) {
+      for (uint32_t k = 0; k < kPutSlots; ++k) {
+        a.cp_len[k * m + i] = 0;
+        a.cp_cost[k * m + i] = 0;
+        a.crc_len[k * m + i] = 0;
+        a.crc_off[k * m + i] = 0;
+        a.crc_in[k * m + i] = 0;
+      }
+      if (a.msg_len) a.msg_len[i] = L.length;
+      put_write_fixed(d, L, a.out + d.out_off);  // the gaps' bytes, which put_stream_kernel's edge pieces read
+      return;
     }
-    return;
+    *a.big = 1u;  // a longer one: the job path runs (every writer stores the same word)
   }
-#endif
   uint8_t* msg = a.out + d.out_off;
   put_write_fixed(d, L, msg);
   uint32_t head_crc = 0;
@@ -116,6 +119,56 @@ __global__ __launch_bounds__(256) void put_seal_kernel(PutArgs a) {
   const uint64_t len = a.crc_len[j];
   if (len == 0) return;  // absent encryption-key record (every present record has >= 6 bytes)
   put_be64(a.out + a.crc_off[j] + len, (uint64_t)a.crc[j]);
+}
+
+// ---------------------------------------------------------------- streamed small messages
+// Pass 2 of copy-mode serialization for messages of at most kStreamPutMax bytes (put_stream_kernel,
+// crc32_kernels.hip, wrote their bytes and the raw CRC of every 64-B output run): one thread per
+// message computes the header CRC from the bytes it builds in registers and each record's CRC from the
+// run sums (region::record_crc: the head and tail runs a record cuts re-read from the output), and
+// writes the big-endian trailers -- the CRCs MessageFormatInputStream emits after each record
+// (MessageFormatInputStream.java:85-93; PutMessageFormatInputStream.java:76-124). Two blocks per CU, as
+// region_msg_kernel, so a thread's lines stay in L2 between its dependent reads.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AMBRY_REGION_WPE))) void put_stream_seal_kernel(
+    StreamPutArgs a) {
+  __shared__ uint32_t tbl[1024];
+  __shared__ uint32_t nib[region::kNibTotal];
+  __shared__ uint32_t hm[kRegAuxWords], bt[kRegByteWords], un[kRegUnWords];
+  stage_slice_tables(tbl, a.img);
+  region::stage_nib(nib, a.img);
+  region::stage_aux(hm, bt, un, a.img);
+  __syncthreads();
+  const region::Aux aux{hm, bt, un};
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.m; i += (uint64_t)gridDim.x * blockDim.x) {
+    const ambrycrc_put_desc d = a.desc[i];
+    PutLayout L;
+    if (!put_layout(d, L) || L.length > kStreamPutMax) continue;
+    const uint64_t m0 = a.oreg0 + d.out_off;
+    uint8_t* msg = a.obase + m0;
+    // message i's run slots, addressed by base-relative run index (record_crc's rk[k])
+    const uint32_t* rk = reinterpret_cast<const uint32_t*>(
+        reinterpret_cast<uintptr_t>(a.rk + kRunPad + i * kStreamPutRuns) - ((m0 >> 6) << 2));
+    uint8_t h[32];
+    const uint32_t hn = put_header_bytes(d, L, h);
+    put_be64(msg + hn, (uint64_t)crc_regs_lds(tbl, 0u, h, hn));
+#pragma unroll 1
+    for (uint32_t k = 1; k < kPutSlots; ++k) {
+      uint64_t off, ln;
+      bool present;
+      put_crc_job(L, k, &off, &ln, &present);
+      if (!present) continue;
+      const uint32_t c = region::record_crc(region::TabC{tbl}, nib, a.obase, rk, m0 + off, ln, aux);
+      put_be64(msg + off + ln, (uint64_t)c);
+    }
+  }
+}
+
+hipError_t launch_put_stream_seal(const StreamPutArgs& a, int num_cu, hipStream_t s) {
+  if (a.m == 0) return hipSuccess;
+  uint64_t blocks = (a.m + 255) / 256;
+  if (blocks > (uint64_t)num_cu * 2) blocks = (uint64_t)num_cu * 2;
+  hipLaunchKernelGGL(put_stream_seal_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, a);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------- gather copy

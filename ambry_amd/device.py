@@ -190,6 +190,12 @@ def set_transform_verdict(device: int, host: bool) -> int:
     return check(lib().ambrycrc_set_transform_verdict(device, 1 if host else 0), "ambrycrc_set_transform_verdict")
 
 
+def set_put_stream_max(device: int, nbytes: int) -> int:
+    """Serialize copy mode streams messages of at most nbytes (ambrycrc_set_put_stream_max; 6144 the default,
+    0 = every message through the job path). Returns the previous value."""
+    return check(lib().ambrycrc_set_put_stream_max(device, int(nbytes)), "ambrycrc_set_put_stream_max")
+
+
 HOST_AUTO, HOST_GPU, HOST_CPU = 0, 1, 2
 
 

@@ -584,6 +584,11 @@ int ambrycrc_last_transform_path(int device);
  * device gate -- asynchronous; 1 = read back by the calling thread (one stream synchronization per
  * call, 256 calls in flight at most; more take the device form). Returns the previous value. */
 int ambrycrc_set_transform_verdict(int device, int host);
+/* Serialize copy mode (ambrycrc_serialize_puts_dev with both source buffers) streams messages of at most
+ * `bytes` bytes (put_stream_kernel + put_stream_seal_kernel; at most 6144, the
+ * default); 0 sends every message through the job path. Returns the previous value, or < 0. For A/B runs
+ * and tests: both forms write the same bytes. */
+long ambrycrc_set_put_stream_max(int device, long bytes);
 /* Grid size of the persistent sweep kernel (workgroups; 0 = one per CU). */
 int ambrycrc_set_grid(int device, int workgroups);
 

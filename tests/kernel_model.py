@@ -427,7 +427,8 @@ class RegionModel:
         return acc[63] ^ 0xFFFFFFFF
 
     def assembly_crc(self, msg: bytes, a0: int, s: int, e: int) -> int:
-        """put_assemble_kernel's record CRC (put_kernels.hip): the message on the output's 16-B grid
+        """Round 4's put_assemble_kernel's record CRC (removed in round 6 for put_stream_kernel; git
+        history, tools/probes/put_assemble.hip): the message on the output's 16-B grid
         (piece p = bytes [16p - a0, 16p - a0 + 16)), each lane's pieces l, l + 64, ... up to q (the
         piece of byte e - 1) hashed from zero with bytes outside [s, e) zeroed and the first four
         XORed with 0xFF, folded by x^(8*1024); lanes rotated so that lane q mod 64 is last, merged by

@@ -23,6 +23,15 @@ def mf():
     return mod
 
 
+@pytest.fixture(autouse=True, params=["stream", "jobs"])
+def put_form(request, gpu):
+    """Every case in both copy-mode forms: messages of at most 6 KiB streamed (put_stream_kernel, the
+    default) and every message through the job path (ambrycrc_set_put_stream_max(dev, 0))."""
+    prev = gpu.set_put_stream_max(0, 6144 if request.param == "stream" else 0)
+    yield request.param
+    gpu.set_put_stream_max(0, prev)
+
+
 def _dev(b):
     import torch
 
@@ -147,7 +156,7 @@ def test_serialize_large_blobs_copy_through(gpu, mf):
 
 def test_serialize_6k_messages(gpu, mf):
     """Messages of 6,100 to 6,200 bytes, byte by byte (round 4's whole-message assembly cut-off, 6,144
-    B; that kernel is now an A/B probe, tools/probes/put_assemble.hip), under header versions 1-3,
+    B; round 6's streamed form has the same cut-off, kStreamPutMax), under header versions 1-3,
     with and without an encryption key, at unaligned output offsets: every byte as the oracle lays
     it out."""
     from ambry_amd.messages import PutMessage, layout

@@ -138,7 +138,7 @@ def test_region_wave_model_matches_zlib(ambry):
 
 
 def test_assembly_model_matches_zlib(ambry):
-    """The serializer's whole-message assembly (A/B probe tools/probes/put_assemble.hip): a record's
+    """Round 4's whole-message assembly (tools/probes/put_assemble.hip until round 6): a record's
     CRC from the message's pieces on the output's 16-B grid -- per-lane piece hashes folded over the
     wave's 1 KiB chunks, the lanes rotated so the record's last piece comes last, the x^(8*16*2^k)
     tree, the x^(-8d) un-shift -- against zlib, for records of 2 B to ~6 KiB at every message
