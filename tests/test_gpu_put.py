@@ -222,3 +222,27 @@ def test_serialize_graph_capture_and_replay(gpu, mf):
     assert offs2 == offs and total2 == total and len(blobs2) == len(blobs)
     b.copy_(_dev(blobs2))
     check(msgs2)
+
+
+def test_serialize_descriptors_out_of_output_order(gpu, mf):
+    """Descriptors in an order unrelated to their output offsets (a permutation; messages back to back,
+    so neighbours share 16-B pieces and 64-B runs but sit at distant indices, taken by different waves
+    and workgroups): every message lands at its own offset byte-exact, gaps untouched, msg_len in
+    descriptor order."""
+    import torch
+
+    from ambry_amd.messages import pack_batch, serialize_dev
+
+    msgs = random_messages(mf, 500, seed=31, max_blob=7000)
+    descs, fields, blobs, offs, total = pack_batch(msgs, out_align=1, field_align=1, gap=0)
+    perm = np.random.default_rng(5).permutation(len(msgs))
+    out = _dev(b"\xAA" * total)
+    mlen = torch.empty(len(msgs), dtype=torch.int64, device="cuda")
+    serialize_dev(_dev(descs[perm].tobytes()), out, _dev(fields), _dev(blobs), msg_len=mlen)
+    torch.cuda.synchronize()
+    exp = bytearray(b"\xAA" * total)
+    for m, o in zip(msgs, offs):
+        e = expected(mf, m)
+        exp[o:o + len(e)] = e
+    assert out.cpu().numpy().tobytes() == bytes(exp)
+    assert mlen.cpu().numpy().tolist() == [len(expected(mf, msgs[i])) for i in perm]
