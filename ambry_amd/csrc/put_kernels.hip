@@ -166,7 +166,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AMBRY_REGIO
 hipError_t launch_put_stream_seal(const StreamPutArgs& a, int num_cu, hipStream_t s) {
   if (a.m == 0) return hipSuccess;
   uint64_t blocks = (a.m + 255) / 256;
-  if (blocks > (uint64_t)num_cu * 2) blocks = (uint64_t)num_cu * 2;
+  if (blocks > (uint64_t)num_cu * AMBRY_SEAL_BPC) blocks = (uint64_t)num_cu * AMBRY_SEAL_BPC;
   hipLaunchKernelGGL(put_stream_seal_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, a);
   return hipGetLastError();
 }
