@@ -41,7 +41,7 @@ def _props_tensor(torch):
     return torch.from_numpy(np.frombuffer(props94(), dtype=np.uint8).copy()).cuda()
 
 
-def run(m, blob_bytes, reps, in_place, um_len=1000):
+def run(m, blob_bytes, reps, in_place, um_len=1000, blob_shift=0):
     import numpy as np
     import torch
 
@@ -62,14 +62,14 @@ def run(m, blob_bytes, reps, in_place, um_len=1000):
     descs["key_src"] = idx * fstride
     descs["props_src"] = idx * fstride + key_len
     descs["usermeta_src"] = idx * fstride + key_len + props_len
-    descs["blob_src"] = idx * blob_bytes
+    descs["blob_src"] = idx * blob_bytes + blob_shift
     descs["blob_len"] = blob_bytes
     descs["key_len"], descs["props_len"], descs["usermeta_len"] = key_len, props_len, um_len
     descs["enckey_len"] = -1
     descs["header_version"] = 3
     d_desc = torch.from_numpy(descs.view(np.uint8).copy()).cuda()
     fields = torch.empty(m * fstride + 16, dtype=torch.uint8, device="cuda")
-    blobs = torch.empty(max(1, m * blob_bytes), dtype=torch.uint8, device="cuda")
+    blobs = torch.empty(max(1, m * blob_bytes + blob_shift), dtype=torch.uint8, device="cuda")
     D.fill_random(fields, 1, 0)
     D.fill_random(blobs, 2, 0)
     fields[: m * fstride].view(m, fstride)[:, key_len:key_len + props_len] = _props_tensor(torch)
@@ -79,7 +79,7 @@ def run(m, blob_bytes, reps, in_place, um_len=1000):
     # check: sampled messages against the host serializer, all of them by the GPU verify
     fh = fields.cpu().numpy().tobytes()
     for i in sorted({0, m // 2, m - 1}):
-        bl = blobs[i * blob_bytes:(i + 1) * blob_bytes].cpu().numpy().tobytes()
+        bl = blobs[i * blob_bytes + blob_shift:(i + 1) * blob_bytes + blob_shift].cpu().numpy().tobytes()
         o = i * fstride
         msg = PutMessage(key=fh[o:o + key_len], props=fh[o + key_len:o + key_len + props_len],
                          usermeta=fh[o + key_len + props_len:o + fstride], blob=bl)
@@ -261,6 +261,8 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--cases", default="64k,4k,4m")
     ap.add_argument("--um-len", type=int, default=1000, help="user metadata bytes per PUT (1005: blob stores aligned)")
+    ap.add_argument("--blob-shift", type=int, default=0,
+                    help="blob source offset within its buffer (11 with the default user metadata: loads aligned)")
     ap.add_argument("--copy-only", action="store_true", help="skip the in-place mode")
     ap.add_argument("--transform", default="64k,4k,4m", help="ValidatingTransformer cases ('' for none)")
     ap.add_argument("--verdict", default="device,host",
@@ -282,8 +284,9 @@ def main():
         for in_place in (False, True):
             if in_place and args.copy_only:
                 continue
-            r = run(m, s, args.reps, in_place, args.um_len)
+            r = run(m, s, args.reps, in_place, args.um_len, args.blob_shift)
             r["usermeta_bytes"] = args.um_len
+            r["blob_shift"] = args.blob_shift
             print(json.dumps(r), flush=True)
             torch.cuda.empty_cache()
     for c in [x for x in args.transform.split(",") if x]:
