@@ -676,6 +676,15 @@ void free_ctx(DevCtx* c) {
     (void)hipEventDestroy(r.done);
   }
   for (void* p : c->ws_kept) (void)hipFree(p);
+  for (DevCtx::XformSide* x : c->xs_list) {
+    if (x->side) (void)hipStreamDestroy(x->side);
+    if (x->d_gates) (void)hipFree(x->d_gates);
+    if (x->d_done) (void)hipFree(x->d_done);
+    if (x->fork) (void)hipEventDestroy(x->fork);
+    for (hipEvent_t e : x->ev)
+      if (e) (void)hipEventDestroy(e);
+    delete x;
+  }
   for (auto& e : c->pending) {
     (void)hipEventDestroy(e.a);
     (void)hipEventDestroy(e.b);
@@ -857,6 +866,12 @@ int ambrycrc_init(int device) {
     char* end = nullptr;
     const unsigned long x = strtoul(v, &end, 10);
     if (end != v && *end == '\0') c->stream_put_max = x < kStreamPutMax ? x : kStreamPutMax;
+  }
+  if (const char* v = getenv("AMBRYCRC_XFORM_SIDE")) c->xform_side = strcmp(v, "0") == 0 ? 0 : 1;  // A/B: §12.9
+  {  // the side-stream verdict needs hipStreamWaitValue32
+    int can = 0;
+    if (hipDeviceGetAttribute(&can, hipDeviceAttributeCanUseStreamWaitValue, device) != hipSuccess || !can)
+      c->xform_side = 0;
   }
   if (const char* v = getenv("AMBRYCRC_XFORM_FAST_MAX")) {  // A/B: the transform fast path's cut-off
     char* end = nullptr;

@@ -95,6 +95,29 @@ struct DevCtx {
   // The transform fast path's verdict read by the host (ambrycrc_set_transform_verdict): off by
   // default -- the general path is then enqueued behind a device gate, and the call never blocks.
   std::atomic<int> xform_host_verdict{0};
+  // The device verdict's side stream, one per caller stream: the general path's
+  // gated kernels go to `side`, forked after the fast path, and the caller's stream waits on the done
+  // signal instead (hipStreamWaitValue32, >= the call's seq) -- which the fast path sets when it took
+  // the batch, and the side chain's last kernel sets always. Each call's gates (fail, xfail) sit in a
+  // slot of a ring, so a side chain still running its no-ops never reads a later call's verdict; a
+  // slot is reused only behind its last chain's event. Entries are never freed before shutdown: the
+  // least recently used is re-keyed to a new caller stream (its seq keeps increasing, so a wait still
+  // pending on the old stream is met). xform_side = 0 (AMBRYCRC_XFORM_SIDE=0): the inline gated chain.
+  static constexpr uint32_t kXformSlots = 32;
+  struct XformSide {
+    hipStream_t stream = nullptr;  // the caller's
+    hipStream_t side = nullptr;    // library-owned, non-blocking
+    uint32_t* d_gates = nullptr;   // [4 * kXformSlots]: slot k's fail at 4k, xfail at 4k + 1
+    uint32_t* d_done = nullptr;    // the low word of one HSA signal (hipMallocSignalMemory)
+    hipEvent_t fork = nullptr;
+    hipEvent_t ev[kXformSlots] = {};  // recorded on `side` after the chain that used slot k
+    uint32_t seq = 0;                 // the last call's target value
+    uint64_t tick = 0;
+  };
+  int xform_side = 1;
+  std::mutex xs_mu;
+  std::vector<XformSide*> xs_list;  // at most kMaxStreamWs
+  uint64_t xs_tick = 0;
   // Pinned words for one-word device-to-host reads (the host verdict): a call holds slot k (busy[k])
   // from its copy until it has read the word, so no two calls in flight share one; with every slot
   // held the call takes the device-gated form instead.

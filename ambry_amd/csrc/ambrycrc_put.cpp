@@ -220,6 +220,47 @@ size_t transform_fast_bytes(const uint8_t* d_region, uint64_t region_len, size_t
 }
 }  // namespace
 
+namespace {
+// The side-stream verdict's entry for caller stream s (c->xs_mu held): its own, else a new one, else the
+// least recently used re-keyed to s (DevCtx::XformSide). Null when one cannot be made.
+DevCtx::XformSide* xform_side_for(DevCtx* c, hipStream_t s) {
+  DevCtx::XformSide* x = nullptr;
+  for (DevCtx::XformSide* e : c->xs_list)
+    if (e->stream == s) x = e;
+  if (!x && c->xs_list.size() < kMaxStreamWs) {
+    auto* n = new DevCtx::XformSide();
+    bool ok = hipStreamCreateWithFlags(&n->side, hipStreamNonBlocking) == hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&n->d_gates), 16 * DevCtx::kXformSlots) == hipSuccess &&
+              hipExtMallocWithFlags(reinterpret_cast<void**>(&n->d_done), 8, hipMallocSignalMemory) == hipSuccess &&
+              hipEventCreateWithFlags(&n->fork, hipEventDisableTiming) == hipSuccess;
+    for (uint32_t k = 0; ok && k < DevCtx::kXformSlots; ++k)
+      ok = hipEventCreateWithFlags(&n->ev[k], hipEventDisableTiming) == hipSuccess;
+    // the signal starts at 0 (seq 0 is never waited for); both words are set before any stream uses them
+    ok = ok && hipMemset(n->d_done, 0, 8) == hipSuccess && hipMemset(n->d_gates, 0, 16 * DevCtx::kXformSlots) == hipSuccess;
+    if (!ok) {
+      if (n->side) (void)hipStreamDestroy(n->side);
+      if (n->d_gates) (void)hipFree(n->d_gates);
+      if (n->d_done) (void)hipFree(n->d_done);
+      if (n->fork) (void)hipEventDestroy(n->fork);
+      for (hipEvent_t e : n->ev)
+        if (e) (void)hipEventDestroy(e);
+      delete n;
+      return nullptr;
+    }
+    c->xs_list.push_back(n);
+    x = n;
+  }
+  if (!x) {
+    x = c->xs_list[0];
+    for (DevCtx::XformSide* e : c->xs_list)
+      if (e->tick < x->tick) x = e;
+  }
+  x->stream = s;
+  x->tick = ++c->xs_tick;
+  return x;
+}
+}  // namespace
+
 uint64_t ambrycrc_transform_out_bound(uint64_t region_len, size_t m) {
   static_assert(AMBRYCRC_TRANSFORM_GROWTH_MAX == (40 - 34) + kPropsAppendixMax + (13 - 10), "growth bound");
   const uint64_t g = (uint64_t)AMBRYCRC_TRANSFORM_GROWTH_MAX;
@@ -299,6 +340,10 @@ int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len
   // then fails verification sets `fail`, and the fallback pass below rebuilds the output exactly as
   // the three-pass form did (verify bits first, then the transform's own, then the placement).
   const uint32_t* general = nullptr;  // the general path's gate (null: it always runs)
+  std::unique_lock<std::mutex> xs_lock;  // held from the side entry's choice to the caller's wait
+  DevCtx::XformSide* xs = nullptr;
+  uint32_t xs_seq = 0, xs_slot = 0;
+  hipStream_t main_stream = stream;
   if (fast) {
     // One pass (region_fused_kernel's copy form, then region_tail_kernel): verify every message
     // while copying the region into the output; when every message qualifies the headers are
@@ -335,11 +380,32 @@ int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len
     // (ctl included) and read their device gate, *xfail, at every launch
     f.xfail = fail + 1;
     f.patch = copy_off;  // (the general path's, unused until then)
-    if (hipMemsetAsync(f.ctl, 0, 8, stream) != hipSuccess || hipMemsetAsync(fail, 0, 8, stream) != hipSuccess)
-      return AMBRYCRC_EHIP;
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(stream, &cap) != hipSuccess) return AMBRYCRC_EHIP;
     const int slot = c->xform_host_verdict && cap == hipStreamCaptureStatusNone ? c->take_host_word() : -1;
+    if (slot < 0 && c->xform_side && cap == hipStreamCaptureStatusNone) {
+      // Device verdict on a side stream: this call's gates in ring slot k, reused
+      // only once the side chain that last read them has completed.
+      xs_lock = std::unique_lock<std::mutex>(c->xs_mu);
+      xs = xform_side_for(c, stream);
+      if (xs) {
+        if (xs->seq >= 0xFFFFFFF0u) {  // before the target wraps: drain both streams, restart at 0
+          if (hipStreamSynchronize(xs->side) != hipSuccess || hipStreamSynchronize(stream) != hipSuccess ||
+              hipMemset(xs->d_done, 0, 8) != hipSuccess)
+            return AMBRYCRC_EHIP;
+          xs->seq = 0;
+        }
+        xs_seq = ++xs->seq;
+        xs_slot = xs_seq % DevCtx::kXformSlots;
+        if (hipEventQuery(xs->ev[xs_slot]) == hipErrorNotReady &&
+            hipStreamWaitEvent(stream, xs->ev[xs_slot], 0) != hipSuccess)
+          return AMBRYCRC_EHIP;
+        fail = xs->d_gates + 4 * xs_slot;
+        f.xfail = fail + 1;
+      }
+    }
+    if (hipMemsetAsync(f.ctl, 0, 8, stream) != hipSuccess || hipMemsetAsync(fail, 0, 8, stream) != hipSuccess)
+      return AMBRYCRC_EHIP;
     f.path_out = slot < 0 ? c->d_path : nullptr;
     if (launch_region_fused(f, c->num_cu, stream) != hipSuccess) {
       if (slot >= 0) c->release_host_word(slot);
@@ -364,15 +430,24 @@ int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len
     } else {
       // Device verdict (the default, and always under stream capture): the general path below is
       // enqueued behind *xfail -- every one of its kernels returns at once when the fast path took
-      // the batch -- so the call only enqueues work, as every *_dev entry does.
+      // the batch -- so the call only enqueues work, as every *_dev entry does. With a side stream
+      // (xs) that chain runs there, and this stream waits only for the done signal.
       general = f.xfail;
       c->last_xform_path.store(2);
+      if (xs) {
+        if (launch_xform_signal(f.xfail, xs->d_done, xs_seq, stream) != hipSuccess ||
+            hipEventRecord(xs->fork, stream) != hipSuccess || hipStreamWaitEvent(xs->side, xs->fork, 0) != hipSuccess)
+          return AMBRYCRC_EHIP;
+        main_stream = stream;
+        stream = xs->side;
+      }
     }
   } else {
     c->last_xform_path.store(0);
   }
   // fail[0] is written only by the general path below; the fast path zeroed it with xfail
   if (!fast && hipMemsetAsync(fail, 0, sizeof(uint32_t), stream) != hipSuccess) return AMBRYCRC_EHIP;
+  t.fail = fail;
   p.gate = general;
   t.gate = general;
   t.gate_when = 1;
@@ -395,7 +470,9 @@ int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len
   if (launch_props_fix(t, stream) != hipSuccess) return AMBRYCRC_EHIP;  // after the copy-through
   t.gate = fail;
   t.gate_when = 0;  // no failure: the final status is the verify's bits, else the transform's own
+  t.gate2 = general;  // (and only when the general path ran)
   if (launch_transform_merge(t, stream) != hipSuccess) return AMBRYCRC_EHIP;
+  t.gate2 = nullptr;
 
   // Fallback pass (only when `fail` is set; every kernel checks it): descriptors from the final
   // verify status, packed placement, layout and a gather copy of the fields from the region.
@@ -408,7 +485,14 @@ int ambrycrc_transform_messages_dev(const uint8_t* d_region, uint64_t region_len
   rc = enqueue_serialize(c, t.desc, m, d_region, d_region, d_out, nullptr, shared, stream, t.in_crc, false, fail,
                          t.pfix);
   if (rc) return rc;
-  return hip_err(launch_props_fix(t, stream));  // after the gather copy (gated as the pass)
+  if (launch_props_fix(t, stream) != hipSuccess) return AMBRYCRC_EHIP;  // after the gather copy (gated as the pass)
+  if (xs) {  // the side chain's end: done = seq whatever the verdict; the caller's stream waits for it
+    if (launch_xform_signal(nullptr, xs->d_done, xs_seq, stream) != hipSuccess ||
+        hipEventRecord(xs->ev[xs_slot], stream) != hipSuccess ||
+        hipStreamWaitValue32(main_stream, xs->d_done, xs_seq, hipStreamWaitValueGte, 0xFFFFFFFFu) != hipSuccess)
+      return AMBRYCRC_EHIP;
+  }
+  return AMBRYCRC_OK;
 }
 
 }  // extern "C"

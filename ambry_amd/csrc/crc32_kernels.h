@@ -313,6 +313,9 @@ struct TransformArgs {
   uint8_t* out;
   const uint32_t* gate;
   int gate_when;
+  // transform_merge_kernel only: also skip it when *gate2 == 0 (the fast path took the batch, so the
+  // general path, whose bits it merges, never ran). Null: no second gate.
+  const uint32_t* gate2;
   // [m] how each transformed message's stored BlobProperties payload becomes its V5 bytes
   // (record_fields.h): written by transform_describe, applied by props_fix_kernel after the
   // payload is copied into place.
@@ -327,6 +330,9 @@ hipError_t launch_transform_place(const TransformArgs& a, const uint64_t* start,
 hipError_t launch_transform_jobs(const TransformArgs& a, hipStream_t s);
 hipError_t launch_transform_finish(const TransformArgs& a, hipStream_t s);
 hipError_t launch_transform_merge(const TransformArgs& a, hipStream_t s);
+// The side-stream device verdict: *done = seq, at system scope -- unconditionally, or
+// (xfail non-null) only when *xfail == 0, i.e. the transform's fast path took the batch.
+hipError_t launch_xform_signal(const uint32_t* xfail, uint32_t* done, uint32_t seq, hipStream_t s);
 hipError_t launch_props_fix(const TransformArgs& a, hipStream_t s);
 
 // ---- copy-mode serialization of small messages by streaming the output (round 6)

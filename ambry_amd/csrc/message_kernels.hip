@@ -487,8 +487,19 @@ __global__ __launch_bounds__(256) void transform_finish_kernel(TransformArgs a) 
 // No fallback: the final status is the verify's bits, or else the transform's own.
 __global__ __launch_bounds__(256) void transform_merge_kernel(TransformArgs a) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.m || gated_off(a.gate, a.gate_when)) return;
+  if (i >= a.m || gated_off(a.gate, a.gate_when) || (a.gate2 && *a.gate2 == 0)) return;
   if (a.status[i] == 0) a.status[i] = a.xstatus[i];
+}
+
+__global__ void xform_signal_kernel(const uint32_t* xfail, uint32_t* done, uint32_t seq) {
+  if (threadIdx.x != 0) return;
+  if (xfail && __hip_atomic_load(xfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+  __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t launch_xform_signal(const uint32_t* xfail, uint32_t* done, uint32_t seq, hipStream_t s) {
+  hipLaunchKernelGGL(xform_signal_kernel, dim3(1), dim3(64), 0, s, xfail, done, seq);
+  return hipGetLastError();
 }
 
 hipError_t launch_transform_jobs(const TransformArgs& a, hipStream_t s) {

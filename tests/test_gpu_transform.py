@@ -725,3 +725,49 @@ def test_transform_negative_life_versions_device_and_cpu_leg(gpu, mf, dense):
         if exp is not None:
             assert coo[i] == pos and cout[pos:pos + len(exp)] == exp, i
             pos += len(exp)
+
+
+def test_transform_back_to_back_verdicts_one_stream(gpu, mf):
+    """The device verdict's side stream: 40 transforms enqueued back to back on one
+    stream -- more than the 32 gate slots -- every third one with a corrupted message (the general path
+    redoes that batch on the side stream while later calls' fast paths run), then ONE synchronize of
+    the caller's stream only: every call's outputs are the oracle's (the clean ones byte-exact with
+    fast_expected), so no side chain read a later call's verdict and the stream waited for every
+    general path it needed."""
+    import torch
+
+    from ambry_amd.messages import transform_dev
+
+    region, offs = dense_v3_region(mf, 120, seed=77)
+    k = 60
+    bad = bytearray(region)
+    bad[offs[k] + 70] ^= 0x08
+    s = torch.cuda.Stream()
+    regions = [torch.frombuffer(bytearray(region), dtype=torch.uint8).cuda(),
+               torch.frombuffer(bytearray(bad), dtype=torch.uint8).cuda()]
+    d_off = torch.tensor(offs, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    results = []
+    with torch.cuda.stream(s):
+        for call in range(40):
+            spoiled = call % 3 == 2
+            results.append((spoiled, transform_dev(regions[int(spoiled)], d_off, stream=s)))
+    s.synchronize()
+    clean_exp = fast_expected(region, offs, len(region))
+    bad_exp = [mf.transform_message(bytes(bad), o, version=3) for o in offs]
+    for call, (spoiled, (out, oo, ol, st)) in enumerate(results):
+        st, oo, ol = st.cpu().numpy().view(np.uint32), oo.cpu().numpy(), ol.cpu().numpy()
+        out_h = out.cpu().numpy().tobytes()
+        if not spoiled:
+            assert st.tolist() == [0] * len(offs), call
+            assert np.array_equal(oo, clean_exp[1]) and np.array_equal(ol, clean_exp[2]), call
+            assert out_h[:len(clean_exp[0])] == clean_exp[0], call
+            continue
+        pos = 0
+        for i, (exp_st, exp) in enumerate(bad_exp):
+            assert int(st[i]) == exp_st, (call, i)
+            if exp is None:
+                assert ol[i] == 0 and oo[i] == -1, (call, i)
+                continue
+            assert oo[i] == pos and out_h[pos:pos + len(exp)] == exp, (call, i)
+            pos += len(exp)
