@@ -1676,18 +1676,37 @@ __device__ __forceinline__ bool stream_msg(const ambrycrc_put_desc& d, const uin
   return true;
 }
 
-// The source of the 16-B output piece at message-relative dd (dd + m0 a multiple of 16) when the piece
-// lies inside one data segment, else 0 -- masked in arithmetically (a select chain on the segment
-// becomes a scratch table).
-__device__ __forceinline__ uint64_t stream_piece_src(const StreamMsg& M, int32_t dd) {
-  uint64_t src = 0;
+// The message's data segments as a per-wave LDS table (4 words each: lo, hi, and the 64-bit
+// source - lo), entry 5 empty, so a lane finds a segment's bounds and source with one ds_read_b128
+// at its own index instead of a select chain over all five (the chain cost ~45 VALU a piece).
+__device__ __forceinline__ void stream_seg_table(const StreamMsg& M, u32x4* tab, uint32_t lane) {
+  __builtin_amdgcn_wave_barrier();  // one wave's LDS operations run in order: keep the program order
+  if (lane == 0) {
 #pragma unroll
-  for (int k = 0; k < 5; ++k) {
-    const uint64_t in = 0 - (uint64_t)(dd >= M.lo[k] && dd + 16 <= M.hi[k]);
-    src |= in & (uint64_t)(M.src[k] + (dd - M.lo[k]));
+    for (int k = 0; k < 5; ++k) {
+      const uint64_t dl = (uint64_t)M.src[k] - (uint64_t)(int64_t)M.lo[k];
+      tab[k] = u32x4{(uint32_t)M.lo[k], (uint32_t)M.hi[k], (uint32_t)dl, (uint32_t)(dl >> 32)};
+    }
+    tab[5] = u32x4{0u, 0u, 0u, 0u};
   }
-  return src;
+  __builtin_amdgcn_wave_barrier();
 }
+
+// The source of the 16-B output piece at message-relative dd (dd + m0 a multiple of 16) when the piece
+// lies inside one data segment, else 0. The segments are in message order with lo nondecreasing, so
+// the only one that can hold the piece is the last whose lo <= dd.
+__device__ __forceinline__ uint64_t stream_piece_src(const StreamMsg& M, const u32x4* tab, int32_t dd) {
+  const uint32_t k = (uint32_t)(dd >= M.lo[1]) + (uint32_t)(dd >= M.lo[2]) + (uint32_t)(dd >= M.lo[3]) +
+                     (uint32_t)(dd >= M.lo[4]);
+  const u32x4 e = tab[k];
+  const bool in = dd >= (int32_t)e.x && dd + 16 <= (int32_t)e.y;
+  const uint64_t src = (((uint64_t)e.w << 32) | e.z) + (uint64_t)(int64_t)dd;
+  return in ? src : 0;
+}
+
+// A 16-B load from a source address held as an integer, kept in the global address space (a generic
+// pointer would make it a flat load, which also counts on lgkmcnt, as the stores above).
+__device__ __forceinline__ u32x4 ld16ug(uint64_t a) { return *reinterpret_cast<const gu32x4*>(a); }
 
 constexpr uint32_t kStreamSbs = 2;  // super-blocks a message's runs span: ceil((63 + kStreamPutMax) / 4096)
 static_assert((63 + kStreamPutMax + kSuperBlock - 1) / kSuperBlock <= kStreamSbs, "streamed message spans");
@@ -1718,6 +1737,7 @@ __global__ __launch_bounds__(1024) void put_stream_kernel(StreamPutArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
   const LaneConst k = make_lane_const(lane);
   uint32_t* buf = g_lds_runs + kSliceBytes / 4 + (threadIdx.x >> 6) * (kRunsBufBytes / 4);
+  u32x4* const tab = reinterpret_cast<u32x4*>(buf + 128);  // the segment table (words 128..151 of the wave's buffer)
   const uint32_t slot = 16u * (lane & 3u) + (lane >> 2);
   const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
   const uint32_t wave = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * gridDim.x + blockIdx.x);
@@ -1733,25 +1753,19 @@ __global__ __launch_bounds__(1024) void put_stream_kernel(StreamPutArgs a) {
     uint8_t* const out = a.obase + m0;
     // edge bytes: slot j < 16 of segment s is byte lo + j (below the first inside piece), j >= 16 byte
     // max(first inside piece, last piece's start) + j - 16 (the rest); 32 slots a segment
+    stream_seg_table(M, tab, lane);
     int32_t ee[3];
     uint32_t eb[3];
 #pragma unroll
     for (uint32_t it = 0; it < 3; ++it) {
       const uint32_t idx = 64 * it + lane, s = idx >> 5, j = idx & 31u;
-      int32_t lo = M.lo[0], hi = M.hi[0];
-      uint64_t src = (uint64_t)M.src[0];
-#pragma unroll
-      for (uint32_t h = 1; h < 5; ++h) {
-        const bool is = s == h;
-        lo = is ? M.lo[h] : lo;
-        hi = is ? M.hi[h] : hi;
-        src = is ? (uint64_t)M.src[h] : src;
-      }
+      const u32x4 t = tab[s < 5 ? s : 5];
+      const int32_t lo = (int32_t)t.x, hi = (int32_t)t.y;
       const int32_t up = ((lo + mis + 15) & ~15) - mis, dn = ((hi + mis) & ~15) - mis;
       const int32_t e = j < 16 ? lo + (int32_t)j : (up > dn ? up : dn) + (int32_t)j - 16;
       const bool live = s < 5 && (j < 16 ? e < (up < hi ? up : hi) : e < hi);
       ee[it] = live ? e : -1;
-      eb[it] = live ? reinterpret_cast<const uint8_t*>(src)[e - lo] : 0u;
+      eb[it] = live ? (uint32_t)*reinterpret_cast<const gu8*>((((uint64_t)t.w << 32) | t.z) + (uint64_t)(int64_t)e) : 0u;
     }
     const int32_t p0 = (int32_t)(S0 - m0) + 16 * (int32_t)lane;
     u32x4 x[kStreamSbs][4];
@@ -1760,9 +1774,9 @@ __global__ __launch_bounds__(1024) void put_stream_kernel(StreamPutArgs a) {
     for (uint32_t sb = 0; sb < kStreamSbs; ++sb)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        ps[sb][q] = stream_piece_src(M, p0 + (int32_t)(kSuperBlock * sb + kBlockBytes * q));
+        ps[sb][q] = stream_piece_src(M, tab, p0 + (int32_t)(kSuperBlock * sb + kBlockBytes * q));
         x[sb][q] = u32x4{0u, 0u, 0u, 0u};
-        if (ps[sb][q]) __builtin_memcpy(&x[sb][q], reinterpret_cast<const uint8_t*>(ps[sb][q]), 16);
+        if (ps[sb][q]) x[sb][q] = ld16ug(ps[sb][q]);
       }
 #pragma unroll
     for (uint32_t it = 0; it < 3; ++it)

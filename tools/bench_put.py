@@ -76,9 +76,11 @@ def run(m, blob_bytes, reps, in_place, um_len=1000, blob_shift=0):
     out = torch.zeros(m * stride, dtype=torch.uint8, device="cuda")
     serialize_dev(d_desc, out, fields, blobs)  # copy mode fills `out`; in-place mode then reuses its bytes
     torch.cuda.synchronize()
-    # check: sampled messages against the host serializer, all of them by the GPU verify
+    # check: sampled messages against the host serializer, all of them by the GPU verify (not for the
+    # timing-only probe builds of tools/ab_build.sh, whose CRCs are wrong by design)
     fh = fields.cpu().numpy().tobytes()
-    for i in sorted({0, m // 2, m - 1}):
+    probe = os.environ.get("AMBRYCRC_ALLOW_PROBE") == "1"
+    for i in sorted({0, m // 2, m - 1}) if not probe else ():
         bl = blobs[i * blob_bytes + blob_shift:(i + 1) * blob_bytes + blob_shift].cpu().numpy().tobytes()
         o = i * fstride
         msg = PutMessage(key=fh[o:o + key_len], props=fh[o + key_len:o + key_len + props_len],
@@ -86,7 +88,7 @@ def run(m, blob_bytes, reps, in_place, um_len=1000, blob_shift=0):
         assert out[i * stride:i * stride + L].cpu().numpy().tobytes() == serialize_host(msg)[0], i
     offs = torch.from_numpy(descs["out_off"].astype(np.int64)).cuda()
     st, _ = D.verify_messages(out, offs, want_end=False)
-    assert int(st.abs().sum().item()) == 0
+    assert probe or int(st.abs().sum().item()) == 0
 
     def step():
         if in_place:
