@@ -27,6 +27,9 @@
 #ifndef AMBRY_REGION_AUX  // region pass 2's LDS helpers (region_crc.h Aux): 1 = LDS byte masks + H0, 2 = x^(8*256)
 #define AMBRY_REGION_AUX 7  // byte tables for the Horner steps, 4 = two-multiply un-shift
 #endif
+#ifndef AMBRY_STREAM_PIPE  // serialize copy mode's streamed form: message i+1's loads in flight while i is hashed
+#define AMBRY_STREAM_PIPE 1
+#endif
 #ifndef AMBRY_SEAL_BPC  // serialize copy mode's streamed form: put_stream_seal_kernel blocks per CU
 #define AMBRY_SEAL_BPC 2
 #endif
@@ -102,7 +105,7 @@
 // X(name, default) for every knob above: ambrycrc_version() reports those that differ.
 #define AMBRY_KNOB_LIST(X)                                                                                  \
   X(AMBRY_PROPS_WIN, 96) X(AMBRY_PARSE_BPC, 2) X(AMBRY_REGION_WPE, 2) X(AMBRY_REGION_BPC, 2)                  \
-  X(AMBRY_REGION_BPC_SMALL, 2) X(AMBRY_REGION_AUX, 7) X(AMBRY_SEAL_BPC, 2) X(AMBRY_HOST_VERIFY_CPU_PCT, 50) X(AMBRY_HOST_XFORM_CPU_PCT, 25)                                                                          \
+  X(AMBRY_REGION_BPC_SMALL, 2) X(AMBRY_REGION_AUX, 7) X(AMBRY_SEAL_BPC, 2) X(AMBRY_STREAM_PIPE, 1) X(AMBRY_HOST_VERIFY_CPU_PCT, 50) X(AMBRY_HOST_XFORM_CPU_PCT, 25)                                                                          \
   X(AMBRY_FUSED_PROC, 0)                                                                                      \
   X(AMBRY_FUSED_WAVES_VERIFY, 12)                                                                               \
   X(AMBRY_FUSED_WAVES_COPY, 8) X(AMBRY_FUSED_NT, 1) X(AMBRY_FUSED_ENDS, 1)                                                                 \

@@ -1724,6 +1724,155 @@ static_assert((63 + kStreamPutMax + kSuperBlock - 1) / kSuperBlock <= kStreamSbs
 // (its neighbours' bytes), or that holds a CRC field, is never summed: put_stream_seal_kernel re-reads
 // those bytes once every field is written. (Software-pipelining two messages per wave measured slower:
 // 128 VGPRs and spills, 0.79 against 0.70 ms.)
+#if AMBRY_STREAM_PIPE
+// Pipelined across messages: while message i's output is stored, its gap pieces loaded back and its
+// runs hashed, message i+1's source loads are in flight. For the hash to wait only for message i's
+// loads, the loads issued after them must be the same in number on every path (the compiler's wait
+// counts are the least over the paths): so every edge-byte and piece load of the next message is
+// issued, a lane or a message with nothing to load reading the table image instead, and the
+// descriptors are read as dwords through the constant address space (scalar loads; a byte field
+// read from a vector load would wait for every load in flight). Piece sources are not kept: a bit
+// mask per lane says which of the 8 pieces came from a source.
+namespace {
+struct StreamUnit {  // wave-uniform: one message's output and its run slots
+  uint8_t* out;      // the message's first byte
+  int32_t p0b;       // (its first run's start) - (its first byte), <= 0
+  int32_t len;
+  uint32_t nruns;    // 0: no message
+  uint32_t* rk;
+};
+}  // namespace
+
+__global__ __launch_bounds__(1024) void put_stream_kernel(StreamPutArgs a) {
+  {  // LDS-DMA of the slice tables (image bytes [0, 128 KiB)), as region_runs_kernel
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (uint32_t c = wv; c < kSliceBytes / 1024; c += nw)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(reinterpret_cast<const uint8_t*>(a.img) + c * 1024 + lane * 16),
+          (__attribute__((address_space(3))) void*)(reinterpret_cast<uint8_t*>(g_lds_runs) + c * 1024), 16, 0, 0);
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+  }
+  const uint32_t lane = threadIdx.x & 63u;
+  const LaneConst k = make_lane_const(lane);
+  uint32_t* buf = g_lds_runs + kSliceBytes / 4 + (threadIdx.x >> 6) * (kRunsBufBytes / 4);
+  u32x4* const tab = reinterpret_cast<u32x4*>(buf + 128);  // the segment table (words 128..151 of the wave's buffer)
+  const uint32_t slot = 16u * (lane & 3u) + (lane >> 2);
+  const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  const uint32_t wave = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * gridDim.x + blockIdx.x);
+  typedef __attribute__((address_space(4))) const uint32_t cword;
+  static_assert(sizeof(ambrycrc_put_desc) == 80, "descriptor words");
+  auto desc_at = [&](uint64_t j) {
+    cword* w = (cword*)(uintptr_t)a.desc + 20 * j;
+    uint32_t r[20];
+#pragma unroll
+    for (int t = 0; t < 20; ++t) r[t] = w[t];
+    ambrycrc_put_desc d;
+    __builtin_memcpy(&d, r, sizeof d);
+    return d;
+  };
+  const uint64_t dummy = (uint64_t)(uintptr_t)a.img;  // loads with nothing to fetch read the table image
+
+  // The next streamed message from i on (i advances past the job path's and invalid ones): its unit,
+  // segment table, edge bytes and source pieces, every load issued, none waited for.
+  uint64_t i = wave;
+  auto start = [&](StreamUnit& u, int32_t (&ee)[3], uint32_t (&eb)[3], u32x4 (&x)[kStreamSbs][4], uint32_t& pm) {
+    StreamMsg M;
+    ambrycrc_put_desc d{};
+    bool ok = false;
+    for (; i < a.m && !ok; i += nwaves) {
+      d = desc_at(i);
+      ok = stream_msg(d, a.fields, a.blobs, M);  // else the job path's (or invalid: nothing written)
+      if (ok) u.rk = a.rk + kRunPad + i * kStreamPutRuns;
+    }
+    const uint64_t m0 = a.oreg0 + d.out_off, S0 = m0 & ~uint64_t(63);
+    const int32_t mis = (int32_t)(m0 & 15u);
+    u.out = a.obase + m0;
+    u.p0b = (int32_t)(S0 - m0);
+    u.len = ok ? M.len : 0;
+    u.nruns = ok ? (uint32_t)((m0 + M.len - S0 + 63) >> 6) : 0u;
+    if (ok) stream_seg_table(M, tab, lane);
+#pragma unroll
+    for (uint32_t it = 0; it < 3; ++it) {
+      const uint32_t idx = 64 * it + lane, s = idx >> 5, j = idx & 31u;
+      const u32x4 t = tab[s < 5 ? s : 5];
+      const int32_t lo = (int32_t)t.x, hi = (int32_t)t.y;
+      const int32_t up = ((lo + mis + 15) & ~15) - mis, dn = ((hi + mis) & ~15) - mis;
+      const int32_t e = j < 16 ? lo + (int32_t)j : (up > dn ? up : dn) + (int32_t)j - 16;
+      const bool live = ok && s < 5 && (j < 16 ? e < (up < hi ? up : hi) : e < hi);
+      ee[it] = live ? e : -1;
+      eb[it] = *reinterpret_cast<const gu8*>(live ? (((uint64_t)t.w << 32) | t.z) + (uint64_t)(int64_t)e : dummy);
+    }
+    const int32_t p0 = u.p0b + 16 * (int32_t)lane;
+    pm = 0;
+#pragma unroll
+    for (uint32_t sb = 0; sb < kStreamSbs; ++sb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint64_t src = ok ? stream_piece_src(M, tab, p0 + (int32_t)(kSuperBlock * sb + kBlockBytes * q)) : 0;
+        x[sb][q] = ld16ug(src ? src : dummy);
+        pm |= src ? 1u << (4 * sb + q) : 0u;
+      }
+    return ok;
+  };
+
+  StreamUnit un;
+  int32_t een[3];
+  uint32_t ebn[3];
+  u32x4 xn[kStreamSbs][4];
+  uint32_t pmn;
+  bool more = start(un, een, ebn, xn, pmn);
+  while (more) {
+    const StreamUnit u = un;
+    int32_t ee[3];
+    uint32_t eb[3];
+    u32x4 x[kStreamSbs][4];
+    const uint32_t pm = pmn;
+#pragma unroll
+    for (int t = 0; t < 3; ++t) ee[t] = een[t], eb[t] = ebn[t];
+#pragma unroll
+    for (uint32_t sb = 0; sb < kStreamSbs; ++sb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) x[sb][q] = xn[sb][q];
+    // this message's stores: the edge bytes, then its source pieces (one base per super-block, shared
+    // with the load-backs below: an address computed between the stores and a load-back would reuse a
+    // stored register and wait for that store to complete)
+    const int32_t p0 = u.p0b + 16 * (int32_t)lane;
+    uint8_t* pb[kStreamSbs] = {u.out + p0, u.out + p0 + kSuperBlock};
+#pragma unroll
+    for (uint32_t sb = 0; sb < kStreamSbs; ++sb) asm volatile("" : "+v"(pb[sb]));  // opaque: kept, not rematerialized
+#pragma unroll
+    for (uint32_t it = 0; it < 3; ++it)
+      if (ee[it] >= 0) st8g(u.out + ee[it], eb[it]);
+#pragma unroll
+    for (uint32_t sb = 0; sb < kStreamSbs; ++sb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (pm & (1u << (4 * sb + q))) st16u_nt(pb[sb] + kBlockBytes * q, x[sb][q]);
+    // its gap pieces loaded back (the layout kernel's bytes and the edge bytes just stored); pieces
+    // outside the message keep what the lane loaded (the table image): the runs they fall in cross the
+    // message's ends or lie outside it, and are never summed
+#pragma unroll
+    for (uint32_t sb = 0; sb < kStreamSbs; ++sb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int32_t dd = p0 + (int32_t)(kSuperBlock * sb + kBlockBytes * q);
+        if (!(pm & (1u << (4 * sb + q))) && dd + 16 > 0 && dd < u.len)
+          x[sb][q] = ld16ug((uint64_t)(uintptr_t)(pb[sb] + kBlockBytes * q));
+      }
+    // the next message's parse and loads, in flight while this one is hashed
+    more = start(un, een, ebn, xn, pmn);
+#pragma unroll
+    for (uint32_t sb = 0; sb < kStreamSbs; ++sb) {
+      if (64 * sb >= u.nruns) break;
+      quad_transpose_asm(x[sb]);
+      buf[slot] = run_crc<4, 1>(x[sb], k, 0u);
+      if (64 * sb + 4 * lane < u.nruns && lane < 16)  // runs 64 sb + 4 lane .. + 3, as region_runs_kernel's stores
+        *reinterpret_cast<u32x4*>(u.rk + 64 * sb + 4 * lane) = *reinterpret_cast<const u32x4*>(buf + 4u * lane);
+    }
+  }
+}
+#else
 __global__ __launch_bounds__(1024) void put_stream_kernel(StreamPutArgs a) {
   {  // LDS-DMA of the slice tables (image bytes [0, 128 KiB)), as region_runs_kernel
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -1805,6 +1954,7 @@ __global__ __launch_bounds__(1024) void put_stream_kernel(StreamPutArgs a) {
     }
   }
 }
+#endif  // AMBRY_STREAM_PIPE
 
 hipError_t launch_put_stream(const StreamPutArgs& a, int num_cu, hipStream_t s) {
   if (a.m == 0) return hipSuccess;
