@@ -107,6 +107,9 @@ int enqueue_serialize(DevCtx* c, const ::ambrycrc_put_desc* d_desc, size_t m, co
     if (launch_put_stream(sa, c->num_cu, stream) != hipSuccess || launch_put_stream_seal(sa, c->num_cu, stream) != hipSuccess)
       return AMBRYCRC_EHIP;
     a.gate = a.big;  // the job path: only when a message was too long to stream
+    PutArgs z = a;   // ... whose first step empties the streamed messages' job entries
+    z.clear_short = true;
+    if (launch_put_layout(z, stream) != hipSuccess) return AMBRYCRC_EHIP;
   }
   if (a.copy_through) {
     // one pass over the fields: the copy-through sweep reads each from its source, writes it into

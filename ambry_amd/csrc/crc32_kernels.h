@@ -265,6 +265,10 @@ struct PutArgs {
   // seal). 0: every message through the job path.
   uint32_t stream_max = 0;
   uint32_t* big = nullptr;
+  // The streamed messages' job entries are left unwritten by the layout pass (they would be 5 x 40 B
+  // of zeros a message that nothing reads unless a long message is present); with clear_short the
+  // kernel only zeroes them, launched gated on *big ahead of the job path.
+  bool clear_short = false;
 };
 
 // Each copy job costs its bytes plus kCopyJobCost: a wave pays about one memory round trip

@@ -29,17 +29,36 @@ __global__ __launch_bounds__(256) void put_layout_kernel(PutArgs a) {
   // bytes it builds in registers, through LDS tables: not over bytes it just stored, read back
   // one dependent global load per byte.
   __shared__ uint32_t tbl[1024];
-  const bool hashes = a.copy_through || a.in_crc;  // kernel-uniform
+  if (a.gate && *a.gate == 0) return;  // grid-uniform
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t m = a.m;
+  const bool live = i < m;
+  ambrycrc_put_desc d;
+  PutLayout L;
+  const bool ok = live && put_layout(d = a.desc[i], L);
+  // copy mode: a message this short is the streamed kernels' (put_stream_kernel) and gets no jobs
+  const bool streamed = a.stream_max && ok && L.length <= a.stream_max;
+  if (a.clear_short) {  // the job path runs (a long message is present): the streamed ones' entries are empty
+    if (streamed) {
+      for (uint32_t k = 0; k < kPutSlots; ++k) {
+        a.cp_len[k * m + i] = 0;
+        a.cp_cost[k * m + i] = 0;
+        a.crc_len[k * m + i] = 0;
+        a.crc_off[k * m + i] = 0;
+        a.crc_in[k * m + i] = 0;
+      }
+    }
+    return;
+  }
+  bool hashes = a.copy_through || a.in_crc;  // kernel-uniform
+  // with streaming, only a block holding a message for the job path hashes (every thread reaches the barrier)
+  if (hashes && a.stream_max) hashes = __syncthreads_or(live && !streamed);
   if (hashes) {
     stage_slice_tables(tbl, a.img);
     __syncthreads();
   }
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.m || (a.gate && *a.gate == 0)) return;
-  const ambrycrc_put_desc d = a.desc[i];
-  PutLayout L;
-  const uint64_t m = a.m;
-  if (!put_layout(d, L)) {  // the host checks descriptors it can see; a bad one here writes nothing
+  if (!live) return;
+  if (!ok) {  // the host checks descriptors it can see; a bad one here writes nothing
     for (uint32_t k = 0; k < kPutSlots; ++k) {
       a.cp_len[k * m + i] = 0;
       a.cp_cost[k * m + i] = 0;
@@ -50,15 +69,8 @@ __global__ __launch_bounds__(256) void put_layout_kernel(PutArgs a) {
     if (a.msg_len) a.msg_len[i] = 0;
     return;
   }
-  if (a.stream_max) {  // copy mode: messages this short are the streamed kernels' (put_stream_kernel): no jobs
-    if (L.length <= a.stream_max) {
-      for (uint32_t k = 0; k < kPutSlots; ++k) {
-        a.cp_len[k * m + i] = 0;
-        a.cp_cost[k * m + i] = 0;
-        a.crc_len[k * m + i] = 0;
-        a.crc_off[k * m + i] = 0;
-        a.crc_in[k * m + i] = 0;
-      }
+  if (a.stream_max) {
+    if (streamed) {  // its job entries: zeroed by the clear_short launch only if the job path runs
       if (a.msg_len) a.msg_len[i] = L.length;
       put_write_fixed(d, L, a.out + d.out_off);  // the gaps' bytes, which put_stream_kernel's edge pieces read
       return;

@@ -246,3 +246,61 @@ def test_serialize_descriptors_out_of_output_order(gpu, mf):
         exp[o:o + len(e)] = e
     assert out.cpu().numpy().tobytes() == bytes(exp)
     assert mlen.cpu().numpy().tolist() == [len(expected(mf, msgs[i])) for i in perm]
+
+
+def test_serialize_streamed_after_job_batch(gpu, mf):
+    """The streamed messages' job entries are only zeroed when the job path runs (a gated clear launch,
+    put_layout_kernel with clear_short): a batch of long messages fills the stream's workspace with job
+    entries, then a batch of the same size, mostly short with a few long, reuses it -- every byte as the
+    oracle lays it out, so no stale entry of the first batch is copied or hashed into the second."""
+    import dataclasses
+
+    from datagen import stream_bytes
+
+    n = 200
+    longs = random_messages(mf, n, seed=41, max_blob=9000)
+    longs = [dataclasses.replace(m, blob=stream_bytes(900 + i, 1, 7000 + i).tobytes(),
+                                 props=mf.blob_properties_bytes(7000 + i)) for i, m in enumerate(longs)]
+    _run(gpu, mf, longs, 1, 1, 0)
+    mixed = random_messages(mf, n, seed=43, max_blob=3000)
+    mixed = [dataclasses.replace(m, blob=stream_bytes(700 + i, 2, 8000).tobytes(),
+                                 props=mf.blob_properties_bytes(8000)) if i % 37 == 5 else m
+             for i, m in enumerate(mixed)]
+    _run(gpu, mf, mixed, 1, 3, 1)
+
+
+def test_serialize_back_to_back_one_stream(gpu, mf):
+    """The streamed form's job path runs on the stream's side stream (ring slot per call, the caller's
+    stream waiting on the done signal): 40 calls on one stream -- past the 32 ring slots -- every third
+    batch with long messages (the job path runs), each into its own output, then one synchronize of
+    that stream only. Every output is the oracle's layout."""
+    import dataclasses
+
+    import torch
+
+    from ambry_amd.messages import pack_batch, serialize_dev
+    from datagen import stream_bytes
+
+    s = torch.cuda.Stream()
+    cases = []
+    with torch.cuda.stream(s):
+        for c in range(40):
+            msgs = random_messages(mf, 60, seed=300 + c, max_blob=2000)
+            if c % 3 == 1:
+                msgs = [dataclasses.replace(m, blob=stream_bytes(c * 97 + i, 4, 6500 + i).tobytes(),
+                                            props=mf.blob_properties_bytes(6500 + i)) if i % 7 == 2 else m
+                        for i, m in enumerate(msgs)]
+            descs, fields, blobs, offs, total = pack_batch(msgs, out_align=1, field_align=1, gap=1)
+            d = torch.frombuffer(bytearray(descs.tobytes()), dtype=torch.uint8).to("cuda", non_blocking=False)
+            f = torch.frombuffer(bytearray(fields), dtype=torch.uint8).to("cuda")
+            b = torch.frombuffer(bytearray(blobs if len(blobs) else b"\0"), dtype=torch.uint8).to("cuda")
+            out = torch.full((total,), 0xAA, dtype=torch.uint8, device="cuda")
+            serialize_dev(d, out, f, b)
+            cases.append((msgs, offs, total, out, (d, f, b)))
+    s.synchronize()
+    for msgs, offs, total, out, _ in cases:
+        exp = bytearray(b"\xAA" * total)
+        for m, o in zip(msgs, offs):
+            e = expected(mf, m)
+            exp[o:o + len(e)] = e
+        assert out.cpu().numpy().tobytes() == bytes(exp)
